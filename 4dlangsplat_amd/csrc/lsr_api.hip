@@ -1,0 +1,448 @@
+// lsr_api.hip -- the C ABI (include/lsr.h): argument checks, workspace carving, launch order.
+//
+// Forward  = preprocess -> depth sort of the P Gaussians -> tile counts in depth order -> scan
+//            -> (host reads K) -> emit K instances -> stable tile sort -> tile ranges -> composite.
+// Backward = composite backward (per-Gaussian screen-space sums) -> preprocess backward.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/lsr.h"
+#include "lsr_common.h"
+#include "lsr_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define LSR_HIP(expr)                                                                        \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess) return fail(LSR_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+#define LSR_LAUNCHED(name, st, debug)                                                        \
+    do {                                                                                     \
+        hipError_t e_ = hipGetLastError();                                                   \
+        if (e_ == hipSuccess && (debug)) e_ = hipStreamSynchronize(st);                      \
+        if (e_ != hipSuccess) return fail(LSR_EHIP, std::string(name) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+// ---- per-phase event timing (lsr_profile_*) ----------------------------------------------------
+struct Profiler {
+    std::mutex mu;
+    bool on = false;
+    std::vector<hipEvent_t> pool;
+    struct Rec { int phase; hipEvent_t a, b; };
+    std::vector<Rec> pending;
+    double ms[LSR_NUM_PHASES] = {};
+    int64_t n[LSR_NUM_PHASES] = {};
+    hipEvent_t get() {
+        if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+        hipEvent_t e = nullptr;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        return e;
+    }
+};
+Profiler g_prof;
+
+struct PhaseTimer {
+    int phase;
+    hipStream_t st;
+    hipEvent_t a = nullptr, b = nullptr;
+    PhaseTimer(int p, hipStream_t s) : phase(p), st(s) {
+        std::lock_guard<std::mutex> l(g_prof.mu);
+        if (!g_prof.on) return;
+        a = g_prof.get();
+        b = g_prof.get();
+        if (a) (void)hipEventRecord(a, st);
+    }
+    ~PhaseTimer() {
+        if (!a || !b) return;
+        (void)hipEventRecord(b, st);
+        std::lock_guard<std::mutex> l(g_prof.mu);
+        g_prof.pending.push_back({phase, a, b});
+    }
+};
+
+constexpr size_t kAlign = 256;
+inline size_t al(size_t x) { return (x + kAlign - 1) / kAlign * kAlign; }
+
+// Bump allocator over a caller-owned workspace; the same carve order gives the size query.
+struct Carver {
+    char* base;
+    size_t off = 0;
+    explicit Carver(void* b) : base(static_cast<char*>(b)) {}
+    template <typename T>
+    T* take(size_t n) {
+        T* p = base ? reinterpret_cast<T*>(base + off) : nullptr;
+        off += al(n * sizeof(T));
+        return p;
+    }
+};
+
+struct Geom {
+    float2* xy;
+    float4* conic_o;
+    float4* rgbd;
+    uint8_t* clamped;
+    uint32_t* tiles;
+    uint32_t *key_a, *key_b, *val_a, *val_b;
+    uint32_t* counts;
+    uint32_t* offsets;
+    uint32_t* inst_off;
+    uint32_t* total;
+    void* sort_tmp;
+    void* scan_tmp;
+};
+Geom carve_geom(void* base, size_t P, size_t* bytes) {
+    Carver c(base);
+    Geom g;
+    g.xy = c.take<float2>(P);
+    g.conic_o = c.take<float4>(P);
+    g.rgbd = c.take<float4>(P);
+    g.clamped = c.take<uint8_t>(P);
+    g.tiles = c.take<uint32_t>(P);
+    g.key_a = c.take<uint32_t>(P);
+    g.key_b = c.take<uint32_t>(P);
+    g.val_a = c.take<uint32_t>(P);
+    g.val_b = c.take<uint32_t>(P);
+    g.counts = c.take<uint32_t>(P);
+    g.offsets = c.take<uint32_t>(P);
+    g.inst_off = c.take<uint32_t>(P);
+    g.total = c.take<uint32_t>(4);
+    g.sort_tmp = c.take<char>(lsr::radix_temp_bytes(P));
+    g.scan_tmp = c.take<char>(lsr::scan_temp_bytes(P));
+    if (bytes) *bytes = c.off;
+    return g;
+}
+
+struct Binning {
+    uint32_t *key_a, *key_b, *val_a, *val_b;
+    void* sort_tmp;
+};
+Binning carve_binning(void* base, size_t K, size_t* bytes) {
+    Carver c(base);
+    Binning b;
+    b.key_a = c.take<uint32_t>(K);
+    b.key_b = c.take<uint32_t>(K);
+    b.val_a = c.take<uint32_t>(K);
+    b.val_b = c.take<uint32_t>(K);
+    b.sort_tmp = c.take<char>(lsr::radix_temp_bytes(K));
+    if (bytes) *bytes = c.off;
+    return b;
+}
+
+struct Img {
+    uint2* ranges;
+    uint32_t* tile_max;
+    float* final_T;
+    uint32_t* n_contrib;
+};
+Img carve_img(void* base, int W, int H, size_t* bytes) {
+    const size_t gx = (W + LSR_TILE_X - 1) / LSR_TILE_X, gy = (H + LSR_TILE_Y - 1) / LSR_TILE_Y;
+    Carver c(base);
+    Img m;
+    m.ranges = c.take<uint2>(gx * gy);
+    m.tile_max = c.take<uint32_t>(gx * gy);
+    m.final_T = c.take<float>((size_t)W * H);
+    m.n_contrib = c.take<uint32_t>((size_t)W * H);
+    if (bytes) *bytes = c.off;
+    return m;
+}
+
+struct Scratch {
+    float2* g_mean2D;
+    float4* g_conic;
+    float* g_color;
+    size_t zero_bytes;   // leading region zeroed per call
+};
+Scratch carve_scratch(void* base, size_t P, size_t* bytes) {
+    Carver c(base);
+    Scratch s;
+    s.g_mean2D = c.take<float2>(P);
+    s.g_conic = c.take<float4>(P);
+    s.g_color = c.take<float>(3 * P);
+    s.zero_bytes = c.off;
+    if (bytes) *bytes = c.off;
+    return s;
+}
+
+int depth_sort_result_in_b() { return 0; }  // 32 key bits = 4 passes: result back in the (a) buffers
+
+int tile_bits(int ntiles) {
+    int b = 1;
+    while ((1 << b) < ntiles) ++b;
+    return b;
+}
+bool tile_sort_in_b(int ntiles) { return ((tile_bits(ntiles) + 7) / 8) % 2 == 1; }
+
+int check_common(const lsr_settings* s, const lsr_fwd_in* in) {
+    if (!s || !in) return fail(LSR_EINVAL, "null settings or inputs");
+    if (s->image_width <= 0 || s->image_height <= 0) return fail(LSR_EINVAL, "image size must be positive");
+    if (in->P < 0) return fail(LSR_EINVAL, "P must be >= 0");
+    if (!s->viewmatrix || !s->projmatrix || !s->bg || !s->campos)
+        return fail(LSR_EINVAL, "viewmatrix, projmatrix, bg and campos are required");
+    if (in->P > 0 && (!in->means3D || !in->opacities)) return fail(LSR_EINVAL, "means3D and opacities are required");
+    if ((in->shs == nullptr) == (in->colors_precomp == nullptr))
+        return fail(LSR_EINVAL, "Please provide excatly one of either SHs or precomputed colors!");
+    const bool sr = in->scales != nullptr || in->rotations != nullptr;
+    if ((!(in->scales && in->rotations) && !in->cov3D_precomp) || (sr && in->cov3D_precomp))
+        return fail(LSR_EINVAL, "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
+    if (in->shs && (s->sh_degree < 0 || s->sh_degree > 3 || in->M < (s->sh_degree + 1) * (s->sh_degree + 1)))
+        return fail(LSR_EINVAL, "sh_degree must be in [0, 3] and shs must hold (sh_degree + 1)^2 coefficients");
+    if (in->C < 0 || in->C > 64) return fail(LSR_EINVAL, "language feature channels must be in [0, 64]");
+    if (s->include_feature && in->C > 0 && in->P > 0 && !in->language_feature)
+        return fail(LSR_EINVAL, "language_feature is required when C > 0");
+    return LSR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lsr_version(void) { return LSR_API_VERSION; }
+const char* lsr_last_error(void) { return g_err.c_str(); }
+
+int64_t lsr_geom_bytes(int32_t P) {
+    size_t b;
+    carve_geom(nullptr, (size_t)(P > 0 ? P : 1), &b);
+    return (int64_t)b;
+}
+int64_t lsr_binning_bytes(int64_t K) {
+    size_t b;
+    carve_binning(nullptr, (size_t)(K > 0 ? K : 1), &b);
+    return (int64_t)b;
+}
+int64_t lsr_img_bytes(int32_t W, int32_t H) {
+    size_t b;
+    carve_img(nullptr, W, H, &b);
+    return (int64_t)b;
+}
+int64_t lsr_backward_bytes(int32_t P, int64_t K, int32_t C) {
+    (void)K;
+    (void)C;
+    size_t b;
+    carve_scratch(nullptr, (size_t)(P > 0 ? P : 1), &b);
+    return (int64_t)b;
+}
+
+int lsr_forward_preprocess(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_out* out, void* geom,
+                           int64_t* num_rendered, lsr_stream_t stream) {
+    int rc = check_common(s, in);
+    if (rc) return rc;
+    if (!out || (!out->radii && in->P > 0)) return fail(LSR_EINVAL, "radii output is required");
+    if (!geom || !num_rendered) return fail(LSR_EINVAL, "geom workspace and num_rendered are required");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int P = in->P, W = s->image_width, H = s->image_height;
+    const int gx = (W + LSR_TILE_X - 1) / LSR_TILE_X, gy = (H + LSR_TILE_Y - 1) / LSR_TILE_Y;
+    Geom g = carve_geom(geom, (size_t)(P > 0 ? P : 1), nullptr);
+    if (P == 0) {
+        *num_rendered = 0;
+        return LSR_OK;
+    }
+    lsr::PreprocessArgs a{};
+    a.P = P; a.M = in->M; a.deg = s->sh_degree; a.W = W; a.H = H; a.grid_x = gx; a.grid_y = gy;
+    a.tanfovx = s->tanfovx; a.tanfovy = s->tanfovy;
+    a.focal_x = (float)W / (2.0f * s->tanfovx);
+    a.focal_y = (float)H / (2.0f * s->tanfovy);
+    a.scale_modifier = s->scale_modifier;
+    a.means3D = in->means3D; a.scales = in->scales; a.rotations = in->rotations; a.opacities = in->opacities;
+    a.shs = in->shs; a.colors_precomp = in->colors_precomp; a.cov3D_precomp = in->cov3D_precomp;
+    a.view = s->viewmatrix; a.proj = s->projmatrix; a.campos = s->campos;
+    a.radii = out->radii; a.tiles = g.tiles; a.key = g.key_a; a.xy = g.xy; a.conic_o = g.conic_o; a.rgbd = g.rgbd;
+    a.clamped = g.clamped;
+    LSR_HIP(hipMemsetAsync(g.clamped, 0, (size_t)P, st));
+    {
+        PhaseTimer t(LSR_PHASE_PREPROCESS, st);
+        lsr::launch_preprocess(a, st);
+    }
+    LSR_LAUNCHED("preprocess", st, s->debug);
+    // depth order of all Gaussians (culled ones carry key 0xFFFFFFFF and sort last), stable in id
+    bool in_b;
+    {
+        PhaseTimer t(LSR_PHASE_DEPTH_SORT, st);
+        lsr::launch_iota(P, g.val_a, st);
+        in_b = lsr::radix_sort_pairs(g.key_a, g.val_a, g.key_b, g.val_b, (size_t)P, 0, 32, g.sort_tmp, st);
+    }
+    if (in_b != (bool)depth_sort_result_in_b()) return fail(LSR_EHIP, "internal: depth sort parity");
+    LSR_LAUNCHED("depth sort", st, s->debug);
+    {
+        PhaseTimer t(LSR_PHASE_INSTANCE_SCAN, st);
+        lsr::launch_gather_tile_counts(P, g.val_a, g.tiles, g.counts, st);
+        lsr::exclusive_scan_u32(g.counts, g.offsets, (size_t)P, g.total, g.scan_tmp, st);
+    }
+    LSR_LAUNCHED("instance scan", st, s->debug);
+    uint32_t K = 0;
+    LSR_HIP(hipMemcpyAsync(&K, g.total, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    LSR_HIP(hipStreamSynchronize(st));
+    *num_rendered = (int64_t)K;
+    return LSR_OK;
+}
+
+int lsr_forward_render(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_out* out, void* geom, void* binning,
+                       void* img, int64_t num_rendered, lsr_stream_t stream) {
+    int rc = check_common(s, in);
+    if (rc) return rc;
+    if (!out || !out->out_color || !out->out_depth) return fail(LSR_EINVAL, "color and depth outputs are required");
+    if (in->C > 0 && !out->out_language_feature) return fail(LSR_EINVAL, "language feature output is required when C > 0");
+    if (!geom || !img || (num_rendered > 0 && !binning)) return fail(LSR_EINVAL, "workspaces are required");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int P = in->P, W = s->image_width, H = s->image_height, C = in->C;
+    const int gx = (W + LSR_TILE_X - 1) / LSR_TILE_X, gy = (H + LSR_TILE_Y - 1) / LSR_TILE_Y;
+    const size_t K = (size_t)num_rendered;
+    Geom g = carve_geom(geom, (size_t)(P > 0 ? P : 1), nullptr);
+    Binning b = carve_binning(binning, K > 0 ? K : 1, nullptr);
+    Img m = carve_img(img, W, H, nullptr);
+    LSR_HIP(hipMemsetAsync(m.ranges, 0, sizeof(uint2) * (size_t)gx * gy, st));
+    const uint32_t* point_list = nullptr;
+    if (K > 0) {
+        {
+            PhaseTimer t(LSR_PHASE_EMIT, st);
+            lsr::launch_emit_instances(P, g.val_a, g.offsets, g.tiles, g.xy, out->radii, gx, gy, b.key_a, b.val_a,
+                                       g.inst_off, st);
+        }
+        LSR_LAUNCHED("emit", st, s->debug);
+        bool in_b;
+        {
+            PhaseTimer t(LSR_PHASE_TILE_SORT, st);
+            in_b = lsr::radix_sort_pairs(b.key_a, b.val_a, b.key_b, b.val_b, K, 0, tile_bits(gx * gy), b.sort_tmp, st);
+        }
+        const uint32_t* keys = in_b ? b.key_b : b.key_a;
+        point_list = in_b ? b.val_b : b.val_a;
+        LSR_LAUNCHED("tile sort", st, s->debug);
+        {
+            PhaseTimer t(LSR_PHASE_TILE_RANGES, st);
+            lsr::launch_tile_ranges(K, keys, m.ranges, st);
+        }
+        LSR_LAUNCHED("tile ranges", st, s->debug);
+    }
+    lsr::RenderFwdArgs r{};
+    r.W = W; r.H = H; r.grid_x = gx; r.grid_y = gy; r.C = C; r.include_feature = s->include_feature;
+    r.ranges = m.ranges; r.point_list = point_list; r.xy = g.xy; r.conic_o = g.conic_o; r.rgbd = g.rgbd;
+    r.lang = in->language_feature; r.bg = s->bg; r.final_T = m.final_T; r.n_contrib = m.n_contrib;
+    r.tile_max_contrib = m.tile_max; r.out_color = out->out_color; r.out_lang = out->out_language_feature;
+    r.out_depth = out->out_depth;
+    if (C > 0 && !s->include_feature)
+        LSR_HIP(hipMemsetAsync(out->out_language_feature, 0, sizeof(float) * (size_t)C * W * H, st));
+    {
+        PhaseTimer t(LSR_PHASE_RENDER_FWD, st);
+        lsr::launch_render_fwd(r, st);
+    }
+    LSR_LAUNCHED("render forward", st, s->debug);
+    return LSR_OK;
+}
+
+int lsr_backward(const lsr_settings* s, const lsr_fwd_in* in, const lsr_bwd_in* gin, lsr_bwd_out* gout,
+                 const void* geom, const void* binning, const void* img, void* scratch, int64_t num_rendered,
+                 int32_t accumulate, lsr_stream_t stream) {
+    int rc = check_common(s, in);
+    if (rc) return rc;
+    if (!gin || !gin->dL_dout_color || !gout) return fail(LSR_EINVAL, "dL_dout_color and outputs are required");
+    if (!geom || !img || !scratch || (num_rendered > 0 && !binning)) return fail(LSR_EINVAL, "workspaces are required");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int P = in->P, W = s->image_width, H = s->image_height, C = in->C;
+    if (P == 0) return LSR_OK;
+    const int gx = (W + LSR_TILE_X - 1) / LSR_TILE_X, gy = (H + LSR_TILE_Y - 1) / LSR_TILE_Y;
+    const size_t K = (size_t)num_rendered;
+    Geom g = carve_geom(const_cast<void*>(geom), (size_t)P, nullptr);
+    Binning b = carve_binning(const_cast<void*>(binning), K > 0 ? K : 1, nullptr);
+    Img m = carve_img(const_cast<void*>(img), W, H, nullptr);
+    Scratch sc = carve_scratch(scratch, (size_t)P, nullptr);
+    LSR_HIP(hipMemsetAsync(scratch, 0, sc.zero_bytes, st));
+    if (!accumulate) {
+        if (gout->dL_dlanguage_feature && C > 0)
+            LSR_HIP(hipMemsetAsync(gout->dL_dlanguage_feature, 0, sizeof(float) * (size_t)P * C, st));
+        if (gout->dL_dopacity) LSR_HIP(hipMemsetAsync(gout->dL_dopacity, 0, sizeof(float) * (size_t)P, st));
+    }
+    const uint32_t* point_list = tile_sort_in_b(gx * gy) ? b.val_b : b.val_a;
+    if (K > 0) {
+        lsr::RenderBwdArgs r{};
+        r.W = W; r.H = H; r.grid_x = gx; r.grid_y = gy; r.C = C; r.include_feature = s->include_feature;
+        r.ranges = m.ranges; r.point_list = point_list; r.xy = g.xy; r.conic_o = g.conic_o; r.rgbd = g.rgbd;
+        r.lang = in->language_feature; r.bg = s->bg; r.final_T = m.final_T; r.n_contrib = m.n_contrib;
+        r.tile_max_contrib = m.tile_max;
+        r.dL_dcolor = gin->dL_dout_color; r.dL_dlang = gin->dL_dout_language_feature; r.dL_ddepth = gin->dL_dout_depth;
+        r.g_mean2D = sc.g_mean2D; r.g_conic = sc.g_conic; r.g_color = sc.g_color;
+        r.g_lang = gout->dL_dlanguage_feature; r.g_opacity = gout->dL_dopacity;
+        {
+            PhaseTimer t(LSR_PHASE_RENDER_BWD, st);
+            lsr::launch_render_bwd(r, st);
+        }
+        LSR_LAUNCHED("render backward", st, s->debug);
+    }
+    lsr::PreprocessBwdArgs a{};
+    a.P = P; a.M = in->M; a.deg = s->sh_degree;
+    a.tanfovx = s->tanfovx; a.tanfovy = s->tanfovy;
+    a.focal_x = (float)W / (2.0f * s->tanfovx);
+    a.focal_y = (float)H / (2.0f * s->tanfovy);
+    a.scale_modifier = s->scale_modifier;
+    a.means3D = in->means3D; a.scales = in->scales; a.rotations = in->rotations; a.shs = in->shs;
+    a.cov3D_precomp = in->cov3D_precomp; a.view = s->viewmatrix; a.proj = s->projmatrix; a.campos = s->campos;
+    a.clamped = g.clamped;
+    a.g_mean2D = sc.g_mean2D; a.g_conic = sc.g_conic; a.g_color = sc.g_color;
+    a.dmeans3D = gout->dL_dmeans3D; a.dmeans2D = gout->dL_dmeans2D; a.dcolors = gout->dL_dcolors;
+    a.dcov3D = gout->dL_dcov3D; a.dsh = in->shs ? gout->dL_dsh : nullptr; a.dscales = gout->dL_dscales;
+    a.drots = gout->dL_drotations;
+    a.tiles = g.tiles;
+    {
+        PhaseTimer t(LSR_PHASE_PREPROCESS_BWD, st);
+        lsr::launch_preprocess_bwd(a, accumulate != 0, st);
+    }
+    LSR_LAUNCHED("preprocess backward", st, s->debug);
+    return LSR_OK;
+}
+
+int lsr_mark_visible(int32_t P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                     uint8_t* present, lsr_stream_t stream) {
+    (void)projmatrix;
+    if (P < 0 || (P > 0 && (!means3D || !viewmatrix || !present))) return fail(LSR_EINVAL, "bad mark_visible arguments");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    lsr::launch_mark_visible(P, means3D, viewmatrix, present, st);
+    LSR_LAUNCHED("mark_visible", st, false);
+    return LSR_OK;
+}
+
+int lsr_profile_enable(int32_t on) {
+    std::lock_guard<std::mutex> l(g_prof.mu);
+    for (auto& r : g_prof.pending) {
+        (void)hipEventSynchronize(r.b);
+        g_prof.pool.push_back(r.a);
+        g_prof.pool.push_back(r.b);
+    }
+    g_prof.pending.clear();
+    for (int i = 0; i < LSR_NUM_PHASES; ++i) { g_prof.ms[i] = 0.0; g_prof.n[i] = 0; }
+    g_prof.on = on != 0;
+    return LSR_OK;
+}
+
+int lsr_profile_read(double* ms_total, int64_t* launches, int32_t n) {
+    std::lock_guard<std::mutex> l(g_prof.mu);
+    for (auto& r : g_prof.pending) {
+        if (hipEventSynchronize(r.b) != hipSuccess) return fail(LSR_EHIP, "profile: event synchronize failed");
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+            g_prof.ms[r.phase] += ms;
+            g_prof.n[r.phase] += 1;
+        }
+        g_prof.pool.push_back(r.a);
+        g_prof.pool.push_back(r.b);
+    }
+    g_prof.pending.clear();
+    for (int i = 0; i < n && i < LSR_NUM_PHASES; ++i) {
+        if (ms_total) ms_total[i] = g_prof.ms[i];
+        if (launches) launches[i] = g_prof.n[i];
+    }
+    return LSR_NUM_PHASES;
+}
+
+}  // extern "C"

@@ -1,0 +1,124 @@
+// lsr_internal.h -- kernel argument blocks and launcher declarations shared by the HIP sources.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lsr {
+
+struct PreprocessArgs {
+    int P, M, deg, W, H, grid_x, grid_y;
+    float tanfovx, tanfovy, focal_x, focal_y, scale_modifier;
+    const float* means3D;
+    const float* scales;
+    const float* rotations;
+    const float* opacities;
+    const float* shs;
+    const float* colors_precomp;
+    const float* cov3D_precomp;
+    const float* view;
+    const float* proj;
+    const float* campos;
+    // outputs
+    int* radii;
+    uint32_t* tiles;
+    uint32_t* key;
+    float2* xy;
+    float4* conic_o;
+    float4* rgbd;
+    uint8_t* clamped;
+};
+
+struct PreprocessBwdArgs {
+    int P, M, deg;
+    float tanfovx, tanfovy, focal_x, focal_y, scale_modifier;
+    const float* means3D;
+    const float* scales;
+    const float* rotations;
+    const float* shs;
+    const float* cov3D_precomp;
+    const float* view;
+    const float* proj;
+    const float* campos;
+    const uint32_t* tiles;    // tiles touched (0 = culled; same as radii == 0)
+    const uint8_t* clamped;
+    // per-Gaussian screen-space gradients from the compositor backward
+    const float2* g_mean2D;   // NDC units
+    const float4* g_conic;    // (conic a, conic b [half, upstream convention], conic c, depth)
+    const float* g_color;     // [P,3]
+    // outputs (nullable)
+    float* dmeans3D;
+    float* dmeans2D;
+    float* dcolors;
+    float* dcov3D;
+    float* dsh;
+    float* dscales;
+    float* drots;
+};
+
+struct RenderFwdArgs {
+    int W, H, grid_x, grid_y, C, include_feature;
+    const uint2* ranges;
+    const uint32_t* point_list;
+    const float2* xy;
+    const float4* conic_o;
+    const float4* rgbd;
+    const float* lang;
+    const float* bg;
+    float* final_T;
+    uint32_t* n_contrib;
+    uint32_t* tile_max_contrib;   // per tile: max n_contrib over its pixels (bounds the backward replay)
+    float* out_color;
+    float* out_lang;
+    float* out_depth;
+};
+
+struct RenderBwdArgs {
+    int W, H, grid_x, grid_y, C, include_feature;
+    const uint2* ranges;
+    const uint32_t* point_list;
+    const float2* xy;
+    const float4* conic_o;
+    const float4* rgbd;
+    const float* lang;
+    const float* bg;
+    const float* final_T;
+    const uint32_t* n_contrib;
+    const uint32_t* tile_max_contrib;
+    const float* dL_dcolor;   // [3,H,W]
+    const float* dL_dlang;    // [C,H,W] or null
+    const float* dL_ddepth;   // [H,W] or null
+    // outputs (atomically accumulated)
+    float2* g_mean2D;
+    float4* g_conic;
+    float* g_color;
+    float* g_lang;            // [P,C] user buffer (accumulated), may be null
+    float* g_opacity;         // [P]   user buffer (accumulated), may be null
+};
+
+void launch_preprocess(const PreprocessArgs& a, hipStream_t st);
+void launch_preprocess_bwd(const PreprocessBwdArgs& a, bool accumulate, hipStream_t st);
+void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st);
+
+// device-wide primitives (sort.hip)
+size_t scan_temp_bytes(size_t n);
+// exclusive scan of n u32 values; writes the total to *total (device) if non-null
+void exclusive_scan_u32(const uint32_t* in, uint32_t* out, size_t n, uint32_t* total, void* temp, hipStream_t st);
+size_t radix_temp_bytes(size_t n);
+// stable LSD sort of (key, val) pairs on key bits [begin_bit, end_bit).  Ping-pongs between the
+// (a) and (b) buffers; returns true when the sorted result ends in the (b) buffers.
+bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b, size_t n,
+                      int begin_bit, int end_bit, void* temp, hipStream_t st);
+
+// binning (binning.hip)
+void launch_iota(int n, uint32_t* out, hipStream_t st);
+void launch_gather_tile_counts(int P, const uint32_t* order, const uint32_t* tiles, uint32_t* counts, hipStream_t st);
+void launch_emit_instances(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* tiles,
+                           const float2* xy, const int* radii, int grid_x, int grid_y, uint32_t* keys,
+                           uint32_t* vals, uint32_t* inst_offset_by_id, hipStream_t st);
+void launch_tile_ranges(size_t K, const uint32_t* keys, uint2* ranges, hipStream_t st);
+
+// compositing (render_fwd.hip / render_bwd.hip)
+void launch_render_fwd(const RenderFwdArgs& a, hipStream_t st);
+void launch_render_bwd(const RenderBwdArgs& a, hipStream_t st);
+
+}  // namespace lsr

@@ -1,0 +1,441 @@
+// preprocess.hip -- per-Gaussian projection (forward) and the matching backward.
+//
+// Forward restates the upstream preprocessCUDA (call site gaussian_renderer/__init__.py:219-228;
+// constants in SURVEY.md 8a row a8): near cull z <= 0.2, EWA covariance with the 1.3 tan-fov clamp
+// and +0.3 low-pass, conic, 3-sigma radius, tile count, SH degree <= 3 colour.  One lane per
+// Gaussian; outputs are written as packed SoA records the compositor gathers in 8/16-byte pieces:
+//   xy      float2  pixel-space mean
+//   conic_o float4  (conic a, b, c, opacity)
+//   rgbd    float4  (r, g, b, view-space depth)
+//   key     u32     depth bits of visible Gaussians, 0xFFFFFFFF for culled ones (sort key)
+// Backward (rows a12 of SURVEY.md 8a) is fused with the per-Gaussian reduction of the
+// compositor's screen-space gradients: one lane per Gaussian walks conic -> cov2D -> cov3D ->
+// (scale, rotation), the projection Jacobian for means2D, the depth row, and the SH chain.
+#include "lsr_common.h"
+#include "lsr_internal.h"
+
+namespace lsr {
+
+struct m3 { float m[3][3]; };  // glm layout: m[column][row]
+
+__device__ __forceinline__ m3 mul(const m3& a, const m3& b) {
+    m3 o;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+            o.m[c][r] = a.m[0][r] * b.m[c][0] + a.m[1][r] * b.m[c][1] + a.m[2][r] * b.m[c][2];
+    return o;
+}
+__device__ __forceinline__ m3 tr(const m3& a) {
+    m3 o;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int r = 0; r < 3; ++r) o.m[c][r] = a.m[r][c];
+    return o;
+}
+__device__ __forceinline__ m3 quat_R(float4 q) {
+    const float r = q.x, x = q.y, y = q.z, z = q.w;
+    m3 R;
+    R.m[0][0] = 1.0f - 2.0f * (y * y + z * z); R.m[0][1] = 2.0f * (x * y - r * z); R.m[0][2] = 2.0f * (x * z + r * y);
+    R.m[1][0] = 2.0f * (x * y + r * z); R.m[1][1] = 1.0f - 2.0f * (x * x + z * z); R.m[1][2] = 2.0f * (y * z - r * x);
+    R.m[2][0] = 2.0f * (x * z - r * y); R.m[2][1] = 2.0f * (y * z + r * x); R.m[2][2] = 1.0f - 2.0f * (x * x + y * y);
+    return R;
+}
+__device__ __forceinline__ m3 zero3() {
+    m3 o;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int r = 0; r < 3; ++r) o.m[c][r] = 0.0f;
+    return o;
+}
+
+__device__ __forceinline__ void cov3d(float3 s, float mod, float4 q, float* cov) {
+    m3 S = zero3();
+    S.m[0][0] = mod * s.x; S.m[1][1] = mod * s.y; S.m[2][2] = mod * s.z;
+    const m3 Rm = quat_R(q);
+    const m3 M = mul(S, Rm);
+    const m3 Sig = mul(tr(M), M);
+    cov[0] = Sig.m[0][0]; cov[1] = Sig.m[0][1]; cov[2] = Sig.m[0][2];
+    cov[3] = Sig.m[1][1]; cov[4] = Sig.m[1][2]; cov[5] = Sig.m[2][2];
+}
+
+__device__ __forceinline__ m3 view_W(const float* __restrict__ v) {
+    m3 W;
+    W.m[0][0] = v[0]; W.m[0][1] = v[4]; W.m[0][2] = v[8];
+    W.m[1][0] = v[1]; W.m[1][1] = v[5]; W.m[1][2] = v[9];
+    W.m[2][0] = v[2]; W.m[2][1] = v[6]; W.m[2][2] = v[10];
+    return W;
+}
+__device__ __forceinline__ m3 sym3(const float* c) {
+    m3 V;
+    V.m[0][0] = c[0]; V.m[0][1] = c[1]; V.m[0][2] = c[2];
+    V.m[1][0] = c[1]; V.m[1][1] = c[3]; V.m[1][2] = c[4];
+    V.m[2][0] = c[2]; V.m[2][1] = c[4]; V.m[2][2] = c[5];
+    return V;
+}
+
+__constant__ float SH_C0 = 0.28209479177387814f;
+__constant__ float SH_C1 = 0.4886025119029199f;
+__constant__ float SH_C2[5] = {1.0925484305920792f, -1.0925484305920792f, 0.31539156525252005f,
+                               -1.0925484305920792f, 0.5462742152960396f};
+__constant__ float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570457994644658f,
+                               0.3731763325901154f, -0.4570457994644658f, 1.445305721320277f,
+                               -0.5900435899266435f};
+
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.P) return;
+    a.radii[i] = 0;
+    a.tiles[i] = 0;
+    a.key[i] = 0xFFFFFFFFu;
+    const float3 p = make_float3(a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]);
+    const float4 ph = xform4x4(a.proj, p);
+    const float3 pv = xform4x3(a.view, p);
+    if (pv.z <= 0.2f) return;
+    const float pw = 1.0f / (ph.w + 0.0000001f);
+    const float3 pp = make_float3(ph.x * pw, ph.y * pw, ph.z * pw);
+
+    float c3[6];
+    if (a.cov3D_precomp) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) c3[k] = a.cov3D_precomp[6 * (size_t)i + k];
+    } else {
+        const float3 s = make_float3(a.scales[3 * i], a.scales[3 * i + 1], a.scales[3 * i + 2]);
+        const float4 q = reinterpret_cast<const float4*>(a.rotations)[i];
+        cov3d(s, a.scale_modifier, q, c3);
+    }
+    // EWA projection (computeCov2D)
+    float3 t = pv;
+    const float limx = 1.3f * a.tanfovx, limy = 1.3f * a.tanfovy;
+    const float txtz = t.x / t.z, tytz = t.y / t.z;
+    t.x = fminf(limx, fmaxf(-limx, txtz)) * t.z;
+    t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
+    m3 J = zero3();
+    J.m[0][0] = a.focal_x / t.z; J.m[0][2] = -(a.focal_x * t.x) / (t.z * t.z);
+    J.m[1][1] = a.focal_y / t.z; J.m[1][2] = -(a.focal_y * t.y) / (t.z * t.z);
+    const m3 T = mul(view_W(a.view), J);
+    const m3 V = sym3(c3);
+    const m3 A = mul(tr(T), tr(V));
+    const m3 cv = mul(A, T);
+    const float ca = cv.m[0][0] + 0.3f, cb = cv.m[0][1], cc = cv.m[1][1] + 0.3f;
+    const float det = ca * cc - cb * cb;
+    if (det == 0.0f) return;
+    const float det_inv = 1.0f / det;
+    const float4 conic = make_float4(cc * det_inv, -cb * det_inv, ca * det_inv, a.opacities[i]);
+    const float mid = 0.5f * (ca + cc);
+    const float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float l2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+    const int radius = (int)ceilf(3.0f * sqrtf(fmaxf(l1, l2)));
+    const float2 pix = make_float2(ndc2pix(pp.x, a.W), ndc2pix(pp.y, a.H));
+    int2 rmin, rmax;
+    tile_rect(pix, radius, a.grid_x, a.grid_y, rmin, rmax);
+    const int ntiles = (rmax.y - rmin.y) * (rmax.x - rmin.x);
+    if (ntiles == 0) return;
+
+    float rgb[3];
+    if (a.colors_precomp) {
+        rgb[0] = a.colors_precomp[3 * i]; rgb[1] = a.colors_precomp[3 * i + 1]; rgb[2] = a.colors_precomp[3 * i + 2];
+    } else {
+        float3 dir = make_float3(p.x - a.campos[0], p.y - a.campos[1], p.z - a.campos[2]);
+        const float len = sqrtf(dir.x * dir.x + dir.y * dir.y + dir.z * dir.z);
+        dir.x = dir.x / len; dir.y = dir.y / len; dir.z = dir.z / len;
+        const float* sh = a.shs + (size_t)i * a.M * 3;
+        uint8_t cl = 0;
+        const int deg = a.deg;
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+#define SHc(k) sh[(k) * 3 + ch]
+            float res = SH_C0 * SHc(0);
+            if (deg > 0) {
+                const float x = dir.x, y = dir.y, z = dir.z;
+                res = res - SH_C1 * y * SHc(1) + SH_C1 * z * SHc(2) - SH_C1 * x * SHc(3);
+                if (deg > 1) {
+                    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+                    res = res + SH_C2[0] * xy * SHc(4) + SH_C2[1] * yz * SHc(5) +
+                          SH_C2[2] * (2.0f * zz - xx - yy) * SHc(6) + SH_C2[3] * xz * SHc(7) +
+                          SH_C2[4] * (xx - yy) * SHc(8);
+                    if (deg > 2) {
+                        res = res + SH_C3[0] * y * (3.0f * xx - yy) * SHc(9) + SH_C3[1] * xy * z * SHc(10) +
+                              SH_C3[2] * y * (4.0f * zz - xx - yy) * SHc(11) +
+                              SH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * SHc(12) +
+                              SH_C3[4] * x * (4.0f * zz - xx - yy) * SHc(13) + SH_C3[5] * z * (xx - yy) * SHc(14) +
+                              SH_C3[6] * x * (xx - 3.0f * yy) * SHc(15);
+                    }
+                }
+            }
+#undef SHc
+            res = res + 0.5f;
+            cl |= (res < 0.0f ? 1 : 0) << ch;
+            rgb[ch] = res < 0.0f ? 0.0f : res;
+        }
+        a.clamped[i] = cl;
+    }
+    a.radii[i] = radius;
+    a.tiles[i] = (uint32_t)ntiles;
+    a.key[i] = __float_as_uint(pv.z);
+    a.xy[i] = pix;
+    a.conic_o[i] = conic;
+    a.rgbd[i] = make_float4(rgb[0], rgb[1], rgb[2], pv.z);
+}
+
+void launch_preprocess(const PreprocessArgs& a, hipStream_t st) {
+    if (a.P == 0) return;
+    hipLaunchKernelGGL(k_preprocess, dim3((a.P + 255) / 256), dim3(256), 0, st, a);
+}
+
+// ---------------------------------------------------------------------------------------------
+// mark_visible
+__global__ void k_mark_visible(int P, const float* __restrict__ means3D, const float* __restrict__ view,
+                               uint8_t* __restrict__ present) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const float3 p = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
+    present[i] = xform4x3(view, p).z > 0.2f;
+}
+void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st) {
+    if (P == 0) return;
+    hipLaunchKernelGGL(k_mark_visible, dim3((P + 255) / 256), dim3(256), 0, st, P, means3D, view, present);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Backward.  g_* are the per-Gaussian screen-space gradients summed by the compositor backward.
+__device__ void cov2d_bwd(float3 mean, const float* c3, float fx, float fy, float tanfovx, float tanfovy,
+                          const float* __restrict__ view, float3 dconic, float3& dmean, float* dcov) {
+    float3 t = xform4x3(view, mean);
+    const float limx = 1.3f * tanfovx, limy = 1.3f * tanfovy;
+    const float txtz = t.x / t.z, tytz = t.y / t.z;
+    t.x = fminf(limx, fmaxf(-limx, txtz)) * t.z;
+    t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
+    const float x_grad_mul = (txtz < -limx || txtz > limx) ? 0.0f : 1.0f;
+    const float y_grad_mul = (tytz < -limy || tytz > limy) ? 0.0f : 1.0f;
+    m3 J = zero3();
+    J.m[0][0] = fx / t.z; J.m[0][2] = -(fx * t.x) / (t.z * t.z);
+    J.m[1][1] = fy / t.z; J.m[1][2] = -(fy * t.y) / (t.z * t.z);
+    const m3 W = view_W(view);
+    const m3 V = sym3(c3);
+    const m3 T = mul(W, J);
+    const m3 cv = mul(mul(tr(T), tr(V)), T);
+    const float a = cv.m[0][0] + 0.3f, b = cv.m[0][1], c = cv.m[1][1] + 0.3f;
+    const float denom = a * c - b * b;
+    float dL_da = 0.0f, dL_db = 0.0f, dL_dc = 0.0f;
+    const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+    const float (*Tm)[3] = T.m;
+    if (denom2inv != 0.0f) {
+        dL_da = denom2inv * (-c * c * dconic.x + 2.0f * b * c * dconic.y + (denom - a * c) * dconic.z);
+        dL_dc = denom2inv * (-a * a * dconic.z + 2.0f * a * b * dconic.y + (denom - a * c) * dconic.x);
+        dL_db = denom2inv * 2.0f * (b * c * dconic.x - (denom + 2.0f * b * b) * dconic.y + a * b * dconic.z);
+        dcov[0] = Tm[0][0] * Tm[0][0] * dL_da + Tm[0][0] * Tm[1][0] * dL_db + Tm[1][0] * Tm[1][0] * dL_dc;
+        dcov[3] = Tm[0][1] * Tm[0][1] * dL_da + Tm[0][1] * Tm[1][1] * dL_db + Tm[1][1] * Tm[1][1] * dL_dc;
+        dcov[5] = Tm[0][2] * Tm[0][2] * dL_da + Tm[0][2] * Tm[1][2] * dL_db + Tm[1][2] * Tm[1][2] * dL_dc;
+        dcov[1] = 2.0f * Tm[0][0] * Tm[0][1] * dL_da + (Tm[0][0] * Tm[1][1] + Tm[0][1] * Tm[1][0]) * dL_db + 2.0f * Tm[1][0] * Tm[1][1] * dL_dc;
+        dcov[2] = 2.0f * Tm[0][0] * Tm[0][2] * dL_da + (Tm[0][0] * Tm[1][2] + Tm[0][2] * Tm[1][0]) * dL_db + 2.0f * Tm[1][0] * Tm[1][2] * dL_dc;
+        dcov[4] = 2.0f * Tm[0][2] * Tm[0][1] * dL_da + (Tm[0][1] * Tm[1][2] + Tm[0][2] * Tm[1][1]) * dL_db + 2.0f * Tm[1][1] * Tm[1][2] * dL_dc;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) dcov[k] = 0.0f;
+    }
+    const float (*Vm)[3] = V.m;
+    const float dT00 = 2.0f * (Tm[0][0] * Vm[0][0] + Tm[0][1] * Vm[0][1] + Tm[0][2] * Vm[0][2]) * dL_da +
+                       (Tm[1][0] * Vm[0][0] + Tm[1][1] * Vm[0][1] + Tm[1][2] * Vm[0][2]) * dL_db;
+    const float dT01 = 2.0f * (Tm[0][0] * Vm[1][0] + Tm[0][1] * Vm[1][1] + Tm[0][2] * Vm[1][2]) * dL_da +
+                       (Tm[1][0] * Vm[1][0] + Tm[1][1] * Vm[1][1] + Tm[1][2] * Vm[1][2]) * dL_db;
+    const float dT02 = 2.0f * (Tm[0][0] * Vm[2][0] + Tm[0][1] * Vm[2][1] + Tm[0][2] * Vm[2][2]) * dL_da +
+                       (Tm[1][0] * Vm[2][0] + Tm[1][1] * Vm[2][1] + Tm[1][2] * Vm[2][2]) * dL_db;
+    const float dT10 = 2.0f * (Tm[1][0] * Vm[0][0] + Tm[1][1] * Vm[0][1] + Tm[1][2] * Vm[0][2]) * dL_dc +
+                       (Tm[0][0] * Vm[0][0] + Tm[0][1] * Vm[0][1] + Tm[0][2] * Vm[0][2]) * dL_db;
+    const float dT11 = 2.0f * (Tm[1][0] * Vm[1][0] + Tm[1][1] * Vm[1][1] + Tm[1][2] * Vm[1][2]) * dL_dc +
+                       (Tm[0][0] * Vm[1][0] + Tm[0][1] * Vm[1][1] + Tm[0][2] * Vm[1][2]) * dL_db;
+    const float dT12 = 2.0f * (Tm[1][0] * Vm[2][0] + Tm[1][1] * Vm[2][1] + Tm[1][2] * Vm[2][2]) * dL_dc +
+                       (Tm[0][0] * Vm[2][0] + Tm[0][1] * Vm[2][1] + Tm[0][2] * Vm[2][2]) * dL_db;
+    const float (*Wm)[3] = W.m;
+    const float dJ00 = Wm[0][0] * dT00 + Wm[0][1] * dT01 + Wm[0][2] * dT02;
+    const float dJ02 = Wm[2][0] * dT00 + Wm[2][1] * dT01 + Wm[2][2] * dT02;
+    const float dJ11 = Wm[1][0] * dT10 + Wm[1][1] * dT11 + Wm[1][2] * dT12;
+    const float dJ12 = Wm[2][0] * dT10 + Wm[2][1] * dT11 + Wm[2][2] * dT12;
+    const float tz = 1.0f / t.z, tz2 = tz * tz, tz3 = tz2 * tz;
+    const float dtx = x_grad_mul * -fx * tz2 * dJ02;
+    const float dty = y_grad_mul * -fy * tz2 * dJ12;
+    const float dtz = -fx * tz2 * dJ00 - fy * tz2 * dJ11 + (2.0f * fx * t.x) * tz3 * dJ02 + (2.0f * fy * t.y) * tz3 * dJ12;
+    dmean.x = view[0] * dtx + view[1] * dty + view[2] * dtz;
+    dmean.y = view[4] * dtx + view[5] * dty + view[6] * dtz;
+    dmean.z = view[8] * dtx + view[9] * dty + view[10] * dtz;
+}
+
+__device__ void cov3d_bwd(float3 sc, float mod, float4 q, const float* dcov, float3& dscale, float4& drot) {
+    const float r = q.x, x = q.y, y = q.z, z = q.w;
+    const m3 Rm = quat_R(q);
+    const float s[3] = {mod * sc.x, mod * sc.y, mod * sc.z};
+    m3 S = zero3();
+    S.m[0][0] = s[0]; S.m[1][1] = s[1]; S.m[2][2] = s[2];
+    const m3 M = mul(S, Rm);
+    m3 dS;
+    dS.m[0][0] = dcov[0]; dS.m[0][1] = 0.5f * dcov[1]; dS.m[0][2] = 0.5f * dcov[2];
+    dS.m[1][0] = 0.5f * dcov[1]; dS.m[1][1] = dcov[3]; dS.m[1][2] = 0.5f * dcov[4];
+    dS.m[2][0] = 0.5f * dcov[2]; dS.m[2][1] = 0.5f * dcov[4]; dS.m[2][2] = dcov[5];
+    m3 M2;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) M2.m[c][k] = 2.0f * M.m[c][k];
+    const m3 dM = mul(M2, dS);
+    const m3 Rt = tr(Rm);
+    m3 d = tr(dM);
+    float ds[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) ds[k] = (Rt.m[k][0] * d.m[k][0] + Rt.m[k][1] * d.m[k][1] + Rt.m[k][2] * d.m[k][2]) * mod;
+    dscale = make_float3(ds[0], ds[1], ds[2]);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { d.m[0][k] *= s[0]; d.m[1][k] *= s[1]; d.m[2][k] *= s[2]; }
+    drot.x = 2.0f * z * (d.m[0][1] - d.m[1][0]) + 2.0f * y * (d.m[2][0] - d.m[0][2]) + 2.0f * x * (d.m[1][2] - d.m[2][1]);
+    drot.y = 2.0f * y * (d.m[1][0] + d.m[0][1]) + 2.0f * z * (d.m[2][0] + d.m[0][2]) + 2.0f * r * (d.m[1][2] - d.m[2][1]) -
+             4.0f * x * (d.m[2][2] + d.m[1][1]);
+    drot.z = 2.0f * x * (d.m[1][0] + d.m[0][1]) + 2.0f * r * (d.m[2][0] - d.m[0][2]) + 2.0f * z * (d.m[1][2] + d.m[2][1]) -
+             4.0f * y * (d.m[2][2] + d.m[0][0]);
+    drot.w = 2.0f * r * (d.m[0][1] - d.m[1][0]) + 2.0f * x * (d.m[2][0] + d.m[0][2]) + 2.0f * y * (d.m[1][2] + d.m[2][1]) -
+             4.0f * z * (d.m[1][1] + d.m[0][0]);
+}
+
+template <bool ACC>
+__device__ __forceinline__ void put(float* p, float v) {
+    if (ACC) *p += v; else *p = v;
+}
+
+template <bool ACC>
+__global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.P) return;
+    const bool vis = a.tiles[i] > 0;
+    // pass-through gradients first (means2D in NDC units, colours)
+    const float2 g2 = vis ? a.g_mean2D[i] : make_float2(0.0f, 0.0f);
+    const float gx = g2.x, gy = g2.y;
+    float3 gcol = make_float3(0.0f, 0.0f, 0.0f);
+    if (vis) gcol = make_float3(a.g_color[3 * i], a.g_color[3 * i + 1], a.g_color[3 * i + 2]);
+    if (a.dmeans2D) { put<ACC>(a.dmeans2D + 3 * (size_t)i, gx); put<ACC>(a.dmeans2D + 3 * (size_t)i + 1, gy); put<ACC>(a.dmeans2D + 3 * (size_t)i + 2, 0.0f); }
+    if (a.dcolors) { put<ACC>(a.dcolors + 3 * (size_t)i, gcol.x); put<ACC>(a.dcolors + 3 * (size_t)i + 1, gcol.y); put<ACC>(a.dcolors + 3 * (size_t)i + 2, gcol.z); }
+
+    float3 dm = make_float3(0.0f, 0.0f, 0.0f);
+    float dcov[6] = {0, 0, 0, 0, 0, 0};
+    float3 dscale = make_float3(0.0f, 0.0f, 0.0f);
+    float4 drot = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const int M = a.M;
+    if (vis) {
+        const float3 p = make_float3(a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]);
+        float c3[6];
+        float3 sc = make_float3(0.0f, 0.0f, 0.0f);
+        float4 q = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (a.cov3D_precomp) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k) c3[k] = a.cov3D_precomp[6 * (size_t)i + k];
+        } else {
+            sc = make_float3(a.scales[3 * i], a.scales[3 * i + 1], a.scales[3 * i + 2]);
+            q = reinterpret_cast<const float4*>(a.rotations)[i];
+            cov3d(sc, a.scale_modifier, q, c3);
+        }
+        const float4 gc = a.g_conic[i];   // (x, y, w) of the upstream float4, packed as x, y, z
+        cov2d_bwd(p, c3, a.focal_x, a.focal_y, a.tanfovx, a.tanfovy, a.view, make_float3(gc.x, gc.y, gc.z), dm, dcov);
+        // projection of the mean
+        const float* pm = a.proj;
+        const float4 mh = xform4x4(pm, p);
+        const float mw = 1.0f / (mh.w + 0.0000001f);
+        const float mul1 = (pm[0] * p.x + pm[4] * p.y + pm[8] * p.z + pm[12]) * mw * mw;
+        const float mul2 = (pm[1] * p.x + pm[5] * p.y + pm[9] * p.z + pm[13]) * mw * mw;
+        dm.x += (pm[0] * mw - pm[3] * mul1) * gx + (pm[1] * mw - pm[3] * mul2) * gy;
+        dm.y += (pm[4] * mw - pm[7] * mul1) * gx + (pm[5] * mw - pm[7] * mul2) * gy;
+        dm.z += (pm[8] * mw - pm[11] * mul1) * gx + (pm[9] * mw - pm[11] * mul2) * gy;
+        // depth row
+        const float gd = gc.w;
+        dm.x += a.view[2] * gd;
+        dm.y += a.view[6] * gd;
+        dm.z += a.view[10] * gd;
+        // SH
+        if (a.shs) {
+            const float3 dir_orig = make_float3(p.x - a.campos[0], p.y - a.campos[1], p.z - a.campos[2]);
+            const float len = sqrtf(dir_orig.x * dir_orig.x + dir_orig.y * dir_orig.y + dir_orig.z * dir_orig.z);
+            const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
+            const uint8_t cl = a.clamped[i];
+            const float dR[3] = {(cl & 1) ? 0.0f : gcol.x, (cl & 2) ? 0.0f : gcol.y, (cl & 4) ? 0.0f : gcol.z};
+            const float* sh = a.shs + (size_t)i * M * 3;
+            float* dsh = a.dsh ? a.dsh + (size_t)i * M * 3 : nullptr;
+            const int deg = a.deg;
+            float dRdx[3] = {0, 0, 0}, dRdy[3] = {0, 0, 0}, dRdz[3] = {0, 0, 0};
+            float g[16];
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) {
+#define SHc(k) sh[(k) * 3 + ch]
+#pragma unroll
+                for (int k = 0; k < 16; ++k) g[k] = 0.0f;
+                g[0] = SH_C0 * dR[ch];
+                if (deg > 0) {
+                    g[1] = -SH_C1 * y * dR[ch]; g[2] = SH_C1 * z * dR[ch]; g[3] = -SH_C1 * x * dR[ch];
+                    dRdx[ch] = -SH_C1 * SHc(3); dRdy[ch] = -SH_C1 * SHc(1); dRdz[ch] = SH_C1 * SHc(2);
+                    if (deg > 1) {
+                        const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+                        g[4] = SH_C2[0] * xy * dR[ch]; g[5] = SH_C2[1] * yz * dR[ch];
+                        g[6] = SH_C2[2] * (2.0f * zz - xx - yy) * dR[ch]; g[7] = SH_C2[3] * xz * dR[ch];
+                        g[8] = SH_C2[4] * (xx - yy) * dR[ch];
+                        dRdx[ch] += SH_C2[0] * y * SHc(4) + SH_C2[2] * 2.0f * -x * SHc(6) + SH_C2[3] * z * SHc(7) + SH_C2[4] * 2.0f * x * SHc(8);
+                        dRdy[ch] += SH_C2[0] * x * SHc(4) + SH_C2[1] * z * SHc(5) + SH_C2[2] * 2.0f * -y * SHc(6) + SH_C2[4] * 2.0f * -y * SHc(8);
+                        dRdz[ch] += SH_C2[1] * y * SHc(5) + SH_C2[2] * 2.0f * 2.0f * z * SHc(6) + SH_C2[3] * x * SHc(7);
+                        if (deg > 2) {
+                            g[9] = SH_C3[0] * y * (3.0f * xx - yy) * dR[ch];
+                            g[10] = SH_C3[1] * xy * z * dR[ch];
+                            g[11] = SH_C3[2] * y * (4.0f * zz - xx - yy) * dR[ch];
+                            g[12] = SH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * dR[ch];
+                            g[13] = SH_C3[4] * x * (4.0f * zz - xx - yy) * dR[ch];
+                            g[14] = SH_C3[5] * z * (xx - yy) * dR[ch];
+                            g[15] = SH_C3[6] * x * (xx - 3.0f * yy) * dR[ch];
+                            dRdx[ch] += SH_C3[0] * SHc(9) * 3.0f * 2.0f * xy + SH_C3[1] * SHc(10) * yz + SH_C3[2] * SHc(11) * -2.0f * xy +
+                                        SH_C3[3] * SHc(12) * -3.0f * 2.0f * xz + SH_C3[4] * SHc(13) * (-3.0f * xx + 4.0f * zz - yy) +
+                                        SH_C3[5] * SHc(14) * 2.0f * xz + SH_C3[6] * SHc(15) * 3.0f * (xx - yy);
+                            dRdy[ch] += SH_C3[0] * SHc(9) * 3.0f * (xx - yy) + SH_C3[1] * SHc(10) * xz +
+                                        SH_C3[2] * SHc(11) * (-3.0f * yy + 4.0f * zz - xx) + SH_C3[3] * SHc(12) * -3.0f * 2.0f * yz +
+                                        SH_C3[4] * SHc(13) * -2.0f * xy + SH_C3[5] * SHc(14) * -2.0f * yz + SH_C3[6] * SHc(15) * -3.0f * 2.0f * xy;
+                            dRdz[ch] += SH_C3[1] * SHc(10) * xy + SH_C3[2] * SHc(11) * 4.0f * 2.0f * yz +
+                                        SH_C3[3] * SHc(12) * 3.0f * (2.0f * zz - xx - yy) + SH_C3[4] * SHc(13) * 4.0f * 2.0f * xz +
+                                        SH_C3[5] * SHc(14) * (xx - yy);
+                        }
+                    }
+                }
+#undef SHc
+                if (dsh) {
+                    for (int k = 0; k < M; ++k) put<ACC>(dsh + k * 3 + ch, k < 16 ? g[k] : 0.0f);
+                }
+            }
+            const float dLdx = dRdx[0] * dR[0] + dRdx[1] * dR[1] + dRdx[2] * dR[2];
+            const float dLdy = dRdy[0] * dR[0] + dRdy[1] * dR[1] + dRdy[2] * dR[2];
+            const float dLdz = dRdz[0] * dR[0] + dRdz[1] * dR[1] + dRdz[2] * dR[2];
+            const float3 v = dir_orig;
+            const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
+            const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+            dm.x += ((sum2 - v.x * v.x) * dLdx - v.y * v.x * dLdy - v.z * v.x * dLdz) * invsum32;
+            dm.y += (-v.x * v.y * dLdx + (sum2 - v.y * v.y) * dLdy - v.z * v.y * dLdz) * invsum32;
+            dm.z += (-v.x * v.z * dLdx - v.y * v.z * dLdy + (sum2 - v.z * v.z) * dLdz) * invsum32;
+        }
+        if (!a.cov3D_precomp) cov3d_bwd(sc, a.scale_modifier, q, dcov, dscale, drot);
+    } else if (a.dsh && !ACC) {
+        float* dsh = a.dsh + (size_t)i * M * 3;
+        for (int k = 0; k < 3 * M; ++k) dsh[k] = 0.0f;
+    }
+    if (a.dmeans3D) { put<ACC>(a.dmeans3D + 3 * (size_t)i, dm.x); put<ACC>(a.dmeans3D + 3 * (size_t)i + 1, dm.y); put<ACC>(a.dmeans3D + 3 * (size_t)i + 2, dm.z); }
+    if (a.dcov3D) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) put<ACC>(a.dcov3D + 6 * (size_t)i + k, a.cov3D_precomp ? dcov[k] : dcov[k]);
+    }
+    if (a.dscales) { put<ACC>(a.dscales + 3 * (size_t)i, dscale.x); put<ACC>(a.dscales + 3 * (size_t)i + 1, dscale.y); put<ACC>(a.dscales + 3 * (size_t)i + 2, dscale.z); }
+    if (a.drots) {
+        put<ACC>(a.drots + 4 * (size_t)i, drot.x); put<ACC>(a.drots + 4 * (size_t)i + 1, drot.y);
+        put<ACC>(a.drots + 4 * (size_t)i + 2, drot.z); put<ACC>(a.drots + 4 * (size_t)i + 3, drot.w);
+    }
+}
+
+void launch_preprocess_bwd(const PreprocessBwdArgs& a, bool accumulate, hipStream_t st) {
+    if (a.P == 0) return;
+    if (accumulate) hipLaunchKernelGGL(k_preprocess_bwd<true>, dim3((a.P + 255) / 256), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(k_preprocess_bwd<false>, dim3((a.P + 255) / 256), dim3(256), 0, st, a);
+}
+
+}  // namespace lsr

@@ -1,0 +1,306 @@
+"""diff_gaussian_rasterization -- drop-in Python surface of the 4D-LangSplat rasterizer, backed by
+the MI355X-native liblsr.so (HIP, gfx950) through its C ABI (include/lsr.h).
+
+Mirrors what the reference imports and calls (the submodule zrporz/4d-langsplat-rasterization is
+un-vendored, so the surface is taken from its call sites):
+  from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+      gaussian_renderer/__init__.py:15, scene/dataset_readers.py:492
+  GaussianRasterizationSettings(image_height, image_width, tanfovx, tanfovy, bg, scale_modifier,
+      viewmatrix, projmatrix, sh_degree, campos, prefiltered, debug, include_feature)
+      gaussian_renderer/__init__.py:49-63 (include_feature defaults to True because
+      scene/dataset_readers.py:502-515 builds the settings without it)
+  rasterizer(means3D=, means2D=, shs=, colors_precomp=, language_feature_precomp=, opacities=,
+      scales=, rotations=, cov3D_precomp=) -> (color [3,H,W], language_feature [C,H,W],
+      radii int32 [P], depth [1,H,W])            gaussian_renderer/__init__.py:219-228
+  rasterizer.markVisible(positions) -> bool [P]
+Errors follow upstream: exactly one of shs / colors_precomp, exactly one of (scales, rotations) /
+cov3D_precomp, else an Exception with the upstream message; native failures raise RuntimeError.
+means2D's values are ignored; its .grad receives the screen-space gradient (NDC units).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import NamedTuple, Optional
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+
+__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "RasterizerState",
+           "forward_native", "backward_native"]
+
+_lib.load()   # fail loudly at import if the native library is missing
+
+
+class GaussianRasterizationSettings(NamedTuple):
+    image_height: int
+    image_width: int
+    tanfovx: float
+    tanfovy: float
+    bg: torch.Tensor
+    scale_modifier: float
+    viewmatrix: torch.Tensor
+    projmatrix: torch.Tensor
+    sh_degree: int
+    campos: torch.Tensor
+    prefiltered: bool
+    debug: bool
+    include_feature: bool = True
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _opt(t):
+    """upstream passes torch.Tensor([]) for 'not provided'"""
+    if t is None or t.numel() == 0:
+        return None
+    return t
+
+
+def _f32(t, device):
+    return t.detach().to(device=device, dtype=torch.float32).contiguous()
+
+
+class _NativeSettings:
+    """Keeps the device copies of the small settings tensors alive for the duration of a call."""
+
+    def __init__(self, rs: GaussianRasterizationSettings, device):
+        self.bg = _f32(rs.bg, device).reshape(-1)
+        self.view = _f32(rs.viewmatrix, device).reshape(-1)
+        self.proj = _f32(rs.projmatrix, device).reshape(-1)
+        self.campos = _f32(rs.campos, device).reshape(-1)
+        if self.bg.numel() != 3 or self.view.numel() != 16 or self.proj.numel() != 16 or self.campos.numel() != 3:
+            raise ValueError("bg/campos must have 3 elements and view/proj matrices 16")
+        s = _lib.Settings()
+        s.image_height, s.image_width = int(rs.image_height), int(rs.image_width)
+        s.tanfovx, s.tanfovy = float(rs.tanfovx), float(rs.tanfovy)
+        s.bg, s.scale_modifier = self.bg.data_ptr(), float(rs.scale_modifier)
+        s.viewmatrix, s.projmatrix = self.view.data_ptr(), self.proj.data_ptr()
+        s.sh_degree, s.campos = int(rs.sh_degree), self.campos.data_ptr()
+        s.prefiltered, s.debug = int(bool(rs.prefiltered)), int(bool(rs.debug))
+        s.include_feature = int(bool(rs.include_feature))
+        self.c = s
+
+
+class RasterizerState:
+    """What the forward leaves for the backward (upstream: num_rendered + geom/binning/img buffers)."""
+
+    def __init__(self, settings, inputs, fin, geom, binning, img, num_rendered, radii):
+        self.settings, self.inputs, self.fin = settings, inputs, fin
+        self.geom, self.binning, self.img = geom, binning, img
+        self.num_rendered, self.radii = num_rendered, radii
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def forward_native(raster_settings, means3D, opacities, shs=None, colors_precomp=None, language_feature=None,
+                   scales=None, rotations=None, cov3D_precomp=None):
+    """Forward through liblsr.so.  Returns (color, language_feature, radii, depth, state)."""
+    device = means3D.device
+    if device.type != "cuda":
+        raise RuntimeError("the rasterizer runs on the GPU only (no CPU fallback); got tensors on " + str(device))
+    L = _lib.load()
+    st = _NativeSettings(raster_settings, device)
+    P = means3D.shape[0]
+    means3D = _f32(means3D, device)
+    opacities = _f32(opacities, device)
+    shs = _opt(shs)
+    colors_precomp = _opt(colors_precomp)
+    language_feature = _opt(language_feature)
+    scales, rotations, cov3D_precomp = _opt(scales), _opt(rotations), _opt(cov3D_precomp)
+    shs = _f32(shs, device) if shs is not None else None
+    colors_precomp = _f32(colors_precomp, device) if colors_precomp is not None else None
+    language_feature = _f32(language_feature, device).reshape(P, -1) if language_feature is not None else None
+    scales = _f32(scales, device) if scales is not None else None
+    rotations = _f32(rotations, device) if rotations is not None else None
+    cov3D_precomp = _f32(cov3D_precomp, device) if cov3D_precomp is not None else None
+    M = shs.reshape(P, -1, 3).shape[1] if shs is not None else 0
+    C = language_feature.shape[1] if language_feature is not None else 0
+    fin = _lib.FwdIn()
+    fin.P, fin.M, fin.C = P, M, C
+    fin.means3D, fin.shs, fin.colors_precomp = means3D.data_ptr(), _ptr(shs), _ptr(colors_precomp)
+    fin.language_feature, fin.opacities = _ptr(language_feature), opacities.data_ptr()
+    fin.scales, fin.rotations, fin.cov3D_precomp = _ptr(scales), _ptr(rotations), _ptr(cov3D_precomp)
+    H, W = int(raster_settings.image_height), int(raster_settings.image_width)
+    radii = torch.empty(P, dtype=torch.int32, device=device)
+    color = torch.empty(3, H, W, dtype=torch.float32, device=device)
+    lang_out = torch.empty(C, H, W, dtype=torch.float32, device=device)
+    depth = torch.empty(1, H, W, dtype=torch.float32, device=device)
+    fout = _lib.FwdOut()
+    fout.out_color, fout.out_language_feature = color.data_ptr(), _ptr(lang_out) if C > 0 else None
+    fout.radii, fout.out_depth = radii.data_ptr(), depth.data_ptr()
+    geom = torch.empty(int(L.lsr_geom_bytes(P)), dtype=torch.uint8, device=device)
+    K = ctypes.c_int64(0)
+    stream = _stream(device)
+    try:
+        _lib.check(L.lsr_forward_preprocess(ctypes.byref(st.c), ctypes.byref(fin), ctypes.byref(fout),
+                                            ctypes.c_void_p(geom.data_ptr()), ctypes.byref(K), stream),
+                   "lsr_forward_preprocess")
+        binning = torch.empty(int(L.lsr_binning_bytes(K.value)), dtype=torch.uint8, device=device)
+        img = torch.empty(int(L.lsr_img_bytes(W, H)), dtype=torch.uint8, device=device)
+        _lib.check(L.lsr_forward_render(ctypes.byref(st.c), ctypes.byref(fin), ctypes.byref(fout),
+                                        ctypes.c_void_p(geom.data_ptr()), ctypes.c_void_p(binning.data_ptr()),
+                                        ctypes.c_void_p(img.data_ptr()), K, stream), "lsr_forward_render")
+    except RuntimeError:
+        if raster_settings.debug:
+            torch.save(dict(means3D=means3D.cpu(), opacities=opacities.cpu(), shs=None if shs is None else shs.cpu(),
+                            colors_precomp=None if colors_precomp is None else colors_precomp.cpu(),
+                            scales=None if scales is None else scales.cpu(),
+                            rotations=None if rotations is None else rotations.cpu()), "snapshot_fw.dump")
+            print("\nAn error occured in forward. Writing snapshot_fw.dump for debugging.")
+        raise
+    inputs = dict(means3D=means3D, opacities=opacities, shs=shs, colors_precomp=colors_precomp,
+                  language_feature=language_feature, scales=scales, rotations=rotations, cov3D_precomp=cov3D_precomp)
+    state = RasterizerState(st, inputs, fin, geom, binning, img, K.value, radii)
+    return color, lang_out, radii, depth, state
+
+
+def backward_native(state: RasterizerState, grad_color, grad_lang=None, grad_depth=None, out=None,
+                    accumulate=False, need=None):
+    """Backward through liblsr.so.  `out` may hold preallocated gradient buffers (dict); with
+    accumulate=True they are added to.  Returns the dict of gradient tensors."""
+    L = _lib.load()
+    inp = state.inputs
+    means3D = inp["means3D"]
+    device = means3D.device
+    P, M, C = state.fin.P, state.fin.M, state.fin.C
+    H, W = state.settings.c.image_height, state.settings.c.image_width
+    need = need or {}
+
+    def buf(name, shape, wanted=True):
+        if not wanted:
+            return None
+        if out is not None and name in out and out[name] is not None:
+            return out[name]
+        return torch.zeros(shape, dtype=torch.float32, device=device) if accumulate else \
+            torch.empty(shape, dtype=torch.float32, device=device)
+
+    g = dict(
+        means3D=buf("means3D", (P, 3), need.get("means3D", True)),
+        means2D=buf("means2D", (P, 3), need.get("means2D", True)),
+        colors=buf("colors", (P, 3), need.get("colors", True)),
+        language_feature=buf("language_feature", (P, C), need.get("language_feature", True) and C > 0),
+        opacities=buf("opacities", (P, 1), need.get("opacities", True)),
+        cov3D=buf("cov3D", (P, 6), need.get("cov3D", True) and inp["cov3D_precomp"] is not None),
+        sh=buf("sh", (P, max(M, 1), 3), need.get("sh", True) and M > 0),
+        scales=buf("scales", (P, 3), need.get("scales", True) and inp["scales"] is not None),
+        rotations=buf("rotations", (P, 4), need.get("rotations", True) and inp["rotations"] is not None),
+    )
+    gc = grad_color.detach().to(torch.float32).contiguous() if grad_color is not None else \
+        torch.zeros(3, H, W, dtype=torch.float32, device=device)
+    gl = grad_lang.detach().to(torch.float32).contiguous() if (grad_lang is not None and C > 0) else None
+    gd = grad_depth.detach().to(torch.float32).contiguous() if grad_depth is not None else None
+    gin = _lib.BwdIn()
+    gin.dL_dout_color, gin.dL_dout_language_feature, gin.dL_dout_depth = gc.data_ptr(), _ptr(gl), _ptr(gd)
+    gout = _lib.BwdOut()
+    gout.dL_dmeans3D, gout.dL_dmeans2D, gout.dL_dcolors = _ptr(g["means3D"]), _ptr(g["means2D"]), _ptr(g["colors"])
+    gout.dL_dlanguage_feature, gout.dL_dopacity = _ptr(g["language_feature"]), _ptr(g["opacities"])
+    gout.dL_dcov3D, gout.dL_dsh = _ptr(g["cov3D"]), _ptr(g["sh"])
+    gout.dL_dscales, gout.dL_drotations = _ptr(g["scales"]), _ptr(g["rotations"])
+    scratch = torch.empty(int(L.lsr_backward_bytes(P, state.num_rendered, C)), dtype=torch.uint8, device=device)
+    rc = L.lsr_backward(ctypes.byref(state.settings.c), ctypes.byref(state.fin), ctypes.byref(gin), ctypes.byref(gout),
+                        ctypes.c_void_p(state.geom.data_ptr()), ctypes.c_void_p(state.binning.data_ptr()),
+                        ctypes.c_void_p(state.img.data_ptr()), ctypes.c_void_p(scratch.data_ptr()),
+                        ctypes.c_int64(state.num_rendered), ctypes.c_int32(1 if accumulate else 0), _stream(device))
+    if rc != 0 and state.settings.c.debug:
+        print("\nAn error occured in backward. Writing snapshot_bw.dump for debugging.")
+        torch.save(dict(grad_color=gc.cpu()), "snapshot_bw.dump")
+    _lib.check(rc, "lsr_backward")
+    return g
+
+
+class _RasterizeGaussians(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, means3D, means2D, sh, colors_precomp, language_feature_precomp, opacities, scales, rotations,
+                cov3Ds_precomp, raster_settings):
+        color, lang, radii, depth, state = forward_native(
+            raster_settings, means3D, opacities, shs=sh, colors_precomp=colors_precomp,
+            language_feature=language_feature_precomp if raster_settings.include_feature else None,
+            scales=scales, rotations=rotations, cov3D_precomp=cov3Ds_precomp)
+        if not raster_settings.include_feature and language_feature_precomp is not None \
+                and language_feature_precomp.numel() > 0:
+            # base stages: the caller passes zeros [P, hiddendim] and discards the output
+            lang = torch.zeros((language_feature_precomp.shape[-1],) + tuple(color.shape[1:]),
+                               dtype=color.dtype, device=color.device)
+        ctx.state = state
+        ctx.shapes = dict(sh=None if sh is None else sh.shape, opacities=opacities.shape,
+                          lang=None if language_feature_precomp is None else language_feature_precomp.shape)
+        ctx.include_feature = raster_settings.include_feature
+        ctx.mark_non_differentiable(radii)
+        ctx.set_materialize_grads(False)
+        return color, lang, radii, depth
+
+    @staticmethod
+    def backward(ctx, grad_color, grad_lang, grad_radii, grad_depth):
+        st = ctx.state
+        ng = ctx.needs_input_grad
+        need = dict(means3D=ng[0], means2D=ng[1], sh=ng[2], colors=True, language_feature=ng[4], opacities=ng[5],
+                    scales=ng[6], rotations=ng[7], cov3D=ng[8])
+        g = backward_native(st, grad_color, grad_lang if ctx.include_feature else None, grad_depth, need=need)
+        shp = ctx.shapes
+
+        def like(t, shape):
+            return None if (t is None or shape is None) else t.reshape(shape)
+
+        grad_lang_in = None
+        if ng[4] and shp["lang"] is not None and len(shp["lang"]) > 0:
+            if g["language_feature"] is not None:
+                grad_lang_in = g["language_feature"].reshape(shp["lang"])
+            else:
+                grad_lang_in = torch.zeros(shp["lang"], dtype=torch.float32, device=st.inputs["means3D"].device)
+        return (g["means3D"] if ng[0] else None,
+                g["means2D"] if ng[1] else None,
+                like(g["sh"], shp["sh"]) if ng[2] else None,
+                g["colors"] if ng[3] else None,
+                grad_lang_in,
+                like(g["opacities"], shp["opacities"]) if ng[5] else None,
+                g["scales"] if ng[6] else None,
+                g["rotations"] if ng[7] else None,
+                g["cov3D"] if ng[8] else None,
+                None)
+
+
+def rasterize_gaussians(means3D, means2D, sh, colors_precomp, language_feature_precomp, opacities, scales, rotations,
+                        cov3Ds_precomp, raster_settings):
+    return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, language_feature_precomp, opacities,
+                                     scales, rotations, cov3Ds_precomp, raster_settings)
+
+
+class GaussianRasterizer(nn.Module):
+    def __init__(self, raster_settings):
+        super().__init__()
+        self.raster_settings = raster_settings
+
+    def markVisible(self, positions):
+        with torch.no_grad():
+            rs = self.raster_settings
+            pos = _f32(positions, positions.device)
+            view = _f32(rs.viewmatrix, positions.device).reshape(-1)
+            proj = _f32(rs.projmatrix, positions.device).reshape(-1)
+            out = torch.empty(pos.shape[0], dtype=torch.uint8, device=positions.device)
+            L = _lib.load()
+            _lib.check(L.lsr_mark_visible(pos.shape[0], ctypes.c_void_p(pos.data_ptr()), ctypes.c_void_p(view.data_ptr()),
+                                          ctypes.c_void_p(proj.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                          _stream(positions.device)), "lsr_mark_visible")
+            return out.bool()
+
+    def forward(self, means3D, means2D, opacities, shs=None, colors_precomp=None, language_feature_precomp=None,
+                scales=None, rotations=None, cov3D_precomp=None):
+        rs = self.raster_settings
+        if (shs is None and colors_precomp is None) or (shs is not None and colors_precomp is not None):
+            raise Exception('Please provide excatly one of either SHs or precomputed colors!')
+        if ((scales is None or rotations is None) and cov3D_precomp is None) or \
+                ((scales is not None or rotations is not None) and cov3D_precomp is not None):
+            raise Exception('Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!')
+        empty = torch.Tensor([])
+        return rasterize_gaussians(means3D, means2D, shs if shs is not None else empty,
+                                   colors_precomp if colors_precomp is not None else empty,
+                                   language_feature_precomp if language_feature_precomp is not None else empty,
+                                   opacities, scales if scales is not None else empty,
+                                   rotations if rotations is not None else empty,
+                                   cov3D_precomp if cov3D_precomp is not None else empty, rs)

@@ -1,0 +1,116 @@
+"""ctypes binding of liblsr.so (include/lsr.h).  No torch types cross the boundary: only device
+pointers, sizes and the HIP stream handle.
+
+The library is built in-tree (4dlangsplat_amd/csrc/Makefile -> 4dlangsplat_amd/build/liblsr.so).
+There is no fallback: if the library is missing, importing the rasterizer raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("LSR_LIBRARY", os.path.join(_PKG, "build", "liblsr.so"))
+
+c_float_p = ctypes.c_void_p  # device pointers are passed as opaque addresses
+
+
+class Settings(ctypes.Structure):
+    _fields_ = [
+        ("image_height", ctypes.c_int32), ("image_width", ctypes.c_int32),
+        ("tanfovx", ctypes.c_float), ("tanfovy", ctypes.c_float),
+        ("bg", ctypes.c_void_p), ("scale_modifier", ctypes.c_float),
+        ("viewmatrix", ctypes.c_void_p), ("projmatrix", ctypes.c_void_p),
+        ("sh_degree", ctypes.c_int32), ("campos", ctypes.c_void_p),
+        ("prefiltered", ctypes.c_int32), ("debug", ctypes.c_int32), ("include_feature", ctypes.c_int32),
+    ]
+
+
+class FwdIn(ctypes.Structure):
+    _fields_ = [
+        ("P", ctypes.c_int32), ("M", ctypes.c_int32), ("C", ctypes.c_int32),
+        ("means3D", ctypes.c_void_p), ("shs", ctypes.c_void_p), ("colors_precomp", ctypes.c_void_p),
+        ("language_feature", ctypes.c_void_p), ("opacities", ctypes.c_void_p), ("scales", ctypes.c_void_p),
+        ("rotations", ctypes.c_void_p), ("cov3D_precomp", ctypes.c_void_p),
+    ]
+
+
+class FwdOut(ctypes.Structure):
+    _fields_ = [("out_color", ctypes.c_void_p), ("out_language_feature", ctypes.c_void_p),
+                ("radii", ctypes.c_void_p), ("out_depth", ctypes.c_void_p)]
+
+
+class BwdIn(ctypes.Structure):
+    _fields_ = [("dL_dout_color", ctypes.c_void_p), ("dL_dout_language_feature", ctypes.c_void_p),
+                ("dL_dout_depth", ctypes.c_void_p)]
+
+
+class BwdOut(ctypes.Structure):
+    _fields_ = [("dL_dmeans3D", ctypes.c_void_p), ("dL_dmeans2D", ctypes.c_void_p), ("dL_dcolors", ctypes.c_void_p),
+                ("dL_dlanguage_feature", ctypes.c_void_p), ("dL_dopacity", ctypes.c_void_p),
+                ("dL_dcov3D", ctypes.c_void_p), ("dL_dsh", ctypes.c_void_p), ("dL_dscales", ctypes.c_void_p),
+                ("dL_drotations", ctypes.c_void_p)]
+
+
+# every symbol include/lsr.h declares, with its ctypes signature
+SIGNATURES = {
+    "lsr_version": (ctypes.c_int, []),
+    "lsr_last_error": (ctypes.c_char_p, []),
+    "lsr_geom_bytes": (ctypes.c_int64, [ctypes.c_int32]),
+    "lsr_binning_bytes": (ctypes.c_int64, [ctypes.c_int64]),
+    "lsr_img_bytes": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32]),
+    "lsr_backward_bytes": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int64, ctypes.c_int32]),
+    "lsr_forward_preprocess": (ctypes.c_int, [ctypes.POINTER(Settings), ctypes.POINTER(FwdIn), ctypes.POINTER(FwdOut),
+                                              ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
+    "lsr_forward_render": (ctypes.c_int, [ctypes.POINTER(Settings), ctypes.POINTER(FwdIn), ctypes.POINTER(FwdOut),
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                          ctypes.c_void_p]),
+    "lsr_backward": (ctypes.c_int, [ctypes.POINTER(Settings), ctypes.POINTER(FwdIn), ctypes.POINTER(BwdIn),
+                                    ctypes.POINTER(BwdOut), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p]),
+    "lsr_mark_visible": (ctypes.c_int, [ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p]),
+    "lsr_profile_enable": (ctypes.c_int, [ctypes.c_int32]),
+    "lsr_profile_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64),
+                                        ctypes.c_int32]),
+}
+
+PHASES = ["preprocess", "depth_sort", "instance_scan", "emit", "tile_sort", "tile_ranges", "render_fwd",
+          "render_bwd", "preprocess_bwd"]
+
+
+def profile_enable(on=True):
+    load().lsr_profile_enable(1 if on else 0)
+
+
+def profile_read():
+    """{phase: (total_ms, launches)} of the event-timed phases since profile_enable()."""
+    n = len(PHASES)
+    ms = (ctypes.c_double * n)()
+    cnt = (ctypes.c_int64 * n)()
+    load().lsr_profile_read(ms, cnt, n)
+    return {PHASES[i]: (ms[i], cnt[i]) for i in range(n)}
+
+_LIB = None
+
+
+def load():
+    """Load liblsr.so (raises if it has not been built)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"liblsr.so not found at {LIB_PATH}; build it with `make -C 4dlangsplat_amd/csrc` "
+                              "(or __graft_entry__.build()).  There is no CPU fallback.")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = lib
+    return _LIB
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = load().lsr_last_error()
+        raise RuntimeError(f"{what} failed (code {rc}): {msg.decode() if msg else ''}")

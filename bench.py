@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""bench.py -- rasterizer fwd+bwd frames/s at 2M Gaussians, 1352x1014, 32 language channels.
+
+Workload (BASELINE.json configs[2] per GPU, configs[3] across GPUs): the synthetic S2M scene of
+SURVEY.md 8(d) (seeded; the Neu3D checkpoints are not available offline), replicated on every
+rank; each rank renders V views per step (default 8 = the 64-view batch of configs[3] over 8
+GPUs), forward + full backward of the rasterizer for each view, accumulating all Gaussian
+gradients in one flat fp32 buffer (means3D, scales, rotations, opacities, SH, language
+features = 59 + C floats per Gaussian); with N > 1 ranks the buffer is SUM all-reduced (RCCL)
+once per step.  Upstream gradients dL/dcolor, dL/dlanguage are fixed seeded tensors, so the
+step is the rasterizer alone.  Inputs are resident in HBM before the timed region.
+
+value = frames (views) rendered fwd+bwd by all ranks / max over ranks of the timed wall time.
+roofline: the dominant kernel (largest event-timed phase), algorithmic bytes per launch (the
+per-phase formulas below) / its mean launch time (hipEvents on the launch stream).
+cpu_baseline: the C oracle (oracle/, OpenMP) on one headline frame fwd+bwd, rank 0 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "4dlangsplat_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def phase_bytes(phase, P, Pvis, K, npix, ntiles, C, M=16):
+    """Algorithmic HBM bytes of one launch of each phase (each byte counted once)."""
+    rec = 4 + 8 + 16 + 16 + 4 * C          # id + xy + conic/opacity + rgb/depth + language row
+    if phase == "preprocess":
+        return P * (12 + 12 + 16 + 4 + 4 * 3 * M) + P * (4 + 4 + 4) + Pvis * (8 + 16 + 16 + 1)
+    if phase == "depth_sort":
+        return 4 * P * (4 + 16) + 4 * P     # 4 passes: count reads keys, scatter reads + writes pairs
+    if phase == "instance_scan":
+        return P * (4 + 4 + 4 + 4)
+    if phase == "emit":
+        return Pvis * (4 + 4 + 4 + 8 + 4 + 4) + K * 8
+    if phase == "tile_sort":
+        return 2 * K * (4 + 16)
+    if phase == "tile_ranges":
+        return K * 4 + ntiles * 8
+    if phase == "render_fwd":
+        return K * rec + ntiles * 12 + npix * (4 * (3 + C + 1) + 8)
+    if phase == "render_bwd":
+        return K * rec + ntiles * 12 + npix * (4 * (3 + C + 1) + 8) + Pvis * (8 + 16 + 12 + 4 + 4 * C)
+    if phase == "preprocess_bwd":
+        return Pvis * (12 + 12 + 16 + 4 * 3 * M + 1 + 4 + 8 + 16 + 12) + P * 4 * (3 + 3 + 4 + 3 * M)
+    return 0
+
+
+def cpu_baseline(scene, cam, C, threads):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    s = oracle.OracleSettings(cam.image_height, cam.image_width, cam.tanfovx, cam.tanfovy, np.ones(3, np.float32),
+                              1.0, cam.world_view_transform.numpy(), cam.full_proj_transform.numpy(), 3,
+                              cam.camera_center.numpy(), True)
+    H, W = cam.image_height, cam.image_width
+    rng = np.random.default_rng(0)
+    gc = rng.normal(size=(3, H, W)).astype(np.float32)
+    gl = rng.normal(size=(C, H, W)).astype(np.float32)
+    args = dict(shs=scene.shs.numpy(), lang=scene.lang.numpy(), scales=scene.scales.numpy(),
+                rotations=scene.rotations.numpy(), nthreads=threads)
+    t0 = time.perf_counter()
+    r = oracle.forward(s, scene.means3D.numpy(), scene.opacities.numpy(), **args)
+    t1 = time.perf_counter()
+    r.backward(gc, gl, None, nthreads=threads)
+    t2 = time.perf_counter()
+    r.close()
+    return t2 - t0, t1 - t0, t2 - t1
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--views", type=int, default=8, help="views per GPU per step")
+    ap.add_argument("--gaussians", type=int, default=2_000_000)
+    ap.add_argument("--channels", type=int, default=32)
+    ap.add_argument("--width", type=int, default=1352)
+    ap.add_argument("--height", type=int, default=1014)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="oracle threads (0 = min(16, cpus))")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import diff_gaussian_rasterization as dgr
+    from diff_gaussian_rasterization import _lib
+    import synthetic
+
+    P, C, W, H, V = args.gaussians, args.channels, args.width, args.height, args.views
+    tanfovx = 0.6
+    scene_cpu = synthetic.make_scene(P, C=C, tanfovx=tanfovx, tanfovy=tanfovx * H / W)
+    scene = scene_cpu.to(dev)
+    cams = synthetic.camera_batch(world * V, W, H, tanfovx=tanfovx, seed=1)[rank * V:(rank + 1) * V]
+    bg = torch.ones(3, device=dev)
+    settings = [dgr.GaussianRasterizationSettings(H, W, c.tanfovx, c.tanfovy, bg, 1.0, c.world_view_transform.to(dev),
+                                                  c.full_proj_transform.to(dev), 3, c.camera_center.to(dev), False,
+                                                  False, True) for c in cams]
+    g = torch.Generator(device="cpu").manual_seed(123)
+    gcol = (torch.randn(3, H, W, generator=g) * 1e-3).to(dev)
+    glang = (torch.randn(C, H, W, generator=g) * 1e-3).to(dev)
+    M = scene.shs.shape[1]
+    nfl = 3 + 3 + 4 + 1 + 3 * M + C
+    flat = torch.zeros(P * nfl, device=dev)
+    views, o = {}, 0
+    for name, w in (("means3D", 3), ("scales", 3), ("rotations", 4), ("opacities", 1), ("sh", 3 * M),
+                    ("language_feature", C)):
+        views[name] = flat[o * P:(o + w) * P].view(P, w) if name != "sh" else flat[o * P:(o + w) * P].view(P, M, 3)
+        o += w
+    need = dict(means2D=False, colors=False, cov3D=False)
+    stream = torch.cuda.current_stream(dev)
+    Ks = []
+
+    def step():
+        flat.zero_()
+        for rs in settings:
+            _, _, _, _, st = dgr.forward_native(rs, scene.means3D, scene.opacities, shs=scene.shs,
+                                                language_feature=scene.lang, scales=scene.scales,
+                                                rotations=scene.rotations)
+            Ks.append(st.num_rendered)
+            dgr.backward_native(st, gcol, glang, None, out=views, accumulate=True, need=need)
+        if world > 1:
+            dist.all_reduce(flat)
+
+    for _ in range(args.warmup):
+        step()
+    Ks.clear()
+    if not args.no_profile:
+        torch.cuda.synchronize(dev)
+        _lib.profile_enable(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    prof = _lib.profile_read() if not args.no_profile else {}
+    _lib.profile_enable(False)
+    el = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    frames = world * V * args.steps
+    value = frames / elapsed
+    del stream
+
+    if rank == 0:
+        Kmean = float(np.mean(Ks)) if Ks else 0.0
+        with torch.no_grad():
+            _, _, radii, _, _ = dgr.forward_native(settings[0], scene.means3D, scene.opacities, shs=scene.shs,
+                                                   language_feature=scene.lang, scales=scene.scales,
+                                                   rotations=scene.rotations)
+            Pvis = int((radii > 0).sum())
+        ntiles = ((W + 15) // 16) * ((H + 15) // 16)
+        roof = None
+        phases = {}
+        if prof:
+            for k, (ms, n) in prof.items():
+                if n:
+                    phases[k] = dict(mean_ms=ms / n, launches=n, gbs=phase_bytes(k, P, Pvis, Kmean, W * H, ntiles, C, M)
+                                     / (ms / n * 1e-3) / 1e9)
+            dom = max(prof, key=lambda k: prof[k][0])
+            ms, n = prof[dom]
+            byts = phase_bytes(dom, P, Pvis, Kmean, W * H, ntiles, C, M)
+            ach = byts / (ms / n * 1e-3) / 1e9
+            traffic = None
+            pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+            if os.path.exists(pmc):
+                try:
+                    traffic = json.load(open(pmc)).get(dom, {}).get("hbm_bytes_per_launch")
+                except Exception:
+                    traffic = None
+            roof = dict(kernel=dom, bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                        frac=round(ach / HBM_PEAK_GBS, 4), traffic=traffic, algorithmic_bytes=int(byts),
+                        mean_launch_ms=round(ms / n, 4))
+        cpu = None
+        if not args.no_cpu_baseline:
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            tot, tf, tb = cpu_baseline(scene_cpu, synthetic.camera_batch(1, W, H, tanfovx=tanfovx, seed=1)[0], C, threads)
+            cpu = dict(value=round(1.0 / tot, 5), unit="frames/s", cores=threads, kind="port",
+                       sample=f"1 headline frame (P={P}, {W}x{H}, C={C}) fwd {tf:.2f}s + bwd {tb:.2f}s, "
+                              f"C oracle oracle/lsr_oracle.c, OpenMP {threads} threads")
+        line = dict(
+            metric="rasterizer fwd+bwd frames/sec @ 2M Gaussians, 1352x1014, 32-ch features",
+            value=round(value, 3), unit="frames/s", n_gpus=world, steps=args.steps, warmup=args.warmup,
+            ms_per_step=round(elapsed / args.steps * 1e3, 3), higher_is_better=True, scaling="weak",
+            vs_baseline=None, dtype="f32", data="synthetic",
+            config=dict(workload="S2M synthetic (BASELINE configs[2] per GPU; configs[3] batch split)",
+                        gaussians=P, width=W, height=H, channels=C, views_per_gpu_per_step=V,
+                        global_batch=world * V, parallelism=f"dp{world}", num_rendered_mean=int(Kmean),
+                        visible=Pvis),
+            roofline=roof, cpu_baseline=cpu,
+            phases={k: dict(mean_ms=round(v["mean_ms"], 4), gbs=round(v["gbs"], 1)) for k, v in phases.items()},
+        )
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,154 @@
+/*
+ * lsr.h -- C ABI of liblsr.so, the MI355X-native (gfx950, HIP) 4D language-feature Gaussian
+ * rasterizer.  Drop-in for the native half of diff_gaussian_rasterization as used by 4D-LangSplat.
+ *
+ * Reference interface this replaces (the un-vendored submodule zrporz/4d-langsplat-rasterization,
+ * /root/reference/.gitmodules:4-6; source absent, so the binding is cited at its call sites):
+ *   - GaussianRasterizationSettings(...)            gaussian_renderer/__init__.py:49-63,
+ *                                                    scene/dataset_readers.py:502-515
+ *   - GaussianRasterizer(raster_settings)(means3D, means2D, shs, colors_precomp,
+ *       language_feature_precomp, opacities, scales, rotations, cov3D_precomp)
+ *       -> (color [3,H,W], language_feature [C,H,W], radii int32 [P], depth [1,H,W])
+ *                                                    gaussian_renderer/__init__.py:79,219-228
+ *   - _C.rasterize_gaussians            -> lsr_forward_preprocess + lsr_forward_render
+ *   - _C.rasterize_gaussians_backward   -> lsr_backward
+ *   - _C.mark_visible                   -> lsr_mark_visible
+ *   The upstream byte buffers (geomBuffer / binningBuffer / imgBuffer, sized through resize
+ *   callbacks) become caller-owned workspaces sized by the *_bytes queries below.
+ *
+ * Conventions
+ *   - Every pointer is a DEVICE pointer to contiguous memory: float32 except radii (int32) and
+ *     present (uint8).  Matrices are the torch world_view_transform / full_proj_transform
+ *     (flat 16 floats, row-vector convention: row 0 of the transform is m[0], m[4], m[8], m[12]).
+ *   - The library allocates nothing; the caller owns every input, output and workspace buffer.
+ *   - Every launch goes on `stream` (a hipStream_t).  The only host synchronisation is the read
+ *     of num_rendered at the end of lsr_forward_preprocess (as upstream).
+ *   - Return value: 0 = success, otherwise an LSR_E* code; lsr_last_error() describes the last
+ *     failure of the calling thread.
+ *   - C (language channels) is a runtime value.  include_feature = 0 skips the language
+ *     channels (their output is written as zeros), as the 'base' training stages do.
+ */
+#ifndef LSR_H_
+#define LSR_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LSR_API_VERSION 1
+
+#define LSR_OK 0
+#define LSR_EINVAL 1     /* bad argument (null pointer, exactly-one-of violation, size) */
+#define LSR_EHIP 2       /* HIP runtime / launch error */
+#define LSR_ECAPACITY 3  /* workspace too small */
+
+typedef void *lsr_stream_t; /* hipStream_t */
+
+typedef struct lsr_settings {
+    int32_t image_height;
+    int32_t image_width;
+    float tanfovx;
+    float tanfovy;
+    const float *bg;          /* [3] */
+    float scale_modifier;
+    const float *viewmatrix;  /* [16] world_view_transform */
+    const float *projmatrix;  /* [16] full_proj_transform */
+    int32_t sh_degree;        /* active SH degree, 0..3 */
+    const float *campos;      /* [3] camera centre */
+    int32_t prefiltered;
+    int32_t debug;            /* 1: synchronise and check after every kernel */
+    int32_t include_feature;
+} lsr_settings;
+
+typedef struct lsr_fwd_in {
+    int32_t P;                        /* Gaussians */
+    int32_t M;                        /* SH coefficients per Gaussian (shs.shape[1]); 0 if shs == NULL */
+    int32_t C;                        /* language-feature channels (0 allowed) */
+    const float *means3D;             /* [P,3] */
+    const float *shs;                 /* [P,M,3]  exactly one of shs / colors_precomp */
+    const float *colors_precomp;      /* [P,3] */
+    const float *language_feature;    /* [P,C]  (may be NULL when C == 0) */
+    const float *opacities;           /* [P]    activated */
+    const float *scales;              /* [P,3]  activated; with rotations, or cov3D_precomp */
+    const float *rotations;           /* [P,4]  activated (normalised) */
+    const float *cov3D_precomp;       /* [P,6] */
+} lsr_fwd_in;
+
+typedef struct lsr_fwd_out {
+    float *out_color;                 /* [3,H,W] */
+    float *out_language_feature;      /* [C,H,W] (may be NULL when C == 0) */
+    int32_t *radii;                   /* [P] */
+    float *out_depth;                 /* [1,H,W] */
+} lsr_fwd_out;
+
+typedef struct lsr_bwd_in {
+    const float *dL_dout_color;              /* [3,H,W] */
+    const float *dL_dout_language_feature;   /* [C,H,W] or NULL (treated as zero) */
+    const float *dL_dout_depth;              /* [1,H,W] or NULL (treated as zero) */
+} lsr_bwd_in;
+
+typedef struct lsr_bwd_out {                 /* any pointer may be NULL if that gradient is unused */
+    float *dL_dmeans3D;               /* [P,3] */
+    float *dL_dmeans2D;               /* [P,3] NDC units (x 0.5 W, 0.5 H), z = 0 */
+    float *dL_dcolors;                /* [P,3] */
+    float *dL_dlanguage_feature;      /* [P,C] */
+    float *dL_dopacity;               /* [P]   */
+    float *dL_dcov3D;                 /* [P,6] */
+    float *dL_dsh;                    /* [P,M,3] */
+    float *dL_dscales;                /* [P,3] */
+    float *dL_drotations;             /* [P,4] */
+} lsr_bwd_out;
+
+int lsr_version(void);
+const char *lsr_last_error(void);
+
+/* Workspace sizes in bytes (upstream geomBuffer / binningBuffer / imgBuffer + backward scratch). */
+int64_t lsr_geom_bytes(int32_t P);
+int64_t lsr_binning_bytes(int64_t num_rendered);
+int64_t lsr_img_bytes(int32_t image_width, int32_t image_height);
+int64_t lsr_backward_bytes(int32_t P, int64_t num_rendered, int32_t C);
+
+/* Forward, phase 1: per-Gaussian preprocess (cull, EWA projection, SH colour, tile count) and
+ * the depth ordering of the visible set.  Writes out->radii.  Returns num_rendered, the number of
+ * (Gaussian, tile) instances; the caller then sizes `binning`.  Synchronises `stream`. */
+int lsr_forward_preprocess(const lsr_settings *s, const lsr_fwd_in *in, lsr_fwd_out *out, void *geom,
+                           int64_t *num_rendered, lsr_stream_t stream);
+
+/* Forward, phase 2: tile binning and compositing of RGB + C language channels + depth.
+ * `geom` is the buffer phase 1 filled; `binning` holds >= lsr_binning_bytes(num_rendered) bytes. */
+int lsr_forward_render(const lsr_settings *s, const lsr_fwd_in *in, lsr_fwd_out *out, void *geom,
+                       void *binning, void *img, int64_t num_rendered, lsr_stream_t stream);
+
+/* Backward through compositing and preprocess.  accumulate != 0 adds into the outputs instead of
+ * overwriting them (multi-view gradient accumulation).  `scratch` holds >= lsr_backward_bytes. */
+int lsr_backward(const lsr_settings *s, const lsr_fwd_in *in, const lsr_bwd_in *gin, lsr_bwd_out *gout,
+                 const void *geom, const void *binning, const void *img, void *scratch, int64_t num_rendered,
+                 int32_t accumulate, lsr_stream_t stream);
+
+/* markVisible: present[i] = (view-space z of means3D[i]) > 0.2 */
+int lsr_mark_visible(int32_t P, const float *means3D, const float *viewmatrix, const float *projmatrix,
+                     uint8_t *present, lsr_stream_t stream);
+
+/* Per-phase GPU timing (profiling aid): when enabled, every phase below is bracketed by hipEvents
+ * recorded on the caller's stream.  lsr_profile_read waits for the recorded events, adds their
+ * durations to per-phase totals (milliseconds) and launch counts, and returns LSR_NUM_PHASES. */
+#define LSR_PHASE_PREPROCESS 0
+#define LSR_PHASE_DEPTH_SORT 1
+#define LSR_PHASE_INSTANCE_SCAN 2
+#define LSR_PHASE_EMIT 3
+#define LSR_PHASE_TILE_SORT 4
+#define LSR_PHASE_TILE_RANGES 5
+#define LSR_PHASE_RENDER_FWD 6
+#define LSR_PHASE_RENDER_BWD 7
+#define LSR_PHASE_PREPROCESS_BWD 8
+#define LSR_NUM_PHASES 9
+int lsr_profile_enable(int32_t on);   /* resets the totals */
+int lsr_profile_read(double *ms_total, int64_t *launches, int32_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LSR_H_ */

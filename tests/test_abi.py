@@ -1,0 +1,69 @@
+"""CPU checks of the C ABI: liblsr.so builds for gfx950, loads, and exports exactly what
+include/lsr.h declares; the workspace size queries behave (no GPU compute is called here)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "lsr.h")
+
+
+def declared():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char \*)\s*(lsr_\w+)\s*\(", txt, re.M)))
+
+
+def test_header_declares_the_boundary():
+    names = declared()
+    for n in ("lsr_forward_preprocess", "lsr_forward_render", "lsr_backward", "lsr_mark_visible",
+              "lsr_geom_bytes", "lsr_binning_bytes", "lsr_img_bytes", "lsr_backward_bytes", "lsr_last_error",
+              "lsr_version"):
+        assert n in names
+
+
+def test_library_exports_every_declared_symbol():
+    from diff_gaussian_rasterization import _lib
+    lib = _lib.load()
+    for n in declared():
+        assert hasattr(lib, n), n
+    assert set(declared()) == set(_lib.SIGNATURES)
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (lsr_\w+)", out))
+    assert exported == set(declared())
+
+
+def test_library_is_built_for_gfx950():
+    from diff_gaussian_rasterization import _lib
+    out = subprocess.run(["strings", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    assert "gfx950" in out
+
+
+def test_size_queries():
+    from diff_gaussian_rasterization import _lib
+    lib = _lib.load()
+    assert lib.lsr_version() == 1
+    g1, g2 = lib.lsr_geom_bytes(1000), lib.lsr_geom_bytes(2_000_000)
+    assert 0 < g1 < g2 and g2 >= 2_000_000 * 60
+    assert lib.lsr_binning_bytes(8_600_000) >= 8_600_000 * 16
+    assert lib.lsr_img_bytes(1352, 1014) >= 1352 * 1014 * 8
+    assert lib.lsr_backward_bytes(2_000_000, 8_600_000, 32) >= 2_000_000 * 36
+
+
+def test_settings_validation_messages():
+    """Upstream's exactly-one-of errors are raised before anything touches a device."""
+    import torch
+    import diff_gaussian_rasterization as dgr
+    rs = dgr.GaussianRasterizationSettings(8, 8, 0.5, 0.5, torch.ones(3), 1.0, torch.eye(4), torch.eye(4), 0,
+                                           torch.zeros(3), False, False)
+    assert rs.include_feature is True       # dataset_readers.py:502-515 builds it without the field
+    r = dgr.GaussianRasterizer(rs)
+    m = torch.zeros(4, 3)
+    with pytest.raises(Exception, match="excatly one of either SHs or precomputed colors"):
+        r(means3D=m, means2D=m, opacities=torch.ones(4, 1), scales=m, rotations=torch.zeros(4, 4))
+    with pytest.raises(Exception, match="exactly one of either scale/rotation pair"):
+        r(means3D=m, means2D=m, opacities=torch.ones(4, 1), shs=torch.zeros(4, 16, 3))
+    with pytest.raises(RuntimeError, match="GPU only"):
+        r(means3D=m, means2D=m, opacities=torch.ones(4, 1), shs=torch.zeros(4, 16, 3), scales=m,
+          rotations=torch.zeros(4, 4))
