@@ -100,6 +100,7 @@ struct Geom {
     uint32_t* counts;
     uint32_t* offsets;
     uint32_t* inst_off;
+    int* radius;
     uint32_t* total;
     void* sort_tmp;
     void* scan_tmp;
@@ -119,6 +120,7 @@ Geom carve_geom(void* base, size_t P, size_t* bytes) {
     g.counts = c.take<uint32_t>(P);
     g.offsets = c.take<uint32_t>(P);
     g.inst_off = c.take<uint32_t>(P);
+    g.radius = c.take<int>(P);
     g.total = c.take<uint32_t>(4);
     g.sort_tmp = c.take<char>(lsr::radix_temp_bytes(P));
     g.scan_tmp = c.take<char>(lsr::scan_temp_bytes(P));
@@ -161,18 +163,14 @@ Img carve_img(void* base, int W, int H, size_t* bytes) {
 }
 
 struct Scratch {
-    float2* g_mean2D;
-    float4* g_conic;
-    float* g_color;
-    size_t zero_bytes;   // leading region zeroed per call
+    float* rec;          // [K, record_floats(C)] per-(Gaussian, tile) gradient records
+    uint8_t* flags;      // [K] record written
 };
-Scratch carve_scratch(void* base, size_t P, size_t* bytes) {
+Scratch carve_scratch(void* base, size_t K, int recq, size_t* bytes) {
     Carver c(base);
     Scratch s;
-    s.g_mean2D = c.take<float2>(P);
-    s.g_conic = c.take<float4>(P);
-    s.g_color = c.take<float>(3 * P);
-    s.zero_bytes = c.off;
+    s.rec = c.take<float>(K * (size_t)recq);
+    s.flags = c.take<uint8_t>(K);
     if (bytes) *bytes = c.off;
     return s;
 }
@@ -193,6 +191,7 @@ int check_common(const lsr_settings* s, const lsr_fwd_in* in) {
     if (!s->viewmatrix || !s->projmatrix || !s->bg || !s->campos)
         return fail(LSR_EINVAL, "viewmatrix, projmatrix, bg and campos are required");
     if (in->P > 0 && (!in->means3D || !in->opacities)) return fail(LSR_EINVAL, "means3D and opacities are required");
+    if (in->P == 0) return LSR_OK;   // nothing to validate or render (upstream returns early too)
     if ((in->shs == nullptr) == (in->colors_precomp == nullptr))
         return fail(LSR_EINVAL, "Please provide excatly one of either SHs or precomputed colors!");
     const bool sr = in->scales != nullptr || in->rotations != nullptr;
@@ -229,10 +228,9 @@ int64_t lsr_img_bytes(int32_t W, int32_t H) {
     return (int64_t)b;
 }
 int64_t lsr_backward_bytes(int32_t P, int64_t K, int32_t C) {
-    (void)K;
-    (void)C;
+    (void)P;
     size_t b;
-    carve_scratch(nullptr, (size_t)(P > 0 ? P : 1), &b);
+    carve_scratch(nullptr, (size_t)(K > 0 ? K : 1), lsr::record_floats(C > 0 ? C : 0), &b);
     return (int64_t)b;
 }
 
@@ -259,7 +257,7 @@ int lsr_forward_preprocess(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_
     a.means3D = in->means3D; a.scales = in->scales; a.rotations = in->rotations; a.opacities = in->opacities;
     a.shs = in->shs; a.colors_precomp = in->colors_precomp; a.cov3D_precomp = in->cov3D_precomp;
     a.view = s->viewmatrix; a.proj = s->projmatrix; a.campos = s->campos;
-    a.radii = out->radii; a.tiles = g.tiles; a.key = g.key_a; a.xy = g.xy; a.conic_o = g.conic_o; a.rgbd = g.rgbd;
+    a.radii = out->radii; a.radius = g.radius; a.tiles = g.tiles; a.key = g.key_a; a.xy = g.xy; a.conic_o = g.conic_o; a.rgbd = g.rgbd;
     a.clamped = g.clamped;
     LSR_HIP(hipMemsetAsync(g.clamped, 0, (size_t)P, st));
     {
@@ -357,23 +355,20 @@ int lsr_backward(const lsr_settings* s, const lsr_fwd_in* in, const lsr_bwd_in* 
     Geom g = carve_geom(const_cast<void*>(geom), (size_t)P, nullptr);
     Binning b = carve_binning(const_cast<void*>(binning), K > 0 ? K : 1, nullptr);
     Img m = carve_img(const_cast<void*>(img), W, H, nullptr);
-    Scratch sc = carve_scratch(scratch, (size_t)P, nullptr);
-    LSR_HIP(hipMemsetAsync(scratch, 0, sc.zero_bytes, st));
-    if (!accumulate) {
-        if (gout->dL_dlanguage_feature && C > 0)
-            LSR_HIP(hipMemsetAsync(gout->dL_dlanguage_feature, 0, sizeof(float) * (size_t)P * C, st));
-        if (gout->dL_dopacity) LSR_HIP(hipMemsetAsync(gout->dL_dopacity, 0, sizeof(float) * (size_t)P, st));
-    }
+    const int Ceff = s->include_feature ? C : 0;
+    const int recq = lsr::record_floats(Ceff);
+    Scratch sc = carve_scratch(scratch, K > 0 ? K : 1, recq, nullptr);
+    if (K > 0) LSR_HIP(hipMemsetAsync(sc.flags, 0, K, st));
     const uint32_t* point_list = tile_sort_in_b(gx * gy) ? b.val_b : b.val_a;
     if (K > 0) {
         lsr::RenderBwdArgs r{};
         r.W = W; r.H = H; r.grid_x = gx; r.grid_y = gy; r.C = C; r.include_feature = s->include_feature;
         r.ranges = m.ranges; r.point_list = point_list; r.xy = g.xy; r.conic_o = g.conic_o; r.rgbd = g.rgbd;
+        r.radius = g.radius; r.inst_off = g.inst_off;
         r.lang = in->language_feature; r.bg = s->bg; r.final_T = m.final_T; r.n_contrib = m.n_contrib;
         r.tile_max_contrib = m.tile_max;
         r.dL_dcolor = gin->dL_dout_color; r.dL_dlang = gin->dL_dout_language_feature; r.dL_ddepth = gin->dL_dout_depth;
-        r.g_mean2D = sc.g_mean2D; r.g_conic = sc.g_conic; r.g_color = sc.g_color;
-        r.g_lang = gout->dL_dlanguage_feature; r.g_opacity = gout->dL_dopacity;
+        r.rec = sc.rec; r.flags = sc.flags; r.recq = recq;
         {
             PhaseTimer t(LSR_PHASE_RENDER_BWD, st);
             lsr::launch_render_bwd(r, st);
@@ -388,15 +383,19 @@ int lsr_backward(const lsr_settings* s, const lsr_fwd_in* in, const lsr_bwd_in* 
     a.scale_modifier = s->scale_modifier;
     a.means3D = in->means3D; a.scales = in->scales; a.rotations = in->rotations; a.shs = in->shs;
     a.cov3D_precomp = in->cov3D_precomp; a.view = s->viewmatrix; a.proj = s->projmatrix; a.campos = s->campos;
+    a.tiles = g.tiles;
     a.clamped = g.clamped;
-    a.g_mean2D = sc.g_mean2D; a.g_conic = sc.g_conic; a.g_color = sc.g_color;
+    a.rec = sc.rec; a.flags = sc.flags; a.inst_off = g.inst_off; a.recq = recq;
+    a.dopacity = gout->dL_dopacity;
     a.dmeans3D = gout->dL_dmeans3D; a.dmeans2D = gout->dL_dmeans2D; a.dcolors = gout->dL_dcolors;
     a.dcov3D = gout->dL_dcov3D; a.dsh = in->shs ? gout->dL_dsh : nullptr; a.dscales = gout->dL_dscales;
     a.drots = gout->dL_drotations;
-    a.tiles = g.tiles;
     {
         PhaseTimer t(LSR_PHASE_PREPROCESS_BWD, st);
         lsr::launch_preprocess_bwd(a, accumulate != 0, st);
+        if (Ceff > 0)
+            lsr::launch_reduce_lang(P, C, lsr::lang_pad(C), recq, sc.rec, sc.flags, g.inst_off, g.tiles,
+                                    gout->dL_dlanguage_feature, accumulate != 0, st);
     }
     LSR_LAUNCHED("preprocess backward", st, s->debug);
     return LSR_OK;

@@ -2,8 +2,8 @@
 //
 // The whole library is compiled with -ffp-contract=off and correctly rounded f32 divide/sqrt, so
 // the preprocess arithmetic and the compositing decisions (alpha >= 1/255, T >= 1e-4, radius =
-// ceil(3 sqrt(lambda))) are reproducible bit for bit on the host; FMAs are written explicitly only
-// where a value is accumulated (channel sums), never where it feeds a comparison.
+// ceil(3 sqrt(lambda))) are reproducible bit for bit on the host; FMAs are written explicitly,
+// either where the host does the same fmaf (exp) or where a value is only accumulated.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -15,23 +15,30 @@
 
 namespace lsr {
 
-// Falloff exp for x <= 0: Cody-Waite reduction + degree-7 Horner, exponent assembled by bits.
-// <= 2 ulp, like CUDA expf; written with IEEE +,-,*, rint only so that it is reproducible.
+// Falloff exp for x <= 0: Cody-Waite reduction + degree-7 Horner in fma, exponent assembled by
+// bits.  <= 2 ulp, like CUDA expf; made of correctly rounded operations only (mul, fma, rint) so
+// the host oracle reproduces it bit for bit.
 __device__ __forceinline__ float expf_repro(float x) {
     if (!(x >= -87.0f)) return 0.0f;
     const float kf = __builtin_rintf(x * 1.44269504088896341f);
-    float r = x - kf * 0.693145751953125f;
-    r = r - kf * 1.428606765330187045e-06f;
+    float r = __builtin_fmaf(kf, -0.693145751953125f, x);
+    r = __builtin_fmaf(kf, -1.428606765330187045e-06f, r);
     float p = 1.98412698412698413e-04f;
-    p = p * r + 1.38888888888888889e-03f;
-    p = p * r + 8.33333333333333333e-03f;
-    p = p * r + 4.16666666666666667e-02f;
-    p = p * r + 1.66666666666666667e-01f;
-    p = p * r + 0.5f;
-    p = p * r + 1.0f;
-    p = p * r + 1.0f;
+    p = __builtin_fmaf(p, r, 1.38888888888888889e-03f);
+    p = __builtin_fmaf(p, r, 8.33333333333333333e-03f);
+    p = __builtin_fmaf(p, r, 4.16666666666666667e-02f);
+    p = __builtin_fmaf(p, r, 1.66666666666666667e-01f);
+    p = __builtin_fmaf(p, r, 0.5f);
+    p = __builtin_fmaf(p, r, 1.0f);
+    p = __builtin_fmaf(p, r, 1.0f);
     const int k = (int)kf;
     return p * __uint_as_float((uint32_t)(k + 127) << 23);
+}
+
+// Power threshold below which alpha = min(0.99, o exp(power)) < 1/255 for certain (margin 1e-3 in
+// the exponent, far above float error): lets a lane skip exp without changing any decision.
+__device__ __forceinline__ float skip_power(float opacity) {
+    return opacity > 0.0f ? -__logf(255.0f * opacity) - 1e-3f : __builtin_inff();
 }
 
 __device__ __forceinline__ float3 xform4x3(const float* __restrict__ m, float3 p) {
@@ -56,20 +63,106 @@ __device__ __forceinline__ void tile_rect(float2 p, int r, int gx, int gy, int2&
     rmax.y = min(gy, max(0, (int)((p.y + (float)r + (float)(LSR_TILE_Y - 1)) / (float)LSR_TILE_Y)));
 }
 
-// Wave-wide sum, result valid in every lane (DPP rows, then the four row sums via readlane).
-__device__ __forceinline__ float wave_sum(float v) {
-    v += __shfl_xor(v, 1);
-    v += __shfl_xor(v, 2);
-    v += __shfl_xor(v, 4);
-    v += __shfl_xor(v, 8);
-    v += __shfl_xor(v, 16);
-    v += __shfl_xor(v, 32);
-    return v;
-}
-
 __device__ __forceinline__ uint64_t lanemask_lt() {
     const uint32_t lane = __lane_id();
     return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+// ---- cross-lane movement without LDS ---------------------------------------------------------
+// DPP controls (GFX9 encoding): quad_perm, row_mirror, row_half_mirror.
+constexpr int DPP_XOR1 = 0xB1;        // quad_perm [1,0,3,2]
+constexpr int DPP_XOR2 = 0x4E;        // quad_perm [2,3,0,1]
+constexpr int DPP_HALF_MIRROR = 0x141;
+constexpr int DPP_MIRROR = 0x140;
+
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// v_permlane32_swap: lanes 32-63 of a <-> lanes 0-31 of b.
+__device__ __forceinline__ void swap32(float& a, float& b) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+}
+// v_permlane16_swap: odd rows (16 lanes) of a <-> even rows of b.
+__device__ __forceinline__ void swap16(float& a, float& b) {
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+}
+
+// Transpose-reduce (reduce-scatter) of Q per-lane values over the 64 lanes of a wave.
+// Six halving steps: lanes (l, l^32) via permlane32_swap, (l, l^16) via permlane16_swap, then
+// inside each row of 16 the DPP involutions mirror, half-mirror, xor2, xor1.  Each step keeps
+// half of the values and adds the partner's copy of them, so Q values cost ~Q swaps/adds instead
+// of 6 Q.  Afterwards register k < max(1, Q/64) of lane l holds the wave total of quantity
+//   q = k + (Q/64) l                    when Q >= 64,
+//   q = (Q/2) b5 + (Q/4) b4 + ...       (the first log2 Q lane bits, from bit 5 down) when Q < 64.
+// Values are destroyed.  Q must be a power of two >= 2.
+template <int Q>
+__device__ __forceinline__ void wave_transpose_reduce(float (&v)[Q]) {
+    const int lane = __lane_id();
+    const int r = lane & 15;
+    int n = Q;
+    // step 1: pairs across halves of the wave
+    if constexpr (Q >= 2) {
+#pragma unroll
+        for (int k = 0; k < Q / 2; ++k) {
+            float a = v[k], b = v[k + Q / 2];
+            swap32(a, b);
+            v[k] = a + b;
+        }
+        n = Q / 2;
+    }
+    // step 2: pairs across row pairs
+    if constexpr (Q >= 4) {
+#pragma unroll
+        for (int k = 0; k < Q / 4; ++k) {
+            float a = v[k], b = v[k + Q / 4];
+            swap16(a, b);
+            v[k] = a + b;
+        }
+        n = Q / 4;
+    } else {
+        float a = v[0], b = v[0];
+        swap16(a, b);
+        v[0] = a + b;
+    }
+    // steps 3-6 inside each row: keep the first half on the low side of the pairing
+#define LSR_DPP_STEP(CTRL, DIV, HIGH)                                              \
+    if constexpr (Q >= 4 * DIV) {                                                  \
+        _Pragma("unroll") for (int k = 0; k < Q / (4 * DIV); ++k) {                \
+            const float a = v[k], b = v[k + Q / (4 * DIV)];                        \
+            const float s1 = a + dpp<CTRL>(a), s2 = b + dpp<CTRL>(b);              \
+            v[k] = (HIGH) ? s2 : s1;                                               \
+        }                                                                          \
+    } else {                                                                       \
+        v[0] = v[0] + dpp<CTRL>(v[0]);                                             \
+    }
+    LSR_DPP_STEP(DPP_MIRROR, 2, r >= 8)
+    LSR_DPP_STEP(DPP_HALF_MIRROR, 4, (r & 7) >= 4)
+    LSR_DPP_STEP(DPP_XOR2, 8, (r & 2) != 0)
+    LSR_DPP_STEP(DPP_XOR1, 16, (r & 1) != 0)
+#undef LSR_DPP_STEP
+    (void)n;
+}
+
+// Quantity held in register 0 of `lane` after wave_transpose_reduce<Q> (Q <= 64).
+template <int Q>
+__device__ __forceinline__ int transpose_reduce_slot(int lane) {
+    int q = 0;
+    int half = Q / 2;
+    const int bits[6] = {(lane >> 5) & 1, (lane >> 4) & 1, (lane >> 3) & 1, (lane >> 2) & 1, (lane >> 1) & 1, lane & 1};
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+        if (half >= 1) {
+            q += bits[s] * half;
+            half >>= 1;
+        }
+    }
+    return q;
 }
 
 }  // namespace lsr

@@ -20,6 +20,7 @@ struct PreprocessArgs {
     const float* campos;
     // outputs
     int* radii;
+    int* radius;      // internal copy of radii (the backward recomputes tile rectangles)
     uint32_t* tiles;
     uint32_t* key;
     float2* xy;
@@ -41,11 +42,14 @@ struct PreprocessBwdArgs {
     const float* campos;
     const uint32_t* tiles;    // tiles touched (0 = culled; same as radii == 0)
     const uint8_t* clamped;
-    // per-Gaussian screen-space gradients from the compositor backward
-    const float2* g_mean2D;   // NDC units
-    const float4* g_conic;    // (conic a, conic b [half, upstream convention], conic c, depth)
-    const float* g_color;     // [P,3]
+    // per-(Gaussian, tile) records of the compositor backward (render_bwd.hip), contiguous per
+    // Gaussian from inst_off[g]; flags[e] = 1 where the record was written
+    const float* rec;
+    const uint8_t* flags;
+    const uint32_t* inst_off;
+    int recq;
     // outputs (nullable)
+    float* dopacity;
     float* dmeans3D;
     float* dmeans2D;
     float* dcolors;
@@ -79,6 +83,8 @@ struct RenderBwdArgs {
     const float2* xy;
     const float4* conic_o;
     const float4* rgbd;
+    const int* radius;
+    const uint32_t* inst_off;
     const float* lang;
     const float* bg;
     const float* final_T;
@@ -87,16 +93,22 @@ struct RenderBwdArgs {
     const float* dL_dcolor;   // [3,H,W]
     const float* dL_dlang;    // [C,H,W] or null
     const float* dL_ddepth;   // [H,W] or null
-    // outputs (atomically accumulated)
-    float2* g_mean2D;
-    float4* g_conic;
-    float* g_color;
-    float* g_lang;            // [P,C] user buffer (accumulated), may be null
-    float* g_opacity;         // [P]   user buffer (accumulated), may be null
+    // outputs: one record of recq floats per (Gaussian, tile) instance that has a contributing pixel
+    //   [0..2] dL/dcolor, [3] dL/ddepth, [4..5] dL/dmean2D (NDC), [6..8] dL/dconic (x, y, w),
+    //   [9] dL/dopacity, [10..11] 0, [12..12+C) dL/dlanguage
+    float* rec;
+    uint8_t* flags;
+    int recq;
 };
+
+// record width for C language channels (multiple of 4 floats)
+inline int lang_pad(int C) { return C == 0 ? 0 : C <= 4 ? 4 : C <= 8 ? 8 : C <= 16 ? 16 : C <= 32 ? 32 : 64; }
+inline int record_floats(int C) { return 12 + lang_pad(C); }
 
 void launch_preprocess(const PreprocessArgs& a, hipStream_t st);
 void launch_preprocess_bwd(const PreprocessBwdArgs& a, bool accumulate, hipStream_t st);
+void launch_reduce_lang(int P, int C, int cpad, int recq, const float* rec, const uint8_t* flags,
+                        const uint32_t* inst_off, const uint32_t* tiles, float* dlang, bool accumulate, hipStream_t st);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st);
 
 // device-wide primitives (sort.hip)

@@ -86,10 +86,35 @@ __constant__ float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570
                                -0.5900435899266435f};
 
 // ---------------------------------------------------------------------------------------------
+// Copy the [rows x M3] SH block of this workgroup into LDS rows of pitch M3 + 1 with coalesced
+// loads (the per-Gaussian 48-float rows are otherwise read 64 rows at a time per instruction).
+template <int M3>
+__device__ __forceinline__ void stage_rows(float* __restrict__ lds, const float* __restrict__ src, int rows) {
+    if constexpr (M3 > 0) {
+        constexpr int SP = M3 + 1;
+        const int n = rows * M3;
+        for (int e = threadIdx.x; e < n; e += blockDim.x) {
+            const int r = e / M3, c = e - r * M3;
+            lds[r * SP + c] = src[e];
+        }
+    }
+}
+
+template <int MS>  // staged SH coefficients (0 = read from global directly)
 __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
+    constexpr int M3 = MS * 3, SP = M3 + 1;
+    __shared__ float s_sh[MS > 0 ? 256 * SP : 1];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if constexpr (MS > 0) {
+        const int g0 = blockIdx.x * blockDim.x;
+        if (a.shs && !a.colors_precomp) {
+            stage_rows<M3>(s_sh, a.shs + (size_t)g0 * M3, min(256, a.P - g0));
+            __syncthreads();
+        }
+    }
     if (i >= a.P) return;
     a.radii[i] = 0;
+    a.radius[i] = 0;
     a.tiles[i] = 0;
     a.key[i] = 0xFFFFFFFFu;
     const float3 p = make_float3(a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]);
@@ -143,7 +168,7 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
         float3 dir = make_float3(p.x - a.campos[0], p.y - a.campos[1], p.z - a.campos[2]);
         const float len = sqrtf(dir.x * dir.x + dir.y * dir.y + dir.z * dir.z);
         dir.x = dir.x / len; dir.y = dir.y / len; dir.z = dir.z / len;
-        const float* sh = a.shs + (size_t)i * a.M * 3;
+        const float* sh = MS > 0 ? s_sh + threadIdx.x * SP : a.shs + (size_t)i * a.M * 3;
         uint8_t cl = 0;
         const int deg = a.deg;
 #pragma unroll
@@ -175,6 +200,7 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
         a.clamped[i] = cl;
     }
     a.radii[i] = radius;
+    a.radius[i] = radius;
     a.tiles[i] = (uint32_t)ntiles;
     a.key[i] = __float_as_uint(pv.z);
     a.xy[i] = pix;
@@ -184,7 +210,15 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
 
 void launch_preprocess(const PreprocessArgs& a, hipStream_t st) {
     if (a.P == 0) return;
-    hipLaunchKernelGGL(k_preprocess, dim3((a.P + 255) / 256), dim3(256), 0, st, a);
+    const dim3 grid((a.P + 255) / 256), block(256);
+    const int ms = (a.shs && !a.colors_precomp) ? a.M : 0;
+    switch (ms) {
+        case 1: hipLaunchKernelGGL(k_preprocess<1>, grid, block, 0, st, a); break;
+        case 4: hipLaunchKernelGGL(k_preprocess<4>, grid, block, 0, st, a); break;
+        case 9: hipLaunchKernelGGL(k_preprocess<9>, grid, block, 0, st, a); break;
+        case 16: hipLaunchKernelGGL(k_preprocess<16>, grid, block, 0, st, a); break;
+        default: hipLaunchKernelGGL(k_preprocess<0>, grid, block, 0, st, a); break;
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -304,138 +338,242 @@ __device__ __forceinline__ void put(float* p, float v) {
     if (ACC) *p += v; else *p = v;
 }
 
-template <bool ACC>
+template <bool ACC, int MS>
 __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.P) return;
-    const bool vis = a.tiles[i] > 0;
-    // pass-through gradients first (means2D in NDC units, colours)
-    const float2 g2 = vis ? a.g_mean2D[i] : make_float2(0.0f, 0.0f);
-    const float gx = g2.x, gy = g2.y;
-    float3 gcol = make_float3(0.0f, 0.0f, 0.0f);
-    if (vis) gcol = make_float3(a.g_color[3 * i], a.g_color[3 * i + 1], a.g_color[3 * i + 2]);
-    if (a.dmeans2D) { put<ACC>(a.dmeans2D + 3 * (size_t)i, gx); put<ACC>(a.dmeans2D + 3 * (size_t)i + 1, gy); put<ACC>(a.dmeans2D + 3 * (size_t)i + 2, 0.0f); }
-    if (a.dcolors) { put<ACC>(a.dcolors + 3 * (size_t)i, gcol.x); put<ACC>(a.dcolors + 3 * (size_t)i + 1, gcol.y); put<ACC>(a.dcolors + 3 * (size_t)i + 2, gcol.z); }
-
-    float3 dm = make_float3(0.0f, 0.0f, 0.0f);
-    float dcov[6] = {0, 0, 0, 0, 0, 0};
-    float3 dscale = make_float3(0.0f, 0.0f, 0.0f);
-    float4 drot = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    const int M = a.M;
-    if (vis) {
-        const float3 p = make_float3(a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]);
-        float c3[6];
-        float3 sc = make_float3(0.0f, 0.0f, 0.0f);
-        float4 q = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        if (a.cov3D_precomp) {
+    constexpr int M3 = MS * 3, SP = M3 + 1;
+    __shared__ float s_sh[MS > 0 ? 256 * SP : 1];
+    const int g0 = blockIdx.x * blockDim.x;
+    const int rows = min(256, a.P - g0);
+    const int i = g0 + threadIdx.x;
+    const bool stage = MS > 0 && a.shs != nullptr;
+    if (stage) {
+        stage_rows<M3>(s_sh, a.shs + (size_t)g0 * M3, rows);
+        __syncthreads();
+    }
+    if (i < a.P) {
+        const uint32_t ntile = a.tiles[i];
+        const bool vis = ntile > 0;
+        // sum the compositor's per-(Gaussian, tile) records: contiguous per Gaussian
+        float rs[12];
 #pragma unroll
-            for (int k = 0; k < 6; ++k) c3[k] = a.cov3D_precomp[6 * (size_t)i + k];
-        } else {
-            sc = make_float3(a.scales[3 * i], a.scales[3 * i + 1], a.scales[3 * i + 2]);
-            q = reinterpret_cast<const float4*>(a.rotations)[i];
-            cov3d(sc, a.scale_modifier, q, c3);
-        }
-        const float4 gc = a.g_conic[i];   // (x, y, w) of the upstream float4, packed as x, y, z
-        cov2d_bwd(p, c3, a.focal_x, a.focal_y, a.tanfovx, a.tanfovy, a.view, make_float3(gc.x, gc.y, gc.z), dm, dcov);
-        // projection of the mean
-        const float* pm = a.proj;
-        const float4 mh = xform4x4(pm, p);
-        const float mw = 1.0f / (mh.w + 0.0000001f);
-        const float mul1 = (pm[0] * p.x + pm[4] * p.y + pm[8] * p.z + pm[12]) * mw * mw;
-        const float mul2 = (pm[1] * p.x + pm[5] * p.y + pm[9] * p.z + pm[13]) * mw * mw;
-        dm.x += (pm[0] * mw - pm[3] * mul1) * gx + (pm[1] * mw - pm[3] * mul2) * gy;
-        dm.y += (pm[4] * mw - pm[7] * mul1) * gx + (pm[5] * mw - pm[7] * mul2) * gy;
-        dm.z += (pm[8] * mw - pm[11] * mul1) * gx + (pm[9] * mw - pm[11] * mul2) * gy;
-        // depth row
-        const float gd = gc.w;
-        dm.x += a.view[2] * gd;
-        dm.y += a.view[6] * gd;
-        dm.z += a.view[10] * gd;
-        // SH
-        if (a.shs) {
-            const float3 dir_orig = make_float3(p.x - a.campos[0], p.y - a.campos[1], p.z - a.campos[2]);
-            const float len = sqrtf(dir_orig.x * dir_orig.x + dir_orig.y * dir_orig.y + dir_orig.z * dir_orig.z);
-            const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
-            const uint8_t cl = a.clamped[i];
-            const float dR[3] = {(cl & 1) ? 0.0f : gcol.x, (cl & 2) ? 0.0f : gcol.y, (cl & 4) ? 0.0f : gcol.z};
-            const float* sh = a.shs + (size_t)i * M * 3;
-            float* dsh = a.dsh ? a.dsh + (size_t)i * M * 3 : nullptr;
-            const int deg = a.deg;
-            float dRdx[3] = {0, 0, 0}, dRdy[3] = {0, 0, 0}, dRdz[3] = {0, 0, 0};
-            float g[16];
+        for (int k = 0; k < 12; ++k) rs[k] = 0.0f;
+        if (vis) {
+            const uint32_t e0 = a.inst_off[i];
+            for (uint32_t e = e0; e < e0 + ntile; ++e) {
+                if (!a.flags[e]) continue;
+                const float4* r4 = reinterpret_cast<const float4*>(a.rec + (size_t)e * a.recq);
 #pragma unroll
-            for (int ch = 0; ch < 3; ++ch) {
-#define SHc(k) sh[(k) * 3 + ch]
-#pragma unroll
-                for (int k = 0; k < 16; ++k) g[k] = 0.0f;
-                g[0] = SH_C0 * dR[ch];
-                if (deg > 0) {
-                    g[1] = -SH_C1 * y * dR[ch]; g[2] = SH_C1 * z * dR[ch]; g[3] = -SH_C1 * x * dR[ch];
-                    dRdx[ch] = -SH_C1 * SHc(3); dRdy[ch] = -SH_C1 * SHc(1); dRdz[ch] = SH_C1 * SHc(2);
-                    if (deg > 1) {
-                        const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-                        g[4] = SH_C2[0] * xy * dR[ch]; g[5] = SH_C2[1] * yz * dR[ch];
-                        g[6] = SH_C2[2] * (2.0f * zz - xx - yy) * dR[ch]; g[7] = SH_C2[3] * xz * dR[ch];
-                        g[8] = SH_C2[4] * (xx - yy) * dR[ch];
-                        dRdx[ch] += SH_C2[0] * y * SHc(4) + SH_C2[2] * 2.0f * -x * SHc(6) + SH_C2[3] * z * SHc(7) + SH_C2[4] * 2.0f * x * SHc(8);
-                        dRdy[ch] += SH_C2[0] * x * SHc(4) + SH_C2[1] * z * SHc(5) + SH_C2[2] * 2.0f * -y * SHc(6) + SH_C2[4] * 2.0f * -y * SHc(8);
-                        dRdz[ch] += SH_C2[1] * y * SHc(5) + SH_C2[2] * 2.0f * 2.0f * z * SHc(6) + SH_C2[3] * x * SHc(7);
-                        if (deg > 2) {
-                            g[9] = SH_C3[0] * y * (3.0f * xx - yy) * dR[ch];
-                            g[10] = SH_C3[1] * xy * z * dR[ch];
-                            g[11] = SH_C3[2] * y * (4.0f * zz - xx - yy) * dR[ch];
-                            g[12] = SH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * dR[ch];
-                            g[13] = SH_C3[4] * x * (4.0f * zz - xx - yy) * dR[ch];
-                            g[14] = SH_C3[5] * z * (xx - yy) * dR[ch];
-                            g[15] = SH_C3[6] * x * (xx - 3.0f * yy) * dR[ch];
-                            dRdx[ch] += SH_C3[0] * SHc(9) * 3.0f * 2.0f * xy + SH_C3[1] * SHc(10) * yz + SH_C3[2] * SHc(11) * -2.0f * xy +
-                                        SH_C3[3] * SHc(12) * -3.0f * 2.0f * xz + SH_C3[4] * SHc(13) * (-3.0f * xx + 4.0f * zz - yy) +
-                                        SH_C3[5] * SHc(14) * 2.0f * xz + SH_C3[6] * SHc(15) * 3.0f * (xx - yy);
-                            dRdy[ch] += SH_C3[0] * SHc(9) * 3.0f * (xx - yy) + SH_C3[1] * SHc(10) * xz +
-                                        SH_C3[2] * SHc(11) * (-3.0f * yy + 4.0f * zz - xx) + SH_C3[3] * SHc(12) * -3.0f * 2.0f * yz +
-                                        SH_C3[4] * SHc(13) * -2.0f * xy + SH_C3[5] * SHc(14) * -2.0f * yz + SH_C3[6] * SHc(15) * -3.0f * 2.0f * xy;
-                            dRdz[ch] += SH_C3[1] * SHc(10) * xy + SH_C3[2] * SHc(11) * 4.0f * 2.0f * yz +
-                                        SH_C3[3] * SHc(12) * 3.0f * (2.0f * zz - xx - yy) + SH_C3[4] * SHc(13) * 4.0f * 2.0f * xz +
-                                        SH_C3[5] * SHc(14) * (xx - yy);
-                        }
-                    }
-                }
-#undef SHc
-                if (dsh) {
-                    for (int k = 0; k < M; ++k) put<ACC>(dsh + k * 3 + ch, k < 16 ? g[k] : 0.0f);
+                for (int k4 = 0; k4 < 3; ++k4) {
+                    const float4 v = r4[k4];
+                    rs[4 * k4] += v.x; rs[4 * k4 + 1] += v.y; rs[4 * k4 + 2] += v.z; rs[4 * k4 + 3] += v.w;
                 }
             }
-            const float dLdx = dRdx[0] * dR[0] + dRdx[1] * dR[1] + dRdx[2] * dR[2];
-            const float dLdy = dRdy[0] * dR[0] + dRdy[1] * dR[1] + dRdy[2] * dR[2];
-            const float dLdz = dRdz[0] * dR[0] + dRdz[1] * dR[1] + dRdz[2] * dR[2];
-            const float3 v = dir_orig;
-            const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
-            const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
-            dm.x += ((sum2 - v.x * v.x) * dLdx - v.y * v.x * dLdy - v.z * v.x * dLdz) * invsum32;
-            dm.y += (-v.x * v.y * dLdx + (sum2 - v.y * v.y) * dLdy - v.z * v.y * dLdz) * invsum32;
-            dm.z += (-v.x * v.z * dLdx - v.y * v.z * dLdy + (sum2 - v.z * v.z) * dLdz) * invsum32;
         }
-        if (!a.cov3D_precomp) cov3d_bwd(sc, a.scale_modifier, q, dcov, dscale, drot);
-    } else if (a.dsh && !ACC) {
-        float* dsh = a.dsh + (size_t)i * M * 3;
-        for (int k = 0; k < 3 * M; ++k) dsh[k] = 0.0f;
-    }
-    if (a.dmeans3D) { put<ACC>(a.dmeans3D + 3 * (size_t)i, dm.x); put<ACC>(a.dmeans3D + 3 * (size_t)i + 1, dm.y); put<ACC>(a.dmeans3D + 3 * (size_t)i + 2, dm.z); }
-    if (a.dcov3D) {
+        // record layout: rgb 0-2, depth 3, mean2D 4-5 (NDC), conic 6-8 (upstream x, y, w), opacity 9
+        const float3 gcol = make_float3(rs[0], rs[1], rs[2]);
+        const float gx = rs[4], gy = rs[5];
+        if (a.dmeans2D) { put<ACC>(a.dmeans2D + 3 * (size_t)i, gx); put<ACC>(a.dmeans2D + 3 * (size_t)i + 1, gy); put<ACC>(a.dmeans2D + 3 * (size_t)i + 2, 0.0f); }
+        if (a.dcolors) { put<ACC>(a.dcolors + 3 * (size_t)i, gcol.x); put<ACC>(a.dcolors + 3 * (size_t)i + 1, gcol.y); put<ACC>(a.dcolors + 3 * (size_t)i + 2, gcol.z); }
+        if (a.dopacity) put<ACC>(a.dopacity + i, rs[9]);
+
+        float3 dm = make_float3(0.0f, 0.0f, 0.0f);
+        float dcov[6] = {0, 0, 0, 0, 0, 0};
+        float3 dscale = make_float3(0.0f, 0.0f, 0.0f);
+        float4 drot = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        const int M = a.M;
+        float* srow = stage ? s_sh + threadIdx.x * SP : nullptr;
+        if (vis) {
+            const float3 p = make_float3(a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]);
+            float c3[6];
+            float3 sc = make_float3(0.0f, 0.0f, 0.0f);
+            float4 q = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (a.cov3D_precomp) {
 #pragma unroll
-        for (int k = 0; k < 6; ++k) put<ACC>(a.dcov3D + 6 * (size_t)i + k, a.cov3D_precomp ? dcov[k] : dcov[k]);
+                for (int k = 0; k < 6; ++k) c3[k] = a.cov3D_precomp[6 * (size_t)i + k];
+            } else {
+                sc = make_float3(a.scales[3 * i], a.scales[3 * i + 1], a.scales[3 * i + 2]);
+                q = reinterpret_cast<const float4*>(a.rotations)[i];
+                cov3d(sc, a.scale_modifier, q, c3);
+            }
+            cov2d_bwd(p, c3, a.focal_x, a.focal_y, a.tanfovx, a.tanfovy, a.view, make_float3(rs[6], rs[7], rs[8]), dm, dcov);
+            // projection of the mean
+            const float* pm = a.proj;
+            const float4 mh = xform4x4(pm, p);
+            const float mw = 1.0f / (mh.w + 0.0000001f);
+            const float mul1 = (pm[0] * p.x + pm[4] * p.y + pm[8] * p.z + pm[12]) * mw * mw;
+            const float mul2 = (pm[1] * p.x + pm[5] * p.y + pm[9] * p.z + pm[13]) * mw * mw;
+            dm.x += (pm[0] * mw - pm[3] * mul1) * gx + (pm[1] * mw - pm[3] * mul2) * gy;
+            dm.y += (pm[4] * mw - pm[7] * mul1) * gx + (pm[5] * mw - pm[7] * mul2) * gy;
+            dm.z += (pm[8] * mw - pm[11] * mul1) * gx + (pm[9] * mw - pm[11] * mul2) * gy;
+            // depth row
+            const float gd = rs[3];
+            dm.x += a.view[2] * gd;
+            dm.y += a.view[6] * gd;
+            dm.z += a.view[10] * gd;
+            // SH
+            if (a.shs) {
+                const float3 dir_orig = make_float3(p.x - a.campos[0], p.y - a.campos[1], p.z - a.campos[2]);
+                const float len = sqrtf(dir_orig.x * dir_orig.x + dir_orig.y * dir_orig.y + dir_orig.z * dir_orig.z);
+                const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
+                const uint8_t cl = a.clamped[i];
+                const float dR[3] = {(cl & 1) ? 0.0f : gcol.x, (cl & 2) ? 0.0f : gcol.y, (cl & 4) ? 0.0f : gcol.z};
+                const float* sh = stage ? srow : a.shs + (size_t)i * M * 3;
+                float* dsh = stage ? srow : (a.dsh ? a.dsh + (size_t)i * M * 3 : nullptr);
+                const int deg = a.deg;
+                float dRdx[3] = {0, 0, 0}, dRdy[3] = {0, 0, 0}, dRdz[3] = {0, 0, 0};
+                float g[16];
+#pragma unroll
+                for (int ch = 0; ch < 3; ++ch) {
+#define SHc(k) sh[(k) * 3 + ch]
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) g[k] = 0.0f;
+                    g[0] = SH_C0 * dR[ch];
+                    if (deg > 0) {
+                        g[1] = -SH_C1 * y * dR[ch]; g[2] = SH_C1 * z * dR[ch]; g[3] = -SH_C1 * x * dR[ch];
+                        dRdx[ch] = -SH_C1 * SHc(3); dRdy[ch] = -SH_C1 * SHc(1); dRdz[ch] = SH_C1 * SHc(2);
+                        if (deg > 1) {
+                            const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+                            g[4] = SH_C2[0] * xy * dR[ch]; g[5] = SH_C2[1] * yz * dR[ch];
+                            g[6] = SH_C2[2] * (2.0f * zz - xx - yy) * dR[ch]; g[7] = SH_C2[3] * xz * dR[ch];
+                            g[8] = SH_C2[4] * (xx - yy) * dR[ch];
+                            dRdx[ch] += SH_C2[0] * y * SHc(4) + SH_C2[2] * 2.0f * -x * SHc(6) + SH_C2[3] * z * SHc(7) + SH_C2[4] * 2.0f * x * SHc(8);
+                            dRdy[ch] += SH_C2[0] * x * SHc(4) + SH_C2[1] * z * SHc(5) + SH_C2[2] * 2.0f * -y * SHc(6) + SH_C2[4] * 2.0f * -y * SHc(8);
+                            dRdz[ch] += SH_C2[1] * y * SHc(5) + SH_C2[2] * 2.0f * 2.0f * z * SHc(6) + SH_C2[3] * x * SHc(7);
+                            if (deg > 2) {
+                                g[9] = SH_C3[0] * y * (3.0f * xx - yy) * dR[ch];
+                                g[10] = SH_C3[1] * xy * z * dR[ch];
+                                g[11] = SH_C3[2] * y * (4.0f * zz - xx - yy) * dR[ch];
+                                g[12] = SH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * dR[ch];
+                                g[13] = SH_C3[4] * x * (4.0f * zz - xx - yy) * dR[ch];
+                                g[14] = SH_C3[5] * z * (xx - yy) * dR[ch];
+                                g[15] = SH_C3[6] * x * (xx - 3.0f * yy) * dR[ch];
+                                dRdx[ch] += SH_C3[0] * SHc(9) * 3.0f * 2.0f * xy + SH_C3[1] * SHc(10) * yz + SH_C3[2] * SHc(11) * -2.0f * xy +
+                                            SH_C3[3] * SHc(12) * -3.0f * 2.0f * xz + SH_C3[4] * SHc(13) * (-3.0f * xx + 4.0f * zz - yy) +
+                                            SH_C3[5] * SHc(14) * 2.0f * xz + SH_C3[6] * SHc(15) * 3.0f * (xx - yy);
+                                dRdy[ch] += SH_C3[0] * SHc(9) * 3.0f * (xx - yy) + SH_C3[1] * SHc(10) * xz +
+                                            SH_C3[2] * SHc(11) * (-3.0f * yy + 4.0f * zz - xx) + SH_C3[3] * SHc(12) * -3.0f * 2.0f * yz +
+                                            SH_C3[4] * SHc(13) * -2.0f * xy + SH_C3[5] * SHc(14) * -2.0f * yz + SH_C3[6] * SHc(15) * -3.0f * 2.0f * xy;
+                                dRdz[ch] += SH_C3[1] * SHc(10) * xy + SH_C3[2] * SHc(11) * 4.0f * 2.0f * yz +
+                                            SH_C3[3] * SHc(12) * 3.0f * (2.0f * zz - xx - yy) + SH_C3[4] * SHc(13) * 4.0f * 2.0f * xz +
+                                            SH_C3[5] * SHc(14) * (xx - yy);
+                            }
+                        }
+                    }
+#undef SHc
+                    // this channel's coefficients have all been read: overwrite them with the gradient
+                    if (stage) {
+#pragma unroll
+                        for (int k = 0; k < MS; ++k) dsh[k * 3 + ch] = k < 16 ? g[k] : 0.0f;
+                    } else if (dsh) {
+                        for (int k = 0; k < M; ++k) put<ACC>(dsh + k * 3 + ch, k < 16 ? g[k] : 0.0f);
+                    }
+                }
+                const float dLdx = dRdx[0] * dR[0] + dRdx[1] * dR[1] + dRdx[2] * dR[2];
+                const float dLdy = dRdy[0] * dR[0] + dRdy[1] * dR[1] + dRdy[2] * dR[2];
+                const float dLdz = dRdz[0] * dR[0] + dRdz[1] * dR[1] + dRdz[2] * dR[2];
+                const float3 v = dir_orig;
+                const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
+                const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+                dm.x += ((sum2 - v.x * v.x) * dLdx - v.y * v.x * dLdy - v.z * v.x * dLdz) * invsum32;
+                dm.y += (-v.x * v.y * dLdx + (sum2 - v.y * v.y) * dLdy - v.z * v.y * dLdz) * invsum32;
+                dm.z += (-v.x * v.z * dLdx - v.y * v.z * dLdy + (sum2 - v.z * v.z) * dLdz) * invsum32;
+            }
+            if (!a.cov3D_precomp) cov3d_bwd(sc, a.scale_modifier, q, dcov, dscale, drot);
+        } else if (stage) {
+#pragma unroll
+            for (int k = 0; k < M3; ++k) srow[k] = 0.0f;
+        } else if (a.dsh && !ACC) {
+            float* dsh = a.dsh + (size_t)i * M * 3;
+            for (int k = 0; k < 3 * M; ++k) dsh[k] = 0.0f;
+        }
+        if (a.dmeans3D) { put<ACC>(a.dmeans3D + 3 * (size_t)i, dm.x); put<ACC>(a.dmeans3D + 3 * (size_t)i + 1, dm.y); put<ACC>(a.dmeans3D + 3 * (size_t)i + 2, dm.z); }
+        if (a.dcov3D) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k) put<ACC>(a.dcov3D + 6 * (size_t)i + k, dcov[k]);
+        }
+        if (a.dscales) { put<ACC>(a.dscales + 3 * (size_t)i, dscale.x); put<ACC>(a.dscales + 3 * (size_t)i + 1, dscale.y); put<ACC>(a.dscales + 3 * (size_t)i + 2, dscale.z); }
+        if (a.drots) {
+            put<ACC>(a.drots + 4 * (size_t)i, drot.x); put<ACC>(a.drots + 4 * (size_t)i + 1, drot.y);
+            put<ACC>(a.drots + 4 * (size_t)i + 2, drot.z); put<ACC>(a.drots + 4 * (size_t)i + 3, drot.w);
+        }
     }
-    if (a.dscales) { put<ACC>(a.dscales + 3 * (size_t)i, dscale.x); put<ACC>(a.dscales + 3 * (size_t)i + 1, dscale.y); put<ACC>(a.dscales + 3 * (size_t)i + 2, dscale.z); }
-    if (a.drots) {
-        put<ACC>(a.drots + 4 * (size_t)i, drot.x); put<ACC>(a.drots + 4 * (size_t)i + 1, drot.y);
-        put<ACC>(a.drots + 4 * (size_t)i + 2, drot.z); put<ACC>(a.drots + 4 * (size_t)i + 3, drot.w);
+    if (stage && a.dsh) {   // coalesced write-out of the block's SH gradient rows
+        __syncthreads();
+        float* dst = a.dsh + (size_t)g0 * M3;
+        if constexpr (M3 > 0) {
+            for (int e = threadIdx.x; e < rows * M3; e += blockDim.x) {
+                const int r = e / M3, c = e - r * M3;
+                put<ACC>(dst + e, s_sh[r * SP + c]);
+            }
+        }
+    }
+}
+
+template <bool ACC>
+static void go_pbwd(const PreprocessBwdArgs& a, hipStream_t st) {
+    const dim3 grid((a.P + 255) / 256), block(256);
+    switch (a.shs ? a.M : 0) {
+        case 1: hipLaunchKernelGGL((k_preprocess_bwd<ACC, 1>), grid, block, 0, st, a); break;
+        case 4: hipLaunchKernelGGL((k_preprocess_bwd<ACC, 4>), grid, block, 0, st, a); break;
+        case 9: hipLaunchKernelGGL((k_preprocess_bwd<ACC, 9>), grid, block, 0, st, a); break;
+        case 16: hipLaunchKernelGGL((k_preprocess_bwd<ACC, 16>), grid, block, 0, st, a); break;
+        default: hipLaunchKernelGGL((k_preprocess_bwd<ACC, 0>), grid, block, 0, st, a); break;
     }
 }
 
 void launch_preprocess_bwd(const PreprocessBwdArgs& a, bool accumulate, hipStream_t st) {
     if (a.P == 0) return;
-    if (accumulate) hipLaunchKernelGGL(k_preprocess_bwd<true>, dim3((a.P + 255) / 256), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(k_preprocess_bwd<false>, dim3((a.P + 255) / 256), dim3(256), 0, st, a);
+    if (accumulate) go_pbwd<true>(a, st);
+    else go_pbwd<false>(a, st);
+}
+
+// Language-feature gradient: sum of the records' C channels of each Gaussian.  A Gaussian's
+// records are contiguous; CPAD/4 lanes per Gaussian read them as float4 (coalesced rows).
+template <bool ACC, int CPAD>
+__global__ void __launch_bounds__(256) k_reduce_lang(int P, int C, int recq, const float* __restrict__ rec,
+                                                     const uint8_t* __restrict__ flags, const uint32_t* __restrict__ inst_off,
+                                                     const uint32_t* __restrict__ tiles, float* __restrict__ dlang) {
+    constexpr int LPG = CPAD / 4, GPB = 256 / LPG;
+    const int g = blockIdx.x * GPB + threadIdx.x / LPG;
+    const int c4 = threadIdx.x % LPG;
+    if (g >= P) return;
+    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const uint32_t n = tiles[g];
+    if (n > 0) {
+        const uint32_t e0 = inst_off[g];
+        for (uint32_t e = e0; e < e0 + n; ++e) {
+            if (!flags[e]) continue;
+            const float4 v = reinterpret_cast<const float4*>(rec + (size_t)e * recq + 12)[c4];
+            acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        }
+    }
+    float* d = dlang + (size_t)g * C;
+    const float vals[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int c = 4 * c4 + j;
+        if (c < C) put<ACC>(d + c, vals[j]);
+    }
+}
+
+void launch_reduce_lang(int P, int C, int cpad, int recq, const float* rec, const uint8_t* flags,
+                        const uint32_t* inst_off, const uint32_t* tiles, float* dlang, bool accumulate, hipStream_t st) {
+    if (P == 0 || C == 0 || !dlang) return;
+#define LSR_GO(CP)                                                                                        \
+    {                                                                                                     \
+        constexpr int GPB = 256 / ((CP) / 4);                                                            \
+        const dim3 grid((P + GPB - 1) / GPB);                                                             \
+        if (accumulate) hipLaunchKernelGGL((k_reduce_lang<true, CP>), grid, dim3(256), 0, st, P, C, recq, rec, flags, inst_off, tiles, dlang); \
+        else hipLaunchKernelGGL((k_reduce_lang<false, CP>), grid, dim3(256), 0, st, P, C, recq, rec, flags, inst_off, tiles, dlang); \
+    }
+    switch (cpad) {
+        case 4: LSR_GO(4) break;
+        case 8: LSR_GO(8) break;
+        case 16: LSR_GO(16) break;
+        case 32: LSR_GO(32) break;
+        default: LSR_GO(64) break;
+    }
+#undef LSR_GO
 }
 
 }  // namespace lsr

@@ -5,26 +5,36 @@
 // ignored in dL/dG; the background enters through -T_final / (1 - alpha) (bg . dL/dpix_rgb);
 // means2D gradients are in NDC units (x 0.5 W, 0.5 H).
 //
-// Differences in mechanics (same mathematics):
-//   * accum_rec is carried as one scalar per pixel, accum_rec . dL/dpix, since dL/dalpha only
-//     needs that dot product: sum_ch (c_ch - accum_rec_ch) g_ch = c . g - accum_rec . g, and
-//     accum_rec . g obeys the same linear recurrence.  This drops 2 (3 + C + 1) registers.
-//   * the replay starts at the tile's largest n_contrib (recorded by the forward), not at the end
-//     of the list;
-//   * per-pixel contributions are summed over the wave before one atomic per (Gaussian, wave),
-//     instead of one atomic per (Gaussian, pixel); waves with no contributing pixel skip it.
+// Mechanics (same mathematics, different data movement):
+//   * accum_rec is carried as one scalar per pixel, accum_rec . dL/dpix: dL/dalpha only needs
+//     sum_ch (c_ch - accum_rec_ch) g_ch = c . g - accum_rec . g, and accum_rec . g obeys the same
+//     linear recurrence.  This removes 2 (3 + C + 1) registers per pixel.
+//   * the replay starts at the tile's largest n_contrib (recorded by the forward);
+//   * lanes skip exp when power < ln(1 / (255 o)) - 1e-3 (alpha < 1/255 for certain);
+//   * per (Gaussian, wave) the 10 + C per-pixel contributions are summed over the 64 lanes by a
+//     transpose-reduce (permlane32/16 swaps + DPP), which leaves one quantity per lane; the four
+//     waves of the tile add them into an LDS record (one ds_add per lane); each (Gaussian, tile)
+//     record is then written once with plain stores at the Gaussian's instance slot, where the
+//     per-Gaussian reduction (preprocess.hip) reads them back contiguously.  No global atomics:
+//     the backward is deterministic.
 #include "lsr_common.h"
 #include "lsr_internal.h"
 
 namespace lsr {
 
-template <int CPAD, int BATCH>
+template <int CPAD, int BATCH, int Q>
 __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
-    __shared__ uint32_t s_id[BATCH];
-    __shared__ float2 s_xy[BATCH];
+    constexpr int RECQ = 12 + CPAD;
+    static_assert(RECQ <= Q || Q == 128, "quantities must fit the transpose-reduce width");
+    __shared__ float s_rec[BATCH * RECQ];
+    __shared__ float s_lang[CPAD > 0 ? BATCH * CPAD : 1];
     __shared__ float4 s_co[BATCH];
     __shared__ float4 s_rgbd[BATCH];
-    __shared__ float s_lang[CPAD > 0 ? BATCH * CPAD : 1];
+    __shared__ float2 s_xy[BATCH];
+    __shared__ float s_thr[BATCH];
+    __shared__ uint32_t s_id[BATCH];
+    __shared__ uint32_t s_inst[BATCH];
+    __shared__ uint32_t s_act[BATCH];
 
     const int tile = blockIdx.x;
     const int tx = tile % a.grid_x, ty = tile / a.grid_x;
@@ -63,14 +73,22 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
     for (int end = (int)nreplay; end > 0; end -= BATCH) {
         const int nb = min(BATCH, end);
         const int first = end - nb;             // list position of batch slot 0
-        __syncthreads();
+        __syncthreads();                        // previous batch fully written out
         if (tid < nb) {
             const uint32_t gid = a.point_list[range.x + first + tid];
+            const float2 xy = a.xy[gid];
+            const float4 co = a.conic_o[gid];
             s_id[tid] = gid;
-            s_xy[tid] = a.xy[gid];
-            s_co[tid] = a.conic_o[gid];
+            s_xy[tid] = xy;
+            s_co[tid] = co;
             s_rgbd[tid] = a.rgbd[gid];
+            s_thr[tid] = skip_power(co.w);
+            int2 rmin, rmax;
+            tile_rect(xy, a.radius[gid], a.grid_x, a.grid_y, rmin, rmax);
+            s_inst[tid] = a.inst_off[gid] + (uint32_t)((ty - rmin.y) * (rmax.x - rmin.x) + (tx - rmin.x));
+            s_act[tid] = 0;
         }
+        for (int e = tid; e < nb * RECQ; e += 256) s_rec[e] = 0.0f;
         if constexpr (CPAD > 0) {
             __syncthreads();
             for (int e = tid; e < nb * CPAD; e += 256) {
@@ -88,12 +106,13 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
                 const float4 co = s_co[j];
                 const float dx = xy.x - pxf, dy = xy.y - pyf;
                 const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-                if (power <= 0.0f) {
+                if (power <= 0.0f && power >= s_thr[j]) {
                     const float G = expf_repro(power);
                     const float alpha = fminf(0.99f, co.w * G);
                     if (alpha >= 1.0f / 255.0f) {
                         active = true;
-                        T = T / (1.0f - alpha);
+                        const float om = 1.0f - alpha;
+                        T = T * __builtin_amdgcn_rcpf(om);
                         w = alpha * T;
                         const float4 cd = s_rgbd[j];
                         float dot = cd.x * g[0];
@@ -111,11 +130,11 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
                                 dot = __builtin_fmaf(f.w, gL[4 * c4 + 3], dot);
                             }
                         }
-                        acc_dot = last_alpha * last_dot + (1.0f - last_alpha) * acc_dot;
+                        acc_dot = __builtin_fmaf(last_alpha, last_dot, (1.0f - last_alpha) * acc_dot);
                         last_dot = dot;
                         float dL_dalpha = (dot - acc_dot) * T;
                         last_alpha = alpha;
-                        dL_dalpha += (-T_final / (1.0f - alpha)) * bg_dot;
+                        dL_dalpha = __builtin_fmaf(-T_final * __builtin_amdgcn_rcpf(om), bg_dot, dL_dalpha);
                         const float dL_dG = co.w * dL_dalpha;
                         const float gdx = G * dx, gdy = G * dy;
                         const float dG_ddelx = -gdx * co.x - gdy * co.y;
@@ -130,54 +149,57 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
                 }
             }
             if (!__any(active)) continue;
-            // wave sums; lane (q mod 64) of round q / 64 then issues the atomic for quantity q
-            constexpr int NQ = 10 + CPAD, ROUNDS = (NQ + 63) / 64;
-            const uint32_t gid = s_id[j];
-            float mine[ROUNDS];
-            float* dst[ROUNDS];
+            float v[Q];
+            v[0] = w * g[0]; v[1] = w * g[1]; v[2] = w * g[2]; v[3] = w * gD;
+            v[4] = gm2x; v[5] = gm2y; v[6] = gcx; v[7] = gcy; v[8] = gcw; v[9] = gop;
+            v[10] = 0.0f; v[11] = 0.0f;
 #pragma unroll
-            for (int r = 0; r < ROUNDS; ++r) { mine[r] = 0.0f; dst[r] = nullptr; }
-#define LSR_TAKE(q, expr, ptr)                                   \
-            {                                                    \
-                const float v_ = wave_sum(expr);                 \
-                if (lane == ((q) & 63)) { mine[(q) >> 6] = v_; dst[(q) >> 6] = (ptr); } \
+            for (int c = 0; c < CPAD; ++c) v[12 + c] = w * gL[c];
+#pragma unroll
+            for (int q = RECQ; q < Q; ++q) v[q] = 0.0f;
+            wave_transpose_reduce<Q>(v);
+            float* rec = s_rec + j * RECQ;
+            if constexpr (Q <= 64) {
+                const int q = transpose_reduce_slot<Q>(lane);
+                if ((lane & (64 / Q - 1)) == 0 && q < RECQ) atomicAdd(rec + q, v[0]);
+            } else {
+#pragma unroll
+                for (int kk = 0; kk < Q / 64; ++kk) {
+                    const int q = kk + (Q / 64) * lane;
+                    if (q < RECQ) atomicAdd(rec + q, v[kk]);
+                }
             }
-            LSR_TAKE(0, w * g[0], a.g_color + 3 * (size_t)gid)
-            LSR_TAKE(1, w * g[1], a.g_color + 3 * (size_t)gid + 1)
-            LSR_TAKE(2, w * g[2], a.g_color + 3 * (size_t)gid + 2)
-            LSR_TAKE(3, gm2x, &a.g_mean2D[gid].x)
-            LSR_TAKE(4, gm2y, &a.g_mean2D[gid].y)
-            LSR_TAKE(5, gcx, &a.g_conic[gid].x)
-            LSR_TAKE(6, gcy, &a.g_conic[gid].y)
-            LSR_TAKE(7, gcw, &a.g_conic[gid].z)
-            LSR_TAKE(8, w * gD, &a.g_conic[gid].w)
-            LSR_TAKE(9, gop, a.g_opacity ? a.g_opacity + gid : nullptr)
-            if constexpr (CPAD > 0) {
-#pragma unroll
-                for (int c = 0; c < CPAD; ++c)
-                    LSR_TAKE(10 + c, w * gL[c], (a.g_lang && c < C) ? a.g_lang + (size_t)gid * C + c : nullptr)
-            }
-#undef LSR_TAKE
-#pragma unroll
-            for (int r = 0; r < ROUNDS; ++r)
-                if (dst[r]) atomicAdd(dst[r], mine[r]);
+            if (lane == 0) s_act[j] = 1u;
         }
+        __syncthreads();
+        // write the batch's records (only entries with a contributing pixel), float4 at a time
+        constexpr int R4 = RECQ / 4;
+        for (int e = tid; e < nb * R4; e += 256) {
+            const int j = e / R4, c4 = e - j * R4;
+            if (s_act[j]) {
+                reinterpret_cast<float4*>(a.rec + (size_t)s_inst[j] * RECQ)[c4] =
+                    reinterpret_cast<const float4*>(s_rec + j * RECQ)[c4];
+            }
+        }
+        if (tid < nb && s_act[tid]) a.flags[s_inst[tid]] = 1;
     }
 }
 
-template <int CPAD, int BATCH>
+template <int CPAD, int BATCH, int Q>
 static void go_bwd(const RenderBwdArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL((k_render_bwd<CPAD, BATCH>), dim3(a.grid_x * a.grid_y), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((k_render_bwd<CPAD, BATCH, Q>), dim3(a.grid_x * a.grid_y), dim3(256), 0, st, a);
 }
 
 void launch_render_bwd(const RenderBwdArgs& a, hipStream_t st) {
     const int C = a.include_feature ? a.C : 0;
-    if (C == 0) go_bwd<0, 256>(a, st);
-    else if (C <= 4) go_bwd<4, 256>(a, st);
-    else if (C <= 8) go_bwd<8, 256>(a, st);
-    else if (C <= 16) go_bwd<16, 128>(a, st);
-    else if (C <= 32) go_bwd<32, 128>(a, st);
-    else go_bwd<64, 64>(a, st);
+    switch (lang_pad(C)) {
+        case 0: go_bwd<0, 64, 16>(a, st); break;
+        case 4: go_bwd<4, 64, 16>(a, st); break;
+        case 8: go_bwd<8, 64, 32>(a, st); break;
+        case 16: go_bwd<16, 64, 32>(a, st); break;
+        case 32: go_bwd<32, 64, 64>(a, st); break;
+        default: go_bwd<64, 32, 128>(a, st); break;
+    }
 }
 
 }  // namespace lsr

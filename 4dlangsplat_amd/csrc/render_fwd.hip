@@ -5,6 +5,7 @@
 // background, depth = sum z alpha T).  One 256-thread workgroup per 16x16 tile, each wave owning
 // an 8x8 quadrant (compact footprint: fewer waves touched per splat).  The tile's list is streamed
 // through LDS in batches; the per-Gaussian record is gathered as float2 + 2 x float4 + C floats.
+// Lanes skip exp where alpha < 1/255 is certain from the power alone (skip_power).
 // The workgroup stops early once every pixel has saturated.  Also writes, per tile, the largest
 // n_contrib of its pixels, which bounds the backward replay.
 #include "lsr_common.h"
@@ -18,6 +19,7 @@ __global__ void __launch_bounds__(256) k_render_fwd(RenderFwdArgs a) {
     __shared__ float2 s_xy[BATCH];
     __shared__ float4 s_co[BATCH];
     __shared__ float4 s_rgbd[BATCH];
+    __shared__ float s_thr[BATCH];
     __shared__ float s_lang[CPAD > 0 ? BATCH * CPAD : 1];
     __shared__ uint32_t s_max;
 
@@ -48,8 +50,10 @@ __global__ void __launch_bounds__(256) k_render_fwd(RenderFwdArgs a) {
             const uint32_t g = a.point_list[start + tid];
             s_id[tid] = g;
             s_xy[tid] = a.xy[g];
-            s_co[tid] = a.conic_o[g];
+            const float4 co = a.conic_o[g];
+            s_co[tid] = co;
             s_rgbd[tid] = a.rgbd[g];
+            s_thr[tid] = skip_power(co.w);
         }
         if constexpr (CPAD > 0) {
             __syncthreads();
@@ -66,7 +70,7 @@ __global__ void __launch_bounds__(256) k_render_fwd(RenderFwdArgs a) {
             const float4 co = s_co[j];
             const float dx = xy.x - pxf, dy = xy.y - pyf;
             const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-            if (power > 0.0f) continue;
+            if (power > 0.0f || power < s_thr[j]) continue;   // the second test never changes a decision
             const float alpha = fminf(0.99f, co.w * expf_repro(power));
             if (alpha < 1.0f / 255.0f) continue;
             const float test_T = T * (1.0f - alpha);

@@ -37,8 +37,8 @@
  *   pinned by fp64 finite differences (compile with -DORC_DOUBLE) wherever no clamp is active.
  *
  * Floating point
- *   Compiled with -ffp-contract=off.  exp() of the Gaussian falloff uses orc_expf, a
- *   Cody-Waite + degree-7 Horner exp (<= 2 ulp) written only with IEEE +,-,*, rint and exponent
+ *   Compiled with -ffp-contract=off.  exp() of the Gaussian falloff uses orc_exp, a
+ *   Cody-Waite + degree-7 Horner exp (<= 2 ulp) written only with IEEE *, fmaf, rint and exponent
  *   bit assembly, so that the product kernels can reproduce the contributor decisions
  *   (alpha < 1/255, T < 1e-4) bit for bit.  The CUDA original uses expf (<= 2 ulp as well).
  */
@@ -65,20 +65,21 @@ typedef float real;
 #define RCEIL ceilf
 #define RMIN fminf
 #define RMAX fmaxf
-/* exp for x <= 0; bit-reproducible with the HIP kernels' lsr_expf. */
+/* exp for x <= 0; bit-reproducible with the HIP kernels' expf_repro (fmaf is correctly rounded on
+ * both sides, so the sequence of roundings is identical). */
 static inline float orc_exp(float x) {
     if (!(x >= -87.0f)) return 0.0f;
     const float kf = rintf(x * 1.44269504088896341f);
-    float r = x - kf * 0.693145751953125f;
-    r = r - kf * 1.428606765330187045e-06f;
+    float r = fmaf(kf, -0.693145751953125f, x);
+    r = fmaf(kf, -1.428606765330187045e-06f, r);
     float p = 1.98412698412698413e-04f;  /* 1/5040 */
-    p = p * r + 1.38888888888888889e-03f; /* 1/720 */
-    p = p * r + 8.33333333333333333e-03f; /* 1/120 */
-    p = p * r + 4.16666666666666667e-02f; /* 1/24 */
-    p = p * r + 1.66666666666666667e-01f; /* 1/6 */
-    p = p * r + 0.5f;
-    p = p * r + 1.0f;
-    p = p * r + 1.0f;
+    p = fmaf(p, r, 1.38888888888888889e-03f); /* 1/720 */
+    p = fmaf(p, r, 8.33333333333333333e-03f); /* 1/120 */
+    p = fmaf(p, r, 4.16666666666666667e-02f); /* 1/24 */
+    p = fmaf(p, r, 1.66666666666666667e-01f); /* 1/6 */
+    p = fmaf(p, r, 0.5f);
+    p = fmaf(p, r, 1.0f);
+    p = fmaf(p, r, 1.0f);
     const int k = (int)kf;
     union { uint32_t u; float f; } s;
     s.u = (uint32_t)(k + 127) << 23;

@@ -1,0 +1,17 @@
+"""Unit checks of device building blocks on exact integer data (GPU)."""
+import os
+import subprocess
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_wave_transpose_reduce(tmp_path):
+    src = os.path.join(ROOT, "tests", "kernels", "t_transpose_reduce.hip")
+    exe = str(tmp_path / "t_tr")
+    subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-o", exe, src], check=True)
+    r = subprocess.run(["timeout", "-k", "5", "60", exe], capture_output=True, text=True)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
