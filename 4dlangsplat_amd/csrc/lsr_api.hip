@@ -163,14 +163,19 @@ Img carve_img(void* base, int W, int H, size_t* bytes) {
 }
 
 struct Scratch {
-    float* rec;          // [K, record_floats(C)] per-(Gaussian, tile) gradient records
+    float* acc_small;    // [P,12] atomic mode accumulators (zeroed per call)
+    float* rec;          // [K, record_floats(C)] deterministic mode records
     uint8_t* flags;      // [K] record written
 };
-Scratch carve_scratch(void* base, size_t K, int recq, size_t* bytes) {
+Scratch carve_scratch(void* base, size_t P, size_t K, int recq, bool det, size_t* bytes) {
     Carver c(base);
-    Scratch s;
-    s.rec = c.take<float>(K * (size_t)recq);
-    s.flags = c.take<uint8_t>(K);
+    Scratch s{};
+    if (det) {
+        s.rec = c.take<float>(K * (size_t)recq);
+        s.flags = c.take<uint8_t>(K);
+    } else {
+        s.acc_small = c.take<float>(P * 12);
+    }
     if (bytes) *bytes = c.off;
     return s;
 }
@@ -227,10 +232,10 @@ int64_t lsr_img_bytes(int32_t W, int32_t H) {
     carve_img(nullptr, W, H, &b);
     return (int64_t)b;
 }
-int64_t lsr_backward_bytes(int32_t P, int64_t K, int32_t C) {
-    (void)P;
+int64_t lsr_backward_bytes(int32_t P, int64_t K, int32_t C, int32_t deterministic) {
     size_t b;
-    carve_scratch(nullptr, (size_t)(K > 0 ? K : 1), lsr::record_floats(C > 0 ? C : 0), &b);
+    carve_scratch(nullptr, (size_t)(P > 0 ? P : 1), (size_t)(K > 0 ? K : 1), lsr::record_floats(C > 0 ? C : 0),
+                  deterministic != 0, &b);
     return (int64_t)b;
 }
 
@@ -357,8 +362,14 @@ int lsr_backward(const lsr_settings* s, const lsr_fwd_in* in, const lsr_bwd_in* 
     Img m = carve_img(const_cast<void*>(img), W, H, nullptr);
     const int Ceff = s->include_feature ? C : 0;
     const int recq = lsr::record_floats(Ceff);
-    Scratch sc = carve_scratch(scratch, K > 0 ? K : 1, recq, nullptr);
-    if (K > 0) LSR_HIP(hipMemsetAsync(sc.flags, 0, K, st));
+    const bool det = gin->deterministic != 0;
+    Scratch sc = carve_scratch(scratch, (size_t)P, K > 0 ? K : 1, recq, det, nullptr);
+    if (det && K > 0) LSR_HIP(hipMemsetAsync(sc.flags, 0, K, st));
+    if (!det) {
+        LSR_HIP(hipMemsetAsync(sc.acc_small, 0, sizeof(float) * 12 * (size_t)P, st));
+        if (!accumulate && Ceff > 0 && gout->dL_dlanguage_feature)
+            LSR_HIP(hipMemsetAsync(gout->dL_dlanguage_feature, 0, sizeof(float) * (size_t)P * C, st));
+    }
     const uint32_t* point_list = tile_sort_in_b(gx * gy) ? b.val_b : b.val_a;
     if (K > 0) {
         lsr::RenderBwdArgs r{};
@@ -368,7 +379,8 @@ int lsr_backward(const lsr_settings* s, const lsr_fwd_in* in, const lsr_bwd_in* 
         r.lang = in->language_feature; r.bg = s->bg; r.final_T = m.final_T; r.n_contrib = m.n_contrib;
         r.tile_max_contrib = m.tile_max;
         r.dL_dcolor = gin->dL_dout_color; r.dL_dlang = gin->dL_dout_language_feature; r.dL_ddepth = gin->dL_dout_depth;
-        r.rec = sc.rec; r.flags = sc.flags; r.recq = recq;
+        r.rec = sc.rec; r.flags = sc.flags; r.recq = recq; r.deterministic = det;
+        r.acc_small = sc.acc_small; r.acc_lang = gout->dL_dlanguage_feature;
         {
             PhaseTimer t(LSR_PHASE_RENDER_BWD, st);
             lsr::launch_render_bwd(r, st);
@@ -386,6 +398,7 @@ int lsr_backward(const lsr_settings* s, const lsr_fwd_in* in, const lsr_bwd_in* 
     a.tiles = g.tiles;
     a.clamped = g.clamped;
     a.rec = sc.rec; a.flags = sc.flags; a.inst_off = g.inst_off; a.recq = recq;
+    a.deterministic = det; a.acc_small = sc.acc_small;
     a.dopacity = gout->dL_dopacity;
     a.dmeans3D = gout->dL_dmeans3D; a.dmeans2D = gout->dL_dmeans2D; a.dcolors = gout->dL_dcolors;
     a.dcov3D = gout->dL_dcov3D; a.dsh = in->shs ? gout->dL_dsh : nullptr; a.dscales = gout->dL_dscales;
@@ -393,7 +406,7 @@ int lsr_backward(const lsr_settings* s, const lsr_fwd_in* in, const lsr_bwd_in* 
     {
         PhaseTimer t(LSR_PHASE_PREPROCESS_BWD, st);
         lsr::launch_preprocess_bwd(a, accumulate != 0, st);
-        if (Ceff > 0)
+        if (Ceff > 0 && det)
             lsr::launch_reduce_lang(P, C, lsr::lang_pad(C), recq, sc.rec, sc.flags, g.inst_off, g.tiles,
                                     gout->dL_dlanguage_feature, accumulate != 0, st);
     }

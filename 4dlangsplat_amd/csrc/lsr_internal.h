@@ -48,6 +48,8 @@ struct PreprocessBwdArgs {
     const uint8_t* flags;
     const uint32_t* inst_off;
     int recq;
+    int deterministic;
+    const float* acc_small;   // atomic mode: [P,12] summed records
     // outputs (nullable)
     float* dopacity;
     float* dmeans3D;
@@ -99,6 +101,10 @@ struct RenderBwdArgs {
     float* rec;
     uint8_t* flags;
     int recq;
+    int deterministic;
+    // default (atomic) mode: per-Gaussian accumulators
+    float* acc_small;         // [P,12] record layout [0..11]
+    float* acc_lang;          // [P,C] (the caller's dL/dlanguage buffer), may be null
 };
 
 // record width for C language channels (multiple of 4 floats)

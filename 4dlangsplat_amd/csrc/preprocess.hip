@@ -211,7 +211,7 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
 void launch_preprocess(const PreprocessArgs& a, hipStream_t st) {
     if (a.P == 0) return;
     const dim3 grid((a.P + 255) / 256), block(256);
-    const int ms = (a.shs && !a.colors_precomp) ? a.M : 0;
+    const int ms = 0;   // direct SH reads measured faster than LDS staging here (occupancy)
     switch (ms) {
         case 1: hipLaunchKernelGGL(k_preprocess<1>, grid, block, 0, st, a); break;
         case 4: hipLaunchKernelGGL(k_preprocess<4>, grid, block, 0, st, a); break;
@@ -357,7 +357,14 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
         float rs[12];
 #pragma unroll
         for (int k = 0; k < 12; ++k) rs[k] = 0.0f;
-        if (vis) {
+        if (vis && !a.deterministic) {
+            const float4* r4 = reinterpret_cast<const float4*>(a.acc_small + (size_t)i * 12);
+#pragma unroll
+            for (int k4 = 0; k4 < 3; ++k4) {
+                const float4 v = r4[k4];
+                rs[4 * k4] = v.x; rs[4 * k4 + 1] = v.y; rs[4 * k4 + 2] = v.z; rs[4 * k4 + 3] = v.w;
+            }
+        } else if (vis) {
             const uint32_t e0 = a.inst_off[i];
             for (uint32_t e = e0; e < e0 + ntile; ++e) {
                 if (!a.flags[e]) continue;

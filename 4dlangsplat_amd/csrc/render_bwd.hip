@@ -13,16 +13,20 @@
 //   * lanes skip exp when power < ln(1 / (255 o)) - 1e-3 (alpha < 1/255 for certain);
 //   * per (Gaussian, wave) the 10 + C per-pixel contributions are summed over the 64 lanes by a
 //     transpose-reduce (permlane32/16 swaps + DPP), which leaves one quantity per lane; the four
-//     waves of the tile add them into an LDS record (one ds_add per lane); each (Gaussian, tile)
-//     record is then written once with plain stores at the Gaussian's instance slot, where the
-//     per-Gaussian reduction (preprocess.hip) reads them back contiguously.  No global atomics:
-//     the backward is deterministic.
+//     waves of the tile add them into an LDS record (one ds_add per lane).  Then, per
+//     (Gaussian, tile):
+//       default        one atomic wave-instruction adds the record to the Gaussian's accumulators
+//                      (10 floats + the C language floats: two contiguous segments); the atomics
+//                      overlap the replay, which is VALU-bound;
+//       deterministic  the record is written with plain stores at the Gaussian's instance slot
+//                      and the per-Gaussian reduction (preprocess.hip) sums them in a fixed order,
+//                      so the gradients are bitwise reproducible.
 #include "lsr_common.h"
 #include "lsr_internal.h"
 
 namespace lsr {
 
-template <int CPAD, int BATCH, int Q>
+template <int CPAD, int BATCH, int Q, bool DET>
 __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
     constexpr int RECQ = 12 + CPAD;
     static_assert(RECQ <= Q || Q == 128, "quantities must fit the transpose-reduce width");
@@ -172,22 +176,34 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
             if (lane == 0) s_act[j] = 1u;
         }
         __syncthreads();
-        // write the batch's records (only entries with a contributing pixel), float4 at a time
-        constexpr int R4 = RECQ / 4;
-        for (int e = tid; e < nb * R4; e += 256) {
-            const int j = e / R4, c4 = e - j * R4;
-            if (s_act[j]) {
-                reinterpret_cast<float4*>(a.rec + (size_t)s_inst[j] * RECQ)[c4] =
-                    reinterpret_cast<const float4*>(s_rec + j * RECQ)[c4];
+        if constexpr (DET) {
+            // write the batch's records (only entries with a contributing pixel), float4 at a time
+            constexpr int R4 = RECQ / 4;
+            for (int e = tid; e < nb * R4; e += 256) {
+                const int j = e / R4, c4 = e - j * R4;
+                if (s_act[j]) {
+                    reinterpret_cast<float4*>(a.rec + (size_t)s_inst[j] * RECQ)[c4] =
+                        reinterpret_cast<const float4*>(s_rec + j * RECQ)[c4];
+                }
+            }
+            if (tid < nb && s_act[tid]) a.flags[s_inst[tid]] = 1;
+        } else {
+            // one atomic per quantity of each active entry; consecutive lanes -> consecutive addresses
+            for (int e = tid; e < nb * RECQ; e += 256) {
+                const int j = e / RECQ, q = e - j * RECQ;
+                if (!s_act[j] || q == 10 || q == 11) continue;
+                const uint32_t gid = s_id[j];
+                if (q < 12) atomicAdd(a.acc_small + (size_t)gid * 12 + q, s_rec[e]);
+                else if (a.acc_lang && q - 12 < C) atomicAdd(a.acc_lang + (size_t)gid * C + (q - 12), s_rec[e]);
             }
         }
-        if (tid < nb && s_act[tid]) a.flags[s_inst[tid]] = 1;
     }
 }
 
 template <int CPAD, int BATCH, int Q>
 static void go_bwd(const RenderBwdArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL((k_render_bwd<CPAD, BATCH, Q>), dim3(a.grid_x * a.grid_y), dim3(256), 0, st, a);
+    if (a.deterministic) hipLaunchKernelGGL((k_render_bwd<CPAD, BATCH, Q, true>), dim3(a.grid_x * a.grid_y), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((k_render_bwd<CPAD, BATCH, Q, false>), dim3(a.grid_x * a.grid_y), dim3(256), 0, st, a);
 }
 
 void launch_render_bwd(const RenderBwdArgs& a, hipStream_t st) {

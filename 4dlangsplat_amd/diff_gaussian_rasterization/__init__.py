@@ -161,9 +161,10 @@ def forward_native(raster_settings, means3D, opacities, shs=None, colors_precomp
 
 
 def backward_native(state: RasterizerState, grad_color, grad_lang=None, grad_depth=None, out=None,
-                    accumulate=False, need=None):
+                    accumulate=False, need=None, deterministic=False):
     """Backward through liblsr.so.  `out` may hold preallocated gradient buffers (dict); with
-    accumulate=True they are added to.  Returns the dict of gradient tensors."""
+    accumulate=True they are added to.  deterministic=True selects the fixed-order reduction
+    (bitwise reproducible gradients).  Returns the dict of gradient tensors."""
     L = _lib.load()
     inp = state.inputs
     means3D = inp["means3D"]
@@ -197,12 +198,14 @@ def backward_native(state: RasterizerState, grad_color, grad_lang=None, grad_dep
     gd = grad_depth.detach().to(torch.float32).contiguous() if grad_depth is not None else None
     gin = _lib.BwdIn()
     gin.dL_dout_color, gin.dL_dout_language_feature, gin.dL_dout_depth = gc.data_ptr(), _ptr(gl), _ptr(gd)
+    gin.deterministic = 1 if deterministic else 0
     gout = _lib.BwdOut()
     gout.dL_dmeans3D, gout.dL_dmeans2D, gout.dL_dcolors = _ptr(g["means3D"]), _ptr(g["means2D"]), _ptr(g["colors"])
     gout.dL_dlanguage_feature, gout.dL_dopacity = _ptr(g["language_feature"]), _ptr(g["opacities"])
     gout.dL_dcov3D, gout.dL_dsh = _ptr(g["cov3D"]), _ptr(g["sh"])
     gout.dL_dscales, gout.dL_drotations = _ptr(g["scales"]), _ptr(g["rotations"])
-    scratch = torch.empty(int(L.lsr_backward_bytes(P, state.num_rendered, C)), dtype=torch.uint8, device=device)
+    scratch = torch.empty(int(L.lsr_backward_bytes(P, state.num_rendered, C, 1 if deterministic else 0)),
+                          dtype=torch.uint8, device=device)
     rc = L.lsr_backward(ctypes.byref(state.settings.c), ctypes.byref(state.fin), ctypes.byref(gin), ctypes.byref(gout),
                         ctypes.c_void_p(state.geom.data_ptr()), ctypes.c_void_p(state.binning.data_ptr()),
                         ctypes.c_void_p(state.img.data_ptr()), ctypes.c_void_p(scratch.data_ptr()),

@@ -42,7 +42,7 @@ class FwdOut(ctypes.Structure):
 
 class BwdIn(ctypes.Structure):
     _fields_ = [("dL_dout_color", ctypes.c_void_p), ("dL_dout_language_feature", ctypes.c_void_p),
-                ("dL_dout_depth", ctypes.c_void_p)]
+                ("dL_dout_depth", ctypes.c_void_p), ("deterministic", ctypes.c_int32)]
 
 
 class BwdOut(ctypes.Structure):
@@ -59,7 +59,7 @@ SIGNATURES = {
     "lsr_geom_bytes": (ctypes.c_int64, [ctypes.c_int32]),
     "lsr_binning_bytes": (ctypes.c_int64, [ctypes.c_int64]),
     "lsr_img_bytes": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32]),
-    "lsr_backward_bytes": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int64, ctypes.c_int32]),
+    "lsr_backward_bytes": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
     "lsr_forward_preprocess": (ctypes.c_int, [ctypes.POINTER(Settings), ctypes.POINTER(FwdIn), ctypes.POINTER(FwdOut),
                                               ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
     "lsr_forward_render": (ctypes.c_int, [ctypes.POINTER(Settings), ctypes.POINTER(FwdIn), ctypes.POINTER(FwdOut),

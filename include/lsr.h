@@ -88,6 +88,8 @@ typedef struct lsr_bwd_in {
     const float *dL_dout_color;              /* [3,H,W] */
     const float *dL_dout_language_feature;   /* [C,H,W] or NULL (treated as zero) */
     const float *dL_dout_depth;              /* [1,H,W] or NULL (treated as zero) */
+    int32_t deterministic;                   /* 1: fixed-order reduction, bitwise reproducible
+                                                gradients (slower); 0: float atomics, as upstream */
 } lsr_bwd_in;
 
 typedef struct lsr_bwd_out {                 /* any pointer may be NULL if that gradient is unused */
@@ -109,7 +111,7 @@ const char *lsr_last_error(void);
 int64_t lsr_geom_bytes(int32_t P);
 int64_t lsr_binning_bytes(int64_t num_rendered);
 int64_t lsr_img_bytes(int32_t image_width, int32_t image_height);
-int64_t lsr_backward_bytes(int32_t P, int64_t num_rendered, int32_t C);
+int64_t lsr_backward_bytes(int32_t P, int64_t num_rendered, int32_t C, int32_t deterministic);
 
 /* Forward, phase 1: per-Gaussian preprocess (cull, EWA projection, SH colour, tile count) and
  * the depth ordering of the visible set.  Writes out->radii.  Returns num_rendered, the number of

@@ -48,7 +48,8 @@ def test_size_queries():
     assert 0 < g1 < g2 and g2 >= 2_000_000 * 60
     assert lib.lsr_binning_bytes(8_600_000) >= 8_600_000 * 16
     assert lib.lsr_img_bytes(1352, 1014) >= 1352 * 1014 * 8
-    assert lib.lsr_backward_bytes(2_000_000, 8_600_000, 32) >= 2_000_000 * 36
+    assert lib.lsr_backward_bytes(2_000_000, 8_600_000, 32, 0) >= 2_000_000 * 48
+    assert lib.lsr_backward_bytes(2_000_000, 8_600_000, 32, 1) >= 8_600_000 * 44 * 4
 
 
 def test_settings_validation_messages():
