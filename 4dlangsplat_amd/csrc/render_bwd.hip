@@ -30,7 +30,8 @@ template <int CPAD, int BATCH, int Q, bool DET>
 __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
     constexpr int RECQ = 12 + CPAD;
     static_assert(RECQ <= Q || Q == 128, "quantities must fit the transpose-reduce width");
-    __shared__ float s_rec[BATCH * RECQ];
+    constexpr int NSLOT = DET ? 4 : 1;          // deterministic: one partial record per wave, summed in order
+    __shared__ float s_rec[NSLOT * BATCH * RECQ];
     __shared__ float s_lang[CPAD > 0 ? BATCH * CPAD : 1];
     __shared__ float4 s_co[BATCH];
     __shared__ float4 s_rgbd[BATCH];
@@ -92,7 +93,7 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
             s_inst[tid] = a.inst_off[gid] + (uint32_t)((ty - rmin.y) * (rmax.x - rmin.x) + (tx - rmin.x));
             s_act[tid] = 0;
         }
-        for (int e = tid; e < nb * RECQ; e += 256) s_rec[e] = 0.0f;
+        for (int e = tid; e < NSLOT * BATCH * RECQ; e += 256) s_rec[e] = 0.0f;
         if constexpr (CPAD > 0) {
             __syncthreads();
             for (int e = tid; e < nb * CPAD; e += 256) {
@@ -162,15 +163,21 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
 #pragma unroll
             for (int q = RECQ; q < Q; ++q) v[q] = 0.0f;
             wave_transpose_reduce<Q>(v);
-            float* rec = s_rec + j * RECQ;
+            float* rec = s_rec + ((DET ? wave * BATCH : 0) + j) * RECQ;
             if constexpr (Q <= 64) {
                 const int q = transpose_reduce_slot<Q>(lane);
-                if ((lane & (64 / Q - 1)) == 0 && q < RECQ) atomicAdd(rec + q, v[0]);
+                if ((lane & (64 / Q - 1)) == 0 && q < RECQ) {
+                    if constexpr (DET) rec[q] = v[0];
+                    else atomicAdd(rec + q, v[0]);
+                }
             } else {
 #pragma unroll
                 for (int kk = 0; kk < Q / 64; ++kk) {
                     const int q = kk + (Q / 64) * lane;
-                    if (q < RECQ) atomicAdd(rec + q, v[kk]);
+                    if (q < RECQ) {
+                        if constexpr (DET) rec[q] = v[kk];
+                        else atomicAdd(rec + q, v[kk]);
+                    }
                 }
             }
             if (lane == 0) s_act[j] = 1u;
@@ -182,8 +189,13 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
             for (int e = tid; e < nb * R4; e += 256) {
                 const int j = e / R4, c4 = e - j * R4;
                 if (s_act[j]) {
-                    reinterpret_cast<float4*>(a.rec + (size_t)s_inst[j] * RECQ)[c4] =
-                        reinterpret_cast<const float4*>(s_rec + j * RECQ)[c4];
+                    float4 t = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+                    for (int w4 = 0; w4 < NSLOT; ++w4) {   // fixed order over the waves
+                        const float4 u = reinterpret_cast<const float4*>(s_rec + (w4 * BATCH + j) * RECQ)[c4];
+                        t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+                    }
+                    reinterpret_cast<float4*>(a.rec + (size_t)s_inst[j] * RECQ)[c4] = t;
                 }
             }
             if (tid < nb && s_act[tid]) a.flags[s_inst[tid]] = 1;
@@ -202,7 +214,7 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
 
 template <int CPAD, int BATCH, int Q>
 static void go_bwd(const RenderBwdArgs& a, hipStream_t st) {
-    if (a.deterministic) hipLaunchKernelGGL((k_render_bwd<CPAD, BATCH, Q, true>), dim3(a.grid_x * a.grid_y), dim3(256), 0, st, a);
+    if (a.deterministic) hipLaunchKernelGGL((k_render_bwd<CPAD, (BATCH > 32 ? 32 : BATCH), Q, true>), dim3(a.grid_x * a.grid_y), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((k_render_bwd<CPAD, BATCH, Q, false>), dim3(a.grid_x * a.grid_y), dim3(256), 0, st, a);
 }
 
