@@ -15,3 +15,12 @@ def test_wave_transpose_reduce(tmp_path):
     r = subprocess.run(["timeout", "-k", "5", "60", exe], capture_output=True, text=True)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_mfma_bf16_layout(tmp_path):
+    src = os.path.join(ROOT, "tests", "kernels", "t_mfma_layout.hip")
+    exe = str(tmp_path / "t_mfma")
+    subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-o", exe, src], check=True)
+    r = subprocess.run(["timeout", "-k", "5", "60", exe], capture_output=True, text=True)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
