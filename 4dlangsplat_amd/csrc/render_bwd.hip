@@ -225,7 +225,10 @@ void launch_render_bwd(const RenderBwdArgs& a, hipStream_t st) {
         case 4: go_bwd<4, 64, 16>(a, st); break;
         case 8: go_bwd<8, 64, 32>(a, st); break;
         case 16: go_bwd<16, 64, 32>(a, st); break;
-        case 32: go_bwd<32, 64, 64>(a, st); break;
+        case 32:
+            if (a.deterministic) go_bwd<32, 64, 64>(a, st);
+            else launch_render_bwd_mfma(a, st);   // language channels on matrix cores
+            break;
         default: go_bwd<64, 32, 128>(a, st); break;
     }
 }

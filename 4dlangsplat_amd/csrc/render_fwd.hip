@@ -322,7 +322,7 @@ void launch_render_fwd(const RenderFwdArgs& a, hipStream_t st) {
     else if (C <= 4) go_fwd<4, 256>(a, st);
     else if (C <= 8) go_fwd<8, 256>(a, st);
     else if (C <= 16) go_fwd<16, 128>(a, st);
-    else if (C <= 32) hipLaunchKernelGGL(k_render_fwd_mfma<1>, dim3(a.grid_x * a.grid_y), dim3(256), 0, st, a);
+    else if (C <= 32) go_fwd<32, 128>(a, st);   // VALU variant measured faster at 32 channels (serial-loop bound)
     else hipLaunchKernelGGL(k_render_fwd_mfma<2>, dim3(a.grid_x * a.grid_y), dim3(256), 0, st, a);
 }
 
