@@ -57,14 +57,14 @@ __device__ __forceinline__ bf16x4 ds_read_tr_b16(const __bf16* p) {
 #define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
 
 constexpr int BG = 32;     // entries per MFMA group
-constexpr int BSB = 64;    // entries staged per LDS batch (2 groups)
+constexpr int BSB = 32;    // entries staged per LDS batch (1 group)
 constexpr int FPT = 40;    // F row pitch in bf16 (32 channels + 8 pad)
-constexpr int WPT = 40;    // W row pitch in bf16 (32 entries + 8 pad)
+constexpr int WPT = 36;    // W row pitch in bf16 (32 entries + 4 pad; 8-byte aligned rows for the tr reads)
 constexpr int GTP = 72;    // G^T row pitch in bf16 (64 pixels + 8 pad)
 constexpr int RQ = 12;     // scalar record: rgb 0-2, depth 3, mean2D 4-5, conic 6-8, opacity 9
 
 template <bool DUMMY>
-__global__ void __launch_bounds__(256) k_render_bwd_mfma(RenderBwdArgs a) {
+__global__ void __launch_bounds__(256, 3) k_render_bwd_mfma(RenderBwdArgs a) {
     __shared__ __attribute__((aligned(16))) __bf16 s_Fh[BSB][FPT];
     __shared__ __attribute__((aligned(16))) __bf16 s_Fl[BSB][FPT];
     __shared__ __attribute__((aligned(16))) __bf16 s_W[4][2][64][WPT];     // per wave: hi, lo rows [px][e]
