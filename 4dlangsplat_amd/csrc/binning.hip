@@ -18,50 +18,89 @@ void launch_iota(int n, uint32_t* out, hipStream_t st) {
     if (n > 0) hipLaunchKernelGGL(k_iota, dim3((n + 255) / 256), dim3(256), 0, st, n, out);
 }
 
+// Depth-order pass: the one random gather of the binning (8 B per Gaussian), after which the
+// emission reads only coalesced depth-ordered arrays.
 __global__ void __launch_bounds__(256) k_gather_tile_counts(int P, const uint32_t* __restrict__ order,
-                                                            const uint32_t* __restrict__ tiles,
-                                                            uint32_t* __restrict__ counts) {
+                                                            const uint2* __restrict__ rect,
+                                                            uint32_t* __restrict__ counts,
+                                                            uint2* __restrict__ rect_sorted) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= P) return;
-    counts[r] = tiles[order[r]];
+    const uint2 rc = rect[order[r]];
+    rect_sorted[r] = rc;
+    counts[r] = ((rc.y & 0xFFFFu) - (rc.x & 0xFFFFu)) * ((rc.y >> 16) - (rc.x >> 16));
 }
 
-void launch_gather_tile_counts(int P, const uint32_t* order, const uint32_t* tiles, uint32_t* counts, hipStream_t st) {
+void launch_gather_tile_counts(int P, const uint32_t* order, const uint2* rect, uint32_t* counts, uint2* rect_sorted,
+                               hipStream_t st) {
     if (P == 0) return;
-    hipLaunchKernelGGL(k_gather_tile_counts, dim3((P + 255) / 256), dim3(256), 0, st, P, order, tiles, counts);
+    hipLaunchKernelGGL(k_gather_tile_counts, dim3((P + 255) / 256), dim3(256), 0, st, P, order, rect, counts,
+                       rect_sorted);
 }
 
-// One lane per depth rank: the tiles of its rectangle in row-major order, keys = tile id,
-// values = Gaussian id.  inst_offset_by_id[g] = first instance slot of Gaussian g (the backward
-// writes per-instance gradient records there, contiguous per Gaussian).
+// Instance emission, one wave per 64 consecutive depth ranks.  Their instances occupy one
+// contiguous slot range [offsets[r0], offsets[r0+63] + counts[r0+63]), so the wave walks that
+// range with consecutive lanes on consecutive slots (fully coalesced key/value stores); a lane
+// finds the rank owning its slot by binary search over the 64 start offsets in LDS.  Slot order
+// inside a Gaussian is its rectangle in row-major order (as upstream's duplicateWithKeys).
 __global__ void __launch_bounds__(256) k_emit(int P, const uint32_t* __restrict__ order,
                                               const uint32_t* __restrict__ offsets,
-                                              const uint32_t* __restrict__ tiles, const float2* __restrict__ xy,
-                                              const int* __restrict__ radii, int gx, int gy,
-                                              uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
-                                              uint32_t* __restrict__ inst_offset_by_id) {
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= P) return;
-    const uint32_t g = order[r];
-    if (tiles[g] == 0) return;
-    uint32_t off = offsets[r];
-    if (inst_offset_by_id) inst_offset_by_id[g] = off;
-    int2 rmin, rmax;
-    tile_rect(xy[g], radii[g], gx, gy, rmin, rmax);
-    for (int y = rmin.y; y < rmax.y; ++y)
-        for (int x = rmin.x; x < rmax.x; ++x) {
-            keys[off] = (uint32_t)(y * gx + x);
-            vals[off] = g;
-            ++off;
-        }
+                                              const uint32_t* __restrict__ counts,
+                                              const uint2* __restrict__ rect_sorted, int gx,
+                                              uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+    __shared__ uint32_t s_off[4][64];
+    __shared__ uint2 s_rc[4][64];
+    __shared__ uint32_t s_id[4][64];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int base = (blockIdx.x * 4 + w) * 64;
+    if (base >= P) return;                                   // wave-uniform
+    const int r = base + lane;
+    const bool ok = r < P;
+    const uint32_t cnt = ok ? counts[r] : 0u;
+    const uint32_t off = ok ? offsets[r] : 0u;
+    const int last = min(P - 1 - base, 63);
+    const uint32_t end = __shfl(off + cnt, last);
+    const uint32_t start = __shfl(off, 0);
+    s_off[w][lane] = ok ? off : end;                         // past-the-end lanes never own a slot
+    s_rc[w][lane] = ok ? rect_sorted[r] : make_uint2(0u, 0u);
+    s_id[w][lane] = ok ? order[r] : 0u;
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t j = start + lane; j < end; j += 64) {
+        int k = 0;                                           // last rank with s_off <= j
+#pragma unroll
+        for (int step = 32; step >= 1; step >>= 1)
+            if (s_off[w][k + step] <= j) k += step;
+        const uint2 rc = s_rc[w][k];
+        const uint32_t x0 = rc.x & 0xFFFFu, y0 = rc.x >> 16, wd = (rc.y & 0xFFFFu) - x0;
+        const uint32_t loc = j - s_off[w][k];
+        const uint32_t dy = loc / wd;
+        keys[j] = (y0 + dy) * (uint32_t)gx + x0 + (loc - dy * wd);
+        vals[j] = s_id[w][k];
+    }
 }
 
-void launch_emit_instances(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* tiles,
-                           const float2* xy, const int* radii, int grid_x, int grid_y, uint32_t* keys,
-                           uint32_t* vals, uint32_t* inst_offset_by_id, hipStream_t st) {
+void launch_emit_instances(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* counts,
+                           const uint2* rect_sorted, int grid_x, uint32_t* keys, uint32_t* vals, hipStream_t st) {
     if (P == 0) return;
-    hipLaunchKernelGGL(k_emit, dim3((P + 255) / 256), dim3(256), 0, st, P, order, offsets, tiles, xy, radii,
-                       grid_x, grid_y, keys, vals, inst_offset_by_id);
+    hipLaunchKernelGGL(k_emit, dim3((P + 255) / 256), dim3(256), 0, st, P, order, offsets, counts, rect_sorted,
+                       grid_x, keys, vals);
+}
+
+// inst_off[g] = first instance slot of Gaussian g: only the deterministic backward needs it (its
+// per-(Gaussian, tile) records are addressed by it), so it is scattered there, not in the forward.
+__global__ void __launch_bounds__(256) k_scatter_inst_off(int P, const uint32_t* __restrict__ order,
+                                                          const uint32_t* __restrict__ offsets,
+                                                          const uint32_t* __restrict__ counts,
+                                                          uint32_t* __restrict__ inst_off) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < P && counts[r] > 0) inst_off[order[r]] = offsets[r];
+}
+
+void launch_scatter_inst_off(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* counts,
+                             uint32_t* inst_off, hipStream_t st) {
+    if (P == 0) return;
+    hipLaunchKernelGGL(k_scatter_inst_off, dim3((P + 255) / 256), dim3(256), 0, st, P, order, offsets, counts,
+                       inst_off);
 }
 
 __global__ void __launch_bounds__(256) k_tile_ranges(size_t K, const uint32_t* __restrict__ keys,

@@ -101,6 +101,8 @@ struct Geom {
     uint32_t* offsets;
     uint32_t* inst_off;
     int* radius;
+    uint2* rect;          // by id, written by preprocess
+    uint2* rect_sorted;   // depth order
     uint32_t* total;
     void* sort_tmp;
     void* scan_tmp;
@@ -121,6 +123,8 @@ Geom carve_geom(void* base, size_t P, size_t* bytes) {
     g.offsets = c.take<uint32_t>(P);
     g.inst_off = c.take<uint32_t>(P);
     g.radius = c.take<int>(P);
+    g.rect = c.take<uint2>(P);
+    g.rect_sorted = c.take<uint2>(P);
     g.total = c.take<uint32_t>(4);
     g.sort_tmp = c.take<char>(lsr::radix_temp_bytes(P));
     g.scan_tmp = c.take<char>(lsr::scan_temp_bytes(P));
@@ -192,6 +196,8 @@ bool tile_sort_in_b(int ntiles) { return ((tile_bits(ntiles) + 7) / 8) % 2 == 1;
 int check_common(const lsr_settings* s, const lsr_fwd_in* in) {
     if (!s || !in) return fail(LSR_EINVAL, "null settings or inputs");
     if (s->image_width <= 0 || s->image_height <= 0) return fail(LSR_EINVAL, "image size must be positive");
+    if (s->image_width > 65535 * LSR_TILE_X || s->image_height > 65535 * LSR_TILE_Y)
+        return fail(LSR_EINVAL, "image size exceeds 65535 tiles per axis");
     if (in->P < 0) return fail(LSR_EINVAL, "P must be >= 0");
     if (!s->viewmatrix || !s->projmatrix || !s->bg || !s->campos)
         return fail(LSR_EINVAL, "viewmatrix, projmatrix, bg and campos are required");
@@ -262,7 +268,7 @@ int lsr_forward_preprocess(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_
     a.means3D = in->means3D; a.scales = in->scales; a.rotations = in->rotations; a.opacities = in->opacities;
     a.shs = in->shs; a.colors_precomp = in->colors_precomp; a.cov3D_precomp = in->cov3D_precomp;
     a.view = s->viewmatrix; a.proj = s->projmatrix; a.campos = s->campos;
-    a.radii = out->radii; a.radius = g.radius; a.tiles = g.tiles; a.key = g.key_a; a.xy = g.xy; a.conic_o = g.conic_o; a.rgbd = g.rgbd;
+    a.radii = out->radii; a.radius = g.radius; a.tiles = g.tiles; a.rect = g.rect; a.key = g.key_a; a.xy = g.xy; a.conic_o = g.conic_o; a.rgbd = g.rgbd;
     a.clamped = g.clamped;
     LSR_HIP(hipMemsetAsync(g.clamped, 0, (size_t)P, st));
     {
@@ -281,7 +287,7 @@ int lsr_forward_preprocess(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_
     LSR_LAUNCHED("depth sort", st, s->debug);
     {
         PhaseTimer t(LSR_PHASE_INSTANCE_SCAN, st);
-        lsr::launch_gather_tile_counts(P, g.val_a, g.tiles, g.counts, st);
+        lsr::launch_gather_tile_counts(P, g.val_a, g.rect, g.counts, g.rect_sorted, st);
         lsr::exclusive_scan_u32(g.counts, g.offsets, (size_t)P, g.total, g.scan_tmp, st);
     }
     LSR_LAUNCHED("instance scan", st, s->debug);
@@ -311,8 +317,7 @@ int lsr_forward_render(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_out*
     if (K > 0) {
         {
             PhaseTimer t(LSR_PHASE_EMIT, st);
-            lsr::launch_emit_instances(P, g.val_a, g.offsets, g.tiles, g.xy, out->radii, gx, gy, b.key_a, b.val_a,
-                                       g.inst_off, st);
+            lsr::launch_emit_instances(P, g.val_a, g.offsets, g.counts, g.rect_sorted, gx, b.key_a, b.val_a, st);
         }
         LSR_LAUNCHED("emit", st, s->debug);
         bool in_b;
@@ -364,7 +369,10 @@ int lsr_backward(const lsr_settings* s, const lsr_fwd_in* in, const lsr_bwd_in* 
     const int recq = lsr::record_floats(Ceff);
     const bool det = gin->deterministic != 0;
     Scratch sc = carve_scratch(scratch, (size_t)P, K > 0 ? K : 1, recq, det, nullptr);
-    if (det && K > 0) LSR_HIP(hipMemsetAsync(sc.flags, 0, K, st));
+    if (det && K > 0) {
+        LSR_HIP(hipMemsetAsync(sc.flags, 0, K, st));
+        lsr::launch_scatter_inst_off(P, g.val_a, g.offsets, g.counts, g.inst_off, st);
+    }
     if (!det) {
         LSR_HIP(hipMemsetAsync(sc.acc_small, 0, sizeof(float) * 12 * (size_t)P, st));
         if (!accumulate && Ceff > 0 && gout->dL_dlanguage_feature)

@@ -22,6 +22,7 @@ struct PreprocessArgs {
     int* radii;
     int* radius;      // internal copy of radii (the backward recomputes tile rectangles)
     uint32_t* tiles;
+    uint2* rect;      // tile rectangle, packed (x0 | y0 << 16, x1 | y1 << 16); 0 when culled
     uint32_t* key;
     float2* xy;
     float4* conic_o;
@@ -129,10 +130,12 @@ bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint
 
 // binning (binning.hip)
 void launch_iota(int n, uint32_t* out, hipStream_t st);
-void launch_gather_tile_counts(int P, const uint32_t* order, const uint32_t* tiles, uint32_t* counts, hipStream_t st);
-void launch_emit_instances(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* tiles,
-                           const float2* xy, const int* radii, int grid_x, int grid_y, uint32_t* keys,
-                           uint32_t* vals, uint32_t* inst_offset_by_id, hipStream_t st);
+void launch_gather_tile_counts(int P, const uint32_t* order, const uint2* rect, uint32_t* counts, uint2* rect_sorted,
+                               hipStream_t st);
+void launch_emit_instances(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* counts,
+                           const uint2* rect_sorted, int grid_x, uint32_t* keys, uint32_t* vals, hipStream_t st);
+void launch_scatter_inst_off(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* counts,
+                             uint32_t* inst_off, hipStream_t st);
 void launch_tile_ranges(size_t K, const uint32_t* keys, uint2* ranges, hipStream_t st);
 
 // compositing (render_fwd.hip / render_bwd.hip)

@@ -116,6 +116,7 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
     a.radii[i] = 0;
     a.radius[i] = 0;
     a.tiles[i] = 0;
+    a.rect[i] = make_uint2(0u, 0u);
     a.key[i] = 0xFFFFFFFFu;
     const float3 p = make_float3(a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]);
     const float4 ph = xform4x4(a.proj, p);
@@ -202,6 +203,7 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
     a.radii[i] = radius;
     a.radius[i] = radius;
     a.tiles[i] = (uint32_t)ntiles;
+    a.rect[i] = make_uint2((uint32_t)rmin.x | ((uint32_t)rmin.y << 16), (uint32_t)rmax.x | ((uint32_t)rmax.y << 16));
     a.key[i] = __float_as_uint(pv.z);
     a.xy[i] = pix;
     a.conic_o[i] = conic;
@@ -338,21 +340,50 @@ __device__ __forceinline__ void put(float* p, float v) {
     if (ACC) *p += v; else *p = v;
 }
 
+// Rows of culled Gaussians (no tiles) are neither read nor, when accumulating, written: their
+// gradient is exactly zero.  float4 loads (a row is 3*MS floats, 16-B aligned for MS = 16).
+template <int M3>
+__device__ __forceinline__ void stage_visible_rows(float* __restrict__ lds, const float* __restrict__ src, int rows,
+                                                   const uint8_t* __restrict__ s_vis) {
+    if constexpr (M3 > 0) {
+        constexpr int SP = M3 + 1;
+        if constexpr (M3 % 4 == 0) {
+            constexpr int R4 = M3 / 4;
+            const float4* s4 = reinterpret_cast<const float4*>(src);
+            for (int e = threadIdx.x; e < rows * R4; e += blockDim.x) {
+                const int r = e / R4, c = 4 * (e - r * R4);
+                if (!s_vis[r]) continue;
+                const float4 v = s4[e];
+                float* d = lds + r * SP + c;
+                d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+            }
+        } else {
+            for (int e = threadIdx.x; e < rows * M3; e += blockDim.x) {
+                const int r = e / M3, c = e - r * M3;
+                if (s_vis[r]) lds[r * SP + c] = src[e];
+            }
+        }
+    }
+}
+
 template <bool ACC, int MS>
 __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
     constexpr int M3 = MS * 3, SP = M3 + 1;
     __shared__ float s_sh[MS > 0 ? 256 * SP : 1];
+    __shared__ uint8_t s_vis[256];
     const int g0 = blockIdx.x * blockDim.x;
     const int rows = min(256, a.P - g0);
     const int i = g0 + threadIdx.x;
+    const uint32_t ntile = i < a.P ? a.tiles[i] : 0u;
+    const bool vis = ntile > 0;
     const bool stage = MS > 0 && a.shs != nullptr;
     if (stage) {
-        stage_rows<M3>(s_sh, a.shs + (size_t)g0 * M3, rows);
+        s_vis[threadIdx.x] = vis ? 1 : 0;
+        __syncthreads();
+        stage_visible_rows<M3>(s_sh, a.shs + (size_t)g0 * M3, rows, s_vis);
         __syncthreads();
     }
-    if (i < a.P) {
-        const uint32_t ntile = a.tiles[i];
-        const bool vis = ntile > 0;
+    if (i < a.P && (vis || !ACC)) {
         // sum the compositor's per-(Gaussian, tile) records: contiguous per Gaussian
         float rs[12];
 #pragma unroll
@@ -510,7 +541,7 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
         if constexpr (M3 > 0) {
             for (int e = threadIdx.x; e < rows * M3; e += blockDim.x) {
                 const int r = e / M3, c = e - r * M3;
-                put<ACC>(dst + e, s_sh[r * SP + c]);
+                if (!ACC || s_vis[r]) put<ACC>(dst + e, s_sh[r * SP + c]);
             }
         }
     }

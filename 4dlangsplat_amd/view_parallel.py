@@ -1,0 +1,142 @@
+"""Per-view data parallelism for the rasterizer step.
+
+The reference renders the views of one training batch sequentially on one GPU and lets
+autograd sum their gradients (train.py:242-268, loss.backward() at :339).  Three per-view
+statistics are reduced alongside the gradients:
+  * radii      -> MAX over views           (train.py:270)
+  * visibility -> ANY over views = radii>0  (train.py:271)
+  * viewspace (means2D) gradient -> SUM over views (train.py:350-352), later consumed by
+    add_densification_stats (scene/gaussian_model.py:744-746).
+
+Here the Gaussians are replicated on every rank, the view batch is split into contiguous
+per-rank slices (view_slice), each rank accumulates its views' gradients into ONE flat fp32
+bucket (GradBucket; the rasterizer backward accumulates in place, no per-view copies), and a
+step ends with one SUM all-reduce of that bucket plus, when densification statistics are
+requested, one MAX all-reduce of the int32 radii.  On MI355X the process group is "nccl"
+(= RCCL over xGMI); the CPU tests drive the same code over "gloo".  There is no other
+data-path collective: views are independent (SURVEY.md 8(e) "Shards naturally? Yes").
+
+The per-view work is a callback so that the same step runs the native HIP rasterizer
+(native_view_renderer, the product path) or, in tests only, the CPU oracle.
+"""
+from typing import Callable, Dict, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+# gradient fields of the flat bucket, in order; None = width depends on M (SH) or C (language)
+GRAD_FIELDS = (("means3D", 3), ("scales", 3), ("rotations", 4), ("opacities", 1), ("sh", None),
+               ("language_feature", None))
+
+
+def view_slice(n_views: int, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous, balanced [start, stop) of the batch's views owned by `rank` (the first
+    n_views % world ranks take one extra view)."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} for world size {world}")
+    base, extra = divmod(n_views, world)
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+class GradBucket:
+    """One flat fp32 buffer holding every per-Gaussian gradient of a step, field-major
+    ([P,3] means3D | [P,3] scales | [P,4] rotations | [P,1] opacities | [P,M,3] SH | [P,C]
+    language | optional [P,3] means2D), so one collective moves all of it.  `views` maps the
+    rasterizer's gradient names onto slices of `flat` (pass it as backward_native(out=...))."""
+
+    def __init__(self, P: int, M: int, C: int, device, densify_stats: bool = False):
+        self.P, self.M, self.C = P, M, C
+        self.densify_stats = densify_stats
+        fields = [(n, w if w is not None else (3 * M if n == "sh" else C)) for n, w in GRAD_FIELDS]
+        if densify_stats:
+            fields.append(("means2D", 3))
+        self.floats_per_gaussian = sum(w for _, w in fields)
+        self.flat = torch.zeros(P * self.floats_per_gaussian, dtype=torch.float32, device=device)
+        self.views: Dict[str, Optional[torch.Tensor]] = {}
+        o = 0
+        for name, w in fields:
+            seg = self.flat[o * P:(o + w) * P]
+            if w == 0:
+                self.views[name] = None
+            elif name == "sh":
+                self.views[name] = seg.view(P, M, 3)
+            else:
+                self.views[name] = seg.view(P, w)
+            o += w
+        self.radii = torch.zeros(P, dtype=torch.int32, device=device) if densify_stats else None
+
+    def zero_(self):
+        self.flat.zero_()
+        if self.radii is not None:
+            self.radii.zero_()
+
+    def need(self) -> Dict[str, bool]:
+        """The `need` mask for backward_native: only the bucket's fields are produced."""
+        return dict(means3D=True, scales=True, rotations=True, opacities=True, sh=self.M > 0,
+                    language_feature=self.C > 0, means2D=self.densify_stats, colors=False, cov3D=False)
+
+    @property
+    def nbytes(self) -> int:
+        return self.flat.numel() * 4
+
+
+class ViewParallelStep:
+    """One data-parallel step over a batch of `n_views` views.
+
+    run(render_view) calls render_view(v, bucket) for every view v this rank owns; the callback
+    adds view v's gradients into bucket.views (and returns view v's int32 radii [P], or None).
+    Afterwards the bucket holds the SUM over ALL views of the batch on every rank, and
+    bucket.radii the MAX over all views (when densify_stats)."""
+
+    def __init__(self, bucket: GradBucket, n_views: int, group=None):
+        self.bucket = bucket
+        self.n_views = n_views
+        self.group = group
+        self.distributed = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if self.distributed else 1
+        self.rank = dist.get_rank(group) if self.distributed else 0
+        self.views = range(*view_slice(n_views, self.world, self.rank))
+
+    def run(self, render_view: Callable[[int, GradBucket], Optional[torch.Tensor]]) -> GradBucket:
+        b = self.bucket
+        b.zero_()
+        for v in self.views:
+            radii = render_view(v, b)
+            if b.radii is not None and radii is not None:
+                torch.maximum(b.radii, radii.to(torch.int32), out=b.radii)
+        if self.world > 1:
+            dist.all_reduce(b.flat, op=dist.ReduceOp.SUM, group=self.group)
+            if b.radii is not None:
+                dist.all_reduce(b.radii, op=dist.ReduceOp.MAX, group=self.group)
+        return b
+
+    def visibility(self) -> torch.Tensor:
+        """ANY over the batch's views (train.py:271): a Gaussian is visible if some view gave it
+        a positive radius."""
+        if self.bucket.radii is None:
+            raise RuntimeError("visibility needs GradBucket(densify_stats=True)")
+        return self.bucket.radii > 0
+
+
+def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool = False):
+    """render_view callback for ViewParallelStep on the HIP rasterizer (the product path).
+
+    scene    : object with means3D, opacities, shs, lang, scales, rotations device tensors
+    settings : list of GaussianRasterizationSettings, indexed by view
+    grad_fn  : grad_fn(v, color, lang, depth) -> (dL_dcolor, dL_dlang, dL_ddepth) for view v
+    Forward + backward of view v with the gradients accumulated straight into the bucket."""
+    import diff_gaussian_rasterization as dgr
+
+    def render_view(v: int, bucket: GradBucket):
+        color, lang, radii, depth, st = dgr.forward_native(
+            settings[v], scene.means3D, scene.opacities, shs=scene.shs, language_feature=scene.lang,
+            scales=scene.scales, rotations=scene.rotations)
+        gc, gl, gd = grad_fn(v, color, lang, depth)
+        dgr.backward_native(st, gc, gl, gd, out=bucket.views, accumulate=True, need=bucket.need(),
+                            deterministic=deterministic)
+        render_view.last_num_rendered = st.num_rendered
+        return radii
+
+    render_view.last_num_rendered = 0
+    return render_view

@@ -31,17 +31,17 @@ import torch.distributed as dist  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-def phase_bytes(phase, P, Pvis, K, npix, ntiles, C, M=16):
-    """Algorithmic HBM bytes of one launch of each phase (each byte counted once)."""
+def phase_bytes(phase, P, Pvis, K, npix, ntiles, C, M=16, accumulate=True):
+    """Algorithmic HBM bytes of one launch of each phase (each byte counted once; DESIGN.md 4)."""
     rec = 4 + 8 + 16 + 16 + 4 * C          # id + xy + conic/opacity + rgb/depth + language row
-    if phase == "preprocess":
-        return P * (12 + 12 + 16 + 4 + 4 * 3 * M) + P * (4 + 4 + 4) + Pvis * (8 + 16 + 16 + 1)
+    if phase == "preprocess":              # inputs; radii, radius, tiles, key, rect; screen records
+        return P * (12 + 12 + 16 + 4 + 4 * 3 * M) + P * (4 + 4 + 4 + 4 + 8) + Pvis * (8 + 16 + 16 + 1)
     if phase == "depth_sort":
         return 4 * P * (4 + 16) + 4 * P     # 4 passes: count reads keys, scatter reads + writes pairs
-    if phase == "instance_scan":
-        return P * (4 + 4 + 4 + 4)
-    if phase == "emit":
-        return Pvis * (4 + 4 + 4 + 8 + 4 + 4) + K * 8
+    if phase == "instance_scan":           # order + rect gather -> counts + depth-ordered rect; scan
+        return P * (4 + 8 + 4 + 8) + P * (4 + 4)
+    if phase == "emit":                    # order, offsets, counts, rect (depth order) -> keys, values
+        return P * (4 + 4 + 4 + 8) + K * 8
     if phase == "tile_sort":
         return 2 * K * (4 + 16)
     if phase == "tile_ranges":
@@ -50,8 +50,9 @@ def phase_bytes(phase, P, Pvis, K, npix, ntiles, C, M=16):
         return K * rec + ntiles * 12 + npix * (4 * (3 + C + 1) + 8)
     if phase == "render_bwd":
         return K * rec + ntiles * 12 + npix * (4 * (3 + C + 1) + 8) + Pvis * (8 + 16 + 12 + 4 + 4 * C)
-    if phase == "preprocess_bwd":
-        return Pvis * (12 + 12 + 16 + 4 * 3 * M + 1 + 4 + 8 + 16 + 12) + P * 4 * (3 + 3 + 4 + 3 * M)
+    if phase == "preprocess_bwd":          # visible rows: inputs + screen grads; gradient rows (RMW if accumulating)
+        grads = 4 * (3 + 3 + 4 + 1 + 3 * M)
+        return P * 4 + Pvis * (12 + 12 + 16 + 4 * 3 * M + 1 + 48) + (2 * Pvis * grads if accumulate else P * grads)
     return 0
 
 
@@ -109,36 +110,29 @@ def main():
     tanfovx = 0.6
     scene_cpu = synthetic.make_scene(P, C=C, tanfovx=tanfovx, tanfovy=tanfovx * H / W)
     scene = scene_cpu.to(dev)
-    cams = synthetic.camera_batch(world * V, W, H, tanfovx=tanfovx, seed=1)[rank * V:(rank + 1) * V]
+    from view_parallel import GradBucket, ViewParallelStep, native_view_renderer
+    M = scene.shs.shape[1]
+    bucket = GradBucket(P, M, C, dev)                      # flat grads, 59 + C floats per Gaussian
+    dp = ViewParallelStep(bucket, world * V)               # this rank's slice of the world*V batch
+    all_cams = synthetic.camera_batch(world * V, W, H, tanfovx=tanfovx, seed=1)
     bg = torch.ones(3, device=dev)
-    settings = [dgr.GaussianRasterizationSettings(H, W, c.tanfovx, c.tanfovy, bg, 1.0, c.world_view_transform.to(dev),
-                                                  c.full_proj_transform.to(dev), 3, c.camera_center.to(dev), False,
-                                                  False, True) for c in cams]
+    settings = {v: dgr.GaussianRasterizationSettings(H, W, c.tanfovx, c.tanfovy, bg, 1.0,
+                                                     c.world_view_transform.to(dev), c.full_proj_transform.to(dev),
+                                                     3, c.camera_center.to(dev), False, False, True)
+                for v, c in enumerate(all_cams) if v in dp.views}
     g = torch.Generator(device="cpu").manual_seed(123)
     gcol = (torch.randn(3, H, W, generator=g) * 1e-3).to(dev)
     glang = (torch.randn(C, H, W, generator=g) * 1e-3).to(dev)
-    M = scene.shs.shape[1]
-    nfl = 3 + 3 + 4 + 1 + 3 * M + C
-    flat = torch.zeros(P * nfl, device=dev)
-    views, o = {}, 0
-    for name, w in (("means3D", 3), ("scales", 3), ("rotations", 4), ("opacities", 1), ("sh", 3 * M),
-                    ("language_feature", C)):
-        views[name] = flat[o * P:(o + w) * P].view(P, w) if name != "sh" else flat[o * P:(o + w) * P].view(P, M, 3)
-        o += w
-    need = dict(means2D=False, colors=False, cov3D=False)
-    stream = torch.cuda.current_stream(dev)
+    render = native_view_renderer(scene, settings, lambda v, color, lang, depth: (gcol, glang, None))
     Ks = []
 
+    def render_view(v, b):
+        r = render(v, b)
+        Ks.append(render.last_num_rendered)
+        return r
+
     def step():
-        flat.zero_()
-        for rs in settings:
-            _, _, _, _, st = dgr.forward_native(rs, scene.means3D, scene.opacities, shs=scene.shs,
-                                                language_feature=scene.lang, scales=scene.scales,
-                                                rotations=scene.rotations)
-            Ks.append(st.num_rendered)
-            dgr.backward_native(st, gcol, glang, None, out=views, accumulate=True, need=need)
-        if world > 1:
-            dist.all_reduce(flat)
+        dp.run(render_view)                                # fwd+bwd per view, SUM all-reduce (RCCL) if world > 1
 
     for _ in range(args.warmup):
         step()
@@ -164,12 +158,11 @@ def main():
     elapsed = float(el.item())
     frames = world * V * args.steps
     value = frames / elapsed
-    del stream
 
     if rank == 0:
         Kmean = float(np.mean(Ks)) if Ks else 0.0
         with torch.no_grad():
-            _, _, radii, _, _ = dgr.forward_native(settings[0], scene.means3D, scene.opacities, shs=scene.shs,
+            _, _, radii, _, _ = dgr.forward_native(settings[dp.views[0]], scene.means3D, scene.opacities, shs=scene.shs,
                                                    language_feature=scene.lang, scales=scene.scales,
                                                    rotations=scene.rotations)
             Pvis = int((radii > 0).sum())
@@ -210,7 +203,7 @@ def main():
             config=dict(workload="S2M synthetic (BASELINE configs[2] per GPU; configs[3] batch split)",
                         gaussians=P, width=W, height=H, channels=C, views_per_gpu_per_step=V,
                         global_batch=world * V, parallelism=f"dp{world}", num_rendered_mean=int(Kmean),
-                        visible=Pvis),
+                        visible=Pvis, grad_bucket_mb=round(bucket.nbytes / 2**20, 1)),
             roofline=roof, cpu_baseline=cpu,
             phases={k: dict(mean_ms=round(v["mean_ms"], 4), gbs=round(v["gbs"], 1)) for k, v in phases.items()},
         )

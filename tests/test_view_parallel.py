@@ -1,0 +1,141 @@
+"""Per-view data parallelism on CPU: view partitioning, the flat gradient
+bucket, and a world_size-2 gloo step whose SUM / MAX reductions must equal one process
+rendering the whole batch (the reference's sequential multi-view loop, train.py:242-271,350-352).
+The per-view renderer here is the CPU oracle (test infrastructure); on the GPU the same
+ViewParallelStep runs native_view_renderer (bench.py)."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle
+import synthetic
+from helpers import oracle_settings
+from view_parallel import GradBucket, ViewParallelStep, view_slice
+
+N_VIEWS, P, W, H, C = 5, 1500, 64, 48, 4
+
+
+@pytest.mark.parametrize("n,world", [(64, 8), (5, 2), (3, 4), (0, 3), (7, 1), (9, 4)])
+def test_view_slice_partitions_batch(n, world):
+    seen = []
+    sizes = []
+    for r in range(world):
+        a, b = view_slice(n, world, r)
+        seen.extend(range(a, b))
+        sizes.append(b - a)
+    assert seen == list(range(n))
+    assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        view_slice(n, world, world)
+
+
+@pytest.mark.parametrize("densify", [False, True])
+def test_bucket_layout(densify):
+    b = GradBucket(10, 16, 32, "cpu", densify_stats=densify)
+    assert b.floats_per_gaussian == 3 + 3 + 4 + 1 + 48 + 32 + (3 if densify else 0)
+    assert b.views["sh"].shape == (10, 16, 3) and b.views["language_feature"].shape == (10, 32)
+    # every view aliases the flat buffer, fields do not overlap and cover it exactly
+    ptrs = sorted((v.data_ptr(), v.numel()) for v in b.views.values() if v is not None)
+    o = b.flat.data_ptr()
+    for p, n in ptrs:
+        assert p == o
+        o += 4 * n
+    assert o == b.flat.data_ptr() + b.nbytes
+    assert b.need()["means2D"] == densify and not b.need()["colors"]
+    b.views["opacities"].fill_(1)
+    b.zero_()
+    assert float(b.flat.abs().sum()) == 0
+
+
+def _scene_and_cams():
+    sc = synthetic.make_scene(P, C=C, tanfovx=0.6, tanfovy=0.6 * H / W, seed=3, logscale_mean=-4.0)
+    cams = synthetic.camera_batch(N_VIEWS, W, H, tanfovx=0.6, seed=1)
+    return sc, cams
+
+
+def _view_grads(v):
+    g = np.random.default_rng(100 + v)
+    return g.normal(size=(3, H, W)).astype(np.float32), g.normal(size=(C, H, W)).astype(np.float32)
+
+
+def oracle_renderer(sc, cams):
+    names = dict(means3D="means3D", scales="scales", rotations="rotations", opacity="opacities", sh="sh",
+                 lang="language_feature", means2D="means2D")
+
+    def render_view(v, bucket):
+        r = oracle.forward(oracle_settings(cams[v]), sc.means3D.numpy(), sc.opacities.numpy(), shs=sc.shs.numpy(),
+                           lang=sc.lang.numpy(), scales=sc.scales.numpy(), rotations=sc.rotations.numpy())
+        gc, gl = _view_grads(v)
+        g = r.backward(gc, gl, None, nthreads=1)
+        for k, name in names.items():
+            if bucket.views.get(name) is not None:
+                bucket.views[name] += torch.from_numpy(g[k])
+        radii = torch.from_numpy(r.radii.copy())
+        r.close()
+        return radii
+
+    return render_view
+
+
+def _serial_reference(densify):
+    sc, cams = _scene_and_cams()
+    b = GradBucket(P, sc.shs.shape[1], C, "cpu", densify_stats=densify)
+    step = ViewParallelStep(b, N_VIEWS)
+    assert list(step.views) == list(range(N_VIEWS))
+    step.run(oracle_renderer(sc, cams))
+    return b
+
+
+def _worker(rank, world, port, outdir, densify):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sc, cams = _scene_and_cams()
+        b = GradBucket(P, sc.shs.shape[1], C, "cpu", densify_stats=densify)
+        step = ViewParallelStep(b, N_VIEWS)
+        assert step.world == world and step.rank == rank
+        calls = []
+        render = oracle_renderer(sc, cams)
+
+        def counted(v, bucket):
+            calls.append(v)
+            return render(v, bucket)
+
+        step.run(counted)
+        assert calls == list(range(*view_slice(N_VIEWS, world, rank)))
+        torch.save(dict(flat=b.flat.clone(), radii=None if b.radii is None else b.radii.clone(),
+                        vis=step.visibility() if densify else None, calls=calls),
+                   os.path.join(outdir, f"rank{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("densify", [False, True])
+def test_two_rank_step_equals_serial_batch(densify):
+    ref = _serial_reference(densify)
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(2, _free_port(), d, densify), nprocs=2, join=True)
+        outs = [torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(2)]
+    assert sorted(outs[0]["calls"] + outs[1]["calls"]) == list(range(N_VIEWS))
+    # both ranks hold the same reduced bucket, equal to the serial sum up to fp32 reassociation
+    assert torch.equal(outs[0]["flat"], outs[1]["flat"])
+    scale = float(ref.flat.abs().max())
+    assert scale > 0
+    err = float((outs[0]["flat"] - ref.flat).abs().max())
+    assert err <= 1e-5 * scale, err
+    if densify:
+        assert torch.equal(outs[0]["radii"], ref.radii) and torch.equal(outs[1]["radii"], ref.radii)
+        assert torch.equal(outs[0]["vis"], ref.radii > 0)
+        assert int(ref.radii.gt(0).sum()) > 0

@@ -12,4 +12,4 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INS
     rc=$?; echo "pass $i ($grp) rc=$rc"
     if [ $rc -ne 0 ]; then tail -5 gpurun_out/pmc/p$i.log; exit $rc; fi
 done
-python3 tools/pmc_summary.py gpurun_out/pmc > gpurun_out/pmc/summary.txt 2>&1; cat gpurun_out/pmc/summary.txt
+python3 tools/pmc_summary.py gpurun_out/pmc --json gpurun_out/pmc/pmc_traffic.json > gpurun_out/pmc/summary.txt 2>&1; cat gpurun_out/pmc/summary.txt

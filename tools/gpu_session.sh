@@ -12,4 +12,4 @@ step() {  # step <name> <timeout> <cmd...>
 }
 step pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ${PYTEST_ARGS:-}
 [ "${SKIP_BENCH:-0}" = 1 ] && exit 0
-step bench 600 python bench.py --steps ${STEPS:-3} --warmup 1 ${BENCH_ARGS:---no-cpu-baseline}
+step bench 600 python bench.py --steps ${STEPS:-3} --warmup 1 ${BENCH_ARGS---no-cpu-baseline}
