@@ -227,7 +227,11 @@ void launch_render_bwd(const RenderBwdArgs& a, hipStream_t st) {
         case 16: go_bwd<16, 64, 32>(a, st); break;
         case 32:
             if (a.deterministic) go_bwd<32, 64, 64>(a, st);
-            else launch_render_bwd_mfma(a, st);   // language channels on matrix cores
+#ifdef LSR_BWD_BLOCK_MFMA
+            else launch_render_bwd_mfma(a, st);
+#else
+            else launch_render_bwd_wave(a, st);   // compacted per-quadrant waves, language on matrix cores
+#endif
             break;
         default: go_bwd<64, 32, 128>(a, st); break;
     }

@@ -166,7 +166,11 @@ __global__ void __launch_bounds__(256, 3) k_render_bwd_mfma(RenderBwdArgs a) {
         __syncthreads();
         for (int e = tid; e < BSB * 32; e += 256) {
             const int j = e >> 5, c = e & 31;
+#ifdef LSR_ABL_NOLANG
+            const float x = (j < nb && c < C) ? (float)(s_id[j] & 7) : 0.0f;
+#else
             const float x = (j < nb && c < C) ? a.lang[(size_t)s_id[j] * C + c] : 0.0f;
+#endif
             __bf16 h, l;
             split2(x, h, l);
             s_Fh[j][c] = h;
@@ -177,6 +181,7 @@ __global__ void __launch_bounds__(256, 3) k_render_bwd_mfma(RenderBwdArgs a) {
             const int j0 = grp * BG;
             // ---- MFMA1: S[e][px] for the group's 32 entries and the wave's 64 pixels ----------
             f32x16 d0 = f32x16{}, d1 = f32x16{};
+#ifndef LSR_ABL_NOMFMA
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
                 const bf16x8 ah = *reinterpret_cast<const bf16x8*>(&s_Fh[j0 + lr][16 * ks + 8 * lh]);
@@ -184,6 +189,7 @@ __global__ void __launch_bounds__(256, 3) k_render_bwd_mfma(RenderBwdArgs a) {
                 d0 = MFMA(ah, b1h[ks][0], d0); d0 = MFMA(ah, b1l[ks][0], d0); d0 = MFMA(al, b1h[ks][0], d0);
                 d1 = MFMA(ah, b1h[ks][1], d1); d1 = MFMA(ah, b1l[ks][1], d1); d1 = MFMA(al, b1h[ks][1], d1);
             }
+#endif
             // fold: afterwards S of entry (r&3) + 8(r>>2) is d0[r], of entry +4 is d1[r], own pixel
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
@@ -245,9 +251,16 @@ __global__ void __launch_bounds__(256, 3) k_render_bwd_mfma(RenderBwdArgs a) {
                     v[4] = gm2x; v[5] = gm2y; v[6] = gcx; v[7] = gcy; v[8] = gcw; v[9] = gop;
 #pragma unroll
                     for (int q = 10; q < 16; ++q) v[q] = 0.0f;
+#ifdef LSR_ABL_NORED
+                    float sv = 0.0f;
+#pragma unroll
+                    for (int q = 0; q < 10; ++q) sv += v[q];
+                    if (sv == 1234.5f) atomicAdd(&s_rec[j][0], sv);
+#else
                     wave_transpose_reduce<16>(v);
                     const int q = transpose_reduce_slot<16>(lane);
                     if ((lane & 3) == 0 && q < 10) atomicAdd(&s_rec[j][q], v[0]);
+#endif
                     if (lane == 0) s_act[j] = 1u;
                 }
             }
@@ -275,6 +288,7 @@ __global__ void __launch_bounds__(256, 3) k_render_bwd_mfma(RenderBwdArgs a) {
                 const int ecol = 16 * (grpl & 1);
                 const int qrow = li >> 2, pcol = 4 * (li & 3);
                 f32x16 acc2 = f32x16{};
+#ifndef LSR_ABL_NOMFMA
 #pragma unroll
                 for (int ks = 0; ks < 4; ++ks) {
                     const int r0 = 16 * ks + 8 * lh + qrow;
@@ -288,6 +302,7 @@ __global__ void __launch_bounds__(256, 3) k_render_bwd_mfma(RenderBwdArgs a) {
                     acc2 = MFMA(ah, b2l[ks], acc2);
                     acc2 = MFMA(al, b2h[ks], acc2);
                 }
+#endif
                 // acc2[r]: entry (r&3) + 8(r>>2) + 4 lh, channel lr
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {

@@ -98,10 +98,11 @@ def load():
     """Load liblsr.so (raises if it has not been built)."""
     global _LIB
     if _LIB is None:
-        if not os.path.exists(LIB_PATH):
+        path = os.environ.get("LSR_LIBRARY", LIB_PATH)   # variant builds for profiling experiments
+        if not os.path.exists(path):
             raise ImportError(f"liblsr.so not found at {LIB_PATH}; build it with `make -C 4dlangsplat_amd/csrc` "
                               "(or __graft_entry__.build()).  There is no CPU fallback.")
-        lib = ctypes.CDLL(LIB_PATH)
+        lib = ctypes.CDLL(path)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(lib, name)
             fn.restype = res

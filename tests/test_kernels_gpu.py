@@ -24,3 +24,14 @@ def test_mfma_bf16_layout(tmp_path):
     r = subprocess.run(["timeout", "-k", "5", "60", exe], capture_output=True, text=True)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_mfma16_helpers(tmp_path):
+    """16x16x32 bf16 MFMA lane maps, the lane-group transpose and ds_read_tr16 (lsr_mfma.h)."""
+    src = os.path.join(ROOT, "tests", "kernels", "t_mfma16.hip")
+    exe = str(tmp_path / "t_mfma16")
+    subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-o", exe, src], check=True)
+    r = subprocess.run(["timeout", "-k", "5", "60", exe], capture_output=True, text=True)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
