@@ -313,6 +313,7 @@ int lsr_forward_render(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_out*
     Binning b = carve_binning(binning, K > 0 ? K : 1, nullptr);
     Img m = carve_img(img, W, H, nullptr);
     LSR_HIP(hipMemsetAsync(m.ranges, 0, sizeof(uint2) * (size_t)gx * gy, st));
+    LSR_HIP(hipMemsetAsync(m.tile_max, 0, sizeof(uint32_t) * (size_t)gx * gy, st));
     const uint32_t* point_list = nullptr;
     if (K > 0) {
         {

@@ -142,6 +142,7 @@ void launch_tile_ranges(size_t K, const uint32_t* keys, uint2* ranges, hipStream
 void launch_render_fwd(const RenderFwdArgs& a, hipStream_t st);
 void launch_render_bwd(const RenderBwdArgs& a, hipStream_t st);
 void launch_render_bwd_mfma(const RenderBwdArgs& a, hipStream_t st);
+void launch_render_fwd_wave(const RenderFwdArgs& a, hipStream_t st);
 void launch_render_bwd_wave(const RenderBwdArgs& a, hipStream_t st);
 
 }  // namespace lsr

@@ -27,36 +27,6 @@ constexpr int WFP = 40;      // F / G row pitch in bf16 (32 channels + 8): 80-by
 constexpr int WWP = 20;      // W row pitch in bf16 (16 entries + 4): 40-byte rows, 8-byte aligned
 constexpr int WFIFO = 128;   // compacted entries waiting (list positions and ids); power of two
 
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): this wave's LDS writes have landed
-    __builtin_amdgcn_wave_barrier();
-}
-
-// May the splat (xy, conic+opacity) pass the per-pixel prefilter power >= skip_power(o) at some
-// pixel centre of the box [x0, x1] x [y0, y1]?  min over the box of q(d) = a dx^2 + 2b dx dy +
-// c dy^2 (power = -q/2), d = xy - p, taken on the box edges when 0 is outside.  The box
-// endpoints are computed like the per-pixel dx, dy, so every pixel's (dx, dy) lies inside it; the
-// margin covers the float evaluation of q at the pixels (terms up to M).  False only when the
-// compositor would skip the splat at every pixel of the box.
-__device__ __forceinline__ bool quad_may_touch(float2 xy, float4 co, float x0, float x1, float y0, float y1) {
-    const float thr = skip_power(co.w);
-    const float dxl = xy.x - x1, dxh = xy.x - x0, dyl = xy.y - y1, dyh = xy.y - y0;
-    const float a = co.x, b = co.y, c = co.z;
-    float mq = 0.0f;
-    if (!(dxl <= 0.0f && dxh >= 0.0f && dyl <= 0.0f && dyh >= 0.0f)) {
-        const float tyl = fminf(fmaxf(-b * dxl / c, dyl), dyh), tyh = fminf(fmaxf(-b * dxh / c, dyl), dyh);
-        const float txl = fminf(fmaxf(-b * dyl / a, dxl), dxh), txh = fminf(fmaxf(-b * dyh / a, dxl), dxh);
-        const float q1 = a * dxl * dxl + 2.0f * b * dxl * tyl + c * tyl * tyl;
-        const float q2 = a * dxh * dxh + 2.0f * b * dxh * tyh + c * tyh * tyh;
-        const float q3 = a * txl * txl + 2.0f * b * txl * dyl + c * dyl * dyl;
-        const float q4 = a * txh * txh + 2.0f * b * txh * dyh + c * dyh * dyh;
-        mq = fminf(fminf(q1, q2), fminf(q3, q4));
-    }
-    const float mx = fmaxf(-dxl, dxh), my = fmaxf(-dyl, dyh);
-    const float M = a * mx * mx + c * my * my + 2.0f * fabsf(b) * mx * my;
-    return mq <= -2.0f * thr + 1e-5f * M + 1e-4f;
-}
-
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3)))
 k_render_bwd_wave(RenderBwdArgs a) {
     __shared__ __attribute__((aligned(16))) __bf16 s_GW[64 * WFP];      // G rows once, then W hi | lo

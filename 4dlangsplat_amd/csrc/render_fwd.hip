@@ -317,6 +317,10 @@ static void go_fwd(const RenderFwdArgs& a, hipStream_t st) {
 }
 
 void launch_render_fwd(const RenderFwdArgs& a, hipStream_t st) {
+#ifndef LSR_FWD_BLOCK
+    launch_render_fwd_wave(a, st);   // compacted per-quadrant waves (render_fwd_wave.hip)
+    return;
+#endif
     const int C = a.include_feature ? a.C : 0;
     if (C == 0) go_fwd<0, 256>(a, st);
     else if (C <= 4) go_fwd<4, 256>(a, st);

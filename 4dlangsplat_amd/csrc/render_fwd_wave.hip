@@ -1,0 +1,181 @@
+// render_fwd_wave.hip -- front-to-back compositing, one independent wave per 8x8 pixel quadrant.
+//
+// Same mathematics and per-pixel operation order as k_render_fwd (render_fwd.hip; upstream
+// renderCUDA).  About two thirds of a tile's list entries touch no pixel of
+// a given quadrant; an entry that no pixel of the quadrant blends leaves every pixel's T and
+// sums unchanged, and the contributor count upstream writes to n_contrib is the list position of
+// the last blended entry + 1, so skipping such entries is exact.  Each wave
+//   1. scans the tile list front to back, 64 entries per round, one per lane: a conservative
+//      ellipse-vs-quadrant test (quad_may_touch, lsr_common.h) and a ballot compaction into a
+//      per-wave FIFO in LDS (list order kept);
+//   2. composites the surviving entries in groups of GF staged in LDS (geometry + language row),
+//      and stops as soon as every pixel of the quadrant has saturated.
+// 64-thread blocks, no block barriers; the four quadrants of a tile run on one XCD.
+#include "lsr_common.h"
+#include "lsr_internal.h"
+
+namespace lsr {
+
+template <int CPAD>
+__global__ void __launch_bounds__(64) k_render_fwd_wave(RenderFwdArgs a) {
+    constexpr int GF = 32, FIFO = 128, LP = CPAD > 0 ? CPAD : 1;
+    __shared__ float4 s_co[GF];
+    __shared__ float4 s_rgbd[GF];
+    __shared__ float2 s_xy[GF];
+    __shared__ float s_thr[GF];
+    __shared__ uint32_t s_k[GF];
+    __shared__ __attribute__((aligned(16))) float s_lang[GF * LP];
+    __shared__ uint32_t s_fk[FIFO];
+    __shared__ uint32_t s_fg[FIFO];
+
+    const int b = blockIdx.x;
+    const int tile = (b >> 5) * 8 + (b & 7), quad = (b >> 3) & 3;
+    if (tile >= a.grid_x * a.grid_y) return;
+    const int lane = threadIdx.x;
+    const int tx = tile % a.grid_x, ty = tile / a.grid_x;
+    const int qx0 = tx * LSR_TILE_X + (quad & 1) * 8, qy0 = ty * LSR_TILE_Y + (quad >> 1) * 8;
+    const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
+    const bool inside = px < a.W && py < a.H;
+    const float pxf = (float)px, pyf = (float)py;
+    const uint2 range = a.ranges[tile];
+    const int C = a.C;
+    const float bx0 = (float)qx0, bx1 = (float)min(qx0 + 7, a.W - 1);
+    const float by0 = (float)qy0, by1 = (float)min(qy0 + 7, a.H - 1);
+
+    float T = 1.0f;
+    uint32_t last = 0;
+    float acc[3] = {0.0f, 0.0f, 0.0f};
+    float accL[LP];
+#pragma unroll
+    for (int c = 0; c < LP; ++c) accL[c] = 0.0f;
+    float accD = 0.0f;
+    bool done = !inside;
+
+    uint32_t pos = range.x;  // list entries [pos, range.y) not yet scanned
+    int head = 0, tail = 0;  // FIFO counters (wave-uniform)
+    while (!__all(done)) {
+        // ---- 1. scan + compaction -----------------------------------------------------------
+        while (tail - head < GF && pos < range.y) {
+            const uint32_t idx = pos + lane;
+            bool cand = false;
+            uint32_t gid = 0;
+            if (idx < range.y) {
+                gid = a.point_list[idx];
+                cand = quad_may_touch(a.xy[gid], a.conic_o[gid], bx0, bx1, by0, by1);
+            }
+            const uint64_t m = __ballot(cand);
+            if (cand) {
+                const int s = (tail + __popcll(m & lanemask_lt())) & (FIFO - 1);
+                s_fk[s] = idx - range.x;
+                s_fg[s] = gid;
+            }
+            tail += __popcll(m);
+            pos += 64;
+        }
+        const int cnt = min(GF, tail - head);
+        if (cnt == 0) break;
+        wave_lds_sync();
+        // ---- 2. stage the group ---------------------------------------------------------------
+        if (lane < GF) {
+            const bool ok = lane < cnt;
+            const int s = (head + lane) & (FIFO - 1);
+            const uint32_t gid = ok ? s_fg[s] : 0u;
+            const float4 co = ok ? a.conic_o[gid] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            s_k[lane] = ok ? s_fk[s] : 0u;
+            s_xy[lane] = ok ? a.xy[gid] : make_float2(0.0f, 0.0f);
+            s_co[lane] = co;
+            s_rgbd[lane] = ok ? a.rgbd[gid] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            s_thr[lane] = ok ? skip_power(co.w) : __builtin_inff();
+        }
+        if constexpr (CPAD > 0) {
+            if (C == CPAD) {   // whole rows as float4
+                constexpr int R4 = CPAD / 4;
+                for (int q = lane; q < cnt * R4; q += 64) {
+                    const int e = q / R4, c4 = q - e * R4;
+                    const uint32_t gid = s_fg[(head + e) & (FIFO - 1)];
+                    reinterpret_cast<float4*>(s_lang)[q] = reinterpret_cast<const float4*>(a.lang + (size_t)gid * CPAD)[c4];
+                }
+            } else {
+                for (int q = lane; q < cnt * CPAD; q += 64) {
+                    const int e = q / CPAD, c = q - e * CPAD;
+                    const uint32_t gid = s_fg[(head + e) & (FIFO - 1)];
+                    s_lang[q] = c < C ? a.lang[(size_t)gid * C + c] : 0.0f;
+                }
+            }
+        }
+        head += cnt;
+        wave_lds_sync();
+        // ---- 3. composite the group in list order --------------------------------------------
+        for (int e = 0; e < cnt; ++e) {
+            if (done) continue;
+            const float2 xy = s_xy[e];
+            const float4 co = s_co[e];
+            const float dx = xy.x - pxf, dy = xy.y - pyf;
+            const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+            if (power > 0.0f || power < s_thr[e]) continue;   // the second test never changes a decision
+            const float alpha = fminf(0.99f, co.w * expf_repro(power));
+            if (alpha < 1.0f / 255.0f) continue;
+            const float test_T = T * (1.0f - alpha);
+            if (test_T < 0.0001f) { done = true; continue; }
+            const float w = alpha * T;
+            const float4 cd = s_rgbd[e];
+            acc[0] = __builtin_fmaf(cd.x, w, acc[0]);
+            acc[1] = __builtin_fmaf(cd.y, w, acc[1]);
+            acc[2] = __builtin_fmaf(cd.z, w, acc[2]);
+            accD = __builtin_fmaf(cd.w, w, accD);
+            if constexpr (CPAD > 0) {
+                const float4* f4 = reinterpret_cast<const float4*>(s_lang + e * CPAD);
+#pragma unroll
+                for (int c4 = 0; c4 < CPAD / 4; ++c4) {
+                    const float4 f = f4[c4];
+                    accL[4 * c4 + 0] = __builtin_fmaf(f.x, w, accL[4 * c4 + 0]);
+                    accL[4 * c4 + 1] = __builtin_fmaf(f.y, w, accL[4 * c4 + 1]);
+                    accL[4 * c4 + 2] = __builtin_fmaf(f.z, w, accL[4 * c4 + 2]);
+                    accL[4 * c4 + 3] = __builtin_fmaf(f.w, w, accL[4 * c4 + 3]);
+                }
+            }
+            T = test_T;
+            last = s_k[e] + 1;
+        }
+        wave_lds_sync();
+    }
+    if (inside) {
+        const size_t HW = (size_t)a.H * a.W, pid = (size_t)py * a.W + px;
+        a.final_T[pid] = T;
+        a.n_contrib[pid] = last;
+        a.out_color[pid] = acc[0] + T * a.bg[0];
+        a.out_color[HW + pid] = acc[1] + T * a.bg[1];
+        a.out_color[2 * HW + pid] = acc[2] + T * a.bg[2];
+        a.out_depth[pid] = accD;
+        if constexpr (CPAD > 0) {
+#pragma unroll
+            for (int c = 0; c < CPAD; ++c)
+                if (c < C) a.out_lang[(size_t)c * HW + pid] = accL[c];
+        }
+    }
+    // per-tile bound for the backward replay (tile_max_contrib is zeroed before the launch)
+    uint32_t m = last;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+    if (lane == 0 && m > 0) atomicMax(a.tile_max_contrib + tile, m);
+}
+
+template <int CPAD>
+static void go_fwd_wave(const RenderFwdArgs& a, hipStream_t st) {
+    const int ntiles = a.grid_x * a.grid_y;
+    hipLaunchKernelGGL(k_render_fwd_wave<CPAD>, dim3(((ntiles + 7) / 8) * 32), dim3(64), 0, st, a);
+}
+
+void launch_render_fwd_wave(const RenderFwdArgs& a, hipStream_t st) {
+    const int C = a.include_feature ? a.C : 0;
+    switch (lang_pad(C)) {
+        case 0: go_fwd_wave<0>(a, st); break;
+        case 4: go_fwd_wave<4>(a, st); break;
+        case 8: go_fwd_wave<8>(a, st); break;
+        case 16: go_fwd_wave<16>(a, st); break;
+        case 32: go_fwd_wave<32>(a, st); break;
+        default: go_fwd_wave<64>(a, st); break;
+    }
+}
+
+}  // namespace lsr
