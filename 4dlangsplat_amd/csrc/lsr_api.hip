@@ -281,7 +281,8 @@ int lsr_forward_preprocess(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_
     {
         PhaseTimer t(LSR_PHASE_DEPTH_SORT, st);
         lsr::launch_iota(P, g.val_a, st);
-        in_b = lsr::radix_sort_pairs(g.key_a, g.val_a, g.key_b, g.val_b, (size_t)P, 0, 32, g.sort_tmp, st);
+        LSR_HIP(hipMemsetAsync(g.total, 0, 2 * sizeof(uint32_t), st));   // [0] K, [1] sort error word
+        in_b = lsr::radix_sort_pairs(g.key_a, g.val_a, g.key_b, g.val_b, (size_t)P, 0, 32, g.sort_tmp, g.total + 1, st);
     }
     if (in_b != (bool)depth_sort_result_in_b()) return fail(LSR_EHIP, "internal: depth sort parity");
     LSR_LAUNCHED("depth sort", st, s->debug);
@@ -291,9 +292,11 @@ int lsr_forward_preprocess(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_
         lsr::exclusive_scan_u32(g.counts, g.offsets, (size_t)P, g.total, g.scan_tmp, st);
     }
     LSR_LAUNCHED("instance scan", st, s->debug);
-    uint32_t K = 0;
-    LSR_HIP(hipMemcpyAsync(&K, g.total, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    uint32_t tot[2] = {0, 0};
+    LSR_HIP(hipMemcpyAsync(tot, g.total, sizeof(tot), hipMemcpyDeviceToHost, st));
     LSR_HIP(hipStreamSynchronize(st));
+    if (tot[1]) return fail(LSR_EHIP, "depth sort: look-back timed out");
+    const uint32_t K = tot[0];
     *num_rendered = (int64_t)K;
     return LSR_OK;
 }
@@ -324,7 +327,8 @@ int lsr_forward_render(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_out*
         bool in_b;
         {
             PhaseTimer t(LSR_PHASE_TILE_SORT, st);
-            in_b = lsr::radix_sort_pairs(b.key_a, b.val_a, b.key_b, b.val_b, K, 0, tile_bits(gx * gy), b.sort_tmp, st);
+            in_b = lsr::radix_sort_pairs(b.key_a, b.val_a, b.key_b, b.val_b, K, 0, tile_bits(gx * gy), b.sort_tmp,
+                                         nullptr, st);
         }
         const uint32_t* keys = in_b ? b.key_b : b.key_a;
         point_list = in_b ? b.val_b : b.val_a;

@@ -123,10 +123,10 @@ size_t scan_temp_bytes(size_t n);
 // exclusive scan of n u32 values; writes the total to *total (device) if non-null
 void exclusive_scan_u32(const uint32_t* in, uint32_t* out, size_t n, uint32_t* total, void* temp, hipStream_t st);
 size_t radix_temp_bytes(size_t n);
-// stable LSD sort of (key, val) pairs on key bits [begin_bit, end_bit).  Ping-pongs between the
-// (a) and (b) buffers; returns true when the sorted result ends in the (b) buffers.
+// stable LSD sort of (key, value) pairs on bits [begin_bit, end_bit); returns true when the result
+// is in (keys_b, vals_b).  err (device word, may be null) is set non-zero if a look-back timed out.
 bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b, size_t n,
-                      int begin_bit, int end_bit, void* temp, hipStream_t st);
+                      int begin_bit, int end_bit, void* temp, uint32_t* err, hipStream_t st);
 
 // binning (binning.hip)
 void launch_iota(int n, uint32_t* out, hipStream_t st);

@@ -14,8 +14,6 @@ namespace lsr {
 
 constexpr int SCAN_ITEMS = 8;
 constexpr int SCAN_TILE = 256 * SCAN_ITEMS;
-constexpr int RADIX_ITEMS = 16;
-constexpr int RADIX_TILE = 256 * RADIX_ITEMS;
 
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -103,7 +101,25 @@ void exclusive_scan_u32(const uint32_t* in, uint32_t* out, size_t n, uint32_t* t
                        (uint32_t*)nullptr);
 }
 
-// ---- radix sort -------------------------------------------------------------------------------
+// ---- radix sort ---------------------------------------------------------------------------------
+// One histogram kernel for all passes (a pass permutes keys, it does not change the digit counts),
+// then ONE kernel per 8-bit pass with decoupled look-back:
+//   * blocks take tickets in launch order, so a block only ever waits for blocks already running;
+//   * each wave ranks its 1024 keys (16 rounds of 64) against its own digit counters in LDS with
+//     ballot digit matching -- stable, no block barriers while ranking;
+//   * thread d of the block publishes the block's count of digit d, sums predecessors' counts
+//     (status words {flag, count}: the data is the flag, agent-scope relaxed atomics = sc1, so
+//     no fences; MI355X_MICROARCH.md, inter-workgroup visibility) until an inclusive prefix, and
+//     publishes its own inclusive prefix;
+//   * the tile is placed digit-sorted in LDS and written out in runs (coalesced stores).
+// A look-back spin is bounded: on timeout the pass sets the caller's error word and finishes
+// (results invalid, never a hang).
+constexpr int OS_ITEMS = 16;
+constexpr int OS_TILE = 256 * OS_ITEMS;       // keys per block
+constexpr uint32_t OS_AGG = 1u << 30, OS_PRE = 2u << 30, OS_CNT = (1u << 30) - 1u;
+
+typedef __attribute__((address_space(1))) uint32_t gu32;
+
 // Peers of this lane's digit inside the wave (lanes with the same digit among the valid lanes).
 __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid, int nbits) {
     uint64_t peers = __ballot(valid);
@@ -115,96 +131,208 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid, int nbit
     return peers;
 }
 
-__global__ void __launch_bounds__(256) k_radix_count(const uint32_t* __restrict__ keys, size_t n, int shift,
-                                                     int nbits, uint32_t* __restrict__ counts, uint32_t nb) {
-    __shared__ uint32_t s_h[256];
-    const int tid = threadIdx.x;
-    s_h[tid] = 0;
-    __syncthreads();
-    const uint32_t mask = (1u << nbits) - 1u;
-    const uint64_t lt = lanemask_lt();
-    const size_t base = (size_t)blockIdx.x * RADIX_TILE;
-    for (int r = 0; r < RADIX_ITEMS; ++r) {
-        const size_t idx = base + (size_t)r * 256 + tid;
-        const bool valid = idx < n;
-        const uint32_t d = valid ? (keys[idx] >> shift) & mask : 0u;
-        const uint64_t peers = match_digit(d, valid, nbits);
-        if (valid && __popcll(peers & lt) == 0) atomicAdd(&s_h[d], (uint32_t)__popcll(peers));
+// exclusive scan of one value per thread over a 256-thread block
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t x, uint32_t* s_wave) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t inc = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(inc, o);
+        if (lane >= o) inc += t;
     }
+    if (lane == 63) s_wave[wave] = inc;
     __syncthreads();
-    counts[(size_t)tid * nb + blockIdx.x] = s_h[tid];
+    uint32_t off = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) off += (w < wave) ? s_wave[w] : 0u;
+    __syncthreads();
+    return off + inc - x;
 }
 
-__global__ void __launch_bounds__(256) k_radix_scatter(const uint32_t* __restrict__ keys_in,
-                                                       const uint32_t* __restrict__ vals_in,
-                                                       uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
-                                                       size_t n, int shift, int nbits,
-                                                       const uint32_t* __restrict__ offsets, uint32_t nb) {
-    __shared__ uint32_t s_run[256];
-    __shared__ uint32_t s_cnt[4][256];
-    __shared__ uint32_t s_off[4][256];
-    const int tid = threadIdx.x, wave = tid >> 6;
-    s_run[tid] = offsets[(size_t)tid * nb + blockIdx.x];
+// Digit counts of every pass in one read of the keys (a pass permutes keys, it does not change
+// the counts).  A CU-sized grid strides over the keys (16 loads in flight per thread), so each
+// global counter takes at most one atomic per block.
+constexpr int OS_HIST_BLOCKS = 512;
+__global__ void __launch_bounds__(256) k_radix_hist(const uint32_t* __restrict__ keys, size_t n, int begin_bit,
+                                                    int end_bit, uint32_t* __restrict__ hist) {
+    __shared__ uint32_t s_h[4][256];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) s_cnt[w][tid] = 0;
+    for (int p = 0; p < 4; ++p) s_h[p][tid] = 0;
     __syncthreads();
-    const uint32_t mask = (1u << nbits) - 1u;
     const uint64_t lt = lanemask_lt();
-    const size_t base = (size_t)blockIdx.x * RADIX_TILE;
-    for (int r = 0; r < RADIX_ITEMS; ++r) {
-        const size_t idx = base + (size_t)r * 256 + tid;
-        const bool valid = idx < n;
-        uint32_t key = 0, val = 0, d = 0;
-        if (valid) { key = keys_in[idx]; val = vals_in[idx]; d = (key >> shift) & mask; }
-        const uint64_t peers = match_digit(d, valid, nbits);
-        const uint32_t rank = (uint32_t)__popcll(peers & lt);
-        if (valid && rank == 0) s_cnt[wave][d] = (uint32_t)__popcll(peers);
-        __syncthreads();
-        {
-            uint32_t run = s_run[tid];
+    for (size_t base = ((size_t)blockIdx.x * 4 + wave) * (64 * OS_ITEMS); base < n;
+         base += (size_t)gridDim.x * 4 * (64 * OS_ITEMS)) {
+        uint32_t key[OS_ITEMS];
 #pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                const uint32_t c = s_cnt[w][tid];
-                s_off[w][tid] = run;
-                run += c;
-                s_cnt[w][tid] = 0;
-            }
-            s_run[tid] = run;
+        for (int r = 0; r < OS_ITEMS; ++r) {
+            const size_t idx = base + (size_t)r * 64 + lane;
+            key[r] = idx < n ? keys[idx] : 0u;
         }
-        __syncthreads();
-        if (valid) {
-            const uint32_t dst = s_off[wave][d] + rank;
-            keys_out[dst] = key;
-            vals_out[dst] = val;
+#pragma unroll
+        for (int r = 0; r < OS_ITEMS; ++r) {
+            const bool valid = base + (size_t)r * 64 + lane < n;
+            int p = 0;
+            for (int shift = begin_bit; shift < end_bit; shift += 8, ++p) {
+                const int nbits = min(8, end_bit - shift);
+                const uint32_t d = (key[r] >> shift) & ((1u << nbits) - 1u);
+                const uint64_t peers = match_digit(d, valid, nbits);
+                if (valid && (peers & lt) == 0) atomicAdd(&s_h[p][d], (uint32_t)__popcll(peers));
+            }
         }
     }
+    __syncthreads();
+    int p = 0;
+    for (int shift = begin_bit; shift < end_bit; shift += 8, ++p)
+        if (s_h[p][tid]) atomicAdd(hist + p * 256 + tid, s_h[p][tid]);
 }
+
+__global__ void __launch_bounds__(256) k_radix_pass(const uint32_t* __restrict__ keys_in,
+                                                    const uint32_t* __restrict__ vals_in,
+                                                    uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
+                                                    size_t n, int shift, int nbits,
+                                                    const uint32_t* __restrict__ hist, uint32_t* status,
+                                                    uint32_t* ticket, uint32_t* err) {
+    __shared__ uint32_t s_key[OS_TILE];
+    __shared__ uint32_t s_val[OS_TILE];
+    __shared__ uint32_t s_wcnt[4][256];
+    __shared__ uint32_t s_gbase[256];
+    __shared__ uint32_t s_lbase[256];
+    __shared__ uint32_t s_wave[4];
+    __shared__ uint32_t s_bid;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    if (tid == 0) s_bid = atomicAdd(ticket, 1u);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) s_wcnt[w][tid] = 0;
+
+    __syncthreads();
+    const uint32_t bid = s_bid;
+    const uint32_t mask = (1u << nbits) - 1u;
+    const uint64_t lt = lanemask_lt();
+    const size_t base = (size_t)bid * OS_TILE + (size_t)wave * (64 * OS_ITEMS);
+    uint32_t key[OS_ITEMS], val[OS_ITEMS], rank[OS_ITEMS];
+#pragma unroll
+    for (int r = 0; r < OS_ITEMS; ++r) {
+        const size_t idx = base + (size_t)r * 64 + lane;
+        const bool valid = idx < n;
+        key[r] = valid ? keys_in[idx] : 0u;
+        val[r] = valid ? vals_in[idx] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < OS_ITEMS; ++r) {
+        const bool valid = base + (size_t)r * 64 + lane < n;
+        const uint32_t d = (key[r] >> shift) & mask;
+        const uint64_t peers = match_digit(d, valid, nbits);
+        const uint32_t before = s_wcnt[wave][d];
+        const uint32_t pr = (uint32_t)__popcll(peers & lt);
+        rank[r] = before + pr;
+        __builtin_amdgcn_wave_barrier();
+        if (valid && pr == 0) s_wcnt[wave][d] = before + (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+
+    // thread tid = digit: block count, per-wave offsets, look-back, local and global bases
+    const uint32_t c0 = s_wcnt[0][tid], c1 = s_wcnt[1][tid], c2 = s_wcnt[2][tid], c3 = s_wcnt[3][tid];
+    const uint32_t total = c0 + c1 + c2 + c3;
+    s_wcnt[0][tid] = 0; s_wcnt[1][tid] = c0; s_wcnt[2][tid] = c0 + c1; s_wcnt[3][tid] = c0 + c1 + c2;
+    gu32* st = (gu32*)status;   // global address space: agent-scope atomics compile to global_* sc1
+    uint32_t prefix = 0;
+#ifdef LSR_ABL_NOLOOKBACK
+    if (true) {
+#else
+    if (bid == 0) {
+#endif
+        __hip_atomic_store(st + tid, OS_PRE | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        __hip_atomic_store(st + (size_t)bid * 256 + tid, OS_AGG | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // window of 8 predecessors per round trip, nearest first; stop at an inclusive prefix,
+        // resume at the first one not published yet.  Block 0 always publishes a prefix.
+        uint32_t p = bid;   // predecessors p-1, p-2, ... not consumed yet
+        uint32_t spins = 0;
+        while (true) {
+            constexpr int LB = 8;
+            uint32_t v[LB];
+#pragma unroll
+            for (int j = 0; j < LB; ++j)
+                v[j] = (uint32_t)j < p ? __hip_atomic_load(st + (size_t)(p - 1 - j) * 256 + tid, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT)
+                                       : 0u;
+            bool found = false;
+            uint32_t used = 0;
+#pragma unroll
+            for (int j = 0; j < LB; ++j) {
+                if (found || used != (uint32_t)j || (uint32_t)j >= p) continue;
+                if (v[j] & OS_PRE) { prefix += v[j] & OS_CNT; found = true; }
+                else if (v[j] & OS_AGG) { prefix += v[j] & OS_CNT; ++used; }
+            }
+            if (found) break;
+            p -= used;
+            if (used == 0) {
+                if (++spins > (1u << 22)) { atomicOr(err, 1u); break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        __hip_atomic_store(st + (size_t)bid * 256 + tid, OS_PRE | (prefix + total), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const uint32_t dstart = block_excl_scan256(hist[tid], s_wave);   // global start of digit tid
+    const uint32_t lbase = block_excl_scan256(total, s_wave);        // local start of digit tid
+    s_lbase[tid] = lbase;
+    s_gbase[tid] = dstart + prefix - lbase;
+    __syncthreads();
+    // digit-sorted placement in LDS, then runs to global
+    const size_t tile0 = (size_t)bid * OS_TILE;
+    const int ntile = (int)min((size_t)OS_TILE, n - min(n, tile0));
+#pragma unroll
+    for (int r = 0; r < OS_ITEMS; ++r) {
+        const bool valid = base + (size_t)r * 64 + lane < n;
+        if (valid) {
+            const uint32_t d = (key[r] >> shift) & mask;
+            const uint32_t pos = s_lbase[d] + s_wcnt[wave][d] + rank[r];
+            s_key[pos] = key[r];
+            s_val[pos] = val[r];
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < ntile; i += 256) {
+        const uint32_t k = s_key[i];
+        const uint32_t dst = s_gbase[(k >> shift) & mask] + (uint32_t)i;
+        keys_out[dst] = k;
+        vals_out[dst] = s_val[i];
+    }
+}
+
+static size_t os_blocks(size_t n) { return (n + OS_TILE - 1) / OS_TILE; }
 
 size_t radix_temp_bytes(size_t n) {
-    const size_t nb = (n + RADIX_TILE - 1) / RADIX_TILE;
-    const size_t nc = nb * 256;
-    return align_up(nc * 4, 256) * 2 + scan_temp_bytes(nc);
+    // hist [4][256] | tickets [4] | err [1] (padded) | status [4][blocks][256]
+    return align_up(4 * 256 * 4 + 64, 256) + align_up(4 * os_blocks(n) * 256 * 4, 256);
 }
 
 bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b, size_t n,
-                      int begin_bit, int end_bit, void* temp, hipStream_t st) {
+                      int begin_bit, int end_bit, void* temp, uint32_t* err, hipStream_t st) {
     if (n == 0 || end_bit <= begin_bit) return false;
-    const size_t nb = (n + RADIX_TILE - 1) / RADIX_TILE;
-    const size_t nc = nb * 256;
-    uint32_t* counts = reinterpret_cast<uint32_t*>(temp);
-    uint32_t* offs = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(temp) + align_up(nc * 4, 256));
-    void* scan_tmp = reinterpret_cast<char*>(temp) + 2 * align_up(nc * 4, 256);
+    const size_t nb = os_blocks(n);
+    uint32_t* hist = reinterpret_cast<uint32_t*>(temp);
+    uint32_t* tickets = hist + 4 * 256;
+    uint32_t* own_err = tickets + 4;
+    uint32_t* status = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(temp) + align_up(4 * 256 * 4 + 64, 256));
+    const int npass = (end_bit - begin_bit + 7) / 8;
+    (void)hipMemsetAsync(temp, 0, align_up(4 * 256 * 4 + 64, 256) + (size_t)npass * nb * 256 * 4, st);
+    const unsigned hb = (unsigned)min((size_t)OS_HIST_BLOCKS, (n + 64 * OS_ITEMS * 4 - 1) / (64 * OS_ITEMS * 4));
+    hipLaunchKernelGGL(k_radix_hist, dim3(hb), dim3(256), 0, st, (const uint32_t*)keys_a, n, begin_bit, end_bit, hist);
     bool in_b = false;
-    for (int shift = begin_bit; shift < end_bit; shift += 8) {
+    int p = 0;
+    for (int shift = begin_bit; shift < end_bit; shift += 8, ++p) {
         const int nbits = (end_bit - shift) < 8 ? (end_bit - shift) : 8;
         const uint32_t* kin = in_b ? keys_b : keys_a;
         const uint32_t* vin = in_b ? vals_b : vals_a;
         uint32_t* kout = in_b ? keys_a : keys_b;
         uint32_t* vout = in_b ? vals_a : vals_b;
-        hipLaunchKernelGGL(k_radix_count, dim3((unsigned)nb), dim3(256), 0, st, kin, n, shift, nbits, counts, (uint32_t)nb);
-        exclusive_scan_u32(counts, offs, nc, (uint32_t*)nullptr, scan_tmp, st);
-        hipLaunchKernelGGL(k_radix_scatter, dim3((unsigned)nb), dim3(256), 0, st, kin, vin, kout, vout, n, shift, nbits,
-                           (const uint32_t*)offs, (uint32_t)nb);
+        hipLaunchKernelGGL(k_radix_pass, dim3((unsigned)nb), dim3(256), 0, st, kin, vin, kout, vout, n, shift, nbits,
+                           (const uint32_t*)(hist + p * 256), status + (size_t)p * nb * 256, tickets + p,
+                           err ? err : own_err);
         in_b = !in_b;
     }
     return in_b;

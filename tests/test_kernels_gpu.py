@@ -35,3 +35,14 @@ def test_mfma16_helpers(tmp_path):
     r = subprocess.run(["timeout", "-k", "5", "60", exe], capture_output=True, text=True)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_radix_sort(tmp_path):
+    """Stable device radix sort (sort.hip) vs std::stable_sort at the binning's shapes."""
+    src = os.path.join(ROOT, "tests", "kernels", "t_sort.hip")
+    exe = str(tmp_path / "t_sort")
+    subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+                    "-I", os.path.join(ROOT, "4dlangsplat_amd", "csrc"), "-o", exe, src], check=True)
+    r = subprocess.run(["timeout", "-k", "5", "120", exe], capture_output=True, text=True)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr

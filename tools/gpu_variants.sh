@@ -3,6 +3,7 @@
 # the per-phase times.  Each run has its own time limit; the first failure ends the script.
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/var
+shopt -s nullglob
 for lib in 4dlangsplat_amd/build/liblsr.so 4dlangsplat_amd/build/variants/*.so; do
     n=$(basename $lib .so)
     LSR_LIBRARY=$PWD/$lib timeout -k 10 300 python bench.py --steps ${STEPS:-2} --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/var/$n.log 2>&1
