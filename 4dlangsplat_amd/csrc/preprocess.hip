@@ -100,18 +100,10 @@ __device__ __forceinline__ void stage_rows(float* __restrict__ lds, const float*
     }
 }
 
-template <int MS>  // staged SH coefficients (0 = read from global directly)
+template <int MS>  // SH coefficients per Gaussian known at compile time (0 = any M, read from global)
 __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
-    constexpr int M3 = MS * 3, SP = M3 + 1;
-    __shared__ float s_sh[MS > 0 ? 256 * SP : 1];
+    constexpr int M3 = MS * 3;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if constexpr (MS > 0) {
-        const int g0 = blockIdx.x * blockDim.x;
-        if (a.shs && !a.colors_precomp) {
-            stage_rows<M3>(s_sh, a.shs + (size_t)g0 * M3, min(256, a.P - g0));
-            __syncthreads();
-        }
-    }
     if (i >= a.P) return;
     a.radii[i] = 0;
     a.radius[i] = 0;
@@ -169,7 +161,22 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
         float3 dir = make_float3(p.x - a.campos[0], p.y - a.campos[1], p.z - a.campos[2]);
         const float len = sqrtf(dir.x * dir.x + dir.y * dir.y + dir.z * dir.z);
         dir.x = dir.x / len; dir.y = dir.y / len; dir.z = dir.z / len;
-        const float* sh = MS > 0 ? s_sh + threadIdx.x * SP : a.shs + (size_t)i * a.M * 3;
+        // the row in registers, every load in flight at once (float4 when 16-byte aligned)
+        float shr[48];   // static indices reach coefficient 15; only the first M3 are loaded (deg validated)
+        if constexpr (MS > 0) {
+            const float* src = a.shs + (size_t)i * M3;
+            if (M3 % 4 == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+#pragma unroll
+                for (int q = 0; q < M3 / 4; ++q) {
+                    const float4 v = reinterpret_cast<const float4*>(src)[q];
+                    shr[4 * q] = v.x; shr[4 * q + 1] = v.y; shr[4 * q + 2] = v.z; shr[4 * q + 3] = v.w;
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < M3; ++q) shr[q] = src[q];
+            }
+        }
+        const float* sh = MS > 0 ? shr : a.shs + (size_t)i * a.M * 3;
         uint8_t cl = 0;
         const int deg = a.deg;
 #pragma unroll
@@ -213,8 +220,7 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
 void launch_preprocess(const PreprocessArgs& a, hipStream_t st) {
     if (a.P == 0) return;
     const dim3 grid((a.P + 255) / 256), block(256);
-    const int ms = 0;   // direct SH reads measured faster than LDS staging here (occupancy)
-    switch (ms) {
+    switch ((a.shs && !a.colors_precomp) ? a.M : 0) {
         case 1: hipLaunchKernelGGL(k_preprocess<1>, grid, block, 0, st, a); break;
         case 4: hipLaunchKernelGGL(k_preprocess<4>, grid, block, 0, st, a); break;
         case 9: hipLaunchKernelGGL(k_preprocess<9>, grid, block, 0, st, a); break;
@@ -350,18 +356,62 @@ __device__ __forceinline__ void stage_visible_rows(float* __restrict__ lds, cons
         if constexpr (M3 % 4 == 0) {
             constexpr int R4 = M3 / 4;
             const float4* s4 = reinterpret_cast<const float4*>(src);
-            for (int e = threadIdx.x; e < rows * R4; e += blockDim.x) {
-                const int r = e / R4, c = 4 * (e - r * R4);
-                if (!s_vis[r]) continue;
-                const float4 v = s4[e];
-                float* d = lds + r * SP + c;
-                d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+            if (rows == 256 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+                // full block: every load in flight at once (compile-time trip count)
+                float4 v[R4];
+#pragma unroll
+                for (int j = 0; j < R4; ++j) {
+                    const int e = threadIdx.x + 256 * j;
+                    v[j] = s_vis[e / R4] ? s4[e] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                }
+#pragma unroll
+                for (int j = 0; j < R4; ++j) {
+                    const int e = threadIdx.x + 256 * j, r = e / R4, c = 4 * (e - r * R4);
+                    float* d = lds + r * SP + c;
+                    d[0] = v[j].x; d[1] = v[j].y; d[2] = v[j].z; d[3] = v[j].w;
+                }
+                return;
             }
-        } else {
-            for (int e = threadIdx.x; e < rows * M3; e += blockDim.x) {
-                const int r = e / M3, c = e - r * M3;
-                if (s_vis[r]) lds[r * SP + c] = src[e];
+        }
+        for (int e = threadIdx.x; e < rows * M3; e += blockDim.x) {
+            const int r = e / M3, c = e - r * M3;
+            if (s_vis[r]) lds[r * SP + c] = src[e];
+        }
+    }
+}
+
+// Coalesced write-out (or accumulation) of a block's staged SH gradient rows; culled rows are
+// skipped when accumulating (their gradient is zero).
+template <bool ACC, int M3>
+__device__ __forceinline__ void write_rows(float* __restrict__ dst, const float* __restrict__ lds, int rows,
+                                           const uint8_t* __restrict__ s_vis) {
+    if constexpr (M3 > 0) {
+        constexpr int SP = M3 + 1;
+        if constexpr (M3 % 4 == 0) {
+            constexpr int R4 = M3 / 4;
+            float4* d4 = reinterpret_cast<float4*>(dst);
+            if (rows == 256 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+                float4 cur[R4];
+                bool ok[R4];
+#pragma unroll
+                for (int j = 0; j < R4; ++j) {
+                    const int e = threadIdx.x + 256 * j;
+                    ok[j] = !ACC || s_vis[e / R4];
+                    cur[j] = (ACC && ok[j]) ? d4[e] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                }
+#pragma unroll
+                for (int j = 0; j < R4; ++j) {
+                    const int e = threadIdx.x + 256 * j, r = e / R4, c = 4 * (e - r * R4);
+                    if (!ok[j]) continue;
+                    const float* l = lds + r * SP + c;
+                    d4[e] = make_float4(cur[j].x + l[0], cur[j].y + l[1], cur[j].z + l[2], cur[j].w + l[3]);
+                }
+                return;
             }
+        }
+        for (int e = threadIdx.x; e < rows * M3; e += blockDim.x) {
+            const int r = e / M3, c = e - r * M3;
+            if (!ACC || s_vis[r]) put<ACC>(dst + e, lds[r * SP + c]);
         }
     }
 }
@@ -537,13 +587,7 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
     }
     if (stage && a.dsh) {   // coalesced write-out of the block's SH gradient rows
         __syncthreads();
-        float* dst = a.dsh + (size_t)g0 * M3;
-        if constexpr (M3 > 0) {
-            for (int e = threadIdx.x; e < rows * M3; e += blockDim.x) {
-                const int r = e / M3, c = e - r * M3;
-                if (!ACC || s_vis[r]) put<ACC>(dst + e, s_sh[r * SP + c]);
-            }
-        }
+        write_rows<ACC, M3>(a.dsh + (size_t)g0 * M3, s_sh, rows, s_vis);
     }
 }
 
