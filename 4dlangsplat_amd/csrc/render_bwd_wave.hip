@@ -1,5 +1,5 @@
-// render_bwd_wave.hip -- compositor backward, one independent wave per 8x8 pixel quadrant, with
-// the language channels (C <= 32) on matrix cores.
+// render_bwd_wave.hip -- compositor backward, one independent wave per 8x8 pixel quadrant, every
+// per-Gaussian sum over pixels on matrix cores.
 //
 // Same mathematics as render_bwd.hip (upstream backward).  Measured on the
 // headline scene, only a third of the replayed list entries touch any pixel of a given 8x8
@@ -8,13 +8,16 @@
 //   1. scans its replay range (up to the largest n_contrib of its pixels) back to front, 64
 //      entries per round, one per lane: a conservative ellipse-vs-quadrant test
 //      (quad_may_touch) and a ballot compaction into a per-wave FIFO in LDS;
-//   2. processes the surviving entries in groups of 16 (WG):
-//        MFMA1  S[e][px]  = sum_c F[e][c] G[px][c]    the language part of dot(c_e, dL/dpix)
-//        serial           the per-pixel back-to-front recurrence and the 10 scalar gradients,
-//                         summed over the wave by a transpose-reduce, one global atomic each
-//        MFMA2  dF[e][c]  = sum_px W[px][e] G[px][c]  the language gradient, W = alpha T,
-//                         one global atomic per (entry, channel)
-//      both on v_mfma_f32_16x16x32_bf16 with hi/lo bf16 splits (lsr_mfma.h).
+//   2. processes the surviving entries in groups of 16 (WG).  Per group, with pixels p on lanes:
+//        MFMA1   S[e][p] = sum_c F[e][c] G[p][c]           language part of dot(c_e, dL/dpix)
+//        serial  the back-to-front recurrence per pixel: w = alpha T and t = G dL/dalpha
+//        MFMA-W  sum_p w[p][e] [G[p][c] | g_rgb,depth[p]]   dL/dlanguage, dL/dcolour, dL/ddepth
+//        MFMA-T  sum_p t[p][e] {1, x, y, x^2, xy, y^2}(p)   pixel moments, from which the mean2D,
+//                                                         conic and opacity gradients follow exactly
+//                                                         (dx = X_e - x, dy = Y_e - y in quadrant-
+//                                                         local coordinates: well conditioned)
+//      all on v_mfma_f32_16x16x32_bf16 with hi/lo bf16 splits (lsr_mfma.h; the moment operand is
+//      small integers, exact in bf16), then one global atomic per (entry, quantity).
 // No block barriers: 64-thread blocks, the four quadrants of a tile on one XCD.
 #include "lsr_common.h"
 #include "lsr_internal.h"
@@ -23,21 +26,22 @@
 namespace lsr {
 
 constexpr int WG = 16;       // compacted entries per MFMA group
-constexpr int WFP = 40;      // F / G row pitch in bf16 (32 channels + 8): 80-byte rows, 16-byte aligned
-constexpr int WWP = 20;      // W row pitch in bf16 (16 entries + 4): 40-byte rows, 8-byte aligned
+constexpr int WFP = 40;      // F row pitch in bf16 (32 channels + 8): 80-byte rows, 16-byte aligned
+constexpr int WGB = 48;      // G row pitch in bf16 at the one-off build: 32 language + 4 rgb/depth + 12 zero
+constexpr int WWP = 20;      // W / t row pitch in bf16 (16 entries + 4): 40-byte rows, 8-byte aligned
 constexpr int WFIFO = 128;   // compacted entries waiting (list positions and ids); power of two
 
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 k_render_bwd_wave(RenderBwdArgs a) {
-    __shared__ __attribute__((aligned(16))) __bf16 s_GW[64 * WFP];      // G rows once, then W hi | lo
-    __shared__ __attribute__((aligned(16))) __bf16 s_Fh[WG * WFP];
-    __shared__ __attribute__((aligned(16))) __bf16 s_Fl[WG * WFP];
+    __shared__ __attribute__((aligned(16))) __bf16 s_FR[64 * WGB];       // G rows (build), then F / W / t rows
     __shared__ float4 s_co[WG];
     __shared__ float4 s_rgbd[WG];
     __shared__ float2 s_xy[WG];
     __shared__ float s_thr[WG];
     __shared__ uint32_t s_gid[WG];
     __shared__ uint32_t s_k[WG];
+    __shared__ float s_mom[WG][8];
+    __shared__ float s_q[WG][10];   // per-entry scalar gradients in acc_small record order
     __shared__ uint32_t s_fk[WFIFO];
     __shared__ uint32_t s_fg[WFIFO];
 
@@ -69,47 +73,63 @@ k_render_bwd_wave(RenderBwdArgs a) {
         if (a.dL_ddepth) gD = a.dL_ddepth[pid];
     }
 
-    // ---- G fragments (this wave's 64 pixels x 32 channels), built once through LDS rows [px][c]
-    // b1[pb]     : MFMA1 B, K = channel 8 g4 + j, N = pixel 16 pb + l16
-    // b2[kb][nb] : MFMA2 B, K = pixel 32 kb + 8 g4 + j, N = channel 16 nb + l16
-    bf16x8 b1h[4], b1l[4], b2h[2][2], b2l[2][2];
+    // ---- B fragments, built once through LDS rows [p][c] (c < 32 language, 32..35 rgb + depth):
+    // b1[pb]     : MFMA1 B,  K = channel 8 g4 + j,       N = pixel 16 pb + l16
+    // b2[kb][nb] : MFMA-W B, K = pixel 32 kb + 8 g4 + j, N = column 16 nb + l16 (nb = 2: rgb, depth)
+    // bm[kb]     : MFMA-T B, K = pixel 32 kb + 8 g4 + j, N = moment l16 (exact small integers)
+    bf16x8 b1h[4], b1l[4], b2h[2][3], b2l[2][3], bm[2];
     {
-        float gl[32];
+        float gl[40];
 #pragma unroll
         for (int c = 0; c < 32; ++c)
             gl[c] = (inside && a.dL_dlang && c < C) ? a.dL_dlang[(size_t)c * HW + pid] : 0.0f;
+        gl[32] = g0; gl[33] = g1; gl[34] = g2; gl[35] = gD;
+#pragma unroll
+        for (int c = 36; c < 40; ++c) gl[c] = 0.0f;
 #pragma unroll
         for (int part = 0; part < 2; ++part) {
 #pragma unroll
-            for (int c8 = 0; c8 < 4; ++c8) {
+            for (int c8 = 0; c8 < 6; ++c8) {
                 bf16x8 v;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     __bf16 h, l;
-                    split_bf16(gl[8 * c8 + j], h, l);
+                    split_bf16(c8 < 5 ? gl[8 * c8 + j] : 0.0f, h, l);
                     v[j] = part == 0 ? h : l;
                 }
-                *reinterpret_cast<bf16x8*>(s_GW + lane * WFP + 8 * c8) = v;
+                *reinterpret_cast<bf16x8*>(s_FR + lane * WGB + 8 * c8) = v;
             }
             wave_lds_sync();
             bf16x8* B1 = part == 0 ? b1h : b1l;
 #pragma unroll
             for (int pb = 0; pb < 4; ++pb)
-                B1[pb] = *reinterpret_cast<const bf16x8*>(s_GW + (16 * pb + l16) * WFP + 8 * g4);
+                B1[pb] = *reinterpret_cast<const bf16x8*>(s_FR + (16 * pb + l16) * WGB + 8 * g4);
 #pragma unroll
             for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-                for (int nb = 0; nb < 2; ++nb) {
-                    const __bf16* p = s_GW + (32 * kb + 8 * g4 + (l16 >> 2)) * WFP + 16 * nb + 4 * (l16 & 3);
-                    const bf16x4 lo4 = ds_read_tr16(p), hi4 = ds_read_tr16(p + 4 * WFP);
+                for (int nb = 0; nb < 3; ++nb) {
+                    const __bf16* p = s_FR + (32 * kb + 8 * g4 + (l16 >> 2)) * WGB + 16 * nb + 4 * (l16 & 3);
+                    const bf16x4 lo4 = ds_read_tr16(p), hi4 = ds_read_tr16(p + 4 * WGB);
                     const bf16x8 v = __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7);
                     if (part == 0) b2h[kb][nb] = v; else b2l[kb][nb] = v;
                 }
             wave_lds_sync();
         }
+        // pixel p = 32 kb + 8 g4 + j has local x = j, y = 4 kb + g4
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float x = (float)j, y = (float)(4 * kb + g4);
+                const float m = l16 == 0 ? 1.0f : l16 == 1 ? x : l16 == 2 ? y : l16 == 3 ? x * x
+                              : l16 == 4 ? x * y : l16 == 5 ? y * y : 0.0f;
+                bm[kb][j] = (__bf16)m;
+            }
     }
-    __bf16* s_Wh = s_GW;
-    __bf16* s_Wl = s_GW + 64 * WWP;
+    __bf16* s_Fh = s_FR;              // F rows [e][c] of the group (MFMA1 A), hi
+    __bf16* s_Fl = s_FR + WG * WFP;   // lo
+    __bf16* s_Rh = s_FR;              // after MFMA1: W or t rows [p][e], hi
+    __bf16* s_Rl = s_FR + 64 * WWP;   // lo
 
     const float bg_dot = a.bg[0] * g0 + a.bg[1] * g1 + a.bg[2] * g2;
     const float ddelx_dx = 0.5f * (float)a.W, ddely_dy = 0.5f * (float)a.H;
@@ -118,17 +138,28 @@ k_render_bwd_wave(RenderBwdArgs a) {
 
     int pos = (int)nrep;     // list positions [0, pos) not yet scanned
     int head = 0, tail = 0;  // FIFO counters (wave-uniform)
-    while (true) {
-        // ---- 1. scan + compaction until a group is available or the range is exhausted -----
-        while (tail - head < WG && pos > 0) {
-            const int base = max(pos - 64, 0);
-            const int k = base + lane;
-            bool cand = false;
-            uint32_t gid = 0;
-            if (k < pos) {
-                gid = a.point_list[range.x + k];
-                cand = quad_may_touch(a.xy[gid], a.conic_o[gid], bx0, bx1, by0, by1);
+    // scan prefetch: ids, centres and conics of the round at positions [pos - 64, pos)
+    uint32_t sc_gid = 0;
+    float2 sc_xy = make_float2(0.0f, 0.0f);
+    float4 sc_co = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (pos - 64 + lane >= 0) {
+        sc_gid = a.point_list[range.x + pos - 64 + lane];
+        sc_xy = a.xy[sc_gid];
+        sc_co = a.conic_o[sc_gid];
+    }
+    // scan rounds until `want` entries wait in the FIFO or the range is exhausted
+    auto scan_fill = [&](int want) {
+        while (tail - head < want && pos > 0) {
+            const int k = pos - 64 + lane;       // this round's positions (k < 0: before the list)
+            const uint32_t gid = sc_gid;
+            const float2 xy = sc_xy;
+            const float4 co = sc_co;
+            if (k - 64 >= 0) {                   // next round's loads in flight during this one
+                sc_gid = a.point_list[range.x + k - 64];
+                sc_xy = a.xy[sc_gid];
+                sc_co = a.conic_o[sc_gid];
             }
+            const bool cand = k >= 0 && quad_may_touch(xy, co, bx0, bx1, by0, by1);
             const uint64_t m = __ballot(cand);
             if (cand) {   // back to front: higher list positions first
                 const int rank = lane == 63 ? 0 : __popcll(m >> (lane + 1));
@@ -137,52 +168,75 @@ k_render_bwd_wave(RenderBwdArgs a) {
                 s_fg[s] = gid;
             }
             tail += __popcll(m);
-            pos = base;
+            pos = max(pos - 64, 0);
         }
-        const int cnt = min(WG, tail - head);
-        if (cnt == 0) break;
         wave_lds_sync();
-        // ---- 2. stage the group: geometry (lanes 0-15), language rows (lane -> entry lane/4) ----
+    };
+    // group prefetch registers: geometry of entry `lane` (lanes < WG), language row slice
+    // (entry lane / 4, channels 8 (lane & 3) .. +7)
+    uint32_t pf_gid = 0, pf_k = 0xFFFFFFFFu;
+    float2 pf_xy = make_float2(0.0f, 0.0f);
+    float4 pf_co = make_float4(0.0f, 0.0f, 0.0f, 0.0f), pf_rgbd = pf_co, pf_f0 = pf_co, pf_f1 = pf_co;
+    auto load_group = [&](int n) {   // issue the loads of FIFO entries [head, head + n)
         if (lane < WG) {
-            const bool ok = lane < cnt;
+            const bool ok = lane < n;
             const int s = (head + lane) & (WFIFO - 1);
-            const uint32_t gid = ok ? s_fg[s] : 0u;
-            const float4 co = ok ? a.conic_o[gid] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            s_gid[lane] = gid;
-            s_k[lane] = ok ? s_fk[s] : 0xFFFFFFFFu;
-            s_xy[lane] = ok ? a.xy[gid] : make_float2(0.0f, 0.0f);
-            s_co[lane] = co;
-            s_rgbd[lane] = ok ? a.rgbd[gid] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            s_thr[lane] = ok ? skip_power(co.w) : __builtin_inff();
+            pf_gid = ok ? s_fg[s] : 0u;
+            pf_k = ok ? s_fk[s] : 0xFFFFFFFFu;
+            pf_xy = ok ? a.xy[pf_gid] : make_float2(0.0f, 0.0f);
+            pf_co = ok ? a.conic_o[pf_gid] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            pf_rgbd = ok ? a.rgbd[pf_gid] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         }
-        {
-            const int e = lane >> 2, c0 = 8 * (lane & 3);
-            const bool ok = e < cnt;
-            const uint32_t gid = ok ? s_fg[(head + e) & (WFIFO - 1)] : 0u;
+        const int e = lane >> 2, c0 = 8 * (lane & 3);
+        const bool ok = e < n;
+        const uint32_t gid = ok ? s_fg[(head + e) & (WFIFO - 1)] : 0u;
+        if (C == 32) {
+            const float4* r = reinterpret_cast<const float4*>(a.lang + (size_t)gid * 32 + c0);
+            pf_f0 = ok ? r[0] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            pf_f1 = ok ? r[1] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        } else {
             float f[8];
-            if (C == 32) {
-                const float4* r = reinterpret_cast<const float4*>(a.lang + (size_t)gid * 32 + c0);
-                const float4 v0 = ok ? r[0] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                const float4 v1 = ok ? r[1] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                f[0] = v0.x; f[1] = v0.y; f[2] = v0.z; f[3] = v0.w; f[4] = v1.x; f[5] = v1.y; f[6] = v1.z; f[7] = v1.w;
-            } else {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) f[j] = (ok && c0 + j < C) ? a.lang[(size_t)gid * C + c0 + j] : 0.0f;
-            }
-            bf16x8 h8, l8;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                __bf16 h, l;
-                split_bf16(f[j], h, l);
-                h8[j] = h; l8[j] = l;
-            }
-            *reinterpret_cast<bf16x8*>(s_Fh + e * WFP + c0) = h8;
-            *reinterpret_cast<bf16x8*>(s_Fl + e * WFP + c0) = l8;
+            for (int j = 0; j < 8; ++j) f[j] = (ok && c0 + j < C) ? a.lang[(size_t)gid * C + c0 + j] : 0.0f;
+            pf_f0 = make_float4(f[0], f[1], f[2], f[3]);
+            pf_f1 = make_float4(f[4], f[5], f[6], f[7]);
         }
-        head += cnt;
+        head += n;
+    };
+    auto store_group = [&]() {       // prefetched group -> LDS staging
+        if (lane < WG) {
+            s_gid[lane] = pf_gid;
+            s_k[lane] = pf_k;
+            s_xy[lane] = pf_xy;
+            s_co[lane] = pf_co;
+            s_rgbd[lane] = pf_rgbd;
+            s_thr[lane] = pf_k != 0xFFFFFFFFu ? skip_power(pf_co.w) : __builtin_inff();
+        }
+        const int e = lane >> 2, c0 = 8 * (lane & 3);
+        const float f[8] = {pf_f0.x, pf_f0.y, pf_f0.z, pf_f0.w, pf_f1.x, pf_f1.y, pf_f1.z, pf_f1.w};
+        bf16x8 h8, l8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            __bf16 h, l;
+            split_bf16(f[j], h, l);
+            h8[j] = h; l8[j] = l;
+        }
+        *reinterpret_cast<bf16x8*>(s_Fh + e * WFP + c0) = h8;
+        *reinterpret_cast<bf16x8*>(s_Fl + e * WFP + c0) = l8;
         wave_lds_sync();
+    };
 
-        // ---- 3. MFMA1: S[e][px], then to one pixel per lane -----------------------------------
+    scan_fill(WG);
+    int cnt = min(WG, tail - head);
+    if (cnt > 0) load_group(cnt);
+    while (cnt > 0) {
+        store_group();
+        // next group's loads in flight while this one computes
+        scan_fill(WG);
+        const int next_cnt = min(WG, tail - head);
+        if (next_cnt > 0) load_group(next_cnt);
+
+        // ---- 3. MFMA1: S[e][p], then to one pixel per lane -------------------------------------
         float S[WG];
         {
             const bf16x8 ah = *reinterpret_cast<const bf16x8*>(s_Fh + l16 * WFP + 8 * g4);
@@ -195,6 +249,7 @@ k_render_bwd_wave(RenderBwdArgs a) {
                 d[pb] = LSR_MFMA16(ah, b1l[pb], d[pb]);
                 d[pb] = LSR_MFMA16(al, b1h[pb], d[pb]);
             }
+            wave_lds_sync();   // F read before W overwrites it
             // d[pb][i] at lane (g4, c): entry 4 g4 + i, pixel 16 pb + c
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -205,14 +260,13 @@ k_render_bwd_wave(RenderBwdArgs a) {
             }
         }
 
-        // ---- 4. serial back-to-front replay of the group ---------------------------------------
-        float wv[WG];
+        // ---- 4. serial back-to-front replay of the group: w = alpha T, t = G dL/dalpha --------
+        float wv[WG], tv[WG];
 #pragma unroll
         for (int e = 0; e < WG; ++e) {
             wv[e] = 0.0f;
+            tv[e] = 0.0f;
             if (e >= cnt) continue;                                  // wave-uniform
-            bool active = false;
-            float w = 0.0f, gm2x = 0.0f, gm2y = 0.0f, gcx = 0.0f, gcy = 0.0f, gcw = 0.0f, gop = 0.0f;
             if (s_k[e] < last_contributor) {
                 const float2 xy = s_xy[e];
                 const float4 co = s_co[e];
@@ -222,10 +276,8 @@ k_render_bwd_wave(RenderBwdArgs a) {
                     const float G = expf_repro(power);
                     const float alpha = fminf(0.99f, co.w * G);
                     if (alpha >= 1.0f / 255.0f) {
-                        active = true;
                         const float rom = __builtin_amdgcn_rcpf(1.0f - alpha);
                         T = T * rom;
-                        w = alpha * T;
                         const float4 cd = s_rgbd[e];
                         float dot = cd.x * g0;
                         dot = __builtin_fmaf(cd.y, g1, dot);
@@ -237,78 +289,115 @@ k_render_bwd_wave(RenderBwdArgs a) {
                         float dL_dalpha = (dot - acc_dot) * T;
                         last_alpha = alpha;
                         dL_dalpha = __builtin_fmaf(-T_final * rom, bg_dot, dL_dalpha);
-                        const float dL_dG = co.w * dL_dalpha;
-                        const float gdx = G * dx, gdy = G * dy;
-                        const float dG_ddelx = -gdx * co.x - gdy * co.y;
-                        const float dG_ddely = -gdy * co.z - gdx * co.y;
-                        gm2x = dL_dG * dG_ddelx * ddelx_dx;
-                        gm2y = dL_dG * dG_ddely * ddely_dy;
-                        gcx = -0.5f * gdx * dx * dL_dG;
-                        gcy = -0.5f * gdx * dy * dL_dG;
-                        gcw = -0.5f * gdy * dy * dL_dG;
-                        gop = G * dL_dalpha;
+                        wv[e] = alpha * T;
+                        tv[e] = G * dL_dalpha;
                     }
                 }
             }
-            wv[e] = w;
-            if (__any(active)) {
-                float v[16];
-                v[0] = w * g0; v[1] = w * g1; v[2] = w * g2; v[3] = w * gD;
-                v[4] = gm2x; v[5] = gm2y; v[6] = gcx; v[7] = gcy; v[8] = gcw; v[9] = gop;
-#pragma unroll
-                for (int q = 10; q < 16; ++q) v[q] = 0.0f;
-                wave_transpose_reduce<16>(v);
-                const int q = transpose_reduce_slot<16>(lane);
-                if ((lane & 3) == 0 && q < 10) atomicAdd(a.acc_small + (size_t)s_gid[e] * 12 + q, v[0]);
-            }
         }
 
-        // ---- 5. MFMA2: dF[e][c] = sum_px W[px][e] G[px][c] --------------------------------------
-        {
+        // ---- 5. sums over the wave's pixels on matrix cores -----------------------------------
+        // rows [p][e] of R (W, then t) in LDS; the A operand R^T comes from transposing reads
+        auto write_rows = [&](const float (&r)[WG]) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 bf16x4 h4, l4;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     __bf16 h, l;
-                    split_bf16(wv[4 * q + j], h, l);
+                    split_bf16(r[4 * q + j], h, l);
                     h4[j] = h; l4[j] = l;
                 }
-                *reinterpret_cast<bf16x4*>(s_Wh + lane * WWP + 4 * q) = h4;
-                *reinterpret_cast<bf16x4*>(s_Wl + lane * WWP + 4 * q) = l4;
+                *reinterpret_cast<bf16x4*>(s_Rh + lane * WWP + 4 * q) = h4;
+                *reinterpret_cast<bf16x4*>(s_Rl + lane * WWP + 4 * q) = l4;
             }
             wave_lds_sync();
-            f32x4 dacc[2] = {f32x4{0.0f, 0.0f, 0.0f, 0.0f}, f32x4{0.0f, 0.0f, 0.0f, 0.0f}};
+        };
+        auto read_a = [&](int kb, bf16x8& ah, bf16x8& al) {
+            const int row = 32 * kb + 8 * g4 + (l16 >> 2), col = 4 * (l16 & 3);
+            const bf16x4 h0 = ds_read_tr16(s_Rh + row * WWP + col), h1 = ds_read_tr16(s_Rh + (row + 4) * WWP + col);
+            const bf16x4 l0 = ds_read_tr16(s_Rl + row * WWP + col), l1 = ds_read_tr16(s_Rl + (row + 4) * WWP + col);
+            ah = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+            al = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+        };
+        // MFMA-W: dacc[nb][i] at lane (g4, c) = sum_p w[p][4 g4 + i] Gx[p][16 nb + c]
+        f32x4 dacc[3] = {f32x4{0.0f, 0.0f, 0.0f, 0.0f}, f32x4{0.0f, 0.0f, 0.0f, 0.0f}, f32x4{0.0f, 0.0f, 0.0f, 0.0f}};
+        write_rows(wv);
 #pragma unroll
-            for (int kb = 0; kb < 2; ++kb) {
-                const int row = 32 * kb + 8 * g4 + (l16 >> 2), col = 4 * (l16 & 3);
-                const bf16x4 h0 = ds_read_tr16(s_Wh + row * WWP + col), h1 = ds_read_tr16(s_Wh + (row + 4) * WWP + col);
-                const bf16x4 l0 = ds_read_tr16(s_Wl + row * WWP + col), l1 = ds_read_tr16(s_Wl + (row + 4) * WWP + col);
-                const bf16x8 ah = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
-                const bf16x8 al = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+        for (int kb = 0; kb < 2; ++kb) {
+            bf16x8 ah, al;
+            read_a(kb, ah, al);
+#pragma unroll
+            for (int nb = 0; nb < 3; ++nb) {
+                dacc[nb] = LSR_MFMA16(ah, b2h[kb][nb], dacc[nb]);
+                dacc[nb] = LSR_MFMA16(ah, b2l[kb][nb], dacc[nb]);
+                dacc[nb] = LSR_MFMA16(al, b2h[kb][nb], dacc[nb]);
+            }
+        }
+        wave_lds_sync();   // W rows read before t overwrites them
+        // MFMA-T: dmom[i] at lane (g4, n) = sum_p t[p][4 g4 + i] moment_n(p)
+        f32x4 dmom = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        write_rows(tv);
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            bf16x8 ah, al;
+            read_a(kb, ah, al);
+            dmom = LSR_MFMA16(ah, bm[kb], dmom);
+            dmom = LSR_MFMA16(al, bm[kb], dmom);
+        }
+        if (l16 < 6) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) s_mom[4 * g4 + i][l16] = dmom[i];
+        }
+        if (l16 < 4) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) s_q[4 * g4 + i][l16] = dacc[2][i];   // rgb 0-2, depth 3
+        }
+        // ---- 6. atomics: language rows straight from the MFMA layout (4 entries x 16 channels per
+        //      instruction), then the 10 scalars of each entry, consecutive lanes on one record --
+        if (a.acc_lang) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int e = 4 * g4 + i;
+                if (e >= cnt) continue;
+                const size_t rowoff = (size_t)s_gid[e] * C;
 #pragma unroll
                 for (int nb = 0; nb < 2; ++nb) {
-                    dacc[nb] = LSR_MFMA16(ah, b2h[kb][nb], dacc[nb]);
-                    dacc[nb] = LSR_MFMA16(ah, b2l[kb][nb], dacc[nb]);
-                    dacc[nb] = LSR_MFMA16(al, b2h[kb][nb], dacc[nb]);
+                    const int ch = 16 * nb + l16;
+                    if (ch < C && dacc[nb][i] != 0.0f) atomicAdd(a.acc_lang + rowoff + ch, dacc[nb][i]);
                 }
             }
-            // dacc[nb][i] at lane (g4, c): entry 4 g4 + i, channel 16 nb + c
-            if (a.acc_lang) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int e = 4 * g4 + i;
-                    if (e >= cnt) continue;
-                    const size_t rowoff = (size_t)s_gid[e] * C;
-#pragma unroll
-                    for (int nb = 0; nb < 2; ++nb) {
-                        const int ch = 16 * nb + l16;
-                        if (ch < C && dacc[nb][i] != 0.0f) atomicAdd(a.acc_lang + rowoff + ch, dacc[nb][i]);
-                    }
-                }
-            }
-            wave_lds_sync();
         }
+        wave_lds_sync();
+        if (lane < cnt) {   // moments -> mean2D (4-5), conic (6-8), opacity (9)
+            const int e = lane;
+            const float M0 = s_mom[e][0], Mx = s_mom[e][1], My = s_mom[e][2];
+            const float Mxx = s_mom[e][3], Mxy = s_mom[e][4], Myy = s_mom[e][5];
+            const float2 xy = s_xy[e];
+            const float4 co = s_co[e];
+            const float X = xy.x - bx0, Y = xy.y - by0;      // quadrant-local centre
+            const float Sdx = X * M0 - Mx, Sdy = Y * M0 - My;
+            const float Sdxdx = X * X * M0 - 2.0f * X * Mx + Mxx;
+            const float Sdxdy = X * Y * M0 - X * My - Y * Mx + Mxy;
+            const float Sdydy = Y * Y * M0 - 2.0f * Y * My + Myy;
+            s_q[e][4] = -co.w * ddelx_dx * (co.x * Sdx + co.y * Sdy);
+            s_q[e][5] = -co.w * ddely_dy * (co.z * Sdy + co.y * Sdx);
+            s_q[e][6] = -0.5f * co.w * Sdxdx;
+            s_q[e][7] = -0.5f * co.w * Sdxdy;
+            s_q[e][8] = -0.5f * co.w * Sdydy;
+            s_q[e][9] = M0;
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int r = 0; r < (WG * 10 + 63) / 64; ++r) {
+            const int idx = lane + 64 * r, e = idx / 10, q = idx - 10 * e;
+            if (idx < cnt * 10) {
+                const float v = s_q[e][q];
+                if (v != 0.0f) atomicAdd(a.acc_small + (size_t)s_gid[e] * 12 + q, v);
+            }
+        }
+        wave_lds_sync();
+        cnt = next_cnt;
     }
 }
 

@@ -53,16 +53,16 @@ __global__ void __launch_bounds__(64) k_render_fwd_wave(RenderFwdArgs a) {
 
     uint32_t pos = range.x;  // list entries [pos, range.y) not yet scanned
     int head = 0, tail = 0;  // FIFO counters (wave-uniform)
+    // ids of the next scan round, loaded one round ahead
+    uint32_t gid_next = pos + lane < range.y ? a.point_list[pos + lane] : 0u;
     while (!__all(done)) {
         // ---- 1. scan + compaction -----------------------------------------------------------
         while (tail - head < GF && pos < range.y) {
             const uint32_t idx = pos + lane;
+            const uint32_t gid = gid_next;
+            gid_next = idx + 64 < range.y ? a.point_list[idx + 64] : 0u;
             bool cand = false;
-            uint32_t gid = 0;
-            if (idx < range.y) {
-                gid = a.point_list[idx];
-                cand = quad_may_touch(a.xy[gid], a.conic_o[gid], bx0, bx1, by0, by1);
-            }
+            if (idx < range.y) cand = quad_may_touch(a.xy[gid], a.conic_o[gid], bx0, bx1, by0, by1);
             const uint64_t m = __ballot(cand);
             if (cand) {
                 const int s = (tail + __popcll(m & lanemask_lt())) & (FIFO - 1);
@@ -88,12 +88,19 @@ __global__ void __launch_bounds__(64) k_render_fwd_wave(RenderFwdArgs a) {
             s_thr[lane] = ok ? skip_power(co.w) : __builtin_inff();
         }
         if constexpr (CPAD > 0) {
-            if (C == CPAD) {   // whole rows as float4
-                constexpr int R4 = CPAD / 4;
-                for (int q = lane; q < cnt * R4; q += 64) {
-                    const int e = q / R4, c4 = q - e * R4;
-                    const uint32_t gid = s_fg[(head + e) & (FIFO - 1)];
-                    reinterpret_cast<float4*>(s_lang)[q] = reinterpret_cast<const float4*>(a.lang + (size_t)gid * CPAD)[c4];
+            if (C == CPAD) {   // whole rows as float4, every load in flight at once
+                constexpr int R4 = CPAD / 4, NQ = (GF * R4 + 63) / 64;
+                float4 v[NQ];
+#pragma unroll
+                for (int j = 0; j < NQ; ++j) {
+                    const int q = lane + 64 * j, e = q / R4, c4 = q - e * R4;
+                    v[j] = q < cnt * R4 ? reinterpret_cast<const float4*>(a.lang + (size_t)s_fg[(head + e) & (FIFO - 1)] * CPAD)[c4]
+                                        : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                }
+#pragma unroll
+                for (int j = 0; j < NQ; ++j) {
+                    const int q = lane + 64 * j;
+                    if (q < GF * R4) reinterpret_cast<float4*>(s_lang)[q] = v[j];
                 }
             } else {
                 for (int q = lane; q < cnt * CPAD; q += 64) {

@@ -233,7 +233,9 @@ def test_deterministic_backward_is_bitwise_reproducible():
         if v is None:
             continue
         assert torch.equal(v, g2[k]), k
-        assert grad_err(ga[k].cpu().numpy(), v.cpu().numpy()) < 1e-5, k
+        # the default path sums over pixels on matrix cores (bf16 x3 products, ~1e-5 relative);
+        # both modes are held to the oracle at 1e-4 below and in test_backward_matches_oracle
+        assert grad_err(ga[k].cpu().numpy(), v.cpu().numpy()) < 5e-5, k
     # and the deterministic gradients match the oracle like the default ones
     ref = run_oracle(sc, cam)
     rg = ref.backward(gc.cpu().numpy(), gl.cpu().numpy(), None)
