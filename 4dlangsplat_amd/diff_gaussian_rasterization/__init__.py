@@ -98,13 +98,33 @@ def _stream(device):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
-def forward_native(raster_settings, means3D, opacities, shs=None, colors_precomp=None, language_feature=None,
-                   scales=None, rotations=None, cov3D_precomp=None):
-    """Forward through liblsr.so.  Returns (color, language_feature, radii, depth, state)."""
+class PendingForward:
+    """Phase 1 of a forward (preprocess, depth order, instance count) done; render_native finishes
+    it.  Holds the inputs, the geom workspace and num_rendered (K)."""
+
+    def __init__(self, raster_settings, settings, fin, inputs, geom, radii, K, device, H, W):
+        self.raster_settings, self.settings, self.fin, self.inputs = raster_settings, settings, fin, inputs
+        self.geom, self.radii, self.num_rendered, self.device, self.H, self.W = geom, radii, K, device, H, W
+
+
+def _dump_forward(raster_settings, inputs):
+    if raster_settings.debug:
+        torch.save({k: (None if v is None else v.cpu()) for k, v in inputs.items()
+                    if k in ("means3D", "opacities", "shs", "colors_precomp", "scales", "rotations")},
+                   "snapshot_fw.dump")
+        print("\nAn error occured in forward. Writing snapshot_fw.dump for debugging.")
+
+
+def preprocess_native(raster_settings, means3D, opacities, shs=None, colors_precomp=None, language_feature=None,
+                      scales=None, rotations=None, cov3D_precomp=None, stream=None):
+    """Forward phase 1 through liblsr.so (lsr_forward_preprocess) on `stream` (a torch stream,
+    default: the current one).  Synchronises that stream once to read num_rendered (as upstream).
+    Workspaces are allocated on `stream`; render_native may run on another stream."""
     device = means3D.device
     if device.type != "cuda":
         raise RuntimeError("the rasterizer runs on the GPU only (no CPU fallback); got tensors on " + str(device))
     L = _lib.load()
+    stream = stream or torch.cuda.current_stream(device)
     st = _NativeSettings(raster_settings, device)
     P = means3D.shape[0]
     means3D = _f32(means3D, device)
@@ -127,37 +147,60 @@ def forward_native(raster_settings, means3D, opacities, shs=None, colors_precomp
     fin.language_feature, fin.opacities = _ptr(language_feature), opacities.data_ptr()
     fin.scales, fin.rotations, fin.cov3D_precomp = _ptr(scales), _ptr(rotations), _ptr(cov3D_precomp)
     H, W = int(raster_settings.image_height), int(raster_settings.image_width)
-    radii = torch.empty(P, dtype=torch.int32, device=device)
+    inputs = dict(means3D=means3D, opacities=opacities, shs=shs, colors_precomp=colors_precomp,
+                  language_feature=language_feature, scales=scales, rotations=rotations, cov3D_precomp=cov3D_precomp)
+    with torch.cuda.stream(stream):
+        radii = torch.empty(P, dtype=torch.int32, device=device)
+        geom = torch.empty(int(L.lsr_geom_bytes(P)), dtype=torch.uint8, device=device)
+    fout = _lib.FwdOut()
+    fout.radii = radii.data_ptr()
+    K = ctypes.c_int64(0)
+    try:
+        _lib.check(L.lsr_forward_preprocess(ctypes.byref(st.c), ctypes.byref(fin), ctypes.byref(fout),
+                                            ctypes.c_void_p(geom.data_ptr()), ctypes.byref(K),
+                                            ctypes.c_void_p(stream.cuda_stream)), "lsr_forward_preprocess")
+    except RuntimeError:
+        _dump_forward(raster_settings, inputs)
+        raise
+    return PendingForward(raster_settings, st, fin, inputs, geom, radii, K.value, device, H, W)
+
+
+def render_native(pending: PendingForward):
+    """Forward phase 2 (binning, compositing) on the current stream.  Returns (color,
+    language_feature, radii, depth, state)."""
+    L = _lib.load()
+    device, H, W, C = pending.device, pending.H, pending.W, pending.fin.C
+    stream = torch.cuda.current_stream(device)
+    pending.geom.record_stream(stream)    # allocated on the preprocess stream, used from here on
+    pending.radii.record_stream(stream)
     color = torch.empty(3, H, W, dtype=torch.float32, device=device)
     lang_out = torch.empty(C, H, W, dtype=torch.float32, device=device)
     depth = torch.empty(1, H, W, dtype=torch.float32, device=device)
     fout = _lib.FwdOut()
     fout.out_color, fout.out_language_feature = color.data_ptr(), _ptr(lang_out) if C > 0 else None
-    fout.radii, fout.out_depth = radii.data_ptr(), depth.data_ptr()
-    geom = torch.empty(int(L.lsr_geom_bytes(P)), dtype=torch.uint8, device=device)
-    K = ctypes.c_int64(0)
-    stream = _stream(device)
+    fout.radii, fout.out_depth = pending.radii.data_ptr(), depth.data_ptr()
+    K = pending.num_rendered
+    binning = torch.empty(int(L.lsr_binning_bytes(K)), dtype=torch.uint8, device=device)
+    img = torch.empty(int(L.lsr_img_bytes(W, H)), dtype=torch.uint8, device=device)
     try:
-        _lib.check(L.lsr_forward_preprocess(ctypes.byref(st.c), ctypes.byref(fin), ctypes.byref(fout),
-                                            ctypes.c_void_p(geom.data_ptr()), ctypes.byref(K), stream),
-                   "lsr_forward_preprocess")
-        binning = torch.empty(int(L.lsr_binning_bytes(K.value)), dtype=torch.uint8, device=device)
-        img = torch.empty(int(L.lsr_img_bytes(W, H)), dtype=torch.uint8, device=device)
-        _lib.check(L.lsr_forward_render(ctypes.byref(st.c), ctypes.byref(fin), ctypes.byref(fout),
-                                        ctypes.c_void_p(geom.data_ptr()), ctypes.c_void_p(binning.data_ptr()),
-                                        ctypes.c_void_p(img.data_ptr()), K, stream), "lsr_forward_render")
+        _lib.check(L.lsr_forward_render(ctypes.byref(pending.settings.c), ctypes.byref(pending.fin), ctypes.byref(fout),
+                                        ctypes.c_void_p(pending.geom.data_ptr()), ctypes.c_void_p(binning.data_ptr()),
+                                        ctypes.c_void_p(img.data_ptr()), ctypes.c_int64(K), _stream(device)),
+                   "lsr_forward_render")
     except RuntimeError:
-        if raster_settings.debug:
-            torch.save(dict(means3D=means3D.cpu(), opacities=opacities.cpu(), shs=None if shs is None else shs.cpu(),
-                            colors_precomp=None if colors_precomp is None else colors_precomp.cpu(),
-                            scales=None if scales is None else scales.cpu(),
-                            rotations=None if rotations is None else rotations.cpu()), "snapshot_fw.dump")
-            print("\nAn error occured in forward. Writing snapshot_fw.dump for debugging.")
+        _dump_forward(pending.raster_settings, pending.inputs)
         raise
-    inputs = dict(means3D=means3D, opacities=opacities, shs=shs, colors_precomp=colors_precomp,
-                  language_feature=language_feature, scales=scales, rotations=rotations, cov3D_precomp=cov3D_precomp)
-    state = RasterizerState(st, inputs, fin, geom, binning, img, K.value, radii)
-    return color, lang_out, radii, depth, state
+    state = RasterizerState(pending.settings, pending.inputs, pending.fin, pending.geom, binning, img, K, pending.radii)
+    return color, lang_out, pending.radii, depth, state
+
+
+def forward_native(raster_settings, means3D, opacities, shs=None, colors_precomp=None, language_feature=None,
+                   scales=None, rotations=None, cov3D_precomp=None):
+    """Forward through liblsr.so on the current stream.  Returns (color, language_feature, radii,
+    depth, state)."""
+    return render_native(preprocess_native(raster_settings, means3D, opacities, shs=shs, colors_precomp=colors_precomp,
+                                           language_feature=language_feature, scales=scales, rotations=rotations,
+                                           cov3D_precomp=cov3D_precomp))
 
 
 def backward_native(state: RasterizerState, grad_color, grad_lang=None, grad_depth=None, out=None,

@@ -119,23 +119,47 @@ class ViewParallelStep:
         return self.bucket.radii > 0
 
 
-def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool = False):
+def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool = False, overlap: bool = True):
     """render_view callback for ViewParallelStep on the HIP rasterizer (the product path).
 
     scene    : object with means3D, opacities, shs, lang, scales, rotations device tensors
-    settings : list of GaussianRasterizationSettings, indexed by view
+    settings : dict (or list) of GaussianRasterizationSettings, indexed by view
     grad_fn  : grad_fn(v, color, lang, depth) -> (dL_dcolor, dL_dlang, dL_ddepth) for view v
-    Forward + backward of view v with the gradients accumulated straight into the bucket."""
+    Forward + backward of view v with the gradients accumulated straight into the bucket.
+
+    overlap=True pipelines the views: once view v's render and backward are enqueued, view v+1's
+    preprocess (its depth order and instance count, the one host synchronisation of a forward)
+    runs on a side stream, concurrently with them, so the device never waits for the host
+    between views.  Results are identical to the sequential order (the preprocess only reads the
+    Gaussians and writes its own workspace)."""
     import diff_gaussian_rasterization as dgr
 
+    side = torch.cuda.Stream(device=scene.means3D.device) if overlap else None
+    pending = {}
+    params_ready = torch.cuda.Event() if overlap else None
+
+    def has_view(v):
+        return v in settings if isinstance(settings, dict) else 0 <= v < len(settings)
+
+    def preprocess(v, stream=None):
+        return dgr.preprocess_native(settings[v], scene.means3D, scene.opacities, shs=scene.shs,
+                                     language_feature=scene.lang, scales=scene.scales, rotations=scene.rotations,
+                                     stream=stream)
+
     def render_view(v: int, bucket: GradBucket):
-        color, lang, radii, depth, st = dgr.forward_native(
-            settings[v], scene.means3D, scene.opacities, shs=scene.shs, language_feature=scene.lang,
-            scales=scene.scales, rotations=scene.rotations)
+        pf = pending.pop(v, None)
+        if pf is None:                    # first view of a step: the Gaussians are final here
+            pf = preprocess(v)
+            if params_ready is not None:
+                params_ready.record(torch.cuda.current_stream())
+        color, lang, radii, depth, st = dgr.render_native(pf)
         gc, gl, gd = grad_fn(v, color, lang, depth)
         dgr.backward_native(st, gc, gl, gd, out=bucket.views, accumulate=True, need=bucket.need(),
                             deterministic=deterministic)
         render_view.last_num_rendered = st.num_rendered
+        if side is not None and has_view(v + 1):
+            side.wait_event(params_ready)     # orders after the parameters, not after view v's work
+            pending[v + 1] = preprocess(v + 1, stream=side)
         return radii
 
     render_view.last_num_rendered = 0
