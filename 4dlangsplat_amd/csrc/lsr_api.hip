@@ -471,3 +471,8 @@ int lsr_profile_read(double* ms_total, int64_t* launches, int32_t n) {
 }
 
 }  // extern "C"
+
+namespace lsr {
+// shared with the other C-ABI translation units (deform_api.hip)
+int fail(int code, const std::string& msg) { return ::fail(code, msg); }
+}  // namespace lsr

@@ -112,6 +112,28 @@ struct RenderBwdArgs {
 inline int lang_pad(int C) { return C == 0 ? 0 : C <= 4 ? 4 : C <= 8 ? 8 : C <= 16 ? 16 : C <= 32 ? 32 : 64; }
 inline int record_floats(int C) { return 12 + lang_pad(C); }
 
+// deformation field forward (deform.hip)
+struct DeformArgs {
+    int P;
+    const float* means3D;
+    const float* time;
+    const float* aabb;                // [2][3] device: xyz_max, xyz_min
+    const float* planes;              // packed channel-last planes
+    int64_t poff[12];                 // float offset of plane 6 s + ci
+    int pw[12], ph[12];               // its width / height
+    const __bf16 *wf_h, *wf_l;        // [128][32]
+    const __bf16 *w1_h, *w1_l;        // [5][128][128]
+    const __bf16 *w2_h, *w2_l;        // [5][64][128] (rows past the head's outputs are zero)
+    const float* b_feat;
+    const float* b1[5];
+    const float* b2[5];
+    const float* in[5];               // means3D, scales, rotations, opacity, shs
+    float* out[5];
+};
+void launch_deform_fwd(const DeformArgs& a, hipStream_t st);
+void launch_pack_plane(const float* src, float* dst, int H, int W, hipStream_t st);
+void launch_pack_weight(const float* src, __bf16* hi, __bf16* lo, int rows, int rows_pad, int cols, hipStream_t st);
+
 void launch_preprocess(const PreprocessArgs& a, hipStream_t st);
 void launch_preprocess_bwd(const PreprocessBwdArgs& a, bool accumulate, hipStream_t st);
 void launch_reduce_lang(int P, int C, int cpad, int recq, const float* rec, const uint8_t* flags,

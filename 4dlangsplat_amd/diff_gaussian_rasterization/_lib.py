@@ -53,6 +53,15 @@ class BwdOut(ctypes.Structure):
 
 
 # every symbol include/lsr.h declares, with its ctypes signature
+class DeformNet(ctypes.Structure):
+    """include/lsr_deform.h lsr_deform_net"""
+    _fields_ = [("n_scales", ctypes.c_int32), ("channels", ctypes.c_int32), ("width", ctypes.c_int32),
+                ("res", ctypes.c_int32 * 4), ("multires", ctypes.c_int32 * 4), ("aabb", ctypes.c_void_p),
+                ("planes", (ctypes.c_void_p * 6) * 4), ("w_feat", ctypes.c_void_p), ("b_feat", ctypes.c_void_p),
+                ("w1", ctypes.c_void_p * 5), ("b1", ctypes.c_void_p * 5), ("w2", ctypes.c_void_p * 5),
+                ("b2", ctypes.c_void_p * 5)]
+
+
 SIGNATURES = {
     "lsr_version": (ctypes.c_int, []),
     "lsr_last_error": (ctypes.c_char_p, []),
@@ -71,6 +80,10 @@ SIGNATURES = {
     "lsr_mark_visible": (ctypes.c_int, [ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p]),
     "lsr_profile_enable": (ctypes.c_int, [ctypes.c_int32]),
+    "lsr_deform_workspace_bytes": (ctypes.c_int64, [ctypes.POINTER(DeformNet)]),
+    "lsr_deform_prepare": (ctypes.c_int, [ctypes.POINTER(DeformNet), ctypes.c_void_p, ctypes.c_void_p]),
+    "lsr_deform_forward": (ctypes.c_int, [ctypes.POINTER(DeformNet), ctypes.c_void_p, ctypes.c_int32]
+                           + [ctypes.c_void_p] * 11 + [ctypes.c_void_p]),
     "lsr_profile_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64),
                                         ctypes.c_int32]),
 }

@@ -1,5 +1,5 @@
 """CPU checks of the C ABI: liblsr.so builds for gfx950, loads, and exports exactly what
-include/lsr.h declares; the workspace size queries behave (no GPU compute is called here)."""
+include/*.h declare; the workspace size queries behave (no GPU compute is called here)."""
 import os
 import re
 import subprocess
@@ -7,11 +7,11 @@ import subprocess
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "lsr.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in sorted(os.listdir(os.path.join(ROOT, "include"))) if h.endswith(".h")]
 
 
 def declared():
-    txt = open(HEADER).read()
+    txt = "".join(open(h).read() for h in HEADERS)
     return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char \*)\s*(lsr_\w+)\s*\(", txt, re.M)))
 
 

@@ -1,0 +1,78 @@
+"""Deformation field forward on the GPU (csrc/deform.hip through include/lsr_deform.h) against
+the reference module's golden outputs and the float64 oracle (oracle/deform_oracle.py)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from deform_oracle import DeformOracle
+from deformation import DeformationField
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = ("means3D", "scales", "rotations", "opacity", "shs")
+
+
+def _rel(a, b):
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def _field(params, res, multires):
+    return DeformationField({k: torch.tensor(np.asarray(v, np.float32)) .cuda() for k, v in params.items()}, res, multires)
+
+
+def _run(field, inp, time):
+    out = field.forward(*[torch.tensor(np.asarray(inp[k], np.float32)).cuda() for k in KEYS],
+                        torch.zeros(inp["means3D"].shape[0], 3).cuda(),
+                        torch.tensor(np.asarray(time, np.float32)).cuda() if np.ndim(time) else float(time))
+    return {k: v.cpu().numpy() for k, v in zip(KEYS, out[:5])}
+
+
+def test_forward_matches_reference_golden():
+    z = np.load(os.path.join(ROOT, "tests", "golden", "deform_golden.npz"))
+    params = {k[len("param/"):]: z[k] for k in z.files if k.startswith("param/")}
+    params["grid.aabb"] = z["aabb"]
+    f = _field(params, list(z["res"]), list(z["multires"]))
+    out = _run(f, {k: z[k] for k in KEYS}, z["time"][:, 0])
+    for k in KEYS:
+        # deformed value = input + MLP offset: compare the offsets (what the kernel computes)
+        assert _rel(out[k] - z[k], z["out_" + k] - z[k]) < 2e-5, k
+
+
+def _neu3d_case(P, seed=0):
+    rng = np.random.default_rng(seed)
+    res, multires = [64, 64, 64, 150], [1, 2]
+    params = {}
+    for s, m in enumerate(multires):
+        rs = [r * m for r in res[:3]] + [res[3]]
+        for ci, (c0, c1) in enumerate([(0, 1), (0, 2), (0, 3), (1, 2), (1, 3), (2, 3)]):
+            params[f"grid.grids.{s}.{ci}"] = rng.uniform(0.1, 1.5, size=(1, 16, rs[c1], rs[c0]))
+    params["grid.aabb"] = np.array([[1.5, 1.2, 3.0], [-1.4, -1.1, 0.5]])
+    params["feature_out.0.weight"] = rng.normal(scale=0.2, size=(128, 32))
+    params["feature_out.0.bias"] = rng.normal(scale=0.05, size=128)
+    for name, n in zip(("pos_deform", "scales_deform", "rotations_deform", "opacity_deform", "shs_deform"),
+                       (3, 3, 4, 1, 48)):
+        params[name + ".1.weight"] = rng.normal(scale=0.1, size=(128, 128))
+        params[name + ".1.bias"] = rng.normal(scale=0.05, size=128)
+        params[name + ".3.weight"] = rng.normal(scale=0.1, size=(n, 128))
+        params[name + ".3.bias"] = rng.normal(scale=0.05, size=n)
+    params = {k: np.asarray(v, np.float32).astype(np.float64) for k, v in params.items()}
+    lo, hi = params["grid.aabb"][1], params["grid.aabb"][0]
+    inp = dict(means3D=rng.uniform(lo - 0.1, hi + 0.1, size=(P, 3)), scales=rng.normal(-4, 0.5, size=(P, 3)),
+               rotations=rng.normal(size=(P, 4)), opacity=rng.normal(size=(P, 1)),
+               shs=rng.normal(scale=0.3, size=(P, 16, 3)))
+    inp = {k: np.asarray(v, np.float32).astype(np.float64) for k, v in inp.items()}
+    return params, res, multires, inp
+
+
+@pytest.mark.parametrize("P,time", [(20000, 0.37), (777, -0.8)])
+def test_forward_matches_oracle_at_neu3d_resolution(P, time):
+    params, res, multires, inp = _neu3d_case(P)
+    f = _field(params, res, multires)
+    out = _run(f, inp, time)                      # scalar time (the render() path)
+    o = DeformOracle({k: v for k, v in params.items() if k != "grid.aabb"}, params["grid.aabb"])
+    ref = o.forward(inp["means3D"], inp["scales"], inp["rotations"], inp["opacity"], inp["shs"], None,
+                    np.full((P, 1), time))
+    for k in KEYS:
+        assert _rel(out[k] - inp[k], ref[k] - inp[k]) < 2e-5, k
