@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Deformation field forward throughput (csrc/deform.hip) at the Neu3D structure: P Gaussians,
+planes 64/64/64/150 x multires [1, 2] x 16 channels, width-128 MLP with five heads.
+Prints one JSON line: Gaussians/s, ms per call, and the matrix-core roofline of the MLP
+(useful fp32-equivalent flops; the bf16 hi/lo split issues 3 MFMAs per product)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "4dlangsplat_amd"))
+
+import torch  # noqa: E402
+
+from deformation import DeformationField, HEADS, HEAD_OUT  # noqa: E402
+
+BF16_DENSE_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: dense bf16 MFMA
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gaussians", type=int, default=2_000_000)
+    ap.add_argument("--iters", type=int, default=20)
+    args = ap.parse_args()
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(0)
+    res, multires = [64, 64, 64, 150], [1, 2]
+    params = {}
+    for s, m in enumerate(multires):
+        rs = [r * m for r in res[:3]] + [res[3]]
+        for ci, (c0, c1) in enumerate([(0, 1), (0, 2), (0, 3), (1, 2), (1, 3), (2, 3)]):
+            params[f"grid.grids.{s}.{ci}"] = torch.rand(1, 16, rs[c1], rs[c0], generator=g) * 1.4 + 0.1
+    params["grid.aabb"] = torch.tensor([[1.5, 1.2, 10.0], [-1.5, -1.2, 2.0]])
+    params["feature_out.0.weight"] = torch.randn(128, 32, generator=g) * 0.2
+    params["feature_out.0.bias"] = torch.randn(128, generator=g) * 0.05
+    for name, n in zip(HEADS, HEAD_OUT):
+        params[name + ".1.weight"] = torch.randn(128, 128, generator=g) * 0.1
+        params[name + ".1.bias"] = torch.randn(128, generator=g) * 0.05
+        params[name + ".3.weight"] = torch.randn(n, 128, generator=g) * 0.1
+        params[name + ".3.bias"] = torch.randn(n, generator=g) * 0.05
+    field = DeformationField({k: v.to(dev) for k, v in params.items()}, res, multires)
+    P = args.gaussians
+    means = (torch.rand(P, 3, generator=g) * torch.tensor([3.0, 2.4, 8.0]) + torch.tensor([-1.5, -1.2, 2.0])).to(dev)
+    ins = [means, torch.randn(P, 3, generator=g).to(dev), torch.randn(P, 4, generator=g).to(dev),
+           torch.randn(P, 1, generator=g).to(dev), torch.randn(P, 16, 3, generator=g).to(dev),
+           torch.zeros(P, 3, device=dev)]
+    for _ in range(3):
+        field.forward(*ins, 0.4)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(args.iters):
+        field.forward(*ins, 0.4)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / args.iters
+    macs = 32 * 128 + sum(128 * 128 + 128 * n for n in HEAD_OUT)   # per Gaussian
+    useful_tflops = 2.0 * macs * P / (ms * 1e-3) / 1e12
+    print(json.dumps(dict(metric="deformation forward Gaussians/s (Neu3D structure)", value=round(P / (ms * 1e-3)),
+                          unit="Gaussians/s", ms_per_call=round(ms, 4), gaussians=P,
+                          roofline=dict(bound="mfma", achieved=round(useful_tflops, 1), unit="TFLOP/s",
+                                        peak=BF16_DENSE_PEAK_TFLOPS / 3, note="useful fp32-equivalent flops vs "
+                                        "dense bf16 peak / 3 (hi/lo split: 3 MFMAs per product)",
+                                        frac=round(useful_tflops / (BF16_DENSE_PEAK_TFLOPS / 3), 4)))))
+
+
+if __name__ == "__main__":
+    main()

@@ -21,7 +21,7 @@ def short(name):
 
 # bench phase -> the one kernel it launches (non-deterministic backward)
 PHASE_KERNEL = {"preprocess": "k_preprocess", "emit": "k_emit", "tile_ranges": "k_tile_ranges",
-                "render_fwd": "k_render_fwd", "render_bwd": "k_render_bwd_mfma",
+                "render_fwd": "k_render_fwd_wave", "render_bwd": "k_render_bwd_wave",
                 "preprocess_bwd": "k_preprocess_bwd"}
 
 
