@@ -31,51 +31,55 @@ __device__ __forceinline__ void dsplit(float x, __bf16& hi, __bf16& lo) {
     lo = (__bf16)(x - (float)hi);
 }
 
-// Y[64 x 32*ntiles] (+)= X[64 x K] W^T for the N tiles `nt0 .. nt0 + NT - 1` of this wave's M tile.
-template <int K, int NT>
-__device__ __forceinline__ void mlp_tiles(df32x16 (&acc)[NT], const __bf16* __restrict__ xh, const __bf16* __restrict__ xl,
-                                          int xp, int mt, int nt0, const __bf16* __restrict__ wh,
-                                          const __bf16* __restrict__ wl) {
+// Y[64 x 32] (+)= X[64 x K] W^T for N tile `nt`: both M tiles (the block's 64 Gaussians) share
+// every weight fragment, so a block reads each weight once per layer.
+template <int K>
+__device__ __forceinline__ void mlp_ntile(df32x16 (&acc)[2], const __bf16* __restrict__ xh, const __bf16* __restrict__ xl,
+                                          int xp, int nt, const __bf16* __restrict__ wh, const __bf16* __restrict__ wl) {
     const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+    // every weight fragment of the tile in flight at once (L2-resident, one round trip)
+    dbf16x8 bh[K / 16], bl[K / 16];
+#pragma unroll
+    for (int ks = 0; ks < K / 16; ++ks) {
+        const size_t wo = (size_t)(32 * nt + r) * K + 16 * ks + 8 * h;
+        bh[ks] = *reinterpret_cast<const dbf16x8*>(wh + wo);
+        bl[ks] = *reinterpret_cast<const dbf16x8*>(wl + wo);
+    }
+    __builtin_amdgcn_sched_barrier(0);   // keep the loads issued here, ahead of the MFMAs
 #pragma unroll
     for (int ks = 0; ks < K / 16; ++ks) {
         const int k0 = 16 * ks + 8 * h;
-        const dbf16x8 ah = *reinterpret_cast<const dbf16x8*>(xh + (32 * mt + r) * xp + k0);
-        const dbf16x8 al = *reinterpret_cast<const dbf16x8*>(xl + (32 * mt + r) * xp + k0);
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const size_t wo = (size_t)(32 * (nt0 + t) + r) * K + k0;
-            const dbf16x8 bh = *reinterpret_cast<const dbf16x8*>(wh + wo);
-            const dbf16x8 bl = *reinterpret_cast<const dbf16x8*>(wl + wo);
-            acc[t] = DMFMA(ah, bh, acc[t]);
-            acc[t] = DMFMA(ah, bl, acc[t]);
-            acc[t] = DMFMA(al, bh, acc[t]);
+        for (int mt = 0; mt < 2; ++mt) {
+            const dbf16x8 ah = *reinterpret_cast<const dbf16x8*>(xh + (32 * mt + r) * xp + k0);
+            const dbf16x8 al = *reinterpret_cast<const dbf16x8*>(xl + (32 * mt + r) * xp + k0);
+            acc[mt] = DMFMA(ah, bh[ks], acc[mt]);
+            acc[mt] = DMFMA(ah, bl[ks], acc[mt]);
+            acc[mt] = DMFMA(al, bh[ks], acc[mt]);
         }
     }
 }
 
-// epilogue to LDS rows: relu(acc + bias) as bf16 hi/lo
-template <int NT>
-__device__ __forceinline__ void store_hidden(const df32x16 (&acc)[NT], int mt, int nt0, const float* __restrict__ bias,
+// epilogue to LDS rows: relu(acc + bias) as bf16 hi/lo, N tile `nt`, both M tiles
+__device__ __forceinline__ void store_hidden(const df32x16 (&acc)[2], int nt, const float* __restrict__ bias,
                                              __bf16* __restrict__ yh, __bf16* __restrict__ yl) {
     const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
+    const int col = 32 * nt + c;
+    const float b = bias[col];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        const int col = 32 * (nt0 + t) + c;
-        const float b = bias[col];
+    for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             const int row = 32 * mt + (q & 3) + 8 * (q >> 2) + 4 * h;
-            const float v = fmaxf(acc[t][q] + b, 0.0f);
+            const float v = fmaxf(acc[mt][q] + b, 0.0f);
             __bf16 hi, lo;
             dsplit(v, hi, lo);
             yh[row * DAP + col] = hi;
             yl[row * DAP + col] = lo;
         }
-    }
 }
 
-__global__ void __launch_bounds__(256) k_deform_fwd(DeformArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) k_deform_fwd(DeformArgs a) {
     __shared__ __attribute__((aligned(16))) __bf16 s_xh[DN * DXP];
     __shared__ __attribute__((aligned(16))) __bf16 s_xl[DN * DXP];
     __shared__ __attribute__((aligned(16))) __bf16 s_ah[DN * DAP];
@@ -93,8 +97,8 @@ __global__ void __launch_bounds__(256) k_deform_fwd(DeformArgs a) {
         // normalize_aabb: (p - aabb[0]) * (2 / (aabb[1] - aabb[0])) - 1, aabb = [xyz_max, xyz_min]
 #pragma unroll
         for (int c = 0; c < 3; ++c)
-            crd[c] = (a.means3D[3 * g + c] - a.aabb[c]) * (2.0f / (a.aabb[3 + c] - a.aabb[c])) - 1.0f;
-        crd[3] = a.time[g];
+            crd[c] = (__builtin_nontemporal_load(a.means3D + 3 * g + c) - a.aabb[c]) * (2.0f / (a.aabb[3 + c] - a.aabb[c])) - 1.0f;
+        crd[3] = __builtin_nontemporal_load(a.time + g);
         const int c0s[6] = {0, 0, 0, 1, 1, 2}, c1s[6] = {1, 2, 3, 2, 3, 3};
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
@@ -129,41 +133,51 @@ __global__ void __launch_bounds__(256) k_deform_fwd(DeformArgs a) {
     }
     __syncthreads();
 
-    // ---- stage 2: hidden = relu(feat W_f^T + b_f) ------------------------------------------------
-    const int mt = wave & 1, ntp = (wave >> 1) * 2;   // this wave: M tile mt, N tiles ntp, ntp + 1
+    // ---- stage 2: hidden = relu(feat W_f^T + b_f); wave w owns hidden columns 32 w .. 32 w + 31 ----
     {
         df32x16 acc[2] = {df32x16{}, df32x16{}};
-        mlp_tiles<DFEAT, 2>(acc, s_xh, s_xl, DXP, mt, ntp, a.wf_h, a.wf_l);
-        store_hidden<2>(acc, mt, ntp, a.b_feat, s_ah, s_al);
+        mlp_ntile<DFEAT>(acc, s_xh, s_xl, DXP, wave, a.wf_h, a.wf_l);
+        store_hidden(acc, wave, a.b_feat, s_ah, s_al);
     }
     __syncthreads();
 
     // ---- heads: out = in + (relu(hidden W1^T + b1) W2^T + b2) -------------------------------------
     for (int hd = 0; hd < 5; ++hd) {
+        const int nout = kHeadOut[hd];
+        const bool owner = wave < (nout + 31) / 32;     // 1 N tile, or 2 for the 48 SH coefficients
+        const int col = 32 * wave + (lane & 31), h = lane >> 5;
+        // the residual inputs of this wave's outputs, loaded now so the head's first layer hides
+        // their latency (streamed once: non-temporal, the weights and planes keep the L2)
+        float resid[2][16];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int g = g0 + 32 * mt + (q & 3) + 8 * (q >> 2) + 4 * h;
+                resid[mt][q] = (owner && col < nout && g < a.P)
+                                   ? __builtin_nontemporal_load(a.in[hd] + (size_t)g * nout + col) : 0.0f;
+            }
         {
             df32x16 acc[2] = {df32x16{}, df32x16{}};
-            mlp_tiles<DWID, 2>(acc, s_ah, s_al, DAP, mt, ntp, a.w1_h + (size_t)hd * DWID * DWID,
-                               a.w1_l + (size_t)hd * DWID * DWID);
-            store_hidden<2>(acc, mt, ntp, a.b1[hd], s_bh, s_bl);
+            mlp_ntile<DWID>(acc, s_ah, s_al, DAP, wave, a.w1_h + (size_t)hd * DWID * DWID,
+                            a.w1_l + (size_t)hd * DWID * DWID);
+            store_hidden(acc, wave, a.b1[hd], s_bh, s_bl);
         }
         __syncthreads();
-        const int nout = kHeadOut[hd];
-        const int ntiles = (nout + 31) / 32;           // 1, or 2 for the 48 SH coefficients
-        const int nt = wave >> 1;                      // waves 0,1: N tile 0; waves 2,3: N tile 1
-        if (nt < ntiles) {
-            df32x16 acc[1] = {df32x16{}};
-            mlp_tiles<DWID, 1>(acc, s_bh, s_bl, DAP, mt, nt, a.w2_h + (size_t)hd * DW2ROWS * DWID,
-                               a.w2_l + (size_t)hd * DW2ROWS * DWID);
-            const int col = 32 * nt + (lane & 31), h = lane >> 5;
+        if (owner) {
+            df32x16 acc[2] = {df32x16{}, df32x16{}};
+            mlp_ntile<DWID>(acc, s_bh, s_bl, DAP, wave, a.w2_h + (size_t)hd * DW2ROWS * DWID,
+                            a.w2_l + (size_t)hd * DW2ROWS * DWID);
             if (col < nout) {
                 const float b = a.b2[hd][col];
-                const float* in = a.in[hd];
                 float* out = a.out[hd];
 #pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    const int g = g0 + 32 * mt + (q & 3) + 8 * (q >> 2) + 4 * h;
-                    if (g < a.P) out[(size_t)g * nout + col] = in[(size_t)g * nout + col] + (acc[0][q] + b);
-                }
+                for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) {
+                        const int g = g0 + 32 * mt + (q & 3) + 8 * (q >> 2) + 4 * h;
+                        if (g < a.P) __builtin_nontemporal_store(resid[mt][q] + (acc[mt][q] + b), out + (size_t)g * nout + col);
+                    }
             }
         }
         __syncthreads();
