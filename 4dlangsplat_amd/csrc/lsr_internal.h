@@ -86,7 +86,7 @@ struct RenderBwdArgs {
     const float2* xy;
     const float4* conic_o;
     const float4* rgbd;
-    const int* radius;
+    const uint2* rect;        // binning rectangles (deterministic records are indexed within them)
     const uint32_t* inst_off;
     const float* lang;
     const float* bg;

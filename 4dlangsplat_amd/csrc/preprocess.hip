@@ -151,8 +151,27 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
     const float2 pix = make_float2(ndc2pix(pp.x, a.W), ndc2pix(pp.y, a.H));
     int2 rmin, rmax;
     tile_rect(pix, radius, a.grid_x, a.grid_y, rmin, rmax);
-    const int ntiles = (rmax.y - rmin.y) * (rmax.x - rmin.x);
-    if (ntiles == 0) return;
+    if ((rmax.y - rmin.y) * (rmax.x - rmin.x) == 0) return;   // upstream: culled (radius 0)
+    // Binning rectangle: upstream's 3-sigma square intersected with the bounding box of the ellipse
+    // where a pixel can pass the compositors' exact alpha prefilter (power >= skip_power(o), i.e.
+    // q(d) <= -2 skip_power(o)).  Every dropped (Gaussian, tile) would be skipped at every pixel of
+    // the tile, so the rendered result is unchanged; radii (user-visible) stay upstream's.  The
+    // margin covers the float evaluation of q at the pixels (terms bounded inside the square).
+    const float thr = skip_power(conic.w);
+    int ntiles = 0;
+    int2 cmin = make_int2(0, 0), cmax = make_int2(0, 0);
+    if (thr <= 0.0f) {
+        const float rr = (float)radius + 16.0f;
+        const float mt = (fabsf(conic.x) + fabsf(conic.z) + 2.0f * fabsf(conic.y)) * rr * rr;
+        const float qm = -2.0f * thr + 1e-6f * mt + 1e-4f;
+        const float hx = sqrtf(qm * ca) + 0.01f, hy = sqrtf(qm * cc) + 0.01f;
+        cmin.x = max(rmin.x, (int)floorf((pix.x - hx) / (float)LSR_TILE_X));
+        cmin.y = max(rmin.y, (int)floorf((pix.y - hy) / (float)LSR_TILE_Y));
+        cmax.x = min(rmax.x, (int)floorf((pix.x + hx) / (float)LSR_TILE_X) + 1);
+        cmax.y = min(rmax.y, (int)floorf((pix.y + hy) / (float)LSR_TILE_Y) + 1);
+        if (cmax.x > cmin.x && cmax.y > cmin.y) ntiles = (cmax.x - cmin.x) * (cmax.y - cmin.y);
+        else cmin = cmax = make_int2(0, 0);
+    }
 
     float rgb[3];
     if (a.colors_precomp) {
@@ -210,7 +229,7 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
     a.radii[i] = radius;
     a.radius[i] = radius;
     a.tiles[i] = (uint32_t)ntiles;
-    a.rect[i] = make_uint2((uint32_t)rmin.x | ((uint32_t)rmin.y << 16), (uint32_t)rmax.x | ((uint32_t)rmax.y << 16));
+    a.rect[i] = make_uint2((uint32_t)cmin.x | ((uint32_t)cmin.y << 16), (uint32_t)cmax.x | ((uint32_t)cmax.y << 16));
     a.key[i] = __float_as_uint(pv.z);
     a.xy[i] = pix;
     a.conic_o[i] = conic;

@@ -88,9 +88,9 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
             s_co[tid] = co;
             s_rgbd[tid] = a.rgbd[gid];
             s_thr[tid] = skip_power(co.w);
-            int2 rmin, rmax;
-            tile_rect(xy, a.radius[gid], a.grid_x, a.grid_y, rmin, rmax);
-            s_inst[tid] = a.inst_off[gid] + (uint32_t)((ty - rmin.y) * (rmax.x - rmin.x) + (tx - rmin.x));
+            const uint2 rc = a.rect[gid];   // the binning rectangle (preprocess), packed 16-bit
+            const int rx0 = (int)(rc.x & 0xFFFFu), ry0 = (int)(rc.x >> 16), rx1 = (int)(rc.y & 0xFFFFu);
+            s_inst[tid] = a.inst_off[gid] + (uint32_t)((ty - ry0) * (rx1 - rx0) + (tx - rx0));
             s_act[tid] = 0;
         }
         for (int e = tid; e < NSLOT * BATCH * RECQ; e += 256) s_rec[e] = 0.0f;

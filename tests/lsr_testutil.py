@@ -52,6 +52,47 @@ def decode_point_list(state):
     return raw[off:off + K * 4].view(np.uint32)
 
 
+def check_binning_against_upstream(state, ref_state, W, H):
+    """The native binning drops (Gaussian, tile) instances whose splat cannot pass the alpha
+    prefilter at any pixel of the tile (preprocess.hip, binning rectangle).  Checks, against the
+    oracle's upstream binning: every tile list is an ordered subsequence of upstream's; every dropped
+    entry has alpha < 1/255 at every pixel of its tile (so dropping it changes nothing); and each
+    pixel's last contributor (n_contrib, a list position) is the same Gaussian."""
+    ranges, _, fT, nc = decode_img(state)
+    pl = decode_point_list(state).astype(np.int64)
+    rr, rpl, rnc = ref_state["ranges"], ref_state["point_list"].astype(np.int64), ref_state["n_contrib"]
+    xy, co = ref_state["xy"].astype(np.float64), ref_state["conic_o"].astype(np.float64)
+    gx = (W + 15) // 16
+    assert ranges[:, 1].max(initial=0) <= len(pl) and len(pl) <= len(rpl)
+    dropped_total = 0
+    for t in range(len(ranges)):
+        g = pl[ranges[t, 0]:ranges[t, 1]]
+        u = rpl[rr[t, 0]:rr[t, 1]]
+        pos = {gid: k for k, gid in enumerate(u)}
+        idx = np.array([pos[gid] for gid in g], dtype=np.int64)       # KeyError: entry not upstream
+        assert (np.diff(idx) > 0).all(), f"tile {t}: order differs from upstream"
+        dropped = np.setdiff1d(u, g)
+        dropped_total += len(dropped)
+        tx, ty = t % gx, t // gx
+        px, py = np.meshgrid(np.arange(16 * tx, min(16 * tx + 16, W)), np.arange(16 * ty, min(16 * ty + 16, H)))
+        px, py = px.ravel().astype(np.float64), py.ravel().astype(np.float64)
+        if len(dropped):
+            dx = xy[dropped, 0][:, None] - px[None]
+            dy = xy[dropped, 1][:, None] - py[None]
+            a, b, c, o = (co[dropped, k][:, None] for k in range(4))
+            power = -0.5 * (a * dx * dx + c * dy * dy) - b * dx * dy
+            alpha = np.minimum(0.99, o * np.exp(np.minimum(power, 0.0)))
+            assert (alpha < (1.0 / 255.0) * (1 - 1e-6)).all(), f"tile {t}: a dropped entry contributes"
+        # last contributor of each pixel of the tile: the same Gaussian
+        for yy, xx in zip(py.astype(int), px.astype(int)):
+            n, rn = int(nc[yy, xx]), int(rnc[yy, xx])
+            assert (n == 0) == (rn == 0), (t, yy, xx)
+            if n:
+                assert g[n - 1] == u[rn - 1], (t, yy, xx)
+    np.testing.assert_array_equal(fT, ref_state["final_T"])
+    return dropped_total
+
+
 def run_native(scene, cam, bg=(1.0, 1.0, 1.0), include_feature=True, use_precomp_cov=False, colors_precomp=None,
                sh_degree=3):
     dev = "cuda"

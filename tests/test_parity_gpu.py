@@ -2,8 +2,11 @@
 
 Forward contract (north star): RGB within 1e-4, language features within 1e-3 of the reference.
 Against the oracle the preprocess and the contributor decisions are bit-exact (same IEEE
-operation order, reproducible exp), so radii, tile lists, final_T and n_contrib are compared
-exactly; channel sums differ only by FMA rounding.  Gradients are compared relative to the
+operation order, reproducible exp), so radii and final_T are compared exactly.  The native
+binning drops instances that cannot contribute to their tile; the tile lists are checked to be
+ordered subsequences of upstream's with every dropped entry provably inactive, and every pixel's
+last contributor is the same Gaussian (check_binning_against_upstream).  Channel sums differ only
+by FMA rounding.  Gradients are compared relative to the
 largest magnitude of each tensor (float atomics + a different summation order), 1e-4.
 """
 import math
@@ -20,8 +23,8 @@ if not torch.cuda.is_available():  # CPU container: the driver only runs these o
 import diff_gaussian_rasterization as dgr  # noqa: E402
 import synthetic  # noqa: E402
 from helpers import axis_camera, small_case  # noqa: E402
-from lsr_testutil import (decode_img, decode_point_list, grad_err, raster_settings, run_native,  # noqa: E402
-                          run_oracle)
+from lsr_testutil import (check_binning_against_upstream, decode_img, decode_point_list, grad_err,  # noqa: E402
+                          raster_settings, run_native, run_oracle)
 
 RGB_TOL, LANG_TOL = 1e-4, 1e-3
 GRAD_TOL = 1e-4
@@ -30,14 +33,11 @@ GRAD_TOL = 1e-4
 def _assert_forward(nat, ref, C, exact_state=True):
     color, lang, radii, depth, st = nat
     np.testing.assert_array_equal(radii.cpu().numpy(), ref.radii)
-    assert st.num_rendered == ref.num_rendered
+    assert st.num_rendered <= ref.num_rendered
     rs = ref.state()
     if exact_state:
-        ranges, tmax, fT, nc = decode_img(st)
-        np.testing.assert_array_equal(ranges, rs["ranges"])
-        np.testing.assert_array_equal(nc, rs["n_contrib"])
-        np.testing.assert_array_equal(fT, rs["final_T"])
-        np.testing.assert_array_equal(decode_point_list(st), rs["point_list"])
+        H, W = color.shape[1], color.shape[2]
+        check_binning_against_upstream(st, rs, W, H)
     assert np.abs(color.cpu().numpy() - ref.color).max() <= RGB_TOL
     if C > 0:
         assert np.abs(lang.cpu().numpy() - ref.lang).max() <= LANG_TOL
@@ -203,7 +203,7 @@ def test_headline_properties_2m():
     vis = radii.cpu().numpy() > 0
     assert 1_500_000 < vis.sum() < 1_950_000
     K = st.num_rendered
-    assert 6_000_000 < K < 12_000_000
+    assert 4_000_000 < K < 12_000_000        # after dropping instances that cannot contribute
     # ranges tile the list in order
     nz = ranges[:, 1] > ranges[:, 0]
     assert ranges[nz, 1].sum() - ranges[nz, 0].sum() == K
