@@ -378,11 +378,12 @@ int lsr_backward(const lsr_settings* s, const lsr_fwd_in* in, const lsr_bwd_in* 
         LSR_HIP(hipMemsetAsync(sc.flags, 0, K, st));
         lsr::launch_scatter_inst_off(P, g.val_a, g.offsets, g.counts, g.inst_off, st);
     }
-    if (!det) {
-        LSR_HIP(hipMemsetAsync(sc.acc_small, 0, sizeof(float) * 12 * (size_t)P, st));
-        if (!accumulate && Ceff > 0 && gout->dL_dlanguage_feature)
-            LSR_HIP(hipMemsetAsync(gout->dL_dlanguage_feature, 0, sizeof(float) * (size_t)P * C, st));
-    }
+    if (!det) LSR_HIP(hipMemsetAsync(sc.acc_small, 0, sizeof(float) * 12 * (size_t)P, st));
+    // dL/dlanguage: the atomic path adds into it, so zero it unless accumulating; with the language
+    // channels off (include_feature = 0) it is exactly zero (the deterministic path writes it only
+    // when they are on)
+    if (!accumulate && C > 0 && gout->dL_dlanguage_feature && (!det || Ceff == 0))
+        LSR_HIP(hipMemsetAsync(gout->dL_dlanguage_feature, 0, sizeof(float) * (size_t)P * C, st));
     const uint32_t* point_list = tile_sort_in_b(gx * gy) ? b.val_b : b.val_a;
     if (K > 0) {
         lsr::RenderBwdArgs r{};

@@ -220,19 +220,16 @@ static void go_bwd(const RenderBwdArgs& a, hipStream_t st) {
 
 void launch_render_bwd(const RenderBwdArgs& a, hipStream_t st) {
     const int C = a.include_feature ? a.C : 0;
-    switch (lang_pad(C)) {
+    if (!a.deterministic && C <= 32) {
+        launch_render_bwd_wave(a, st);   // compacted per-quadrant waves, pixel sums on matrix cores
+        return;
+    }
+    switch (lang_pad(C)) {               // deterministic records, or 64 channels
         case 0: go_bwd<0, 64, 16>(a, st); break;
         case 4: go_bwd<4, 64, 16>(a, st); break;
         case 8: go_bwd<8, 64, 32>(a, st); break;
         case 16: go_bwd<16, 64, 32>(a, st); break;
-        case 32:
-            if (a.deterministic) go_bwd<32, 64, 64>(a, st);
-#ifdef LSR_BWD_BLOCK_MFMA
-            else launch_render_bwd_mfma(a, st);
-#else
-            else launch_render_bwd_wave(a, st);   // compacted per-quadrant waves, language on matrix cores
-#endif
-            break;
+        case 32: go_bwd<32, 64, 64>(a, st); break;
         default: go_bwd<64, 32, 128>(a, st); break;
     }
 }

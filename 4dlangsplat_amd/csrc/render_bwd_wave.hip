@@ -61,7 +61,7 @@ k_render_bwd_wave(RenderBwdArgs a) {
     nrep = __builtin_amdgcn_readfirstlane(nrep);
     if (nrep == 0) return;                                           // wave-uniform
     const uint2 range = a.ranges[tile];
-    const int C = a.C;
+    const int C = a.include_feature ? a.C : 0;   // language channels in play
     const float bx0 = (float)qx0, bx1 = (float)min(qx0 + 7, a.W - 1);
     const float by0 = (float)qy0, by1 = (float)min(qy0 + 7, a.H - 1);
 

@@ -77,6 +77,18 @@ def test_include_feature_false_writes_zero_language():
     ref = run_oracle(sc, cam, include_feature=False)
     assert lang.shape == (6, 64, 64) and float(lang.abs().max()) == 0.0
     assert np.abs(color.cpu().numpy() - ref.color).max() <= RGB_TOL
+    # backward: language channels off -> exactly zero language gradient (buffer pre-filled), both modes
+    rng = np.random.default_rng(4)
+    gc = rng.normal(size=(3, 64, 64)).astype(np.float32)
+    gl = rng.normal(size=(6, 64, 64)).astype(np.float32)
+    rg = ref.backward(gc, gl, None)
+    for det in (False, True):
+        out = dict(language_feature=torch.full((1000, 6), 7.0, device="cuda"))
+        g = dgr.backward_native(st, torch.tensor(gc, device="cuda"), torch.tensor(gl, device="cuda"), None, out=out,
+                                deterministic=det)
+        assert float(g["language_feature"].abs().max()) == 0.0, det
+        assert grad_err(g["means3D"].cpu().numpy(), rg["means3D"]) < GRAD_TOL, det
+        assert grad_err(g["opacities"].cpu().numpy(), rg["opacity"]) < GRAD_TOL, det
 
 
 def test_empty_and_all_culled():
