@@ -301,23 +301,19 @@ int lsr_forward_preprocess(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_
     return LSR_OK;
 }
 
-int lsr_forward_render(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_out* out, void* geom, void* binning,
-                       void* img, int64_t num_rendered, lsr_stream_t stream) {
+int lsr_forward_binning(const lsr_settings* s, const lsr_fwd_in* in, void* geom, void* binning, void* img,
+                        int64_t num_rendered, lsr_stream_t stream) {
     int rc = check_common(s, in);
     if (rc) return rc;
-    if (!out || !out->out_color || !out->out_depth) return fail(LSR_EINVAL, "color and depth outputs are required");
-    if (in->C > 0 && !out->out_language_feature) return fail(LSR_EINVAL, "language feature output is required when C > 0");
     if (!geom || !img || (num_rendered > 0 && !binning)) return fail(LSR_EINVAL, "workspaces are required");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const int P = in->P, W = s->image_width, H = s->image_height, C = in->C;
+    const int P = in->P, W = s->image_width, H = s->image_height;
     const int gx = (W + LSR_TILE_X - 1) / LSR_TILE_X, gy = (H + LSR_TILE_Y - 1) / LSR_TILE_Y;
     const size_t K = (size_t)num_rendered;
     Geom g = carve_geom(geom, (size_t)(P > 0 ? P : 1), nullptr);
     Binning b = carve_binning(binning, K > 0 ? K : 1, nullptr);
     Img m = carve_img(img, W, H, nullptr);
     LSR_HIP(hipMemsetAsync(m.ranges, 0, sizeof(uint2) * (size_t)gx * gy, st));
-    LSR_HIP(hipMemsetAsync(m.tile_max, 0, sizeof(uint32_t) * (size_t)gx * gy, st));
-    const uint32_t* point_list = nullptr;
     if (K > 0) {
         {
             PhaseTimer t(LSR_PHASE_EMIT, st);
@@ -330,8 +326,8 @@ int lsr_forward_render(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_out*
             in_b = lsr::radix_sort_pairs(b.key_a, b.val_a, b.key_b, b.val_b, K, 0, tile_bits(gx * gy), b.sort_tmp,
                                          nullptr, st);
         }
+        if (in_b != tile_sort_in_b(gx * gy)) return fail(LSR_EHIP, "internal: tile sort parity");
         const uint32_t* keys = in_b ? b.key_b : b.key_a;
-        point_list = in_b ? b.val_b : b.val_a;
         LSR_LAUNCHED("tile sort", st, s->debug);
         {
             PhaseTimer t(LSR_PHASE_TILE_RANGES, st);
@@ -339,6 +335,25 @@ int lsr_forward_render(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_out*
         }
         LSR_LAUNCHED("tile ranges", st, s->debug);
     }
+    return LSR_OK;
+}
+
+int lsr_forward_composite(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_out* out, const void* geom,
+                          const void* binning, void* img, int64_t num_rendered, lsr_stream_t stream) {
+    int rc = check_common(s, in);
+    if (rc) return rc;
+    if (!out || !out->out_color || !out->out_depth) return fail(LSR_EINVAL, "color and depth outputs are required");
+    if (in->C > 0 && !out->out_language_feature) return fail(LSR_EINVAL, "language feature output is required when C > 0");
+    if (!geom || !img || (num_rendered > 0 && !binning)) return fail(LSR_EINVAL, "workspaces are required");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int P = in->P, W = s->image_width, H = s->image_height, C = in->C;
+    const int gx = (W + LSR_TILE_X - 1) / LSR_TILE_X, gy = (H + LSR_TILE_Y - 1) / LSR_TILE_Y;
+    const size_t K = (size_t)num_rendered;
+    Geom g = carve_geom(const_cast<void*>(geom), (size_t)(P > 0 ? P : 1), nullptr);
+    Binning b = carve_binning(const_cast<void*>(binning), K > 0 ? K : 1, nullptr);
+    Img m = carve_img(img, W, H, nullptr);
+    LSR_HIP(hipMemsetAsync(m.tile_max, 0, sizeof(uint32_t) * (size_t)gx * gy, st));
+    const uint32_t* point_list = K > 0 ? (tile_sort_in_b(gx * gy) ? b.val_b : b.val_a) : nullptr;
     lsr::RenderFwdArgs r{};
     r.W = W; r.H = H; r.grid_x = gx; r.grid_y = gy; r.C = C; r.include_feature = s->include_feature;
     r.ranges = m.ranges; r.point_list = point_list; r.xy = g.xy; r.conic_o = g.conic_o; r.rgbd = g.rgbd;
@@ -353,6 +368,14 @@ int lsr_forward_render(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_out*
     }
     LSR_LAUNCHED("render forward", st, s->debug);
     return LSR_OK;
+}
+
+int lsr_forward_render(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_out* out, void* geom, void* binning,
+                       void* img, int64_t num_rendered, lsr_stream_t stream) {
+    if (!out || !out->out_color || !out->out_depth) return fail(LSR_EINVAL, "color and depth outputs are required");
+    int rc = lsr_forward_binning(s, in, geom, binning, img, num_rendered, stream);
+    if (rc) return rc;
+    return lsr_forward_composite(s, in, out, geom, binning, img, num_rendered, stream);
 }
 
 int lsr_backward(const lsr_settings* s, const lsr_fwd_in* in, const lsr_bwd_in* gin, lsr_bwd_out* gout,

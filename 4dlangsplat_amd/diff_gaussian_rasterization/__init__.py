@@ -31,6 +31,7 @@ __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gau
            "forward_native", "backward_native"]
 
 _lib.load()   # fail loudly at import if the native library is missing
+_BINNING_DELAY_CYCLES = 0   # tests only: GPU cycles slept on the stream before a side-stream binning
 
 
 class GaussianRasterizationSettings(NamedTuple):
@@ -105,6 +106,8 @@ class PendingForward:
     def __init__(self, raster_settings, settings, fin, inputs, geom, radii, K, device, H, W):
         self.raster_settings, self.settings, self.fin, self.inputs = raster_settings, settings, fin, inputs
         self.geom, self.radii, self.num_rendered, self.device, self.H, self.W = geom, radii, K, device, H, W
+        self.binning = self.img = None     # set when the binning already ran (preprocess_native(binning=True))
+        self.ready = None                  # event recorded after that binning
 
 
 def _dump_forward(raster_settings, inputs):
@@ -116,10 +119,12 @@ def _dump_forward(raster_settings, inputs):
 
 
 def preprocess_native(raster_settings, means3D, opacities, shs=None, colors_precomp=None, language_feature=None,
-                      scales=None, rotations=None, cov3D_precomp=None, stream=None):
+                      scales=None, rotations=None, cov3D_precomp=None, stream=None, binning=False):
     """Forward phase 1 through liblsr.so (lsr_forward_preprocess) on `stream` (a torch stream,
     default: the current one).  Synchronises that stream once to read num_rendered (as upstream).
-    Workspaces are allocated on `stream`; render_native may run on another stream."""
+    binning=True also runs the tile binning there (lsr_forward_binning), so that render_native
+    only composites.  Workspaces are allocated on `stream`; render_native may run on another
+    stream."""
     device = means3D.device
     if device.type != "cuda":
         raise RuntimeError("the rasterizer runs on the GPU only (no CPU fallback); got tensors on " + str(device))
@@ -162,12 +167,30 @@ def preprocess_native(raster_settings, means3D, opacities, shs=None, colors_prec
     except RuntimeError:
         _dump_forward(raster_settings, inputs)
         raise
-    return PendingForward(raster_settings, st, fin, inputs, geom, radii, K.value, device, H, W)
+    pf = PendingForward(raster_settings, st, fin, inputs, geom, radii, K.value, device, H, W)
+    if binning:
+        if _BINNING_DELAY_CYCLES:         # test hook: holds the binning back to expose missing waits
+            with torch.cuda.stream(stream):
+                torch.cuda._sleep(_BINNING_DELAY_CYCLES)
+        with torch.cuda.stream(stream):
+            pf.binning = torch.empty(int(L.lsr_binning_bytes(K.value)), dtype=torch.uint8, device=device)
+            pf.img = torch.empty(int(L.lsr_img_bytes(W, H)), dtype=torch.uint8, device=device)
+        try:
+            _lib.check(L.lsr_forward_binning(ctypes.byref(st.c), ctypes.byref(fin), ctypes.c_void_p(geom.data_ptr()),
+                                             ctypes.c_void_p(pf.binning.data_ptr()), ctypes.c_void_p(pf.img.data_ptr()),
+                                             ctypes.c_int64(K.value), ctypes.c_void_p(stream.cuda_stream)),
+                       "lsr_forward_binning")
+        except RuntimeError:
+            _dump_forward(raster_settings, inputs)
+            raise
+        pf.ready = torch.cuda.Event()
+        pf.ready.record(stream)           # render_native's stream waits for the binning
+    return pf
 
 
 def render_native(pending: PendingForward):
-    """Forward phase 2 (binning, compositing) on the current stream.  Returns (color,
-    language_feature, radii, depth, state)."""
+    """Forward phase 2 (binning unless preprocess_native already did it, then compositing) on the
+    current stream.  Returns (color, language_feature, radii, depth, state)."""
     L = _lib.load()
     device, H, W, C = pending.device, pending.H, pending.W, pending.fin.C
     stream = torch.cuda.current_stream(device)
@@ -180,13 +203,21 @@ def render_native(pending: PendingForward):
     fout.out_color, fout.out_language_feature = color.data_ptr(), _ptr(lang_out) if C > 0 else None
     fout.radii, fout.out_depth = pending.radii.data_ptr(), depth.data_ptr()
     K = pending.num_rendered
-    binning = torch.empty(int(L.lsr_binning_bytes(K)), dtype=torch.uint8, device=device)
-    img = torch.empty(int(L.lsr_img_bytes(W, H)), dtype=torch.uint8, device=device)
+    binned = pending.binning is not None
+    if binned:
+        binning, img = pending.binning, pending.img
+        stream.wait_event(pending.ready)
+        binning.record_stream(stream)
+        img.record_stream(stream)
+    else:
+        binning = torch.empty(int(L.lsr_binning_bytes(K)), dtype=torch.uint8, device=device)
+        img = torch.empty(int(L.lsr_img_bytes(W, H)), dtype=torch.uint8, device=device)
+    fn, what = (L.lsr_forward_composite, "lsr_forward_composite") if binned else (L.lsr_forward_render,
+                                                                                   "lsr_forward_render")
     try:
-        _lib.check(L.lsr_forward_render(ctypes.byref(pending.settings.c), ctypes.byref(pending.fin), ctypes.byref(fout),
-                                        ctypes.c_void_p(pending.geom.data_ptr()), ctypes.c_void_p(binning.data_ptr()),
-                                        ctypes.c_void_p(img.data_ptr()), ctypes.c_int64(K), _stream(device)),
-                   "lsr_forward_render")
+        _lib.check(fn(ctypes.byref(pending.settings.c), ctypes.byref(pending.fin), ctypes.byref(fout),
+                      ctypes.c_void_p(pending.geom.data_ptr()), ctypes.c_void_p(binning.data_ptr()),
+                      ctypes.c_void_p(img.data_ptr()), ctypes.c_int64(K), _stream(device)), what)
     except RuntimeError:
         _dump_forward(pending.raster_settings, pending.inputs)
         raise

@@ -129,9 +129,10 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
 
     overlap=True pipelines the views: once view v's render and backward are enqueued, view v+1's
     preprocess (its depth order and instance count, the one host synchronisation of a forward)
-    runs on a side stream, concurrently with them, so the device never waits for the host
-    between views.  Results are identical to the sequential order (the preprocess only reads the
-    Gaussians and writes its own workspace)."""
+    and its tile binning run on a side stream, concurrently with them, so the device never waits
+    for the host between views and the main stream only composites.  Results are identical to
+    the sequential order (preprocess and binning only read the Gaussians and write their own
+    workspaces)."""
     import diff_gaussian_rasterization as dgr
 
     side = torch.cuda.Stream(device=scene.means3D.device) if overlap else None
@@ -144,7 +145,7 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
     def preprocess(v, stream=None):
         return dgr.preprocess_native(settings[v], scene.means3D, scene.opacities, shs=scene.shs,
                                      language_feature=scene.lang, scales=scene.scales, rotations=scene.rotations,
-                                     stream=stream)
+                                     stream=stream, binning=stream is not None)
 
     def render_view(v: int, bucket: GradBucket):
         pf = pending.pop(v, None)

@@ -124,6 +124,16 @@ int lsr_forward_preprocess(const lsr_settings *s, const lsr_fwd_in *in, lsr_fwd_
 int lsr_forward_render(const lsr_settings *s, const lsr_fwd_in *in, lsr_fwd_out *out, void *geom,
                        void *binning, void *img, int64_t num_rendered, lsr_stream_t stream);
 
+/* lsr_forward_render in two halves, so that the binning of one view can run on a side stream
+ * while another view composites (lsr_forward_render == binning then composite on one stream).
+ * Binning: instance emission, stable tile sort, per-tile ranges (fills `binning`, and the tile
+ * ranges in `img`).  Composite: front-to-back compositing of the binned lists (fills `out` and the
+ * rest of `img`).  Neither synchronises the host. */
+int lsr_forward_binning(const lsr_settings *s, const lsr_fwd_in *in, void *geom, void *binning, void *img,
+                        int64_t num_rendered, lsr_stream_t stream);
+int lsr_forward_composite(const lsr_settings *s, const lsr_fwd_in *in, lsr_fwd_out *out, const void *geom,
+                          const void *binning, void *img, int64_t num_rendered, lsr_stream_t stream);
+
 /* Backward through compositing and preprocess.  accumulate != 0 adds into the outputs instead of
  * overwriting them (multi-view gradient accumulation).  `scratch` holds >= lsr_backward_bytes. */
 int lsr_backward(const lsr_settings *s, const lsr_fwd_in *in, const lsr_bwd_in *gin, lsr_bwd_out *gout,

@@ -44,6 +44,16 @@ def test_pipelined_step_equals_sequential():
     assert float(f0.abs().sum()) > 0 and int((r0 > 0).sum()) > 0
 
 
+def test_pipelined_step_waits_for_side_stream_binning(monkeypatch):
+    """The side stream's binning is held back (about 20 ms per view) so that the main stream would
+    composite unfinished lists if it did not wait for it."""
+    sc, settings, grads = _setup(n_views=3)
+    f0, r0 = _run(sc, settings, grads, overlap=False, deterministic=True)
+    monkeypatch.setattr(dgr, "_BINNING_DELAY_CYCLES", 40_000_000)
+    f1, r1 = _run(sc, settings, grads, overlap=True, deterministic=True)
+    assert torch.equal(f0, f1) and torch.equal(r0, r1)
+
+
 def test_bucket_is_sum_of_views():
     sc, settings, grads = _setup(n_views=3)
     flat, radii = _run(sc, settings, grads, overlap=True, deterministic=False)
