@@ -184,14 +184,13 @@ Scratch carve_scratch(void* base, size_t P, size_t K, int recq, bool det, size_t
     return s;
 }
 
-int depth_sort_result_in_b() { return 0; }  // 32 key bits = 4 passes: result back in the (a) buffers
-
 int tile_bits(int ntiles) {
     int b = 1;
     while ((1 << b) < ntiles) ++b;
     return b;
 }
 bool tile_sort_in_b(int ntiles) { return ((tile_bits(ntiles) + 7) / 8) % 2 == 1; }
+int depth_sort_result_in_b() { return 0; }  // 32 key bits = 4 passes: result back in the (a) buffers
 
 int check_common(const lsr_settings* s, const lsr_fwd_in* in) {
     if (!s || !in) return fail(LSR_EINVAL, "null settings or inputs");
@@ -449,6 +448,124 @@ int lsr_backward(const lsr_settings* s, const lsr_fwd_in* in, const lsr_bwd_in* 
     }
     LSR_LAUNCHED("preprocess backward", st, s->debug);
     return LSR_OK;
+}
+
+int lsr_backward_composite(const lsr_settings* s, const lsr_fwd_in* in, const lsr_bwd_in* gin, float* dL_dlanguage,
+                           const void* geom, const void* binning, const void* img, void* scratch,
+                           int64_t num_rendered, lsr_stream_t stream) {
+    int rc = check_common(s, in);
+    if (rc) return rc;
+    if (!gin || !gin->dL_dout_color) return fail(LSR_EINVAL, "dL_dout_color is required");
+    if (gin->deterministic)
+        return fail(LSR_EINVAL, "the split backward reduces with float atomics; use lsr_backward for deterministic "
+                                "gradients");
+    if (!geom || !img || !scratch || (num_rendered > 0 && !binning)) return fail(LSR_EINVAL, "workspaces are required");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int P = in->P, C = in->C, W = s->image_width, H = s->image_height;
+    if (P == 0) return LSR_OK;
+    const int gx = (W + LSR_TILE_X - 1) / LSR_TILE_X, gy = (H + LSR_TILE_Y - 1) / LSR_TILE_Y;
+    const size_t K = (size_t)num_rendered;
+    Geom g = carve_geom(const_cast<void*>(geom), (size_t)P, nullptr);
+    Binning b = carve_binning(const_cast<void*>(binning), K > 0 ? K : 1, nullptr);
+    Img m = carve_img(const_cast<void*>(img), W, H, nullptr);
+    const int recq = lsr::record_floats(s->include_feature ? C : 0);
+    Scratch sc = carve_scratch(scratch, (size_t)P, K > 0 ? K : 1, recq, false, nullptr);
+    LSR_HIP(hipMemsetAsync(sc.acc_small, 0, sizeof(float) * 12 * (size_t)P, st));
+    if (K == 0) return LSR_OK;
+    lsr::RenderBwdArgs r{};
+    r.W = W; r.H = H; r.grid_x = gx; r.grid_y = gy; r.C = C; r.include_feature = s->include_feature;
+    r.ranges = m.ranges; r.point_list = tile_sort_in_b(gx * gy) ? b.val_b : b.val_a;
+    r.xy = g.xy; r.conic_o = g.conic_o; r.rgbd = g.rgbd;
+    r.rect = g.rect; r.inst_off = g.inst_off;
+    r.lang = in->language_feature; r.bg = s->bg; r.final_T = m.final_T; r.n_contrib = m.n_contrib;
+    r.tile_max_contrib = m.tile_max;
+    r.dL_dcolor = gin->dL_dout_color; r.dL_dlang = gin->dL_dout_language_feature; r.dL_ddepth = gin->dL_dout_depth;
+    r.recq = recq; r.deterministic = 0;
+    r.acc_small = sc.acc_small; r.acc_lang = dL_dlanguage;
+    {
+        PhaseTimer t(LSR_PHASE_RENDER_BWD, st);
+        lsr::launch_render_bwd(r, st);
+    }
+    LSR_LAUNCHED("render backward", st, s->debug);
+    return LSR_OK;
+}
+
+int lsr_backward_preprocess_views(int32_t n_views, const lsr_settings* const* s, const lsr_fwd_in* in,
+                                  lsr_bwd_out* gout, const void* const* geom, const void* const* scratch,
+                                  const int64_t* num_rendered, int32_t accumulate, lsr_stream_t stream) {
+    if (n_views < 1) return fail(LSR_EINVAL, "n_views must be >= 1");
+    if (!s || !in || !gout || !geom || !scratch || !num_rendered) return fail(LSR_EINVAL, "null argument");
+    for (int v = 0; v < n_views; ++v) {
+        int rc = check_common(s[v], in);
+        if (rc) return rc;
+        if (!geom[v] || !scratch[v]) return fail(LSR_EINVAL, "workspaces are required for every view");
+        if (s[v]->scale_modifier != s[0]->scale_modifier) return fail(LSR_EINVAL, "all views must share scale_modifier");
+    }
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int P = in->P;
+    if (P == 0) return LSR_OK;
+    // one launch per LSR_MAX_VIEWS views: Gaussian rows read and gradient rows written once
+    for (int v0 = 0; v0 < n_views; v0 += lsr::LSR_MAX_VIEWS) {
+        const int nv = std::min(lsr::LSR_MAX_VIEWS, n_views - v0);
+        lsr::PreprocessBwdViewsArgs a{};
+        a.P = P; a.M = in->M; a.nv = nv; a.scale_modifier = s[0]->scale_modifier;
+        a.means3D = in->means3D; a.scales = in->scales; a.rotations = in->rotations; a.shs = in->shs;
+        a.cov3D_precomp = in->cov3D_precomp;
+        for (int j = 0; j < nv; ++j) {
+            const int v = v0 + j;
+            const lsr_settings* sv = s[v];
+            const size_t K = (size_t)num_rendered[v];
+            Geom g = carve_geom(const_cast<void*>(geom[v]), (size_t)P, nullptr);
+            Scratch sc = carve_scratch(const_cast<void*>(scratch[v]), (size_t)P, K > 0 ? K : 1,
+                                       lsr::record_floats(sv->include_feature ? in->C : 0), false, nullptr);
+            lsr::ViewCam& c = a.cam[j];
+            c.view = sv->viewmatrix; c.proj = sv->projmatrix; c.campos = sv->campos;
+            c.tanfovx = sv->tanfovx; c.tanfovy = sv->tanfovy;
+            c.focal_x = (float)sv->image_width / (2.0f * sv->tanfovx);
+            c.focal_y = (float)sv->image_height / (2.0f * sv->tanfovy);
+            c.deg = sv->sh_degree;
+            c.tiles = g.tiles; c.clamped = g.clamped; c.acc_small = sc.acc_small;
+        }
+        a.dopacity = gout->dL_dopacity;
+        a.dmeans3D = gout->dL_dmeans3D; a.dmeans2D = gout->dL_dmeans2D; a.dcolors = gout->dL_dcolors;
+        a.dcov3D = gout->dL_dcov3D; a.dsh = in->shs ? gout->dL_dsh : nullptr; a.dscales = gout->dL_dscales;
+        a.drots = gout->dL_drotations;
+        {
+            PhaseTimer t(LSR_PHASE_PREPROCESS_BWD_VIEWS, st);
+            lsr::launch_preprocess_bwd_views(a, accumulate != 0 || v0 > 0, st);
+        }
+        LSR_LAUNCHED("preprocess backward (views)", st, s[0]->debug);
+    }
+    return LSR_OK;
+}
+
+int lsr_backward_views(int32_t n_views, const lsr_settings* const* s, const lsr_fwd_in* in,
+                       const lsr_bwd_in* const* gin, lsr_bwd_out* gout, const void* const* geom,
+                       const void* const* binning, const void* const* img, void* const* scratch,
+                       const int64_t* num_rendered, int32_t accumulate, lsr_stream_t stream) {
+    if (n_views < 1) return fail(LSR_EINVAL, "n_views must be >= 1");
+    if (!s || !in || !gin || !gout || !geom || !binning || !img || !scratch || !num_rendered)
+        return fail(LSR_EINVAL, "null argument");
+    for (int v = 0; v < n_views; ++v) {   // validate every view before anything is launched
+        int rc = check_common(s[v], in);
+        if (rc) return rc;
+        if (!gin[v] || !gin[v]->dL_dout_color) return fail(LSR_EINVAL, "dL_dout_color is required for every view");
+        if (gin[v]->deterministic)
+            return fail(LSR_EINVAL, "lsr_backward_views reduces with float atomics; use lsr_backward per view for "
+                                    "deterministic gradients");
+        if (s[v]->scale_modifier != s[0]->scale_modifier) return fail(LSR_EINVAL, "all views must share scale_modifier");
+    }
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int P = in->P, C = in->C;
+    if (P == 0) return LSR_OK;
+    if (!accumulate && C > 0 && gout->dL_dlanguage_feature)
+        LSR_HIP(hipMemsetAsync(gout->dL_dlanguage_feature, 0, sizeof(float) * (size_t)P * C, st));
+    for (int v = 0; v < n_views; ++v) {
+        int rc = lsr_backward_composite(s[v], in, gin[v], gout->dL_dlanguage_feature, geom[v], binning[v], img[v],
+                                        scratch[v], num_rendered[v], stream);
+        if (rc) return rc;
+    }
+    return lsr_backward_preprocess_views(n_views, s, in, gout, geom, scratch, num_rendered, accumulate, stream);
 }
 
 int lsr_mark_visible(int32_t P, const float* means3D, const float* viewmatrix, const float* projmatrix,

@@ -62,6 +62,41 @@ struct PreprocessBwdArgs {
     float* drots;
 };
 
+// Preprocess backward of several views of the same Gaussians in one pass (lsr_backward_views):
+// per Gaussian, the view-independent rows (mean, scale, rotation, SH) are read once, each view's
+// screen-space sums (acc_small of its compositor backward) are pushed through that view's camera,
+// and the summed gradient rows are written (or accumulated) once.
+constexpr int LSR_MAX_VIEWS = 8;   // views per launch; more are processed in chunks
+struct ViewCam {
+    const float* view;
+    const float* proj;
+    const float* campos;
+    float tanfovx, tanfovy, focal_x, focal_y;
+    int deg;
+    const uint32_t* tiles;    // tiles touched in this view (0 = culled)
+    const uint8_t* clamped;
+    const float* acc_small;   // [P,12] the view's summed records
+};
+struct PreprocessBwdViewsArgs {
+    int P, M, nv;
+    float scale_modifier;
+    const float* means3D;
+    const float* scales;
+    const float* rotations;
+    const float* shs;
+    const float* cov3D_precomp;
+    ViewCam cam[LSR_MAX_VIEWS];
+    float* dopacity;
+    float* dmeans3D;
+    float* dmeans2D;
+    float* dcolors;
+    float* dcov3D;
+    float* dsh;
+    float* dscales;
+    float* drots;
+};
+void launch_preprocess_bwd_views(const PreprocessBwdViewsArgs& a, bool accumulate, hipStream_t st);
+
 struct RenderFwdArgs {
     int W, H, grid_x, grid_y, C, include_feature;
     const uint2* ranges;

@@ -109,7 +109,7 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
     a.radius[i] = 0;
     a.tiles[i] = 0;
     a.rect[i] = make_uint2(0u, 0u);
-    a.key[i] = 0xFFFFFFFFu;
+    if (a.key) a.key[i] = 0xFFFFFFFFu;
     const float3 p = make_float3(a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]);
     const float4 ph = xform4x4(a.proj, p);
     const float3 pv = xform4x3(a.view, p);
@@ -230,7 +230,7 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
     a.radius[i] = radius;
     a.tiles[i] = (uint32_t)ntiles;
     a.rect[i] = make_uint2((uint32_t)cmin.x | ((uint32_t)cmin.y << 16), (uint32_t)cmax.x | ((uint32_t)cmax.y << 16));
-    a.key[i] = __float_as_uint(pv.z);
+    if (a.key) a.key[i] = __float_as_uint(pv.z);
     a.xy[i] = pix;
     a.conic_o[i] = conic;
     a.rgbd[i] = make_float4(rgb[0], rgb[1], rgb[2], pv.z);
@@ -358,6 +358,49 @@ __device__ void cov3d_bwd(float3 sc, float mod, float4 q, const float* dcov, flo
              4.0f * y * (d.m[2][2] + d.m[0][0]);
     drot.w = 2.0f * r * (d.m[0][1] - d.m[1][0]) + 2.0f * x * (d.m[2][0] + d.m[0][2]) + 2.0f * y * (d.m[1][2] + d.m[2][1]) -
              4.0f * z * (d.m[1][1] + d.m[0][0]);
+}
+
+// SH backward of colour channel ch (upstream computeColorFromSH backward): g[k] = dL/dsh[k][ch]
+// for k < 16 (zero past the active degree), and this channel's d colour / d direction partials
+// (assigned, not accumulated, into dRdx, dRdy, dRdz; left as given at degree 0).
+__device__ __forceinline__ void sh_bwd_channel(const float* __restrict__ sh, int ch, int deg, float x, float y, float z,
+                                               float dRc, float (&g)[16], float& dRdx, float& dRdy, float& dRdz) {
+#define SHc(k) sh[(k) * 3 + ch]
+#pragma unroll
+    for (int k = 0; k < 16; ++k) g[k] = 0.0f;
+    g[0] = SH_C0 * dRc;
+    if (deg > 0) {
+        g[1] = -SH_C1 * y * dRc; g[2] = SH_C1 * z * dRc; g[3] = -SH_C1 * x * dRc;
+        dRdx = -SH_C1 * SHc(3); dRdy = -SH_C1 * SHc(1); dRdz = SH_C1 * SHc(2);
+        if (deg > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+            g[4] = SH_C2[0] * xy * dRc; g[5] = SH_C2[1] * yz * dRc;
+            g[6] = SH_C2[2] * (2.0f * zz - xx - yy) * dRc; g[7] = SH_C2[3] * xz * dRc;
+            g[8] = SH_C2[4] * (xx - yy) * dRc;
+            dRdx += SH_C2[0] * y * SHc(4) + SH_C2[2] * 2.0f * -x * SHc(6) + SH_C2[3] * z * SHc(7) + SH_C2[4] * 2.0f * x * SHc(8);
+            dRdy += SH_C2[0] * x * SHc(4) + SH_C2[1] * z * SHc(5) + SH_C2[2] * 2.0f * -y * SHc(6) + SH_C2[4] * 2.0f * -y * SHc(8);
+            dRdz += SH_C2[1] * y * SHc(5) + SH_C2[2] * 2.0f * 2.0f * z * SHc(6) + SH_C2[3] * x * SHc(7);
+            if (deg > 2) {
+                g[9] = SH_C3[0] * y * (3.0f * xx - yy) * dRc;
+                g[10] = SH_C3[1] * xy * z * dRc;
+                g[11] = SH_C3[2] * y * (4.0f * zz - xx - yy) * dRc;
+                g[12] = SH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * dRc;
+                g[13] = SH_C3[4] * x * (4.0f * zz - xx - yy) * dRc;
+                g[14] = SH_C3[5] * z * (xx - yy) * dRc;
+                g[15] = SH_C3[6] * x * (xx - 3.0f * yy) * dRc;
+                dRdx += SH_C3[0] * SHc(9) * 3.0f * 2.0f * xy + SH_C3[1] * SHc(10) * yz + SH_C3[2] * SHc(11) * -2.0f * xy +
+                        SH_C3[3] * SHc(12) * -3.0f * 2.0f * xz + SH_C3[4] * SHc(13) * (-3.0f * xx + 4.0f * zz - yy) +
+                        SH_C3[5] * SHc(14) * 2.0f * xz + SH_C3[6] * SHc(15) * 3.0f * (xx - yy);
+                dRdy += SH_C3[0] * SHc(9) * 3.0f * (xx - yy) + SH_C3[1] * SHc(10) * xz +
+                        SH_C3[2] * SHc(11) * (-3.0f * yy + 4.0f * zz - xx) + SH_C3[3] * SHc(12) * -3.0f * 2.0f * yz +
+                        SH_C3[4] * SHc(13) * -2.0f * xy + SH_C3[5] * SHc(14) * -2.0f * yz + SH_C3[6] * SHc(15) * -3.0f * 2.0f * xy;
+                dRdz += SH_C3[1] * SHc(10) * xy + SH_C3[2] * SHc(11) * 4.0f * 2.0f * yz +
+                        SH_C3[3] * SHc(12) * 3.0f * (2.0f * zz - xx - yy) + SH_C3[4] * SHc(13) * 4.0f * 2.0f * xz +
+                        SH_C3[5] * SHc(14) * (xx - yy);
+            }
+        }
+    }
+#undef SHc
 }
 
 template <bool ACC>
@@ -531,42 +574,7 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
                 float g[16];
 #pragma unroll
                 for (int ch = 0; ch < 3; ++ch) {
-#define SHc(k) sh[(k) * 3 + ch]
-#pragma unroll
-                    for (int k = 0; k < 16; ++k) g[k] = 0.0f;
-                    g[0] = SH_C0 * dR[ch];
-                    if (deg > 0) {
-                        g[1] = -SH_C1 * y * dR[ch]; g[2] = SH_C1 * z * dR[ch]; g[3] = -SH_C1 * x * dR[ch];
-                        dRdx[ch] = -SH_C1 * SHc(3); dRdy[ch] = -SH_C1 * SHc(1); dRdz[ch] = SH_C1 * SHc(2);
-                        if (deg > 1) {
-                            const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-                            g[4] = SH_C2[0] * xy * dR[ch]; g[5] = SH_C2[1] * yz * dR[ch];
-                            g[6] = SH_C2[2] * (2.0f * zz - xx - yy) * dR[ch]; g[7] = SH_C2[3] * xz * dR[ch];
-                            g[8] = SH_C2[4] * (xx - yy) * dR[ch];
-                            dRdx[ch] += SH_C2[0] * y * SHc(4) + SH_C2[2] * 2.0f * -x * SHc(6) + SH_C2[3] * z * SHc(7) + SH_C2[4] * 2.0f * x * SHc(8);
-                            dRdy[ch] += SH_C2[0] * x * SHc(4) + SH_C2[1] * z * SHc(5) + SH_C2[2] * 2.0f * -y * SHc(6) + SH_C2[4] * 2.0f * -y * SHc(8);
-                            dRdz[ch] += SH_C2[1] * y * SHc(5) + SH_C2[2] * 2.0f * 2.0f * z * SHc(6) + SH_C2[3] * x * SHc(7);
-                            if (deg > 2) {
-                                g[9] = SH_C3[0] * y * (3.0f * xx - yy) * dR[ch];
-                                g[10] = SH_C3[1] * xy * z * dR[ch];
-                                g[11] = SH_C3[2] * y * (4.0f * zz - xx - yy) * dR[ch];
-                                g[12] = SH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * dR[ch];
-                                g[13] = SH_C3[4] * x * (4.0f * zz - xx - yy) * dR[ch];
-                                g[14] = SH_C3[5] * z * (xx - yy) * dR[ch];
-                                g[15] = SH_C3[6] * x * (xx - 3.0f * yy) * dR[ch];
-                                dRdx[ch] += SH_C3[0] * SHc(9) * 3.0f * 2.0f * xy + SH_C3[1] * SHc(10) * yz + SH_C3[2] * SHc(11) * -2.0f * xy +
-                                            SH_C3[3] * SHc(12) * -3.0f * 2.0f * xz + SH_C3[4] * SHc(13) * (-3.0f * xx + 4.0f * zz - yy) +
-                                            SH_C3[5] * SHc(14) * 2.0f * xz + SH_C3[6] * SHc(15) * 3.0f * (xx - yy);
-                                dRdy[ch] += SH_C3[0] * SHc(9) * 3.0f * (xx - yy) + SH_C3[1] * SHc(10) * xz +
-                                            SH_C3[2] * SHc(11) * (-3.0f * yy + 4.0f * zz - xx) + SH_C3[3] * SHc(12) * -3.0f * 2.0f * yz +
-                                            SH_C3[4] * SHc(13) * -2.0f * xy + SH_C3[5] * SHc(14) * -2.0f * yz + SH_C3[6] * SHc(15) * -3.0f * 2.0f * xy;
-                                dRdz[ch] += SH_C3[1] * SHc(10) * xy + SH_C3[2] * SHc(11) * 4.0f * 2.0f * yz +
-                                            SH_C3[3] * SHc(12) * 3.0f * (2.0f * zz - xx - yy) + SH_C3[4] * SHc(13) * 4.0f * 2.0f * xz +
-                                            SH_C3[5] * SHc(14) * (xx - yy);
-                            }
-                        }
-                    }
-#undef SHc
+                    sh_bwd_channel(sh, ch, deg, x, y, z, dR[ch], g, dRdx[ch], dRdy[ch], dRdz[ch]);
                     // this channel's coefficients have all been read: overwrite them with the gradient
                     if (stage) {
 #pragma unroll
@@ -608,6 +616,161 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
         __syncthreads();
         write_rows<ACC, M3>(a.dsh + (size_t)g0 * M3, s_sh, rows, s_vis);
     }
+}
+
+// Several views at once (lsr_backward_views): the same per-view chain as k_preprocess_bwd, summed
+// over the views in which the Gaussian has tiles.  The view-independent work is done once: the
+// Gaussian's rows are read once, cov3D is built once, and the scale / rotation backward runs once
+// on the summed dL/dcov3D (it is linear in it); the gradient rows are written once.
+template <bool ACC, int MS>
+__global__ void __launch_bounds__(256) k_preprocess_bwd_views(PreprocessBwdViewsArgs a) {
+    constexpr int M3 = MS * 3, SP = M3 + 1;
+    __shared__ float s_sh[MS > 0 ? 256 * SP : 1];
+    __shared__ uint8_t s_vis[256];
+    const int g0 = blockIdx.x * blockDim.x;
+    const int rows = min(256, a.P - g0);
+    const int i = g0 + threadIdx.x;
+    uint32_t vmask = 0;
+#pragma unroll
+    for (int v = 0; v < LSR_MAX_VIEWS; ++v)
+        if (v < a.nv && i < a.P && a.cam[v].tiles[i] > 0) vmask |= 1u << v;
+    const bool vis = vmask != 0;
+    const bool stage = MS > 0 && a.shs != nullptr;
+    if (stage) {
+        s_vis[threadIdx.x] = vis ? 1 : 0;
+        __syncthreads();
+        stage_visible_rows<M3>(s_sh, a.shs + (size_t)g0 * M3, rows, s_vis);
+        __syncthreads();
+    }
+    if (i < a.P && (vis || !ACC)) {
+        float gcol[3] = {0.0f, 0.0f, 0.0f}, g2d[2] = {0.0f, 0.0f}, gop = 0.0f;
+        float3 dm = make_float3(0.0f, 0.0f, 0.0f);
+        float dcov[6] = {0, 0, 0, 0, 0, 0};
+        float dsh[48];
+#pragma unroll
+        for (int k = 0; k < 48; ++k) dsh[k] = 0.0f;
+        float3 dscale = make_float3(0.0f, 0.0f, 0.0f);
+        float4 drot = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        const int M = a.M;
+        float* srow = stage ? s_sh + threadIdx.x * SP : nullptr;
+        if (vis) {
+            const float3 p = make_float3(a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]);
+            float c3[6];
+            float3 sc = make_float3(0.0f, 0.0f, 0.0f);
+            float4 q = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (a.cov3D_precomp) {
+#pragma unroll
+                for (int k = 0; k < 6; ++k) c3[k] = a.cov3D_precomp[6 * (size_t)i + k];
+            } else {
+                sc = make_float3(a.scales[3 * i], a.scales[3 * i + 1], a.scales[3 * i + 2]);
+                q = reinterpret_cast<const float4*>(a.rotations)[i];
+                cov3d(sc, a.scale_modifier, q, c3);
+            }
+            const float* sh = stage ? srow : (a.shs ? a.shs + (size_t)i * M * 3 : nullptr);
+#pragma unroll
+            for (int v = 0; v < LSR_MAX_VIEWS; ++v) {
+                if (!((vmask >> v) & 1u)) continue;
+                const ViewCam& cm = a.cam[v];
+                float rs[12];
+                const float4* r4 = reinterpret_cast<const float4*>(cm.acc_small + (size_t)i * 12);
+#pragma unroll
+                for (int k4 = 0; k4 < 3; ++k4) {
+                    const float4 t = r4[k4];
+                    rs[4 * k4] = t.x; rs[4 * k4 + 1] = t.y; rs[4 * k4 + 2] = t.z; rs[4 * k4 + 3] = t.w;
+                }
+                gcol[0] += rs[0]; gcol[1] += rs[1]; gcol[2] += rs[2];
+                const float gx = rs[4], gy = rs[5];
+                g2d[0] += gx; g2d[1] += gy;
+                gop += rs[9];
+                float3 dmv;
+                float dcv[6];
+                cov2d_bwd(p, c3, cm.focal_x, cm.focal_y, cm.tanfovx, cm.tanfovy, cm.view, make_float3(rs[6], rs[7], rs[8]),
+                          dmv, dcv);
+#pragma unroll
+                for (int k = 0; k < 6; ++k) dcov[k] += dcv[k];
+                const float* pm = cm.proj;
+                const float4 mh = xform4x4(pm, p);
+                const float mw = 1.0f / (mh.w + 0.0000001f);
+                const float mul1 = (pm[0] * p.x + pm[4] * p.y + pm[8] * p.z + pm[12]) * mw * mw;
+                const float mul2 = (pm[1] * p.x + pm[5] * p.y + pm[9] * p.z + pm[13]) * mw * mw;
+                dmv.x += (pm[0] * mw - pm[3] * mul1) * gx + (pm[1] * mw - pm[3] * mul2) * gy;
+                dmv.y += (pm[4] * mw - pm[7] * mul1) * gx + (pm[5] * mw - pm[7] * mul2) * gy;
+                dmv.z += (pm[8] * mw - pm[11] * mul1) * gx + (pm[9] * mw - pm[11] * mul2) * gy;
+                const float gd = rs[3];
+                dmv.x += cm.view[2] * gd;
+                dmv.y += cm.view[6] * gd;
+                dmv.z += cm.view[10] * gd;
+                if (sh) {
+                    const float3 dir_orig = make_float3(p.x - cm.campos[0], p.y - cm.campos[1], p.z - cm.campos[2]);
+                    const float len = sqrtf(dir_orig.x * dir_orig.x + dir_orig.y * dir_orig.y + dir_orig.z * dir_orig.z);
+                    const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
+                    const uint8_t cl = cm.clamped[i];
+                    const float dR[3] = {(cl & 1) ? 0.0f : rs[0], (cl & 2) ? 0.0f : rs[1], (cl & 4) ? 0.0f : rs[2]};
+                    float dRdx[3] = {0, 0, 0}, dRdy[3] = {0, 0, 0}, dRdz[3] = {0, 0, 0};
+                    float g[16];
+#pragma unroll
+                    for (int ch = 0; ch < 3; ++ch) {
+                        sh_bwd_channel(sh, ch, cm.deg, x, y, z, dR[ch], g, dRdx[ch], dRdy[ch], dRdz[ch]);
+#pragma unroll
+                        for (int k = 0; k < 16; ++k) dsh[k * 3 + ch] += g[k];
+                    }
+                    const float dLdx = dRdx[0] * dR[0] + dRdx[1] * dR[1] + dRdx[2] * dR[2];
+                    const float dLdy = dRdy[0] * dR[0] + dRdy[1] * dR[1] + dRdy[2] * dR[2];
+                    const float dLdz = dRdz[0] * dR[0] + dRdz[1] * dR[1] + dRdz[2] * dR[2];
+                    const float3 w = dir_orig;
+                    const float sum2 = w.x * w.x + w.y * w.y + w.z * w.z;
+                    const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+                    dmv.x += ((sum2 - w.x * w.x) * dLdx - w.y * w.x * dLdy - w.z * w.x * dLdz) * invsum32;
+                    dmv.y += (-w.x * w.y * dLdx + (sum2 - w.y * w.y) * dLdy - w.z * w.y * dLdz) * invsum32;
+                    dmv.z += (-w.x * w.z * dLdx - w.y * w.z * dLdy + (sum2 - w.z * w.z) * dLdz) * invsum32;
+                }
+                dm.x += dmv.x; dm.y += dmv.y; dm.z += dmv.z;
+            }
+            if (!a.cov3D_precomp) cov3d_bwd(sc, a.scale_modifier, q, dcov, dscale, drot);
+        }
+        if (a.dmeans2D) { put<ACC>(a.dmeans2D + 3 * (size_t)i, g2d[0]); put<ACC>(a.dmeans2D + 3 * (size_t)i + 1, g2d[1]); put<ACC>(a.dmeans2D + 3 * (size_t)i + 2, 0.0f); }
+        if (a.dcolors) { put<ACC>(a.dcolors + 3 * (size_t)i, gcol[0]); put<ACC>(a.dcolors + 3 * (size_t)i + 1, gcol[1]); put<ACC>(a.dcolors + 3 * (size_t)i + 2, gcol[2]); }
+        if (a.dopacity) put<ACC>(a.dopacity + i, gop);
+        if (a.dmeans3D) { put<ACC>(a.dmeans3D + 3 * (size_t)i, dm.x); put<ACC>(a.dmeans3D + 3 * (size_t)i + 1, dm.y); put<ACC>(a.dmeans3D + 3 * (size_t)i + 2, dm.z); }
+        if (a.dcov3D) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k) put<ACC>(a.dcov3D + 6 * (size_t)i + k, dcov[k]);
+        }
+        if (a.dscales) { put<ACC>(a.dscales + 3 * (size_t)i, dscale.x); put<ACC>(a.dscales + 3 * (size_t)i + 1, dscale.y); put<ACC>(a.dscales + 3 * (size_t)i + 2, dscale.z); }
+        if (a.drots) {
+            put<ACC>(a.drots + 4 * (size_t)i, drot.x); put<ACC>(a.drots + 4 * (size_t)i + 1, drot.y);
+            put<ACC>(a.drots + 4 * (size_t)i + 2, drot.z); put<ACC>(a.drots + 4 * (size_t)i + 3, drot.w);
+        }
+        if (stage) {
+#pragma unroll
+            for (int k = 0; k < M3; ++k) srow[k] = k < 48 ? dsh[k] : 0.0f;
+        } else if (a.dsh && a.shs) {
+            float* d = a.dsh + (size_t)i * M * 3;
+#pragma unroll
+            for (int k = 0; k < 48; ++k)
+                if (k < 3 * M) put<ACC>(d + k, dsh[k]);
+            for (int k = 48; k < 3 * M; ++k) put<ACC>(d + k, 0.0f);
+        }
+    }
+    if (stage && a.dsh) {
+        __syncthreads();
+        write_rows<ACC, M3>(a.dsh + (size_t)g0 * M3, s_sh, rows, s_vis);
+    }
+}
+
+void launch_preprocess_bwd_views(const PreprocessBwdViewsArgs& a, bool accumulate, hipStream_t st) {
+    if (a.P == 0 || a.nv == 0) return;
+    const dim3 grid((a.P + 255) / 256), block(256);
+#define LSR_GOV(ACC, MS) hipLaunchKernelGGL((k_preprocess_bwd_views<ACC, MS>), grid, block, 0, st, a)
+    const int m = a.shs ? a.M : 0;
+    if (accumulate) {
+        switch (m) { case 1: LSR_GOV(true, 1); break; case 4: LSR_GOV(true, 4); break; case 9: LSR_GOV(true, 9); break;
+                     case 16: LSR_GOV(true, 16); break; default: LSR_GOV(true, 0); break; }
+    } else {
+        switch (m) { case 1: LSR_GOV(false, 1); break; case 4: LSR_GOV(false, 4); break; case 9: LSR_GOV(false, 9); break;
+                     case 16: LSR_GOV(false, 16); break; default: LSR_GOV(false, 0); break; }
+    }
+#undef LSR_GOV
 }
 
 template <bool ACC>

@@ -28,7 +28,8 @@ import torch.nn as nn
 from . import _lib
 
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "RasterizerState",
-           "forward_native", "backward_native"]
+           "forward_native", "backward_native", "backward_views_native", "backward_composite_native",
+           "backward_preprocess_views_native"]
 
 _lib.load()   # fail loudly at import if the native library is missing
 _BINNING_DELAY_CYCLES = 0   # tests only: GPU cycles slept on the stream before a side-stream binning
@@ -289,6 +290,184 @@ def backward_native(state: RasterizerState, grad_color, grad_lang=None, grad_dep
         torch.save(dict(grad_color=gc.cpu()), "snapshot_bw.dump")
     _lib.check(rc, "lsr_backward")
     return g
+
+
+def backward_views_native(states, grad_colors, grad_langs=None, grad_depths=None, out=None, accumulate=False,
+                          need=None):
+    """Backward of several views of the SAME Gaussians through liblsr.so (lsr_backward_views):
+    the gradients of every view are summed, as train.py's loss.backward() sums its per-view renders
+    (train.py:242-268,339).  Each view's compositor backward runs, then one preprocess backward
+    per 8 views reads the Gaussian rows and writes the gradient rows once.  Float-atomic reduction
+    (for bitwise-reproducible gradients use backward_native(deterministic=True) per view).
+    `states` are the RasterizerState of the views' forwards; grad_* are per-view lists (entries may
+    be None).  Returns the dict of gradient tensors (out's buffers when given)."""
+    L = _lib.load()
+    n = len(states)
+    if n == 0:
+        raise ValueError("backward_views_native needs at least one view")
+    st0 = states[0]
+    inp = st0.inputs
+    for s in states[1:]:
+        if s.inputs["means3D"].data_ptr() != inp["means3D"].data_ptr():
+            raise ValueError("all views must render the same Gaussians")
+    device = inp["means3D"].device
+    P, M, C = st0.fin.P, st0.fin.M, st0.fin.C
+    need = need or {}
+    grad_langs = grad_langs or [None] * n
+    grad_depths = grad_depths or [None] * n
+
+    def buf(name, shape, wanted=True):
+        if not wanted:
+            return None
+        if out is not None and name in out and out[name] is not None:
+            return out[name]
+        return torch.zeros(shape, dtype=torch.float32, device=device) if accumulate else \
+            torch.empty(shape, dtype=torch.float32, device=device)
+
+    g = dict(
+        means3D=buf("means3D", (P, 3), need.get("means3D", True)),
+        means2D=buf("means2D", (P, 3), need.get("means2D", True)),
+        colors=buf("colors", (P, 3), need.get("colors", True)),
+        language_feature=buf("language_feature", (P, C), need.get("language_feature", True) and C > 0),
+        opacities=buf("opacities", (P, 1), need.get("opacities", True)),
+        cov3D=buf("cov3D", (P, 6), need.get("cov3D", True) and inp["cov3D_precomp"] is not None),
+        sh=buf("sh", (P, max(M, 1), 3), need.get("sh", True) and M > 0),
+        scales=buf("scales", (P, 3), need.get("scales", True) and inp["scales"] is not None),
+        rotations=buf("rotations", (P, 4), need.get("rotations", True) and inp["rotations"] is not None),
+    )
+    keep = []
+    gins = []
+    for v, s in enumerate(states):
+        H, W = s.settings.c.image_height, s.settings.c.image_width
+        gc = grad_colors[v].detach().to(torch.float32).contiguous() if grad_colors[v] is not None else \
+            torch.zeros(3, H, W, dtype=torch.float32, device=device)
+        gl = grad_langs[v].detach().to(torch.float32).contiguous() if (grad_langs[v] is not None and C > 0) else None
+        gd = grad_depths[v].detach().to(torch.float32).contiguous() if grad_depths[v] is not None else None
+        keep += [gc, gl, gd]
+        gi = _lib.BwdIn()
+        gi.dL_dout_color, gi.dL_dout_language_feature, gi.dL_dout_depth = gc.data_ptr(), _ptr(gl), _ptr(gd)
+        gi.deterministic = 0
+        gins.append(gi)
+    gout = _lib.BwdOut()
+    gout.dL_dmeans3D, gout.dL_dmeans2D, gout.dL_dcolors = _ptr(g["means3D"]), _ptr(g["means2D"]), _ptr(g["colors"])
+    gout.dL_dlanguage_feature, gout.dL_dopacity = _ptr(g["language_feature"]), _ptr(g["opacities"])
+    gout.dL_dcov3D, gout.dL_dsh = _ptr(g["cov3D"]), _ptr(g["sh"])
+    gout.dL_dscales, gout.dL_drotations = _ptr(g["scales"]), _ptr(g["rotations"])
+    scratch = [torch.empty(int(L.lsr_backward_bytes(P, s.num_rendered, C, 0)), dtype=torch.uint8, device=device)
+               for s in states]
+    SP = ctypes.POINTER(_lib.Settings)
+    BP = ctypes.POINTER(_lib.BwdIn)
+    s_arr = (SP * n)(*[ctypes.pointer(s.settings.c) for s in states])
+    g_arr = (BP * n)(*[ctypes.pointer(gi) for gi in gins])
+    vp = ctypes.c_void_p * n
+    geom = vp(*[s.geom.data_ptr() for s in states])
+    binning = vp(*[s.binning.data_ptr() for s in states])
+    img = vp(*[s.img.data_ptr() for s in states])
+    scr = vp(*[t.data_ptr() for t in scratch])
+    K = (ctypes.c_int64 * n)(*[s.num_rendered for s in states])
+    _lib.check(L.lsr_backward_views(n, s_arr, ctypes.byref(st0.fin), g_arr, ctypes.byref(gout), geom, binning, img,
+                                    scr, K, 1 if accumulate else 0, _stream(device)), "lsr_backward_views")
+    return g
+
+
+class CompositeGrad:
+    """A view whose compositor backward ran (backward_composite_native): its forward state and the
+    per-Gaussian screen-space sums (scratch) that backward_preprocess_views_native consumes."""
+
+    def __init__(self, state, scratch, keep):
+        self.state, self.scratch, self._keep = state, scratch, keep
+
+
+def backward_composite_native(state: RasterizerState, grad_color, grad_lang=None, grad_depth=None,
+                              dL_dlanguage=None) -> CompositeGrad:
+    """First half of backward_views_native for ONE view (lsr_backward_composite), on the current
+    stream: the compositor backward; the language gradient is ADDED to dL_dlanguage [P,C] (the
+    caller zeroes it once per batch).  Finish a batch with backward_preprocess_views_native."""
+    L = _lib.load()
+    device = state.inputs["means3D"].device
+    P, C = state.fin.P, state.fin.C
+    H, W = state.settings.c.image_height, state.settings.c.image_width
+    gc = grad_color.detach().to(torch.float32).contiguous() if grad_color is not None else \
+        torch.zeros(3, H, W, dtype=torch.float32, device=device)
+    gl = grad_lang.detach().to(torch.float32).contiguous() if (grad_lang is not None and C > 0) else None
+    gd = grad_depth.detach().to(torch.float32).contiguous() if grad_depth is not None else None
+    gi = _lib.BwdIn()
+    gi.dL_dout_color, gi.dL_dout_language_feature, gi.dL_dout_depth = gc.data_ptr(), _ptr(gl), _ptr(gd)
+    gi.deterministic = 0
+    if dL_dlanguage is not None and (dL_dlanguage.shape != (P, C) or not dL_dlanguage.is_contiguous()):
+        raise ValueError("dL_dlanguage must be a contiguous [P, C] tensor")
+    scratch = torch.empty(int(L.lsr_backward_bytes(P, state.num_rendered, C, 0)), dtype=torch.uint8, device=device)
+    _lib.check(L.lsr_backward_composite(ctypes.byref(state.settings.c), ctypes.byref(state.fin), ctypes.byref(gi),
+                                        _ptr(dL_dlanguage if C > 0 else None), ctypes.c_void_p(state.geom.data_ptr()),
+                                        ctypes.c_void_p(state.binning.data_ptr()),
+                                        ctypes.c_void_p(state.img.data_ptr()), ctypes.c_void_p(scratch.data_ptr()),
+                                        ctypes.c_int64(state.num_rendered), _stream(device)), "lsr_backward_composite")
+    return CompositeGrad(state, scratch, (gc, gl, gd))
+
+
+def backward_preprocess_views_native(parts, out=None, accumulate=False, need=None):
+    """Second half of backward_views_native (lsr_backward_preprocess_views): the preprocess backward
+    of every view in `parts` (CompositeGrad), summed into one set of gradient rows.  The language
+    gradient is not touched here (the composite halves added it).  Returns the dict of gradients."""
+    L = _lib.load()
+    n = len(parts)
+    if n == 0:
+        raise ValueError("backward_preprocess_views_native needs at least one view")
+    st0 = parts[0].state
+    inp = st0.inputs
+    for p_ in parts[1:]:
+        if p_.state.inputs["means3D"].data_ptr() != inp["means3D"].data_ptr():
+            raise ValueError("all views must render the same Gaussians")
+    device = inp["means3D"].device
+    need = dict(need or {})
+    need["language_feature"] = False
+    g = _grad_buffers(st0, out, accumulate, need)
+    gout = _bwd_out(g)
+    SP = ctypes.POINTER(_lib.Settings)
+    vp = ctypes.c_void_p * n
+    _lib.check(L.lsr_backward_preprocess_views(n, (SP * n)(*[ctypes.pointer(p_.state.settings.c) for p_ in parts]),
+                                               ctypes.byref(st0.fin), ctypes.byref(gout),
+                                               vp(*[p_.state.geom.data_ptr() for p_ in parts]),
+                                               vp(*[p_.scratch.data_ptr() for p_ in parts]),
+                                               (ctypes.c_int64 * n)(*[p_.state.num_rendered for p_ in parts]),
+                                               1 if accumulate else 0, _stream(device)),
+               "lsr_backward_preprocess_views")
+    return g
+
+
+def _grad_buffers(state, out, accumulate, need):
+    inp = state.inputs
+    device = inp["means3D"].device
+    P, M, C = state.fin.P, state.fin.M, state.fin.C
+
+    def buf(name, shape, wanted=True):
+        if not wanted:
+            return None
+        if out is not None and name in out and out[name] is not None:
+            return out[name]
+        return torch.zeros(shape, dtype=torch.float32, device=device) if accumulate else \
+            torch.empty(shape, dtype=torch.float32, device=device)
+
+    return dict(
+        means3D=buf("means3D", (P, 3), need.get("means3D", True)),
+        means2D=buf("means2D", (P, 3), need.get("means2D", True)),
+        colors=buf("colors", (P, 3), need.get("colors", True)),
+        language_feature=buf("language_feature", (P, C), need.get("language_feature", True) and C > 0),
+        opacities=buf("opacities", (P, 1), need.get("opacities", True)),
+        cov3D=buf("cov3D", (P, 6), need.get("cov3D", True) and inp["cov3D_precomp"] is not None),
+        sh=buf("sh", (P, max(M, 1), 3), need.get("sh", True) and M > 0),
+        scales=buf("scales", (P, 3), need.get("scales", True) and inp["scales"] is not None),
+        rotations=buf("rotations", (P, 4), need.get("rotations", True) and inp["rotations"] is not None),
+    )
+
+
+def _bwd_out(g):
+    gout = _lib.BwdOut()
+    gout.dL_dmeans3D, gout.dL_dmeans2D, gout.dL_dcolors = _ptr(g["means3D"]), _ptr(g["means2D"]), _ptr(g["colors"])
+    gout.dL_dlanguage_feature, gout.dL_dopacity = _ptr(g["language_feature"]), _ptr(g["opacities"])
+    gout.dL_dcov3D, gout.dL_dsh = _ptr(g["cov3D"]), _ptr(g["sh"])
+    gout.dL_dscales, gout.dL_drotations = _ptr(g["scales"]), _ptr(g["rotations"])
+    return gout
 
 
 class _RasterizeGaussians(torch.autograd.Function):

@@ -105,6 +105,9 @@ class ViewParallelStep:
             radii = render_view(v, b)
             if b.radii is not None and radii is not None:
                 torch.maximum(b.radii, radii.to(torch.int32), out=b.radii)
+        flush = getattr(render_view, "flush", None)
+        if flush is not None:        # renderers that batch the backward over the rank's views
+            flush(b)
         if self.world > 1:
             dist.all_reduce(b.flat, op=dist.ReduceOp.SUM, group=self.group)
             if b.radii is not None:
@@ -119,13 +122,20 @@ class ViewParallelStep:
         return self.bucket.radii > 0
 
 
-def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool = False, overlap: bool = True):
+def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool = False, overlap: bool = True,
+                         batch_backward: bool = True):
     """render_view callback for ViewParallelStep on the HIP rasterizer (the product path).
 
     scene    : object with means3D, opacities, shs, lang, scales, rotations device tensors
     settings : dict (or list) of GaussianRasterizationSettings, indexed by view
     grad_fn  : grad_fn(v, color, lang, depth) -> (dL_dcolor, dL_dlang, dL_ddepth) for view v
     Forward + backward of view v with the gradients accumulated straight into the bucket.
+
+    batch_backward=True (atomic mode only) runs each view's compositor backward right after its
+    forward (lsr_backward_composite, language gradients straight into the bucket) and the
+    preprocess backward of all the rank's views once at the end of the step
+    (lsr_backward_preprocess_views): the Gaussian rows are read and the bucket's gradient rows
+    written once per step instead of once per view.
 
     overlap=True pipelines the views: once view v's render and backward are enqueued, view v+1's
     preprocess (its depth order and instance count, the one host synchronisation of a forward)
@@ -147,6 +157,9 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
                                      language_feature=scene.lang, scales=scene.scales, rotations=scene.rotations,
                                      stream=stream, binning=stream is not None)
 
+    batched = batch_backward and not deterministic
+    held = []                             # (state, dL_dcolor, dL_dlang, dL_ddepth) awaiting flush
+
     def render_view(v: int, bucket: GradBucket):
         pf = pending.pop(v, None)
         if pf is None:                    # first view of a step: the Gaussians are final here
@@ -155,13 +168,23 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
                 params_ready.record(torch.cuda.current_stream())
         color, lang, radii, depth, st = dgr.render_native(pf)
         gc, gl, gd = grad_fn(v, color, lang, depth)
-        dgr.backward_native(st, gc, gl, gd, out=bucket.views, accumulate=True, need=bucket.need(),
-                            deterministic=deterministic)
+        if batched:                   # compositor backward now, preprocess backward at flush
+            held.append(dgr.backward_composite_native(st, gc, gl, gd, dL_dlanguage=bucket.views["language_feature"]))
+        else:
+            dgr.backward_native(st, gc, gl, gd, out=bucket.views, accumulate=True, need=bucket.need(),
+                                deterministic=deterministic)
         render_view.last_num_rendered = st.num_rendered
         if side is not None and has_view(v + 1):
             side.wait_event(params_ready)     # orders after the parameters, not after view v's work
             pending[v + 1] = preprocess(v + 1, stream=side)
         return radii
 
+    def flush(bucket: GradBucket):
+        if held:
+            dgr.backward_preprocess_views_native(held, out=bucket.views, accumulate=True, need=bucket.need())
+            held.clear()
+
     render_view.last_num_rendered = 0
+    if batched:
+        render_view.flush = flush
     return render_view

@@ -31,8 +31,10 @@ import torch.distributed as dist  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-def phase_bytes(phase, P, Pvis, K, npix, ntiles, C, M=16, accumulate=True):
-    """Algorithmic HBM bytes of one launch of each phase (each byte counted once)."""
+def phase_bytes(phase, P, Pvis, K, npix, ntiles, C, M=16, accumulate=True, V=1, Pvis_sum=None, Pany=None):
+    """Algorithmic HBM bytes of one launch of each phase (each byte counted once).
+    preprocess_bwd_views covers V views: Pvis_sum = visible Gaussians summed over them, Pany =
+    Gaussians visible in at least one."""
     rec = 4 + 8 + 16 + 16 + 4 * C          # id + xy + conic/opacity + rgb/depth + language row
     if phase == "preprocess":              # inputs; radii, radius, tiles, key, rect; screen records
         return P * (12 + 12 + 16 + 4 + 4 * 3 * M) + P * (4 + 4 + 4 + 4 + 8) + Pvis * (8 + 16 + 16 + 1)
@@ -53,6 +55,9 @@ def phase_bytes(phase, P, Pvis, K, npix, ntiles, C, M=16, accumulate=True):
     if phase == "preprocess_bwd":          # visible rows: inputs + screen grads; gradient rows (RMW if accumulating)
         grads = 4 * (3 + 3 + 4 + 1 + 3 * M)
         return P * 4 + Pvis * (12 + 12 + 16 + 4 * 3 * M + 1 + 48) + (2 * Pvis * grads if accumulate else P * grads)
+    if phase == "preprocess_bwd_views":    # per view: tiles, and for its visible rows clamped + screen sums;
+        grads = 4 * (3 + 3 + 4 + 1 + 3 * M)  # once: Gaussian rows of the visible-anywhere set, gradient RMW
+        return V * P * 4 + Pvis_sum * (1 + 48) + Pany * (12 + 12 + 16 + 4 * 3 * M) + 2 * Pany * grads
     return 0
 
 
@@ -96,6 +101,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=3, help="headline frames timed on the CPU oracle")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-overlap", action="store_true", help="diagnostic: no side stream (uncontended phase times)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -129,13 +135,17 @@ def main():
     g = torch.Generator(device="cpu").manual_seed(123)
     gcol = (torch.randn(3, H, W, generator=g) * 1e-3).to(dev)
     glang = (torch.randn(C, H, W, generator=g) * 1e-3).to(dev)
-    render = native_view_renderer(scene, settings, lambda v, color, lang, depth: (gcol, glang, None))
+    render = native_view_renderer(scene, settings, lambda v, color, lang, depth: (gcol, glang, None),
+                                  overlap=not args.no_overlap)
     Ks = []
 
     def render_view(v, b):
         r = render(v, b)
         Ks.append(render.last_num_rendered)
         return r
+
+    if hasattr(render, "flush"):                           # batched backward of the step's views
+        render_view.flush = render.flush
 
     def step():
         dp.run(render_view)                                # fwd+bwd per view, SUM all-reduce (RCCL) if world > 1
@@ -158,6 +168,8 @@ def main():
     elapsed = time.perf_counter() - t0
     prof = _lib.profile_read() if not args.no_profile else {}
     _lib.profile_enable(False)
+    if prof and prof["render_bwd"][1] != V * args.steps:   # every view's backward ran in the timed region
+        raise RuntimeError(f"expected {V * args.steps} backward launches, profiled {prof['render_bwd'][1]}")
     el = torch.tensor([elapsed], device=dev, dtype=torch.float64)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -168,21 +180,28 @@ def main():
     if rank == 0:
         Kmean = float(np.mean(Ks)) if Ks else 0.0
         with torch.no_grad():
-            _, _, radii, _, _ = dgr.forward_native(settings[dp.views[0]], scene.means3D, scene.opacities, shs=scene.shs,
-                                                   language_feature=scene.lang, scales=scene.scales,
-                                                   rotations=scene.rotations)
-            Pvis = int((radii > 0).sum())
+            vis_sum, any_vis = 0, torch.zeros(P, dtype=torch.bool, device=dev)
+            for v in dp.views:
+                _, _, radii, _, _ = dgr.forward_native(settings[v], scene.means3D, scene.opacities, shs=scene.shs,
+                                                       language_feature=scene.lang, scales=scene.scales,
+                                                       rotations=scene.rotations)
+                vis_sum += int((radii > 0).sum())
+                any_vis |= radii > 0
+                if v == dp.views[0]:
+                    Pvis = int((radii > 0).sum())
+            Pany = int(any_vis.sum())
+        pb = dict(V=len(dp.views), Pvis_sum=vis_sum, Pany=Pany)
         ntiles = ((W + 15) // 16) * ((H + 15) // 16)
         roof = None
         phases = {}
         if prof:
             for k, (ms, n) in prof.items():
                 if n:
-                    phases[k] = dict(mean_ms=ms / n, launches=n, gbs=phase_bytes(k, P, Pvis, Kmean, W * H, ntiles, C, M)
+                    phases[k] = dict(mean_ms=ms / n, launches=n, gbs=phase_bytes(k, P, Pvis, Kmean, W * H, ntiles, C, M, **pb)
                                      / (ms / n * 1e-3) / 1e9)
             dom = max(prof, key=lambda k: prof[k][0])
             ms, n = prof[dom]
-            byts = phase_bytes(dom, P, Pvis, Kmean, W * H, ntiles, C, M)
+            byts = phase_bytes(dom, P, Pvis, Kmean, W * H, ntiles, C, M, **pb)
             ach = byts / (ms / n * 1e-3) / 1e9
             traffic = None
             pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -210,7 +229,7 @@ def main():
             config=dict(workload="S2M synthetic (BASELINE configs[2] per GPU; configs[3] batch split)",
                         gaussians=P, width=W, height=H, channels=C, views_per_gpu_per_step=V,
                         global_batch=world * V, parallelism=f"dp{world}", num_rendered_mean=int(Kmean),
-                        visible=Pvis, grad_bucket_mb=round(bucket.nbytes / 2**20, 1)),
+                        visible=Pvis, visible_any_view=Pany, grad_bucket_mb=round(bucket.nbytes / 2**20, 1)),
             roofline=roof, cpu_baseline=cpu,
             phases={k: dict(mean_ms=round(v["mean_ms"], 4), gbs=round(v["gbs"], 1)) for k, v in phases.items()},
         )

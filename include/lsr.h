@@ -140,6 +140,37 @@ int lsr_backward(const lsr_settings *s, const lsr_fwd_in *in, const lsr_bwd_in *
                  const void *geom, const void *binning, const void *img, void *scratch, int64_t num_rendered,
                  int32_t accumulate, lsr_stream_t stream);
 
+/* Backward of n_views >= 1 views of the same Gaussians `in` (one training batch), summed:
+ * gout (+)= sum_v dL_v/d(inputs) (accumulate != 0 adds to gout; otherwise gout is overwritten).
+ * This is what train.py's loss.backward() does over its per-view renders
+ * (/root/reference/train.py:242-268,339), in one call: every view's compositor backward runs on
+ * `stream`, then ONE preprocess backward per 8 views reads each Gaussian's rows and writes its
+ * gradient rows once instead of once per view.  Float-atomic reduction only (every gin[v] must
+ * have deterministic == 0; lsr_backward per view gives the deterministic mode).  All views must
+ * share scale_modifier.  s[v], gin[v], geom[v], binning[v], img[v], num_rendered[v] are view v's
+ * forward state; scratch[v] holds >= lsr_backward_bytes(P, num_rendered[v], C, 0) bytes.  The
+ * pointer arrays are HOST arrays of device pointers. */
+int lsr_backward_views(int32_t n_views, const lsr_settings *const *s, const lsr_fwd_in *in,
+                       const lsr_bwd_in *const *gin, lsr_bwd_out *gout, const void *const *geom,
+                       const void *const *binning, const void *const *img, void *const *scratch,
+                       const int64_t *num_rendered, int32_t accumulate, lsr_stream_t stream);
+
+/* lsr_backward_views in two halves, so that a view's compositor backward can run as soon as its
+ * upstream gradients exist (and overlap the next view's preprocess on another stream), while the
+ * preprocess backward still runs once per batch:
+ *  - lsr_backward_composite: compositor backward of ONE view; its per-Gaussian screen-space sums
+ *    go to `scratch` (>= lsr_backward_bytes(P, num_rendered, C, 0)), its language gradients are
+ *    ADDED to dL_dlanguage [P,C] (zero it first; NULL skips them).  Float atomics only.
+ *  - lsr_backward_preprocess_views: the preprocess backward of n_views views whose composite
+ *    backward filled scratch[v]: gout (+)= sum_v (every output except dL_dlanguage_feature, which
+ *    the composite calls already filled). */
+int lsr_backward_composite(const lsr_settings *s, const lsr_fwd_in *in, const lsr_bwd_in *gin, float *dL_dlanguage,
+                           const void *geom, const void *binning, const void *img, void *scratch,
+                           int64_t num_rendered, lsr_stream_t stream);
+int lsr_backward_preprocess_views(int32_t n_views, const lsr_settings *const *s, const lsr_fwd_in *in,
+                                  lsr_bwd_out *gout, const void *const *geom, const void *const *scratch,
+                                  const int64_t *num_rendered, int32_t accumulate, lsr_stream_t stream);
+
 /* markVisible: present[i] = (view-space z of means3D[i]) > 0.2 */
 int lsr_mark_visible(int32_t P, const float *means3D, const float *viewmatrix, const float *projmatrix,
                      uint8_t *present, lsr_stream_t stream);
@@ -156,7 +187,8 @@ int lsr_mark_visible(int32_t P, const float *means3D, const float *viewmatrix, c
 #define LSR_PHASE_RENDER_FWD 6
 #define LSR_PHASE_RENDER_BWD 7
 #define LSR_PHASE_PREPROCESS_BWD 8
-#define LSR_NUM_PHASES 9
+#define LSR_PHASE_PREPROCESS_BWD_VIEWS 9   /* lsr_backward_views: one launch per <= 8 views */
+#define LSR_NUM_PHASES 10
 int lsr_profile_enable(int32_t on);   /* resets the totals */
 int lsr_profile_read(double *ms_total, int64_t *launches, int32_t n);
 

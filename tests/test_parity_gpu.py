@@ -21,6 +21,7 @@ if not torch.cuda.is_available():  # CPU container: the driver only runs these o
     pytest.skip("needs a GPU", allow_module_level=True)
 
 import diff_gaussian_rasterization as dgr  # noqa: E402
+import oracle  # noqa: E402
 import synthetic  # noqa: E402
 from helpers import axis_camera, small_case  # noqa: E402
 from lsr_testutil import (check_binning_against_upstream, decode_img, decode_point_list, grad_err,  # noqa: E402
@@ -60,6 +61,17 @@ def test_forward_odd_size_and_big_splats():
     ref = run_oracle(sc, cam)
     assert (ref.radii[:50] == 0).all()
     _assert_forward(nat, ref, 8)
+
+
+def test_long_tile_lists():
+    """Dense tiles: 12000 wide Gaussians over a 48x32 image (6 tiles), lists of > 4096 entries
+    (many FIFO refills per quadrant wave, long back-to-front replays)."""
+    sc, cam = small_case(P=12000, W=48, H=32, C=3, seed=12, logscale_mean=-1.5, big_frac=0.0)
+    nat = run_native(sc, cam)
+    ref = run_oracle(sc, cam)
+    ranges, *_ = decode_img(nat[4])
+    assert int((ranges[:, 1] - ranges[:, 0]).max()) > 4096
+    _assert_forward(nat, ref, 3)
 
 
 def test_precomputed_paths():
@@ -194,6 +206,87 @@ def test_accumulate_mode_sums_views():
                 total[k] += single[k]
     for k in total:
         assert grad_err(out[k].cpu().numpy(), total[k].cpu().numpy()) < 1e-5, k
+
+
+def _views_forward(sc_dev, cams, include_feature=True, precomp=False):
+    states = []
+    for c in cams:
+        rs = raster_settings(c, bg=(0.3, 0.6, 0.9), include_feature=include_feature)
+        kw = dict(cov3D_precomp=sc_dev.cov3D) if precomp else dict(scales=sc_dev.scales, rotations=sc_dev.rotations)
+        if precomp:
+            kw["colors_precomp"] = sc_dev.colors
+        else:
+            kw["shs"] = sc_dev.shs
+        *_, st = dgr.forward_native(rs, sc_dev.means3D, sc_dev.opacities, language_feature=sc_dev.lang, **kw)
+        states.append(st)
+    return states
+
+
+def test_backward_views_matches_oracle_sum():
+    """lsr_backward_views over 3 views == the sum of the oracle's per-view backward."""
+    C = 8
+    sc, _ = small_case(P=1500, W=80, H=64, C=C, seed=31)
+    cams = synthetic.camera_batch(3, 80, 64, seed=31)
+    states = _views_forward(sc.to("cuda"), cams)
+    rng = np.random.default_rng(3)
+    gcs = [rng.normal(size=(3, 64, 80)).astype(np.float32) for _ in cams]
+    gls = [rng.normal(size=(C, 64, 80)).astype(np.float32) for _ in cams]
+    g = dgr.backward_views_native(states, [torch.tensor(x, device="cuda") for x in gcs],
+                                  [torch.tensor(x, device="cuda") for x in gls])
+    total = None
+    for c, gc, gl in zip(cams, gcs, gls):
+        rg = run_oracle(sc, c, bg=(0.3, 0.6, 0.9)).backward(gc, gl, None)
+        total = {k: v.astype(np.float64) for k, v in rg.items()} if total is None else \
+            {k: total[k] + rg[k] for k in total}
+    pairs = [("means3D", "means3D"), ("means2D", "means2D"), ("colors", "colors"), ("opacities", "opacity"),
+             ("scales", "scales"), ("rotations", "rotations"), ("sh", "sh"), ("language_feature", "lang")]
+    errs = {n: grad_err(g[n].cpu().numpy().reshape(total[o].shape), total[o]) for n, o in pairs}
+    assert all(e <= GRAD_TOL for e in errs.values()), errs
+
+
+@pytest.mark.parametrize("precomp", [False, True])
+def test_backward_views_equals_per_view_sum(precomp):
+    """10 views (two launches of the 8-view kernel), accumulating onto existing buffers: equal to
+    the per-view lsr_backward sum.  precomp: colors_precomp + cov3D_precomp (no SH rows)."""
+    C = 4
+    sc, _ = small_case(P=1200, W=64, H=48, C=C, seed=8)
+    dev = sc.to("cuda")
+    if precomp:
+        dev.cov3D = torch.tensor(oracle.cov3d(sc.scales.numpy(), sc.rotations.numpy())).cuda()
+        dev.colors = torch.rand(sc.means3D.shape[0], 3, generator=torch.Generator().manual_seed(1)).cuda()
+    cams = synthetic.camera_batch(10, 64, 48, seed=8)
+    states = _views_forward(dev, cams, precomp=precomp)
+    g = torch.Generator(device="cpu").manual_seed(2)
+    gcs = [torch.randn(3, 48, 64, generator=g).cuda() for _ in cams]
+    gls = [torch.randn(C, 48, 64, generator=g).cuda() for _ in cams]
+    base = None
+    ref = None
+    for st, gc, gl in zip(states, gcs, gls):
+        one = dgr.backward_native(st, gc, gl)
+        if base is None:
+            base = {k: torch.randn_like(v) for k, v in one.items() if v is not None}
+            ref = {k: v.clone() for k, v in base.items()}
+        for k in ref:
+            ref[k] += one[k]
+    out = {k: v.clone() for k, v in base.items()}
+    got = dgr.backward_views_native(states, gcs, gls, out=out, accumulate=True)
+    for k in ref:
+        assert got[k] is out[k]
+        assert grad_err(got[k].cpu().numpy(), ref[k].cpu().numpy()) <= 1e-5, k
+    with pytest.raises(RuntimeError, match="deterministic"):
+        import ctypes
+        from diff_gaussian_rasterization import _lib
+        L = _lib.load()
+        gi = _lib.BwdIn()
+        gi.dL_dout_color, gi.deterministic = gcs[0].data_ptr(), 1
+        st = states[0]
+        SP, BP = ctypes.POINTER(_lib.Settings), ctypes.POINTER(_lib.BwdIn)
+        vp = ctypes.c_void_p * 1
+        gout = _lib.BwdOut()
+        _lib.check(L.lsr_backward_views(1, (SP * 1)(ctypes.pointer(st.settings.c)), ctypes.byref(st.fin),
+                                        (BP * 1)(ctypes.pointer(gi)), ctypes.byref(gout), vp(st.geom.data_ptr()),
+                                        vp(st.binning.data_ptr()), vp(st.img.data_ptr()), vp(st.geom.data_ptr()),
+                                        (ctypes.c_int64 * 1)(st.num_rendered), 0, None), "lsr_backward_views")
 
 
 def test_full_size_forward_matches_oracle():
