@@ -37,7 +37,6 @@ k_render_bwd_wave(RenderBwdArgs a) {
     __shared__ float4 s_co[WG];
     __shared__ float4 s_rgbd[WG];
     __shared__ float2 s_xy[WG];
-    __shared__ float s_thr[WG];
     __shared__ uint32_t s_gid[WG];
     __shared__ uint32_t s_k[WG];
     __shared__ float s_mom[WG][8];
@@ -210,7 +209,6 @@ k_render_bwd_wave(RenderBwdArgs a) {
             s_xy[lane] = pf_xy;
             s_co[lane] = pf_co;
             s_rgbd[lane] = pf_rgbd;
-            s_thr[lane] = pf_k != 0xFFFFFFFFu ? skip_power(pf_co.w) : __builtin_inff();
         }
         const int e = lane >> 2, c0 = 8 * (lane & 3);
         const float f[8] = {pf_f0.x, pf_f0.y, pf_f0.z, pf_f0.w, pf_f1.x, pf_f1.y, pf_f1.z, pf_f1.w};
@@ -261,39 +259,49 @@ k_render_bwd_wave(RenderBwdArgs a) {
         }
 
         // ---- 4. serial back-to-front replay of the group: w = alpha T, t = G dL/dalpha --------
+        // Per entry, everything but the T / accumulator recurrence is independent of the other
+        // entries: computed branch-free for the whole group first (exp chains overlap), then the
+        // recurrence runs with selects (an inactive entry leaves T and the accumulators unchanged
+        // and gets w = t = 0, as in upstream's skip).
         float wv[WG], tv[WG];
+        constexpr int RB = 4;   // entries per branch-free batch (register budget)
 #pragma unroll
-        for (int e = 0; e < WG; ++e) {
-            wv[e] = 0.0f;
-            tv[e] = 0.0f;
-            if (e >= cnt) continue;                                  // wave-uniform
-            if (s_k[e] < last_contributor) {
-                const float2 xy = s_xy[e];
-                const float4 co = s_co[e];
-                const float dx = xy.x - pxf, dy = xy.y - pyf;
-                const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-                if (power <= 0.0f && power >= s_thr[e]) {
-                    const float G = expf_repro(power);
-                    const float alpha = fminf(0.99f, co.w * G);
-                    if (alpha >= 1.0f / 255.0f) {
-                        const float rom = __builtin_amdgcn_rcpf(1.0f - alpha);
-                        T = T * rom;
-                        const float4 cd = s_rgbd[e];
-                        float dot = cd.x * g0;
-                        dot = __builtin_fmaf(cd.y, g1, dot);
-                        dot = __builtin_fmaf(cd.z, g2, dot);
-                        dot = __builtin_fmaf(cd.w, gD, dot);
-                        dot += S[e];
-                        acc_dot = __builtin_fmaf(last_alpha, last_dot, (1.0f - last_alpha) * acc_dot);
-                        last_dot = dot;
-                        float dL_dalpha = (dot - acc_dot) * T;
-                        last_alpha = alpha;
-                        dL_dalpha = __builtin_fmaf(-T_final * rom, bg_dot, dL_dalpha);
-                        wv[e] = alpha * T;
-                        tv[e] = G * dL_dalpha;
-                    }
-                }
-            }
+        for (int e0 = 0; e0 < WG; e0 += RB) {
+        float Gv[RB], alv[RB], romv[RB], dotv[RB];
+        bool act[RB];
+#pragma unroll
+        for (int u = 0; u < RB; ++u) {
+            const int e = e0 + u;
+            const float2 xy = s_xy[e];
+            const float4 co = s_co[e];
+            const float dx = xy.x - pxf, dy = xy.y - pyf;
+            const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+            Gv[u] = expf_repro(power);
+            alv[u] = fminf(0.99f, co.w * Gv[u]);
+            act[u] = e < cnt && s_k[e] < last_contributor && power <= 0.0f && alv[u] >= 1.0f / 255.0f;
+            romv[u] = __builtin_amdgcn_rcpf(1.0f - alv[u]);
+            const float4 cd = s_rgbd[e];
+            float dot = cd.x * g0;
+            dot = __builtin_fmaf(cd.y, g1, dot);
+            dot = __builtin_fmaf(cd.z, g2, dot);
+            dot = __builtin_fmaf(cd.w, gD, dot);
+            dotv[u] = dot + S[e];
+        }
+#pragma unroll
+        for (int u = 0; u < RB; ++u) {
+            const int e = e0 + u;
+            const bool on = act[u];
+            const float alpha = alv[u], rom = romv[u], dot = dotv[u];
+            T = on ? T * rom : T;
+            const float acc_new = __builtin_fmaf(last_alpha, last_dot, (1.0f - last_alpha) * acc_dot);
+            acc_dot = on ? acc_new : acc_dot;
+            last_dot = on ? dot : last_dot;
+            last_alpha = on ? alpha : last_alpha;
+            float dL_dalpha = (dot - acc_dot) * T;
+            dL_dalpha = __builtin_fmaf(-T_final * rom, bg_dot, dL_dalpha);
+            wv[e] = on ? alpha * T : 0.0f;
+            tv[e] = on ? Gv[u] * dL_dalpha : 0.0f;
+        }
         }
 
         // ---- 5. sums over the wave's pixels on matrix cores -----------------------------------
@@ -355,7 +363,11 @@ k_render_bwd_wave(RenderBwdArgs a) {
         }
         // ---- 6. atomics: language rows straight from the MFMA layout (4 entries x 16 channels per
         //      instruction), then the 10 scalars of each entry, consecutive lanes on one record --
+#ifdef LSR_ABL_NOLANGATOM
+        if (false) {
+#else
         if (a.acc_lang) {
+#endif
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int e = 4 * g4 + i;
@@ -393,7 +405,9 @@ k_render_bwd_wave(RenderBwdArgs a) {
             const int idx = lane + 64 * r, e = idx / 10, q = idx - 10 * e;
             if (idx < cnt * 10) {
                 const float v = s_q[e][q];
+#ifndef LSR_ABL_NOSMALLATOM
                 if (v != 0.0f) atomicAdd(a.acc_small + (size_t)s_gid[e] * 12 + q, v);
+#endif
             }
         }
         wave_lds_sync();

@@ -22,7 +22,6 @@ __global__ void __launch_bounds__(64) k_render_fwd_wave(RenderFwdArgs a) {
     __shared__ float4 s_co[GF];
     __shared__ float4 s_rgbd[GF];
     __shared__ float2 s_xy[GF];
-    __shared__ float s_thr[GF];
     __shared__ uint32_t s_k[GF];
     __shared__ __attribute__((aligned(16))) float s_lang[GF * LP];
     __shared__ uint32_t s_fk[FIFO];
@@ -85,7 +84,6 @@ __global__ void __launch_bounds__(64) k_render_fwd_wave(RenderFwdArgs a) {
             s_xy[lane] = ok ? a.xy[gid] : make_float2(0.0f, 0.0f);
             s_co[lane] = co;
             s_rgbd[lane] = ok ? a.rgbd[gid] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            s_thr[lane] = ok ? skip_power(co.w) : __builtin_inff();
         }
         if constexpr (CPAD > 0) {
             if (C == CPAD) {   // whole rows as float4, every load in flight at once
@@ -112,37 +110,60 @@ __global__ void __launch_bounds__(64) k_render_fwd_wave(RenderFwdArgs a) {
         }
         head += cnt;
         wave_lds_sync();
-        // ---- 3. composite the group in list order --------------------------------------------
-        for (int e = 0; e < cnt; ++e) {
-            if (done) continue;
-            const float2 xy = s_xy[e];
-            const float4 co = s_co[e];
-            const float dx = xy.x - pxf, dy = xy.y - pyf;
-            const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-            if (power > 0.0f || power < s_thr[e]) continue;   // the second test never changes a decision
-            const float alpha = fminf(0.99f, co.w * expf_repro(power));
-            if (alpha < 1.0f / 255.0f) continue;
-            const float test_T = T * (1.0f - alpha);
-            if (test_T < 0.0001f) { done = true; continue; }
-            const float w = alpha * T;
-            const float4 cd = s_rgbd[e];
-            acc[0] = __builtin_fmaf(cd.x, w, acc[0]);
-            acc[1] = __builtin_fmaf(cd.y, w, acc[1]);
-            acc[2] = __builtin_fmaf(cd.z, w, acc[2]);
-            accD = __builtin_fmaf(cd.w, w, accD);
-            if constexpr (CPAD > 0) {
-                const float4* f4 = reinterpret_cast<const float4*>(s_lang + e * CPAD);
+        // ---- 3. composite the group in list order, FB entries at a time: the per-entry alphas are
+        //      independent of T, so they are computed branch-free for the whole batch first (their
+        //      exp chains overlap); then the serial front-to-back update uses selects, with the
+        //      channel accumulation skipped only when no lane of the wave blends the entry.
+        //      Per pixel the arithmetic and its order are upstream's (a skipped entry adds exact
+        //      zeros nowhere: its accumulation is not executed or has w = 0 and is not applied).
+        constexpr int FB = 8;
+        for (int e0 = 0; e0 < cnt; e0 += FB) {
+            float al[FB];
+            bool ok[FB];
 #pragma unroll
-                for (int c4 = 0; c4 < CPAD / 4; ++c4) {
-                    const float4 f = f4[c4];
-                    accL[4 * c4 + 0] = __builtin_fmaf(f.x, w, accL[4 * c4 + 0]);
-                    accL[4 * c4 + 1] = __builtin_fmaf(f.y, w, accL[4 * c4 + 1]);
-                    accL[4 * c4 + 2] = __builtin_fmaf(f.z, w, accL[4 * c4 + 2]);
-                    accL[4 * c4 + 3] = __builtin_fmaf(f.w, w, accL[4 * c4 + 3]);
-                }
+            for (int u = 0; u < FB; ++u) {
+                const int e = e0 + u;
+                const float2 xy = s_xy[e];
+                const float4 co = s_co[e];
+                const float dx = xy.x - pxf, dy = xy.y - pyf;
+                const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+                al[u] = fminf(0.99f, co.w * expf_repro(power));
+                ok[u] = e < cnt && power <= 0.0f && al[u] >= 1.0f / 255.0f;
             }
-            T = test_T;
-            last = s_k[e] + 1;
+#pragma unroll
+            for (int u = 0; u < FB; ++u) {
+                const float alpha = al[u];
+                const float test_T = T * (1.0f - alpha);
+                bool blend = ok[u] && !done;
+                done = done || (blend && test_T < 0.0001f);
+                blend = blend && !done;
+                if (!__any(blend)) continue;                       // wave-uniform
+                const int e = e0 + u;
+                const float w = blend ? alpha * T : 0.0f;   // w = 0: fma(c, 0, acc) == acc
+                const float4 cd = s_rgbd[e];
+                acc[0] = __builtin_fmaf(cd.x, w, acc[0]);
+                acc[1] = __builtin_fmaf(cd.y, w, acc[1]);
+                acc[2] = __builtin_fmaf(cd.z, w, acc[2]);
+                accD = __builtin_fmaf(cd.w, w, accD);
+#ifdef LSR_ABL_NOLANGACC
+                if constexpr (false) {
+#else
+                if constexpr (CPAD > 0) {
+#endif
+                    const float4* f4 = reinterpret_cast<const float4*>(s_lang + e * CPAD);
+#pragma unroll
+                    for (int c4 = 0; c4 < CPAD / 4; ++c4) {
+                        const float4 f = f4[c4];
+                        accL[4 * c4 + 0] = __builtin_fmaf(f.x, w, accL[4 * c4 + 0]);
+                        accL[4 * c4 + 1] = __builtin_fmaf(f.y, w, accL[4 * c4 + 1]);
+                        accL[4 * c4 + 2] = __builtin_fmaf(f.z, w, accL[4 * c4 + 2]);
+                        accL[4 * c4 + 3] = __builtin_fmaf(f.w, w, accL[4 * c4 + 3]);
+                    }
+                }
+                T = blend ? test_T : T;
+                last = blend ? s_k[e] + 1 : last;
+            }
+            if (__all(done)) break;
         }
         wave_lds_sync();
     }
