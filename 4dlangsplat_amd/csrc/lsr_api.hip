@@ -178,7 +178,7 @@ Scratch carve_scratch(void* base, size_t P, size_t K, int recq, bool det, size_t
         s.rec = c.take<float>(K * (size_t)recq);
         s.flags = c.take<uint8_t>(K);
     } else {
-        s.acc_small = c.take<float>(P * 12);
+        s.acc_small = c.take<float>(P * lsr::ACC_PITCH);
     }
     if (bytes) *bytes = c.off;
     return s;
@@ -400,7 +400,7 @@ int lsr_backward(const lsr_settings* s, const lsr_fwd_in* in, const lsr_bwd_in* 
         LSR_HIP(hipMemsetAsync(sc.flags, 0, K, st));
         lsr::launch_scatter_inst_off(P, g.val_a, g.offsets, g.counts, g.inst_off, st);
     }
-    if (!det) LSR_HIP(hipMemsetAsync(sc.acc_small, 0, sizeof(float) * 12 * (size_t)P, st));
+    if (!det) LSR_HIP(hipMemsetAsync(sc.acc_small, 0, sizeof(float) * lsr::ACC_PITCH * (size_t)P, st));
     // dL/dlanguage: the atomic path adds into it, so zero it unless accumulating; with the language
     // channels off (include_feature = 0) it is exactly zero (the deterministic path writes it only
     // when they are on)
@@ -470,7 +470,7 @@ int lsr_backward_composite(const lsr_settings* s, const lsr_fwd_in* in, const ls
     Img m = carve_img(const_cast<void*>(img), W, H, nullptr);
     const int recq = lsr::record_floats(s->include_feature ? C : 0);
     Scratch sc = carve_scratch(scratch, (size_t)P, K > 0 ? K : 1, recq, false, nullptr);
-    LSR_HIP(hipMemsetAsync(sc.acc_small, 0, sizeof(float) * 12 * (size_t)P, st));
+    LSR_HIP(hipMemsetAsync(sc.acc_small, 0, sizeof(float) * lsr::ACC_PITCH * (size_t)P, st));
     if (K == 0) return LSR_OK;
     lsr::RenderBwdArgs r{};
     r.W = W; r.H = H; r.grid_x = gx; r.grid_y = gy; r.C = C; r.include_feature = s->include_feature;

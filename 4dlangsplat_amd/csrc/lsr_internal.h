@@ -5,6 +5,11 @@
 
 namespace lsr {
 
+// Pitch (floats) of the per-Gaussian screen-space gradient accumulators of the atomic backward
+// ([P, ACC_PITCH], fields 0..9 used: rgb 0-2, depth 3, mean2D 4-5, conic 6-8, opacity 9): 64-byte
+// records, so the atomics of one entry are one 64-byte memory-side request.
+constexpr int ACC_PITCH = 16;
+
 struct PreprocessArgs {
     int P, M, deg, W, H, grid_x, grid_y;
     float tanfovx, tanfovy, focal_x, focal_y, scale_modifier;
@@ -200,6 +205,7 @@ void launch_render_fwd(const RenderFwdArgs& a, hipStream_t st);
 void launch_render_bwd(const RenderBwdArgs& a, hipStream_t st);
 void launch_render_bwd_mfma(const RenderBwdArgs& a, hipStream_t st);
 void launch_render_fwd_wave(const RenderFwdArgs& a, hipStream_t st);
+void launch_render_fwd_wave_mfma(const RenderFwdArgs& a, hipStream_t st);   // 17..32 channels
 void launch_render_bwd_wave(const RenderBwdArgs& a, hipStream_t st);
 
 }  // namespace lsr

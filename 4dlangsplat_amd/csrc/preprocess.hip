@@ -501,7 +501,7 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
 #pragma unroll
         for (int k = 0; k < 12; ++k) rs[k] = 0.0f;
         if (vis && !a.deterministic) {
-            const float4* r4 = reinterpret_cast<const float4*>(a.acc_small + (size_t)i * 12);
+            const float4* r4 = reinterpret_cast<const float4*>(a.acc_small + (size_t)i * ACC_PITCH);
 #pragma unroll
             for (int k4 = 0; k4 < 3; ++k4) {
                 const float4 v = r4[k4];
@@ -672,7 +672,7 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd_views(PreprocessBwdViews
                 if (!((vmask >> v) & 1u)) continue;
                 const ViewCam& cm = a.cam[v];
                 float rs[12];
-                const float4* r4 = reinterpret_cast<const float4*>(cm.acc_small + (size_t)i * 12);
+                const float4* r4 = reinterpret_cast<const float4*>(cm.acc_small + (size_t)i * ACC_PITCH);
 #pragma unroll
                 for (int k4 = 0; k4 < 3; ++k4) {
                     const float4 t = r4[k4];

@@ -205,7 +205,7 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
                 const int j = e / RECQ, q = e - j * RECQ;
                 if (!s_act[j] || q == 10 || q == 11) continue;
                 const uint32_t gid = s_id[j];
-                if (q < 12) atomicAdd(a.acc_small + (size_t)gid * 12 + q, s_rec[e]);
+                if (q < 12) atomicAdd(a.acc_small + (size_t)gid * ACC_PITCH + q, s_rec[e]);
                 else if (a.acc_lang && q - 12 < C) atomicAdd(a.acc_lang + (size_t)gid * C + (q - 12), s_rec[e]);
             }
         }

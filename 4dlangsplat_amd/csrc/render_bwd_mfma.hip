@@ -317,7 +317,7 @@ __global__ void __launch_bounds__(256, 3) k_render_bwd_mfma(RenderBwdArgs a) {
             const int j = e / (RQ + 32), q = e - j * (RQ + 32);
             if (!s_act[j]) continue;
             const uint32_t gid = s_id[j];
-            if (q < 10) atomicAdd(a.acc_small + (size_t)gid * 12 + q, s_rec[j][q]);
+            if (q < 10) atomicAdd(a.acc_small + (size_t)gid * ACC_PITCH + q, s_rec[j][q]);
             else if (q >= RQ && q - RQ < C && a.acc_lang) atomicAdd(a.acc_lang + (size_t)gid * C + (q - RQ), s_lrec[j][q - RQ]);
         }
     }

@@ -406,7 +406,7 @@ k_render_bwd_wave(RenderBwdArgs a) {
             if (idx < cnt * 10) {
                 const float v = s_q[e][q];
 #ifndef LSR_ABL_NOSMALLATOM
-                if (v != 0.0f) atomicAdd(a.acc_small + (size_t)s_gid[e] * 12 + q, v);
+                if (v != 0.0f) atomicAdd(a.acc_small + (size_t)s_gid[e] * ACC_PITCH + q, v);
 #endif
             }
         }

@@ -1,0 +1,258 @@
+// render_fwd_mfma_wave.hip -- front-to-back compositing for 17..32 language channels, the channel
+// sums on matrix cores.
+//
+// Same waves, entry compaction and per-pixel arithmetic as k_render_fwd_wave (render_fwd_wave.hip;
+// upstream renderCUDA): one independent wave per 8x8 quadrant, the tile
+// list scanned front to back with the conservative ellipse-vs-quadrant test, groups of 32
+// compacted entries staged in LDS.  T, the contributor count, RGB and depth stay per-pixel fp32
+// VALU arithmetic in upstream's order (so n_contrib, final_T and the colour are those of the
+// scalar kernel).  The language channels are the dense part: per group,
+//     L[c][p] += sum_e F[e][c] w[e][p],      w = alpha T (0 where the entry does not blend)
+// a [32 channels x 32 entries] x [32 entries x 64 pixels] product, 8 v_mfma_f32_16x16x32_bf16
+// blocks, each operand split in bf16 hi + lo (three products, ~2^-17 relative, fp32
+// accumulation; lsr_mfma.h).  A = F^T comes from the group's bf16 rows [e][c] in LDS through
+// transposing reads; B = w is built in registers: each lane packs its pixel's 32 weights in four
+// octets and a 4x4 lane-group transpose (permlane swaps) hands every lane the octet of the pixel
+// its B fragment needs.  This takes the 32 per-entry channel FMAs off the VALU.
+#include "lsr_common.h"
+#include "lsr_internal.h"
+#include "lsr_mfma.h"
+
+namespace lsr {
+
+namespace {
+constexpr int MG = 32;      // entries per group (= MFMA K)
+constexpr int MFP = 40;     // F row pitch in bf16: 32 channels + 8 (80-byte rows)
+constexpr int MFIFO = 128;  // compacted entries waiting; power of two
+
+// pack 8 weights as bf16 hi / lo octets
+__device__ __forceinline__ void pack_octet(const float (&w)[8], bf16x8& h, bf16x8& l) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        __bf16 hh, ll;
+        split_bf16(w[j], hh, ll);
+        h[j] = hh;
+        l[j] = ll;
+    }
+}
+
+// lane group g holds octets x[0..3] (one per entry octet o) of its own pixel; afterwards it holds
+// in x[nb] the octet g of pixel 16 nb + (lane & 15): the MFMA B fragments, nb = pixel block
+__device__ __forceinline__ void octets_to_b(bf16x8 (&x)[4]) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {   // per dword of the octets
+        float t[4];
+#pragma unroll
+        for (int o = 0; o < 4; ++o) t[o] = __builtin_bit_cast(f4v, x[o])[d];
+        transpose_lane_groups(t);
+#pragma unroll
+        for (int o = 0; o < 4; ++o) {
+            f4v v = __builtin_bit_cast(f4v, x[o]);
+            v[d] = t[o];
+            x[o] = __builtin_bit_cast(bf16x8, v);
+        }
+    }
+}
+}  // namespace
+
+__global__ void __launch_bounds__(64) k_render_fwd_wave_mfma(RenderFwdArgs a) {
+    __shared__ float4 s_co[MG];
+    __shared__ float4 s_rgbd[MG];
+    __shared__ float2 s_xy[MG];
+    __shared__ uint32_t s_k[MG];
+    __shared__ __attribute__((aligned(16))) __bf16 s_Fh[MG * MFP];
+    __shared__ __attribute__((aligned(16))) __bf16 s_Fl[MG * MFP];
+    __shared__ uint32_t s_fk[MFIFO];
+    __shared__ uint32_t s_fg[MFIFO];
+
+    const int b = blockIdx.x;
+    const int tile = (b >> 5) * 8 + (b & 7), quad = (b >> 3) & 3;
+    if (tile >= a.grid_x * a.grid_y) return;
+    const int lane = threadIdx.x, g4 = lane >> 4, l16 = lane & 15;
+    const int tx = tile % a.grid_x, ty = tile / a.grid_x;
+    const int qx0 = tx * LSR_TILE_X + (quad & 1) * 8, qy0 = ty * LSR_TILE_Y + (quad >> 1) * 8;
+    const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
+    const bool inside = px < a.W && py < a.H;
+    const float pxf = (float)px, pyf = (float)py;
+    const uint2 range = a.ranges[tile];
+    const int C = a.C;
+    const float bx0 = (float)qx0, bx1 = (float)min(qx0 + 7, a.W - 1);
+    const float by0 = (float)qy0, by1 = (float)min(qy0 + 7, a.H - 1);
+
+    float T = 1.0f;
+    uint32_t last = 0;
+    float acc[3] = {0.0f, 0.0f, 0.0f};
+    float accD = 0.0f;
+    f32x4 L[2][4];   // L[mb][nb]: channels 16 mb + 4 g4 + i, pixels 16 nb + l16
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) L[mb][nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    bool done = !inside;
+
+    uint32_t pos = range.x;  // list entries [pos, range.y) not yet scanned
+    int head = 0, tail = 0;  // FIFO counters (wave-uniform)
+    uint32_t gid_next = pos + lane < range.y ? a.point_list[pos + lane] : 0u;
+    while (!__all(done)) {
+        // ---- 1. scan + compaction (as k_render_fwd_wave) --------------------------------------
+        while (tail - head < MG && pos < range.y) {
+            const uint32_t idx = pos + lane;
+            const uint32_t gid = gid_next;
+            gid_next = idx + 64 < range.y ? a.point_list[idx + 64] : 0u;
+            bool cand = false;
+            if (idx < range.y) cand = quad_may_touch(a.xy[gid], a.conic_o[gid], bx0, bx1, by0, by1);
+            const uint64_t m = __ballot(cand);
+            if (cand) {
+                const int s = (tail + __popcll(m & lanemask_lt())) & (MFIFO - 1);
+                s_fk[s] = idx - range.x;
+                s_fg[s] = gid;
+            }
+            tail += __popcll(m);
+            pos += 64;
+        }
+        const int cnt = min(MG, tail - head);
+        if (cnt == 0) break;
+        wave_lds_sync();
+        // ---- 2. stage the group: geometry, and the language rows as bf16 hi / lo -------------
+        if (lane < MG) {
+            const bool ok = lane < cnt;
+            const int s = (head + lane) & (MFIFO - 1);
+            const uint32_t gid = ok ? s_fg[s] : 0u;
+            s_k[lane] = ok ? s_fk[s] : 0u;
+            s_xy[lane] = ok ? a.xy[gid] : make_float2(0.0f, 0.0f);
+            s_co[lane] = ok ? a.conic_o[gid] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            s_rgbd[lane] = ok ? a.rgbd[gid] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        }
+        {
+            // lane -> entry lane / 2, channels 16 (lane & 1) .. +15: four float4 loads in flight
+            const int e = lane >> 1, c0 = 16 * (lane & 1);
+            const bool ok = e < cnt;
+            const uint32_t gid = ok ? s_fg[(head + e) & (MFIFO - 1)] : 0u;
+            float f[16];
+            if (C == 32) {
+                const float4* r = reinterpret_cast<const float4*>(a.lang + (size_t)gid * 32 + c0);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 v = ok ? r[q] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                    f[4 * q] = v.x; f[4 * q + 1] = v.y; f[4 * q + 2] = v.z; f[4 * q + 3] = v.w;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) f[j] = (ok && c0 + j < C) ? a.lang[(size_t)gid * C + c0 + j] : 0.0f;
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                bf16x8 vh, vl;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    __bf16 hh, ll;
+                    split_bf16(f[8 * h + j], hh, ll);
+                    vh[j] = hh;
+                    vl[j] = ll;
+                }
+                *reinterpret_cast<bf16x8*>(s_Fh + e * MFP + c0 + 8 * h) = vh;
+                *reinterpret_cast<bf16x8*>(s_Fl + e * MFP + c0 + 8 * h) = vl;
+            }
+        }
+        head += cnt;
+        wave_lds_sync();
+        // ---- 3. per pixel, front to back: alphas of 8 entries branch-free, then the serial
+        //      update with selects (as k_render_fwd_wave); the weights go to octets ----------------
+        bf16x8 oh[4], ol[4];
+#pragma unroll
+        for (int o = 0; o < 4; ++o) {
+            float w8[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) w8[u] = 0.0f;
+            if (8 * o < cnt && !__all(done)) {                    // wave-uniform
+                float al[8];
+                bool ok[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int e = 8 * o + u;
+                    const float2 xy = s_xy[e];
+                    const float4 co = s_co[e];
+                    const float dx = xy.x - pxf, dy = xy.y - pyf;
+                    const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+                    al[u] = fminf(0.99f, co.w * expf_repro(power));
+                    ok[u] = e < cnt && power <= 0.0f && al[u] >= 1.0f / 255.0f;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int e = 8 * o + u;
+                    const float alpha = al[u];
+                    const float test_T = T * (1.0f - alpha);
+                    bool blend = ok[u] && !done;
+                    done = done || (blend && test_T < 0.0001f);
+                    blend = blend && !done;
+                    const float w = blend ? alpha * T : 0.0f;   // w = 0: fma(c, 0, acc) == acc
+                    const float4 cd = s_rgbd[e];
+                    acc[0] = __builtin_fmaf(cd.x, w, acc[0]);
+                    acc[1] = __builtin_fmaf(cd.y, w, acc[1]);
+                    acc[2] = __builtin_fmaf(cd.z, w, acc[2]);
+                    accD = __builtin_fmaf(cd.w, w, accD);
+                    w8[u] = w;
+                    T = blend ? test_T : T;
+                    last = blend ? s_k[e] + 1 : last;
+                }
+            }
+            pack_octet(w8, oh[o], ol[o]);
+        }
+        // ---- 4. language channels on matrix cores -----------------------------------------------
+        octets_to_b(oh);
+        octets_to_b(ol);
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) {
+            // A[m = channel 16 mb + l16][k = entry 8 g4 + j] from the rows [e][c]
+            const int off = (8 * g4 + (l16 >> 2)) * MFP + 16 * mb + 4 * (l16 & 3);
+            const bf16x8 ah = __builtin_shufflevector(ds_read_tr16(s_Fh + off), ds_read_tr16(s_Fh + off + 4 * MFP),
+                                                      0, 1, 2, 3, 4, 5, 6, 7);
+            const bf16x8 alo = __builtin_shufflevector(ds_read_tr16(s_Fl + off), ds_read_tr16(s_Fl + off + 4 * MFP),
+                                                       0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb) {
+                L[mb][nb] = LSR_MFMA16(ah, oh[nb], L[mb][nb]);
+                L[mb][nb] = LSR_MFMA16(ah, ol[nb], L[mb][nb]);
+                L[mb][nb] = LSR_MFMA16(alo, oh[nb], L[mb][nb]);
+            }
+        }
+        wave_lds_sync();   // the group's LDS rows are read before the next staging
+    }
+    if (inside) {
+        const size_t HW = (size_t)a.H * a.W, pid = (size_t)py * a.W + px;
+        a.final_T[pid] = T;
+        a.n_contrib[pid] = last;
+        a.out_color[pid] = acc[0] + T * a.bg[0];
+        a.out_color[HW + pid] = acc[1] + T * a.bg[1];
+        a.out_color[2 * HW + pid] = acc[2] + T * a.bg[2];
+        a.out_depth[pid] = accD;
+    }
+    {   // language: block (mb, nb), register i -> channel 16 mb + 4 g4 + i, pixel 16 nb + l16
+        const size_t HW = (size_t)a.H * a.W;
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb) {
+            const int p = 16 * nb + l16, qx = qx0 + (p & 7), qy = qy0 + (p >> 3);
+            if (qx >= a.W || qy >= a.H) continue;
+            const size_t pid = (size_t)qy * a.W + qx;
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int c = 16 * mb + 4 * g4 + i;
+                    if (c < C) a.out_lang[(size_t)c * HW + pid] = L[mb][nb][i];
+                }
+        }
+    }
+    uint32_t m = last;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+    if (lane == 0 && m > 0) atomicMax(a.tile_max_contrib + tile, m);
+}
+
+void launch_render_fwd_wave_mfma(const RenderFwdArgs& a, hipStream_t st) {
+    const int ntiles = a.grid_x * a.grid_y;
+    hipLaunchKernelGGL(k_render_fwd_wave_mfma, dim3(((ntiles + 7) / 8) * 32), dim3(64), 0, st, a);
+}
+
+}  // namespace lsr

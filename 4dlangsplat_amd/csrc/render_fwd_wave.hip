@@ -201,7 +201,11 @@ void launch_render_fwd_wave(const RenderFwdArgs& a, hipStream_t st) {
         case 4: go_fwd_wave<4>(a, st); break;
         case 8: go_fwd_wave<8>(a, st); break;
         case 16: go_fwd_wave<16>(a, st); break;
+#ifdef LSR_FWD_VALU32
         case 32: go_fwd_wave<32>(a, st); break;
+#else
+        case 32: launch_render_fwd_wave_mfma(a, st); break;   // channel sums on matrix cores
+#endif
         default: go_fwd_wave<64>(a, st); break;
     }
 }
