@@ -1,0 +1,362 @@
+"""Gaussian scene I/O and the per-view render() of the reference, on the MI355X rasterizer.
+
+SURVEY.md 8(f) row 2 (and 8(a) row a1).  Restates, from the reference:
+  * the parameter layout and activations of GaussianModel   scene/gaussian_model.py:31-46,168-172
+  * its PLY format (attribute list, order, float32 vertex element)
+                                                             scene/gaussian_model.py:331-345,370-389,396-444
+  * render(): settings, stage logic, deformation, activations, rasterizer call, output dict
+                                                             gaussian_renderer/__init__.py:19-248
+  * render.py's per-frame loop: FPS print, renders_npy/{idx:05d}.npy as [H, W, C], PCA of
+    language maps with C > 3 for the PNGs                    render.py:52-65,67-161
+The reference reads and writes PLY with `plyfile` (not installed here); this module parses and
+writes the same binary_little_endian vertex element itself (numpy structured arrays).  The
+rasterizer is diff_gaussian_rasterization (liblsr.so) and the deformation the HIP
+DeformationField (deformation.py): no CPU fallback.
+"""
+from __future__ import annotations
+
+import math
+import os
+import time as _time
+import zlib
+import struct
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+_PLY_TYPES = {"float": "f4", "float32": "f4", "double": "f8", "float64": "f8", "uchar": "u1", "uint8": "u1",
+              "char": "i1", "int8": "i1", "ushort": "u2", "uint16": "u2", "short": "i2", "int16": "i2",
+              "uint": "u4", "uint32": "u4", "int": "i4", "int32": "i4"}
+
+
+@dataclass
+class GaussianScene:
+    """Raw (pre-activation) Gaussian parameters, the reference's GaussianModel tensors
+    (_xyz, _features_dc, _features_rest, _language_feature, _opacity, _scaling, _rotation)."""
+    xyz: torch.Tensor                 # [P, 3]
+    features_dc: torch.Tensor         # [P, 1, 3]
+    features_rest: torch.Tensor       # [P, (deg+1)^2 - 1, 3]
+    language_feature: torch.Tensor    # [P, C]
+    opacity: torch.Tensor             # [P, 1] logit
+    scaling: torch.Tensor             # [P, 3] log scale
+    rotation: torch.Tensor            # [P, 4] unnormalised quaternion (r, x, y, z)
+    max_sh_degree: int = 3
+    active_sh_degree: int = 3
+    deformation: Optional[object] = None   # deformation.DeformationField for the 'fine' stages
+    extra: Dict[str, np.ndarray] = field(default_factory=dict)
+
+    @property
+    def P(self) -> int:
+        return self.xyz.shape[0]
+
+    # activations: gaussian_model.py:38-46 (exp, normalize, sigmoid)
+    @property
+    def get_xyz(self):
+        return self.xyz
+
+    @property
+    def get_features(self):
+        return torch.cat((self.features_dc, self.features_rest), dim=1)
+
+    @property
+    def get_scaling(self):
+        return torch.exp(self.scaling)
+
+    @property
+    def get_rotation(self):
+        return torch.nn.functional.normalize(self.rotation)
+
+    @property
+    def get_opacity(self):
+        return torch.sigmoid(self.opacity)
+
+    @property
+    def get_language_feature(self):
+        return self.language_feature
+
+    def to(self, device):
+        t = lambda x: x.to(device)   # noqa: E731
+        return GaussianScene(t(self.xyz), t(self.features_dc), t(self.features_rest), t(self.language_feature),
+                             t(self.opacity), t(self.scaling), t(self.rotation), self.max_sh_degree,
+                             self.active_sh_degree, self.deformation, dict(self.extra))
+
+    # ---- PLY (gaussian_model.py:331-345 attribute list, :370-389 save, :396-444 load) ---------
+    def attribute_names(self) -> List[str]:
+        names = ["x", "y", "z", "nx", "ny", "nz"]
+        names += [f"f_dc_{i}" for i in range(self.features_dc.shape[1] * self.features_dc.shape[2])]
+        names += [f"f_rest_{i}" for i in range(self.features_rest.shape[1] * self.features_rest.shape[2])]
+        names += [f"f_lang_{i}" for i in range(self.language_feature.shape[1])]
+        names += ["opacity"]
+        names += [f"scale_{i}" for i in range(self.scaling.shape[1])]
+        names += [f"rot_{i}" for i in range(self.rotation.shape[1])]
+        return names
+
+    def save_ply(self, path: str) -> None:
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        c = lambda x: x.detach().float().cpu().numpy()   # noqa: E731
+        xyz = c(self.xyz)
+        # features are stored channel-major: transpose(1, 2).flatten (gaussian_model.py:375-376)
+        f_dc = c(self.features_dc.transpose(1, 2).flatten(start_dim=1))
+        f_rest = c(self.features_rest.transpose(1, 2).flatten(start_dim=1))
+        cols = np.concatenate([xyz, np.zeros_like(xyz), f_dc, f_rest, c(self.language_feature), c(self.opacity),
+                               c(self.scaling), c(self.rotation)], axis=1).astype(np.float32)
+        write_ply_vertices(path, self.attribute_names(), cols)
+
+    @classmethod
+    def load_ply(cls, path: str, max_sh_degree: int = 3, device="cpu") -> "GaussianScene":
+        v = read_ply_vertices(path)
+        P = len(v["x"])
+        col = lambda n: np.asarray(v[n], dtype=np.float32)   # noqa: E731
+
+        def group(prefix):
+            names = sorted((n for n in v if n.startswith(prefix)), key=lambda n: int(n.split("_")[-1]))
+            return np.stack([col(n) for n in names], axis=1) if names else np.zeros((P, 0), np.float32)
+
+        xyz = np.stack([col("x"), col("y"), col("z")], axis=1)
+        f_dc = np.stack([col("f_dc_0"), col("f_dc_1"), col("f_dc_2")], axis=1)[:, :, None]      # [P, 3, 1]
+        rest = group("f_rest_")
+        n_rest = 3 * (max_sh_degree + 1) ** 2 - 3
+        if rest.shape[1] != n_rest:
+            raise ValueError(f"{path}: {rest.shape[1]} f_rest_* attributes, expected {n_rest} for SH degree "
+                             f"{max_sh_degree}")
+        rest = rest.reshape(P, 3, (max_sh_degree + 1) ** 2 - 1)
+        t = lambda a: torch.tensor(a, dtype=torch.float32, device=device)   # noqa: E731
+        return cls(xyz=t(xyz), features_dc=t(f_dc).transpose(1, 2).contiguous(),
+                   features_rest=t(rest).transpose(1, 2).contiguous(), language_feature=t(group("f_lang_")),
+                   opacity=t(col("opacity"))[:, None], scaling=t(group("scale_")), rotation=t(group("rot")),
+                   max_sh_degree=max_sh_degree, active_sh_degree=max_sh_degree)
+
+
+def write_ply_vertices(path: str, names: List[str], cols: np.ndarray) -> None:
+    """binary_little_endian PLY with one float32 `vertex` element (what plyfile writes for the
+    reference's save_ply)."""
+    cols = np.ascontiguousarray(cols, dtype="<f4")
+    if cols.ndim != 2 or cols.shape[1] != len(names):
+        raise ValueError("one column per attribute name")
+    header = ["ply", "format binary_little_endian 1.0", f"element vertex {cols.shape[0]}"]
+    header += [f"property float {n}" for n in names]
+    header += ["end_header"]
+    with open(path, "wb") as f:
+        f.write(("\n".join(header) + "\n").encode("ascii"))
+        f.write(cols.tobytes())
+
+
+def read_ply_vertices(path: str) -> Dict[str, np.ndarray]:
+    """The `vertex` element of a PLY file (binary little/big endian or ascii; scalar properties)."""
+    with open(path, "rb") as f:
+        if f.readline().strip() != b"ply":
+            raise ValueError(f"{path}: not a PLY file")
+        fmt, elements, cur = None, [], None
+        while True:
+            line = f.readline()
+            if not line:
+                raise ValueError(f"{path}: no end_header")
+            tok = line.decode("ascii", "replace").split()
+            if not tok or tok[0] in ("comment", "obj_info"):
+                continue
+            if tok[0] == "end_header":
+                break
+            if tok[0] == "format":
+                fmt = tok[1]
+            elif tok[0] == "element":
+                cur = [tok[1], int(tok[2]), []]
+                elements.append(cur)
+            elif tok[0] == "property":
+                if tok[1] == "list":
+                    raise ValueError(f"{path}: list properties are not supported")
+                cur[2].append((tok[2], _PLY_TYPES[tok[1]]))
+        out = None
+        for name, count, props in elements:
+            if fmt == "ascii":
+                rows = [f.readline().split() for _ in range(count)]
+                arr = np.array(rows, dtype=np.float64).reshape(count, len(props)) if count else \
+                    np.zeros((0, len(props)))
+                data = {p: arr[:, i].astype(t) for i, (p, t) in enumerate(props)}
+            else:
+                end = "<" if fmt == "binary_little_endian" else ">"
+                dt = np.dtype([(p, end + t) for p, t in props])
+                rec = np.frombuffer(f.read(dt.itemsize * count), dtype=dt, count=count)
+                data = {p: rec[p].astype(rec[p].dtype.newbyteorder("=")) for p, _ in props}
+            if name == "vertex":
+                out = data
+                break
+        if out is None:
+            raise ValueError(f"{path}: no vertex element")
+        return out
+
+
+# ---- render(): gaussian_renderer/__init__.py:19-248 -----------------------------------------------
+def render(viewpoint_camera, pc: GaussianScene, bg_color: torch.Tensor, scaling_modifier: float = 1.0,
+           override_color=None, stage: str = "fine-lang", compute_cov3D_python: bool = False,
+           convert_SHs_python: bool = False, debug: bool = False, nonormalized: bool = False,
+           language_feature_hiddendim: int = 3):
+    """The reference's render() on this build's rasterizer.  viewpoint_camera: FoVx, FoVy,
+    image_width, image_height, world_view_transform, full_proj_transform, camera_center, time
+    (synthetic.Camera or the reference Camera).  Environment switches of the reference
+    (nonormalized, language_feature_hiddendim) are arguments here."""
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+
+    dev = pc.xyz.device
+    screenspace_points = torch.zeros_like(pc.get_xyz, requires_grad=True, device=dev) + 0
+    try:
+        screenspace_points.retain_grad()
+    except RuntimeError:
+        pass
+    means3D = pc.get_xyz
+    include_feature = "base" not in stage
+    raster_settings = GaussianRasterizationSettings(
+        image_height=int(viewpoint_camera.image_height), image_width=int(viewpoint_camera.image_width),
+        tanfovx=math.tan(viewpoint_camera.FoVx * 0.5), tanfovy=math.tan(viewpoint_camera.FoVy * 0.5),
+        bg=bg_color, scale_modifier=scaling_modifier, viewmatrix=viewpoint_camera.world_view_transform.to(dev),
+        projmatrix=viewpoint_camera.full_proj_transform.to(dev), sh_degree=pc.active_sh_degree,
+        campos=viewpoint_camera.camera_center.to(dev), prefiltered=False, debug=debug,
+        include_feature=include_feature)
+    t = torch.tensor(float(viewpoint_camera.time), device=dev).repeat(means3D.shape[0], 1)
+    rasterizer = GaussianRasterizer(raster_settings=raster_settings)
+    opacity = pc.opacity
+    shs = pc.get_features
+    if include_feature:
+        lang = pc.get_language_feature
+        if not nonormalized:
+            lang = lang / (lang.norm(dim=-1, keepdim=True) + 1e-9)
+    else:
+        lang = torch.zeros((pc.P, language_feature_hiddendim), dtype=opacity.dtype, device=dev)
+    scales = rotations = cov3D_precomp = None
+    if compute_cov3D_python:
+        cov3D_precomp = _covariance(pc.get_scaling, scaling_modifier, pc.rotation)
+    else:
+        scales, rotations = pc.scaling, pc.rotation
+    coff = None
+    if "coarse" in stage:
+        m3, s3, r3, o3, sh3, l3 = means3D, scales, rotations, opacity, shs, lang
+    elif "fine" in stage:
+        if pc.deformation is None:
+            raise ValueError("a 'fine' stage needs the scene's deformation field")
+        if cov3D_precomp is not None:
+            raise ValueError("compute_cov3D_python with a deformation field is not supported")
+        m3, s3, r3, o3, sh3, l3, coff = pc.deformation(means3D, scales, rotations, opacity, shs, lang, t)
+    else:
+        raise NotImplementedError(stage)
+    s3 = torch.exp(s3) if s3 is not None else None
+    r3 = torch.nn.functional.normalize(r3) if r3 is not None else None
+    o3 = torch.sigmoid(o3)
+    colors_precomp = None
+    if override_color is not None:
+        colors_precomp = override_color
+    elif convert_SHs_python:
+        # as the reference (gaussian_renderer/__init__.py:200-205): undeformed means and features
+        shs_view = pc.get_features.transpose(1, 2).view(-1, 3, (pc.max_sh_degree + 1) ** 2)
+        dir_pp = pc.get_xyz - viewpoint_camera.camera_center.to(dev).repeat(pc.P, 1)
+        dirs = dir_pp / dir_pp.norm(dim=1, keepdim=True)
+        colors_precomp = torch.clamp_min(eval_sh(pc.active_sh_degree, shs_view, dirs) + 0.5, 0.0)
+    image, lang_img, radii, depth = rasterizer(
+        means3D=m3, means2D=screenspace_points, shs=None if colors_precomp is not None else sh3,
+        colors_precomp=colors_precomp, language_feature_precomp=l3, opacities=o3, scales=s3, rotations=r3,
+        cov3D_precomp=cov3D_precomp)
+    if "base" in stage:
+        lang_img = None
+    return {"render": image, "language_feature_image": lang_img, "viewspace_points": screenspace_points,
+            "visibility_filter": radii > 0, "radii": radii, "depth": depth, "coff": coff}
+
+
+_SH_C0 = 0.28209479177387814
+_SH_C1 = 0.4886025119029199
+_SH_C2 = (1.0925484305920792, -1.0925484305920792, 0.31539156525252005, -1.0925484305920792, 0.5462742152960396)
+_SH_C3 = (-0.5900435899266435, 2.890611442640554, -0.4570457994644658, 0.3731763325901154, -0.4570457994644658,
+          1.445305721320277, -0.5900435899266435)
+
+
+def eval_sh(deg: int, sh: torch.Tensor, dirs: torch.Tensor) -> torch.Tensor:
+    """SH -> colour for degree <= 3 (utils/sh_utils.py:57-112): sh [..., C, (deg+1)^2], dirs
+    [..., 3] unit."""
+    result = _SH_C0 * sh[..., 0]
+    if deg > 0:
+        x, y, z = dirs[..., 0:1], dirs[..., 1:2], dirs[..., 2:3]
+        result = result - _SH_C1 * y * sh[..., 1] + _SH_C1 * z * sh[..., 2] - _SH_C1 * x * sh[..., 3]
+        if deg > 1:
+            xx, yy, zz, xy, yz, xz = x * x, y * y, z * z, x * y, y * z, x * z
+            result = (result + _SH_C2[0] * xy * sh[..., 4] + _SH_C2[1] * yz * sh[..., 5]
+                      + _SH_C2[2] * (2.0 * zz - xx - yy) * sh[..., 6] + _SH_C2[3] * xz * sh[..., 7]
+                      + _SH_C2[4] * (xx - yy) * sh[..., 8])
+            if deg > 2:
+                result = (result + _SH_C3[0] * y * (3 * xx - yy) * sh[..., 9] + _SH_C3[1] * xy * z * sh[..., 10]
+                          + _SH_C3[2] * y * (4 * zz - xx - yy) * sh[..., 11]
+                          + _SH_C3[3] * z * (2 * zz - 3 * xx - 3 * yy) * sh[..., 12]
+                          + _SH_C3[4] * x * (4 * zz - xx - yy) * sh[..., 13] + _SH_C3[5] * z * (xx - yy) * sh[..., 14]
+                          + _SH_C3[6] * x * (xx - 3 * yy) * sh[..., 15])
+    return result
+
+
+def _covariance(scaling, scaling_modifier, rotation):
+    """build_scaling_rotation + strip_symmetric (utils/general_utils.py:70-116)."""
+    r = torch.nn.functional.normalize(rotation)
+    w, x, y, z = r[:, 0], r[:, 1], r[:, 2], r[:, 3]
+    R = torch.stack([1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y),
+                     2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x),
+                     2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)], dim=1).view(-1, 3, 3)
+    L = R @ torch.diag_embed(scaling_modifier * scaling)
+    S = L @ L.transpose(1, 2)
+    return torch.stack([S[:, 0, 0], S[:, 0, 1], S[:, 0, 2], S[:, 1, 1], S[:, 1, 2], S[:, 2, 2]], dim=1)
+
+
+# ---- render.py's render_set -----------------------------------------------------------------------
+def pca_compress(feature_map: torch.Tensor) -> torch.Tensor:
+    """[C, H, W] -> [H, W, 3] in [0, 1] (render.py:52-65: sklearn PCA over pixels, min-max)."""
+    from sklearn.decomposition import PCA
+    C, H, W = feature_map.shape
+    x = feature_map.permute(1, 2, 0).reshape(-1, C).detach().cpu().numpy()
+    y = PCA(n_components=3).fit_transform(x).reshape(H, W, 3)
+    y = (y - y.min()) / (y.max() - y.min())
+    return torch.from_numpy(y)
+
+
+def write_png(path: str, rgb: np.ndarray) -> None:
+    """8-bit RGB PNG (zlib, no external imaging library)."""
+    rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
+    H, W, _ = rgb.shape
+    raw = b"".join(b"\x00" + rgb[y].tobytes() for y in range(H))
+
+    def chunk(tag, data):
+        return struct.pack(">I", len(data)) + tag + data + struct.pack(">I", zlib.crc32(tag + data) & 0xFFFFFFFF)
+
+    with open(path, "wb") as f:
+        f.write(b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", W, H, 8, 2, 0, 0, 0))
+                + chunk(b"IDAT", zlib.compress(raw, 6)) + chunk(b"IEND", b""))
+
+
+def to8b(x: np.ndarray) -> np.ndarray:
+    return (255 * np.clip(x, 0, 1)).astype(np.uint8)
+
+
+def render_set(model_path: str, name: str, iteration, views, scene: GaussianScene, background: torch.Tensor,
+               output_channel: str = "rgb", stage: str = "fine-lang", save_images: bool = True,
+               save_npy: bool = True, **render_kw) -> float:
+    """render.py:67-161 without ground truth (ONLY_EVAL): renders every view, writes
+    {model_path}/{name}_{output_channel}/ours_{iteration}/renders_npy/{idx:05d}.npy ([H, W, C], the
+    files eval/eval.py reads) and renders/{idx:05d}.png; returns the FPS as render.py prints it."""
+    key = "render" if output_channel == "rgb" else "language_feature_image"
+    base = os.path.join(model_path, f"{name}_{output_channel}", f"ours_{iteration}")
+    render_path, npy_path = os.path.join(base, "renders"), os.path.join(base, "renders_npy")
+    os.makedirs(render_path, exist_ok=True)
+    os.makedirs(npy_path, exist_ok=True)
+    outs, t1 = [], None
+    with torch.no_grad():
+        for idx, view in enumerate(views):
+            if idx == 0:
+                torch.cuda.synchronize()
+                t1 = _time.time()
+            outs.append(render(view, scene, background, stage=stage, **render_kw)[key])
+        torch.cuda.synchronize()
+        t2 = _time.time()
+    fps = (len(views) - 1) / (t2 - t1) if len(views) > 1 else float("nan")
+    print("FPS:", fps)
+    for idx, r in enumerate(outs):
+        if save_npy:
+            np.save(os.path.join(npy_path, f"{idx:05d}.npy"), r.permute(1, 2, 0).cpu().numpy())
+        if save_images:
+            img = r if output_channel == "rgb" else (r + 1.0) / 2
+            img = pca_compress(img).numpy() if img.shape[0] > 3 else img.permute(1, 2, 0).cpu().numpy()
+            write_png(os.path.join(render_path, f"{idx:05d}.png"), to8b(img))
+    return fps

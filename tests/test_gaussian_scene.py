@@ -1,0 +1,86 @@
+"""Scene I/O and render-path helpers (4dlangsplat_amd/gaussian_scene.py) on
+the CPU: the reference's PLY attribute list and round trip, foreign PLY encodings, eval_sh and
+the Python covariance against golden vectors from the reference's own code, PNG output."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import gaussian_scene as gs
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _scene(P=300, C=3, deg=3, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    n = (deg + 1) ** 2
+    return gs.GaussianScene(xyz=torch.randn(P, 3, generator=g), features_dc=torch.randn(P, 1, 3, generator=g),
+                            features_rest=torch.randn(P, n - 1, 3, generator=g),
+                            language_feature=torch.randn(P, C, generator=g), opacity=torch.randn(P, 1, generator=g),
+                            scaling=torch.randn(P, 3, generator=g) - 4, rotation=torch.randn(P, 4, generator=g),
+                            max_sh_degree=deg, active_sh_degree=deg)
+
+
+def test_attribute_list_is_the_references():
+    # gaussian_model.py:331-345 for SH degree 3 and 3 language channels
+    want = (["x", "y", "z", "nx", "ny", "nz", "f_dc_0", "f_dc_1", "f_dc_2"] + [f"f_rest_{i}" for i in range(45)]
+            + ["f_lang_0", "f_lang_1", "f_lang_2", "opacity", "scale_0", "scale_1", "scale_2",
+               "rot_0", "rot_1", "rot_2", "rot_3"])
+    assert _scene().attribute_names() == want
+
+
+@pytest.mark.parametrize("C,deg", [(3, 3), (6, 3), (32, 3), (3, 1)])
+def test_ply_round_trip(tmp_path, C, deg):
+    s = _scene(C=C, deg=deg)
+    p = str(tmp_path / "point_cloud.ply")
+    s.save_ply(p)
+    t = gs.GaussianScene.load_ply(p, max_sh_degree=deg)
+    for name in ("xyz", "features_dc", "features_rest", "language_feature", "opacity", "scaling", "rotation"):
+        assert torch.equal(getattr(s, name), getattr(t, name)), name
+    with open(p, "rb") as f:
+        head = f.read(200)
+    assert head.startswith(b"ply\nformat binary_little_endian 1.0\nelement vertex 300\n")
+    with pytest.raises(ValueError, match="f_rest"):
+        gs.GaussianScene.load_ply(p, max_sh_degree=deg + 1 if deg < 3 else 2)
+
+
+def test_reads_ascii_and_big_endian(tmp_path):
+    names = ["x", "y", "z", "opacity"]
+    cols = np.arange(12, dtype=np.float32).reshape(3, 4) / 7
+    a = tmp_path / "a.ply"
+    a.write_text("ply\nformat ascii 1.0\ncomment x\nelement vertex 3\n" + "".join(f"property float {n}\n" for n in names)
+                 + "end_header\n" + "".join(" ".join(repr(float(v)) for v in r) + "\n" for r in cols))
+    b = tmp_path / "b.ply"
+    with open(b, "wb") as f:
+        f.write(("ply\nformat binary_big_endian 1.0\nelement vertex 3\n" + "".join(f"property float {n}\n" for n in names)
+                 + "end_header\n").encode())
+        f.write(cols.astype(">f4").tobytes())
+    for p in (a, b):
+        v = gs.read_ply_vertices(str(p))
+        for i, n in enumerate(names):
+            np.testing.assert_array_equal(v[n].astype(np.float32), cols[:, i])
+
+
+def test_eval_sh_matches_reference_golden():
+    d = np.load(os.path.join(ROOT, "tests", "golden", "sh_golden.npz"))
+    for deg in range(4):
+        sh = torch.tensor(d[f"sh_{deg}"]).transpose(1, 2)           # [P, 3, 16] as render() views it
+        dirs = torch.tensor(d[f"pos_{deg}"] - d[f"campos_{deg}"])
+        dirs = dirs / dirs.norm(dim=1, keepdim=True)
+        rgb = torch.clamp_min(gs.eval_sh(deg, sh, dirs) + 0.5, 0.0)
+        np.testing.assert_allclose(rgb.numpy(), d[f"rgb_{deg}"], rtol=0, atol=2e-6)
+
+
+def test_covariance_matches_reference_golden():
+    d = np.load(os.path.join(ROOT, "tests", "golden", "cov3d.npz"))
+    cov = gs._covariance(torch.tensor(d["scales"]), float(d["mod"]), torch.tensor(d["rotations"]))
+    np.testing.assert_allclose(cov.numpy(), d["cov"], rtol=1e-5, atol=2e-8)
+
+
+def test_png_writer(tmp_path):
+    from PIL import Image
+    img = (np.random.default_rng(0).uniform(0, 1, (13, 17, 3)))
+    p = str(tmp_path / "x.png")
+    gs.write_png(p, gs.to8b(img))
+    np.testing.assert_array_equal(np.asarray(Image.open(p)), gs.to8b(img))
