@@ -21,8 +21,8 @@ def short(name):
 
 # bench phase -> the one kernel it launches (non-deterministic backward)
 PHASE_KERNEL = {"preprocess": "k_preprocess", "emit": "k_emit", "tile_ranges": "k_tile_ranges",
-                "render_fwd": "k_render_fwd_wave", "render_bwd": "k_render_bwd_wave",
-                "preprocess_bwd": "k_preprocess_bwd"}
+                "render_fwd": "k_render_fwd_wave_mfma", "render_bwd": "k_render_bwd_wave",
+                "preprocess_bwd": "k_preprocess_bwd", "preprocess_bwd_views": "k_preprocess_bwd_views"}
 
 
 def main(d, json_out=None):
@@ -57,7 +57,7 @@ def main(d, json_out=None):
             res[phase] = dict(kernel=ks[0], fetch_size_kb=fetch, write_size_kb=write,
                               hbm_bytes_per_launch=int((2 * fetch + write) * 1024),
                               dispatches=len(f["FETCH_SIZE"]))
-        res["_note"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, bench.py --views 2; "
+        res["_note"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, bench.py --steps 1 (8 views); "
                         "hbm = (2*FETCH_SIZE + WRITE_SIZE)*1024 per MI355X_MICROARCH.md HBM section")
         with open(json_out, "w") as fh:
             json.dump(res, fh, indent=1)
