@@ -47,10 +47,12 @@ __global__ void __launch_bounds__(256) k_emit(int P, const uint32_t* __restrict_
                                               const uint32_t* __restrict__ offsets,
                                               const uint32_t* __restrict__ counts,
                                               const uint2* __restrict__ rect_sorted, int gx,
-                                              uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+                                              uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                              ClearList clear) {
     __shared__ uint32_t s_off[4][64];
     __shared__ uint2 s_rc[4][64];
     __shared__ uint32_t s_id[4][64];
+    clear_words(clear);   // tile ranges, per-tile bounds, tile-sort workspace (used after this kernel)
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int base = (blockIdx.x * 4 + w) * 64;
     if (base >= P) return;                                   // wave-uniform
@@ -80,10 +82,11 @@ __global__ void __launch_bounds__(256) k_emit(int P, const uint32_t* __restrict_
 }
 
 void launch_emit_instances(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* counts,
-                           const uint2* rect_sorted, int grid_x, uint32_t* keys, uint32_t* vals, hipStream_t st) {
+                           const uint2* rect_sorted, int grid_x, uint32_t* keys, uint32_t* vals,
+                           const ClearList& clear, hipStream_t st) {
     if (P == 0) return;
     hipLaunchKernelGGL(k_emit, dim3((P + 255) / 256), dim3(256), 0, st, P, order, offsets, counts, rect_sorted,
-                       grid_x, keys, vals);
+                       grid_x, keys, vals, clear);
 }
 
 // inst_off[g] = first instance slot of Gaussian g: only the deterministic backward needs it (its

@@ -106,6 +106,8 @@ struct Geom {
     uint32_t* total;
     void* sort_tmp;
     void* scan_tmp;
+    float4* acc;          // [P, ACC_PITCH] split-backward accumulators (rows of listed Gaussians
+                          // zeroed by the preprocess; lsr_backward_composite adds into them)
 };
 Geom carve_geom(void* base, size_t P, size_t* bytes) {
     Carver c(base);
@@ -128,6 +130,7 @@ Geom carve_geom(void* base, size_t P, size_t* bytes) {
     g.total = c.take<uint32_t>(4);
     g.sort_tmp = c.take<char>(lsr::radix_temp_bytes(P));
     g.scan_tmp = c.take<char>(lsr::scan_temp_bytes(P));
+    g.acc = c.take<float4>(P * (lsr::ACC_PITCH / 4));
     if (bytes) *bytes = c.off;
     return g;
 }
@@ -269,7 +272,15 @@ int lsr_forward_preprocess(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_
     a.view = s->viewmatrix; a.proj = s->projmatrix; a.campos = s->campos;
     a.radii = out->radii; a.radius = g.radius; a.tiles = g.tiles; a.rect = g.rect; a.key = g.key_a; a.xy = g.xy; a.conic_o = g.conic_o; a.rgbd = g.rgbd;
     a.clamped = g.clamped;
-    LSR_HIP(hipMemsetAsync(g.clamped, 0, (size_t)P, st));
+    // the preprocess also writes the depth sort's initial values (ids), zeroes the split-backward
+    // accumulator rows of listed Gaussians, and clears the sort workspace and the counters
+    // [0] K, [1] sort error word: no separate fill launches
+    a.order = g.val_a;
+    a.acc = g.acc;
+    a.clear.p[0] = reinterpret_cast<uint32_t*>(g.sort_tmp);
+    a.clear.n[0] = (uint32_t)(lsr::radix_temp_zero_bytes((size_t)P, 0, 32) / 4);
+    a.clear.p[1] = g.total;
+    a.clear.n[1] = 2;
     {
         PhaseTimer t(LSR_PHASE_PREPROCESS, st);
         lsr::launch_preprocess(a, st);
@@ -279,9 +290,8 @@ int lsr_forward_preprocess(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_
     bool in_b;
     {
         PhaseTimer t(LSR_PHASE_DEPTH_SORT, st);
-        lsr::launch_iota(P, g.val_a, st);
-        LSR_HIP(hipMemsetAsync(g.total, 0, 2 * sizeof(uint32_t), st));   // [0] K, [1] sort error word
-        in_b = lsr::radix_sort_pairs(g.key_a, g.val_a, g.key_b, g.val_b, (size_t)P, 0, 32, g.sort_tmp, g.total + 1, st);
+        in_b = lsr::radix_sort_pairs(g.key_a, g.val_a, g.key_b, g.val_b, (size_t)P, 0, 32, g.sort_tmp, g.total + 1, st,
+                                     /*temp_zeroed=*/true);
     }
     if (in_b != (bool)depth_sort_result_in_b()) return fail(LSR_EHIP, "internal: depth sort parity");
     LSR_LAUNCHED("depth sort", st, s->debug);
@@ -312,18 +322,30 @@ int lsr_forward_binning(const lsr_settings* s, const lsr_fwd_in* in, void* geom,
     Geom g = carve_geom(geom, (size_t)(P > 0 ? P : 1), nullptr);
     Binning b = carve_binning(binning, K > 0 ? K : 1, nullptr);
     Img m = carve_img(img, W, H, nullptr);
-    LSR_HIP(hipMemsetAsync(m.ranges, 0, sizeof(uint2) * (size_t)gx * gy, st));
-    if (K > 0) {
+    const size_t ntiles = (size_t)gx * gy;
+    if (K == 0) {
+        LSR_HIP(hipMemsetAsync(m.ranges, 0, sizeof(uint2) * ntiles, st));
+        LSR_HIP(hipMemsetAsync(m.tile_max, 0, sizeof(uint32_t) * ntiles, st));
+    } else {
+        // the emission also clears the tile ranges, the per-tile replay bounds and the tile sort's
+        // workspace (no separate fill launches)
+        lsr::ClearList cl{};
+        cl.p[0] = reinterpret_cast<uint32_t*>(m.ranges);
+        cl.n[0] = (uint32_t)(2 * ntiles);
+        cl.p[1] = m.tile_max;
+        cl.n[1] = (uint32_t)ntiles;
+        cl.p[2] = reinterpret_cast<uint32_t*>(b.sort_tmp);
+        cl.n[2] = (uint32_t)(lsr::radix_temp_zero_bytes(K, 0, tile_bits((int)ntiles)) / 4);
         {
             PhaseTimer t(LSR_PHASE_EMIT, st);
-            lsr::launch_emit_instances(P, g.val_a, g.offsets, g.counts, g.rect_sorted, gx, b.key_a, b.val_a, st);
+            lsr::launch_emit_instances(P, g.val_a, g.offsets, g.counts, g.rect_sorted, gx, b.key_a, b.val_a, cl, st);
         }
         LSR_LAUNCHED("emit", st, s->debug);
         bool in_b;
         {
             PhaseTimer t(LSR_PHASE_TILE_SORT, st);
             in_b = lsr::radix_sort_pairs(b.key_a, b.val_a, b.key_b, b.val_b, K, 0, tile_bits(gx * gy), b.sort_tmp,
-                                         nullptr, st);
+                                         nullptr, st, /*temp_zeroed=*/true);
         }
         if (in_b != tile_sort_in_b(gx * gy)) return fail(LSR_EHIP, "internal: tile sort parity");
         const uint32_t* keys = in_b ? b.key_b : b.key_a;
@@ -350,8 +372,7 @@ int lsr_forward_composite(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_o
     const size_t K = (size_t)num_rendered;
     Geom g = carve_geom(const_cast<void*>(geom), (size_t)(P > 0 ? P : 1), nullptr);
     Binning b = carve_binning(const_cast<void*>(binning), K > 0 ? K : 1, nullptr);
-    Img m = carve_img(img, W, H, nullptr);
-    LSR_HIP(hipMemsetAsync(m.tile_max, 0, sizeof(uint32_t) * (size_t)gx * gy, st));
+    Img m = carve_img(img, W, H, nullptr);   // tile_max was zeroed by the binning (atomicMax: idempotent)
     const uint32_t* point_list = K > 0 ? (tile_sort_in_b(gx * gy) ? b.val_b : b.val_a) : nullptr;
     lsr::RenderFwdArgs r{};
     r.W = W; r.H = H; r.grid_x = gx; r.grid_y = gy; r.C = C; r.include_feature = s->include_feature;
@@ -451,26 +472,24 @@ int lsr_backward(const lsr_settings* s, const lsr_fwd_in* in, const lsr_bwd_in* 
 }
 
 int lsr_backward_composite(const lsr_settings* s, const lsr_fwd_in* in, const lsr_bwd_in* gin, float* dL_dlanguage,
-                           const void* geom, const void* binning, const void* img, void* scratch,
-                           int64_t num_rendered, lsr_stream_t stream) {
+                           void* geom, const void* binning, const void* img, int64_t num_rendered,
+                           lsr_stream_t stream) {
     int rc = check_common(s, in);
     if (rc) return rc;
     if (!gin || !gin->dL_dout_color) return fail(LSR_EINVAL, "dL_dout_color is required");
     if (gin->deterministic)
         return fail(LSR_EINVAL, "the split backward reduces with float atomics; use lsr_backward for deterministic "
                                 "gradients");
-    if (!geom || !img || !scratch || (num_rendered > 0 && !binning)) return fail(LSR_EINVAL, "workspaces are required");
+    if (!geom || !img || (num_rendered > 0 && !binning)) return fail(LSR_EINVAL, "workspaces are required");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const int P = in->P, C = in->C, W = s->image_width, H = s->image_height;
     if (P == 0) return LSR_OK;
     const int gx = (W + LSR_TILE_X - 1) / LSR_TILE_X, gy = (H + LSR_TILE_Y - 1) / LSR_TILE_Y;
     const size_t K = (size_t)num_rendered;
-    Geom g = carve_geom(const_cast<void*>(geom), (size_t)P, nullptr);
+    Geom g = carve_geom(geom, (size_t)P, nullptr);   // g.acc: rows of listed Gaussians zeroed by the preprocess
     Binning b = carve_binning(const_cast<void*>(binning), K > 0 ? K : 1, nullptr);
     Img m = carve_img(const_cast<void*>(img), W, H, nullptr);
     const int recq = lsr::record_floats(s->include_feature ? C : 0);
-    Scratch sc = carve_scratch(scratch, (size_t)P, K > 0 ? K : 1, recq, false, nullptr);
-    LSR_HIP(hipMemsetAsync(sc.acc_small, 0, sizeof(float) * lsr::ACC_PITCH * (size_t)P, st));
     if (K == 0) return LSR_OK;
     lsr::RenderBwdArgs r{};
     r.W = W; r.H = H; r.grid_x = gx; r.grid_y = gy; r.C = C; r.include_feature = s->include_feature;
@@ -481,7 +500,7 @@ int lsr_backward_composite(const lsr_settings* s, const lsr_fwd_in* in, const ls
     r.tile_max_contrib = m.tile_max;
     r.dL_dcolor = gin->dL_dout_color; r.dL_dlang = gin->dL_dout_language_feature; r.dL_ddepth = gin->dL_dout_depth;
     r.recq = recq; r.deterministic = 0;
-    r.acc_small = sc.acc_small; r.acc_lang = dL_dlanguage;
+    r.acc_small = reinterpret_cast<float*>(g.acc); r.acc_lang = dL_dlanguage;
     {
         PhaseTimer t(LSR_PHASE_RENDER_BWD, st);
         lsr::launch_render_bwd(r, st);
@@ -491,14 +510,14 @@ int lsr_backward_composite(const lsr_settings* s, const lsr_fwd_in* in, const ls
 }
 
 int lsr_backward_preprocess_views(int32_t n_views, const lsr_settings* const* s, const lsr_fwd_in* in,
-                                  lsr_bwd_out* gout, const void* const* geom, const void* const* scratch,
-                                  const int64_t* num_rendered, int32_t accumulate, lsr_stream_t stream) {
+                                  lsr_bwd_out* gout, const void* const* geom, int32_t accumulate,
+                                  lsr_stream_t stream) {
     if (n_views < 1) return fail(LSR_EINVAL, "n_views must be >= 1");
-    if (!s || !in || !gout || !geom || !scratch || !num_rendered) return fail(LSR_EINVAL, "null argument");
+    if (!s || !in || !gout || !geom) return fail(LSR_EINVAL, "null argument");
     for (int v = 0; v < n_views; ++v) {
         int rc = check_common(s[v], in);
         if (rc) return rc;
-        if (!geom[v] || !scratch[v]) return fail(LSR_EINVAL, "workspaces are required for every view");
+        if (!geom[v]) return fail(LSR_EINVAL, "the geom workspace is required for every view");
         if (s[v]->scale_modifier != s[0]->scale_modifier) return fail(LSR_EINVAL, "all views must share scale_modifier");
     }
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -514,17 +533,14 @@ int lsr_backward_preprocess_views(int32_t n_views, const lsr_settings* const* s,
         for (int j = 0; j < nv; ++j) {
             const int v = v0 + j;
             const lsr_settings* sv = s[v];
-            const size_t K = (size_t)num_rendered[v];
             Geom g = carve_geom(const_cast<void*>(geom[v]), (size_t)P, nullptr);
-            Scratch sc = carve_scratch(const_cast<void*>(scratch[v]), (size_t)P, K > 0 ? K : 1,
-                                       lsr::record_floats(sv->include_feature ? in->C : 0), false, nullptr);
             lsr::ViewCam& c = a.cam[j];
             c.view = sv->viewmatrix; c.proj = sv->projmatrix; c.campos = sv->campos;
             c.tanfovx = sv->tanfovx; c.tanfovy = sv->tanfovy;
             c.focal_x = (float)sv->image_width / (2.0f * sv->tanfovx);
             c.focal_y = (float)sv->image_height / (2.0f * sv->tanfovy);
             c.deg = sv->sh_degree;
-            c.tiles = g.tiles; c.clamped = g.clamped; c.acc_small = sc.acc_small;
+            c.tiles = g.tiles; c.clamped = g.clamped; c.acc_small = reinterpret_cast<const float*>(g.acc);
         }
         a.dopacity = gout->dL_dopacity;
         a.dmeans3D = gout->dL_dmeans3D; a.dmeans2D = gout->dL_dmeans2D; a.dcolors = gout->dL_dcolors;
@@ -540,11 +556,11 @@ int lsr_backward_preprocess_views(int32_t n_views, const lsr_settings* const* s,
 }
 
 int lsr_backward_views(int32_t n_views, const lsr_settings* const* s, const lsr_fwd_in* in,
-                       const lsr_bwd_in* const* gin, lsr_bwd_out* gout, const void* const* geom,
-                       const void* const* binning, const void* const* img, void* const* scratch,
-                       const int64_t* num_rendered, int32_t accumulate, lsr_stream_t stream) {
+                       const lsr_bwd_in* const* gin, lsr_bwd_out* gout, void* const* geom,
+                       const void* const* binning, const void* const* img, const int64_t* num_rendered,
+                       int32_t accumulate, lsr_stream_t stream) {
     if (n_views < 1) return fail(LSR_EINVAL, "n_views must be >= 1");
-    if (!s || !in || !gin || !gout || !geom || !binning || !img || !scratch || !num_rendered)
+    if (!s || !in || !gin || !gout || !geom || !binning || !img || !num_rendered)
         return fail(LSR_EINVAL, "null argument");
     for (int v = 0; v < n_views; ++v) {   // validate every view before anything is launched
         int rc = check_common(s[v], in);
@@ -562,10 +578,11 @@ int lsr_backward_views(int32_t n_views, const lsr_settings* const* s, const lsr_
         LSR_HIP(hipMemsetAsync(gout->dL_dlanguage_feature, 0, sizeof(float) * (size_t)P * C, st));
     for (int v = 0; v < n_views; ++v) {
         int rc = lsr_backward_composite(s[v], in, gin[v], gout->dL_dlanguage_feature, geom[v], binning[v], img[v],
-                                        scratch[v], num_rendered[v], stream);
+                                        num_rendered[v], stream);
         if (rc) return rc;
     }
-    return lsr_backward_preprocess_views(n_views, s, in, gout, geom, scratch, num_rendered, accumulate, stream);
+    return lsr_backward_preprocess_views(n_views, s, in, gout, const_cast<const void* const*>(geom), accumulate,
+                                         stream);
 }
 
 int lsr_mark_visible(int32_t P, const float* means3D, const float* viewmatrix, const float* projmatrix,

@@ -10,6 +10,19 @@ namespace lsr {
 // records, so the atomics of one entry are one 64-byte memory-side request.
 constexpr int ACC_PITCH = 16;
 
+// Word ranges a kernel zeroes on the side (grid-stride), for the kernels that follow it in stream
+// order: replaces separate hipMemsetAsync launches (each a dispatch that waits for a free CU).
+struct ClearList {
+    uint32_t* p[4];
+    uint32_t n[4];
+};
+__device__ __forceinline__ void clear_words(const ClearList& c) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        for (uint32_t i = t; i < c.n[k]; i += stride) c.p[k][i] = 0u;
+}
+
 struct PreprocessArgs {
     int P, M, deg, W, H, grid_x, grid_y;
     float tanfovx, tanfovy, focal_x, focal_y, scale_modifier;
@@ -33,6 +46,9 @@ struct PreprocessArgs {
     float4* conic_o;
     float4* rgbd;
     uint8_t* clamped;
+    uint32_t* order;  // if set: order[i] = i (the depth sort's initial values)
+    float4* acc;      // if set: [P, ACC_PITCH / 4] backward accumulators, zeroed for visible rows
+    ClearList clear;  // zeroed on the side (sort workspace, counters)
 };
 
 struct PreprocessBwdArgs {
@@ -187,15 +203,18 @@ void exclusive_scan_u32(const uint32_t* in, uint32_t* out, size_t n, uint32_t* t
 size_t radix_temp_bytes(size_t n);
 // stable LSD sort of (key, value) pairs on bits [begin_bit, end_bit); returns true when the result
 // is in (keys_b, vals_b).  err (device word, may be null) is set non-zero if a look-back timed out.
+// temp_zeroed: the caller already zeroed the first radix_temp_zero_bytes(n, begin, end) bytes of temp
 bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b, size_t n,
-                      int begin_bit, int end_bit, void* temp, uint32_t* err, hipStream_t st);
+                      int begin_bit, int end_bit, void* temp, uint32_t* err, hipStream_t st, bool temp_zeroed = false);
+size_t radix_temp_zero_bytes(size_t n, int begin_bit, int end_bit);
 
 // binning (binning.hip)
 void launch_iota(int n, uint32_t* out, hipStream_t st);
 void launch_gather_tile_counts(int P, const uint32_t* order, const uint2* rect, uint32_t* counts, uint2* rect_sorted,
                                hipStream_t st);
 void launch_emit_instances(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* counts,
-                           const uint2* rect_sorted, int grid_x, uint32_t* keys, uint32_t* vals, hipStream_t st);
+                           const uint2* rect_sorted, int grid_x, uint32_t* keys, uint32_t* vals,
+                           const ClearList& clear, hipStream_t st);
 void launch_scatter_inst_off(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* counts,
                              uint32_t* inst_off, hipStream_t st);
 void launch_tile_ranges(size_t K, const uint32_t* keys, uint2* ranges, hipStream_t st);

@@ -103,12 +103,15 @@ __device__ __forceinline__ void stage_rows(float* __restrict__ lds, const float*
 template <int MS>  // SH coefficients per Gaussian known at compile time (0 = any M, read from global)
 __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
     constexpr int M3 = MS * 3;
+    clear_words(a.clear);
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.P) return;
     a.radii[i] = 0;
     a.radius[i] = 0;
     a.tiles[i] = 0;
     a.rect[i] = make_uint2(0u, 0u);
+    a.clamped[i] = 0;
+    if (a.order) a.order[i] = (uint32_t)i;
     if (a.key) a.key[i] = 0xFFFFFFFFu;
     const float3 p = make_float3(a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]);
     const float4 ph = xform4x4(a.proj, p);
@@ -229,6 +232,11 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
     a.radii[i] = radius;
     a.radius[i] = radius;
     a.tiles[i] = (uint32_t)ntiles;
+    if (a.acc && ntiles > 0) {   // only listed Gaussians receive backward atomics
+        float4* r = a.acc + (size_t)i * (ACC_PITCH / 4);
+#pragma unroll
+        for (int k = 0; k < ACC_PITCH / 4; ++k) r[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
     a.rect[i] = make_uint2((uint32_t)cmin.x | ((uint32_t)cmin.y << 16), (uint32_t)cmax.x | ((uint32_t)cmax.y << 16));
     if (a.key) a.key[i] = __float_as_uint(pv.z);
     a.xy[i] = pix;

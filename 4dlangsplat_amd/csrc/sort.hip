@@ -310,16 +310,21 @@ size_t radix_temp_bytes(size_t n) {
     return align_up(4 * 256 * 4 + 64, 256) + align_up(4 * os_blocks(n) * 256 * 4, 256);
 }
 
+size_t radix_temp_zero_bytes(size_t n, int begin_bit, int end_bit) {
+    if (n == 0 || end_bit <= begin_bit) return 0;
+    const int npass = (end_bit - begin_bit + 7) / 8;
+    return align_up(4 * 256 * 4 + 64, 256) + (size_t)npass * os_blocks(n) * 256 * 4;
+}
+
 bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b, size_t n,
-                      int begin_bit, int end_bit, void* temp, uint32_t* err, hipStream_t st) {
+                      int begin_bit, int end_bit, void* temp, uint32_t* err, hipStream_t st, bool temp_zeroed) {
     if (n == 0 || end_bit <= begin_bit) return false;
     const size_t nb = os_blocks(n);
     uint32_t* hist = reinterpret_cast<uint32_t*>(temp);
     uint32_t* tickets = hist + 4 * 256;
     uint32_t* own_err = tickets + 4;
     uint32_t* status = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(temp) + align_up(4 * 256 * 4 + 64, 256));
-    const int npass = (end_bit - begin_bit + 7) / 8;
-    (void)hipMemsetAsync(temp, 0, align_up(4 * 256 * 4 + 64, 256) + (size_t)npass * nb * 256 * 4, st);
+    if (!temp_zeroed) (void)hipMemsetAsync(temp, 0, radix_temp_zero_bytes(n, begin_bit, end_bit), st);
     const unsigned hb = (unsigned)min((size_t)OS_HIST_BLOCKS, (n + 64 * OS_ITEMS * 4 - 1) / (64 * OS_ITEMS * 4));
     hipLaunchKernelGGL(k_radix_hist, dim3(hb), dim3(256), 0, st, (const uint32_t*)keys_a, n, begin_bit, end_bit, hist);
     bool in_b = false;

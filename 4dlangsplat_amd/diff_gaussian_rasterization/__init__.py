@@ -353,8 +353,6 @@ def backward_views_native(states, grad_colors, grad_langs=None, grad_depths=None
     gout.dL_dlanguage_feature, gout.dL_dopacity = _ptr(g["language_feature"]), _ptr(g["opacities"])
     gout.dL_dcov3D, gout.dL_dsh = _ptr(g["cov3D"]), _ptr(g["sh"])
     gout.dL_dscales, gout.dL_drotations = _ptr(g["scales"]), _ptr(g["rotations"])
-    scratch = [torch.empty(int(L.lsr_backward_bytes(P, s.num_rendered, C, 0)), dtype=torch.uint8, device=device)
-               for s in states]
     SP = ctypes.POINTER(_lib.Settings)
     BP = ctypes.POINTER(_lib.BwdIn)
     s_arr = (SP * n)(*[ctypes.pointer(s.settings.c) for s in states])
@@ -363,19 +361,19 @@ def backward_views_native(states, grad_colors, grad_langs=None, grad_depths=None
     geom = vp(*[s.geom.data_ptr() for s in states])
     binning = vp(*[s.binning.data_ptr() for s in states])
     img = vp(*[s.img.data_ptr() for s in states])
-    scr = vp(*[t.data_ptr() for t in scratch])
     K = (ctypes.c_int64 * n)(*[s.num_rendered for s in states])
     _lib.check(L.lsr_backward_views(n, s_arr, ctypes.byref(st0.fin), g_arr, ctypes.byref(gout), geom, binning, img,
-                                    scr, K, 1 if accumulate else 0, _stream(device)), "lsr_backward_views")
+                                    K, 1 if accumulate else 0, _stream(device)), "lsr_backward_views")
     return g
 
 
 class CompositeGrad:
     """A view whose compositor backward ran (backward_composite_native): its forward state and the
-    per-Gaussian screen-space sums (scratch) that backward_preprocess_views_native consumes."""
+    upstream gradients; the per-Gaussian screen-space sums that backward_preprocess_views_native
+    consumes live in the state's geom buffer."""
 
-    def __init__(self, state, scratch, keep):
-        self.state, self.scratch, self._keep = state, scratch, keep
+    def __init__(self, state, keep):
+        self.state, self._keep = state, keep
 
 
 def backward_composite_native(state: RasterizerState, grad_color, grad_lang=None, grad_depth=None,
@@ -396,13 +394,12 @@ def backward_composite_native(state: RasterizerState, grad_color, grad_lang=None
     gi.deterministic = 0
     if dL_dlanguage is not None and (dL_dlanguage.shape != (P, C) or not dL_dlanguage.is_contiguous()):
         raise ValueError("dL_dlanguage must be a contiguous [P, C] tensor")
-    scratch = torch.empty(int(L.lsr_backward_bytes(P, state.num_rendered, C, 0)), dtype=torch.uint8, device=device)
     _lib.check(L.lsr_backward_composite(ctypes.byref(state.settings.c), ctypes.byref(state.fin), ctypes.byref(gi),
                                         _ptr(dL_dlanguage if C > 0 else None), ctypes.c_void_p(state.geom.data_ptr()),
                                         ctypes.c_void_p(state.binning.data_ptr()),
-                                        ctypes.c_void_p(state.img.data_ptr()), ctypes.c_void_p(scratch.data_ptr()),
+                                        ctypes.c_void_p(state.img.data_ptr()),
                                         ctypes.c_int64(state.num_rendered), _stream(device)), "lsr_backward_composite")
-    return CompositeGrad(state, scratch, (gc, gl, gd))
+    return CompositeGrad(state, (gc, gl, gd))
 
 
 def backward_preprocess_views_native(parts, out=None, accumulate=False, need=None):
@@ -428,8 +425,6 @@ def backward_preprocess_views_native(parts, out=None, accumulate=False, need=Non
     _lib.check(L.lsr_backward_preprocess_views(n, (SP * n)(*[ctypes.pointer(p_.state.settings.c) for p_ in parts]),
                                                ctypes.byref(st0.fin), ctypes.byref(gout),
                                                vp(*[p_.state.geom.data_ptr() for p_ in parts]),
-                                               vp(*[p_.scratch.data_ptr() for p_ in parts]),
-                                               (ctypes.c_int64 * n)(*[p_.state.num_rendered for p_ in parts]),
                                                1 if accumulate else 0, _stream(device)),
                "lsr_backward_preprocess_views")
     return g

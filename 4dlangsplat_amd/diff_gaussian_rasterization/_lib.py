@@ -85,15 +85,14 @@ SIGNATURES = {
     "lsr_backward_views": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(ctypes.POINTER(Settings)), ctypes.POINTER(FwdIn),
                                           ctypes.POINTER(ctypes.POINTER(BwdIn)), ctypes.POINTER(BwdOut),
                                           ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
-                                          ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
-                                          ctypes.POINTER(ctypes.c_int64), ctypes.c_int32, ctypes.c_void_p]),
+                                          ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int64),
+                                          ctypes.c_int32, ctypes.c_void_p]),
     "lsr_backward_composite": (ctypes.c_int, [ctypes.POINTER(Settings), ctypes.POINTER(FwdIn), ctypes.POINTER(BwdIn),
                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                              ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]),
+                                              ctypes.c_int64, ctypes.c_void_p]),
     "lsr_backward_preprocess_views": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(ctypes.POINTER(Settings)),
                                                      ctypes.POINTER(FwdIn), ctypes.POINTER(BwdOut),
-                                                     ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
-                                                     ctypes.POINTER(ctypes.c_int64), ctypes.c_int32, ctypes.c_void_p]),
+                                                     ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32, ctypes.c_void_p]),
     "lsr_mark_visible": (ctypes.c_int, [ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p]),
     "lsr_profile_enable": (ctypes.c_int, [ctypes.c_int32]),

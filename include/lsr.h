@@ -148,28 +148,30 @@ int lsr_backward(const lsr_settings *s, const lsr_fwd_in *in, const lsr_bwd_in *
  * gradient rows once instead of once per view.  Float-atomic reduction only (every gin[v] must
  * have deterministic == 0; lsr_backward per view gives the deterministic mode).  All views must
  * share scale_modifier.  s[v], gin[v], geom[v], binning[v], img[v], num_rendered[v] are view v's
- * forward state; scratch[v] holds >= lsr_backward_bytes(P, num_rendered[v], C, 0) bytes.  The
- * pointer arrays are HOST arrays of device pointers. */
+ * forward state; the per-Gaussian screen-space sums live in geom (its accumulator rows were zeroed
+ * by the forward), so each forward is backpropagated by this call ONCE.  The pointer arrays are
+ * HOST arrays of device pointers. */
 int lsr_backward_views(int32_t n_views, const lsr_settings *const *s, const lsr_fwd_in *in,
-                       const lsr_bwd_in *const *gin, lsr_bwd_out *gout, const void *const *geom,
-                       const void *const *binning, const void *const *img, void *const *scratch,
-                       const int64_t *num_rendered, int32_t accumulate, lsr_stream_t stream);
+                       const lsr_bwd_in *const *gin, lsr_bwd_out *gout, void *const *geom,
+                       const void *const *binning, const void *const *img, const int64_t *num_rendered,
+                       int32_t accumulate, lsr_stream_t stream);
 
 /* lsr_backward_views in two halves, so that a view's compositor backward can run as soon as its
  * upstream gradients exist (and overlap the next view's preprocess on another stream), while the
  * preprocess backward still runs once per batch:
  *  - lsr_backward_composite: compositor backward of ONE view; its per-Gaussian screen-space sums
- *    go to `scratch` (>= lsr_backward_bytes(P, num_rendered, C, 0)), its language gradients are
- *    ADDED to dL_dlanguage [P,C] (zero it first; NULL skips them).  Float atomics only.
+ *    are added to accumulator rows in `geom` (zeroed by lsr_forward_preprocess: call once per
+ *    forward), its language gradients are ADDED to dL_dlanguage [P,C] (zero it first; NULL skips
+ *    them).  Float atomics only.
  *  - lsr_backward_preprocess_views: the preprocess backward of n_views views whose composite
- *    backward filled scratch[v]: gout (+)= sum_v (every output except dL_dlanguage_feature, which
- *    the composite calls already filled). */
+ *    backward ran: gout (+)= sum_v (every output except dL_dlanguage_feature, which the composite
+ *    calls already filled). */
 int lsr_backward_composite(const lsr_settings *s, const lsr_fwd_in *in, const lsr_bwd_in *gin, float *dL_dlanguage,
-                           const void *geom, const void *binning, const void *img, void *scratch,
-                           int64_t num_rendered, lsr_stream_t stream);
+                           void *geom, const void *binning, const void *img, int64_t num_rendered,
+                           lsr_stream_t stream);
 int lsr_backward_preprocess_views(int32_t n_views, const lsr_settings *const *s, const lsr_fwd_in *in,
-                                  lsr_bwd_out *gout, const void *const *geom, const void *const *scratch,
-                                  const int64_t *num_rendered, int32_t accumulate, lsr_stream_t stream);
+                                  lsr_bwd_out *gout, const void *const *geom, int32_t accumulate,
+                                  lsr_stream_t stream);
 
 /* markVisible: present[i] = (view-space z of means3D[i]) > 0.2 */
 int lsr_mark_visible(int32_t P, const float *means3D, const float *viewmatrix, const float *projmatrix,

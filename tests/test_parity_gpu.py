@@ -285,7 +285,7 @@ def test_backward_views_equals_per_view_sum(precomp):
         gout = _lib.BwdOut()
         _lib.check(L.lsr_backward_views(1, (SP * 1)(ctypes.pointer(st.settings.c)), ctypes.byref(st.fin),
                                         (BP * 1)(ctypes.pointer(gi)), ctypes.byref(gout), vp(st.geom.data_ptr()),
-                                        vp(st.binning.data_ptr()), vp(st.img.data_ptr()), vp(st.geom.data_ptr()),
+                                        vp(st.binning.data_ptr()), vp(st.img.data_ptr()),
                                         (ctypes.c_int64 * 1)(st.num_rendered), 0, None), "lsr_backward_views")
 
 
