@@ -1,0 +1,405 @@
+// train.hip -- training-step glue over the Gaussian SoA (include/lsr_train.h):
+// fused multi-group Adam, densification statistics, the densify / prune row maps, the multi-tensor
+// row gather, the split's new positions and scales, and the opacity reset.
+//
+// All of it is HBM-bound elementwise or row-copy work: one launch covers every tensor (the
+// reference issues one torch op per tensor and per group), loads and stores are 16 bytes wide
+// where the rows allow, and the row maps come from the device scan in sort.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <string>
+
+#include "../../include/lsr.h"
+#include "../../include/lsr_train.h"
+#include "lsr_common.h"
+#include "lsr_internal.h"
+
+namespace lsr {
+int fail(int code, const std::string& msg);   // lsr_api.hip (thread-local lsr_last_error)
+}
+
+namespace {
+
+size_t al256(size_t x) { return (x + 255) / 256 * 256; }
+
+// ---------------------------------------------------------------------------------------------
+// Adam.  Blocks own chunks of ADAM_CHUNK floats of one group; group g owns chunks
+// [chunk0[g], chunk0[g + 1]).
+constexpr int ADAM_THREADS = 256;
+constexpr int ADAM_CHUNK = ADAM_THREADS * 16;
+
+struct AdamGroupDev {
+    float* p;
+    const float* g;
+    float* m;
+    float* v;
+    int64_t n;
+    float w1, b2, w2, bc2s, ss, eps;   // 1-beta1, beta2, 1-beta2, sqrt(1-beta2^t), -lr/(1-beta1^t), eps
+    int vec;                            // all four pointers 16-byte aligned
+};
+struct AdamArgs {
+    AdamGroupDev grp[LSR_ADAM_MAX_GROUPS];
+    int64_t chunk0[LSR_ADAM_MAX_GROUPS + 1];
+    int ng;
+};
+
+// torch's foreach Adam element update (lerp, mul, addcmul, sqrt, div, add, addcdiv), in float32
+// with no contraction (the build uses -ffp-contract=off)
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, const AdamGroupDev& c) {
+    m = m + c.w1 * (g - m);
+    v = v * c.b2;
+    v = v + c.w2 * (g * g);
+    const float den = sqrtf(v) / c.bc2s + c.eps;
+    p = p + c.ss * (m / den);
+}
+
+__global__ void __launch_bounds__(ADAM_THREADS) k_adam(AdamArgs a) {
+    const int64_t b = blockIdx.x;
+    int gi = 0;
+    for (int k = 1; k < a.ng; ++k) gi = b >= a.chunk0[k] ? k : gi;   // block-uniform
+    const AdamGroupDev& c = a.grp[gi];
+    const int64_t lo = (b - a.chunk0[gi]) * ADAM_CHUNK, hi = min(c.n, lo + ADAM_CHUNK);
+    if (c.vec && hi - lo == ADAM_CHUNK) {
+        float4* p4 = reinterpret_cast<float4*>(c.p + lo);
+        const float4* g4 = reinterpret_cast<const float4*>(c.g + lo);
+        float4* m4 = reinterpret_cast<float4*>(c.m + lo);
+        float4* v4 = reinterpret_cast<float4*>(c.v + lo);
+        float4 P[4], G[4], M[4], V[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = r * ADAM_THREADS + threadIdx.x;
+            P[r] = p4[i]; G[r] = g4[i]; M[r] = m4[i]; V[r] = v4[i];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            adam_elem(P[r].x, G[r].x, M[r].x, V[r].x, c);
+            adam_elem(P[r].y, G[r].y, M[r].y, V[r].y, c);
+            adam_elem(P[r].z, G[r].z, M[r].z, V[r].z, c);
+            adam_elem(P[r].w, G[r].w, M[r].w, V[r].w, c);
+            const int i = r * ADAM_THREADS + threadIdx.x;
+            p4[i] = P[r]; m4[i] = M[r]; v4[i] = V[r];
+        }
+    } else {
+        for (int64_t i = lo + threadIdx.x; i < hi; i += ADAM_THREADS) {
+            float p = c.p[i], m = c.m[i], v = c.v[i];
+            adam_elem(p, c.g[i], m, v, c);
+            c.p[i] = p; c.m[i] = m; c.v[i] = v;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+__global__ void k_densify_stats(int P, const int* radii, const float* grad, int stride, float* max_r,
+                                float* accum, float* denom) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const int r = radii[i];
+    if (r <= 0) return;
+    max_r[i] = fmaxf(max_r[i], (float)r);
+    const float gx = grad[(size_t)i * stride], gy = grad[(size_t)i * stride + 1];
+    accum[i] += sqrtf(gx * gx + gy * gy);
+    denom[i] += 1.0f;
+}
+
+__device__ __forceinline__ float max_scale(const float* scaling, int i) {
+    return fmaxf(fmaxf(expf(scaling[3 * i]), expf(scaling[3 * i + 1])), expf(scaling[3 * i + 2]));
+}
+
+__global__ void k_densify_flags(int P, const float* accum, const float* denom, const float* scaling, float thr,
+                                float limit, uint32_t* fclone, uint32_t* fsplit) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    float g = accum[i] / denom[i];
+    if (g != g) g = 0.0f;
+    const float s = max_scale(scaling, i);
+    fclone[i] = (fabsf(g) >= thr && s <= limit) ? 1u : 0u;
+    fsplit[i] = (g >= thr && s > limit) ? 1u : 0u;
+}
+
+// totals: [0] cloned, [1] split (exclusive_scan_u32 totals)
+__global__ void k_densify_index(int P, int copies, const uint32_t* fclone, const uint32_t* fsplit,
+                                const uint32_t* oclone, const uint32_t* osplit, const uint32_t* totals, int* index,
+                                int64_t* counts) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t nclone = totals[0], nsplit = totals[1];
+    const uint32_t kept = (uint32_t)P - nsplit;
+    if (i == 0) {
+        counts[0] = kept; counts[1] = nclone; counts[2] = nsplit;
+    }
+    if (i >= P) return;
+    if (fsplit[i]) {
+        const size_t base = (size_t)kept + nclone + osplit[i];
+        for (int c = 0; c < copies; ++c) index[base + (size_t)c * nsplit] = i;
+    } else {
+        index[i - osplit[i]] = i;
+    }
+    if (fclone[i]) index[kept + oclone[i]] = i;
+}
+
+__global__ void k_prune_flags(int P, const float* opacity, const float* max_r, const float* scaling, float min_op,
+                              float max_screen, float big_ws, uint32_t* keep) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const float o = 1.0f / (1.0f + expf(-opacity[i]));
+    bool prune = o < min_op;
+    if (max_screen > 0.0f) prune = prune || max_r[i] > max_screen || max_scale(scaling, i) > big_ws;
+    keep[i] = prune ? 0u : 1u;
+}
+
+__global__ void k_prune_index(int P, const uint32_t* keep, const uint32_t* off, const uint32_t* total, int* index,
+                              int64_t* counts) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) counts[0] = total[0];
+    if (i < P && keep[i]) index[off[i]] = i;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Row gather: blockIdx.y = tensor; units of 16, 4 or 1 bytes (the widest that divides the row and
+// both base addresses).
+struct GatherTensor {
+    const char* src;
+    char* dst;
+    int64_t row_units, zero_from;
+    int unit;
+};
+struct GatherArgs {
+    GatherTensor t[LSR_GATHER_MAX_TENSORS];
+    int64_t n_rows;
+};
+
+template <typename U>
+__device__ void gather_units(const GatherTensor& t, const int* index, int64_t n_rows) {
+    const U* src = reinterpret_cast<const U*>(t.src);
+    U* dst = reinterpret_cast<U*>(t.dst);
+    const int64_t total = n_rows * t.row_units;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < total; u += stride) {
+        const int64_t j = u / t.row_units, k = u - j * t.row_units;
+        U val;
+        if (j < t.zero_from) val = src[(int64_t)index[j] * t.row_units + k];
+        else val = U{};
+        dst[u] = val;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_gather_rows(GatherArgs a, const int* index) {
+    const GatherTensor& t = a.t[blockIdx.y];
+    if (t.unit == 16) gather_units<uint4>(t, index, a.n_rows);
+    else if (t.unit == 4) gather_units<uint32_t>(t, index, a.n_rows);
+    else gather_units<uint8_t>(t, index, a.n_rows);
+}
+
+__global__ void k_split_fixup(int64_t n_new, int64_t base, float div, const int* index, const float* xyz_src,
+                              const float* sc_src, const float* rot_src, const float* samples, float* xyz_dst,
+                              float* sc_dst) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n_new) return;
+    const int64_t j = base + k;
+    const int i = index[j];
+    // build_rotation (utils/general_utils.py:84-110): normalised quaternion (r, x, y, z)
+    const float q0 = rot_src[4 * i], q1 = rot_src[4 * i + 1], q2 = rot_src[4 * i + 2], q3 = rot_src[4 * i + 3];
+    const float nrm = sqrtf(q0 * q0 + q1 * q1 + q2 * q2 + q3 * q3);
+    const float r = q0 / nrm, x = q1 / nrm, y = q2 / nrm, z = q3 / nrm;
+    const float R[9] = {1.0f - 2.0f * (y * y + z * z), 2.0f * (x * y - r * z), 2.0f * (x * z + r * y),
+                        2.0f * (x * y + r * z), 1.0f - 2.0f * (x * x + z * z), 2.0f * (y * z - r * x),
+                        2.0f * (x * z - r * y), 2.0f * (y * z + r * x), 1.0f - 2.0f * (x * x + y * y)};
+    float s[3], smp[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float sd = expf(sc_src[3 * i + a]);
+        smp[a] = sd * samples[3 * k + a];             // torch.normal(0, std) = std * z
+        s[a] = logf(sd / div);                         // log(get_scaling / (0.8 N))
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float d = R[3 * a] * smp[0] + R[3 * a + 1] * smp[1] + R[3 * a + 2] * smp[2];
+        xyz_dst[3 * j + a] = d + xyz_src[3 * i + a];
+        sc_dst[3 * j + a] = s[a];
+    }
+}
+
+__global__ void k_reset_opacity(int P, float* opacity, float* m, float* v) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const float o = fminf(1.0f / (1.0f + expf(-opacity[i])), 0.01f);
+    opacity[i] = logf(o / (1.0f - o));
+    if (m) m[i] = 0.0f;
+    if (v) v[i] = 0.0f;
+}
+
+struct TrainWs {
+    uint32_t *f0, *f1, *o0, *o1, *totals;
+    void* scan_tmp;
+    size_t bytes;
+};
+TrainWs carve(void* base, size_t P) {
+    char* b = static_cast<char*>(base);
+    TrainWs w{};
+    size_t o = 0;
+    auto take = [&](size_t n) { char* p = b ? b + o : nullptr; o += al256(n); return p; };
+    w.f0 = reinterpret_cast<uint32_t*>(take(4 * P));
+    w.f1 = reinterpret_cast<uint32_t*>(take(4 * P));
+    w.o0 = reinterpret_cast<uint32_t*>(take(4 * P));
+    w.o1 = reinterpret_cast<uint32_t*>(take(4 * P));
+    w.totals = reinterpret_cast<uint32_t*>(take(16));
+    w.scan_tmp = take(lsr::scan_temp_bytes(P));
+    w.bytes = o;
+    return w;
+}
+
+int launched(const char* what) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return lsr::fail(LSR_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+    return LSR_OK;
+}
+
+bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+int lsr_adam_step(const lsr_adam_group* groups, int32_t n_groups, double beta1, double beta2, double eps,
+                  void* stream) {
+    if (n_groups < 0 || n_groups > LSR_ADAM_MAX_GROUPS || (n_groups > 0 && !groups))
+        return lsr::fail(LSR_EINVAL, "lsr_adam_step: 0 <= n_groups <= LSR_ADAM_MAX_GROUPS");
+    AdamArgs a{};
+    int64_t chunks = 0;
+    for (int k = 0; k < n_groups; ++k) {
+        const lsr_adam_group& g = groups[k];
+        if (g.n < 0 || g.step < 1) return lsr::fail(LSR_EINVAL, "lsr_adam_step: n >= 0 and step >= 1 required");
+        if (!g.grad || g.n == 0) continue;
+        if (!g.param || !g.exp_avg || !g.exp_avg_sq) return lsr::fail(LSR_EINVAL, "lsr_adam_step: null tensor");
+        AdamGroupDev& d = a.grp[a.ng];
+        d.p = g.param; d.g = g.grad; d.m = g.exp_avg; d.v = g.exp_avg_sq; d.n = g.n;
+        // torch/optim/adam.py: bias corrections and step size in Python floats (double)
+        const double bc1 = 1.0 - std::pow(beta1, (double)g.step), bc2 = 1.0 - std::pow(beta2, (double)g.step);
+        d.w1 = (float)(1.0 - beta1); d.b2 = (float)beta2; d.w2 = (float)(1.0 - beta2);
+        d.bc2s = (float)std::sqrt(bc2); d.ss = (float)(-(g.lr / bc1)); d.eps = (float)eps;
+        d.vec = al16(g.param) && al16(g.grad) && al16(g.exp_avg) && al16(g.exp_avg_sq);
+        a.chunk0[a.ng] = chunks;
+        chunks += (g.n + ADAM_CHUNK - 1) / ADAM_CHUNK;
+        ++a.ng;
+    }
+    a.chunk0[a.ng] = chunks;
+    if (chunks == 0) return LSR_OK;
+    hipLaunchKernelGGL(k_adam, dim3((unsigned)chunks), dim3(ADAM_THREADS), 0, reinterpret_cast<hipStream_t>(stream), a);
+    return launched("adam");
+}
+
+int lsr_densify_stats(int32_t P, const int32_t* radii, const float* means2D_grad, int32_t grad_stride,
+                      float* max_radii2D, float* xyz_gradient_accum, float* denom, void* stream) {
+    if (P < 0 || grad_stride < 2) return lsr::fail(LSR_EINVAL, "lsr_densify_stats: P >= 0, grad_stride >= 2");
+    if (P == 0) return LSR_OK;
+    if (!radii || !means2D_grad || !max_radii2D || !xyz_gradient_accum || !denom)
+        return lsr::fail(LSR_EINVAL, "lsr_densify_stats: null tensor");
+    hipLaunchKernelGGL(k_densify_stats, dim3((P + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), P,
+                       radii, means2D_grad, grad_stride, max_radii2D, xyz_gradient_accum, denom);
+    return launched("densify stats");
+}
+
+int64_t lsr_train_workspace_bytes(int32_t P) { return (int64_t)carve(nullptr, (size_t)(P > 0 ? P : 1)).bytes; }
+
+int lsr_densify_plan(int32_t P, const float* xyz_gradient_accum, const float* denom, const float* scaling,
+                     float grad_threshold, float percent_dense, float extent, int32_t n_copies, int32_t* index,
+                     int64_t* counts, void* workspace, void* stream) {
+    if (P < 0 || n_copies < 1) return lsr::fail(LSR_EINVAL, "lsr_densify_plan: P >= 0, n_copies >= 1");
+    if (!counts) return lsr::fail(LSR_EINVAL, "lsr_densify_plan: counts required");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (P == 0) {
+        if (hipMemsetAsync(counts, 0, 3 * sizeof(int64_t), st) != hipSuccess) return launched("densify plan");
+        return LSR_OK;
+    }
+    if (!xyz_gradient_accum || !denom || !scaling || !index || !workspace)
+        return lsr::fail(LSR_EINVAL, "lsr_densify_plan: null tensor");
+    TrainWs w = carve(workspace, (size_t)P);
+    const dim3 grid((P + 255) / 256);
+    hipLaunchKernelGGL(k_densify_flags, grid, dim3(256), 0, st, P, xyz_gradient_accum, denom, scaling, grad_threshold,
+                       percent_dense * extent, w.f0, w.f1);
+    lsr::exclusive_scan_u32(w.f0, w.o0, (size_t)P, w.totals, w.scan_tmp, st);
+    lsr::exclusive_scan_u32(w.f1, w.o1, (size_t)P, w.totals + 1, w.scan_tmp, st);
+    hipLaunchKernelGGL(k_densify_index, grid, dim3(256), 0, st, P, n_copies, (const uint32_t*)w.f0,
+                       (const uint32_t*)w.f1, (const uint32_t*)w.o0, (const uint32_t*)w.o1, (const uint32_t*)w.totals,
+                       index, counts);
+    return launched("densify plan");
+}
+
+int lsr_prune_plan(int32_t P, const float* opacity, const float* max_radii2D, const float* scaling,
+                   float min_opacity, float max_screen_size, float extent, int32_t* index, int64_t* counts,
+                   void* workspace, void* stream) {
+    if (P < 0) return lsr::fail(LSR_EINVAL, "lsr_prune_plan: P >= 0");
+    if (!counts) return lsr::fail(LSR_EINVAL, "lsr_prune_plan: counts required");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (P == 0) {
+        if (hipMemsetAsync(counts, 0, sizeof(int64_t), st) != hipSuccess) return launched("prune plan");
+        return LSR_OK;
+    }
+    if (!opacity || !scaling || !index || !workspace || (max_screen_size > 0.0f && !max_radii2D))
+        return lsr::fail(LSR_EINVAL, "lsr_prune_plan: null tensor");
+    TrainWs w = carve(workspace, (size_t)P);
+    const dim3 grid((P + 255) / 256);
+    hipLaunchKernelGGL(k_prune_flags, grid, dim3(256), 0, st, P, opacity, max_radii2D, scaling, min_opacity,
+                       max_screen_size, 0.1f * extent, w.f0);
+    lsr::exclusive_scan_u32(w.f0, w.o0, (size_t)P, w.totals, w.scan_tmp, st);
+    hipLaunchKernelGGL(k_prune_index, grid, dim3(256), 0, st, P, (const uint32_t*)w.f0, (const uint32_t*)w.o0,
+                       (const uint32_t*)w.totals, index, counts);
+    return launched("prune plan");
+}
+
+int lsr_gather_rows(int32_t n_tensors, const lsr_row_tensor* t, const int32_t* index, int64_t n_rows, void* stream) {
+    if (n_tensors < 0 || n_tensors > LSR_GATHER_MAX_TENSORS || n_rows < 0 || (n_tensors > 0 && !t))
+        return lsr::fail(LSR_EINVAL, "lsr_gather_rows: 0 <= n_tensors <= LSR_GATHER_MAX_TENSORS, n_rows >= 0");
+    if (n_tensors == 0 || n_rows == 0) return LSR_OK;
+    GatherArgs a{};
+    a.n_rows = n_rows;
+    int64_t most = 0;
+    bool needs_index = false;
+    for (int k = 0; k < n_tensors; ++k) {
+        const lsr_row_tensor& r = t[k];
+        if (r.row_bytes <= 0 || !r.dst || (r.zero_from > 0 && !r.src))
+            return lsr::fail(LSR_EINVAL, "lsr_gather_rows: row_bytes > 0, dst (and src unless all rows are zero)");
+        const uintptr_t bits = reinterpret_cast<uintptr_t>(r.src) | reinterpret_cast<uintptr_t>(r.dst) |
+                               (uintptr_t)r.row_bytes;
+        const int unit = (bits & 15u) == 0 ? 16 : (bits & 3u) == 0 ? 4 : 1;
+        a.t[k].src = static_cast<const char*>(r.src);
+        a.t[k].dst = static_cast<char*>(r.dst);
+        a.t[k].unit = unit;
+        a.t[k].row_units = r.row_bytes / unit;
+        a.t[k].zero_from = r.zero_from;
+        needs_index = needs_index || r.zero_from > 0;
+        most = std::max(most, n_rows * a.t[k].row_units);
+    }
+    if (needs_index && !index) return lsr::fail(LSR_EINVAL, "lsr_gather_rows: index required");
+    const unsigned bx = (unsigned)std::min<int64_t>((most + 255) / 256, 2048);
+    hipLaunchKernelGGL(k_gather_rows, dim3(bx, n_tensors), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a,
+                       index);
+    return launched("gather rows");
+}
+
+int lsr_split_fixup(int64_t n_new, int64_t base, int32_t n_copies, const int32_t* index, const float* xyz_src,
+                    const float* scaling_src, const float* rotation_src, const float* samples, float* xyz_dst,
+                    float* scaling_dst, void* stream) {
+    if (n_new < 0 || base < 0 || n_copies < 1) return lsr::fail(LSR_EINVAL, "lsr_split_fixup: bad sizes");
+    if (n_new == 0) return LSR_OK;
+    if (!index || !xyz_src || !scaling_src || !rotation_src || !samples || !xyz_dst || !scaling_dst)
+        return lsr::fail(LSR_EINVAL, "lsr_split_fixup: null tensor");
+    // get_scaling / (0.8 * N): the divisor is a Python float, applied in float32
+    const float div = (float)(0.8 * (double)n_copies);
+    hipLaunchKernelGGL(k_split_fixup, dim3((unsigned)((n_new + 255) / 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), n_new, base, div, index, xyz_src, scaling_src,
+                       rotation_src, samples, xyz_dst, scaling_dst);
+    return launched("split fixup");
+}
+
+int lsr_reset_opacity(int32_t P, float* opacity, float* exp_avg, float* exp_avg_sq, void* stream) {
+    if (P < 0) return lsr::fail(LSR_EINVAL, "lsr_reset_opacity: P >= 0");
+    if (P == 0) return LSR_OK;
+    if (!opacity) return lsr::fail(LSR_EINVAL, "lsr_reset_opacity: opacity required");
+    hipLaunchKernelGGL(k_reset_opacity, dim3((P + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), P,
+                       opacity, exp_avg, exp_avg_sq);
+    return launched("reset opacity");
+}
+
+}  // extern "C"

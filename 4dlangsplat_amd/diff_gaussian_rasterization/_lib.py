@@ -62,7 +62,36 @@ class DeformNet(ctypes.Structure):
                 ("b2", ctypes.c_void_p * 5)]
 
 
+class AdamGroup(ctypes.Structure):
+    """include/lsr_train.h lsr_adam_group"""
+    _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
+                ("exp_avg_sq", ctypes.c_void_p), ("n", ctypes.c_int64), ("lr", ctypes.c_double),
+                ("step", ctypes.c_int64)]
+
+
+class RowTensor(ctypes.Structure):
+    """include/lsr_train.h lsr_row_tensor"""
+    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("row_bytes", ctypes.c_int64),
+                ("zero_from", ctypes.c_int64)]
+
+
+ADAM_MAX_GROUPS = 16        # LSR_ADAM_MAX_GROUPS
+GATHER_MAX_TENSORS = 32     # LSR_GATHER_MAX_TENSORS
+
+_vp = ctypes.c_void_p
 SIGNATURES = {
+    "lsr_adam_step": (ctypes.c_int, [ctypes.POINTER(AdamGroup), ctypes.c_int32, ctypes.c_double, ctypes.c_double,
+                                     ctypes.c_double, _vp]),
+    "lsr_densify_stats": (ctypes.c_int, [ctypes.c_int32, _vp, _vp, ctypes.c_int32, _vp, _vp, _vp, _vp]),
+    "lsr_train_workspace_bytes": (ctypes.c_int64, [ctypes.c_int32]),
+    "lsr_densify_plan": (ctypes.c_int, [ctypes.c_int32, _vp, _vp, _vp, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                        ctypes.c_int32, _vp, _vp, _vp, _vp]),
+    "lsr_prune_plan": (ctypes.c_int, [ctypes.c_int32, _vp, _vp, _vp, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                      _vp, _vp, _vp, _vp]),
+    "lsr_gather_rows": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(RowTensor), _vp, ctypes.c_int64, _vp]),
+    "lsr_split_fixup": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, _vp, _vp, _vp, _vp, _vp, _vp,
+                                       _vp, _vp]),
+    "lsr_reset_opacity": (ctypes.c_int, [ctypes.c_int32, _vp, _vp, _vp, _vp]),
     "lsr_version": (ctypes.c_int, []),
     "lsr_last_error": (ctypes.c_char_p, []),
     "lsr_geom_bytes": (ctypes.c_int64, [ctypes.c_int32]),
