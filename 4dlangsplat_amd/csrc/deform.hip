@@ -189,6 +189,365 @@ void launch_deform_fwd(const DeformArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_deform_fwd, dim3((a.P + DN - 1) / DN), dim3(256), 0, st, a);
 }
 
+// ==== backward ====================================================================================
+// Phase A, one block per 64 Gaussians (the forward's tiling): recompute the features X and the
+// hidden rows A0 = relu(X Wf^T + bf); per head, Z1 = A0 W1^T + b1 (A1 = relu(Z1) saved), the
+// upstream gradient G of the head's outputs through the last layer, dZ1 = (G W2) * [Z1 > 0] (saved),
+// and dA0 += dZ1 W1, all on the bf16 hi/lo MFMA of the forward with transposed weight packs; then
+// dH0 = dA0 * [H0 > 0] (saved), dX = dH0 Wf, and per Gaussian the HexPlane backward: each plane's
+// sample gets dX times the product of the other five planes of its scale, scattered to the 4 bilinear
+// taps (float atomics into a channel-last gradient copy: the 16 channels of a tap are one 64-byte
+// segment), and the coordinate gradient (zero where border padding clips) goes to d_means3D.
+constexpr int DGP = 64 + 8;   // LDS row pitch (bf16) of the upstream-gradient rows (K padded to 64)
+
+__global__ void __launch_bounds__(256) k_deform_bwd_a(DeformBwdArgs b) {
+    __shared__ __attribute__((aligned(16))) __bf16 s_xh[DN * DXP];
+    __shared__ __attribute__((aligned(16))) __bf16 s_xl[DN * DXP];
+    __shared__ __attribute__((aligned(16))) __bf16 s_ah[DN * DAP];
+    __shared__ __attribute__((aligned(16))) __bf16 s_al[DN * DAP];
+    __shared__ __attribute__((aligned(16))) __bf16 s_bh[DN * DAP];
+    __shared__ __attribute__((aligned(16))) __bf16 s_bl[DN * DAP];
+    __shared__ __attribute__((aligned(16))) __bf16 s_gh[DN * DGP];
+    __shared__ __attribute__((aligned(16))) __bf16 s_gl[DN * DGP];
+    __shared__ float s_dx[DN][DFEAT + 1];
+    const DeformArgs& a = b.f;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int g0 = blockIdx.x * DN;
+    const int c0s[6] = {0, 0, 0, 1, 1, 2}, c1s[6] = {1, 2, 3, 2, 3, 3};
+
+    // ---- features (as the forward), saved as fp32 for the feature_out weight gradient ----------
+    {
+        const int gl = tid >> 2, q = tid & 3;
+        const int g = min(g0 + gl, a.P - 1);
+        float crd[4];
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            crd[c] = (a.means3D[3 * g + c] - a.aabb[c]) * (2.0f / (a.aabb[3 + c] - a.aabb[c])) - 1.0f;
+        crd[3] = a.time[g];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            float4 prod = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+#pragma unroll
+            for (int ci = 0; ci < 6; ++ci) {
+                const int pi = 6 * s + ci;
+                const int W = a.pw[pi], H = a.ph[pi];
+                const float ix = fminf(fmaxf((crd[c0s[ci]] + 1.0f) * 0.5f * (float)(W - 1), 0.0f), (float)(W - 1));
+                const float iy = fminf(fmaxf((crd[c1s[ci]] + 1.0f) * 0.5f * (float)(H - 1), 0.0f), (float)(H - 1));
+                const int x0 = (int)floorf(ix), y0 = (int)floorf(iy);
+                const int x1 = min(x0 + 1, W - 1), y1 = min(y0 + 1, H - 1);
+                const float fx = ix - (float)x0, fy = iy - (float)y0;
+                const float4* pl = reinterpret_cast<const float4*>(a.planes + a.poff[pi]) + q;
+                const float4 v00 = pl[(y0 * W + x0) * 4], v01 = pl[(y0 * W + x1) * 4];
+                const float4 v10 = pl[(y1 * W + x0) * 4], v11 = pl[(y1 * W + x1) * 4];
+                const float w00 = (1.0f - fx) * (1.0f - fy), w01 = fx * (1.0f - fy), w10 = (1.0f - fx) * fy, w11 = fx * fy;
+                prod.x *= v00.x * w00 + v01.x * w01 + v10.x * w10 + v11.x * w11;
+                prod.y *= v00.y * w00 + v01.y * w01 + v10.y * w10 + v11.y * w11;
+                prod.z *= v00.z * w00 + v01.z * w01 + v10.z * w10 + v11.z * w11;
+                prod.w *= v00.w * w00 + v01.w * w01 + v10.w * w10 + v11.w * w11;
+            }
+            const float f[4] = {prod.x, prod.y, prod.z, prod.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                __bf16 hi, lo;
+                dsplit(f[i], hi, lo);
+                s_xh[gl * DXP + 16 * s + 4 * q + i] = hi;
+                s_xl[gl * DXP + 16 * s + 4 * q + i] = lo;
+            }
+            if (g0 + gl < a.P)
+                *reinterpret_cast<float4*>(b.sX + (size_t)(g0 + gl) * DFEAT + 16 * s + 4 * q) = prod;
+        }
+    }
+    __syncthreads();
+
+    const int col = 32 * wave + (lane & 31), hh = lane >> 5;
+    auto row_of = [&](int mt, int q) { return 32 * mt + (q & 3) + 8 * (q >> 2) + 4 * hh; };
+    // ---- A0 = relu(X Wf^T + bf), saved -------------------------------------------------------------
+    {
+        df32x16 acc[2] = {df32x16{}, df32x16{}};
+        mlp_ntile<DFEAT>(acc, s_xh, s_xl, DXP, wave, a.wf_h, a.wf_l);
+        store_hidden(acc, wave, a.b_feat, s_ah, s_al);
+        const float bias = a.b_feat[col];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int g = g0 + row_of(mt, q);
+                if (g < a.P) b.sA0[(size_t)g * DWID + col] = fmaxf(acc[mt][q] + bias, 0.0f);
+            }
+    }
+    __syncthreads();
+
+    df32x16 dA0[2] = {df32x16{}, df32x16{}};
+    for (int hd = 0; hd < 5; ++hd) {
+        const int nout = kHeadOut[hd];
+        // upstream gradient rows of this head, K padded to 64
+        for (int i = tid; i < DN * 64; i += 256) {
+            const int r = i >> 6, k = i & 63, g = g0 + r;
+            const float v = (k < nout && g < a.P) ? b.up[hd][(size_t)g * nout + k] : 0.0f;
+            __bf16 hi, lo;
+            dsplit(v, hi, lo);
+            s_gh[r * DGP + k] = hi;
+            s_gl[r * DGP + k] = lo;
+        }
+        // Z1 for this wave's 32 columns (its rows finish before the sync below)
+        df32x16 z[2] = {df32x16{}, df32x16{}};
+        mlp_ntile<DWID>(z, s_ah, s_al, DAP, wave, a.w1_h + (size_t)hd * DWID * DWID, a.w1_l + (size_t)hd * DWID * DWID);
+        {
+            const float bias = a.b1[hd][col];
+            float* sA1 = b.sA1 + (size_t)hd * a.P * DWID;
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    z[mt][q] += bias;
+                    const int g = g0 + row_of(mt, q);
+                    if (g < a.P) sA1[(size_t)g * DWID + col] = fmaxf(z[mt][q], 0.0f);
+                }
+        }
+        __syncthreads();   // G rows complete
+        df32x16 d[2] = {df32x16{}, df32x16{}};
+        mlp_ntile<64>(d, s_gh, s_gl, DGP, wave, b.w2t_h + (size_t)hd * DWID * 64, b.w2t_l + (size_t)hd * DWID * 64);
+        {
+            float* sdZ1 = b.sdZ1 + (size_t)hd * a.P * DWID;
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const int r = row_of(mt, q), g = g0 + r;
+                    const float v = z[mt][q] > 0.0f ? d[mt][q] : 0.0f;
+                    __bf16 hi, lo;
+                    dsplit(v, hi, lo);
+                    s_bh[r * DAP + col] = hi;
+                    s_bl[r * DAP + col] = lo;
+                    if (g < a.P) sdZ1[(size_t)g * DWID + col] = v;
+                }
+        }
+        __syncthreads();   // dZ1 rows complete
+        mlp_ntile<DWID>(dA0, s_bh, s_bl, DAP, wave, b.w1t_h + (size_t)hd * DWID * DWID,
+                        b.w1t_l + (size_t)hd * DWID * DWID);
+        __syncthreads();   // dZ1 / G rows consumed before the next head rewrites them
+    }
+
+    // ---- dH0 = dA0 * [H0 > 0] (saved), then dX = dH0 Wf --------------------------------------------
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int r = row_of(mt, q), g = g0 + r;
+            const bool on = (float)s_ah[r * DAP + col] + (float)s_al[r * DAP + col] > 0.0f;
+            const float v = on ? dA0[mt][q] : 0.0f;
+            __bf16 hi, lo;
+            dsplit(v, hi, lo);
+            s_bh[r * DAP + col] = hi;
+            s_bl[r * DAP + col] = lo;
+            if (g < a.P) b.sdH0[(size_t)g * DWID + col] = v;
+        }
+    __syncthreads();
+    if (wave == 0) {
+        df32x16 acc[2] = {df32x16{}, df32x16{}};
+        mlp_ntile<DWID>(acc, s_bh, s_bl, DAP, 0, b.wft_h, b.wft_l);
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) s_dx[row_of(mt, q)][lane & 31] = acc[mt][q];
+    }
+    __syncthreads();
+
+    // ---- HexPlane backward: 4 threads per Gaussian, 4 channels each ----------------------------------
+    {
+        const int gl = tid >> 2, q = tid & 3;
+        const bool ok = g0 + gl < a.P;
+        const int g = min(g0 + gl, a.P - 1);
+        float crd[4];
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            crd[c] = (a.means3D[3 * g + c] - a.aabb[c]) * (2.0f / (a.aabb[3 + c] - a.aabb[c])) - 1.0f;
+        crd[3] = a.time[g];
+        float dq[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            float4 v[6];
+#pragma unroll
+            for (int ci = 0; ci < 6; ++ci) {   // the six samples of this scale
+                const int pi = 6 * s + ci;
+                const int W = a.pw[pi], H = a.ph[pi];
+                const float ix = fminf(fmaxf((crd[c0s[ci]] + 1.0f) * 0.5f * (float)(W - 1), 0.0f), (float)(W - 1));
+                const float iy = fminf(fmaxf((crd[c1s[ci]] + 1.0f) * 0.5f * (float)(H - 1), 0.0f), (float)(H - 1));
+                const int x0 = (int)floorf(ix), y0 = (int)floorf(iy);
+                const int x1 = min(x0 + 1, W - 1), y1 = min(y0 + 1, H - 1);
+                const float fx = ix - (float)x0, fy = iy - (float)y0;
+                const float4* pl = reinterpret_cast<const float4*>(a.planes + a.poff[pi]) + q;
+                const float4 v00 = pl[(y0 * W + x0) * 4], v01 = pl[(y0 * W + x1) * 4];
+                const float4 v10 = pl[(y1 * W + x0) * 4], v11 = pl[(y1 * W + x1) * 4];
+                const float w00 = (1.0f - fx) * (1.0f - fy), w01 = fx * (1.0f - fy), w10 = (1.0f - fx) * fy, w11 = fx * fy;
+                v[ci] = make_float4(v00.x * w00 + v01.x * w01 + v10.x * w10 + v11.x * w11,
+                                    v00.y * w00 + v01.y * w01 + v10.y * w10 + v11.y * w11,
+                                    v00.z * w00 + v01.z * w01 + v10.z * w10 + v11.z * w11,
+                                    v00.w * w00 + v01.w * w01 + v10.w * w10 + v11.w * w11);
+            }
+            const float dxv[4] = {s_dx[gl][16 * s + 4 * q], s_dx[gl][16 * s + 4 * q + 1], s_dx[gl][16 * s + 4 * q + 2],
+                                  s_dx[gl][16 * s + 4 * q + 3]};
+#pragma unroll
+            for (int ci = 0; ci < 6; ++ci) {
+                float4 oth = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+#pragma unroll
+                for (int cj = 0; cj < 6; ++cj)
+                    if (cj != ci) {
+                        oth.x *= v[cj].x; oth.y *= v[cj].y; oth.z *= v[cj].z; oth.w *= v[cj].w;
+                    }
+                const float dv[4] = {dxv[0] * oth.x, dxv[1] * oth.y, dxv[2] * oth.z, dxv[3] * oth.w};
+                const int pi = 6 * s + ci;
+                const int W = a.pw[pi], H = a.ph[pi];
+                const float rx = (crd[c0s[ci]] + 1.0f) * 0.5f * (float)(W - 1);
+                const float ry = (crd[c1s[ci]] + 1.0f) * 0.5f * (float)(H - 1);
+                const float ix = fminf(fmaxf(rx, 0.0f), (float)(W - 1));
+                const float iy = fminf(fmaxf(ry, 0.0f), (float)(H - 1));
+                const int x0 = (int)floorf(ix), y0 = (int)floorf(iy);
+                const int x1 = min(x0 + 1, W - 1), y1 = min(y0 + 1, H - 1);
+                const float fx = ix - (float)x0, fy = iy - (float)y0;
+                const float4* pl = reinterpret_cast<const float4*>(a.planes + a.poff[pi]) + q;
+                const float4 t00 = pl[(y0 * W + x0) * 4], t01 = pl[(y0 * W + x1) * 4];
+                const float4 t10 = pl[(y1 * W + x0) * 4], t11 = pl[(y1 * W + x1) * 4];
+                const float w00 = (1.0f - fx) * (1.0f - fy), w01 = fx * (1.0f - fy), w10 = (1.0f - fx) * fy, w11 = fx * fy;
+                if (ok) {
+                    float* gp = b.dplanes + a.poff[pi] + 4 * q;
+                    const size_t o00 = (size_t)(y0 * W + x0) * 16, o01 = (size_t)(y0 * W + x1) * 16;
+                    const size_t o10 = (size_t)(y1 * W + x0) * 16, o11 = (size_t)(y1 * W + x1) * 16;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        if (dv[i] == 0.0f) continue;
+                        atomicAdd(gp + o00 + i, dv[i] * w00);
+                        if (w01 != 0.0f) atomicAdd(gp + o01 + i, dv[i] * w01);
+                        if (w10 != 0.0f) atomicAdd(gp + o10 + i, dv[i] * w10);
+                        if (w11 != 0.0f) atomicAdd(gp + o11 + i, dv[i] * w11);
+                    }
+                }
+                const float a00[4] = {t00.x, t00.y, t00.z, t00.w}, a01[4] = {t01.x, t01.y, t01.z, t01.w};
+                const float a10[4] = {t10.x, t10.y, t10.z, t10.w}, a11[4] = {t11.x, t11.y, t11.z, t11.w};
+                float dix = 0.0f, diy = 0.0f;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    dix += dv[i] * ((a01[i] - a00[i]) * (1.0f - fy) + (a11[i] - a10[i]) * fy);
+                    diy += dv[i] * ((a10[i] - a00[i]) * (1.0f - fx) + (a11[i] - a01[i]) * fx);
+                }
+                if (rx > 0.0f && rx < (float)(W - 1)) dq[c0s[ci]] += dix * 0.5f * (float)(W - 1);
+                if (ry > 0.0f && ry < (float)(H - 1)) dq[c1s[ci]] += diy * 0.5f * (float)(H - 1);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            dq[c] += __shfl_xor(dq[c], 1);
+            dq[c] += __shfl_xor(dq[c], 2);
+        }
+        if (ok && q == 0) {
+            const size_t gg = (size_t)(g0 + gl);
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+                b.d_means3D[3 * gg + c] = b.up[0][3 * gg + c] + dq[c] * (2.0f / (a.aabb[3 + c] - a.aabb[c]));
+        }
+    }
+}
+
+void launch_deform_bwd_a(const DeformBwdArgs& a, hipStream_t st) {
+    if (a.f.P <= 0) return;
+    hipLaunchKernelGGL(k_deform_bwd_a, dim3((a.f.P + DN - 1) / DN), dim3(256), 0, st, a);
+}
+
+// Phase B: C[M][N] += sum_g L[g][m] R[g][n] (M, N <= 128), bias[m] += sum_g L[g][m]; split-K over
+// blocks of rows_per_block rows (blockIdx.x), one job per blockIdx.y.  Per 64-row chunk both
+// operands go to LDS transposed ([m][g], [n][g]) as bf16 hi/lo, the 32x32 output tiles are spread
+// over the 4 waves, and each block adds its partial to C with one atomic per element.
+constexpr int ATB_K = 64, ATB_P = ATB_K + 8;
+
+__global__ void __launch_bounds__(256) k_atb(AtbArgs ga) {
+    __shared__ __attribute__((aligned(16))) __bf16 s_lh[128 * ATB_P];
+    __shared__ __attribute__((aligned(16))) __bf16 s_ll[128 * ATB_P];
+    __shared__ __attribute__((aligned(16))) __bf16 s_rh[128 * ATB_P];
+    __shared__ __attribute__((aligned(16))) __bf16 s_rl[128 * ATB_P];
+    const AtbJob& j = ga.job[blockIdx.y];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+    const int M = j.M, N = j.N, Mt = (M + 31) / 32, Nt = (N + 31) / 32, ntile = Mt * Nt;
+    const int64_t row0 = (int64_t)blockIdx.x * ga.rows_per_block;
+    const int64_t row1 = min((int64_t)ga.P, row0 + ga.rows_per_block);
+    if (row0 >= row1) return;
+    df32x16 acc[4] = {df32x16{}, df32x16{}, df32x16{}, df32x16{}};
+    float bsum = 0.0f;
+    for (int64_t k0 = row0; k0 < row1; k0 += ATB_K) {
+        // stage: element (g, m) of L -> s_l[m][g]; rows past row1 and columns past M are zero
+        for (int i = tid; i < ATB_K * 128; i += 256) {
+            const int gi = i >> 7, m = i & 127;
+            const int64_t g = k0 + gi;
+            const bool in = g < row1;
+            const float lv = (in && m < M) ? j.L[g * M + m] : 0.0f;
+            const float rv = (in && m < N) ? j.R[g * N + m] : 0.0f;
+            __bf16 h, l;
+            dsplit(lv, h, l);
+            s_lh[m * ATB_P + gi] = h;
+            s_ll[m * ATB_P + gi] = l;
+            dsplit(rv, h, l);
+            s_rh[m * ATB_P + gi] = h;
+            s_rl[m * ATB_P + gi] = l;
+            if (j.bias && m < M) bsum += lv;   // thread tid always owns column m = tid & 127
+        }
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int tile = wave + 4 * t;
+            if (tile >= ntile) break;
+            const int mt = tile / Nt, nt = tile - mt * Nt;
+#pragma unroll
+            for (int ks = 0; ks < ATB_K / 16; ++ks) {
+                const int kk = 16 * ks + 8 * hh;
+                const dbf16x8 ah = *reinterpret_cast<const dbf16x8*>(s_lh + (32 * mt + r) * ATB_P + kk);
+                const dbf16x8 al = *reinterpret_cast<const dbf16x8*>(s_ll + (32 * mt + r) * ATB_P + kk);
+                const dbf16x8 bh = *reinterpret_cast<const dbf16x8*>(s_rh + (32 * nt + r) * ATB_P + kk);
+                const dbf16x8 bl = *reinterpret_cast<const dbf16x8*>(s_rl + (32 * nt + r) * ATB_P + kk);
+                acc[t] = DMFMA(ah, bh, acc[t]);
+                acc[t] = DMFMA(ah, bl, acc[t]);
+                acc[t] = DMFMA(al, bh, acc[t]);
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int tile = wave + 4 * t;
+        if (tile >= ntile) break;
+        const int mt = tile / Nt, nt = tile - mt * Nt;
+        const int n = 32 * nt + r;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int m = 32 * mt + (q & 3) + 8 * (q >> 2) + 4 * hh;
+            if (m < M && n < N) atomicAdd(j.C + (size_t)m * N + n, acc[t][q]);
+        }
+    }
+    // bias partials: threads tid and tid + 128 own the same column
+    if (j.bias) {
+        __shared__ float s_b[256];
+        s_b[tid] = bsum;
+        __syncthreads();
+        if (tid < M) atomicAdd(j.bias + tid, s_b[tid] + s_b[tid + 128]);
+    }
+}
+
+void launch_atb(const AtbArgs& a, int njobs, hipStream_t st) {
+    if (a.P <= 0 || njobs <= 0) return;
+    const int nb = (a.P + a.rows_per_block - 1) / a.rows_per_block;
+    hipLaunchKernelGGL(k_atb, dim3(nb, njobs), dim3(256), 0, st, a);
+}
+
+// packed channel-last gradient [H][W][16] -> torch [16][H][W], added
+__global__ void k_unpack_plane_grad(const float* __restrict__ src, float* __restrict__ dst, int H, int W) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;   // over 16 * H * W destination floats
+    if (i >= H * W * 16) return;
+    const int hw = i % (H * W), c = i / (H * W);
+    dst[i] += src[(size_t)hw * 16 + c];
+}
+
+void launch_unpack_plane_grad(const float* src, float* dst, int H, int W, hipStream_t st) {
+    hipLaunchKernelGGL(k_unpack_plane_grad, dim3((H * W * 16 + 255) / 256), dim3(256), 0, st, src, dst, H, W);
+}
+
 // ---- parameter packing ----------------------------------------------------------------------------
 // plane [C=16][H][W] (torch) -> [H][W][16]
 __global__ void k_pack_plane(const float* __restrict__ src, float* __restrict__ dst, int H, int W) {
@@ -208,6 +567,24 @@ __global__ void k_pack_weight(const float* __restrict__ src, __bf16* __restrict_
     dsplit(v, h, l);
     hi[i] = h;
     lo[i] = l;
+}
+
+// fp32 [rows][cols] -> bf16 hi / lo [cols][k_pad], dst[c][r] = src[r][c], zero for r >= rows
+__global__ void k_pack_weight_t(const float* __restrict__ src, __bf16* __restrict__ hi, __bf16* __restrict__ lo,
+                                int rows, int cols, int k_pad) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= cols * k_pad) return;
+    const int c = i / k_pad, r = i - c * k_pad;
+    const float v = r < rows ? src[(size_t)r * cols + c] : 0.0f;
+    __bf16 h, l;
+    dsplit(v, h, l);
+    hi[i] = h;
+    lo[i] = l;
+}
+
+void launch_pack_weight_t(const float* src, __bf16* hi, __bf16* lo, int rows, int cols, int k_pad, hipStream_t st) {
+    hipLaunchKernelGGL(k_pack_weight_t, dim3((cols * k_pad + 255) / 256), dim3(256), 0, st, src, hi, lo, rows, cols,
+                       k_pad);
 }
 
 void launch_pack_plane(const float* src, float* dst, int H, int W, hipStream_t st) {

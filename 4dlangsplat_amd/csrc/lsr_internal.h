@@ -189,6 +189,37 @@ struct DeformArgs {
 void launch_deform_fwd(const DeformArgs& a, hipStream_t st);
 void launch_pack_plane(const float* src, float* dst, int H, int W, hipStream_t st);
 void launch_pack_weight(const float* src, __bf16* hi, __bf16* lo, int rows, int rows_pad, int cols, hipStream_t st);
+// transposed packing: src fp32 [rows][cols] -> hi / lo [cols][k_pad] with dst[c][r] = src[r][c], zero for r >= rows
+void launch_pack_weight_t(const float* src, __bf16* hi, __bf16* lo, int rows, int cols, int k_pad, hipStream_t st);
+
+// deformation backward (deform.hip): phase A per 64 Gaussians (recompute, data gradients, plane
+// scatter, saved activations), phase B the weight gradients as split-K A^T B products
+struct DeformBwdArgs {
+    DeformArgs f;                     // planes, packed weights, biases, means3D, time, aabb
+    const __bf16 *w1t_h, *w1t_l;      // [5][128 in][128 out]
+    const __bf16 *w2t_h, *w2t_l;      // [5][128 in][64 out, zero padded]
+    const __bf16 *wft_h, *wft_l;      // [32 feat][128 hidden]
+    const float* up[5];               // gradients of the five outputs
+    float* d_means3D;
+    float* dplanes;                   // packed channel-last gradient planes (same offsets as f.planes)
+    float *sX, *sA0, *sdH0, *sA1, *sdZ1;   // saved: [P,32], [P,128], [P,128], [5][P,128], [5][P,128]
+};
+void launch_deform_bwd_a(const DeformBwdArgs& a, hipStream_t st);
+struct AtbJob {                        // C[M][N] += sum_g L[g][m] R[g][n]; bias[m] += sum_g L[g][m]
+    const float* L;
+    const float* R;
+    float* C;
+    float* bias;
+    int M, N;
+};
+constexpr int LSR_ATB_MAX_JOBS = 12;
+struct AtbArgs {
+    AtbJob job[LSR_ATB_MAX_JOBS];
+    int P;
+    int rows_per_block;
+};
+void launch_atb(const AtbArgs& a, int njobs, hipStream_t st);
+void launch_unpack_plane_grad(const float* src, float* dst, int H, int W, hipStream_t st);
 
 void launch_preprocess(const PreprocessArgs& a, hipStream_t st);
 void launch_preprocess_bwd(const PreprocessBwdArgs& a, bool accumulate, hipStream_t st);

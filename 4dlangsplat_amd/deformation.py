@@ -8,8 +8,9 @@ language feature passes through (no_dlang, the reference default).  Parameters k
 reference's names (`from_reference_state_dict` accepts `deform_network.state_dict()`), so a
 trained `deformation.pth` loads as is.
 
-This round provides the forward (the render path, e.g. render.py); gradients are not produced,
-so training keeps the reference module for now.  There is no CPU fallback.
+Forward (the render path) and backward (lsr_deform_backward: input gradients, and the gradients
+of every plane and Linear parameter, accumulated into `grads`); `apply` runs the forward inside
+autograd.  There is no CPU fallback.
 """
 import ctypes
 from typing import Dict, Sequence
@@ -89,3 +90,66 @@ class DeformationField:
         return outs + (lang, None)
 
     __call__ = forward
+
+    # ---- backward (lsr_deform_backward) -------------------------------------------------------
+    def zero_grad(self):
+        """Parameter gradients (torch layouts, names as the parameters) set to zero."""
+        self.grads = {k: torch.zeros_like(v) for k, v in self.p.items() if k != "grid.aabb"}
+
+    def backward(self, means3D, time, d_means3D, d_scales, d_rotations, d_opacity, d_shs):
+        """Gradients of forward() given the gradients of its five outputs: returns the input
+        gradients (means3D, scales, rotations, opacity, shs) and ADDS the parameter gradients to
+        self.grads (as torch accumulates .grad).  Call prepare() after parameter updates first."""
+        L = _lib.load()
+        if not hasattr(self, "grads"):
+            self.zero_grad()
+        P = means3D.shape[0]
+        f = lambda t, shape: t.detach().to(self.device, torch.float32).reshape(shape).contiguous()   # noqa: E731
+        m = f(means3D, (P, 3))
+        t = f(time, (P,)) if torch.is_tensor(time) and time.numel() == P else \
+            torch.full((P,), float(time), device=self.device)
+        ups = (f(d_means3D, (P, 3)), f(d_scales, (P, 3)), f(d_rotations, (P, 4)), f(d_opacity, (P, 1)),
+               f(d_shs, (P, 16, 3)))
+        dm = torch.empty_like(m)
+        g = _lib.DeformGrads()
+        for s in range(len(self.multires)):
+            for ci in range(6):
+                g.planes[s][ci] = self.grads[f"grid.grids.{s}.{ci}"].data_ptr()
+        g.w_feat, g.b_feat = self.grads["feature_out.0.weight"].data_ptr(), self.grads["feature_out.0.bias"].data_ptr()
+        for h, name in enumerate(HEADS):
+            g.w1[h], g.b1[h] = self.grads[name + ".1.weight"].data_ptr(), self.grads[name + ".1.bias"].data_ptr()
+            g.w2[h], g.b2[h] = self.grads[name + ".3.weight"].data_ptr(), self.grads[name + ".3.bias"].data_ptr()
+        nbytes = int(L.lsr_deform_backward_scratch_bytes(ctypes.byref(self.net), P))
+        if nbytes < 0:
+            _lib.check(1, "lsr_deform_backward_scratch_bytes")
+        if getattr(self, "_scratch", None) is None or self._scratch.numel() < nbytes:
+            self._scratch = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        vp = ctypes.c_void_p
+        _lib.check(L.lsr_deform_backward(ctypes.byref(self.net), vp(self.workspace.data_ptr()), P, vp(m.data_ptr()),
+                                         vp(t.data_ptr()), *[vp(u.data_ptr()) for u in ups], vp(dm.data_ptr()),
+                                         ctypes.byref(g), vp(self._scratch.data_ptr()),
+                                         vp(torch.cuda.current_stream(self.device).cuda_stream)),
+                   "lsr_deform_backward")
+        return (dm,) + ups[1:]
+
+    def apply(self, means3D, scales, rotations, opacity, shs, lang, time):
+        """forward() inside autograd: the input gradients flow back through lsr_deform_backward and
+        the parameter gradients accumulate into self.grads."""
+        outs = _DeformFunction.apply(self, time, means3D, scales, rotations, opacity, shs)
+        return tuple(outs) + (lang, None)
+
+
+class _DeformFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, field, time, means3D, scales, rotations, opacity, shs):
+        ctx.field, ctx.time = field, time
+        ctx.save_for_backward(means3D)
+        return field.forward(means3D, scales, rotations, opacity, shs, None, time)[:5]
+
+    @staticmethod
+    def backward(ctx, dm, ds, dr, do, dsh):
+        (means3D,) = ctx.saved_tensors
+        P = means3D.shape[0]
+        z = lambda g, n: g if g is not None else torch.zeros(P, n, device=means3D.device)   # noqa: E731
+        grads = ctx.field.backward(means3D, ctx.time, z(dm, 3), z(ds, 3), z(dr, 4), z(do, 1), z(dsh, 48))
+        return (None, None) + tuple(grads)

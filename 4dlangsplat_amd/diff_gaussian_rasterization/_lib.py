@@ -62,6 +62,13 @@ class DeformNet(ctypes.Structure):
                 ("b2", ctypes.c_void_p * 5)]
 
 
+class DeformGrads(ctypes.Structure):
+    """include/lsr_deform.h lsr_deform_grads"""
+    _fields_ = [("planes", (ctypes.c_void_p * 6) * 4), ("w_feat", ctypes.c_void_p), ("b_feat", ctypes.c_void_p),
+                ("w1", ctypes.c_void_p * 5), ("b1", ctypes.c_void_p * 5), ("w2", ctypes.c_void_p * 5),
+                ("b2", ctypes.c_void_p * 5)]
+
+
 class AdamGroup(ctypes.Structure):
     """include/lsr_train.h lsr_adam_group"""
     _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
@@ -132,6 +139,9 @@ SIGNATURES = {
     "lsr_deform_prepare": (ctypes.c_int, [ctypes.POINTER(DeformNet), ctypes.c_void_p, ctypes.c_void_p]),
     "lsr_deform_forward": (ctypes.c_int, [ctypes.POINTER(DeformNet), ctypes.c_void_p, ctypes.c_int32]
                            + [ctypes.c_void_p] * 11 + [ctypes.c_void_p]),
+    "lsr_deform_backward_scratch_bytes": (ctypes.c_int64, [ctypes.POINTER(DeformNet), ctypes.c_int32]),
+    "lsr_deform_backward": (ctypes.c_int, [ctypes.POINTER(DeformNet), ctypes.c_void_p, ctypes.c_int32]
+                            + [ctypes.c_void_p] * 8 + [ctypes.POINTER(DeformGrads), ctypes.c_void_p, ctypes.c_void_p]),
     "lsr_profile_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64),
                                         ctypes.c_int32]),
 }

@@ -49,6 +49,31 @@ int lsr_deform_forward(const lsr_deform_net *net, const void *workspace, int32_t
                        const float *time, float *out_means3D, float *out_scales, float *out_rotations,
                        float *out_opacity, float *out_shs, void *stream);
 
+/* Parameter gradients of the field, torch layouts (planes [C, H, W] as the planes themselves). */
+typedef struct lsr_deform_grads {
+    float *planes[LSR_DEFORM_MAX_SCALES][6];
+    float *w_feat, *b_feat;
+    float *w1[LSR_DEFORM_HEADS], *b1[LSR_DEFORM_HEADS];
+    float *w2[LSR_DEFORM_HEADS], *b2[LSR_DEFORM_HEADS];
+} lsr_deform_grads;
+
+/* Scratch of lsr_deform_backward for P Gaussians (saved activations: 6272 bytes per Gaussian). */
+int64_t lsr_deform_backward_scratch_bytes(const lsr_deform_net *net, int32_t P);
+
+/* Backward of lsr_deform_forward (what autograd does through deform_network.forward_dynamic and
+ * HexPlaneField, scene/deformation.py:103-182, scene/hexplane.py:21-106), given the gradients of
+ * its five outputs d_out_* (same shapes as the outputs):
+ *   d_means3D = d_out_means3D + the gradient through the HexPlane sample coordinates (overwritten);
+ *   the scales / rotations / opacity / SH input gradients equal d_out_* (identity residuals), so
+ *   they are not written here;
+ *   every parameter gradient in `grads` is ACCUMULATED (+=), as torch accumulates .grad.
+ * `workspace` is the prepared forward workspace (its packing must match the current parameters).
+ * Float atomics (plane scatter, weight-gradient partials): not bitwise reproducible. */
+int lsr_deform_backward(const lsr_deform_net *net, const void *workspace, int32_t P, const float *means3D,
+                        const float *time, const float *d_out_means3D, const float *d_out_scales,
+                        const float *d_out_rotations, const float *d_out_opacity, const float *d_out_shs,
+                        float *d_means3D, const lsr_deform_grads *grads, void *scratch, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

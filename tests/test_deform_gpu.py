@@ -78,3 +78,80 @@ def test_forward_matches_oracle_at_neu3d_resolution(P, time):
     # product) and fp32 sampling: held to 1e-4 of each output's range, the north-star RGB bar
     for k in KEYS:
         assert _rel(out[k] - inp[k], ref[k] - inp[k]) < 1e-4, k
+
+
+# ---- backward (lsr_deform_backward) --------------------------------------------------------------
+def test_backward_matches_reference_golden():
+    """Input and parameter gradients against the reference module's autograd (float64 golden)."""
+    z = np.load(os.path.join(ROOT, "tests", "golden", "deform_golden.npz"))
+    params = {k[len("param/"):]: z[k] for k in z.files if k.startswith("param/")}
+    params["grid.aabb"] = z["aabb"]
+    f = _field(params, list(z["res"]), list(z["multires"]))
+    t = lambda a: torch.tensor(np.asarray(a, np.float32)).cuda()   # noqa: E731
+    f.zero_grad()
+    got = f.backward(t(z["means3D"]), t(z["time"][:, 0]), t(z["up_means3D"]), t(z["up_scales"]),
+                     t(z["up_rotations"]), t(z["up_opacity"]), t(z["up_shs"]))
+    torch.cuda.synchronize()
+    for k, g in zip(KEYS, got):
+        assert _rel(g.cpu().numpy().reshape(z["grad_" + k].shape), z["grad_" + k]) < 1e-4, k
+    for name, g in f.grads.items():
+        ref = z["grad/" + name]
+        assert _rel(g.cpu().numpy().reshape(ref.shape), ref) < 1e-4, name
+
+
+@pytest.mark.parametrize("P,time", [(20000, 0.37), (777, -0.8)])
+def test_backward_matches_oracle_at_neu3d_resolution(P, time):
+    """Neu3D resolution (64^3 x 150, multires [1, 2]); gradients accumulate over two calls."""
+    params, res, multires, inp = _neu3d_case(P, seed=3)
+    # the bilinear slope jumps at grid lines: keep the points 1e-3 cells away from every line (and
+    # from the clamped borders), where float32 and float64 coordinates could pick different cells
+    a0, a1 = params["grid.aabb"][0], params["grid.aabb"][1]
+    crd = (inp["means3D"] - a0) * (2.0 / (a1 - a0)) - 1.0
+    keep = np.ones(P, bool)
+    for m in multires:
+        for c in range(3):
+            u = (crd[:, c] + 1.0) * 0.5 * (res[c] * m - 1)
+            keep &= np.abs(u - np.round(u)) > 1e-3
+    inp = {k: v[keep] for k, v in inp.items()}
+    P = int(keep.sum())
+    f = _field(params, res, multires)
+    rng = np.random.default_rng(5)
+    ups = dict(means3D=rng.normal(size=(P, 3)), scales=rng.normal(size=(P, 3)), rotations=rng.normal(size=(P, 4)),
+               opacity=rng.normal(size=(P, 1)), shs=rng.normal(size=(P, 16, 3)) * 0.1)
+    o = DeformOracle({k: v for k, v in params.items() if k != "grid.aabb"}, params["grid.aabb"])
+    o.forward(inp["means3D"], inp["scales"], inp["rotations"], inp["opacity"], inp["shs"], None, np.full((P, 1), time))
+    # A ReLU input within the kernel's error (~1e-5) of 0 may fall on the other side than in float64
+    # and legitimately change that Gaussian's gradients: such Gaussians (|pre-activation| < 1e-4 in
+    # the oracle) get zero upstream gradients in both runs, which removes their every contribution.
+    _, _, h, _, cache, _ = o._cache
+    amb = (np.abs(h) < 1e-4).any(axis=1)
+    for z, _ in cache.values():
+        amb |= (np.abs(z) < 1e-4).any(axis=1)
+    assert amb.mean() < 0.3               # 768 pre-activations per Gaussian: ~17% have one that close
+    for k in KEYS:
+        ups[k][amb] = 0.0
+    g_in, g_p = o.backward(*[np.asarray(ups[k], np.float32).astype(np.float64) for k in KEYS])
+    t = lambda a: torch.tensor(np.asarray(a, np.float32)).cuda()   # noqa: E731
+    f.zero_grad()
+    for _ in range(2):
+        got = f.backward(t(inp["means3D"]), time, *[t(ups[k]) for k in KEYS])
+    torch.cuda.synchronize()
+    # bf16 hi/lo MFMA products (~2^-17 relative) and fp32 atomics: 1e-4 of each tensor's range
+    assert _rel(got[0].cpu().numpy(), g_in["means3D"]) < 1e-4
+    for name, g in f.grads.items():
+        assert _rel(g.cpu().numpy() / 2.0, g_p[name].reshape(g.shape)) < 1e-4, name
+
+
+def test_apply_autograd_path():
+    """apply(): outputs match forward(), and torch autograd reaches the inputs through the kernel."""
+    params, res, multires, inp = _neu3d_case(500, seed=4)
+    f = _field(params, res, multires)
+    xs = [torch.tensor(np.asarray(inp[k], np.float32)).cuda().requires_grad_(True) for k in KEYS]
+    outs = f.apply(*xs, None, 0.25)
+    ref = f.forward(*[x.detach() for x in xs], None, 0.25)
+    for a, b in zip(outs[:5], ref[:5]):
+        assert torch.equal(a.detach(), b)
+    f.zero_grad()
+    (outs[0].sum() + 2.0 * outs[4].sum()).backward()
+    assert torch.equal(xs[4].grad, torch.full_like(xs[4], 2.0)) and torch.equal(xs[1].grad, torch.zeros_like(xs[1]))
+    assert xs[0].grad.abs().sum() > 0 and f.grads["pos_deform.3.bias"][0].item() == pytest.approx(500.0)

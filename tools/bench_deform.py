@@ -64,6 +64,27 @@ def main():
                                         peak=BF16_DENSE_PEAK_TFLOPS / 3, note="useful fp32-equivalent flops vs "
                                         "dense bf16 peak / 3 (hi/lo split: 3 MFMAs per product)",
                                         frac=round(useful_tflops / (BF16_DENSE_PEAK_TFLOPS / 3), 4)))))
+    # backward: upstream gradients of the five outputs; input + parameter gradients
+    ups = [torch.randn(P, 3, generator=g).to(dev), torch.randn(P, 3, generator=g).to(dev),
+           torch.randn(P, 4, generator=g).to(dev), torch.randn(P, 1, generator=g).to(dev),
+           torch.randn(P, 16, 3, generator=g).to(dev)]
+    field.zero_grad()
+    for _ in range(2):
+        field.backward(means, 0.4, *ups)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(args.iters // 2):
+        field.backward(means, 0.4, *ups)
+    e1.record()
+    torch.cuda.synchronize()
+    bms = e0.elapsed_time(e1) / (args.iters // 2)
+    # recompute of the forward MLP + data gradients (2 products per weight) + weight gradients (1)
+    bflops = 2.0 * macs * 4 * P
+    saved = P * (32 + 128 + 128 + 5 * 128 + 5 * 128) * 4          # activations written then read
+    print(json.dumps(dict(metric="deformation backward Gaussians/s (Neu3D structure)", value=round(P / (bms * 1e-3)),
+                          unit="Gaussians/s", ms_per_call=round(bms, 4), gaussians=P,
+                          mlp_tflops=round(bflops / (bms * 1e-3) / 1e12, 1),
+                          saved_activation_gb=round(saved / 1e9, 2))))
 
 
 if __name__ == "__main__":
