@@ -210,6 +210,9 @@ __global__ void __launch_bounds__(256) k_deform_bwd_a(DeformBwdArgs b) {
     __shared__ __attribute__((aligned(16))) __bf16 s_gh[DN * DGP];
     __shared__ __attribute__((aligned(16))) __bf16 s_gl[DN * DGP];
     __shared__ float s_dx[DN][DFEAT + 1];
+    __shared__ float s_sdv[4][16][17];   // plane scatter staging, per wave: dv of 16 Gaussians
+    __shared__ int s_soff[4][16][4];     //   their 4 tap offsets
+    __shared__ float s_sw[4][16][4];     //   and bilinear weights
     const DeformArgs& a = b.f;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int g0 = blockIdx.x * DN;
@@ -409,18 +412,29 @@ __global__ void __launch_bounds__(256) k_deform_bwd_a(DeformBwdArgs b) {
                 const float4 t00 = pl[(y0 * W + x0) * 4], t01 = pl[(y0 * W + x1) * 4];
                 const float4 t10 = pl[(y1 * W + x0) * 4], t11 = pl[(y1 * W + x1) * 4];
                 const float w00 = (1.0f - fx) * (1.0f - fy), w01 = fx * (1.0f - fy), w10 = (1.0f - fx) * fy, w11 = fx * fy;
-                if (ok) {
-                    float* gp = b.dplanes + a.poff[pi] + 4 * q;
-                    const size_t o00 = (size_t)(y0 * W + x0) * 16, o01 = (size_t)(y0 * W + x1) * 16;
-                    const size_t o10 = (size_t)(y1 * W + x0) * 16, o11 = (size_t)(y1 * W + x1) * 16;
+                // scatter: stage the wave's 16 Gaussians (16 channels, 4 taps each) in LDS, then one
+                // atomic instruction per Gaussian covers its 4 taps x 16 channels = four full
+                // 64-byte segments (lane = 16 tap + channel) instead of 16 partial ones; blocks add
+                // into one of b.replicas copies of the gradient planes (summed by the unpack), so
+                // the few cells every Gaussian of a frame shares (the time planes) are not one hot spot
+                {
+                    const int wl = gl & 15;
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        if (dv[i] == 0.0f) continue;
-                        atomicAdd(gp + o00 + i, dv[i] * w00);
-                        if (w01 != 0.0f) atomicAdd(gp + o01 + i, dv[i] * w01);
-                        if (w10 != 0.0f) atomicAdd(gp + o10 + i, dv[i] * w10);
-                        if (w11 != 0.0f) atomicAdd(gp + o11 + i, dv[i] * w11);
+                    for (int i = 0; i < 4; ++i) s_sdv[wave][wl][4 * q + i] = ok ? dv[i] : 0.0f;
+                    if (q == 0) {
+                        s_soff[wave][wl][0] = (y0 * W + x0) * 16; s_soff[wave][wl][1] = (y0 * W + x1) * 16;
+                        s_soff[wave][wl][2] = (y1 * W + x0) * 16; s_soff[wave][wl][3] = (y1 * W + x1) * 16;
+                        s_sw[wave][wl][0] = w00; s_sw[wave][wl][1] = w01; s_sw[wave][wl][2] = w10; s_sw[wave][wl][3] = w11;
                     }
+                    wave_lds_sync();
+                    float* gp = b.dplanes + (size_t)(blockIdx.x % b.replicas) * b.plane_stride + a.poff[pi];
+                    const int tap = lane >> 4, ch = lane & 15;
+#pragma unroll 4
+                    for (int j = 0; j < 16; ++j) {
+                        const float v = s_sdv[wave][j][ch] * s_sw[wave][j][tap];
+                        if (v != 0.0f) atomicAdd(gp + s_soff[wave][j][tap] + ch, v);
+                    }
+                    wave_lds_sync();   // staging read before the next plane rewrites it
                 }
                 const float a00[4] = {t00.x, t00.y, t00.z, t00.w}, a01[4] = {t01.x, t01.y, t01.z, t01.w};
                 const float a10[4] = {t10.x, t10.y, t10.z, t10.w}, a11[4] = {t11.x, t11.y, t11.z, t11.w};
@@ -454,66 +468,65 @@ void launch_deform_bwd_a(const DeformBwdArgs& a, hipStream_t st) {
 }
 
 // Phase B: C[M][N] += sum_g L[g][m] R[g][n] (M, N <= 128), bias[m] += sum_g L[g][m]; split-K over
-// blocks of rows_per_block rows (blockIdx.x), one job per blockIdx.y.  Per 64-row chunk both
-// operands go to LDS transposed ([m][g], [n][g]) as bf16 hi/lo, the 32x32 output tiles are spread
-// over the 4 waves, and each block adds its partial to C with one atomic per element.
-constexpr int ATB_K = 64, ATB_P = ATB_K + 8;
+// blocks of rows_per_block rows (blockIdx.x), one job per blockIdx.y.  The reduction index g is the
+// MFMA's K, so both fragments come straight from the row-major operands: lane (r, h) loads
+// L[g0 + 8h + j][32 mt + r] for j < 8 (each load instruction reads 2 x 128 contiguous bytes) and
+// splits it into bf16 hi / lo in registers; no LDS.  A wave owns a strip of 32x32 output tiles (one
+// M tile and every N tile when M = 128, else one N tile and every M tile), accumulates it over the
+// block's rows and adds it to C with one atomic per element.
+__device__ __forceinline__ void atb_frag(const float* __restrict__ src, int ld, int col, int64_t g, int64_t row1,
+                                         dbf16x8& h8, dbf16x8& l8, float& sum) {
+    float v[8];
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) v[jj] = (g + jj < row1 && col < ld) ? src[(g + jj) * ld + col] : 0.0f;
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+        __bf16 hi, lo;
+        dsplit(v[jj], hi, lo);
+        h8[jj] = hi;
+        l8[jj] = lo;
+        sum += v[jj];
+    }
+}
 
-__global__ void __launch_bounds__(256) k_atb(AtbArgs ga) {
-    __shared__ __attribute__((aligned(16))) __bf16 s_lh[128 * ATB_P];
-    __shared__ __attribute__((aligned(16))) __bf16 s_ll[128 * ATB_P];
-    __shared__ __attribute__((aligned(16))) __bf16 s_rh[128 * ATB_P];
-    __shared__ __attribute__((aligned(16))) __bf16 s_rl[128 * ATB_P];
-    const AtbJob& j = ga.job[blockIdx.y];
+template <bool STRIP_M>   // STRIP_M: wave w owns M tile w and all N tiles (M = 128)
+__device__ __forceinline__ void atb_body(const AtbJob& j, int64_t row0, int64_t row1) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
-    const int M = j.M, N = j.N, Mt = (M + 31) / 32, Nt = (N + 31) / 32, ntile = Mt * Nt;
-    const int64_t row0 = (int64_t)blockIdx.x * ga.rows_per_block;
-    const int64_t row1 = min((int64_t)ga.P, row0 + ga.rows_per_block);
-    if (row0 >= row1) return;
+    const int M = j.M, N = j.N, Mt = (M + 31) / 32, Nt = (N + 31) / 32;
+    const int ntile = STRIP_M ? Nt : (wave < Nt ? Mt : 0);
+    if (ntile == 0) return;
     df32x16 acc[4] = {df32x16{}, df32x16{}, df32x16{}, df32x16{}};
-    float bsum = 0.0f;
-    for (int64_t k0 = row0; k0 < row1; k0 += ATB_K) {
-        // stage: element (g, m) of L -> s_l[m][g]; rows past row1 and columns past M are zero
-        for (int i = tid; i < ATB_K * 128; i += 256) {
-            const int gi = i >> 7, m = i & 127;
-            const int64_t g = k0 + gi;
-            const bool in = g < row1;
-            const float lv = (in && m < M) ? j.L[g * M + m] : 0.0f;
-            const float rv = (in && m < N) ? j.R[g * N + m] : 0.0f;
-            __bf16 h, l;
-            dsplit(lv, h, l);
-            s_lh[m * ATB_P + gi] = h;
-            s_ll[m * ATB_P + gi] = l;
-            dsplit(rv, h, l);
-            s_rh[m * ATB_P + gi] = h;
-            s_rl[m * ATB_P + gi] = l;
-            if (j.bias && m < M) bsum += lv;   // thread tid always owns column m = tid & 127
+    float bsum = 0.0f, dummy = 0.0f;
+    for (int64_t k0 = row0; k0 < row1; k0 += 16) {
+        const int64_t g = k0 + 8 * hh;
+        dbf16x8 ah[4], al[4], bh[4], bl[4];
+        if (STRIP_M) {
+            atb_frag(j.L, M, 32 * wave + r, g, row1, ah[0], al[0], bsum);
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                if (t < ntile) atb_frag(j.R, N, 32 * t + r, g, row1, bh[t], bl[t], dummy);
+        } else {
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                if (t < ntile) atb_frag(j.L, M, 32 * t + r, g, row1, ah[t], al[t], t == wave ? bsum : dummy);
+            atb_frag(j.R, N, 32 * wave + r, g, row1, bh[0], bl[0], dummy);
         }
-        __syncthreads();
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-            const int tile = wave + 4 * t;
-            if (tile >= ntile) break;
-            const int mt = tile / Nt, nt = tile - mt * Nt;
-#pragma unroll
-            for (int ks = 0; ks < ATB_K / 16; ++ks) {
-                const int kk = 16 * ks + 8 * hh;
-                const dbf16x8 ah = *reinterpret_cast<const dbf16x8*>(s_lh + (32 * mt + r) * ATB_P + kk);
-                const dbf16x8 al = *reinterpret_cast<const dbf16x8*>(s_ll + (32 * mt + r) * ATB_P + kk);
-                const dbf16x8 bh = *reinterpret_cast<const dbf16x8*>(s_rh + (32 * nt + r) * ATB_P + kk);
-                const dbf16x8 bl = *reinterpret_cast<const dbf16x8*>(s_rl + (32 * nt + r) * ATB_P + kk);
-                acc[t] = DMFMA(ah, bh, acc[t]);
-                acc[t] = DMFMA(ah, bl, acc[t]);
-                acc[t] = DMFMA(al, bh, acc[t]);
-            }
+            if (t >= ntile) break;
+            const dbf16x8& xh = STRIP_M ? ah[0] : ah[t];
+            const dbf16x8& xl = STRIP_M ? al[0] : al[t];
+            const dbf16x8& yh = STRIP_M ? bh[t] : bh[0];
+            const dbf16x8& yl = STRIP_M ? bl[t] : bl[0];
+            acc[t] = DMFMA(xh, yh, acc[t]);
+            acc[t] = DMFMA(xh, yl, acc[t]);
+            acc[t] = DMFMA(xl, yh, acc[t]);
         }
-        __syncthreads();
     }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-        const int tile = wave + 4 * t;
-        if (tile >= ntile) break;
-        const int mt = tile / Nt, nt = tile - mt * Nt;
+        if (t >= ntile) break;
+        const int mt = STRIP_M ? wave : t, nt = STRIP_M ? t : wave;
         const int n = 32 * nt + r;
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
@@ -521,13 +534,22 @@ __global__ void __launch_bounds__(256) k_atb(AtbArgs ga) {
             if (m < M && n < N) atomicAdd(j.C + (size_t)m * N + n, acc[t][q]);
         }
     }
-    // bias partials: threads tid and tid + 128 own the same column
+    // bias: lanes r and r + 32 hold the two row halves of column 32 mt + r (mt = this wave's M tile)
     if (j.bias) {
-        __shared__ float s_b[256];
-        s_b[tid] = bsum;
-        __syncthreads();
-        if (tid < M) atomicAdd(j.bias + tid, s_b[tid] + s_b[tid + 128]);
+        const float tot = bsum + __shfl_xor(bsum, 32);
+        const int m = 32 * wave + r;
+        if (hh == 0 && m < M && (STRIP_M || wave < Mt)) atomicAdd(j.bias + m, tot);
     }
+    (void)dummy;
+}
+
+__global__ void __launch_bounds__(256) k_atb(AtbArgs ga) {
+    const AtbJob& j = ga.job[blockIdx.y];
+    const int64_t row0 = (int64_t)blockIdx.x * ga.rows_per_block;
+    const int64_t row1 = min((int64_t)ga.P, row0 + ga.rows_per_block);
+    if (row0 >= row1) return;
+    if (j.M > 96) atb_body<true>(j, row0, row1);
+    else atb_body<false>(j, row0, row1);
 }
 
 void launch_atb(const AtbArgs& a, int njobs, hipStream_t st) {
@@ -537,15 +559,20 @@ void launch_atb(const AtbArgs& a, int njobs, hipStream_t st) {
 }
 
 // packed channel-last gradient [H][W][16] -> torch [16][H][W], added
-__global__ void k_unpack_plane_grad(const float* __restrict__ src, float* __restrict__ dst, int H, int W) {
+__global__ void k_unpack_plane_grad(const float* __restrict__ src, float* __restrict__ dst, int H, int W, int replicas,
+                                    int64_t stride) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;   // over 16 * H * W destination floats
     if (i >= H * W * 16) return;
     const int hw = i % (H * W), c = i / (H * W);
-    dst[i] += src[(size_t)hw * 16 + c];
+    float s = 0.0f;
+    for (int r = 0; r < replicas; ++r) s += src[(size_t)r * stride + (size_t)hw * 16 + c];
+    dst[i] += s;
 }
 
-void launch_unpack_plane_grad(const float* src, float* dst, int H, int W, hipStream_t st) {
-    hipLaunchKernelGGL(k_unpack_plane_grad, dim3((H * W * 16 + 255) / 256), dim3(256), 0, st, src, dst, H, W);
+void launch_unpack_plane_grad(const float* src, float* dst, int H, int W, int replicas, int64_t stride,
+                              hipStream_t st) {
+    hipLaunchKernelGGL(k_unpack_plane_grad, dim3((H * W * 16 + 255) / 256), dim3(256), 0, st, src, dst, H, W,
+                       replicas, stride);
 }
 
 // ---- parameter packing ----------------------------------------------------------------------------

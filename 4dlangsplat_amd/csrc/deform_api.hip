@@ -155,7 +155,8 @@ lsr::DeformArgs forward_args(const lsr_deform_net* net, const void* workspace, i
     return a;
 }
 
-// backward scratch: saved activations, then the packed gradient planes
+// backward scratch: saved activations, then kGradReplicas copies of the packed gradient planes
+constexpr int kGradReplicas = 16;
 struct BwdScratch {
     size_t X, A0, dH0, A1, dZ1, dplanes, total;
 };
@@ -168,7 +169,7 @@ BwdScratch bwd_scratch(const lsr_deform_net* net, size_t P) {
     s.dH0 = o; o += align256(P * 128 * f);
     s.A1 = o; o += align256(5 * P * 128 * f);
     s.dZ1 = o; o += align256(5 * P * 128 * f);
-    s.dplanes = o; o += layout(net).planes_end;
+    s.dplanes = o; o += kGradReplicas * layout(net).planes_end;
     s.total = o;
     return s;
 }
@@ -244,7 +245,9 @@ extern "C" int lsr_deform_backward(const lsr_deform_net* net, const void* worksp
     b.sdH0 = reinterpret_cast<float*>(sc + S.dH0);
     b.sA1 = reinterpret_cast<float*>(sc + S.A1);
     b.sdZ1 = reinterpret_cast<float*>(sc + S.dZ1);
-    if (hipMemsetAsync(b.dplanes, 0, L.planes_end, st) != hipSuccess) return lsr::fail(LSR_EHIP, "memset");
+    b.replicas = kGradReplicas;
+    b.plane_stride = (int64_t)(L.planes_end / sizeof(float));
+    if (hipMemsetAsync(b.dplanes, 0, kGradReplicas * L.planes_end, st) != hipSuccess) return lsr::fail(LSR_EHIP, "memset");
     lsr::launch_deform_bwd_a(b, st);
     // weight gradients: 5 x (dW1, dW2) + feature_out, split-K over ~256 row blocks
     lsr::AtbArgs g{};
@@ -263,7 +266,7 @@ extern "C" int lsr_deform_backward(const lsr_deform_net* net, const void* worksp
             int W, H;
             plane_dims(net, s, ci, W, H);
             lsr::launch_unpack_plane_grad(reinterpret_cast<const float*>(sc + S.dplanes + L.plane_off[6 * s + ci]),
-                                          grads->planes[s][ci], H, W, st);
+                                          grads->planes[s][ci], H, W, b.replicas, b.plane_stride, st);
         }
     if (hipGetLastError() != hipSuccess) return lsr::fail(LSR_EHIP, "deformation backward launch failed");
     return LSR_OK;

@@ -201,7 +201,9 @@ struct DeformBwdArgs {
     const __bf16 *wft_h, *wft_l;      // [32 feat][128 hidden]
     const float* up[5];               // gradients of the five outputs
     float* d_means3D;
-    float* dplanes;                   // packed channel-last gradient planes (same offsets as f.planes)
+    float* dplanes;                   // packed channel-last gradient planes (same offsets as f.planes),
+    int64_t plane_stride;             //   `replicas` copies plane_stride floats apart (block b adds
+    int replicas;                     //   into copy b % replicas; the unpack sums them)
     float *sX, *sA0, *sdH0, *sA1, *sdZ1;   // saved: [P,32], [P,128], [P,128], [5][P,128], [5][P,128]
 };
 void launch_deform_bwd_a(const DeformBwdArgs& a, hipStream_t st);
@@ -219,7 +221,8 @@ struct AtbArgs {
     int rows_per_block;
 };
 void launch_atb(const AtbArgs& a, int njobs, hipStream_t st);
-void launch_unpack_plane_grad(const float* src, float* dst, int H, int W, hipStream_t st);
+void launch_unpack_plane_grad(const float* src, float* dst, int H, int W, int replicas, int64_t stride,
+                              hipStream_t st);
 
 void launch_preprocess(const PreprocessArgs& a, hipStream_t st);
 void launch_preprocess_bwd(const PreprocessBwdArgs& a, bool accumulate, hipStream_t st);
