@@ -36,8 +36,9 @@ def phase_bytes(phase, P, Pvis, K, npix, ntiles, C, M=16, accumulate=True, V=1, 
     preprocess_bwd_views covers V views: Pvis_sum = visible Gaussians summed over them, Pany =
     Gaussians visible in at least one."""
     rec = 4 + 8 + 16 + 16 + 4 * C          # id + xy + conic/opacity + rgb/depth + language row
-    if phase == "preprocess":              # inputs; radii, radius, tiles, key, rect; screen records
-        return P * (12 + 12 + 16 + 4 + 4 * 3 * M) + P * (4 + 4 + 4 + 4 + 8) + Pvis * (8 + 16 + 16 + 1)
+    if phase == "preprocess":              # inputs; radii, radius, tiles, key, rect, sort ids; screen
+        return (P * (12 + 12 + 16 + 4 + 4 * 3 * M) + P * (4 + 4 + 4 + 4 + 8 + 4)   # records; zeroed
+                + Pvis * (8 + 16 + 16 + 1 + 64))                                   # accumulator rows
     if phase == "depth_sort":
         return 4 * P * (4 + 16) + 4 * P     # 4 passes: count reads keys, scatter reads + writes pairs
     if phase == "instance_scan":           # order + rect gather -> counts + depth-ordered rect; scan
