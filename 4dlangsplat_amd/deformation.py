@@ -58,6 +58,31 @@ class DeformationField:
         self.workspace = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
         self.prepare()
 
+    @staticmethod
+    def init_params(resolution: Sequence[int], multires: Sequence[int], aabb, channels: int = 16, width: int = 128,
+                    seed: int = 0) -> Dict[str, torch.Tensor]:
+        """A freshly initialised field, as the reference builds one (CPU tensors): spatial planes
+        U(0.1, 0.5) and time planes ones (scene/hexplane.py:48-70), Linear weights Xavier-uniform
+        (scene/deformation.py:254-260) and biases torch's default U(+-1/sqrt(fan_in)).
+        aabb: [[x, y, z]_max, [x, y, z]_min]."""
+        g = torch.Generator().manual_seed(seed)
+        p = {"grid.aabb": torch.as_tensor(aabb, dtype=torch.float32)}
+        for s, m in enumerate(multires):
+            reso = [r * m for r in resolution[:3]] + [resolution[3]]
+            for ci, (c0, c1) in enumerate([(0, 1), (0, 2), (0, 3), (1, 2), (1, 3), (2, 3)]):
+                shape = (1, channels, reso[c1], reso[c0])
+                p[f"grid.grids.{s}.{ci}"] = torch.ones(shape) if c1 == 3 else torch.rand(shape, generator=g) * 0.4 + 0.1
+
+        def linear(name, n_out, n_in):
+            bound = (6.0 / (n_in + n_out)) ** 0.5
+            p[name + ".weight"] = (torch.rand(n_out, n_in, generator=g) * 2 - 1) * bound
+            p[name + ".bias"] = (torch.rand(n_out, generator=g) * 2 - 1) / n_in ** 0.5
+        linear("feature_out.0", width, channels * len(multires))
+        for name, n in zip(HEADS, HEAD_OUT):
+            linear(name + ".1", width, width)
+            linear(name + ".3", n, width)
+        return p
+
     @classmethod
     def from_reference_state_dict(cls, state_dict, resolution, multires, prefix="deformation_net.", device="cuda"):
         """Load `deform_network.state_dict()` (or a Deformation state dict with prefix="")."""

@@ -236,7 +236,10 @@ def render(viewpoint_camera, pc: GaussianScene, bg_color: torch.Tensor, scaling_
             raise ValueError("a 'fine' stage needs the scene's deformation field")
         if cov3D_precomp is not None:
             raise ValueError("compute_cov3D_python with a deformation field is not supported")
-        m3, s3, r3, o3, sh3, l3, coff = pc.deformation(means3D, scales, rotations, opacity, shs, lang, t)
+        # inside autograd (training) the field's backward runs (DeformationField.apply)
+        deform = pc.deformation.apply if (torch.is_grad_enabled() and hasattr(pc.deformation, "apply")) \
+            else pc.deformation
+        m3, s3, r3, o3, sh3, l3, coff = deform(means3D, scales, rotations, opacity, shs, lang, t)
     else:
         raise NotImplementedError(stage)
     s3 = torch.exp(s3) if s3 is not None else None

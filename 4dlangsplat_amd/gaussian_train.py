@@ -270,3 +270,39 @@ class GaussianTrainer:
 
     def state_rows(self) -> Iterable[str]:
         return tuple(self.params)
+
+
+class TensorAdam:
+    """torch.optim.Adam over named tensors whose gradients arrive in a separate dict (the
+    deformation field's planes and MLP weights, DeformationField.grads; gaussian_model.py:250-253,
+    275-276 give them their own groups): lsr_adam_step, up to 16 tensors per launch."""
+
+    def __init__(self, params: Dict[str, torch.Tensor], lr, betas=(0.9, 0.999), eps: float = 1e-15):
+        self._L = _lib.load()
+        self.params = params
+        self.lr = lr if isinstance(lr, dict) else {n: float(lr) for n in params}
+        self.betas, self.eps = betas, eps
+        self.exp_avg = {n: torch.zeros_like(t) for n, t in params.items()}
+        self.exp_avg_sq = {n: torch.zeros_like(t) for n, t in params.items()}
+        self.steps = {n: 0 for n in params}
+
+    def step(self, grads: Dict[str, torch.Tensor]):
+        groups = []
+        for n, p in self.params.items():
+            g = grads.get(n)
+            if g is None or n not in self.lr:
+                continue
+            if g.shape != p.shape or not g.is_contiguous() or not p.is_contiguous():
+                raise ValueError(f"{n}: gradient and parameter must be contiguous and of one shape")
+            self.steps[n] += 1
+            ag = _lib.AdamGroup()
+            ag.param, ag.grad = p.data_ptr(), g.data_ptr()
+            ag.exp_avg, ag.exp_avg_sq = self.exp_avg[n].data_ptr(), self.exp_avg_sq[n].data_ptr()
+            ag.n, ag.lr, ag.step = p.numel(), float(self.lr[n]), self.steps[n]
+            groups.append(ag)
+        dev = next(iter(self.params.values())).device
+        for i in range(0, len(groups), _lib.ADAM_MAX_GROUPS):
+            chunk = groups[i:i + _lib.ADAM_MAX_GROUPS]
+            arr = (_lib.AdamGroup * len(chunk))(*chunk)
+            _lib.check(self._L.lsr_adam_step(arr, len(chunk), self.betas[0], self.betas[1], self.eps, _stream(dev)),
+                       "lsr_adam_step")

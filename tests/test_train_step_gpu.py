@@ -1,0 +1,65 @@
+"""The config-5 loop end to end on the GPU (train_step.TrainStep): deformation field (autograd
+through lsr_deform_backward) -> rasterizer for 2 views -> L1 -> backward -> densification
+statistics -> Adam on the Gaussians (lsr_adam_step) and on the field (TensorAdam), densify and
+prune between iterations.  No oracle: the check is that the pieces compose (shapes, gradient
+flow, every parameter moves) and that the loss falls when fitting renders of a teacher scene."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import synthetic
+from deformation import DeformationField
+from gaussian_scene import render
+from gaussian_train import GaussianTrainer
+from train_step import TrainStep
+
+pytestmark = pytest.mark.gpu
+AABB = [[7.0, 5.5, 10.5], [-7.0, -5.5, 1.5]]
+RES, MULTIRES = [16, 16, 16, 10], [1, 2]
+LRS = {"xyz": 1.6e-4, "f_dc": 2.5e-2, "f_rest": 2.5e-2 / 20, "opacity": 0.05, "scaling": 5e-3, "rotation": 1e-3}
+
+
+def _raw(sc, P):
+    shs = sc.shs
+    return {"xyz": sc.means3D.contiguous(), "f_dc": shs[:, :1].contiguous(), "f_rest": shs[:, 1:].contiguous(),
+            "opacity": torch.logit(sc.opacities.reshape(P, 1)).contiguous(),
+            "scaling": torch.log(sc.scales).contiguous(), "rotation": sc.rotations.contiguous()}
+
+
+def test_train_loop_fits_teacher():
+    P, W, H = 4000, 160, 120
+    dev = torch.device("cuda")
+    sc = synthetic.make_scene(P, C=3, tanfovx=0.6, tanfovy=0.6 * H / W, seed=3, logscale_mean=-3.0).to(dev)
+    cams = synthetic.camera_batch(2, W, H, tanfovx=0.6, seed=2)
+    field_p = DeformationField.init_params(RES, MULTIRES, AABB, seed=1)
+    teacher_field = DeformationField({k: v.to(dev) for k, v in field_p.items()}, RES, MULTIRES)
+    teacher = GaussianTrainer(_raw(sc, P), LRS)
+    with torch.no_grad():
+        tscene = TrainStep(teacher, teacher_field).scene()
+        gts = torch.stack([render(c, tscene, torch.ones(3, device=dev), stage="fine-base")["render"] for c in cams])
+    # student: the same geometry and field, colours perturbed
+    raw = _raw(sc, P)
+    g = torch.Generator(device="cpu").manual_seed(9)
+    raw["f_dc"] = raw["f_dc"] + (torch.randn(P, 1, 3, generator=g) * 0.5).to(dev)
+    field = DeformationField({k: v.to(dev) for k, v in field_p.items()}, RES, MULTIRES)
+    tr = GaussianTrainer(raw, LRS)
+    step = TrainStep(tr, field)
+    plane0 = field.p["grid.grids.1.3"].clone()
+    w0 = field.p["pos_deform.3.weight"].clone()
+    losses = []
+    for it in range(16):
+        losses.append(float(step(cams, gts)))
+        if it == 7:   # the densification / pruning passes between iterations (train.py:388-414)
+            n_clone, n_split = tr.densify(1e-9, 0.005, 8.0)
+            assert tr.P == P + n_clone + n_split and n_clone + n_split > 0
+            tr.prune(1e-9, 0.0, 8.0, None)
+    torch.cuda.synchronize()
+    assert all(math.isfinite(x) for x in losses), losses
+    # the loss falls while fitting; the densify at iteration 7 (every visible Gaussian cloned or split
+    # at this threshold) perturbs the fit, after which it falls again
+    assert losses[7] < 0.8 * losses[0] and losses[15] < losses[8], losses
+    assert tr.steps["f_dc"] == 16 and not torch.equal(field.p["pos_deform.3.weight"], w0)
+    assert not torch.equal(field.p["grid.grids.1.3"], plane0)
+    assert tr.denom.shape[0] == tr.P and np.isfinite(tr.xyz_gradient_accum.cpu().numpy()).all()
