@@ -35,6 +35,29 @@ __device__ __forceinline__ float expf_repro(float x) {
     return p * __uint_as_float((uint32_t)(k + 127) << 23);
 }
 
+// expf_repro of two values at once: the same correctly rounded operations per component, the
+// multiplies and fmas on the packed fp32 pipe (v_pk_mul_f32 / v_pk_fma_f32: two results per
+// instruction), so each component is bit-identical to expf_repro.
+typedef float lsr_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ lsr_f2 expf_repro2(lsr_f2 x) {
+    const lsr_f2 t = x * lsr_f2{1.44269504088896341f, 1.44269504088896341f};
+    const lsr_f2 kf = {__builtin_rintf(t.x), __builtin_rintf(t.y)};
+    lsr_f2 r = __builtin_elementwise_fma(kf, lsr_f2{-0.693145751953125f, -0.693145751953125f}, x);
+    r = __builtin_elementwise_fma(kf, lsr_f2{-1.428606765330187045e-06f, -1.428606765330187045e-06f}, r);
+    lsr_f2 p = {1.98412698412698413e-04f, 1.98412698412698413e-04f};
+    p = __builtin_elementwise_fma(p, r, lsr_f2{1.38888888888888889e-03f, 1.38888888888888889e-03f});
+    p = __builtin_elementwise_fma(p, r, lsr_f2{8.33333333333333333e-03f, 8.33333333333333333e-03f});
+    p = __builtin_elementwise_fma(p, r, lsr_f2{4.16666666666666667e-02f, 4.16666666666666667e-02f});
+    p = __builtin_elementwise_fma(p, r, lsr_f2{1.66666666666666667e-01f, 1.66666666666666667e-01f});
+    p = __builtin_elementwise_fma(p, r, lsr_f2{0.5f, 0.5f});
+    p = __builtin_elementwise_fma(p, r, lsr_f2{1.0f, 1.0f});
+    p = __builtin_elementwise_fma(p, r, lsr_f2{1.0f, 1.0f});
+    const lsr_f2 sc = {__uint_as_float((uint32_t)((int)kf.x + 127) << 23),
+                       __uint_as_float((uint32_t)((int)kf.y + 127) << 23)};
+    const lsr_f2 e = p * sc;
+    return lsr_f2{x.x >= -87.0f ? e.x : 0.0f, x.y >= -87.0f ? e.y : 0.0f};
+}
+
 // Power threshold below which alpha = min(0.99, o exp(power)) < 1/255 for certain (margin 1e-3 in
 // the exponent, far above float error): lets a lane skip exp without changing any decision.
 __device__ __forceinline__ float skip_power(float opacity) {

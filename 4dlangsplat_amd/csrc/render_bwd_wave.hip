@@ -267,16 +267,31 @@ k_render_bwd_wave(RenderBwdArgs a) {
         constexpr int RB = 4;   // entries per branch-free batch (register budget)
 #pragma unroll
         for (int e0 = 0; e0 < WG; e0 += RB) {
-        float Gv[RB], alv[RB], romv[RB], dotv[RB];
+        float Gv[RB], alv[RB], romv[RB], dotv[RB], pw[RB];
         bool act[RB];
 #pragma unroll
         for (int u = 0; u < RB; ++u) {
-            const int e = e0 + u;
-            const float2 xy = s_xy[e];
-            const float4 co = s_co[e];
+            const float2 xy = s_xy[e0 + u];
+            const float4 co = s_co[e0 + u];
             const float dx = xy.x - pxf, dy = xy.y - pyf;
-            const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-            Gv[u] = expf_repro(power);
+            pw[u] = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+        }
+#pragma unroll
+        for (int u = 0; u < RB; u += 2) {   // two entries per packed-fp32 exp
+#ifdef LSR_ABL_NOEXP
+            Gv[u] = fmaxf(1.0f + pw[u], 0.0f);   // timing ablation only
+            Gv[u + 1] = fmaxf(1.0f + pw[u + 1], 0.0f);
+#else
+            const lsr_f2 g2 = expf_repro2(lsr_f2{pw[u], pw[u + 1]});
+            Gv[u] = g2.x;
+            Gv[u + 1] = g2.y;
+#endif
+        }
+#pragma unroll
+        for (int u = 0; u < RB; ++u) {
+            const int e = e0 + u;
+            const float4 co = s_co[e];
+            const float power = pw[u];
             alv[u] = fminf(0.99f, co.w * Gv[u]);
             act[u] = e < cnt && s_k[e] < last_contributor && power <= 0.0f && alv[u] >= 1.0f / 255.0f;
             romv[u] = __builtin_amdgcn_rcpf(1.0f - alv[u]);

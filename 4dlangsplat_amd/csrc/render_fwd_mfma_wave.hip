@@ -166,17 +166,25 @@ __global__ void __launch_bounds__(64) k_render_fwd_wave_mfma(RenderFwdArgs a) {
 #pragma unroll
             for (int u = 0; u < 8; ++u) w8[u] = 0.0f;
             if (8 * o < cnt && !__all(done)) {                    // wave-uniform
-                float al[8];
+                float al[8], pw[8];
                 bool ok[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
-                    const int e = 8 * o + u;
-                    const float2 xy = s_xy[e];
-                    const float4 co = s_co[e];
+                    const float2 xy = s_xy[8 * o + u];
+                    const float4 co = s_co[8 * o + u];
                     const float dx = xy.x - pxf, dy = xy.y - pyf;
-                    const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-                    al[u] = fminf(0.99f, co.w * expf_repro(power));
-                    ok[u] = e < cnt && power <= 0.0f && al[u] >= 1.0f / 255.0f;
+                    pw[u] = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u += 2) {   // two entries per packed-fp32 exp
+                    const lsr_f2 g2 = expf_repro2(lsr_f2{pw[u], pw[u + 1]});
+                    al[u] = fminf(0.99f, s_co[8 * o + u].w * g2.x);
+                    al[u + 1] = fminf(0.99f, s_co[8 * o + u + 1].w * g2.y);
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int e = 8 * o + u;
+                    ok[u] = e < cnt && pw[u] <= 0.0f && al[u] >= 1.0f / 255.0f;
                 }
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {

@@ -118,18 +118,23 @@ __global__ void __launch_bounds__(64) k_render_fwd_wave(RenderFwdArgs a) {
         //      zeros nowhere: its accumulation is not executed or has w = 0 and is not applied).
         constexpr int FB = 8;
         for (int e0 = 0; e0 < cnt; e0 += FB) {
-            float al[FB];
+            float al[FB], pw[FB];
             bool ok[FB];
 #pragma unroll
             for (int u = 0; u < FB; ++u) {
-                const int e = e0 + u;
-                const float2 xy = s_xy[e];
-                const float4 co = s_co[e];
+                const float2 xy = s_xy[e0 + u];
+                const float4 co = s_co[e0 + u];
                 const float dx = xy.x - pxf, dy = xy.y - pyf;
-                const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-                al[u] = fminf(0.99f, co.w * expf_repro(power));
-                ok[u] = e < cnt && power <= 0.0f && al[u] >= 1.0f / 255.0f;
+                pw[u] = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
             }
+#pragma unroll
+            for (int u = 0; u < FB; u += 2) {   // two entries per packed-fp32 exp
+                const lsr_f2 g2 = expf_repro2(lsr_f2{pw[u], pw[u + 1]});
+                al[u] = fminf(0.99f, s_co[e0 + u].w * g2.x);
+                al[u + 1] = fminf(0.99f, s_co[e0 + u + 1].w * g2.y);
+            }
+#pragma unroll
+            for (int u = 0; u < FB; ++u) ok[u] = e0 + u < cnt && pw[u] <= 0.0f && al[u] >= 1.0f / 255.0f;
 #pragma unroll
             for (int u = 0; u < FB; ++u) {
                 const float alpha = al[u];
