@@ -23,6 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gaussians", type=int, default=2_000_000)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--no-torch", action="store_true", help="skip the eager-PyTorch comparison")
     args = ap.parse_args()
     dev = torch.device("cuda")
     g = torch.Generator(device="cpu").manual_seed(0)
@@ -85,6 +86,60 @@ def main():
                           unit="Gaussians/s", ms_per_call=round(bms, 4), gaussians=P,
                           mlp_tflops=round(bflops / (bms * 1e-3) / 1e12, 1),
                           saved_activation_gb=round(saved / 1e9, 2))))
+    if not args.no_torch:
+        torch_baseline(params, res, multires, ins, ups, P, args.iters // 2)
+
+
+def torch_baseline(params, res, multires, ins, ups, P, iters):
+    """The same network in eager PyTorch on the same GPU (F.grid_sample bilinear, align_corners,
+    border padding, product over the 6 planes, concat over scales, the Linear heads), fwd + autograd
+    bwd: what running the reference module on this GPU costs (it cannot travel to the box)."""
+    import torch.nn.functional as F
+    dev = ins[0].device
+    p = {k: v.to(dev).requires_grad_(k != "grid.aabb") for k, v in params.items()}
+    combos = [(0, 1), (0, 2), (0, 3), (1, 2), (1, 3), (2, 3)]
+
+    def run(means, scales, rots, opac, shs, t):
+        a = p["grid.aabb"]
+        pts = (means - a[0]) * (2.0 / (a[1] - a[0])) - 1.0
+        q = torch.cat([pts, torch.full_like(means[:, :1], t)], dim=1)
+        feats = []
+        for s in range(len(multires)):
+            prod = 1.0
+            for ci, (c0, c1) in enumerate(combos):
+                grid = q[:, [c0, c1]].view(1, 1, -1, 2)
+                v = F.grid_sample(p[f"grid.grids.{s}.{ci}"], grid, mode="bilinear", padding_mode="border",
+                                  align_corners=True).view(16, -1).t()
+                prod = prod * v
+            feats.append(prod)
+        h = F.linear(torch.cat(feats, 1), p["feature_out.0.weight"], p["feature_out.0.bias"])
+        outs = []
+        for name, inp in zip(HEADS, (means, scales, rots, opac, shs.reshape(P, 48))):
+            z = F.linear(torch.relu(h), p[name + ".1.weight"], p[name + ".1.bias"])
+            outs.append(inp + F.linear(torch.relu(z), p[name + ".3.weight"], p[name + ".3.bias"]))
+        return outs
+
+    xs = [x.detach().clone().requires_grad_(True) for x in ins[:5]]
+    gs = [ups[0], ups[1], ups[2], ups[3], ups[4].reshape(P, 48)]
+    for _ in range(2):
+        torch.autograd.backward(run(*xs, 0.4), gs)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        with torch.no_grad():
+            run(*xs, 0.4)
+    e1.record()
+    torch.cuda.synchronize()
+    fms = e0.elapsed_time(e1) / iters
+    e0.record()
+    for _ in range(iters):
+        torch.autograd.backward(run(*xs, 0.4), gs)
+    e1.record()
+    torch.cuda.synchronize()
+    fbms = e0.elapsed_time(e1) / iters
+    print(json.dumps(dict(metric="deformation, eager PyTorch on the same GPU (reference structure)", gaussians=P,
+                          forward_ms=round(fms, 3), forward_backward_ms=round(fbms, 3))))
 
 
 if __name__ == "__main__":
