@@ -411,6 +411,58 @@ __device__ __forceinline__ void sh_bwd_channel(const float* __restrict__ sh, int
 #undef SHc
 }
 
+// The direction-only factors of sh_bwd_channel's g[k] (g[k] = b[k] * dRc with the same operation
+// order), computed once for the three colour channels.
+__device__ __forceinline__ void sh_bwd_basis(int deg, float x, float y, float z, float (&b)[16]) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) b[k] = 0.0f;
+    b[0] = SH_C0;
+    if (deg > 0) {
+        b[1] = -SH_C1 * y; b[2] = SH_C1 * z; b[3] = -SH_C1 * x;
+        if (deg > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+            b[4] = SH_C2[0] * xy; b[5] = SH_C2[1] * yz; b[6] = SH_C2[2] * (2.0f * zz - xx - yy); b[7] = SH_C2[3] * xz;
+            b[8] = SH_C2[4] * (xx - yy);
+            if (deg > 2) {
+                b[9] = SH_C3[0] * y * (3.0f * xx - yy);
+                b[10] = SH_C3[1] * xy * z;
+                b[11] = SH_C3[2] * y * (4.0f * zz - xx - yy);
+                b[12] = SH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy);
+                b[13] = SH_C3[4] * x * (4.0f * zz - xx - yy);
+                b[14] = SH_C3[5] * z * (xx - yy);
+                b[15] = SH_C3[6] * x * (xx - 3.0f * yy);
+            }
+        }
+    }
+}
+
+// The d colour / d direction partials of channel ch (the second half of sh_bwd_channel).
+__device__ __forceinline__ void sh_bwd_dir(const float* __restrict__ sh, int ch, int deg, float x, float y, float z,
+                                          float& dRdx, float& dRdy, float& dRdz) {
+#define SHc(k) sh[(k) * 3 + ch]
+    if (deg > 0) {
+        dRdx = -SH_C1 * SHc(3); dRdy = -SH_C1 * SHc(1); dRdz = SH_C1 * SHc(2);
+        if (deg > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+            dRdx += SH_C2[0] * y * SHc(4) + SH_C2[2] * 2.0f * -x * SHc(6) + SH_C2[3] * z * SHc(7) + SH_C2[4] * 2.0f * x * SHc(8);
+            dRdy += SH_C2[0] * x * SHc(4) + SH_C2[1] * z * SHc(5) + SH_C2[2] * 2.0f * -y * SHc(6) + SH_C2[4] * 2.0f * -y * SHc(8);
+            dRdz += SH_C2[1] * y * SHc(5) + SH_C2[2] * 2.0f * 2.0f * z * SHc(6) + SH_C2[3] * x * SHc(7);
+            if (deg > 2) {
+                dRdx += SH_C3[0] * SHc(9) * 3.0f * 2.0f * xy + SH_C3[1] * SHc(10) * yz + SH_C3[2] * SHc(11) * -2.0f * xy +
+                        SH_C3[3] * SHc(12) * -3.0f * 2.0f * xz + SH_C3[4] * SHc(13) * (-3.0f * xx + 4.0f * zz - yy) +
+                        SH_C3[5] * SHc(14) * 2.0f * xz + SH_C3[6] * SHc(15) * 3.0f * (xx - yy);
+                dRdy += SH_C3[0] * SHc(9) * 3.0f * (xx - yy) + SH_C3[1] * SHc(10) * xz +
+                        SH_C3[2] * SHc(11) * (-3.0f * yy + 4.0f * zz - xx) + SH_C3[3] * SHc(12) * -3.0f * 2.0f * yz +
+                        SH_C3[4] * SHc(13) * -2.0f * xy + SH_C3[5] * SHc(14) * -2.0f * yz + SH_C3[6] * SHc(15) * -3.0f * 2.0f * xy;
+                dRdz += SH_C3[1] * SHc(10) * xy + SH_C3[2] * SHc(11) * 4.0f * 2.0f * yz +
+                        SH_C3[3] * SHc(12) * 3.0f * (2.0f * zz - xx - yy) + SH_C3[4] * SHc(13) * 4.0f * 2.0f * xz +
+                        SH_C3[5] * SHc(14) * (xx - yy);
+            }
+        }
+    }
+#undef SHc
+}
+
 template <bool ACC>
 __device__ __forceinline__ void put(float* p, float v) {
     if (ACC) *p += v; else *p = v;
@@ -715,12 +767,13 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd_views(PreprocessBwdViews
                     const uint8_t cl = cm.clamped[i];
                     const float dR[3] = {(cl & 1) ? 0.0f : rs[0], (cl & 2) ? 0.0f : rs[1], (cl & 4) ? 0.0f : rs[2]};
                     float dRdx[3] = {0, 0, 0}, dRdy[3] = {0, 0, 0}, dRdz[3] = {0, 0, 0};
-                    float g[16];
+                    float bs[16];
+                    sh_bwd_basis(cm.deg, x, y, z, bs);   // once for the three channels
 #pragma unroll
                     for (int ch = 0; ch < 3; ++ch) {
-                        sh_bwd_channel(sh, ch, cm.deg, x, y, z, dR[ch], g, dRdx[ch], dRdy[ch], dRdz[ch]);
+                        sh_bwd_dir(sh, ch, cm.deg, x, y, z, dRdx[ch], dRdy[ch], dRdz[ch]);
 #pragma unroll
-                        for (int k = 0; k < 16; ++k) dsh[k * 3 + ch] += g[k];
+                        for (int k = 0; k < 16; ++k) dsh[k * 3 + ch] += bs[k] * dR[ch];
                     }
                     const float dLdx = dRdx[0] * dR[0] + dRdx[1] * dR[1] + dRdx[2] * dR[2];
                     const float dLdy = dRdy[0] * dR[0] + dRdy[1] * dR[1] + dRdy[2] * dR[2];
