@@ -54,9 +54,11 @@ class GradBucket:
         self.floats_per_gaussian = sum(w for _, w in fields)
         self.flat = torch.zeros(P * self.floats_per_gaussian, dtype=torch.float32, device=device)
         self.views: Dict[str, Optional[torch.Tensor]] = {}
+        self.ranges: Dict[str, Tuple[int, int]] = {}     # field -> [start, end) in flat
         o = 0
         for name, w in fields:
             seg = self.flat[o * P:(o + w) * P]
+            self.ranges[name] = (o * P, (o + w) * P)
             if w == 0:
                 self.views[name] = None
             elif name == "sh":
@@ -106,10 +108,23 @@ class ViewParallelStep:
             if b.radii is not None and radii is not None:
                 torch.maximum(b.radii, radii.to(torch.int32), out=b.radii)
         flush = getattr(render_view, "flush", None)
+        early = None
+        lo, hi = b.ranges["language_feature"]
+        if self.world > 1 and flush is not None and hi > lo:
+            # with the batched backward the language gradients are final once the last view's
+            # compositor backward ran; their SUM runs during the flush (the preprocess backward,
+            # which writes every other field) instead of after it
+            early = dist.all_reduce(b.flat[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         if flush is not None:        # renderers that batch the backward over the rank's views
             flush(b)
         if self.world > 1:
-            dist.all_reduce(b.flat, op=dist.ReduceOp.SUM, group=self.group)
+            if early is None:
+                dist.all_reduce(b.flat, op=dist.ReduceOp.SUM, group=self.group)
+            else:
+                for seg in (b.flat[:lo], b.flat[hi:]):
+                    if seg.numel():
+                        dist.all_reduce(seg, op=dist.ReduceOp.SUM, group=self.group)
+                early.wait()
             if b.radii is not None:
                 dist.all_reduce(b.radii, op=dist.ReduceOp.MAX, group=self.group)
         return b

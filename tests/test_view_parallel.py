@@ -64,9 +64,12 @@ def _view_grads(v):
     return g.normal(size=(3, H, W)).astype(np.float32), g.normal(size=(C, H, W)).astype(np.float32)
 
 
-def oracle_renderer(sc, cams):
+def oracle_renderer(sc, cams, batched=False):
+    """batched: like native_view_renderer(batch_backward=True), the language gradient goes into
+    the bucket per view and every other field only at flush (the batched preprocess backward)."""
     names = dict(means3D="means3D", scales="scales", rotations="rotations", opacity="opacities", sh="sh",
                  lang="language_feature", means2D="means2D")
+    held = []
 
     def render_view(v, bucket):
         r = oracle.forward(oracle_settings(cams[v]), sc.means3D.numpy(), sc.opacities.numpy(), shs=sc.shs.numpy(),
@@ -75,11 +78,21 @@ def oracle_renderer(sc, cams):
         g = r.backward(gc, gl, None, nthreads=1)
         for k, name in names.items():
             if bucket.views.get(name) is not None:
-                bucket.views[name] += torch.from_numpy(g[k])
+                if batched and name != "language_feature":
+                    held.append((name, torch.from_numpy(g[k].copy())))
+                else:
+                    bucket.views[name] += torch.from_numpy(g[k])
         radii = torch.from_numpy(r.radii.copy())
         r.close()
         return radii
 
+    def flush(bucket):
+        for name, t in held:
+            bucket.views[name] += t
+        held.clear()
+
+    if batched:
+        render_view.flush = flush
     return render_view
 
 
@@ -92,7 +105,7 @@ def _serial_reference(densify):
     return b
 
 
-def _worker(rank, world, port, outdir, densify):
+def _worker(rank, world, port, outdir, densify, batched=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -101,11 +114,14 @@ def _worker(rank, world, port, outdir, densify):
         step = ViewParallelStep(b, N_VIEWS)
         assert step.world == world and step.rank == rank
         calls = []
-        render = oracle_renderer(sc, cams)
+        render = oracle_renderer(sc, cams, batched)
 
         def counted(v, bucket):
             calls.append(v)
             return render(v, bucket)
+
+        if batched:
+            counted.flush = render.flush
 
         step.run(counted)
         assert calls == list(range(*view_slice(N_VIEWS, world, rank)))
@@ -122,11 +138,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("densify", [False, True])
-def test_two_rank_step_equals_serial_batch(densify):
+@pytest.mark.parametrize("densify,batched", [(False, False), (True, False), (True, True)])
+def test_two_rank_step_equals_serial_batch(densify, batched):
+    """batched: the language field's SUM is issued before the flush and overlaps it."""
     ref = _serial_reference(densify)
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(2, _free_port(), d, densify), nprocs=2, join=True)
+        mp.spawn(_worker, args=(2, _free_port(), d, densify, batched), nprocs=2, join=True)
         outs = [torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(2)]
     assert sorted(outs[0]["calls"] + outs[1]["calls"]) == list(range(N_VIEWS))
     # both ranks hold the same reduced bucket, equal to the serial sum up to fp32 reassociation
