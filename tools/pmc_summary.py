@@ -25,6 +25,19 @@ PHASE_KERNEL = {"preprocess": "k_preprocess", "emit": "k_emit", "tile_ranges": "
                 "preprocess_bwd": "k_preprocess_bwd", "preprocess_bwd_views": "k_preprocess_bwd_views"}
 
 
+N_SIMD, N_XCD = 256 * 4, 8   # MI355X: 256 CUs x 4 SIMDs, 8 XCDs
+
+
+def mfma_frac(c):
+    """Matrix-core busy fraction of a dispatch: SQ_VALU_MFMA_BUSY_CYCLES (summed over the SIMDs;
+    32 per v_mfma_f32_32x32x16_bf16, MI355X_MICROARCH.md) / (dispatch cycles x SIMDs), the dispatch
+    cycles being GRBM_GUI_ACTIVE / 8 (the counter sums the 8 XCDs: checked against the kernel
+    duration x 2.4 GHz)."""
+    busy = sum(c["SQ_VALU_MFMA_BUSY_CYCLES"]) / len(c["SQ_VALU_MFMA_BUSY_CYCLES"])
+    active = sum(c["GRBM_GUI_ACTIVE"]) / len(c["GRBM_GUI_ACTIVE"]) / N_XCD
+    return busy / max(active * N_SIMD, 1.0)
+
+
 def main(d, json_out=None):
     acc = defaultdict(lambda: defaultdict(list))
     for f in sorted(glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True)):
@@ -43,6 +56,8 @@ def main(d, json_out=None):
                 parts.append(f"FETCH_SIZEx2_MB={2 * mean / 1024:.4g}")
             if c == "WRITE_SIZE":
                 parts.append(f"WRITE_MB={mean / 1024:.4g}")
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in acc[k] and "GRBM_GUI_ACTIVE" in acc[k]:
+            parts.append(f"MFMA_BUSY_FRAC={mfma_frac(acc[k]):.4g}")
         print(k, " ".join(parts))
     if json_out:
         import json
@@ -57,6 +72,8 @@ def main(d, json_out=None):
             res[phase] = dict(kernel=ks[0], fetch_size_kb=fetch, write_size_kb=write,
                               hbm_bytes_per_launch=int((2 * fetch + write) * 1024),
                               dispatches=len(f["FETCH_SIZE"]))
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in f and "GRBM_GUI_ACTIVE" in f:
+                res[phase]["mfma_busy_frac"] = round(mfma_frac(f), 4)
         res["_note"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, bench.py --steps 1 (8 views); "
                         "hbm = (2*FETCH_SIZE + WRITE_SIZE)*1024 per MI355X_MICROARCH.md HBM section")
         with open(json_out, "w") as fh:
