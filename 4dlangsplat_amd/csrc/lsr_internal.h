@@ -256,7 +256,6 @@ void launch_tile_ranges(size_t K, const uint32_t* keys, uint2* ranges, hipStream
 // compositing (render_fwd.hip / render_bwd.hip)
 void launch_render_fwd(const RenderFwdArgs& a, hipStream_t st);
 void launch_render_bwd(const RenderBwdArgs& a, hipStream_t st);
-void launch_render_bwd_mfma(const RenderBwdArgs& a, hipStream_t st);
 void launch_render_fwd_wave(const RenderFwdArgs& a, hipStream_t st);
 void launch_render_fwd_wave_mfma(const RenderFwdArgs& a, hipStream_t st);   // 17..32 channels
 void launch_render_bwd_wave(const RenderBwdArgs& a, hipStream_t st);
