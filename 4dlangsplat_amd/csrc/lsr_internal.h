@@ -71,7 +71,7 @@ struct PreprocessBwdArgs {
     const uint32_t* inst_off;
     int recq;
     int deterministic;
-    const float* acc_small;   // atomic mode: [P,12] summed records
+    const float* acc_small;   // atomic mode: [P, ACC_PITCH] summed records
     // outputs (nullable)
     float* dopacity;
     float* dmeans3D;
@@ -96,7 +96,7 @@ struct ViewCam {
     int deg;
     const uint32_t* tiles;    // tiles touched in this view (0 = culled)
     const uint8_t* clamped;
-    const float* acc_small;   // [P,12] the view's summed records
+    const float* acc_small;   // [P, ACC_PITCH] the view's summed records
 };
 struct PreprocessBwdViewsArgs {
     int P, M, nv;
@@ -160,7 +160,7 @@ struct RenderBwdArgs {
     int recq;
     int deterministic;
     // default (atomic) mode: per-Gaussian accumulators
-    float* acc_small;         // [P,12] record layout [0..11]
+    float* acc_small;         // [P, ACC_PITCH], record layout [0..9]
     float* acc_lang;          // [P,C] (the caller's dL/dlanguage buffer), may be null
 };
 
