@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--gaussians", type=int, default=2_000_000)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--no-torch", action="store_true", help="skip the eager-PyTorch comparison")
+    ap.add_argument("--morton", action="store_true", help="store the Gaussians in Morton order (diagnostic)")
     args = ap.parse_args()
     dev = torch.device("cuda")
     g = torch.Generator(device="cpu").manual_seed(0)
@@ -44,6 +45,13 @@ def main():
     field = DeformationField({k: v.to(dev) for k, v in params.items()}, res, multires)
     P = args.gaussians
     means = (torch.rand(P, 3, generator=g) * torch.tensor([3.0, 2.4, 8.0]) + torch.tensor([-1.5, -1.2, 2.0])).to(dev)
+    if args.morton:   # diagnostic: Gaussians stored along a Morton curve (spatially coherent order)
+        q = ((means - means.min(0).values) / (means.max(0).values - means.min(0).values) * 1023).long().cpu()
+        code = torch.zeros(P, dtype=torch.long)
+        for bit in range(10):
+            for c in range(3):
+                code |= ((q[:, c] >> bit) & 1) << (3 * bit + c)
+        means = means[torch.argsort(code).to(dev)].contiguous()
     ins = [means, torch.randn(P, 3, generator=g).to(dev), torch.randn(P, 4, generator=g).to(dev),
            torch.randn(P, 1, generator=g).to(dev), torch.randn(P, 16, 3, generator=g).to(dev),
            torch.zeros(P, 3, device=dev)]
