@@ -114,7 +114,10 @@ void exclusive_scan_u32(const uint32_t* in, uint32_t* out, size_t n, uint32_t* t
 //   * the tile is placed digit-sorted in LDS and written out in runs (coalesced stores).
 // A look-back spin is bounded: on timeout the pass sets the caller's error word and finishes
 // (results invalid, never a hang).
-constexpr int OS_ITEMS = 16;
+#ifndef LSR_OS_ITEMS
+#define LSR_OS_ITEMS 16
+#endif
+constexpr int OS_ITEMS = LSR_OS_ITEMS;   // keys per thread per pass
 constexpr int OS_TILE = 256 * OS_ITEMS;       // keys per block
 constexpr uint32_t OS_AGG = 1u << 30, OS_PRE = 2u << 30, OS_CNT = (1u << 30) - 1u;
 
@@ -151,8 +154,12 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t x, uint32_t* s_w
 
 // Digit counts of every pass in one read of the keys (a pass permutes keys, it does not change
 // the counts).  A CU-sized grid strides over the keys (16 loads in flight per thread), so each
-// global counter takes at most one atomic per block.
+// global counter takes at most one atomic per block.  The counters are kept in HIST_COPIES
+// copies, one per XCD (block b runs on XCD b mod 8): each address then takes 1/8 of the blocks'
+// atomics (same-address device atomics serialise), and the pass kernel sums the copies.
 constexpr int OS_HIST_BLOCKS = 512;
+constexpr int HIST_COPIES = 8;
+constexpr int HIST_WORDS = 4 * 256;   // one copy: [pass][digit]
 __global__ void __launch_bounds__(256) k_radix_hist(const uint32_t* __restrict__ keys, size_t n, int begin_bit,
                                                     int end_bit, uint32_t* __restrict__ hist) {
     __shared__ uint32_t s_h[4][256];
@@ -184,7 +191,7 @@ __global__ void __launch_bounds__(256) k_radix_hist(const uint32_t* __restrict__
     __syncthreads();
     int p = 0;
     for (int shift = begin_bit; shift < end_bit; shift += 8, ++p)
-        if (s_h[p][tid]) atomicAdd(hist + p * 256 + tid, s_h[p][tid]);
+        if (s_h[p][tid]) atomicAdd(hist + (blockIdx.x % HIST_COPIES) * HIST_WORDS + p * 256 + tid, s_h[p][tid]);
 }
 
 __global__ void __launch_bounds__(256) k_radix_pass(const uint32_t* __restrict__ keys_in,
@@ -276,7 +283,10 @@ __global__ void __launch_bounds__(256) k_radix_pass(const uint32_t* __restrict__
         __hip_atomic_store(st + (size_t)bid * 256 + tid, OS_PRE | (prefix + total), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     }
-    const uint32_t dstart = block_excl_scan256(hist[tid], s_wave);   // global start of digit tid
+    uint32_t hcount = 0;
+#pragma unroll
+    for (int c = 0; c < HIST_COPIES; ++c) hcount += hist[c * HIST_WORDS + tid];
+    const uint32_t dstart = block_excl_scan256(hcount, s_wave);      // global start of digit tid
     const uint32_t lbase = block_excl_scan256(total, s_wave);        // local start of digit tid
     s_lbase[tid] = lbase;
     s_gbase[tid] = dstart + prefix - lbase;
@@ -306,14 +316,14 @@ __global__ void __launch_bounds__(256) k_radix_pass(const uint32_t* __restrict__
 static size_t os_blocks(size_t n) { return (n + OS_TILE - 1) / OS_TILE; }
 
 size_t radix_temp_bytes(size_t n) {
-    // hist [4][256] | tickets [4] | err [1] (padded) | status [4][blocks][256]
-    return align_up(4 * 256 * 4 + 64, 256) + align_up(4 * os_blocks(n) * 256 * 4, 256);
+    // hist [HIST_COPIES][4][256] | tickets [4] | err [1] (padded) | status [4][blocks][256]
+    return align_up(HIST_COPIES * HIST_WORDS * 4 + 64, 256) + align_up(4 * os_blocks(n) * 256 * 4, 256);
 }
 
 size_t radix_temp_zero_bytes(size_t n, int begin_bit, int end_bit) {
     if (n == 0 || end_bit <= begin_bit) return 0;
     const int npass = (end_bit - begin_bit + 7) / 8;
-    return align_up(4 * 256 * 4 + 64, 256) + (size_t)npass * os_blocks(n) * 256 * 4;
+    return align_up(HIST_COPIES * HIST_WORDS * 4 + 64, 256) + (size_t)npass * os_blocks(n) * 256 * 4;
 }
 
 bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b, size_t n,
@@ -321,9 +331,10 @@ bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint
     if (n == 0 || end_bit <= begin_bit) return false;
     const size_t nb = os_blocks(n);
     uint32_t* hist = reinterpret_cast<uint32_t*>(temp);
-    uint32_t* tickets = hist + 4 * 256;
+    uint32_t* tickets = hist + HIST_COPIES * HIST_WORDS;
     uint32_t* own_err = tickets + 4;
-    uint32_t* status = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(temp) + align_up(4 * 256 * 4 + 64, 256));
+    uint32_t* status =
+        reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(temp) + align_up(HIST_COPIES * HIST_WORDS * 4 + 64, 256));
     if (!temp_zeroed) (void)hipMemsetAsync(temp, 0, radix_temp_zero_bytes(n, begin_bit, end_bit), st);
     const unsigned hb = (unsigned)min((size_t)OS_HIST_BLOCKS, (n + 64 * OS_ITEMS * 4 - 1) / (64 * OS_ITEMS * 4));
     hipLaunchKernelGGL(k_radix_hist, dim3(hb), dim3(256), 0, st, (const uint32_t*)keys_a, n, begin_bit, end_bit, hist);
