@@ -298,6 +298,42 @@ def test_full_size_forward_matches_oracle():
     _assert_forward(nat, ref, 32)
 
 
+def test_config1_rgb_only_forward_and_backward():
+    """BASELINE.json configs[0] at full size: 50k Gaussians, one 400 x 400 camera (tanfov 0.6 / 0.6),
+    3 channels with include_feature=False and a zeros language tensor (gaussian_renderer/__init__.py:
+    96-99).  Exact lists and radii, RGB within 1e-4, language output and gradient exactly zero, every
+    other gradient within 1e-4 of the oracle."""
+    W = H = 400
+    sc = synthetic.make_scene(50_000, C=3, tanfovx=0.6, tanfovy=0.6, seed=0)
+    sc.lang = torch.zeros_like(sc.lang)
+    cam = synthetic.origin_camera(W, H, tanfovx=0.6, tanfovy=0.6)
+    nat = run_native(sc, cam, include_feature=False)
+    ref = run_oracle(sc, cam, include_feature=False, nthreads=16)
+    _assert_forward(nat, ref, 0)
+    assert float(nat[1].abs().max()) == 0.0
+    rng = np.random.default_rng(7)
+    gc = rng.normal(size=(3, H, W)).astype(np.float32)
+    g = dgr.backward_native(nat[4], torch.tensor(gc, device="cuda"), None, None)
+    rg = ref.backward(gc, None, None, nthreads=16)
+    for n, o in (("means3D", "means3D"), ("means2D", "means2D"), ("opacities", "opacity"), ("scales", "scales"),
+                 ("rotations", "rotations"), ("sh", "sh")):
+        assert grad_err(g[n].cpu().numpy().reshape(rg[o].shape), rg[o]) <= GRAD_TOL, n
+    assert float(g["language_feature"].abs().max()) == 0.0
+
+
+def test_config2_render_forward():
+    """BASELINE.json configs[1] stand-in (the pretrained americano scene is unavailable
+    offline): 300k Gaussians, 960 x 540, RGB + 3 language channels with include_feature=True,
+    forward only as render.py runs it.  Exact lists and radii; RGB 1e-4, language 1e-3."""
+    W, H = 960, 540
+    sc = synthetic.make_scene(300_000, C=3, tanfovx=0.6, tanfovy=0.6 * H / W, seed=2)
+    cam = synthetic.origin_camera(W, H)
+    with torch.no_grad():
+        nat = run_native(sc, cam)
+    ref = run_oracle(sc, cam, nthreads=16)
+    _assert_forward(nat, ref, 3)
+
+
 def test_headline_properties_2m():
     """2M Gaussians: size-independent invariants (sorted per-tile lists, counts, saturation)."""
     sc = synthetic.make_scene(2_000_000, C=32)
