@@ -156,6 +156,7 @@ struct Img {
     uint32_t* tile_max;
     float* final_T;
     uint32_t* n_contrib;
+    uint32_t* tile_order;   // backward scratch: tiles by descending replay length
 };
 Img carve_img(void* base, int W, int H, size_t* bytes) {
     const size_t gx = (W + LSR_TILE_X - 1) / LSR_TILE_X, gy = (H + LSR_TILE_Y - 1) / LSR_TILE_Y;
@@ -165,6 +166,7 @@ Img carve_img(void* base, int W, int H, size_t* bytes) {
     m.tile_max = c.take<uint32_t>(gx * gy);
     m.final_T = c.take<float>((size_t)W * H);
     m.n_contrib = c.take<uint32_t>((size_t)W * H);
+    m.tile_order = c.take<uint32_t>(gx * gy);
     if (bytes) *bytes = c.off;
     return m;
 }
@@ -434,7 +436,7 @@ int lsr_backward(const lsr_settings* s, const lsr_fwd_in* in, const lsr_bwd_in* 
         r.ranges = m.ranges; r.point_list = point_list; r.xy = g.xy; r.conic_o = g.conic_o; r.rgbd = g.rgbd;
         r.rect = g.rect; r.inst_off = g.inst_off;
         r.lang = in->language_feature; r.bg = s->bg; r.final_T = m.final_T; r.n_contrib = m.n_contrib;
-        r.tile_max_contrib = m.tile_max;
+        r.tile_max_contrib = m.tile_max; r.tile_order = m.tile_order;
         r.dL_dcolor = gin->dL_dout_color; r.dL_dlang = gin->dL_dout_language_feature; r.dL_ddepth = gin->dL_dout_depth;
         r.rec = sc.rec; r.flags = sc.flags; r.recq = recq; r.deterministic = det;
         r.acc_small = sc.acc_small; r.acc_lang = gout->dL_dlanguage_feature;
@@ -497,7 +499,7 @@ int lsr_backward_composite(const lsr_settings* s, const lsr_fwd_in* in, const ls
     r.xy = g.xy; r.conic_o = g.conic_o; r.rgbd = g.rgbd;
     r.rect = g.rect; r.inst_off = g.inst_off;
     r.lang = in->language_feature; r.bg = s->bg; r.final_T = m.final_T; r.n_contrib = m.n_contrib;
-    r.tile_max_contrib = m.tile_max;
+    r.tile_max_contrib = m.tile_max; r.tile_order = m.tile_order;
     r.dL_dcolor = gin->dL_dout_color; r.dL_dlang = gin->dL_dout_language_feature; r.dL_ddepth = gin->dL_dout_depth;
     r.recq = recq; r.deterministic = 0;
     r.acc_small = reinterpret_cast<float*>(g.acc); r.acc_lang = dL_dlanguage;

@@ -149,6 +149,7 @@ struct RenderBwdArgs {
     const float* final_T;
     const uint32_t* n_contrib;
     const uint32_t* tile_max_contrib;
+    uint32_t* tile_order;     // [tiles] scratch: the wave backward's longest-first tile order
     const float* dL_dcolor;   // [3,H,W]
     const float* dL_dlang;    // [C,H,W] or null
     const float* dL_ddepth;   // [H,W] or null

@@ -45,8 +45,9 @@ k_render_bwd_wave(RenderBwdArgs a) {
     __shared__ uint32_t s_fg[WFIFO];
 
     const int b = blockIdx.x;
-    const int tile = (b >> 5) * 8 + (b & 7), quad = (b >> 3) & 3;
-    if (tile >= a.grid_x * a.grid_y) return;
+    const int slot = (b >> 5) * 8 + (b & 7), quad = (b >> 3) & 3;   // a slot's 4 quadrants: one XCD
+    if (slot >= a.grid_x * a.grid_y) return;
+    const int tile = a.tile_order ? (int)a.tile_order[slot] : slot;
     const int lane = threadIdx.x, g4 = lane >> 4, l16 = lane & 15;
     const int tx = tile % a.grid_x, ty = tile / a.grid_x;
     const int qx0 = tx * LSR_TILE_X + (quad & 1) * 8, qy0 = ty * LSR_TILE_Y + (quad >> 1) * 8;
@@ -430,8 +431,41 @@ k_render_bwd_wave(RenderBwdArgs a) {
     }
 }
 
+// Longest-first launch order.  Blocks are dispatched in launch order, so with ~10 quadrant waves
+// per wave slot the tiles with the longest replays, launched last, would set the tail.  One block
+// buckets the tiles by their replay bound (tile_max_contrib, written by the forward) in
+// descending order: a counting sort over 1024 buckets of 2 replay entries.  The order inside a
+// bucket is not fixed, which only permutes float atomic summation (this path is non-deterministic).
+constexpr int ORDER_BUCKETS = 1024;
+__global__ void __launch_bounds__(1024) k_tile_order(int ntiles, const uint32_t* __restrict__ tile_max,
+                                                     uint32_t* __restrict__ order) {
+    __shared__ uint32_t s_cnt[ORDER_BUCKETS];
+    __shared__ uint32_t s_wave[16];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    s_cnt[tid] = 0;
+    __syncthreads();
+    auto bucket = [&](int t) { return ORDER_BUCKETS - 1 - (int)min(tile_max[t] >> 1, (uint32_t)ORDER_BUCKETS - 1); };
+    for (int t = tid; t < ntiles; t += 1024) atomicAdd(&s_cnt[bucket(t)], 1u);
+    __syncthreads();
+    const uint32_t x = s_cnt[tid];
+    uint32_t inc = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63) s_wave[wave] = inc;
+    __syncthreads();
+    uint32_t off = 0;
+    for (int w = 0; w < wave; ++w) off += s_wave[w];
+    s_cnt[tid] = off + inc - x;   // exclusive start of bucket tid
+    __syncthreads();
+    for (int t = tid; t < ntiles; t += 1024) order[atomicAdd(&s_cnt[bucket(t)], 1u)] = (uint32_t)t;
+}
+
 void launch_render_bwd_wave(const RenderBwdArgs& a, hipStream_t st) {
     const int ntiles = a.grid_x * a.grid_y;
+    if (a.tile_order) hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, st, ntiles, a.tile_max_contrib, a.tile_order);
     hipLaunchKernelGGL(k_render_bwd_wave, dim3(((ntiles + 7) / 8) * 32), dim3(64), 0, st, a);
 }
 
