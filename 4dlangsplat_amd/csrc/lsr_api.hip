@@ -380,7 +380,8 @@ int lsr_forward_composite(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_o
     r.W = W; r.H = H; r.grid_x = gx; r.grid_y = gy; r.C = C; r.include_feature = s->include_feature;
     r.ranges = m.ranges; r.point_list = point_list; r.xy = g.xy; r.conic_o = g.conic_o; r.rgbd = g.rgbd;
     r.lang = in->language_feature; r.bg = s->bg; r.final_T = m.final_T; r.n_contrib = m.n_contrib;
-    r.tile_max_contrib = m.tile_max; r.out_color = out->out_color; r.out_lang = out->out_language_feature;
+    r.tile_max_contrib = m.tile_max; r.tile_order = m.tile_order;
+    r.out_color = out->out_color; r.out_lang = out->out_language_feature;
     r.out_depth = out->out_depth;
     if (C > 0 && !s->include_feature)
         LSR_HIP(hipMemsetAsync(out->out_language_feature, 0, sizeof(float) * (size_t)C * W * H, st));

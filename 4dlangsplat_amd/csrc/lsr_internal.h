@@ -130,6 +130,7 @@ struct RenderFwdArgs {
     float* final_T;
     uint32_t* n_contrib;
     uint32_t* tile_max_contrib;   // per tile: max n_contrib over its pixels (bounds the backward replay)
+    uint32_t* tile_order;         // [tiles] scratch: longest-list-first launch order (null: tile order)
     float* out_color;
     float* out_lang;
     float* out_depth;
@@ -256,6 +257,9 @@ void launch_tile_ranges(size_t K, const uint32_t* keys, uint2* ranges, hipStream
 
 // compositing (render_fwd.hip / render_bwd.hip)
 void launch_render_fwd(const RenderFwdArgs& a, hipStream_t st);
+// Longest-first launch order of the tiles into order[]: by ranges' list lengths (forward) when
+// ranges is given, else by the forward's replay bounds tile_max (backward).  render_bwd_wave.hip.
+void launch_tile_order(int ntiles, const uint32_t* tile_max, const uint2* ranges, uint32_t* order, hipStream_t st);
 void launch_render_bwd(const RenderBwdArgs& a, hipStream_t st);
 void launch_render_fwd_wave(const RenderFwdArgs& a, hipStream_t st);
 void launch_render_fwd_wave_mfma(const RenderFwdArgs& a, hipStream_t st);   // 17..32 channels

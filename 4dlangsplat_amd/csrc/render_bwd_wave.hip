@@ -438,13 +438,16 @@ k_render_bwd_wave(RenderBwdArgs a) {
 // bucket is not fixed, which only permutes float atomic summation (this path is non-deterministic).
 constexpr int ORDER_BUCKETS = 1024;
 __global__ void __launch_bounds__(1024) k_tile_order(int ntiles, const uint32_t* __restrict__ tile_max,
-                                                     uint32_t* __restrict__ order) {
+                                                     const uint2* __restrict__ ranges, uint32_t* __restrict__ order) {
     __shared__ uint32_t s_cnt[ORDER_BUCKETS];
     __shared__ uint32_t s_wave[16];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     s_cnt[tid] = 0;
     __syncthreads();
-    auto bucket = [&](int t) { return ORDER_BUCKETS - 1 - (int)min(tile_max[t] >> 1, (uint32_t)ORDER_BUCKETS - 1); };
+    auto bucket = [&](int t) {
+        const uint32_t cost = ranges ? (ranges[t].y - ranges[t].x) >> 2 : tile_max[t] >> 1;
+        return ORDER_BUCKETS - 1 - (int)min(cost, (uint32_t)ORDER_BUCKETS - 1);
+    };
     for (int t = tid; t < ntiles; t += 1024) atomicAdd(&s_cnt[bucket(t)], 1u);
     __syncthreads();
     const uint32_t x = s_cnt[tid];
@@ -463,9 +466,13 @@ __global__ void __launch_bounds__(1024) k_tile_order(int ntiles, const uint32_t*
     for (int t = tid; t < ntiles; t += 1024) order[atomicAdd(&s_cnt[bucket(t)], 1u)] = (uint32_t)t;
 }
 
+void launch_tile_order(int ntiles, const uint32_t* tile_max, const uint2* ranges, uint32_t* order, hipStream_t st) {
+    hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, st, ntiles, tile_max, ranges, order);
+}
+
 void launch_render_bwd_wave(const RenderBwdArgs& a, hipStream_t st) {
     const int ntiles = a.grid_x * a.grid_y;
-    if (a.tile_order) hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, st, ntiles, a.tile_max_contrib, a.tile_order);
+    if (a.tile_order) launch_tile_order(ntiles, a.tile_max_contrib, nullptr, a.tile_order, st);
     hipLaunchKernelGGL(k_render_bwd_wave, dim3(((ntiles + 7) / 8) * 32), dim3(64), 0, st, a);
 }
 

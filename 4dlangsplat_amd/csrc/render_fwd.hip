@@ -318,7 +318,13 @@ static void go_fwd(const RenderFwdArgs& a, hipStream_t st) {
 
 void launch_render_fwd(const RenderFwdArgs& a, hipStream_t st) {
 #ifndef LSR_FWD_BLOCK
-    launch_render_fwd_wave(a, st);   // compacted per-quadrant waves (render_fwd_wave.hip)
+    RenderFwdArgs f = a;
+#ifdef LSR_FWD_ORDER
+    if (f.tile_order) launch_tile_order(a.grid_x * a.grid_y, nullptr, a.ranges, f.tile_order, st);
+#else
+    f.tile_order = nullptr;   // tile order: the order scratch is not written
+#endif
+    launch_render_fwd_wave(f, st);   // compacted per-quadrant waves (render_fwd_wave.hip)
     return;
 #endif
     const int C = a.include_feature ? a.C : 0;
