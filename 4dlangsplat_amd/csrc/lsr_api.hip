@@ -41,6 +41,7 @@ int fail(int code, const std::string& msg) {
 struct Profiler {
     std::mutex mu;
     bool on = false;
+    uint32_t mask = ~0u;   // phases timed while on (bit LSR_PHASE_*)
     std::vector<hipEvent_t> pool;
     struct Rec { int phase; hipEvent_t a, b; };
     std::vector<Rec> pending;
@@ -61,7 +62,7 @@ struct PhaseTimer {
     hipEvent_t a = nullptr, b = nullptr;
     PhaseTimer(int p, hipStream_t s) : phase(p), st(s) {
         std::lock_guard<std::mutex> l(g_prof.mu);
-        if (!g_prof.on) return;
+        if (!g_prof.on || !((g_prof.mask >> p) & 1u)) return;
         a = g_prof.get();
         b = g_prof.get();
         if (a) (void)hipEventRecord(a, st);
@@ -249,18 +250,18 @@ int64_t lsr_backward_bytes(int32_t P, int64_t K, int32_t C, int32_t deterministi
     return (int64_t)b;
 }
 
-int lsr_forward_preprocess(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_out* out, void* geom,
-                           int64_t* num_rendered, lsr_stream_t stream) {
+int lsr_forward_preprocess_async(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_out* out, void* geom,
+                                 uint32_t* host_count, lsr_stream_t stream) {
     int rc = check_common(s, in);
     if (rc) return rc;
     if (!out || (!out->radii && in->P > 0)) return fail(LSR_EINVAL, "radii output is required");
-    if (!geom || !num_rendered) return fail(LSR_EINVAL, "geom workspace and num_rendered are required");
+    if (!geom || !host_count) return fail(LSR_EINVAL, "geom workspace and host_count are required");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const int P = in->P, W = s->image_width, H = s->image_height;
     const int gx = (W + LSR_TILE_X - 1) / LSR_TILE_X, gy = (H + LSR_TILE_Y - 1) / LSR_TILE_Y;
     Geom g = carve_geom(geom, (size_t)(P > 0 ? P : 1), nullptr);
     if (P == 0) {
-        *num_rendered = 0;
+        host_count[0] = host_count[1] = 0;
         return LSR_OK;
     }
     lsr::PreprocessArgs a{};
@@ -303,12 +304,19 @@ int lsr_forward_preprocess(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_
         lsr::exclusive_scan_u32(g.counts, g.offsets, (size_t)P, g.total, g.scan_tmp, st);
     }
     LSR_LAUNCHED("instance scan", st, s->debug);
-    uint32_t tot[2] = {0, 0};
-    LSR_HIP(hipMemcpyAsync(tot, g.total, sizeof(tot), hipMemcpyDeviceToHost, st));
-    LSR_HIP(hipStreamSynchronize(st));
+    LSR_HIP(hipMemcpyAsync(host_count, g.total, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    return LSR_OK;
+}
+
+int lsr_forward_preprocess(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_out* out, void* geom,
+                           int64_t* num_rendered, lsr_stream_t stream) {
+    if (!num_rendered) return fail(LSR_EINVAL, "geom workspace and num_rendered are required");
+    uint32_t tot[2] = {0, 0};   // pageable: the copy completes by the synchronisation below
+    int rc = lsr_forward_preprocess_async(s, in, out, geom, tot, stream);
+    if (rc) return rc;
+    LSR_HIP(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
     if (tot[1]) return fail(LSR_EHIP, "depth sort: look-back timed out");
-    const uint32_t K = tot[0];
-    *num_rendered = (int64_t)K;
+    *num_rendered = (int64_t)tot[0];
     return LSR_OK;
 }
 
@@ -595,6 +603,12 @@ int lsr_mark_visible(int32_t P, const float* means3D, const float* viewmatrix, c
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     lsr::launch_mark_visible(P, means3D, viewmatrix, present, st);
     LSR_LAUNCHED("mark_visible", st, false);
+    return LSR_OK;
+}
+
+int lsr_profile_phases(uint32_t mask) {
+    std::lock_guard<std::mutex> l(g_prof.mu);
+    g_prof.mask = mask;
     return LSR_OK;
 }
 

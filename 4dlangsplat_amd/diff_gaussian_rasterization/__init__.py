@@ -109,6 +109,24 @@ class PendingForward:
         self.geom, self.radii, self.num_rendered, self.device, self.H, self.W = geom, radii, K, device, H, W
         self.binning = self.img = None     # set when the binning already ran (preprocess_native(binning=True))
         self.ready = None                  # event recorded after that binning
+        self.count_host = None             # deferred count (preprocess_native(defer_count=True)): pinned
+        self.counted = None                # [K, error word], valid once `counted` (an event) has passed
+        self.stream = None
+
+    def resolve(self, binning=False):
+        """Deferred-count forwards: wait for the instance count (host waits on the event only, not
+        the stream), then optionally enqueue the binning on the preprocess stream.  No-op otherwise."""
+        if self.counted is None:
+            return self
+        self.counted.synchronize()
+        self.counted = None
+        K, err = int(self.count_host[0]), int(self.count_host[1])
+        if err:
+            raise RuntimeError("lsr_forward_preprocess: depth sort: look-back timed out")
+        self.num_rendered = K
+        if binning:
+            _run_binning(self, self.stream)
+        return self
 
 
 def _dump_forward(raster_settings, inputs):
@@ -120,12 +138,17 @@ def _dump_forward(raster_settings, inputs):
 
 
 def preprocess_native(raster_settings, means3D, opacities, shs=None, colors_precomp=None, language_feature=None,
-                      scales=None, rotations=None, cov3D_precomp=None, stream=None, binning=False):
+                      scales=None, rotations=None, cov3D_precomp=None, stream=None, binning=False,
+                      defer_count=False):
     """Forward phase 1 through liblsr.so (lsr_forward_preprocess) on `stream` (a torch stream,
     default: the current one).  Synchronises that stream once to read num_rendered (as upstream).
     binning=True also runs the tile binning there (lsr_forward_binning), so that render_native
     only composites.  Workspaces are allocated on `stream`; render_native may run on another
-    stream."""
+    stream.
+
+    defer_count=True (lsr_forward_preprocess_async) does not synchronise: the count lands in pinned
+    host memory and PendingForward.resolve(binning) reads it later (render_native resolves too),
+    so a caller can enqueue this view's preprocess ahead of another view's work on the same stream."""
     device = means3D.device
     if device.type != "cuda":
         raise RuntimeError("the rasterizer runs on the GPU only (no CPU fallback); got tensors on " + str(device))
@@ -160,6 +183,22 @@ def preprocess_native(raster_settings, means3D, opacities, shs=None, colors_prec
         geom = torch.empty(int(L.lsr_geom_bytes(P)), dtype=torch.uint8, device=device)
     fout = _lib.FwdOut()
     fout.radii = radii.data_ptr()
+    if defer_count:
+        count = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+        try:
+            _lib.check(L.lsr_forward_preprocess_async(ctypes.byref(st.c), ctypes.byref(fin), ctypes.byref(fout),
+                                                      ctypes.c_void_p(geom.data_ptr()),
+                                                      ctypes.c_void_p(count.data_ptr()),
+                                                      ctypes.c_void_p(stream.cuda_stream)),
+                       "lsr_forward_preprocess_async")
+        except RuntimeError:
+            _dump_forward(raster_settings, inputs)
+            raise
+        pf = PendingForward(raster_settings, st, fin, inputs, geom, radii, None, device, H, W)
+        pf.count_host, pf.stream = count, stream
+        pf.counted = torch.cuda.Event()
+        pf.counted.record(stream)
+        return pf
     K = ctypes.c_int64(0)
     try:
         _lib.check(L.lsr_forward_preprocess(ctypes.byref(st.c), ctypes.byref(fin), ctypes.byref(fout),
@@ -170,29 +209,37 @@ def preprocess_native(raster_settings, means3D, opacities, shs=None, colors_prec
         raise
     pf = PendingForward(raster_settings, st, fin, inputs, geom, radii, K.value, device, H, W)
     if binning:
-        if _BINNING_DELAY_CYCLES:         # test hook: holds the binning back to expose missing waits
-            with torch.cuda.stream(stream):
-                torch.cuda._sleep(_BINNING_DELAY_CYCLES)
-        with torch.cuda.stream(stream):
-            pf.binning = torch.empty(int(L.lsr_binning_bytes(K.value)), dtype=torch.uint8, device=device)
-            pf.img = torch.empty(int(L.lsr_img_bytes(W, H)), dtype=torch.uint8, device=device)
-        try:
-            _lib.check(L.lsr_forward_binning(ctypes.byref(st.c), ctypes.byref(fin), ctypes.c_void_p(geom.data_ptr()),
-                                             ctypes.c_void_p(pf.binning.data_ptr()), ctypes.c_void_p(pf.img.data_ptr()),
-                                             ctypes.c_int64(K.value), ctypes.c_void_p(stream.cuda_stream)),
-                       "lsr_forward_binning")
-        except RuntimeError:
-            _dump_forward(raster_settings, inputs)
-            raise
-        pf.ready = torch.cuda.Event()
-        pf.ready.record(stream)           # render_native's stream waits for the binning
+        _run_binning(pf, stream)
     return pf
+
+
+def _run_binning(pf, stream):
+    """lsr_forward_binning of a preprocessed view on `stream`; render_native's stream waits for it."""
+    L = _lib.load()
+    device, H, W, K = pf.device, pf.H, pf.W, pf.num_rendered
+    if _BINNING_DELAY_CYCLES:             # test hook: holds the binning back to expose missing waits
+        with torch.cuda.stream(stream):
+            torch.cuda._sleep(_BINNING_DELAY_CYCLES)
+    with torch.cuda.stream(stream):
+        pf.binning = torch.empty(int(L.lsr_binning_bytes(K)), dtype=torch.uint8, device=device)
+        pf.img = torch.empty(int(L.lsr_img_bytes(W, H)), dtype=torch.uint8, device=device)
+    try:
+        _lib.check(L.lsr_forward_binning(ctypes.byref(pf.settings.c), ctypes.byref(pf.fin),
+                                         ctypes.c_void_p(pf.geom.data_ptr()), ctypes.c_void_p(pf.binning.data_ptr()),
+                                         ctypes.c_void_p(pf.img.data_ptr()), ctypes.c_int64(K),
+                                         ctypes.c_void_p(stream.cuda_stream)), "lsr_forward_binning")
+    except RuntimeError:
+        _dump_forward(pf.raster_settings, pf.inputs)
+        raise
+    pf.ready = torch.cuda.Event()
+    pf.ready.record(stream)               # render_native's stream waits for the binning
 
 
 def render_native(pending: PendingForward):
     """Forward phase 2 (binning unless preprocess_native already did it, then compositing) on the
     current stream.  Returns (color, language_feature, radii, depth, state)."""
     L = _lib.load()
+    pending.resolve()
     device, H, W, C = pending.device, pending.H, pending.W, pending.fin.C
     stream = torch.cuda.current_stream(device)
     pending.geom.record_stream(stream)    # allocated on the preprocess stream, used from here on

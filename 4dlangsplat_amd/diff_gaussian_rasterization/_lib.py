@@ -107,6 +107,9 @@ SIGNATURES = {
     "lsr_backward_bytes": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
     "lsr_forward_preprocess": (ctypes.c_int, [ctypes.POINTER(Settings), ctypes.POINTER(FwdIn), ctypes.POINTER(FwdOut),
                                               ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
+    "lsr_forward_preprocess_async": (ctypes.c_int, [ctypes.POINTER(Settings), ctypes.POINTER(FwdIn),
+                                                    ctypes.POINTER(FwdOut), ctypes.c_void_p, ctypes.c_void_p,
+                                                    ctypes.c_void_p]),
     "lsr_forward_render": (ctypes.c_int, [ctypes.POINTER(Settings), ctypes.POINTER(FwdIn), ctypes.POINTER(FwdOut),
                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                           ctypes.c_void_p]),
@@ -132,6 +135,7 @@ SIGNATURES = {
     "lsr_mark_visible": (ctypes.c_int, [ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p]),
     "lsr_profile_enable": (ctypes.c_int, [ctypes.c_int32]),
+    "lsr_profile_phases": (ctypes.c_int, [ctypes.c_uint32]),
     "lsr_knn_workspace_bytes": (ctypes.c_int64, [ctypes.c_int32]),
     "lsr_knn_mean_dist": (ctypes.c_int, [ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p]),
@@ -150,8 +154,11 @@ PHASES = ["preprocess", "depth_sort", "instance_scan", "emit", "tile_sort", "til
           "render_bwd", "preprocess_bwd", "preprocess_bwd_views"]
 
 
-def profile_enable(on=True):
-    load().lsr_profile_enable(1 if on else 0)
+def profile_enable(on=True, phases=None):
+    """Start (resetting the totals) or stop event timing; `phases` limits it to those names."""
+    L = load()
+    L.lsr_profile_phases(0xFFFFFFFF if phases is None else sum(1 << PHASES.index(p) for p in phases))
+    L.lsr_profile_enable(1 if on else 0)
 
 
 def profile_read():

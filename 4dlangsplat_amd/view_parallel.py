@@ -157,20 +157,27 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
     and its tile binning run on a side stream, concurrently with them, so the device never waits
     for the host between views and the main stream only composites.  Results are identical to
     the sequential order (preprocess and binning only read the Gaussians and write their own
-    workspaces)."""
+    workspaces).
+
+    overlap="lookahead" keeps ONE stream: view v+1's preprocess is enqueued ahead of view v's
+    compositing with its instance count copied to pinned memory (lsr_forward_preprocess_async);
+    the host waits for that count only (an event), while view v's compositing is still queued,
+    then enqueues view v+1's binning behind it.  No host gap between views and no contention
+    between the side chain and the compositors."""
     import diff_gaussian_rasterization as dgr
 
-    side = torch.cuda.Stream(device=scene.means3D.device) if overlap else None
+    lookahead = overlap == "lookahead"
+    side = torch.cuda.Stream(device=scene.means3D.device) if (overlap and not lookahead) else None
     pending = {}
-    params_ready = torch.cuda.Event() if overlap else None
+    params_ready = torch.cuda.Event() if side is not None else None
 
     def has_view(v):
         return v in settings if isinstance(settings, dict) else 0 <= v < len(settings)
 
-    def preprocess(v, stream=None):
+    def preprocess(v, stream=None, defer=False):
         return dgr.preprocess_native(settings[v], scene.means3D, scene.opacities, shs=scene.shs,
                                      language_feature=scene.lang, scales=scene.scales, rotations=scene.rotations,
-                                     stream=stream, binning=stream is not None)
+                                     stream=stream, binning=stream is not None, defer_count=defer)
 
     batched = batch_backward and not deterministic
     held = []                             # (state, dL_dcolor, dL_dlang, dL_ddepth) awaiting flush
@@ -181,6 +188,10 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
             pf = preprocess(v)
             if params_ready is not None:
                 params_ready.record(torch.cuda.current_stream())
+        if lookahead:
+            pf.resolve(binning=True)      # count of view v (enqueued a view earlier), then its binning
+            if has_view(v + 1):           # view v+1's preprocess ahead of view v's compositing
+                pending[v + 1] = preprocess(v + 1, defer=True)
         color, lang, radii, depth, st = dgr.render_native(pf)
         gc, gl, gd = grad_fn(v, color, lang, depth)
         if batched:                   # compositor backward now, preprocess backward at flush

@@ -11,8 +11,10 @@ once per step.  Upstream gradients dL/dcolor, dL/dlanguage are fixed seeded tens
 step is the rasterizer alone.  Inputs are resident in HBM before the timed region.
 
 value = frames (views) rendered fwd+bwd by all ranks / max over ranks of the timed wall time.
-roofline: the dominant kernel (largest event-timed phase), algorithmic bytes per launch (the
-per-phase formulas below) / its mean launch time (hipEvents on the launch stream).
+roofline: the dominant kernel (largest event-timed phase of one untimed all-phase step),
+algorithmic bytes per launch (the per-phase formulas below) / its mean launch time
+(hipEvents on the launch stream, recorded live over the timed region; only that phase carries
+events there, the per-phase breakdown comes from the untimed step).
 cpu_baseline: the C oracle (oracle/, OpenMP) on one headline frame fwd+bwd, rank 0 only.
 """
 import argparse
@@ -103,6 +105,9 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=3, help="headline frames timed on the CPU oracle")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-overlap", action="store_true", help="diagnostic: no side stream (uncontended phase times)")
+    ap.add_argument("--pipeline", choices=("lookahead", "side"), default="lookahead",
+                    help="view pipelining: next view's preprocess queued ahead on one stream with a deferred count "
+                         "(lookahead), or run on a side stream (side)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -137,7 +142,8 @@ def main():
     gcol = (torch.randn(3, H, W, generator=g) * 1e-3).to(dev)
     glang = (torch.randn(C, H, W, generator=g) * 1e-3).to(dev)
     render = native_view_renderer(scene, settings, lambda v, color, lang, depth: (gcol, glang, None),
-                                  overlap=not args.no_overlap)
+                                  overlap=False if args.no_overlap else ("lookahead" if args.pipeline == "lookahead"
+                                                                         else True))
     Ks = []
 
     def render_view(v, b):
@@ -153,10 +159,22 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    Ks.clear()
+    # per-phase breakdown: one untimed step with every phase event-timed; it also picks the
+    # dominant kernel (the single-kernel phase with the most time; multi-kernel phases such as the
+    # sorts cannot be matched to one rocprof kernel line)
+    prof_all, dom = {}, None
     if not args.no_profile:
         torch.cuda.synchronize(dev)
         _lib.profile_enable(True)
+        step()
+        torch.cuda.synchronize(dev)
+        prof_all = _lib.profile_read()
+        single = [k for k in ("render_bwd", "render_fwd", "preprocess", "preprocess_bwd_views", "preprocess_bwd",
+                              "emit", "tile_ranges") if prof_all.get(k, (0, 0))[1]]
+        dom = max(single, key=lambda k: prof_all[k][0])
+        # timed region: only the dominant kernel carries events (two records per launch)
+        _lib.profile_enable(True, phases=[dom])
+    Ks.clear()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -169,7 +187,7 @@ def main():
     elapsed = time.perf_counter() - t0
     prof = _lib.profile_read() if not args.no_profile else {}
     _lib.profile_enable(False)
-    if prof and prof["render_bwd"][1] != V * args.steps:   # every view's backward ran in the timed region
+    if dom == "render_bwd" and prof["render_bwd"][1] != V * args.steps:   # every view's backward ran, timed
         raise RuntimeError(f"expected {V * args.steps} backward launches, profiled {prof['render_bwd'][1]}")
     el = torch.tensor([elapsed], device=dev, dtype=torch.float64)
     if world > 1:
@@ -196,17 +214,11 @@ def main():
         roof = None
         phases = {}
         if prof:
-            for k, (ms, n) in prof.items():
+            for k, (ms, n) in prof_all.items():   # the untimed all-phase step
                 if n:
                     phases[k] = dict(mean_ms=ms / n, launches=n, gbs=phase_bytes(k, P, Pvis, Kmean, W * H, ntiles, C, M, **pb)
                                      / (ms / n * 1e-3) / 1e9)
-            # dominant kernel: the single-kernel phase with the most time (multi-kernel phases such as
-            # the sorts cannot be matched to one rocprof kernel line; side-stream phases' event times
-            # include waiting for CUs held by the compositors)
-            single = [k for k in ("render_bwd", "render_fwd", "preprocess", "preprocess_bwd_views", "preprocess_bwd",
-                                  "emit", "tile_ranges") if prof.get(k, (0, 0))[1]]
-            dom = max(single, key=lambda k: prof[k][0])
-            ms, n = prof[dom]
+            ms, n = prof[dom]                      # live, over the timed region
             byts = phase_bytes(dom, P, Pvis, Kmean, W * H, ntiles, C, M, **pb)
             ach = byts / (ms / n * 1e-3) / 1e9
             traffic = None
@@ -234,7 +246,7 @@ def main():
             vs_baseline=None, dtype="f32", data="synthetic",
             config=dict(workload="S2M synthetic (BASELINE configs[2] per GPU; configs[3] batch split)",
                         gaussians=P, width=W, height=H, channels=C, views_per_gpu_per_step=V,
-                        global_batch=world * V, parallelism=f"dp{world}", num_rendered_mean=int(Kmean),
+                        global_batch=world * V, parallelism=f"dp{world}", pipeline="none" if args.no_overlap else args.pipeline, num_rendered_mean=int(Kmean),
                         visible=Pvis, visible_any_view=Pany, grad_bucket_mb=round(bucket.nbytes / 2**20, 1)),
             roofline=roof, cpu_baseline=cpu,
             phases={k: dict(mean_ms=round(v["mean_ms"], 4), gbs=round(v["gbs"], 1)) for k, v in phases.items()},

@@ -119,6 +119,15 @@ int64_t lsr_backward_bytes(int32_t P, int64_t num_rendered, int32_t C, int32_t d
 int lsr_forward_preprocess(const lsr_settings *s, const lsr_fwd_in *in, lsr_fwd_out *out, void *geom,
                            int64_t *num_rendered, lsr_stream_t stream);
 
+/* lsr_forward_preprocess without the host synchronisation: the same launches, then an
+ * asynchronous copy of two words to `host_count` (page-locked host memory): [0] num_rendered,
+ * [1] nonzero if the depth sort's look-back timed out (results invalid).  Valid once the stream
+ * has passed this point (an event recorded after the call).  Lets a caller enqueue the next
+ * view's preprocess ahead of the current view's compositing on ONE stream and read the count
+ * later, so the device never idles on the host between views. */
+int lsr_forward_preprocess_async(const lsr_settings *s, const lsr_fwd_in *in, lsr_fwd_out *out, void *geom,
+                                 uint32_t *host_count, lsr_stream_t stream);
+
 /* Forward, phase 2: tile binning and compositing of RGB + C language channels + depth.
  * `geom` is the buffer phase 1 filled; `binning` holds >= lsr_binning_bytes(num_rendered) bytes. */
 int lsr_forward_render(const lsr_settings *s, const lsr_fwd_in *in, lsr_fwd_out *out, void *geom,
@@ -192,6 +201,9 @@ int lsr_mark_visible(int32_t P, const float *means3D, const float *viewmatrix, c
 #define LSR_PHASE_PREPROCESS_BWD_VIEWS 9   /* lsr_backward_views: one launch per <= 8 views */
 #define LSR_NUM_PHASES 10
 int lsr_profile_enable(int32_t on);   /* resets the totals */
+/* Which phases are timed while profiling is on: bit (1 << LSR_PHASE_*); default all.  Each timed
+ * phase adds two event records to its stream. */
+int lsr_profile_phases(uint32_t mask);
 int lsr_profile_read(double *ms_total, int64_t *launches, int32_t n);
 
 #ifdef __cplusplus

@@ -36,10 +36,13 @@ def _run(sc, settings, grads, overlap, deterministic):
     return b.flat.clone(), b.radii.clone()
 
 
-def test_pipelined_step_equals_sequential():
+@pytest.mark.parametrize("mode", [True, "lookahead"])
+def test_pipelined_step_equals_sequential(mode):
+    """Side-stream pipelining and the one-stream lookahead (deferred instance counts read from
+    pinned memory after an event) give the sequential result bit for bit."""
     sc, settings, grads = _setup()
     f0, r0 = _run(sc, settings, grads, overlap=False, deterministic=True)
-    f1, r1 = _run(sc, settings, grads, overlap=True, deterministic=True)
+    f1, r1 = _run(sc, settings, grads, overlap=mode, deterministic=True)
     assert torch.equal(f0, f1) and torch.equal(r0, r1)
     assert float(f0.abs().sum()) > 0 and int((r0 > 0).sum()) > 0
 
@@ -54,9 +57,10 @@ def test_pipelined_step_waits_for_side_stream_binning(monkeypatch):
     assert torch.equal(f0, f1) and torch.equal(r0, r1)
 
 
-def test_bucket_is_sum_of_views():
+@pytest.mark.parametrize("mode", [True, "lookahead"])
+def test_bucket_is_sum_of_views(mode):
     sc, settings, grads = _setup(n_views=3)
-    flat, radii = _run(sc, settings, grads, overlap=True, deterministic=False)
+    flat, radii = _run(sc, settings, grads, overlap=mode, deterministic=False)
     b = GradBucket(sc.means3D.shape[0], sc.shs.shape[1], sc.lang.shape[1], "cuda", densify_stats=True)
     ref = torch.zeros_like(b.flat)
     rmax = torch.zeros_like(radii)
