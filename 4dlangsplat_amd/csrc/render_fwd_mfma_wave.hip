@@ -94,15 +94,25 @@ __global__ void __launch_bounds__(64) k_render_fwd_wave_mfma(RenderFwdArgs a) {
 
     uint32_t pos = range.x;  // list entries [pos, range.y) not yet scanned
     int head = 0, tail = 0;  // FIFO counters (wave-uniform)
-    uint32_t gid_next = pos + lane < range.y ? a.point_list[pos + lane] : 0u;
+    // scan prefetch: centres and conics of the round at pos, ids of the round after it (so a
+    // round's geometry loads are issued a round, and its id loads two rounds, before use)
+    uint32_t gid_c = pos + lane < range.y ? a.point_list[pos + lane] : 0u;
+    float2 xy_c = make_float2(0.0f, 0.0f);
+    float4 co_c = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (pos + lane < range.y) { xy_c = a.xy[gid_c]; co_c = a.conic_o[gid_c]; }
+    uint32_t gid_n = pos + 64 + lane < range.y ? a.point_list[pos + 64 + lane] : 0u;
     while (!__all(done)) {
         // ---- 1. scan + compaction (as k_render_fwd_wave) --------------------------------------
         while (tail - head < MG && pos < range.y) {
             const uint32_t idx = pos + lane;
-            const uint32_t gid = gid_next;
-            gid_next = idx + 64 < range.y ? a.point_list[idx + 64] : 0u;
+            const uint32_t gid = gid_c;
+            const float2 xy = xy_c;
+            const float4 co = co_c;
+            gid_c = gid_n;
+            if (idx + 64 < range.y) { xy_c = a.xy[gid_c]; co_c = a.conic_o[gid_c]; }
+            gid_n = idx + 128 < range.y ? a.point_list[idx + 128] : 0u;
             bool cand = false;
-            if (idx < range.y) cand = quad_may_touch(a.xy[gid], a.conic_o[gid], bx0, bx1, by0, by1);
+            if (idx < range.y) cand = quad_may_touch(xy, co, bx0, bx1, by0, by1);
             const uint64_t m = __ballot(cand);
             if (cand) {
                 const int s = (tail + __popcll(m & lanemask_lt())) & (MFIFO - 1);
