@@ -73,6 +73,15 @@ class GradBucket:
         if self.radii is not None:
             self.radii.zero_()
 
+    def zero_accumulated_(self):
+        """Zero only what the views accumulate into (language gradients, radii): for a batched
+        flush that overwrites every other field."""
+        lo, hi = self.ranges["language_feature"]
+        if hi > lo:
+            self.flat[lo:hi].zero_()
+        if self.radii is not None:
+            self.radii.zero_()
+
     def need(self) -> Dict[str, bool]:
         """The `need` mask for backward_native: only the bucket's fields are produced."""
         return dict(means3D=True, scales=True, rotations=True, opacities=True, sh=self.M > 0,
@@ -102,12 +111,15 @@ class ViewParallelStep:
 
     def run(self, render_view: Callable[[int, GradBucket], Optional[torch.Tensor]]) -> GradBucket:
         b = self.bucket
-        b.zero_()
+        flush = getattr(render_view, "flush", None)
+        if getattr(flush, "overwrites", False):
+            b.zero_accumulated_()        # the flush writes every other field (HBM write saved)
+        else:
+            b.zero_()
         for v in self.views:
             radii = render_view(v, b)
             if b.radii is not None and radii is not None:
                 torch.maximum(b.radii, radii.to(torch.int32), out=b.radii)
-        flush = getattr(render_view, "flush", None)
         early = None
         lo, hi = b.ranges["language_feature"]
         if self.world > 1 and flush is not None and hi > lo:
@@ -206,9 +218,17 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
         return radii
 
     def flush(bucket: GradBucket):
+        # overwrites every field but the language gradients (all P rows, culled ones with zeros), so
+        # ViewParallelStep zeroes only the accumulated fields before the views
         if held:
-            dgr.backward_preprocess_views_native(held, out=bucket.views, accumulate=True, need=bucket.need())
+            dgr.backward_preprocess_views_native(held, out=bucket.views, accumulate=False, need=bucket.need())
             held.clear()
+        else:                             # no views on this rank this step
+            lo, hi = bucket.ranges["language_feature"]
+            bucket.flat[:lo].zero_()
+            bucket.flat[hi:].zero_()
+
+    flush.overwrites = True
 
     render_view.last_num_rendered = 0
     if batched:

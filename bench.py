@@ -59,8 +59,9 @@ def phase_bytes(phase, P, Pvis, K, npix, ntiles, C, M=16, accumulate=True, V=1, 
         grads = 4 * (3 + 3 + 4 + 1 + 3 * M)
         return P * 4 + Pvis * (12 + 12 + 16 + 4 * 3 * M + 1 + 48) + (2 * Pvis * grads if accumulate else P * grads)
     if phase == "preprocess_bwd_views":    # per view: tiles, and for its visible rows clamped + screen sums;
-        grads = 4 * (3 + 3 + 4 + 1 + 3 * M)  # once: Gaussian rows of the visible-anywhere set, gradient RMW
-        return V * P * 4 + Pvis_sum * (1 + 48) + Pany * (12 + 12 + 16 + 4 * 3 * M) + 2 * Pany * grads
+        grads = 4 * (3 + 3 + 4 + 1 + 3 * M)  # once: Gaussian rows of the visible-anywhere set; gradient rows
+        return (V * P * 4 + Pvis_sum * (1 + 48) + Pany * (12 + 12 + 16 + 4 * 3 * M)   # RMW, or all P written
+                + (2 * Pany * grads if accumulate else P * grads))
     return 0
 
 
@@ -209,7 +210,8 @@ def main():
                 if v == dp.views[0]:
                     Pvis = int((radii > 0).sum())
             Pany = int(any_vis.sum())
-        pb = dict(V=len(dp.views), Pvis_sum=vis_sum, Pany=Pany)
+        pb = dict(V=len(dp.views), Pvis_sum=vis_sum, Pany=Pany,
+                  accumulate=not getattr(getattr(render, "flush", None), "overwrites", False))
         ntiles = ((W + 15) // 16) * ((H + 15) // 16)
         roof = None
         phases = {}

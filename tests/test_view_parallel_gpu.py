@@ -25,12 +25,15 @@ def _setup(n_views=4, P=20000, W=160, H=120, C=32):
     return sc, settings, grads
 
 
-def _run(sc, settings, grads, overlap, deterministic):
+def _run(sc, settings, grads, overlap, deterministic, prefill=None):
     b = GradBucket(sc.means3D.shape[0], sc.shs.shape[1], sc.lang.shape[1], "cuda", densify_stats=True)
     step = ViewParallelStep(b, len(settings))
     r = native_view_renderer(sc, settings, lambda v, c, l, d: (grads[v][0], grads[v][1], None),
                              deterministic=deterministic, overlap=overlap)
     for _ in range(2):   # second step exercises the pipeline with warm streams and caches
+        if prefill is not None:   # whatever the step does not zero or write shows up
+            b.flat.fill_(prefill)
+            b.radii.fill_(-1)
         step.run(r)
     torch.cuda.synchronize()
     return b.flat.clone(), b.radii.clone()
@@ -60,7 +63,10 @@ def test_pipelined_step_waits_for_side_stream_binning(monkeypatch):
 @pytest.mark.parametrize("mode", [True, "lookahead"])
 def test_bucket_is_sum_of_views(mode):
     sc, settings, grads = _setup(n_views=3)
-    flat, radii = _run(sc, settings, grads, overlap=mode, deterministic=False)
+    # batched backward: the flush overwrites every field but the language gradients, which are
+    # the only ones zeroed before the views; NaN-filled buckets prove every row is written
+    flat, radii = _run(sc, settings, grads, overlap=mode, deterministic=False, prefill=float("nan"))
+    assert not torch.isnan(flat).any()
     b = GradBucket(sc.means3D.shape[0], sc.shs.shape[1], sc.lang.shape[1], "cuda", densify_stats=True)
     ref = torch.zeros_like(b.flat)
     rmax = torch.zeros_like(radii)
