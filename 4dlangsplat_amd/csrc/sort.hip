@@ -118,6 +118,9 @@ void exclusive_scan_u32(const uint32_t* in, uint32_t* out, size_t n, uint32_t* t
 #define LSR_OS_ITEMS 16
 #endif
 constexpr int OS_ITEMS = LSR_OS_ITEMS;   // keys per thread per pass
+#ifndef LSR_LOOKBACK
+#define LSR_LOOKBACK 4   // predecessors read per look-back round trip (1..32 swept: 4 best)
+#endif
 constexpr int OS_TILE = 256 * OS_ITEMS;       // keys per block
 constexpr uint32_t OS_AGG = 1u << 30, OS_PRE = 2u << 30, OS_CNT = (1u << 30) - 1u;
 
@@ -253,12 +256,12 @@ __global__ void __launch_bounds__(256) k_radix_pass(const uint32_t* __restrict__
         __hip_atomic_store(st + tid, OS_PRE | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
         __hip_atomic_store(st + (size_t)bid * 256 + tid, OS_AGG | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // window of 8 predecessors per round trip, nearest first; stop at an inclusive prefix,
+        // window of LSR_LOOKBACK predecessors per round trip, nearest first; stop at an inclusive prefix,
         // resume at the first one not published yet.  Block 0 always publishes a prefix.
         uint32_t p = bid;   // predecessors p-1, p-2, ... not consumed yet
         uint32_t spins = 0;
         while (true) {
-            constexpr int LB = 8;
+            constexpr int LB = LSR_LOOKBACK;
             uint32_t v[LB];
 #pragma unroll
             for (int j = 0; j < LB; ++j)
