@@ -126,15 +126,8 @@ __global__ void __launch_bounds__(64) k_render_fwd_wave_mfma(RenderFwdArgs a) {
         if (cnt == 0) break;
         wave_lds_sync();
         // ---- 2. stage the group: geometry, and the language rows as bf16 hi / lo -------------
-        if (lane < MG) {
-            const bool ok = lane < cnt;
-            const int s = (head + lane) & (MFIFO - 1);
-            const uint32_t gid = ok ? s_fg[s] : 0u;
-            s_k[lane] = ok ? s_fk[s] : 0u;
-            s_xy[lane] = ok ? a.xy[gid] : make_float2(0.0f, 0.0f);
-            s_co[lane] = ok ? a.conic_o[gid] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            s_rgbd[lane] = ok ? a.rgbd[gid] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        }
+        // every gather of the group is issued before the first LDS store (one memory latency per
+        // group instead of three in sequence)
         {
             // lane -> entry lane / 2, channels 16 (lane & 1) .. +15: four float4 loads in flight
             const int e = lane >> 1, c0 = 16 * (lane & 1);
@@ -144,13 +137,28 @@ __global__ void __launch_bounds__(64) k_render_fwd_wave_mfma(RenderFwdArgs a) {
             if (C == 32) {
                 const float4* r = reinterpret_cast<const float4*>(a.lang + (size_t)gid * 32 + c0);
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const float4 v = ok ? r[q] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                for (int q = 0; q < 4; ++q) {   // unmasked (gid 0 is a valid row), zeroed after
+                    const float4 v = r[q];
                     f[4 * q] = v.x; f[4 * q + 1] = v.y; f[4 * q + 2] = v.z; f[4 * q + 3] = v.w;
                 }
             } else {
 #pragma unroll
                 for (int j = 0; j < 16; ++j) f[j] = (ok && c0 + j < C) ? a.lang[(size_t)gid * C + c0 + j] : 0.0f;
+            }
+            float2 g_xy = make_float2(0.0f, 0.0f);
+            float4 g_co = make_float4(0.0f, 0.0f, 0.0f, 0.0f), g_rgbd = g_co;
+            uint32_t g_k = 0u;
+            if (lane < MG && lane < cnt) {
+                const int s = (head + lane) & (MFIFO - 1);
+                const uint32_t gid = s_fg[s];
+                g_k = s_fk[s];
+                g_xy = a.xy[gid];
+                g_co = a.conic_o[gid];
+                g_rgbd = a.rgbd[gid];
+            }
+            if (C == 32) {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) f[j] = ok ? f[j] : 0.0f;
             }
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
@@ -164,6 +172,12 @@ __global__ void __launch_bounds__(64) k_render_fwd_wave_mfma(RenderFwdArgs a) {
                 }
                 *reinterpret_cast<bf16x8*>(s_Fh + e * MFP + c0 + 8 * h) = vh;
                 *reinterpret_cast<bf16x8*>(s_Fl + e * MFP + c0 + 8 * h) = vl;
+            }
+            if (lane < MG) {
+                s_k[lane] = g_k;
+                s_xy[lane] = g_xy;
+                s_co[lane] = g_co;
+                s_rgbd[lane] = g_rgbd;
             }
         }
         head += cnt;
