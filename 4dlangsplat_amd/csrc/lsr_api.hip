@@ -5,6 +5,7 @@
 // Backward = composite backward (per-Gaussian screen-space sums) -> preprocess backward.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -18,6 +19,7 @@
 namespace {
 
 thread_local std::string g_err;
+std::atomic<uint32_t> g_inject_sort_fault{0};   // lsr_test_inject_sort_fault
 
 int fail(int code, const std::string& msg) {
     g_err = msg;
@@ -277,13 +279,13 @@ int lsr_forward_preprocess_async(const lsr_settings* s, const lsr_fwd_in* in, ls
     a.clamped = g.clamped;
     // the preprocess also writes the depth sort's initial values (ids), zeroes the split-backward
     // accumulator rows of listed Gaussians, and clears the sort workspace and the counters
-    // [0] K, [1] sort error word: no separate fill launches
+    // [0] K, [1] depth sort error word, [2] tile sort error word: no separate fill launches
     a.order = g.val_a;
     a.acc = g.acc;
     a.clear.p[0] = reinterpret_cast<uint32_t*>(g.sort_tmp);
     a.clear.n[0] = (uint32_t)(lsr::radix_temp_zero_bytes((size_t)P, 0, 32) / 4);
     a.clear.p[1] = g.total;
-    a.clear.n[1] = 2;
+    a.clear.n[1] = 3;
     {
         PhaseTimer t(LSR_PHASE_PREPROCESS, st);
         lsr::launch_preprocess(a, st);
@@ -297,6 +299,7 @@ int lsr_forward_preprocess_async(const lsr_settings* s, const lsr_fwd_in* in, ls
                                      /*temp_zeroed=*/true);
     }
     if (in_b != (bool)depth_sort_result_in_b()) return fail(LSR_EHIP, "internal: depth sort parity");
+    if (g_inject_sort_fault.load() & 1u) LSR_HIP(hipMemsetAsync(g.total + 1, 1, 1, st));   // test hook
     LSR_LAUNCHED("depth sort", st, s->debug);
     {
         PhaseTimer t(LSR_PHASE_INSTANCE_SCAN, st);
@@ -354,10 +357,13 @@ int lsr_forward_binning(const lsr_settings* s, const lsr_fwd_in* in, void* geom,
         bool in_b;
         {
             PhaseTimer t(LSR_PHASE_TILE_SORT, st);
+            // error word g.total[2] (cleared by the preprocess): the compositor poisons its outputs
+            // and lsr_forward_status reports it
             in_b = lsr::radix_sort_pairs(b.key_a, b.val_a, b.key_b, b.val_b, K, 0, tile_bits(gx * gy), b.sort_tmp,
-                                         nullptr, st, /*temp_zeroed=*/true);
+                                         g.total + 2, st, /*temp_zeroed=*/true);
         }
         if (in_b != tile_sort_in_b(gx * gy)) return fail(LSR_EHIP, "internal: tile sort parity");
+        if (g_inject_sort_fault.load() & 2u) LSR_HIP(hipMemsetAsync(g.total + 2, 1, 1, st));   // test hook
         const uint32_t* keys = in_b ? b.key_b : b.key_a;
         LSR_LAUNCHED("tile sort", st, s->debug);
         {
@@ -389,6 +395,13 @@ int lsr_forward_composite(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_o
     r.ranges = m.ranges; r.point_list = point_list; r.xy = g.xy; r.conic_o = g.conic_o; r.rgbd = g.rgbd;
     r.lang = in->language_feature; r.bg = s->bg; r.final_T = m.final_T; r.n_contrib = m.n_contrib;
     r.tile_max_contrib = m.tile_max; r.tile_order = m.tile_order;
+    r.sort_err = P > 0 ? g.total + 1 : nullptr;
+    if (out->host_sort_status) {
+        void* dptr = nullptr;
+        if (hipHostGetDevicePointer(&dptr, out->host_sort_status, 0) != hipSuccess || !dptr)
+            return fail(LSR_EINVAL, "host_sort_status must be page-locked host memory");
+        r.status_out = static_cast<uint32_t*>(dptr);
+    }
     r.out_color = out->out_color; r.out_lang = out->out_language_feature;
     r.out_depth = out->out_depth;
     if (C > 0 && !s->include_feature)
@@ -398,6 +411,23 @@ int lsr_forward_composite(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_o
         lsr::launch_render_fwd(r, st);
     }
     LSR_LAUNCHED("render forward", st, s->debug);
+    return LSR_OK;
+}
+
+int lsr_forward_status(int32_t P, const void* geom, uint32_t* host_status, lsr_stream_t stream) {
+    if (P < 0 || !geom || !host_status) return fail(LSR_EINVAL, "bad lsr_forward_status arguments");
+    if (P == 0) {
+        host_status[0] = host_status[1] = 0;
+        return LSR_OK;
+    }
+    Geom g = carve_geom(const_cast<void*>(geom), (size_t)P, nullptr);
+    LSR_HIP(hipMemcpyAsync(host_status, g.total + 1, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                           reinterpret_cast<hipStream_t>(stream)));
+    return LSR_OK;
+}
+
+int lsr_test_inject_sort_fault(uint32_t mask) {
+    g_inject_sort_fault.store(mask & 3u);
     return LSR_OK;
 }
 

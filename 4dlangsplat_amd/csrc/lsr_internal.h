@@ -131,6 +131,9 @@ struct RenderFwdArgs {
     uint32_t* n_contrib;
     uint32_t* tile_max_contrib;   // per tile: max n_contrib over its pixels (bounds the backward replay)
     uint32_t* tile_order;         // [tiles] scratch: longest-list-first launch order (null: tile order)
+    const uint32_t* sort_err;     // [2] depth / tile sort look-back timeouts (null: none): NaN outputs
+    uint32_t* status_out;         // [2] host-mapped (device address of pinned memory) or null: block 0
+                                  //     stores sort_err there
     float* out_color;
     float* out_lang;
     float* out_depth;

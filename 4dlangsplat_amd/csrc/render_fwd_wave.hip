@@ -38,6 +38,8 @@ __global__ void __launch_bounds__(64) k_render_fwd_wave(RenderFwdArgs a) {
     const bool inside = px < a.W && py < a.H;
     const float pxf = (float)px, pyf = (float)py;
     const uint2 range = a.ranges[tile];
+    const uint32_t sort_err = a.sort_err ? (a.sort_err[0] | a.sort_err[1]) : 0u;
+    if (a.status_out && b == 0 && lane < 2) a.status_out[lane] = a.sort_err ? a.sort_err[lane] : 0u;
     const int C = a.C;
     const float bx0 = (float)qx0, bx1 = (float)min(qx0 + 7, a.W - 1);
     const float by0 = (float)qy0, by1 = (float)min(qy0 + 7, a.H - 1);
@@ -172,6 +174,12 @@ __global__ void __launch_bounds__(64) k_render_fwd_wave(RenderFwdArgs a) {
             if (__all(done)) break;
         }
         wave_lds_sync();
+    }
+    if (sort_err) {   // a sort's look-back timed out: the lists are invalid, make every output NaN
+        const float nan = __builtin_nanf("");
+        T = accD = acc[0] = acc[1] = acc[2] = nan;
+#pragma unroll
+        for (int c = 0; c < LP; ++c) accL[c] = nan;
     }
     if (inside) {
         const size_t HW = (size_t)a.H * a.W, pid = (size_t)py * a.W + px;

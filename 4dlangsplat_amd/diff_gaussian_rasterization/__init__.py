@@ -88,12 +88,31 @@ class _NativeSettings:
 
 
 class RasterizerState:
-    """What the forward leaves for the backward (upstream: num_rendered + geom/binning/img buffers)."""
+    """What the forward leaves for the backward (upstream: num_rendered + geom/binning/img buffers).
 
-    def __init__(self, settings, inputs, fin, geom, binning, img, num_rendered, radii):
+    sort_status: the forward's sort status words (lsr_forward_status, pinned host memory) and the
+    event after which they are valid; check_sorts() raises if a sort's look-back timed out (the
+    compositor has then already written NaN outputs).  Every backward entry point checks it, which
+    costs no wait: the forward finished long before its backward is enqueued behind it."""
+
+    def __init__(self, settings, inputs, fin, geom, binning, img, num_rendered, radii, sort_status=None):
         self.settings, self.inputs, self.fin = settings, inputs, fin
         self.geom, self.binning, self.img = geom, binning, img
         self.num_rendered, self.radii = num_rendered, radii
+        self.sort_status = sort_status    # (pinned int32 [2], event) or None
+        self.composited = False           # backward_composite_native ran (it may run once)
+
+    def check_sorts(self):
+        if self.sort_status is None:
+            return self
+        words, ev = self.sort_status
+        ev.synchronize()
+        self.sort_status = None
+        bad = [name for name, w in zip(("depth sort", "tile sort"), words.tolist()) if w]
+        if bad:
+            raise RuntimeError("rasterizer forward: " + " and ".join(bad) + " look-back timed out "
+                               "(outputs are NaN; this forward cannot be backpropagated)")
+        return self
 
 
 def _stream(device):
@@ -250,6 +269,8 @@ def render_native(pending: PendingForward):
     fout = _lib.FwdOut()
     fout.out_color, fout.out_language_feature = color.data_ptr(), _ptr(lang_out) if C > 0 else None
     fout.radii, fout.out_depth = pending.radii.data_ptr(), depth.data_ptr()
+    status = torch.zeros(2, dtype=torch.int32, pin_memory=True)   # the compositor writes the sort status here
+    fout.host_sort_status = status.data_ptr()
     K = pending.num_rendered
     binned = pending.binning is not None
     if binned:
@@ -269,7 +290,12 @@ def render_native(pending: PendingForward):
     except RuntimeError:
         _dump_forward(pending.raster_settings, pending.inputs)
         raise
-    state = RasterizerState(pending.settings, pending.inputs, pending.fin, pending.geom, binning, img, K, pending.radii)
+    ev = torch.cuda.Event()
+    ev.record(stream)
+    state = RasterizerState(pending.settings, pending.inputs, pending.fin, pending.geom, binning, img, K, pending.radii,
+                            sort_status=(status, ev))
+    if pending.raster_settings.debug:
+        state.check_sorts()
     return color, lang_out, pending.radii, depth, state
 
 
@@ -288,6 +314,7 @@ def backward_native(state: RasterizerState, grad_color, grad_lang=None, grad_dep
     accumulate=True they are added to.  deterministic=True selects the fixed-order reduction
     (bitwise reproducible gradients).  Returns the dict of gradient tensors."""
     L = _lib.load()
+    state.check_sorts()
     inp = state.inputs
     means3D = inp["means3D"]
     device = means3D.device
@@ -352,6 +379,11 @@ def backward_views_native(states, grad_colors, grad_langs=None, grad_depths=None
     n = len(states)
     if n == 0:
         raise ValueError("backward_views_native needs at least one view")
+    for s in states:
+        if s.composited:
+            raise RuntimeError("a view's forward was already backpropagated through its workspace accumulators "
+                               "(backward_composite_native / backward_views_native run once per forward)")
+        s.check_sorts()
     st0 = states[0]
     inp = st0.inputs
     for s in states[1:]:
@@ -411,6 +443,8 @@ def backward_views_native(states, grad_colors, grad_langs=None, grad_depths=None
     K = (ctypes.c_int64 * n)(*[s.num_rendered for s in states])
     _lib.check(L.lsr_backward_views(n, s_arr, ctypes.byref(st0.fin), g_arr, ctypes.byref(gout), geom, binning, img,
                                     K, 1 if accumulate else 0, _stream(device)), "lsr_backward_views")
+    for s in states:
+        s.composited = True
     return g
 
 
@@ -429,6 +463,10 @@ def backward_composite_native(state: RasterizerState, grad_color, grad_lang=None
     stream: the compositor backward; the language gradient is ADDED to dL_dlanguage [P,C] (the
     caller zeroes it once per batch).  Finish a batch with backward_preprocess_views_native."""
     L = _lib.load()
+    if state.composited:
+        raise RuntimeError("backward_composite_native already ran on this forward: its screen-space sums are "
+                           "accumulated in the forward's workspace, so a second run would double them")
+    state.check_sorts()
     device = state.inputs["means3D"].device
     P, C = state.fin.P, state.fin.C
     H, W = state.settings.c.image_height, state.settings.c.image_width
@@ -446,6 +484,7 @@ def backward_composite_native(state: RasterizerState, grad_color, grad_lang=None
                                         ctypes.c_void_p(state.binning.data_ptr()),
                                         ctypes.c_void_p(state.img.data_ptr()),
                                         ctypes.c_int64(state.num_rendered), _stream(device)), "lsr_backward_composite")
+    state.composited = True
     return CompositeGrad(state, (gc, gl, gd))
 
 

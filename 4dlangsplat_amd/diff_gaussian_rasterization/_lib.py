@@ -37,7 +37,7 @@ class FwdIn(ctypes.Structure):
 
 class FwdOut(ctypes.Structure):
     _fields_ = [("out_color", ctypes.c_void_p), ("out_language_feature", ctypes.c_void_p),
-                ("radii", ctypes.c_void_p), ("out_depth", ctypes.c_void_p)]
+                ("radii", ctypes.c_void_p), ("out_depth", ctypes.c_void_p), ("host_sort_status", ctypes.c_void_p)]
 
 
 class BwdIn(ctypes.Structure):
@@ -118,6 +118,8 @@ SIGNATURES = {
     "lsr_forward_composite": (ctypes.c_int, [ctypes.POINTER(Settings), ctypes.POINTER(FwdIn), ctypes.POINTER(FwdOut),
                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                              ctypes.c_void_p]),
+    "lsr_forward_status": (ctypes.c_int, [ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "lsr_test_inject_sort_fault": (ctypes.c_int, [ctypes.c_uint32]),
     "lsr_backward": (ctypes.c_int, [ctypes.POINTER(Settings), ctypes.POINTER(FwdIn), ctypes.POINTER(BwdIn),
                                     ctypes.POINTER(BwdOut), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p]),

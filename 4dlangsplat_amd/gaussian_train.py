@@ -263,8 +263,11 @@ class GaussianTrainer:
     @torch.no_grad()
     def reset_opacity(self):
         """gaussian_model.py:391-394: opacity <- inverse_sigmoid(min(sigmoid(opacity), 0.01)), its
-        Adam moments zeroed (replace_tensor_to_optimizer, :446-459)."""
+        Adam moments zeroed (replace_tensor_to_optimizer, :446-459).  Like the fresh nn.Parameter
+        the reference installs there, the group has no gradient afterwards (a following step()
+        skips it)."""
         n = "opacity"
+        self.params[n].grad = None
         _lib.check(self._L.lsr_reset_opacity(self.P, _ptr(self.params[n]), _ptr(self.exp_avg[n]),
                                              _ptr(self.exp_avg_sq[n]), _stream(self.device)), "lsr_reset_opacity")
 

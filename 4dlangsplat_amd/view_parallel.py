@@ -111,6 +111,9 @@ class ViewParallelStep:
 
     def run(self, render_view: Callable[[int, GradBucket], Optional[torch.Tensor]]) -> GradBucket:
         b = self.bucket
+        begin = getattr(render_view, "begin_step", None)
+        if begin is not None:             # the renderer may look ahead only within this rank's views
+            begin(self.views)
         flush = getattr(render_view, "flush", None)
         if getattr(flush, "overwrites", False):
             b.zero_accumulated_()        # the flush writes every other field (HBM write saved)
@@ -129,6 +132,9 @@ class ViewParallelStep:
             early = dist.all_reduce(b.flat[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         if flush is not None:        # renderers that batch the backward over the rank's views
             flush(b)
+        end = getattr(render_view, "end_step", None)
+        if end is not None:
+            end()
         if self.world > 1:
             if early is None:
                 dist.all_reduce(b.flat, op=dist.ReduceOp.SUM, group=self.group)
@@ -182,8 +188,13 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
     side = torch.cuda.Stream(device=scene.means3D.device) if (overlap and not lookahead) else None
     pending = {}
     params_ready = torch.cuda.Event() if side is not None else None
+    step_views = [None]                   # this rank's views of the current step (begin_step)
 
     def has_view(v):
+        """v+1 is prefetched only if THIS rank renders it in this step: with list settings and
+        world > 1 the next index may be the next rank's first view."""
+        if step_views[0] is not None and v not in step_views[0]:
+            return False
         return v in settings if isinstance(settings, dict) else 0 <= v < len(settings)
 
     def preprocess(v, stream=None, defer=False):
@@ -230,6 +241,17 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
 
     flush.overwrites = True
 
+    def begin_step(views):
+        pending.clear()
+        step_views[0] = range(views.start, views.stop) if isinstance(views, range) else list(views)
+
+    def end_step():
+        pending.clear()                   # nothing is carried across steps (the Gaussians change)
+        step_views[0] = None
+
+    render_view.begin_step = begin_step
+    render_view.end_step = end_step
+    render_view.pending = pending         # inspection (tests)
     render_view.last_num_rendered = 0
     if batched:
         render_view.flush = flush

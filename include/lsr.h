@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define LSR_API_VERSION 1
+#define LSR_API_VERSION 2   /* 2: lsr_fwd_out.host_sort_status, lsr_forward_status */
 
 #define LSR_OK 0
 #define LSR_EINVAL 1     /* bad argument (null pointer, exactly-one-of violation, size) */
@@ -82,6 +82,11 @@ typedef struct lsr_fwd_out {
     float *out_language_feature;      /* [C,H,W] (may be NULL when C == 0) */
     int32_t *radii;                   /* [P] */
     float *out_depth;                 /* [1,H,W] */
+    uint32_t *host_sort_status;       /* optional, [2] PAGE-LOCKED HOST memory (hipHostMalloc /
+                                         torch pin_memory): the compositor writes the sort status
+                                         words of lsr_forward_status there itself (no copy, no
+                                         launch); valid once the stream has passed the composite.
+                                         NULL: not reported. */
 } lsr_fwd_out;
 
 typedef struct lsr_bwd_in {
@@ -143,6 +148,19 @@ int lsr_forward_binning(const lsr_settings *s, const lsr_fwd_in *in, void *geom,
 int lsr_forward_composite(const lsr_settings *s, const lsr_fwd_in *in, lsr_fwd_out *out, const void *geom,
                           const void *binning, void *img, int64_t num_rendered, lsr_stream_t stream);
 
+/* Sort status of the forward whose phase 1 filled `geom` (P Gaussians): an asynchronous copy of two
+ * words to `host_status` (valid once the stream has passed this point): [0] nonzero if the depth
+ * sort's look-back timed out, [1] the same for the tile sort.  A bounded look-back spin never
+ * hangs; on a timeout the sorted lists are invalid, and the compositor then writes NaN to every
+ * output pixel (colour, language, depth, final T) so that the failure cannot pass silently.
+ * lsr_forward_preprocess reports [0] itself.  The same words reach the host without a copy through
+ * lsr_fwd_out.host_sort_status (a stream-ordered copy per view costs ~25 us on MI355X). */
+int lsr_forward_status(int32_t P, const void *geom, uint32_t *host_status, lsr_stream_t stream);
+
+/* Test hook: the next forwards' sorts report a look-back timeout as if their spin had run out
+ * (bit 0: depth sort, bit 1: tile sort; 0 restores normal operation).  Per process. */
+int lsr_test_inject_sort_fault(uint32_t mask);
+
 /* Backward through compositing and preprocess.  accumulate != 0 adds into the outputs instead of
  * overwriting them (multi-view gradient accumulation).  `scratch` holds >= lsr_backward_bytes. */
 int lsr_backward(const lsr_settings *s, const lsr_fwd_in *in, const lsr_bwd_in *gin, lsr_bwd_out *gout,
@@ -169,9 +187,10 @@ int lsr_backward_views(int32_t n_views, const lsr_settings *const *s, const lsr_
  * upstream gradients exist (and overlap the next view's preprocess on another stream), while the
  * preprocess backward still runs once per batch:
  *  - lsr_backward_composite: compositor backward of ONE view; its per-Gaussian screen-space sums
- *    are added to accumulator rows in `geom` (zeroed by lsr_forward_preprocess: call once per
- *    forward), its language gradients are ADDED to dL_dlanguage [P,C] (zero it first; NULL skips
- *    them).  Float atomics only.
+ *    are added to accumulator rows in `geom` (zeroed by lsr_forward_preprocess), so it runs EXACTLY
+ *    ONCE per forward: a second call on the same forward state doubles every screen-space sum the
+ *    preprocess backward consumes (the Python wrapper raises on reuse).  Its language gradients are
+ *    ADDED to dL_dlanguage [P,C] (zero it first; NULL skips them).  Float atomics only.
  *  - lsr_backward_preprocess_views: the preprocess backward of n_views views whose composite
  *    backward ran: gout (+)= sum_v (every output except dL_dlanguage_feature, which the composite
  *    calls already filled). */

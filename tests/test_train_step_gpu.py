@@ -63,3 +63,36 @@ def test_train_loop_fits_teacher():
     assert tr.steps["f_dc"] == 16 and not torch.equal(field.p["pos_deform.3.weight"], w0)
     assert not torch.equal(field.p["grid.grids.1.3"], plane0)
     assert tr.denom.shape[0] == tr.P and np.isfinite(tr.xyz_gradient_accum.cpu().numpy()).all()
+
+
+def test_densify_callback_runs_before_the_step():
+    """train.py:388-421 order: densification statistics -> densify / prune / reset_opacity ->
+    optimizer.step().  On the iterations the callback rebuilds the rows (densify, prune) the
+    Gaussian groups have no gradient and Adam skips them, as the reference's optimizer skips its
+    fresh nn.Parameters; after a reset only the opacity group is skipped; the field always steps."""
+    P, W, H = 3000, 128, 96
+    dev = torch.device("cuda")
+    sc = synthetic.make_scene(P, C=3, tanfovx=0.6, tanfovy=0.6 * H / W, seed=4, logscale_mean=-3.0).to(dev)
+    cams = synthetic.camera_batch(2, W, H, tanfovx=0.6, seed=2)
+    field_p = DeformationField.init_params(RES, MULTIRES, AABB, seed=1)
+    field = DeformationField({k: v.to(dev) for k, v in field_p.items()}, RES, MULTIRES)
+    tr = GaussianTrainer(_raw(sc, P), LRS)
+    gts = torch.rand(2, 3, H, W, device=dev)
+    calls = []
+
+    def schedule(t, it):
+        calls.append((it, t.P))
+        if it == 3:
+            t.densify(1e-9, 0.005, 8.0)
+        if it == 5:
+            t.reset_opacity()
+
+    step = TrainStep(tr, field, densify=schedule)
+    for _ in range(6):
+        step(cams, gts)
+    torch.cuda.synchronize()
+    assert [c[0] for c in calls] == [1, 2, 3, 4, 5, 6]
+    assert tr.P > P and calls[3][1] == tr.P           # rows rebuilt at iteration 3, seen from 4 on
+    assert tr.steps["f_dc"] == 5 and tr.steps["xyz"] == 5   # iteration 3 skipped
+    assert tr.steps["opacity"] == 4                          # iterations 3 and 5 skipped
+    assert all(p.grad is None for p in tr.params.values())

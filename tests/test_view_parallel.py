@@ -156,3 +156,78 @@ def test_two_rank_step_equals_serial_batch(densify, batched):
         assert torch.equal(outs[0]["radii"], ref.radii) and torch.equal(outs[1]["radii"], ref.radii)
         assert torch.equal(outs[0]["vis"], ref.radii > 0)
         assert int(ref.radii.gt(0).sum()) > 0
+
+
+class _FakePending:
+    def __init__(self, v, log):
+        self.v, self.log, self.num_rendered = v, log, 0
+
+    def resolve(self, binning=False):
+        self.log.append(("resolve", self.v))
+        return self
+
+
+def _lookahead_worker(rank, world, port, outdir):
+    """native_view_renderer's one-stream lookahead with LIST settings (every view of the batch
+    visible to every rank): each rank must preprocess exactly its own views, never the next rank's
+    first view, and leave nothing pending after the step.  The native calls are replaced by
+    recorders (no GPU here); the control flow is the product's."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import diff_gaussian_rasterization as dgr
+        from view_parallel import native_view_renderer
+        log = []
+        Pn = 16
+
+        def preprocess_native(settings, *a, **k):
+            log.append(("preprocess", settings))
+            return _FakePending(settings, log)
+
+        def render_native(pf):
+            log.append(("render", pf.v))
+            z = torch.zeros(3, 4, 4)
+            return z, torch.zeros(2, 4, 4), torch.full((Pn,), pf.v + 1, dtype=torch.int32), z[:1], pf
+
+        def backward_composite_native(st, gc, gl, gd, dL_dlanguage=None):
+            log.append(("composite_bwd", st.v))
+            return st
+
+        def backward_preprocess_views_native(held, out=None, accumulate=False, need=None):
+            log.append(("flush", [h.v for h in held]))
+            for t in out.values():
+                if t is not None:
+                    t.zero_()
+
+        dgr.preprocess_native, dgr.render_native = preprocess_native, render_native
+        dgr.backward_composite_native = backward_composite_native
+        dgr.backward_preprocess_views_native = backward_preprocess_views_native
+
+        class S:
+            means3D = opacities = shs = lang = scales = rotations = torch.zeros(Pn, 3)
+
+        n_views = 5
+        settings = list(range(n_views))          # "settings" of view v is just v here
+        render = native_view_renderer(S(), settings, lambda v, c, l, d: (c, l, d), overlap="lookahead")
+        b = GradBucket(Pn, 1, 2, "cpu", densify_stats=True)
+        step = ViewParallelStep(b, n_views)
+        for _ in range(2):                       # two steps: nothing carried over
+            step.run(render)
+            assert not render.pending
+        mine = list(step.views)
+        pre = [s for k, s in log if k == "preprocess"]
+        assert pre == mine * 2, (rank, pre, mine)
+        assert [s for k, s in log if k == "render"] == mine * 2
+        assert [s for k, s in log if k == "flush"] == [mine] * 2
+        torch.save(dict(radii=b.radii.clone()), os.path.join(outdir, f"rank{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_lookahead_stays_in_rank_slice():
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_lookahead_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        outs = [torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(2)]
+    # radii MAX over all 5 views (the fake radius of view v is v + 1)
+    assert torch.equal(outs[0]["radii"], torch.full((16,), 5, dtype=torch.int32))
+    assert torch.equal(outs[1]["radii"], outs[0]["radii"])
