@@ -18,8 +18,8 @@ void launch_iota(int n, uint32_t* out, hipStream_t st) {
     if (n > 0) hipLaunchKernelGGL(k_iota, dim3((n + 255) / 256), dim3(256), 0, st, n, out);
 }
 
-// Depth-order pass: the one random gather of the binning (8 B per Gaussian), after which the
-// emission reads only coalesced depth-ordered arrays.
+// Depth-order pass: the one random gather of the binning's counts (8 B per Gaussian), after which
+// the emission reads coalesced depth-ordered arrays (and gathers the splats of listed Gaussians).
 __global__ void __launch_bounds__(256) k_gather_tile_counts(int P, const uint32_t* __restrict__ order,
                                                             const uint2* __restrict__ rect,
                                                             uint32_t* __restrict__ counts,
@@ -43,15 +43,22 @@ void launch_gather_tile_counts(int P, const uint32_t* order, const uint2* rect, 
 // range with consecutive lanes on consecutive slots (fully coalesced key/value stores); a lane
 // finds the rank owning its slot by binary search over the 64 start offsets in LDS.  Slot order
 // inside a Gaussian is its rectangle in row-major order (as upstream's duplicateWithKeys).
+// Each instance also gets the 8x8 quadrants of its tile that the splat may reach (a conservative
+// test, emit_quad_mask) that the compositors' per-quadrant waves used to evaluate while scanning
+// every list entry (quad_may_touch); once per instance here, so their scans read only the point
+// list (no centre / conic gathers).  An instance reaching no quadrant would be
+// skipped at every pixel of its tile: it gets the past-the-end tile key (dropped from the lists).
 __global__ void __launch_bounds__(256) k_emit(int P, const uint32_t* __restrict__ order,
                                               const uint32_t* __restrict__ offsets,
                                               const uint32_t* __restrict__ counts,
-                                              const uint2* __restrict__ rect_sorted, int gx,
+                                              const uint2* __restrict__ rect_sorted, int gx, int gy, int W, int H,
+                                              const float2* __restrict__ xy, const float4* __restrict__ conic_o,
                                               uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
                                               ClearList clear) {
     __shared__ uint32_t s_off[4][64];
     __shared__ uint2 s_rc[4][64];
     __shared__ uint32_t s_id[4][64];
+    __shared__ EmitSplat s_sp[4][64];
     clear_words(clear);   // tile ranges, per-tile bounds, tile-sort workspace (used after this kernel)
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int base = (blockIdx.x * 4 + w) * 64;
@@ -65,8 +72,13 @@ __global__ void __launch_bounds__(256) k_emit(int P, const uint32_t* __restrict_
     const uint32_t start = __shfl(off, 0);
     s_off[w][lane] = ok ? off : end;                         // past-the-end lanes never own a slot
     s_rc[w][lane] = ok ? rect_sorted[r] : make_uint2(0u, 0u);
-    s_id[w][lane] = ok ? order[r] : 0u;
+    const uint32_t id = ok ? order[r] : 0u;
+    s_id[w][lane] = id;
+    const bool listed = ok && cnt > 0;
+    s_sp[w][lane] = emit_splat(listed ? xy[id] : make_float2(0.0f, 0.0f),
+                               listed ? conic_o[id] : make_float4(1.0f, 0.0f, 1.0f, 0.0f));
     __builtin_amdgcn_wave_barrier();
+    const uint32_t ntiles = (uint32_t)(gx * gy);
     for (uint32_t j = start + lane; j < end; j += 64) {
         int k = 0;                                           // last rank with s_off <= j
 #pragma unroll
@@ -76,17 +88,20 @@ __global__ void __launch_bounds__(256) k_emit(int P, const uint32_t* __restrict_
         const uint32_t x0 = rc.x & 0xFFFFu, y0 = rc.x >> 16, wd = (rc.y & 0xFFFFu) - x0;
         const uint32_t loc = j - s_off[w][k];
         const uint32_t dy = loc / wd;
-        keys[j] = (y0 + dy) * (uint32_t)gx + x0 + (loc - dy * wd);
-        vals[j] = s_id[w][k];
+        const uint32_t tx = x0 + (loc - dy * wd), ty = y0 + dy;
+        const uint32_t quads = emit_quad_mask(s_sp[w][k], (int)tx * LSR_TILE_X, (int)ty * LSR_TILE_Y, W, H);
+        keys[j] = quads ? ty * (uint32_t)gx + tx : ntiles;
+        vals[j] = s_id[w][k] | (quads << PL_QUAD_SHIFT);
     }
 }
 
 void launch_emit_instances(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* counts,
-                           const uint2* rect_sorted, int grid_x, uint32_t* keys, uint32_t* vals,
-                           const ClearList& clear, hipStream_t st) {
+                           const uint2* rect_sorted, int grid_x, int grid_y, int W, int H, const float2* xy,
+                           const float4* conic_o, uint32_t* keys, uint32_t* vals, const ClearList& clear,
+                           hipStream_t st) {
     if (P == 0) return;
     hipLaunchKernelGGL(k_emit, dim3((P + 255) / 256), dim3(256), 0, st, P, order, offsets, counts, rect_sorted,
-                       grid_x, keys, vals, clear);
+                       grid_x, grid_y, W, H, xy, conic_o, keys, vals, clear);
 }
 
 // inst_off[g] = first instance slot of Gaussian g: only the deterministic backward needs it (its
@@ -106,18 +121,19 @@ void launch_scatter_inst_off(int P, const uint32_t* order, const uint32_t* offse
                        inst_off);
 }
 
-__global__ void __launch_bounds__(256) k_tile_ranges(size_t K, const uint32_t* __restrict__ keys,
+__global__ void __launch_bounds__(256) k_tile_ranges(size_t K, const uint32_t* __restrict__ keys, uint32_t ntiles,
                                                      uint2* __restrict__ ranges) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= K) return;
     const uint32_t t = keys[i];
+    if (t >= ntiles) return;   // dropped instances (past-the-end key)
     if (i == 0 || keys[i - 1] != t) ranges[t].x = (uint32_t)i;
     if (i == K - 1 || keys[i + 1] != t) ranges[t].y = (uint32_t)(i + 1);
 }
 
-void launch_tile_ranges(size_t K, const uint32_t* keys, uint2* ranges, hipStream_t st) {
+void launch_tile_ranges(size_t K, const uint32_t* keys, uint32_t ntiles, uint2* ranges, hipStream_t st) {
     if (K == 0) return;
-    hipLaunchKernelGGL(k_tile_ranges, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, st, K, keys, ranges);
+    hipLaunchKernelGGL(k_tile_ranges, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, st, K, keys, ntiles, ranges);
 }
 
 }  // namespace lsr

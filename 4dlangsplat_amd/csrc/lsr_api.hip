@@ -192,9 +192,11 @@ Scratch carve_scratch(void* base, size_t P, size_t K, int recq, bool det, size_t
     return s;
 }
 
+// tile-sort key bits: keys are tile ids 0..ntiles-1 plus ntiles for instances whose splat
+// reaches no quadrant of their tile (binning.hip k_emit): they sort past every tile's list
 int tile_bits(int ntiles) {
     int b = 1;
-    while ((1 << b) < ntiles) ++b;
+    while ((1 << b) <= ntiles) ++b;
     return b;
 }
 bool tile_sort_in_b(int ntiles) { return ((tile_bits(ntiles) + 7) / 8) % 2 == 1; }
@@ -206,6 +208,11 @@ int check_common(const lsr_settings* s, const lsr_fwd_in* in) {
     if (s->image_width > 65535 * LSR_TILE_X || s->image_height > 65535 * LSR_TILE_Y)
         return fail(LSR_EINVAL, "image size exceeds 65535 tiles per axis");
     if (in->P < 0) return fail(LSR_EINVAL, "P must be >= 0");
+    // point lists carry 28-bit Gaussian ids (the top 4 bits: the tile's quadrants the splat may
+    // reach) and the compositors address rows with 32-bit byte offsets
+    if (in->P >= (1 << 28)) return fail(LSR_EINVAL, "P must be < 2^28");
+    if ((uint64_t)in->P * (uint64_t)(in->C > 16 ? in->C : 16) * 4u >= (1ull << 32))
+        return fail(LSR_EINVAL, "P * max(C, 16) * 4 bytes must be < 2^32");
     if (!s->viewmatrix || !s->projmatrix || !s->bg || !s->campos)
         return fail(LSR_EINVAL, "viewmatrix, projmatrix, bg and campos are required");
     if (in->P > 0 && (!in->means3D || !in->opacities)) return fail(LSR_EINVAL, "means3D and opacities are required");
@@ -351,7 +358,8 @@ int lsr_forward_binning(const lsr_settings* s, const lsr_fwd_in* in, void* geom,
         cl.n[2] = (uint32_t)(lsr::radix_temp_zero_bytes(K, 0, tile_bits((int)ntiles)) / 4);
         {
             PhaseTimer t(LSR_PHASE_EMIT, st);
-            lsr::launch_emit_instances(P, g.val_a, g.offsets, g.counts, g.rect_sorted, gx, b.key_a, b.val_a, cl, st);
+            lsr::launch_emit_instances(P, g.val_a, g.offsets, g.counts, g.rect_sorted, gx, gy, W, H, g.xy, g.conic_o,
+                                       b.key_a, b.val_a, cl, st);
         }
         LSR_LAUNCHED("emit", st, s->debug);
         bool in_b;
@@ -368,7 +376,7 @@ int lsr_forward_binning(const lsr_settings* s, const lsr_fwd_in* in, void* geom,
         LSR_LAUNCHED("tile sort", st, s->debug);
         {
             PhaseTimer t(LSR_PHASE_TILE_RANGES, st);
-            lsr::launch_tile_ranges(K, keys, m.ranges, st);
+            lsr::launch_tile_ranges(K, keys, (uint32_t)ntiles, m.ranges, st);
         }
         LSR_LAUNCHED("tile ranges", st, s->debug);
     }

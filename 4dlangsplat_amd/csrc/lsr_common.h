@@ -86,6 +86,18 @@ __device__ __forceinline__ void tile_rect(float2 p, int r, int gx, int gy, int2&
     rmax.y = min(gy, max(0, (int)((p.y + (float)r + (float)(LSR_TILE_Y - 1)) / (float)LSR_TILE_Y)));
 }
 
+// &base[idx] as a uniform base + a 32-bit byte offset (idx * sizeof(T) < 2^32, checked on the
+// host): the compiler can use the SGPR-base + VGPR-offset addressing forms instead of 64-bit
+// address pairs in VGPRs (two registers and a 64-bit add per gather).
+template <typename T>
+__device__ __forceinline__ T* at32(T* base, uint32_t idx) {
+    return reinterpret_cast<T*>(reinterpret_cast<char*>(base) + idx * (uint32_t)sizeof(T));
+}
+template <typename T>
+__device__ __forceinline__ const T* at32(const T* base, uint32_t idx) {
+    return reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + idx * (uint32_t)sizeof(T));
+}
+
 __device__ __forceinline__ uint64_t lanemask_lt() {
     const uint32_t lane = __lane_id();
     return lane == 0 ? 0ull : (~0ull >> (64 - lane));
@@ -217,6 +229,73 @@ __device__ __forceinline__ bool quad_may_touch(float2 xy, float4 co, float x0, f
     const float mx = fmaxf(-dxl, dxh), my = fmaxf(-dyl, dyh);
     const float M = a * mx * mx + c * my * my + 2.0f * fabsf(b) * mx * my;
     return mq <= -2.0f * thr + 1e-5f * M + 1e-4f;
+}
+
+// Quadrant masks for the binning (k_emit): which 8x8 quadrants of tile (tx, ty) the splat may
+// reach, for every instance.  Separable: per quadrant-row band the x-extent of the region
+// R = {d : q(d) <= Q} (Q = -2 skip_power(o) plus a float margin) is computed in closed form, and
+// a quadrant is kept iff its dx range meets it.  For a fixed dy, R's slice is
+// dx in (-b dy -+ sqrt(a Q - det dy^2)) / a; over a dy band the minimum of the left end is at the
+// ellipse's leftmost point (dy_L = b hx / c) when the band holds it, else at a band end (the left
+// end is convex in dy), and symmetrically on the right.  In real arithmetic this is exactly the
+// box test of quad_may_touch; in float, Q carries the same kind of margin (doubled) and the
+// extents are widened by 1e-4 hx + 1e-3 px, so a quadrant where some pixel passes the
+// compositors' prefilter is never dropped (tests/test_parity_gpu.py checks the bits).
+struct EmitSplat {
+    float X, Y;        // centre (pixels)
+    float a, b;        // conic x^2 and xy terms (q = a dx^2 + 2 b dx dy + c dy^2)
+    float inv_a, det;  // 1 / a, a c - b^2
+    float Q, hx, hy;   // level, x / y half extents of R (hy < 0: R empty)
+    float dyl, dyr;    // dy of R's leftmost / rightmost points
+};
+__device__ __forceinline__ EmitSplat emit_splat(float2 xy, float4 co) {
+    EmitSplat s;
+    s.X = xy.x; s.Y = xy.y;
+    s.a = co.x; s.b = co.y;
+    const float c = co.z;
+    s.det = co.x * c - co.y * co.y;
+    s.inv_a = 1.0f / co.x;
+    const float Q0 = -2.0f * skip_power(co.w);
+    float hx = 0.0f, hy = -1.0f;
+    s.Q = Q0;
+    if (Q0 > 0.0f && s.det > 0.0f) {
+        hx = sqrtf(Q0 * c / s.det);
+        hy = sqrtf(Q0 * co.x / s.det);
+        const float M = co.x * hx * hx + c * hy * hy + 2.0f * fabsf(co.y) * hx * hy;
+        s.Q = Q0 + 2e-5f * M + 2e-4f;
+        hx = sqrtf(s.Q * c / s.det);
+        hy = sqrtf(s.Q * co.x / s.det);
+    }
+    s.hx = hx; s.hy = hy;
+    s.dyl = co.y * hx / c;
+    s.dyr = -s.dyl;
+    return s;
+}
+// mask bit (q = (band) * 2 + (column)) for the four quadrants of the tile at pixel origin (x0, y0)
+__device__ __forceinline__ uint32_t emit_quad_mask(const EmitSplat& s, int x0, int y0, int W, int H) {
+    const float ex = 1e-4f * s.hx + 1e-3f;
+    uint32_t mask = 0;
+#pragma unroll
+    for (int band = 0; band < 2; ++band) {
+        const int yb0 = y0 + 8 * band, yb1 = min(yb0 + 7, H - 1);
+        // dy = Y - y over the band's pixel rows, clipped to R's y extent
+        const float u0 = fmaxf(s.Y - (float)yb1, -s.hy - ex), u1 = fminf(s.Y - (float)yb0, s.hy + ex);
+        const float r0 = sqrtf(fmaxf(0.0f, s.a * s.Q - s.det * u0 * u0));
+        const float r1 = sqrtf(fmaxf(0.0f, s.a * s.Q - s.det * u1 * u1));
+        const float l0 = (-s.b * u0 - r0) * s.inv_a, l1 = (-s.b * u1 - r1) * s.inv_a;
+        const float g0 = (-s.b * u0 + r0) * s.inv_a, g1 = (-s.b * u1 + r1) * s.inv_a;
+        const float xmin = (s.dyl >= u0 && s.dyl <= u1 ? -s.hx : fminf(l0, l1)) - ex;
+        const float xmax = (s.dyr >= u0 && s.dyr <= u1 ? s.hx : fmaxf(g0, g1)) + ex;
+        const bool band_ok = yb0 < H && u0 <= u1 && s.hy >= 0.0f;
+#pragma unroll
+        for (int col = 0; col < 2; ++col) {
+            const int xa = x0 + 8 * col, xb = min(xa + 7, W - 1);
+            // dx = X - x over the column's pixels
+            const bool hit = band_ok && xa < W && s.X - (float)xb <= xmax && s.X - (float)xa >= xmin;
+            mask |= hit ? 1u << (band * 2 + col) : 0u;
+        }
+    }
+    return mask;
 }
 
 }  // namespace lsr

@@ -251,12 +251,18 @@ size_t radix_temp_zero_bytes(size_t n, int begin_bit, int end_bit);
 void launch_iota(int n, uint32_t* out, hipStream_t st);
 void launch_gather_tile_counts(int P, const uint32_t* order, const uint2* rect, uint32_t* counts, uint2* rect_sorted,
                                hipStream_t st);
+// Point-list values: Gaussian id in the low 28 bits, in the top 4 the quadrants (bit 28 + q,
+// q = (y >= 8) * 2 + (x >= 8) inside the 16x16 tile) the splat may reach (quad_may_touch); an
+// instance reaching none gets tile key ntiles and sorts past every list.
+constexpr uint32_t PL_ID_MASK = 0x0FFFFFFFu;
+constexpr int PL_QUAD_SHIFT = 28;
 void launch_emit_instances(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* counts,
-                           const uint2* rect_sorted, int grid_x, uint32_t* keys, uint32_t* vals,
-                           const ClearList& clear, hipStream_t st);
+                           const uint2* rect_sorted, int grid_x, int grid_y, int W, int H, const float2* xy,
+                           const float4* conic_o, uint32_t* keys, uint32_t* vals, const ClearList& clear,
+                           hipStream_t st);
 void launch_scatter_inst_off(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* counts,
                              uint32_t* inst_off, hipStream_t st);
-void launch_tile_ranges(size_t K, const uint32_t* keys, uint2* ranges, hipStream_t st);
+void launch_tile_ranges(size_t K, const uint32_t* keys, uint32_t ntiles, uint2* ranges, hipStream_t st);
 
 // compositing (render_fwd.hip / render_bwd.hip)
 void launch_render_fwd(const RenderFwdArgs& a, hipStream_t st);

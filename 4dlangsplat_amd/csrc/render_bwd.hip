@@ -80,7 +80,7 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
         const int first = end - nb;             // list position of batch slot 0
         __syncthreads();                        // previous batch fully written out
         if (tid < nb) {
-            const uint32_t gid = a.point_list[range.x + first + tid];
+            const uint32_t gid = a.point_list[range.x + first + tid] & PL_ID_MASK;
             const float2 xy = a.xy[gid];
             const float4 co = a.conic_o[gid];
             s_id[tid] = gid;

@@ -6,8 +6,9 @@
 // quadrant.  An entry that no pixel of the quadrant activates changes neither T nor the
 // back-to-front accumulators of any of its pixels, so skipping it is exact.  Each wave therefore
 //   1. scans its replay range (up to the largest n_contrib of its pixels) back to front, 64
-//      entries per round, one per lane: a conservative ellipse-vs-quadrant test
-//      (quad_may_touch) and a ballot compaction into a per-wave FIFO in LDS;
+//      entries per round, one per lane: the entry's quadrant bit (the conservative
+//      ellipse-vs-quadrant test quad_may_touch, evaluated once per instance by the binning,
+//      k_emit) and a ballot compaction into a per-wave FIFO in LDS;
 //   2. processes the surviving entries in groups of 16 (WG).  Per group, with pixels p on lanes:
 //        MFMA1   S[e][p] = sum_c F[e][c] G[p][c]           language part of dot(c_e, dL/dpix)
 //        serial  the back-to-front recurrence per pixel: w = alpha T and t = G dL/dalpha
@@ -31,6 +32,9 @@ constexpr int WGB = 48;      // G row pitch in bf16 at the one-off build: 32 lan
 constexpr int WWP = 20;      // W / t row pitch in bf16 (16 entries + 4): 40-byte rows, 8-byte aligned
 constexpr int WFIFO = 128;   // compacted entries waiting (list positions and ids); power of two
 
+// C32: the 32-channel instantiation (headline), whose language rows are two float4 loads per lane
+// with no per-channel predication
+template <bool C32>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 k_render_bwd_wave(RenderBwdArgs a) {
     __shared__ __attribute__((aligned(16))) __bf16 s_FR[64 * WGB];       // G rows (build), then F / W / t rows
@@ -40,7 +44,10 @@ k_render_bwd_wave(RenderBwdArgs a) {
     __shared__ uint32_t s_gid[WG];
     __shared__ uint32_t s_k[WG];
     __shared__ float s_mom[WG][8];
-    __shared__ float s_q[WG][10];   // per-entry scalar gradients in acc_small record order
+    // results of the previous group, staged for its atomics (issued one iteration late, see 6.)
+    __shared__ float s_q[WG][16];   // per-entry scalar gradients in acc_small record order (0..9)
+    __shared__ float s_lq[WG][33];  // dL/dlanguage rows [e][c] (pitch 33: conflict-free stores)
+    __shared__ uint32_t s_agid[WG];
     __shared__ uint32_t s_fk[WFIFO];
     __shared__ uint32_t s_fg[WFIFO];
 
@@ -61,9 +68,8 @@ k_render_bwd_wave(RenderBwdArgs a) {
     nrep = __builtin_amdgcn_readfirstlane(nrep);
     if (nrep == 0) return;                                           // wave-uniform
     const uint2 range = a.ranges[tile];
-    const int C = a.include_feature ? a.C : 0;   // language channels in play
-    const float bx0 = (float)qx0, bx1 = (float)min(qx0 + 7, a.W - 1);
-    const float by0 = (float)qy0, by1 = (float)min(qy0 + 7, a.H - 1);
+    const int C = C32 ? 32 : (a.include_feature ? a.C : 0);   // language channels in play
+    const float bx0 = (float)qx0, by0 = (float)qy0;
 
     const float T_final = inside ? a.final_T[pid] : 0.0f;
     float T = T_final;
@@ -138,28 +144,19 @@ k_render_bwd_wave(RenderBwdArgs a) {
 
     int pos = (int)nrep;     // list positions [0, pos) not yet scanned
     int head = 0, tail = 0;  // FIFO counters (wave-uniform)
-    // scan prefetch: ids, centres and conics of the round at positions [pos - 64, pos)
-    uint32_t sc_gid = 0;
-    float2 sc_xy = make_float2(0.0f, 0.0f);
-    float4 sc_co = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if (pos - 64 + lane >= 0) {
-        sc_gid = a.point_list[range.x + pos - 64 + lane];
-        sc_xy = a.xy[sc_gid];
-        sc_co = a.conic_o[sc_gid];
-    }
+    // scan prefetch: point-list words (id | quadrant bits) of the round at positions
+    // [pos - 64, pos) and of the round after it
+    uint32_t sc_w = pos - 64 + lane >= 0 ? *at32(a.point_list, range.x + pos - 64 + lane) : 0u;
+    uint32_t sc_nw = pos - 128 + lane >= 0 ? *at32(a.point_list, range.x + pos - 128 + lane) : 0u;
     // scan rounds until `want` entries wait in the FIFO or the range is exhausted
     auto scan_fill = [&](int want) {
         while (tail - head < want && pos > 0) {
             const int k = pos - 64 + lane;       // this round's positions (k < 0: before the list)
-            const uint32_t gid = sc_gid;
-            const float2 xy = sc_xy;
-            const float4 co = sc_co;
-            if (k - 64 >= 0) {                   // next round's loads in flight during this one
-                sc_gid = a.point_list[range.x + k - 64];
-                sc_xy = a.xy[sc_gid];
-                sc_co = a.conic_o[sc_gid];
-            }
-            const bool cand = k >= 0 && quad_may_touch(xy, co, bx0, bx1, by0, by1);
+            const uint32_t word = sc_w;
+            sc_w = sc_nw;
+            sc_nw = k - 128 >= 0 ? *at32(a.point_list, range.x + k - 128) : 0u;
+            const uint32_t gid = word & PL_ID_MASK;
+            const bool cand = k >= 0 && ((word >> (PL_QUAD_SHIFT + quad)) & 1u);
             const uint64_t m = __ballot(cand);
             if (cand) {   // back to front: higher list positions first
                 const int rank = lane == 63 ? 0 : __popcll(m >> (lane + 1));
@@ -173,46 +170,49 @@ k_render_bwd_wave(RenderBwdArgs a) {
         wave_lds_sync();
     };
     // group prefetch registers: geometry of entry `lane` (lanes < WG), language row slice
-    // (entry lane / 4, channels 8 (lane & 3) .. +7)
-    uint32_t pf_gid = 0, pf_k = 0xFFFFFFFFu;
-    float2 pf_xy = make_float2(0.0f, 0.0f);
-    float4 pf_co = make_float4(0.0f, 0.0f, 0.0f, 0.0f), pf_rgbd = pf_co, pf_f0 = pf_co, pf_f1 = pf_co;
-    auto load_group = [&](int n) {   // issue the loads of FIFO entries [head, head + n)
-        if (lane < WG) {
+    // (entry lane / 4, channels 8 (lane & 3) .. +7).  The loads are unconditional (no branches
+    // around them): lanes past the group read row 0 (a valid row; those entries are never active
+    // and their F rows only meet zero weights).
+    struct Pf {
+        uint32_t gid, k;
+        float2 xy;
+        float4 co, rgbd, f0, f1;
+    };
+    auto load_group = [&](Pf& pf, int n) __attribute__((always_inline)) {   // FIFO entries [head, head + n)
+        {
             const bool ok = lane < n;
             const int s = (head + lane) & (WFIFO - 1);
-            pf_gid = ok ? s_fg[s] : 0u;
-            pf_k = ok ? s_fk[s] : 0xFFFFFFFFu;
-            pf_xy = ok ? a.xy[pf_gid] : make_float2(0.0f, 0.0f);
-            pf_co = ok ? a.conic_o[pf_gid] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            pf_rgbd = ok ? a.rgbd[pf_gid] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            pf.gid = ok ? s_fg[s] : 0u;
+            pf.k = ok ? s_fk[s] : 0xFFFFFFFFu;
+            pf.xy = *at32(a.xy, pf.gid);
+            pf.co = *at32(a.conic_o, pf.gid);
+            pf.rgbd = *at32(a.rgbd, pf.gid);
         }
         const int e = lane >> 2, c0 = 8 * (lane & 3);
-        const bool ok = e < n;
-        const uint32_t gid = ok ? s_fg[(head + e) & (WFIFO - 1)] : 0u;
-        if (C == 32) {
-            const float4* r = reinterpret_cast<const float4*>(a.lang + (size_t)gid * 32 + c0);
-            pf_f0 = ok ? r[0] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            pf_f1 = ok ? r[1] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        const uint32_t gid = e < n ? s_fg[(head + e) & (WFIFO - 1)] : 0u;
+        if constexpr (C32) {
+            const float4* r = reinterpret_cast<const float4*>(at32(a.lang, gid * 32u + c0));
+            pf.f0 = r[0];
+            pf.f1 = r[1];
         } else {
             float f[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) f[j] = (ok && c0 + j < C) ? a.lang[(size_t)gid * C + c0 + j] : 0.0f;
-            pf_f0 = make_float4(f[0], f[1], f[2], f[3]);
-            pf_f1 = make_float4(f[4], f[5], f[6], f[7]);
+            for (int j = 0; j < 8; ++j) f[j] = (c0 + j < C) ? *at32(a.lang, gid * (uint32_t)C + c0 + j) : 0.0f;
+            pf.f0 = make_float4(f[0], f[1], f[2], f[3]);
+            pf.f1 = make_float4(f[4], f[5], f[6], f[7]);
         }
         head += n;
     };
-    auto store_group = [&]() {       // prefetched group -> LDS staging
+    auto store_group = [&](const Pf& pf) __attribute__((always_inline)) {   // prefetched group -> LDS
         if (lane < WG) {
-            s_gid[lane] = pf_gid;
-            s_k[lane] = pf_k;
-            s_xy[lane] = pf_xy;
-            s_co[lane] = pf_co;
-            s_rgbd[lane] = pf_rgbd;
+            s_gid[lane] = pf.gid;
+            s_k[lane] = pf.k;
+            s_xy[lane] = pf.xy;
+            s_co[lane] = pf.co;
+            s_rgbd[lane] = pf.rgbd;
         }
         const int e = lane >> 2, c0 = 8 * (lane & 3);
-        const float f[8] = {pf_f0.x, pf_f0.y, pf_f0.z, pf_f0.w, pf_f1.x, pf_f1.y, pf_f1.z, pf_f1.w};
+        const float f[8] = {pf.f0.x, pf.f0.y, pf.f0.z, pf.f0.w, pf.f1.x, pf.f1.y, pf.f1.z, pf.f1.w};
         bf16x8 h8, l8;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -225,15 +225,49 @@ k_render_bwd_wave(RenderBwdArgs a) {
         wave_lds_sync();
     };
 
+    // ---- 6. atomics of a group, from its staged results (s_q, s_lq, s_agid).  vmcnt retires in
+    //      order and counts no-return atomics too, so a wait on any load issued after an atomic
+    //      also waits for the atomic (~1-3k cycles under load).  The atomics are therefore issued
+    //      one iteration late, after the scan (whose point-list loads are waited on within the
+    //      iteration) and just before the next group's prefetch: the first wait behind them is
+    //      the following iteration's, a whole group of compute later.  Offsets are 32-bit (P * 32
+    //      floats < 2^32 bytes) so the addresses are SGPR base + VGPR offset. ---------------------
+    int acnt = 0;   // entries staged
+    auto issue_atomics = [&]() {
+        if (acnt == 0) return;
+#ifndef LSR_ABL_NOLANGATOM
+        if (a.acc_lang) {   // lane -> channel lane & 31 of entries (lane >> 5) + 2 j: 128-byte rows
+            const int ch = lane & 31;
+#pragma unroll
+            for (int j = 0; j < WG / 2; ++j) {
+                const int e = (lane >> 5) + 2 * j;
+                const float v = s_lq[e][ch];
+                if (e < acnt && ch < C && v != 0.0f) atomicAdd(at32(a.acc_lang, s_agid[e] * (uint32_t)C + ch), v);
+            }
+        }
+#endif
+#pragma unroll
+        for (int r = 0; r < WG / 4; ++r) {   // lane -> field lane & 15 of entry (lane >> 4) + 4 r
+            const int e = (lane >> 4) + 4 * r, q = lane & 15;
+            const float v = s_q[e][q];
+#ifndef LSR_ABL_NOSMALLATOM
+            if (e < acnt && q < 10 && v != 0.0f) atomicAdd(at32(a.acc_small, s_agid[e] * (uint32_t)ACC_PITCH + q), v);
+#endif
+        }
+        acnt = 0;
+    };
+
     scan_fill(WG);
     int cnt = min(WG, tail - head);
-    if (cnt > 0) load_group(cnt);
+    Pf pf;
+    if (cnt > 0) load_group(pf, cnt);
     while (cnt > 0) {
-        store_group();
-        // next group's loads in flight while this one computes
+        store_group(pf);
         scan_fill(WG);
+        issue_atomics();   // the previous group's (staging is rewritten only at this group's end)
+        // next group's loads in flight while this one computes
         const int next_cnt = min(WG, tail - head);
-        if (next_cnt > 0) load_group(next_cnt);
+        if (next_cnt > 0) load_group(pf, next_cnt);
 
         // ---- 3. MFMA1: S[e][p], then to one pixel per lane -------------------------------------
         float S[WG];
@@ -377,25 +411,12 @@ k_render_bwd_wave(RenderBwdArgs a) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) s_q[4 * g4 + i][l16] = dacc[2][i];   // rgb 0-2, depth 3
         }
-        // ---- 6. atomics: language rows straight from the MFMA layout (4 entries x 16 channels per
-        //      instruction), then the 10 scalars of each entry, consecutive lanes on one record --
-#ifdef LSR_ABL_NOLANGATOM
-        if (false) {
-#else
-        if (a.acc_lang) {
-#endif
+        // stage the group's results: language rows from the MFMA layout, gids
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int e = 4 * g4 + i;
-                if (e >= cnt) continue;
-                const size_t rowoff = (size_t)s_gid[e] * C;
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int nb = 0; nb < 2; ++nb) {
-                    const int ch = 16 * nb + l16;
-                    if (ch < C && dacc[nb][i] != 0.0f) atomicAdd(a.acc_lang + rowoff + ch, dacc[nb][i]);
-                }
-            }
-        }
+            for (int nb = 0; nb < 2; ++nb) s_lq[4 * g4 + i][16 * nb + l16] = dacc[nb][i];
+        if (lane < WG) s_agid[lane] = s_gid[lane];
         wave_lds_sync();
         if (lane < cnt) {   // moments -> mean2D (4-5), conic (6-8), opacity (9)
             const int e = lane;
@@ -416,19 +437,10 @@ k_render_bwd_wave(RenderBwdArgs a) {
             s_q[e][9] = M0;
         }
         wave_lds_sync();
-#pragma unroll
-        for (int r = 0; r < (WG * 10 + 63) / 64; ++r) {
-            const int idx = lane + 64 * r, e = idx / 10, q = idx - 10 * e;
-            if (idx < cnt * 10) {
-                const float v = s_q[e][q];
-#ifndef LSR_ABL_NOSMALLATOM
-                if (v != 0.0f) atomicAdd(a.acc_small + (size_t)s_gid[e] * ACC_PITCH + q, v);
-#endif
-            }
-        }
-        wave_lds_sync();
+        acnt = cnt;
         cnt = next_cnt;
     }
+    issue_atomics();   // the last group's
 }
 
 // Longest-first launch order.  Blocks are dispatched in launch order, so with ~10 quadrant waves
@@ -473,7 +485,9 @@ void launch_tile_order(int ntiles, const uint32_t* tile_max, const uint2* ranges
 void launch_render_bwd_wave(const RenderBwdArgs& a, hipStream_t st) {
     const int ntiles = a.grid_x * a.grid_y;
     if (a.tile_order) launch_tile_order(ntiles, a.tile_max_contrib, nullptr, a.tile_order, st);
-    hipLaunchKernelGGL(k_render_bwd_wave, dim3(((ntiles + 7) / 8) * 32), dim3(64), 0, st, a);
+    const bool c32 = a.include_feature && a.C == 32;
+    if (c32) hipLaunchKernelGGL(k_render_bwd_wave<true>, dim3(((ntiles + 7) / 8) * 32), dim3(64), 0, st, a);
+    else hipLaunchKernelGGL(k_render_bwd_wave<false>, dim3(((ntiles + 7) / 8) * 32), dim3(64), 0, st, a);
 }
 
 }  // namespace lsr

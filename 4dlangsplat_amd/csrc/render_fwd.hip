@@ -47,7 +47,7 @@ __global__ void __launch_bounds__(256) k_render_fwd(RenderFwdArgs a) {
         if (__syncthreads_count(done) == 256) break;
         const int nb = (int)min((uint32_t)BATCH, range.y - start);
         if (tid < nb) {
-            const uint32_t g = a.point_list[start + tid];
+            const uint32_t g = a.point_list[start + tid] & PL_ID_MASK;
             s_id[tid] = g;
             s_xy[tid] = a.xy[g];
             const float4 co = a.conic_o[g];
@@ -194,7 +194,7 @@ __global__ void __launch_bounds__(256) k_render_fwd_mfma(RenderFwdArgs a) {
         if (__syncthreads_count(done) == 256) break;
         const int nb = (int)min((uint32_t)SB, range.y - start);
         if (tid < nb) {
-            const uint32_t g = a.point_list[start + tid];
+            const uint32_t g = a.point_list[start + tid] & PL_ID_MASK;
             s_id[tid] = g;
             s_xy[tid] = a.xy[g];
             const float4 co = a.conic_o[g];

@@ -80,8 +80,6 @@ __global__ void __launch_bounds__(64) k_render_fwd_wave_mfma(RenderFwdArgs a) {
     const uint32_t sort_err = a.sort_err ? (a.sort_err[0] | a.sort_err[1]) : 0u;
     if (a.status_out && b == 0 && lane < 2) a.status_out[lane] = a.sort_err ? a.sort_err[lane] : 0u;
     const int C = a.C;
-    const float bx0 = (float)qx0, bx1 = (float)min(qx0 + 7, a.W - 1);
-    const float by0 = (float)qy0, by1 = (float)min(qy0 + 7, a.H - 1);
 
     float T = 1.0f;
     uint32_t last = 0;
@@ -96,25 +94,18 @@ __global__ void __launch_bounds__(64) k_render_fwd_wave_mfma(RenderFwdArgs a) {
 
     uint32_t pos = range.x;  // list entries [pos, range.y) not yet scanned
     int head = 0, tail = 0;  // FIFO counters (wave-uniform)
-    // scan prefetch: centres and conics of the round at pos, ids of the round after it (so a
-    // round's geometry loads are issued a round, and its id loads two rounds, before use)
-    uint32_t gid_c = pos + lane < range.y ? a.point_list[pos + lane] : 0u;
-    float2 xy_c = make_float2(0.0f, 0.0f);
-    float4 co_c = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if (pos + lane < range.y) { xy_c = a.xy[gid_c]; co_c = a.conic_o[gid_c]; }
-    uint32_t gid_n = pos + 64 + lane < range.y ? a.point_list[pos + 64 + lane] : 0u;
+    // scan prefetch: point-list words (id | quadrant bits, k_emit) of the next two rounds
+    uint32_t w_c = pos + lane < range.y ? *at32(a.point_list, pos + lane) : 0u;
+    uint32_t w_n = pos + 64 + lane < range.y ? *at32(a.point_list, pos + 64 + lane) : 0u;
     while (!__all(done)) {
         // ---- 1. scan + compaction (as k_render_fwd_wave) --------------------------------------
         while (tail - head < MG && pos < range.y) {
             const uint32_t idx = pos + lane;
-            const uint32_t gid = gid_c;
-            const float2 xy = xy_c;
-            const float4 co = co_c;
-            gid_c = gid_n;
-            if (idx + 64 < range.y) { xy_c = a.xy[gid_c]; co_c = a.conic_o[gid_c]; }
-            gid_n = idx + 128 < range.y ? a.point_list[idx + 128] : 0u;
-            bool cand = false;
-            if (idx < range.y) cand = quad_may_touch(xy, co, bx0, bx1, by0, by1);
+            const uint32_t word = w_c;
+            w_c = w_n;
+            w_n = idx + 128 < range.y ? *at32(a.point_list, idx + 128) : 0u;
+            const uint32_t gid = word & PL_ID_MASK;
+            const bool cand = idx < range.y && ((word >> (PL_QUAD_SHIFT + quad)) & 1u);
             const uint64_t m = __ballot(cand);
             if (cand) {
                 const int s = (tail + __popcll(m & lanemask_lt())) & (MFIFO - 1);

@@ -5,9 +5,10 @@
 // a given quadrant; an entry that no pixel of the quadrant blends leaves every pixel's T and
 // sums unchanged, and the contributor count upstream writes to n_contrib is the list position of
 // the last blended entry + 1, so skipping such entries is exact.  Each wave
-//   1. scans the tile list front to back, 64 entries per round, one per lane: a conservative
-//      ellipse-vs-quadrant test (quad_may_touch, lsr_common.h) and a ballot compaction into a
-//      per-wave FIFO in LDS (list order kept);
+//   1. scans the tile list front to back, 64 entries per round, one per lane: the entry's
+//      quadrant bit (the conservative ellipse-vs-quadrant test quad_may_touch, evaluated once per
+//      instance by the binning, k_emit) and a ballot compaction into a per-wave FIFO in LDS
+//      (list order kept);
 //   2. composites the surviving entries in groups of GF staged in LDS (geometry + language row),
 //      and stops as soon as every pixel of the quadrant has saturated.
 // 64-thread blocks, no block barriers; the four quadrants of a tile run on one XCD.
@@ -41,8 +42,6 @@ __global__ void __launch_bounds__(64) k_render_fwd_wave(RenderFwdArgs a) {
     const uint32_t sort_err = a.sort_err ? (a.sort_err[0] | a.sort_err[1]) : 0u;
     if (a.status_out && b == 0 && lane < 2) a.status_out[lane] = a.sort_err ? a.sort_err[lane] : 0u;
     const int C = a.C;
-    const float bx0 = (float)qx0, bx1 = (float)min(qx0 + 7, a.W - 1);
-    const float by0 = (float)qy0, by1 = (float)min(qy0 + 7, a.H - 1);
 
     float T = 1.0f;
     uint32_t last = 0;
@@ -55,16 +54,16 @@ __global__ void __launch_bounds__(64) k_render_fwd_wave(RenderFwdArgs a) {
 
     uint32_t pos = range.x;  // list entries [pos, range.y) not yet scanned
     int head = 0, tail = 0;  // FIFO counters (wave-uniform)
-    // ids of the next scan round, loaded one round ahead
-    uint32_t gid_next = pos + lane < range.y ? a.point_list[pos + lane] : 0u;
+    // point-list words of the next scan round, loaded one round ahead
+    uint32_t w_next = pos + lane < range.y ? *at32(a.point_list, pos + lane) : 0u;
     while (!__all(done)) {
         // ---- 1. scan + compaction -----------------------------------------------------------
         while (tail - head < GF && pos < range.y) {
             const uint32_t idx = pos + lane;
-            const uint32_t gid = gid_next;
-            gid_next = idx + 64 < range.y ? a.point_list[idx + 64] : 0u;
-            bool cand = false;
-            if (idx < range.y) cand = quad_may_touch(a.xy[gid], a.conic_o[gid], bx0, bx1, by0, by1);
+            const uint32_t word = w_next;
+            w_next = idx + 64 < range.y ? *at32(a.point_list, idx + 64) : 0u;
+            const uint32_t gid = word & PL_ID_MASK;
+            const bool cand = idx < range.y && ((word >> (PL_QUAD_SHIFT + quad)) & 1u);
             const uint64_t m = __ballot(cand);
             if (cand) {
                 const int s = (tail + __popcll(m & lanemask_lt())) & (FIFO - 1);

@@ -38,18 +38,33 @@ def decode_img(state):
     return ranges, tmax, fT, nc
 
 
-def decode_point_list(state):
+def decode_point_words(state):
+    """Raw point-list words: Gaussian id in the low 28 bits, the quadrant bits on top."""
     K = state.num_rendered
     W, H = state.settings.c.image_width, state.settings.c.image_height
     nt = ((W + 15) // 16) * ((H + 15) // 16)
     bits = 1
-    while (1 << bits) < nt:
+    while (1 << bits) <= nt:
         bits += 1
     in_b = ((bits + 7) // 8) % 2 == 1
     raw = state.binning.cpu().numpy()
     blk = _al(K * 4)
     off = 3 * blk if in_b else 2 * blk
     return raw[off:off + K * 4].view(np.uint32)
+
+
+def decode_point_list(state):
+    K = state.num_rendered
+    W, H = state.settings.c.image_width, state.settings.c.image_height
+    nt = ((W + 15) // 16) * ((H + 15) // 16)
+    bits = 1
+    while (1 << bits) <= nt:        # tile keys 0..nt (nt: instances reaching no quadrant)
+        bits += 1
+    in_b = ((bits + 7) // 8) % 2 == 1
+    raw = state.binning.cpu().numpy()
+    blk = _al(K * 4)
+    off = 3 * blk if in_b else 2 * blk
+    return raw[off:off + K * 4].view(np.uint32) & 0x0FFFFFFF   # low 28 bits: Gaussian id
 
 
 def check_binning_against_upstream(state, ref_state, W, H):
