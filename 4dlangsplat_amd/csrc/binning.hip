@@ -28,7 +28,7 @@ __global__ void __launch_bounds__(256) k_gather_tile_counts(int P, const uint32_
     if (r >= P) return;
     const uint2 rc = rect[order[r]];
     rect_sorted[r] = rc;
-    counts[r] = ((rc.y & 0xFFFFu) - (rc.x & 0xFFFFu)) * ((rc.y >> 16) - (rc.x >> 16));
+    counts[r] = rect_count(rc);
 }
 
 void launch_gather_tile_counts(int P, const uint32_t* order, const uint2* rect, uint32_t* counts, uint2* rect_sorted,
@@ -74,9 +74,12 @@ __global__ void __launch_bounds__(256) k_emit(int P, const uint32_t* __restrict_
     s_rc[w][lane] = ok ? rect_sorted[r] : make_uint2(0u, 0u);
     const uint32_t id = ok ? order[r] : 0u;
     s_id[w][lane] = id;
-    const bool listed = ok && cnt > 0;
-    s_sp[w][lane] = emit_splat(listed ? xy[id] : make_float2(0.0f, 0.0f),
-                               listed ? conic_o[id] : make_float4(1.0f, 0.0f, 1.0f, 0.0f));
+    // splats of rectangles beyond 2 x 2 tiles (no precomputed quadrant map): gathered here
+    const uint2 rc_own = ok ? rect_sorted[r] : make_uint2(0u, 0u);
+    uint32_t ox0, oy0, ox1, oy1;
+    rect_unpack(rc_own, ox0, oy0, ox1, oy1);
+    const bool big = ok && cnt > 0 && (ox1 - ox0 > 2 || oy1 - oy0 > 2);
+    if (big) s_sp[w][lane] = emit_splat(xy[id], conic_o[id]);
     __builtin_amdgcn_wave_barrier();
     const uint32_t ntiles = (uint32_t)(gx * gy);
     for (uint32_t j = start + lane; j < end; j += 64) {
@@ -85,11 +88,19 @@ __global__ void __launch_bounds__(256) k_emit(int P, const uint32_t* __restrict_
         for (int step = 32; step >= 1; step >>= 1)
             if (s_off[w][k + step] <= j) k += step;
         const uint2 rc = s_rc[w][k];
-        const uint32_t x0 = rc.x & 0xFFFFu, y0 = rc.x >> 16, wd = (rc.y & 0xFFFFu) - x0;
+        uint32_t x0, y0, x1, y1;
+        rect_unpack(rc, x0, y0, x1, y1);
+        const uint32_t wd = x1 - x0;
         const uint32_t loc = j - s_off[w][k];
         const uint32_t dy = loc / wd;
-        const uint32_t tx = x0 + (loc - dy * wd), ty = y0 + dy;
-        const uint32_t quads = emit_quad_mask(s_sp[w][k], (int)tx * LSR_TILE_X, (int)ty * LSR_TILE_Y, W, H);
+        const uint32_t dx = loc - dy * wd, tx = x0 + dx, ty = y0 + dy;
+        uint32_t quads;
+        if (wd <= 2 && y1 - y0 <= 2) {   // the preprocess's map
+            const uint32_t map = rect_quad_map(rc), sh = 8 * dy + 2 * dx;
+            quads = ((map >> sh) & 3u) | (((map >> (sh + 4)) & 3u) << 2);
+        } else {
+            quads = emit_quad_mask(s_sp[w][k], (int)tx * LSR_TILE_X, (int)ty * LSR_TILE_Y, W, H);
+        }
         keys[j] = quads ? ty * (uint32_t)gx + tx : ntiles;
         vals[j] = s_id[w][k] | (quads << PL_QUAD_SHIFT);
     }

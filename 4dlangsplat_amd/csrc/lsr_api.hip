@@ -205,8 +205,8 @@ int depth_sort_result_in_b() { return 0; }  // 32 key bits = 4 passes: result ba
 int check_common(const lsr_settings* s, const lsr_fwd_in* in) {
     if (!s || !in) return fail(LSR_EINVAL, "null settings or inputs");
     if (s->image_width <= 0 || s->image_height <= 0) return fail(LSR_EINVAL, "image size must be positive");
-    if (s->image_width > 65535 * LSR_TILE_X || s->image_height > 65535 * LSR_TILE_Y)
-        return fail(LSR_EINVAL, "image size exceeds 65535 tiles per axis");
+    if (s->image_width > 4095 * LSR_TILE_X || s->image_height > 4095 * LSR_TILE_Y)
+        return fail(LSR_EINVAL, "image size exceeds 4095 tiles per axis");
     if (in->P < 0) return fail(LSR_EINVAL, "P must be >= 0");
     // point lists carry 28-bit Gaussian ids (the top 4 bits: the tile's quadrants the splat may
     // reach) and the compositors address rows with 32-bit byte offsets

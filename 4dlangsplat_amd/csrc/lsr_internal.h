@@ -23,6 +23,24 @@ __device__ __forceinline__ void clear_words(const ClearList& c) {
         for (uint32_t i = t; i < c.n[k]; i += stride) c.p[k][i] = 0u;
 }
 
+// Packed binning rectangle [x0, x1) x [y0, y1) in tiles (12 bits each: <= 4096 tiles per axis)
+// plus, for rectangles of at most 2 x 2 tiles, the 16-bit map of the quadrants the splat may
+// reach (bit (2 (ty - y0) + band) * 4 + 2 (tx - x0) + column; emit_quad_mask), computed by the
+// preprocess while the splat is in registers so the binning needs no centre / conic gather for
+// them.  .x = x0 | y0 << 12 | map[0:8] << 24, .y = x1 | y1 << 12 | map[8:16] << 24.
+__host__ __device__ __forceinline__ uint2 rect_pack(uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1, uint32_t map) {
+    return make_uint2(x0 | y0 << 12 | (map & 0xFFu) << 24, x1 | y1 << 12 | (map >> 8) << 24);
+}
+__host__ __device__ __forceinline__ void rect_unpack(uint2 r, uint32_t& x0, uint32_t& y0, uint32_t& x1, uint32_t& y1) {
+    x0 = r.x & 0xFFFu; y0 = (r.x >> 12) & 0xFFFu; x1 = r.y & 0xFFFu; y1 = (r.y >> 12) & 0xFFFu;
+}
+__host__ __device__ __forceinline__ uint32_t rect_quad_map(uint2 r) { return (r.x >> 24) | (r.y >> 24) << 8; }
+__host__ __device__ __forceinline__ uint32_t rect_count(uint2 r) {
+    uint32_t x0, y0, x1, y1;
+    rect_unpack(r, x0, y0, x1, y1);
+    return (x1 - x0) * (y1 - y0);
+}
+
 struct PreprocessArgs {
     int P, M, deg, W, H, grid_x, grid_y;
     float tanfovx, tanfovy, focal_x, focal_y, scale_modifier;
@@ -40,7 +58,7 @@ struct PreprocessArgs {
     int* radii;
     int* radius;      // internal copy of radii (the backward recomputes tile rectangles)
     uint32_t* tiles;
-    uint2* rect;      // tile rectangle, packed (x0 | y0 << 16, x1 | y1 << 16); 0 when culled
+    uint2* rect;      // tile rectangle + small-rectangle quadrant map (rect_pack); 0 when culled
     uint32_t* key;
     float2* xy;
     float4* conic_o;

@@ -237,7 +237,17 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
 #pragma unroll
         for (int k = 0; k < ACC_PITCH / 4; ++k) r[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
-    a.rect[i] = make_uint2((uint32_t)cmin.x | ((uint32_t)cmin.y << 16), (uint32_t)cmax.x | ((uint32_t)cmax.y << 16));
+    uint32_t qmap = 0;   // quadrant map of a rectangle of <= 2 x 2 tiles (the binning's emit_quad_mask)
+    if (ntiles > 0 && cmax.x - cmin.x <= 2 && cmax.y - cmin.y <= 2) {
+        const EmitSplat es = emit_splat(pix, conic);
+        for (int ty = cmin.y; ty < cmax.y; ++ty)
+            for (int tx = cmin.x; tx < cmax.x; ++tx) {
+                const uint32_t m = emit_quad_mask(es, tx * LSR_TILE_X, ty * LSR_TILE_Y, a.W, a.H);
+                const uint32_t sh = (uint32_t)(2 * (ty - cmin.y)) * 4 + 2 * (tx - cmin.x);
+                qmap |= ((m & 3u) << sh) | ((m >> 2) << (sh + 4));
+            }
+    }
+    a.rect[i] = rect_pack((uint32_t)cmin.x, (uint32_t)cmin.y, (uint32_t)cmax.x, (uint32_t)cmax.y, qmap);
     if (a.key) a.key[i] = __float_as_uint(pv.z);
     a.xy[i] = pix;
     a.conic_o[i] = conic;

@@ -89,7 +89,9 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
             s_rgbd[tid] = a.rgbd[gid];
             s_thr[tid] = skip_power(co.w);
             const uint2 rc = a.rect[gid];   // the binning rectangle (preprocess), packed 16-bit
-            const int rx0 = (int)(rc.x & 0xFFFFu), ry0 = (int)(rc.x >> 16), rx1 = (int)(rc.y & 0xFFFFu);
+            uint32_t ux0, uy0, ux1, uy1;
+            rect_unpack(rc, ux0, uy0, ux1, uy1);
+            const int rx0 = (int)ux0, ry0 = (int)uy0, rx1 = (int)ux1;
             s_inst[tid] = a.inst_off[gid] + (uint32_t)((ty - ry0) * (rx1 - rx0) + (tx - rx0));
             s_act[tid] = 0;
         }
