@@ -114,13 +114,21 @@ void exclusive_scan_u32(const uint32_t* in, uint32_t* out, size_t n, uint32_t* t
 //   * the tile is placed digit-sorted in LDS and written out in runs (coalesced stores).
 // A look-back spin is bounded: on timeout the pass sets the caller's error word and finishes
 // (results invalid, never a hang).
+#ifndef LSR_SORT_LOOKBACK
+#define LSR_SORT_LOOKBACK 0   // 1: one pass kernel with decoupled look-back; 0: reduce-then-scan
+#endif
 #ifndef LSR_OS_ITEMS
-#define LSR_OS_ITEMS 16
+#if LSR_SORT_LOOKBACK
+#define LSR_OS_ITEMS 16   // look-back: 4..48 swept, 16 best (smaller tiles lengthen the chain)
+#else
+#define LSR_OS_ITEMS 8    // reduce-then-scan: 4 / 8 / 16 swept, 8 best
+#endif
 #endif
 constexpr int OS_ITEMS = LSR_OS_ITEMS;   // keys per thread per pass
 #ifndef LSR_LOOKBACK
 #define LSR_LOOKBACK 4   // predecessors read per look-back round trip (1..32 swept: 4 best)
 #endif
+
 constexpr int OS_TILE = 256 * OS_ITEMS;       // keys per block
 constexpr uint32_t OS_AGG = 1u << 30, OS_PRE = 2u << 30, OS_CNT = (1u << 30) - 1u;
 
@@ -165,7 +173,7 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t x, uint32_t* s_w
 #ifndef LSR_HIST_BLOCKS
 #define LSR_HIST_BLOCKS 4096
 #endif
-constexpr int OS_HIST_BLOCKS = LSR_HIST_BLOCKS;
+[[maybe_unused]] constexpr int OS_HIST_BLOCKS = LSR_HIST_BLOCKS;
 #ifndef LSR_HIST_ITEMS
 #define LSR_HIST_ITEMS 4
 #endif
@@ -325,6 +333,140 @@ __global__ void __launch_bounds__(256) k_radix_pass(const uint32_t* __restrict__
     }
 }
 
+// ---- reduce-then-scan passes (LSR_SORT_LOOKBACK=0) ---------------------------------------------
+// The same stable pass without the decoupled look-back: a count kernel writes every block's 256
+// digit counts, a scan kernel (one block per digit) turns them into each block's offset inside
+// the digit, and the scatter kernel ranks and places exactly as k_radix_pass, its global base
+// read instead of chained.  The look-back chain crosses the 8 XCDs' non-coherent L2s at every
+// hop (each an agent-scope round trip through the fabric, ~0.5-1 us), which bounded a pass by
+// the chain length; here the keys are read once more (4 B / key) and two small launches are
+// added per pass.
+__global__ void __launch_bounds__(256) k_rts_count(const uint32_t* __restrict__ keys, size_t n, int shift, int nbits,
+                                                   uint32_t* __restrict__ counts) {
+    __shared__ uint32_t s_h[4][256];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) s_h[w][tid] = 0;
+    __syncthreads();
+    const uint32_t mask = (1u << nbits) - 1u;
+    const uint64_t lt = lanemask_lt();
+    const size_t base = (size_t)blockIdx.x * OS_TILE + (size_t)wave * (64 * OS_ITEMS);
+    uint32_t key[OS_ITEMS];
+#pragma unroll
+    for (int r = 0; r < OS_ITEMS; ++r) {
+        const size_t idx = base + (size_t)r * 64 + lane;
+        key[r] = idx < n ? keys[idx] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < OS_ITEMS; ++r) {
+        const bool valid = base + (size_t)r * 64 + lane < n;
+        const uint32_t d = (key[r] >> shift) & mask;
+        const uint64_t peers = match_digit(d, valid, nbits);
+        if (valid && (peers & lt) == 0) s_h[wave][d] += (uint32_t)__popcll(peers);   // one leader per digit
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    counts[(size_t)blockIdx.x * 256 + tid] = s_h[0][tid] + s_h[1][tid] + s_h[2][tid] + s_h[3][tid];
+}
+
+// block d: exclusive scan of counts[b][d] over the blocks b, in place; totals[d] = digit d's count
+__global__ void __launch_bounds__(256) k_rts_scan(uint32_t* __restrict__ counts, int nb, uint32_t* __restrict__ totals) {
+    __shared__ uint32_t s_wave[4];
+    const int d = blockIdx.x, tid = threadIdx.x;
+    uint32_t carry = 0;
+    for (int b0 = 0; b0 < nb; b0 += SCAN_TILE) {
+        uint32_t v[SCAN_ITEMS];
+#pragma unroll
+        for (int i = 0; i < SCAN_ITEMS; ++i) {
+            const int b = b0 + tid * SCAN_ITEMS + i;
+            v[i] = b < nb ? counts[(size_t)b * 256 + d] : 0u;
+        }
+        uint32_t total;
+        block_exclusive_scan8(v, s_wave, total);
+#pragma unroll
+        for (int i = 0; i < SCAN_ITEMS; ++i) {
+            const int b = b0 + tid * SCAN_ITEMS + i;
+            if (b < nb) counts[(size_t)b * 256 + d] = v[i] + carry;
+        }
+        carry += total;
+        __syncthreads();   // s_wave reused by the next chunk
+    }
+    if (tid == 0) totals[d] = carry;
+}
+
+__global__ void __launch_bounds__(256) k_rts_scatter(const uint32_t* __restrict__ keys_in,
+                                                     const uint32_t* __restrict__ vals_in,
+                                                     uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
+                                                     size_t n, int shift, int nbits,
+                                                     const uint32_t* __restrict__ totals,
+                                                     const uint32_t* __restrict__ offs) {
+    __shared__ uint32_t s_key[OS_TILE];
+    __shared__ uint32_t s_val[OS_TILE];
+    __shared__ uint32_t s_wcnt[4][256];
+    __shared__ uint32_t s_gbase[256];
+    __shared__ uint32_t s_lbase[256];
+    __shared__ uint32_t s_wave[4];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const uint32_t bid = blockIdx.x;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) s_wcnt[w][tid] = 0;
+    __syncthreads();
+    const uint32_t mask = (1u << nbits) - 1u;
+    const uint64_t lt = lanemask_lt();
+    const size_t base = (size_t)bid * OS_TILE + (size_t)wave * (64 * OS_ITEMS);
+    uint32_t key[OS_ITEMS], val[OS_ITEMS], rank[OS_ITEMS];
+#pragma unroll
+    for (int r = 0; r < OS_ITEMS; ++r) {
+        const size_t idx = base + (size_t)r * 64 + lane;
+        const bool valid = idx < n;
+        key[r] = valid ? keys_in[idx] : 0u;
+        val[r] = valid ? vals_in[idx] : 0u;
+    }
+    // block offsets and digit starts: independent of the ranking, loaded while it runs
+    const uint32_t prefix = offs[(size_t)bid * 256 + tid];
+    const uint32_t hcount = totals[tid];
+#pragma unroll
+    for (int r = 0; r < OS_ITEMS; ++r) {
+        const bool valid = base + (size_t)r * 64 + lane < n;
+        const uint32_t d = (key[r] >> shift) & mask;
+        const uint64_t peers = match_digit(d, valid, nbits);
+        const uint32_t before = s_wcnt[wave][d];
+        const uint32_t pr = (uint32_t)__popcll(peers & lt);
+        rank[r] = before + pr;
+        __builtin_amdgcn_wave_barrier();
+        if (valid && pr == 0) s_wcnt[wave][d] = before + (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    const uint32_t c0 = s_wcnt[0][tid], c1 = s_wcnt[1][tid], c2 = s_wcnt[2][tid], c3 = s_wcnt[3][tid];
+    const uint32_t total = c0 + c1 + c2 + c3;
+    s_wcnt[0][tid] = 0; s_wcnt[1][tid] = c0; s_wcnt[2][tid] = c0 + c1; s_wcnt[3][tid] = c0 + c1 + c2;
+    const uint32_t dstart = block_excl_scan256(hcount, s_wave);      // global start of digit tid
+    const uint32_t lbase = block_excl_scan256(total, s_wave);        // local start of digit tid
+    s_lbase[tid] = lbase;
+    s_gbase[tid] = dstart + prefix - lbase;
+    __syncthreads();
+    const size_t tile0 = (size_t)bid * OS_TILE;
+    const int ntile = (int)min((size_t)OS_TILE, n - min(n, tile0));
+#pragma unroll
+    for (int r = 0; r < OS_ITEMS; ++r) {
+        const bool valid = base + (size_t)r * 64 + lane < n;
+        if (valid) {
+            const uint32_t d = (key[r] >> shift) & mask;
+            const uint32_t pos = s_lbase[d] + s_wcnt[wave][d] + rank[r];
+            s_key[pos] = key[r];
+            s_val[pos] = val[r];
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < ntile; i += 256) {
+        const uint32_t k = s_key[i];
+        const uint32_t dst = s_gbase[(k >> shift) & mask] + (uint32_t)i;
+        keys_out[dst] = k;
+        vals_out[dst] = s_val[i];
+    }
+}
+
 static size_t os_blocks(size_t n) { return (n + OS_TILE - 1) / OS_TILE; }
 
 size_t radix_temp_bytes(size_t n) {
@@ -334,6 +476,7 @@ size_t radix_temp_bytes(size_t n) {
 
 size_t radix_temp_zero_bytes(size_t n, int begin_bit, int end_bit) {
     if (n == 0 || end_bit <= begin_bit) return 0;
+    if (!LSR_SORT_LOOKBACK) return 0;   // reduce-then-scan writes every word it reads
     const int npass = (end_bit - begin_bit + 7) / 8;
     return align_up(HIST_COPIES * HIST_WORDS * 4 + 64, 256) + (size_t)npass * os_blocks(n) * 256 * 4;
 }
@@ -347,10 +490,31 @@ bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint
     uint32_t* own_err = tickets + 4;
     uint32_t* status =
         reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(temp) + align_up(HIST_COPIES * HIST_WORDS * 4 + 64, 256));
-    if (!temp_zeroed) (void)hipMemsetAsync(temp, 0, radix_temp_zero_bytes(n, begin_bit, end_bit), st);
+    const size_t zb = radix_temp_zero_bytes(n, begin_bit, end_bit);
+    if (!temp_zeroed && zb) (void)hipMemsetAsync(temp, 0, zb, st);
+    bool in_b = false;
+#if !LSR_SORT_LOOKBACK
+    // no up-front histogram: each pass's scan kernel yields the digit totals (hist[pass] holds them)
+    (void)err; (void)own_err;
+    int p_ = 0;
+    for (int shift = begin_bit; shift < end_bit; shift += 8, ++p_) {
+        const int nbits = (end_bit - shift) < 8 ? (end_bit - shift) : 8;
+        const uint32_t* kin = in_b ? keys_b : keys_a;
+        const uint32_t* vin = in_b ? vals_b : vals_a;
+        uint32_t* kout = in_b ? keys_a : keys_b;
+        uint32_t* vout = in_b ? vals_a : vals_b;
+        uint32_t* cnt = status + (size_t)p_ * nb * 256;
+        hipLaunchKernelGGL(k_rts_count, dim3((unsigned)nb), dim3(256), 0, st, kin, n, shift, nbits, cnt);
+        hipLaunchKernelGGL(k_rts_scan, dim3(256), dim3(256), 0, st, cnt, (int)nb, hist + p_ * 256);
+        hipLaunchKernelGGL(k_rts_scatter, dim3((unsigned)nb), dim3(256), 0, st, kin, vin, kout, vout, n, shift, nbits,
+                           (const uint32_t*)(hist + p_ * 256), (const uint32_t*)cnt);
+        in_b = !in_b;
+    }
+    return in_b;
+#else
     const unsigned hb = (unsigned)min((size_t)OS_HIST_BLOCKS, (n + 64 * HIST_ITEMS * 4 - 1) / (64 * HIST_ITEMS * 4));
     hipLaunchKernelGGL(k_radix_hist, dim3(hb), dim3(256), 0, st, (const uint32_t*)keys_a, n, begin_bit, end_bit, hist);
-    bool in_b = false;
+#endif
     int p = 0;
     for (int shift = begin_bit; shift < end_bit; shift += 8, ++p) {
         const int nbits = (end_bit - shift) < 8 ? (end_bit - shift) : 8;
