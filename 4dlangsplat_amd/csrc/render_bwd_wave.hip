@@ -34,8 +34,11 @@ constexpr int WFIFO = 128;   // compacted entries waiting (list positions and id
 
 // C32: the 32-channel instantiation (headline), whose language rows are two float4 loads per lane
 // with no per-channel predication
+#ifndef LSR_BWD_WAVES
+#define LSR_BWD_WAVES 2   // waves per SIMD the register budget targets
+#endif
 template <bool C32>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LSR_BWD_WAVES, LSR_BWD_WAVES)))
 k_render_bwd_wave(RenderBwdArgs a) {
     __shared__ __attribute__((aligned(16))) __bf16 s_FR[64 * WGB];       // G rows (build), then F / W / t rows
     __shared__ float4 s_co[WG];

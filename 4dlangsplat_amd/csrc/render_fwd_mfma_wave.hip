@@ -56,7 +56,11 @@ __device__ __forceinline__ void octets_to_b(bf16x8 (&x)[4]) {
 }
 }  // namespace
 
-__global__ void __launch_bounds__(64) k_render_fwd_wave_mfma(RenderFwdArgs a) {
+#ifndef LSR_FWD_WAVES
+#define LSR_FWD_WAVES 4   // waves per SIMD the register budget targets (3: 0.293 ms, 4: 0.268 ms)
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LSR_FWD_WAVES, LSR_FWD_WAVES)))
+k_render_fwd_wave_mfma(RenderFwdArgs a) {
     __shared__ float4 s_co[MG];
     __shared__ float4 s_rgbd[MG];
     __shared__ float2 s_xy[MG];
