@@ -26,6 +26,23 @@
 
 namespace lsr {
 
+// Diagnostic build only (-DLSR_BWD_STAMPS): per-segment s_memtime sums of the group loop, summed
+// over all waves into g_bwd_stamps (read by lsr_debug_bwd_stamps).  Read shares, not times.
+#ifdef LSR_BWD_STAMPS
+__device__ unsigned long long g_bwd_stamps[12];
+#define BWD_STAMP(seg)                                                                           \
+    do {                                                                                         \
+        __builtin_amdgcn_sched_barrier(0);                                                       \
+        unsigned long long t_;                                                                   \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");              \
+        __builtin_amdgcn_sched_barrier(0);                                                       \
+        if ((seg) > 0) st_sum[(seg) - 1] += t_ - st_prev;                                         \
+        st_prev = t_;                                                                            \
+    } while (0)
+#else
+#define BWD_STAMP(seg) do {} while (0)
+#endif
+
 constexpr int WG = 16;       // compacted entries per MFMA group
 constexpr int WFP = 40;      // F row pitch in bf16 (32 channels + 8): 80-byte rows, 16-byte aligned
 constexpr int WGB = 48;      // G row pitch in bf16 at the one-off build: 32 language + 4 rgb/depth + 12 zero
@@ -41,11 +58,13 @@ template <bool C32>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LSR_BWD_WAVES, LSR_BWD_WAVES)))
 k_render_bwd_wave(RenderBwdArgs a) {
     __shared__ __attribute__((aligned(16))) __bf16 s_FR[64 * WGB];       // G rows (build), then F / W / t rows
-    __shared__ float4 s_co[WG];
-    __shared__ float4 s_rgbd[WG];
-    __shared__ float2 s_xy[WG];
+    // group entries' screen-space data, one array per field (a b128 read gives 4 entries, a b64
+    // pair the operand of a packed-fp32 instruction): centre X, Y; conic a, b, c; opacity; rgb,
+    // depth; list position k (0xFFFFFFFF past the group: never active)
+    __shared__ __attribute__((aligned(16))) float s_X[WG], s_Y[WG], s_A[WG], s_B[WG], s_C[WG], s_O[WG];
+    __shared__ __attribute__((aligned(16))) float s_R[WG], s_Gc[WG], s_Bc[WG], s_D[WG];
     __shared__ uint32_t s_gid[WG];
-    __shared__ uint32_t s_k[WG];
+    __shared__ __attribute__((aligned(16))) uint32_t s_k[WG];
     __shared__ float s_mom[WG][8];
     // results of the previous group, staged for its atomics (issued one iteration late, see 6.)
     __shared__ float s_q[WG][16];   // per-entry scalar gradients in acc_small record order (0..9)
@@ -210,9 +229,9 @@ k_render_bwd_wave(RenderBwdArgs a) {
         if (lane < WG) {
             s_gid[lane] = pf.gid;
             s_k[lane] = pf.k;
-            s_xy[lane] = pf.xy;
-            s_co[lane] = pf.co;
-            s_rgbd[lane] = pf.rgbd;
+            s_X[lane] = pf.xy.x; s_Y[lane] = pf.xy.y;
+            s_A[lane] = pf.co.x; s_B[lane] = pf.co.y; s_C[lane] = pf.co.z; s_O[lane] = pf.co.w;
+            s_R[lane] = pf.rgbd.x; s_Gc[lane] = pf.rgbd.y; s_Bc[lane] = pf.rgbd.z; s_D[lane] = pf.rgbd.w;
         }
         const int e = lane >> 2, c0 = 8 * (lane & 3);
         const float f[8] = {pf.f0.x, pf.f0.y, pf.f0.z, pf.f0.w, pf.f1.x, pf.f1.y, pf.f1.z, pf.f1.w};
@@ -238,25 +257,34 @@ k_render_bwd_wave(RenderBwdArgs a) {
     int acnt = 0;   // entries staged
     auto issue_atomics = [&]() {
         if (acnt == 0) return;
-#ifndef LSR_ABL_NOLANGATOM
-        if (a.acc_lang) {   // lane -> channel lane & 31 of entries (lane >> 5) + 2 j: 128-byte rows
-            const int ch = lane & 31;
+        // every staged value and row offset read from LDS first (one wait), then the atomics
+        const int ch = lane & 31, q = lane & 15;
+        float lv[WG / 2], sv[WG / 4];
+        uint32_t lo[WG / 2], so[WG / 4];
 #pragma unroll
-            for (int j = 0; j < WG / 2; ++j) {
-                const int e = (lane >> 5) + 2 * j;
-                const float v = s_lq[e][ch];
-                if (e < acnt && ch < C && v != 0.0f) atomicAdd(at32(a.acc_lang, s_agid[e] * (uint32_t)C + ch), v);
-            }
+        for (int j = 0; j < WG / 2; ++j) {   // lane -> channel lane & 31 of entries (lane >> 5) + 2 j
+            const int e = (lane >> 5) + 2 * j;
+            lv[j] = s_lq[e][ch];
+            lo[j] = s_agid[e] * (uint32_t)C + ch;
         }
-#endif
 #pragma unroll
         for (int r = 0; r < WG / 4; ++r) {   // lane -> field lane & 15 of entry (lane >> 4) + 4 r
-            const int e = (lane >> 4) + 4 * r, q = lane & 15;
-            const float v = s_q[e][q];
-#ifndef LSR_ABL_NOSMALLATOM
-            if (e < acnt && q < 10 && v != 0.0f) atomicAdd(at32(a.acc_small, s_agid[e] * (uint32_t)ACC_PITCH + q), v);
-#endif
+            const int e = (lane >> 4) + 4 * r;
+            sv[r] = s_q[e][q];
+            so[r] = s_agid[e] * (uint32_t)ACC_PITCH + q;
         }
+#ifndef LSR_ABL_NOLANGATOM
+        if (a.acc_lang) {   // 128-byte rows
+#pragma unroll
+            for (int j = 0; j < WG / 2; ++j)
+                if ((lane >> 5) + 2 * j < acnt && ch < C && lv[j] != 0.0f) atomicAdd(at32(a.acc_lang, lo[j]), lv[j]);
+        }
+#endif
+#ifndef LSR_ABL_NOSMALLATOM
+#pragma unroll
+        for (int r = 0; r < WG / 4; ++r)
+            if ((lane >> 4) + 4 * r < acnt && q < 10 && sv[r] != 0.0f) atomicAdd(at32(a.acc_small, so[r]), sv[r]);
+#endif
         acnt = 0;
     };
 
@@ -264,13 +292,21 @@ k_render_bwd_wave(RenderBwdArgs a) {
     int cnt = min(WG, tail - head);
     Pf pf;
     if (cnt > 0) load_group(pf, cnt);
+#ifdef LSR_BWD_STAMPS
+    unsigned long long st_sum[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_prev = 0;
+#endif
     while (cnt > 0) {
+        BWD_STAMP(0);
         store_group(pf);
+        BWD_STAMP(1);
         scan_fill(WG);
+        BWD_STAMP(2);
         issue_atomics();   // the previous group's (staging is rewritten only at this group's end)
+        BWD_STAMP(3);
         // next group's loads in flight while this one computes
         const int next_cnt = min(WG, tail - head);
         if (next_cnt > 0) load_group(pf, next_cnt);
+        BWD_STAMP(4);
 
         // ---- 3. MFMA1: S[e][p], then to one pixel per lane -------------------------------------
         float S[WG];
@@ -296,49 +332,46 @@ k_render_bwd_wave(RenderBwdArgs a) {
             }
         }
 
+        BWD_STAMP(5);
         // ---- 4. serial back-to-front replay of the group: w = alpha T, t = G dL/dalpha --------
         // Per entry, everything but the T / accumulator recurrence is independent of the other
         // entries: computed branch-free for the whole group first (exp chains overlap), then the
         // recurrence runs with selects (an inactive entry leaves T and the accumulators unchanged
         // and gets w = t = 0, as in upstream's skip).
         float wv[WG], tv[WG];
-        constexpr int RB = 4;   // entries per branch-free batch (register budget)
+        constexpr int RB = 2;   // entries per branch-free batch: one packed-fp32 pair (register budget)
+        const lsr_f2 px2 = {pxf, pxf}, py2 = {pyf, pyf};
 #pragma unroll
         for (int e0 = 0; e0 < WG; e0 += RB) {
-        float Gv[RB], alv[RB], romv[RB], dotv[RB], pw[RB];
+        float Gv[RB], alv[RB], romv[RB], dotv[RB];
         bool act[RB];
-#pragma unroll
-        for (int u = 0; u < RB; ++u) {
-            const float2 xy = s_xy[e0 + u];
-            const float4 co = s_co[e0 + u];
-            const float dx = xy.x - pxf, dy = xy.y - pyf;
-            pw[u] = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-        }
-#pragma unroll
-        for (int u = 0; u < RB; u += 2) {   // two entries per packed-fp32 exp
+        {   // the pair's entry data: one broadcast b64 read per field = a packed-fp32 operand
+            auto ld2 = [&](const float* base) { return *reinterpret_cast<const lsr_f2*>(base + e0); };
+            const lsr_f2 X = ld2(s_X), Y = ld2(s_Y), A = ld2(s_A), B = ld2(s_B), Cc = ld2(s_C), O = ld2(s_O);
+            const uint2 kk = *reinterpret_cast<const uint2*>(s_k + e0);
+            // the forward's operation order per component (bit-identical alpha decisions)
+            const lsr_f2 dx = X - px2, dy = Y - py2;
+            const lsr_f2 pw = -0.5f * (A * dx * dx + Cc * dy * dy) - B * dx * dy;
 #ifdef LSR_ABL_NOEXP
-            Gv[u] = fmaxf(1.0f + pw[u], 0.0f);   // timing ablation only
-            Gv[u + 1] = fmaxf(1.0f + pw[u + 1], 0.0f);
+            const lsr_f2 ge = {fmaxf(1.0f + pw.x, 0.0f), fmaxf(1.0f + pw.y, 0.0f)};   // timing ablation only
 #else
-            const lsr_f2 g2 = expf_repro2(lsr_f2{pw[u], pw[u + 1]});
-            Gv[u] = g2.x;
-            Gv[u + 1] = g2.y;
+            const lsr_f2 ge = expf_repro2(pw);
 #endif
-        }
+            const lsr_f2 og = O * ge;
+            lsr_f2 dot = ld2(s_R) * g0;
+            dot = __builtin_elementwise_fma(ld2(s_Gc), lsr_f2{g1, g1}, dot);
+            dot = __builtin_elementwise_fma(ld2(s_Bc), lsr_f2{g2, g2}, dot);
+            dot = __builtin_elementwise_fma(ld2(s_D), lsr_f2{gD, gD}, dot);
 #pragma unroll
-        for (int u = 0; u < RB; ++u) {
-            const int e = e0 + u;
-            const float4 co = s_co[e];
-            const float power = pw[u];
-            alv[u] = fminf(0.99f, co.w * Gv[u]);
-            act[u] = e < cnt && s_k[e] < last_contributor && power <= 0.0f && alv[u] >= 1.0f / 255.0f;
-            romv[u] = __builtin_amdgcn_rcpf(1.0f - alv[u]);
-            const float4 cd = s_rgbd[e];
-            float dot = cd.x * g0;
-            dot = __builtin_fmaf(cd.y, g1, dot);
-            dot = __builtin_fmaf(cd.z, g2, dot);
-            dot = __builtin_fmaf(cd.w, gD, dot);
-            dotv[u] = dot + S[e];
+            for (int u = 0; u < 2; ++u) {
+                const int e = e0 + u;
+                const float power = u ? pw.y : pw.x;
+                Gv[u] = u ? ge.y : ge.x;
+                alv[u] = fminf(0.99f, u ? og.y : og.x);
+                act[u] = (u ? kk.y : kk.x) < last_contributor && power <= 0.0f && alv[u] >= 1.0f / 255.0f;
+                romv[u] = __builtin_amdgcn_rcpf(1.0f - alv[u]);
+                dotv[u] = (u ? dot.y : dot.x) + S[e];
+            }
         }
 #pragma unroll
         for (int u = 0; u < RB; ++u) {
@@ -357,6 +390,7 @@ k_render_bwd_wave(RenderBwdArgs a) {
         }
         }
 
+        BWD_STAMP(6);
         // ---- 5. sums over the wave's pixels on matrix cores -----------------------------------
         // rows [p][e] of R (W, then t) in LDS; the A operand R^T comes from transposing reads
         auto write_rows = [&](const float (&r)[WG]) {
@@ -414,6 +448,7 @@ k_render_bwd_wave(RenderBwdArgs a) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) s_q[4 * g4 + i][l16] = dacc[2][i];   // rgb 0-2, depth 3
         }
+        BWD_STAMP(7);
         // stage the group's results: language rows from the MFMA layout, gids
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -425,8 +460,8 @@ k_render_bwd_wave(RenderBwdArgs a) {
             const int e = lane;
             const float M0 = s_mom[e][0], Mx = s_mom[e][1], My = s_mom[e][2];
             const float Mxx = s_mom[e][3], Mxy = s_mom[e][4], Myy = s_mom[e][5];
-            const float2 xy = s_xy[e];
-            const float4 co = s_co[e];
+            const float2 xy = make_float2(s_X[e], s_Y[e]);
+            const float4 co = make_float4(s_A[e], s_B[e], s_C[e], s_O[e]);
             const float X = xy.x - bx0, Y = xy.y - by0;      // quadrant-local centre
             const float Sdx = X * M0 - Mx, Sdy = Y * M0 - My;
             const float Sdxdx = X * X * M0 - 2.0f * X * Mx + Mxx;
@@ -442,8 +477,18 @@ k_render_bwd_wave(RenderBwdArgs a) {
         wave_lds_sync();
         acnt = cnt;
         cnt = next_cnt;
+        BWD_STAMP(8);
     }
     issue_atomics();   // the last group's
+#ifdef LSR_BWD_STAMPS
+    if (lane < 8) {   // segments 0..7 (a vector atomic per lane)
+        unsigned long long v = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v = lane == k ? st_sum[k] : v;
+        atomicAdd(&g_bwd_stamps[lane], v);
+    }
+    if (lane == 8) atomicAdd(&g_bwd_stamps[8], 1ull);   // waves that ran groups
+#endif
 }
 
 // Longest-first launch order.  Blocks are dispatched in launch order, so with ~10 quadrant waves
@@ -494,3 +539,12 @@ void launch_render_bwd_wave(const RenderBwdArgs& a, hipStream_t st) {
 }
 
 }  // namespace lsr
+
+#ifdef LSR_BWD_STAMPS
+// diagnostic export (not part of include/lsr.h): read and reset the stamp sums
+extern "C" int lsr_debug_bwd_stamps(unsigned long long* out9) {
+    if (hipMemcpyFromSymbol(out9, HIP_SYMBOL(lsr::g_bwd_stamps), 9 * sizeof(unsigned long long)) != hipSuccess) return 2;
+    unsigned long long z[12] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(lsr::g_bwd_stamps), z, sizeof(z)) == hipSuccess ? 0 : 2;
+}
+#endif
