@@ -61,9 +61,10 @@ __device__ __forceinline__ void octets_to_b(bf16x8 (&x)[4]) {
 #endif
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LSR_FWD_WAVES, LSR_FWD_WAVES)))
 k_render_fwd_wave_mfma(RenderFwdArgs a) {
-    __shared__ float4 s_co[MG];
-    __shared__ float4 s_rgbd[MG];
-    __shared__ float2 s_xy[MG];
+    // group entries, one array per field (a b64 read of a pair = one packed-fp32 operand): centre
+    // X, Y; conic a, b, c; opacity (0 past the group: never blends); (r, g) and (b, depth) pairs
+    __shared__ __attribute__((aligned(16))) float s_X[MG], s_Y[MG], s_A[MG], s_B[MG], s_C[MG], s_O[MG];
+    __shared__ lsr_f2 s_RG[MG], s_BD[MG];
     __shared__ uint32_t s_k[MG];
     __shared__ __attribute__((aligned(16))) __bf16 s_Fh[MG * MFP];
     __shared__ __attribute__((aligned(16))) __bf16 s_Fl[MG * MFP];
@@ -87,8 +88,8 @@ k_render_fwd_wave_mfma(RenderFwdArgs a) {
 
     float T = 1.0f;
     uint32_t last = 0;
-    float acc[3] = {0.0f, 0.0f, 0.0f};
-    float accD = 0.0f;
+    lsr_f2 acc_rg = {0.0f, 0.0f}, acc_bd = {0.0f, 0.0f};   // (r, g), (b, depth)
+    const lsr_f2 px2 = {pxf, pxf}, py2 = {pyf, pyf};
     f32x4 L[2][4];   // L[mb][nb]: channels 16 mb + 4 g4 + i, pixels 16 nb + l16
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb)
@@ -172,9 +173,10 @@ k_render_fwd_wave_mfma(RenderFwdArgs a) {
             }
             if (lane < MG) {
                 s_k[lane] = g_k;
-                s_xy[lane] = g_xy;
-                s_co[lane] = g_co;
-                s_rgbd[lane] = g_rgbd;
+                s_X[lane] = g_xy.x; s_Y[lane] = g_xy.y;
+                s_A[lane] = g_co.x; s_B[lane] = g_co.y; s_C[lane] = g_co.z; s_O[lane] = g_co.w;
+                s_RG[lane] = lsr_f2{g_rgbd.x, g_rgbd.y};
+                s_BD[lane] = lsr_f2{g_rgbd.z, g_rgbd.w};
             }
         }
         head += cnt;
@@ -188,25 +190,20 @@ k_render_fwd_wave_mfma(RenderFwdArgs a) {
 #pragma unroll
             for (int u = 0; u < 8; ++u) w8[u] = 0.0f;
             if (8 * o < cnt && !__all(done)) {                    // wave-uniform
-                float al[8], pw[8];
+                float al[8];
                 bool ok[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const float2 xy = s_xy[8 * o + u];
-                    const float4 co = s_co[8 * o + u];
-                    const float dx = xy.x - pxf, dy = xy.y - pyf;
-                    pw[u] = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-                }
-#pragma unroll
-                for (int u = 0; u < 8; u += 2) {   // two entries per packed-fp32 exp
-                    const lsr_f2 g2 = expf_repro2(lsr_f2{pw[u], pw[u + 1]});
-                    al[u] = fminf(0.99f, s_co[8 * o + u].w * g2.x);
-                    al[u + 1] = fminf(0.99f, s_co[8 * o + u + 1].w * g2.y);
-                }
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
+                for (int u = 0; u < 8; u += 2) {   // two entries per packed-fp32 operation
                     const int e = 8 * o + u;
-                    ok[u] = e < cnt && pw[u] <= 0.0f && al[u] >= 1.0f / 255.0f;
+                    auto ld2 = [&](const float* base) { return *reinterpret_cast<const lsr_f2*>(base + e); };
+                    const lsr_f2 X = ld2(s_X), Y = ld2(s_Y), A = ld2(s_A), B = ld2(s_B), Cc = ld2(s_C), O = ld2(s_O);
+                    const lsr_f2 dx = X - px2, dy = Y - py2;
+                    const lsr_f2 pw = -0.5f * (A * dx * dx + Cc * dy * dy) - B * dx * dy;
+                    const lsr_f2 og = O * expf_repro2(pw);
+                    al[u] = fminf(0.99f, og.x);
+                    al[u + 1] = fminf(0.99f, og.y);
+                    ok[u] = pw.x <= 0.0f && al[u] >= 1.0f / 255.0f;        // padding entries: O = 0
+                    ok[u + 1] = pw.y <= 0.0f && al[u + 1] >= 1.0f / 255.0f;
                 }
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
@@ -217,11 +214,8 @@ k_render_fwd_wave_mfma(RenderFwdArgs a) {
                     done = done || (blend && test_T < 0.0001f);
                     blend = blend && !done;
                     const float w = blend ? alpha * T : 0.0f;   // w = 0: fma(c, 0, acc) == acc
-                    const float4 cd = s_rgbd[e];
-                    acc[0] = __builtin_fmaf(cd.x, w, acc[0]);
-                    acc[1] = __builtin_fmaf(cd.y, w, acc[1]);
-                    acc[2] = __builtin_fmaf(cd.z, w, acc[2]);
-                    accD = __builtin_fmaf(cd.w, w, accD);
+                    acc_rg = __builtin_elementwise_fma(s_RG[e], lsr_f2{w, w}, acc_rg);
+                    acc_bd = __builtin_elementwise_fma(s_BD[e], lsr_f2{w, w}, acc_bd);
                     w8[u] = w;
                     T = blend ? test_T : T;
                     last = blend ? s_k[e] + 1 : last;
@@ -251,7 +245,8 @@ k_render_fwd_wave_mfma(RenderFwdArgs a) {
     }
     if (sort_err) {   // a sort's look-back timed out: the lists are invalid, make every output NaN
         const float nan = __builtin_nanf("");
-        T = accD = acc[0] = acc[1] = acc[2] = nan;
+        T = nan;
+        acc_rg = acc_bd = lsr_f2{nan, nan};
 #pragma unroll
         for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
@@ -261,10 +256,10 @@ k_render_fwd_wave_mfma(RenderFwdArgs a) {
         const size_t HW = (size_t)a.H * a.W, pid = (size_t)py * a.W + px;
         a.final_T[pid] = T;
         a.n_contrib[pid] = last;
-        a.out_color[pid] = acc[0] + T * a.bg[0];
-        a.out_color[HW + pid] = acc[1] + T * a.bg[1];
-        a.out_color[2 * HW + pid] = acc[2] + T * a.bg[2];
-        a.out_depth[pid] = accD;
+        a.out_color[pid] = acc_rg.x + T * a.bg[0];
+        a.out_color[HW + pid] = acc_rg.y + T * a.bg[1];
+        a.out_color[2 * HW + pid] = acc_bd.x + T * a.bg[2];
+        a.out_depth[pid] = acc_bd.y;
     }
     {   // language: block (mb, nb), register i -> channel 16 mb + 4 g4 + i, pixel 16 nb + l16
         const size_t HW = (size_t)a.H * a.W;
