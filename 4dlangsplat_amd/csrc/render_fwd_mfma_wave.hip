@@ -36,6 +36,24 @@ __device__ __forceinline__ void pack_octet(const float (&w)[8], bf16x8& h, bf16x
     }
 }
 
+// LDS-DMA gather (global_load_lds): 16 or 4 bytes from this lane's global address to
+// lds_base + lane * size.  Inline asm, M0 written in the same statement (cdna_hip_programming.md,
+// LDS-DMA recipe): issued through the builtin, hipcc cannot tell the DMA's LDS image from the
+// compositing arrays and waits vmcnt(0) before every later ds_read, serialising the prefetch.
+// hipcc does not count these loads: relayout() waits vmcnt(0) itself before reading the image
+// (an untracked VMEM op can only make hipcc's own counted waits wait longer, never too little).
+__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)reinterpret_cast<uintptr_t>(p); }
+__device__ __forceinline__ void lds_dma16(const float* g, uint32_t lds_base) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(lds_base) : "memory");
+}
+__device__ __forceinline__ void lds_dma4(const float* g, uint32_t lds_base) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(lds_base) : "memory");
+}
+
 // lane group g holds octets x[0..3] (one per entry octet o) of its own pixel; afterwards it holds
 // in x[nb] the octet g of pixel 16 nb + (lane & 15): the MFMA B fragments, nb = pixel block
 __device__ __forceinline__ void octets_to_b(bf16x8 (&x)[4]) {
@@ -56,10 +74,41 @@ __device__ __forceinline__ void octets_to_b(bf16x8 (&x)[4]) {
 }
 }  // namespace
 
+// Diagnostic build only (-DLSR_FWD_STAMPS): per-segment s_memtime sums of the group loop into
+// g_fwd_stamps (lsr_debug_fwd_stamps).  Read shares, not times.
+#ifdef LSR_FWD_STAMPS
+__device__ unsigned long long g_fwd_stamps[8];
+#define FWD_STAMP(seg)                                                                           \
+    do {                                                                                         \
+        __builtin_amdgcn_sched_barrier(0);                                                       \
+        unsigned long long t_;                                                                   \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");              \
+        __builtin_amdgcn_sched_barrier(0);                                                       \
+        if ((seg) > 0) st_sum[(seg) - 1] += t_ - st_prev;                                         \
+        st_prev = t_;                                                                            \
+    } while (0)
+#else
+#define FWD_STAMP(seg) do {} while (0)
+#endif
+
 #ifndef LSR_FWD_WAVES
 #define LSR_FWD_WAVES 4   // waves per SIMD the register budget targets (3: 0.293 ms, 4: 0.268 ms)
 #endif
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LSR_FWD_WAVES, LSR_FWD_WAVES)))
+#ifndef LSR_FWD_DMA
+// 1: the LDS-DMA staged variant for 32 channels.  Measured slower (0.272 vs 0.255 ms): per wave
+// its loop runs in ~0.75x the cycles (the gathers no longer stall it), but its staging buffers
+// (12.9 KB of LDS per wave) allow 3 waves per SIMD instead of 4.
+#define LSR_FWD_DMA 0
+#endif
+#ifndef LSR_FWD_DMA_WAVES
+#define LSR_FWD_DMA_WAVES 3   // the LDS-DMA staged variant: its staging buffers leave room for 3
+#endif
+// DMA: 32 channels, the next group's rows and geometry gathered straight into LDS (LDS-DMA,
+// global_load_lds) while the current group composites, so a group's gathers no longer stall
+// the wave (52 % of the loop's cycles in the register-staged version, tools/fwd_stamps.py)
+template <bool DMA>
+__global__ void __launch_bounds__(64)
+__attribute__((amdgpu_waves_per_eu(DMA ? LSR_FWD_DMA_WAVES : LSR_FWD_WAVES, DMA ? LSR_FWD_DMA_WAVES : LSR_FWD_WAVES)))
 k_render_fwd_wave_mfma(RenderFwdArgs a) {
     // group entries, one array per field (a b64 read of a pair = one packed-fp32 operand): centre
     // X, Y; conic a, b, c; opacity (0 past the group: never blends); (r, g) and (b, depth) pairs
@@ -70,6 +119,12 @@ k_render_fwd_wave_mfma(RenderFwdArgs a) {
     __shared__ __attribute__((aligned(16))) __bf16 s_Fl[MG * MFP];
     __shared__ uint32_t s_fk[MFIFO];
     __shared__ uint32_t s_fg[MFIFO];
+    // DMA staging of one group (wave-instruction images, lane-linear), one array: language rows
+    // [e][c] at 0, conic_o [0, MG) then rgbd [MG, 2 MG) as float4 at SG_GEO, X [0, MG) then
+    // Y [MG, 2 MG) at SG_XY.  (Separate __shared__ arrays as LDS-DMA targets crash hipcc 7.2's
+    // SIFixSGPRCopies; float pointers into one array do not.)
+    constexpr int SG_GEO = MG * 32, SG_XY = SG_GEO + 2 * MG * 4;
+    __shared__ __attribute__((aligned(16))) float s_stage[DMA ? SG_XY + 2 * MG : 4];
 
     const int b = blockIdx.x;
     const int slot = (b >> 5) * 8 + (b & 7), quad = (b >> 3) & 3;   // a slot's 4 quadrants: one XCD
@@ -100,15 +155,23 @@ k_render_fwd_wave_mfma(RenderFwdArgs a) {
     uint32_t pos = range.x;  // list entries [pos, range.y) not yet scanned
     int head = 0, tail = 0;  // FIFO counters (wave-uniform)
     // scan prefetch: point-list words (id | quadrant bits, k_emit) of the next two rounds
-    uint32_t w_c = pos + lane < range.y ? *at32(a.point_list, pos + lane) : 0u;
-    uint32_t w_n = pos + 64 + lane < range.y ? *at32(a.point_list, pos + 64 + lane) : 0u;
-    while (!__all(done)) {
-        // ---- 1. scan + compaction (as k_render_fwd_wave) --------------------------------------
-        while (tail - head < MG && pos < range.y) {
+    uint32_t w_c = !DMA && pos + lane < range.y ? *at32(a.point_list, pos + lane) : 0u;
+    uint32_t w_n = !DMA && pos + 64 + lane < range.y ? *at32(a.point_list, pos + 64 + lane) : 0u;
+#ifdef LSR_FWD_STAMPS
+    unsigned long long st_sum[4] = {0, 0, 0, 0}, st_prev = 0;
+#endif
+    // scan rounds until `want` entries wait in the FIFO or the list is exhausted
+    auto scan_fill = [&](int want) __attribute__((always_inline)) {
+        while (tail - head < want && pos < range.y) {
             const uint32_t idx = pos + lane;
-            const uint32_t word = w_c;
-            w_c = w_n;
-            w_n = idx + 128 < range.y ? *at32(a.point_list, idx + 128) : 0u;
+            uint32_t word;
+            if constexpr (DMA) {   // loaded here: nothing of the scan stays in flight over the compositing
+                word = idx < range.y ? *at32(a.point_list, idx) : 0u;
+            } else {
+                word = w_c;
+                w_c = w_n;
+                w_n = idx + 128 < range.y ? *at32(a.point_list, idx + 128) : 0u;
+            }
             const uint32_t gid = word & PL_ID_MASK;
             const bool cand = idx < range.y && ((word >> (PL_QUAD_SHIFT + quad)) & 1u);
             const uint64_t m = __ballot(cand);
@@ -120,67 +183,9 @@ k_render_fwd_wave_mfma(RenderFwdArgs a) {
             tail += __popcll(m);
             pos += 64;
         }
-        const int cnt = min(MG, tail - head);
-        if (cnt == 0) break;
-        wave_lds_sync();
-        // ---- 2. stage the group: geometry, and the language rows as bf16 hi / lo -------------
-        // every gather of the group is issued before the first LDS store (one memory latency per
-        // group instead of three in sequence)
-        {
-            // lane -> entry lane / 2, channels 16 (lane & 1) .. +15: four float4 loads in flight
-            const int e = lane >> 1, c0 = 16 * (lane & 1);
-            const bool ok = e < cnt;
-            const uint32_t gid = ok ? s_fg[(head + e) & (MFIFO - 1)] : 0u;
-            float f[16];
-            if (C == 32) {
-                const float4* r = reinterpret_cast<const float4*>(a.lang + (size_t)gid * 32 + c0);
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {   // unmasked (gid 0 is a valid row), zeroed after
-                    const float4 v = r[q];
-                    f[4 * q] = v.x; f[4 * q + 1] = v.y; f[4 * q + 2] = v.z; f[4 * q + 3] = v.w;
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < 16; ++j) f[j] = (ok && c0 + j < C) ? a.lang[(size_t)gid * C + c0 + j] : 0.0f;
-            }
-            float2 g_xy = make_float2(0.0f, 0.0f);
-            float4 g_co = make_float4(0.0f, 0.0f, 0.0f, 0.0f), g_rgbd = g_co;
-            uint32_t g_k = 0u;
-            if (lane < MG && lane < cnt) {
-                const int s = (head + lane) & (MFIFO - 1);
-                const uint32_t gid = s_fg[s];
-                g_k = s_fk[s];
-                g_xy = a.xy[gid];
-                g_co = a.conic_o[gid];
-                g_rgbd = a.rgbd[gid];
-            }
-            if (C == 32) {
-#pragma unroll
-                for (int j = 0; j < 16; ++j) f[j] = ok ? f[j] : 0.0f;
-            }
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                bf16x8 vh, vl;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    __bf16 hh, ll;
-                    split_bf16(f[8 * h + j], hh, ll);
-                    vh[j] = hh;
-                    vl[j] = ll;
-                }
-                *reinterpret_cast<bf16x8*>(s_Fh + e * MFP + c0 + 8 * h) = vh;
-                *reinterpret_cast<bf16x8*>(s_Fl + e * MFP + c0 + 8 * h) = vl;
-            }
-            if (lane < MG) {
-                s_k[lane] = g_k;
-                s_X[lane] = g_xy.x; s_Y[lane] = g_xy.y;
-                s_A[lane] = g_co.x; s_B[lane] = g_co.y; s_C[lane] = g_co.z; s_O[lane] = g_co.w;
-                s_RG[lane] = lsr_f2{g_rgbd.x, g_rgbd.y};
-                s_BD[lane] = lsr_f2{g_rgbd.z, g_rgbd.w};
-            }
-        }
-        head += cnt;
-        wave_lds_sync();
+    };
+    // composite FIFO group [.., cnt) staged in the SoA arrays and F rows, then its channel sums
+    auto composite = [&](int cnt) __attribute__((always_inline)) {
         // ---- 3. per pixel, front to back: alphas of 8 entries branch-free, then the serial
         //      update with selects (as k_render_fwd_wave); the weights go to octets ----------------
         bf16x8 oh[4], ol[4];
@@ -223,6 +228,7 @@ k_render_fwd_wave_mfma(RenderFwdArgs a) {
             }
             pack_octet(w8, oh[o], ol[o]);
         }
+        FWD_STAMP(3);
         // ---- 4. language channels on matrix cores -----------------------------------------------
         octets_to_b(oh);
         octets_to_b(ol);
@@ -241,8 +247,165 @@ k_render_fwd_wave_mfma(RenderFwdArgs a) {
                 L[mb][nb] = LSR_MFMA16(alo, oh[nb], L[mb][nb]);
             }
         }
-        wave_lds_sync();   // the group's LDS rows are read before the next staging
+    };
+    if constexpr (!DMA) {
+        while (!__all(done)) {
+            FWD_STAMP(0);
+            scan_fill(MG);
+            const int cnt = min(MG, tail - head);
+            if (cnt == 0) break;
+            wave_lds_sync();
+            FWD_STAMP(1);
+            // ---- 2. stage the group: geometry, and the language rows as bf16 hi / lo -------------
+            // every gather of the group is issued before the first LDS store (one memory latency per
+            // group instead of three in sequence)
+            {
+                // lane -> entry lane / 2, channels 16 (lane & 1) .. +15: four float4 loads in flight
+                const int e = lane >> 1, c0 = 16 * (lane & 1);
+                const bool ok = e < cnt;
+                const uint32_t gid = ok ? s_fg[(head + e) & (MFIFO - 1)] : 0u;
+                float f[16];
+                if (C == 32) {
+                    const float4* r = reinterpret_cast<const float4*>(a.lang + (size_t)gid * 32 + c0);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {   // unmasked (gid 0 is a valid row), zeroed after
+                        const float4 v = r[q];
+                        f[4 * q] = v.x; f[4 * q + 1] = v.y; f[4 * q + 2] = v.z; f[4 * q + 3] = v.w;
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) f[j] = (ok && c0 + j < C) ? a.lang[(size_t)gid * C + c0 + j] : 0.0f;
+                }
+                float2 g_xy = make_float2(0.0f, 0.0f);
+                float4 g_co = make_float4(0.0f, 0.0f, 0.0f, 0.0f), g_rgbd = g_co;
+                uint32_t g_k = 0u;
+                if (lane < MG && lane < cnt) {
+                    const int s = (head + lane) & (MFIFO - 1);
+                    const uint32_t gid = s_fg[s];
+                    g_k = s_fk[s];
+                    g_xy = a.xy[gid];
+                    g_co = a.conic_o[gid];
+                    g_rgbd = a.rgbd[gid];
+                }
+                if (C == 32) {
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) f[j] = ok ? f[j] : 0.0f;
+                }
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    bf16x8 vh, vl;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        __bf16 hh, ll;
+                        split_bf16(f[8 * h + j], hh, ll);
+                        vh[j] = hh;
+                        vl[j] = ll;
+                    }
+                    *reinterpret_cast<bf16x8*>(s_Fh + e * MFP + c0 + 8 * h) = vh;
+                    *reinterpret_cast<bf16x8*>(s_Fl + e * MFP + c0 + 8 * h) = vl;
+                }
+                if (lane < MG) {
+                    s_k[lane] = g_k;
+                    s_X[lane] = g_xy.x; s_Y[lane] = g_xy.y;
+                    s_A[lane] = g_co.x; s_B[lane] = g_co.y; s_C[lane] = g_co.z; s_O[lane] = g_co.w;
+                    s_RG[lane] = lsr_f2{g_rgbd.x, g_rgbd.y};
+                    s_BD[lane] = lsr_f2{g_rgbd.z, g_rgbd.w};
+                }
+            }
+            head += cnt;
+            wave_lds_sync();
+            FWD_STAMP(2);
+            composite(cnt);
+            wave_lds_sync();   // the group's LDS rows are read before the next staging
+            FWD_STAMP(4);
+        }
+    } else {
+        // issue the gathers of FIFO group [head, head + n) into the staging buffers
+        auto issue_dma = [&](int n) __attribute__((always_inline)) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {   // rows: lane -> entry 8 i + lane / 8, 16-byte chunk lane % 8
+                const int e = 8 * i + (lane >> 3);
+                const uint32_t gid = e < n ? s_fg[(head + e) & (MFIFO - 1)] : 0u;   // row 0: valid, weight 0
+                lds_dma16(a.lang + (size_t)gid * 32 + 4 * (lane & 7), lds_addr(s_stage + 256 * i));
+            }
+            const int e = lane & (MG - 1);   // lanes < MG: conic + opacity, lanes >= MG: rgb + depth
+            const uint32_t gid = e < n ? s_fg[(head + e) & (MFIFO - 1)] : 0u;
+            const float* g = reinterpret_cast<const float*>(lane < MG ? a.conic_o : a.rgbd) + (size_t)gid * 4;
+            lds_dma16(g, lds_addr(s_stage + SG_GEO));
+            const float* xy = reinterpret_cast<const float*>(a.xy) + (size_t)gid * 2 + (lane >> 5);   // x, then y
+            lds_dma4(xy, lds_addr(s_stage + SG_XY));
+        };
+        // staged group (count n) -> SoA arrays and bf16 F rows; frees the staging buffers
+        auto relayout = [&](int n) __attribute__((always_inline)) {
+            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the group's LDS-DMA gathers have landed
+            {
+                const int e = lane >> 1, c0 = 16 * (lane & 1);
+                const float4* r = reinterpret_cast<const float4*>(s_stage + e * 32 + c0);
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const float4 v0 = r[2 * h], v1 = r[2 * h + 1];
+                    const float f[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+                    bf16x8 vh, vl;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        __bf16 hh, ll;
+                        split_bf16(f[j], hh, ll);
+                        vh[j] = hh;
+                        vl[j] = ll;
+                    }
+                    *reinterpret_cast<bf16x8*>(s_Fh + e * MFP + c0 + 8 * h) = vh;
+                    *reinterpret_cast<bf16x8*>(s_Fl + e * MFP + c0 + 8 * h) = vl;
+                }
+            }
+            if (lane < MG) {
+                const bool ok = lane < n;
+                const float4* geo = reinterpret_cast<const float4*>(s_stage + SG_GEO);
+                const float4 co = geo[lane], cd = geo[MG + lane];
+                s_k[lane] = ok ? s_fk[(head + lane) & (MFIFO - 1)] : 0u;
+                s_X[lane] = s_stage[SG_XY + lane]; s_Y[lane] = s_stage[SG_XY + MG + lane];
+                s_A[lane] = co.x; s_B[lane] = co.y; s_C[lane] = co.z; s_O[lane] = ok ? co.w : 0.0f;
+                s_RG[lane] = lsr_f2{cd.x, cd.y};
+                s_BD[lane] = lsr_f2{cd.z, cd.w};
+            }
+        };
+        scan_fill(MG);
+        int cnt = min(MG, tail - head);
+        if (cnt > 0) {
+            wave_lds_sync();
+            issue_dma(cnt);
+        }
+        while (cnt > 0) {
+            FWD_STAMP(0);
+            relayout(cnt);
+            head += cnt;
+            wave_lds_sync();
+            FWD_STAMP(1);
+            int next = 0;
+            if (!__all(done)) {   // the next group's gathers fly while this one composites
+                scan_fill(MG);
+                next = min(MG, tail - head);
+                if (next > 0) {
+                    wave_lds_sync();
+                    issue_dma(next);
+                }
+            }
+            FWD_STAMP(2);
+            composite(cnt);
+            wave_lds_sync();   // the group's LDS rows are read before the next relayout
+            FWD_STAMP(4);
+            cnt = __all(done) ? 0 : next;
+        }
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // no LDS-DMA left in flight when the wave ends
     }
+#ifdef LSR_FWD_STAMPS
+    if (lane < 4) {
+        unsigned long long v = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v = lane == k ? st_sum[k] : v;
+        atomicAdd(&g_fwd_stamps[lane], v);
+    }
+    if (lane == 4) atomicAdd(&g_fwd_stamps[4], 1ull);
+#endif
     if (sort_err) {   // a sort's look-back timed out: the lists are invalid, make every output NaN
         const float nan = __builtin_nanf("");
         T = nan;
@@ -285,7 +448,21 @@ k_render_fwd_wave_mfma(RenderFwdArgs a) {
 
 void launch_render_fwd_wave_mfma(const RenderFwdArgs& a, hipStream_t st) {
     const int ntiles = a.grid_x * a.grid_y;
-    hipLaunchKernelGGL(k_render_fwd_wave_mfma, dim3(((ntiles + 7) / 8) * 32), dim3(64), 0, st, a);
+#if LSR_FWD_DMA
+    if (a.C == 32) {
+        hipLaunchKernelGGL(k_render_fwd_wave_mfma<true>, dim3(((ntiles + 7) / 8) * 32), dim3(64), 0, st, a);
+        return;
+    }
+#endif
+    hipLaunchKernelGGL(k_render_fwd_wave_mfma<false>, dim3(((ntiles + 7) / 8) * 32), dim3(64), 0, st, a);
 }
 
 }  // namespace lsr
+
+#ifdef LSR_FWD_STAMPS
+extern "C" int lsr_debug_fwd_stamps(unsigned long long* out5) {
+    if (hipMemcpyFromSymbol(out5, HIP_SYMBOL(lsr::g_fwd_stamps), 5 * sizeof(unsigned long long)) != hipSuccess) return 2;
+    unsigned long long z[8] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(lsr::g_fwd_stamps), z, sizeof(z)) == hipSuccess ? 0 : 2;
+}
+#endif
