@@ -34,6 +34,15 @@ def test_library_exports_every_declared_symbol():
     assert exported == set(declared())
 
 
+def test_library_has_no_undefined_internal_symbols():
+    """Every kernel launch stub the library references is defined in it (a template kernel whose
+    host-side instantiation is dropped leaves an undefined __device_stub__ that only fails at
+    load time on the GPU box)."""
+    from diff_gaussian_rasterization import _lib
+    out = subprocess.run(["nm", "-D", "--undefined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    assert not [l for l in out.splitlines() if "lsr" in l], out
+
+
 def test_library_is_built_for_gfx950():
     from diff_gaussian_rasterization import _lib
     out = subprocess.run(["strings", _lib.LIB_PATH], capture_output=True, text=True).stdout

@@ -46,3 +46,14 @@ def test_radix_sort(tmp_path):
     r = subprocess.run(["timeout", "-k", "5", "120", exe], capture_output=True, text=True)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_lds_dma_row_gather(tmp_path):
+    """LDS-DMA (global_load_lds, 16 B per lane) row gather as the forward compositor's staged
+    variant uses it: lane-linear LDS image, per-lane source rows."""
+    src = os.path.join(ROOT, "tests", "kernels", "t_glds.hip")
+    exe = str(tmp_path / "t_glds")
+    subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-o", exe, src], check=True)
+    r = subprocess.run(["timeout", "-k", "5", "60", exe], capture_output=True, text=True)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
