@@ -15,12 +15,17 @@
 
 namespace lsr {
 
-// Falloff exp for x <= 0: Cody-Waite reduction + degree-7 Horner in fma, exponent assembled by
-// bits.  <= 2 ulp, like CUDA expf; made of correctly rounded operations only (mul, fma, rint) so
-// the host oracle reproduces it bit for bit.
+// Falloff exp for x <= 0: the argument clamped at -87 (exp(-87) ~ 1.6e-38: every alpha built
+// from it is far below 1/255), Cody-Waite reduction + degree-7 Horner in fma, the exponent
+// assembled by bits.  <= 2 ulp above -87, like CUDA expf; made of correctly rounded operations
+// only (max, mul, add, fma) so the host oracle reproduces it bit for bit.  round-to-nearest-even
+// of t = x log2(e) is (t + 1.5 2^23) - 1.5 2^23 (|t| < 2^22), and the low bits of t + 1.5 2^23
+// hold k, so 2^k = bits((t + 1.5 2^23) << 23 + 127 << 23).
+#define LSR_EXP_MAGIC 12582912.0f
 __device__ __forceinline__ float expf_repro(float x) {
-    if (!(x >= -87.0f)) return 0.0f;
-    const float kf = __builtin_rintf(x * 1.44269504088896341f);
+    x = fmaxf(x, -87.0f);
+    const float y = x * 1.44269504088896341f + LSR_EXP_MAGIC;
+    const float kf = y - LSR_EXP_MAGIC;
     float r = __builtin_fmaf(kf, -0.693145751953125f, x);
     r = __builtin_fmaf(kf, -1.428606765330187045e-06f, r);
     float p = 1.98412698412698413e-04f;
@@ -31,17 +36,18 @@ __device__ __forceinline__ float expf_repro(float x) {
     p = __builtin_fmaf(p, r, 0.5f);
     p = __builtin_fmaf(p, r, 1.0f);
     p = __builtin_fmaf(p, r, 1.0f);
-    const int k = (int)kf;
-    return p * __uint_as_float((uint32_t)(k + 127) << 23);
+    return p * __uint_as_float((__float_as_uint(y) << 23) + 0x3F800000u);
 }
 
 // expf_repro of two values at once: the same correctly rounded operations per component, the
-// multiplies and fmas on the packed fp32 pipe (v_pk_mul_f32 / v_pk_fma_f32: two results per
-// instruction), so each component is bit-identical to expf_repro.
+// multiplies, adds and fmas on the packed fp32 pipe (v_pk_mul_f32 / v_pk_add_f32 / v_pk_fma_f32:
+// two results per instruction), so each component is bit-identical to expf_repro.
 typedef float lsr_f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ lsr_f2 expf_repro2(lsr_f2 x) {
+    x = lsr_f2{fmaxf(x.x, -87.0f), fmaxf(x.y, -87.0f)};
     const lsr_f2 t = x * lsr_f2{1.44269504088896341f, 1.44269504088896341f};
-    const lsr_f2 kf = {__builtin_rintf(t.x), __builtin_rintf(t.y)};
+    const lsr_f2 y = t + lsr_f2{LSR_EXP_MAGIC, LSR_EXP_MAGIC};
+    const lsr_f2 kf = y - lsr_f2{LSR_EXP_MAGIC, LSR_EXP_MAGIC};
     lsr_f2 r = __builtin_elementwise_fma(kf, lsr_f2{-0.693145751953125f, -0.693145751953125f}, x);
     r = __builtin_elementwise_fma(kf, lsr_f2{-1.428606765330187045e-06f, -1.428606765330187045e-06f}, r);
     lsr_f2 p = {1.98412698412698413e-04f, 1.98412698412698413e-04f};
@@ -52,10 +58,24 @@ __device__ __forceinline__ lsr_f2 expf_repro2(lsr_f2 x) {
     p = __builtin_elementwise_fma(p, r, lsr_f2{0.5f, 0.5f});
     p = __builtin_elementwise_fma(p, r, lsr_f2{1.0f, 1.0f});
     p = __builtin_elementwise_fma(p, r, lsr_f2{1.0f, 1.0f});
-    const lsr_f2 sc = {__uint_as_float((uint32_t)((int)kf.x + 127) << 23),
-                       __uint_as_float((uint32_t)((int)kf.y + 127) << 23)};
-    const lsr_f2 e = p * sc;
-    return lsr_f2{x.x >= -87.0f ? e.x : 0.0f, x.y >= -87.0f ? e.y : 0.0f};
+    const lsr_f2 sc = {__uint_as_float((__float_as_uint(y.x) << 23) + 0x3F800000u),
+                       __uint_as_float((__float_as_uint(y.y) << 23) + 0x3F800000u)};
+    return p * sc;
+}
+
+// Gaussian falloff exponent at d = (dx, dy) = centre - pixel from the STAGED conic
+// (A, B, C) = (-a/2, -b, -c/2) of the conic (a, b, c) (exact scalings):
+//   power = -(a dx^2 + c dy^2)/2 - b dx dy = dx (A dx + B dy) + (C dy) dy
+// in five correctly rounded operations, two of them fma; the host oracle (orc_power) evaluates
+// the same sequence, so the contributor decisions stay bit-identical.
+__device__ __forceinline__ float gauss_power(float A, float B, float C, float dx, float dy) {
+    return __builtin_fmaf(dx, __builtin_fmaf(A, dx, B * dy), (C * dy) * dy);
+}
+__device__ __forceinline__ lsr_f2 gauss_power2(lsr_f2 A, lsr_f2 B, lsr_f2 C, lsr_f2 dx, lsr_f2 dy) {
+    return __builtin_elementwise_fma(dx, __builtin_elementwise_fma(A, dx, B * dy), (C * dy) * dy);
+}
+__device__ __forceinline__ float4 stage_conic(float4 co) {   // (a, b, c, o) -> (-a/2, -b, -c/2, o)
+    return make_float4(-0.5f * co.x, -co.y, -0.5f * co.z, co.w);
 }
 
 // Power threshold below which alpha = min(0.99, o exp(power)) < 1/255 for certain (margin 1e-3 in

@@ -112,7 +112,7 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
                 const float2 xy = s_xy[j];
                 const float4 co = s_co[j];
                 const float dx = xy.x - pxf, dy = xy.y - pyf;
-                const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+                const float power = gauss_power(-0.5f * co.x, -co.y, -0.5f * co.z, dx, dy);
                 if (power <= 0.0f && power >= s_thr[j]) {
                     const float G = expf_repro(power);
                     const float alpha = fminf(0.99f, co.w * G);

@@ -45,7 +45,7 @@ __device__ unsigned long long g_bwd_stamps[12];
 
 constexpr int WG = 16;       // compacted entries per MFMA group
 constexpr int WFP = 40;      // F row pitch in bf16 (32 channels + 8): 80-byte rows, 16-byte aligned
-constexpr int WGB = 48;      // G row pitch in bf16 at the one-off build: 32 language + 4 rgb/depth + 12 zero
+constexpr int WGB = 48;      // G row pitch in bf16 at the one-off build: 32 language + 16 pad
 constexpr int WWP = 20;      // W / t row pitch in bf16 (16 entries + 4): 40-byte rows, 8-byte aligned
 constexpr int WFIFO = 128;   // compacted entries waiting (list positions and ids); power of two
 
@@ -59,7 +59,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LSR_BWD
 k_render_bwd_wave(RenderBwdArgs a) {
     __shared__ __attribute__((aligned(16))) __bf16 s_FR[64 * WGB];       // G rows (build), then F / W / t rows
     // group entries' screen-space data, one array per field (a b128 read gives 4 entries, a b64
-    // pair the operand of a packed-fp32 instruction): centre X, Y; conic a, b, c; opacity; rgb,
+    // pair the operand of a packed-fp32 instruction): centre X, Y; staged conic -a/2, -b, -c/2 (gauss_power); opacity; rgb,
     // depth; list position k (0xFFFFFFFF past the group: never active)
     __shared__ __attribute__((aligned(16))) float s_X[WG], s_Y[WG], s_A[WG], s_B[WG], s_C[WG], s_O[WG];
     __shared__ __attribute__((aligned(16))) float s_R[WG], s_Gc[WG], s_Bc[WG], s_D[WG];
@@ -101,28 +101,28 @@ k_render_bwd_wave(RenderBwdArgs a) {
         if (a.dL_ddepth) gD = a.dL_ddepth[pid];
     }
 
-    // ---- B fragments, built once through LDS rows [p][c] (c < 32 language, 32..35 rgb + depth):
+    // ---- B fragments, built once through LDS rows [p][c] (c < 32 language channels):
     // b1[pb]     : MFMA1 B,  K = channel 8 g4 + j,       N = pixel 16 pb + l16
-    // b2[kb][nb] : MFMA-W B, K = pixel 32 kb + 8 g4 + j, N = column 16 nb + l16 (nb = 2: rgb, depth)
-    // bm[kb]     : MFMA-T B, K = pixel 32 kb + 8 g4 + j, N = moment l16 (exact small integers)
-    bf16x8 b1h[4], b1l[4], b2h[2][3], b2l[2][3], bm[2];
+    // b2[kb][nb] : MFMA-W B, K = pixel 32 kb + 8 g4 + j, N = channel 16 nb + l16
+    // bm[kb]     : MFMA-T and the rgb / depth part of MFMA-W, K = pixel 32 kb + 8 g4 + j, N = l16:
+    //              the moments {1, x, y, x^2, xy, y^2} (exact small integers) in columns 0..5, the
+    //              pixel's rgb + depth gradients as bf16 hi in 6..9 and lo in 10..13, 0 in 14, 15
+    //              (one fragment for both products: each reads only its own columns)
+    bf16x8 b1h[4], b1l[4], b2h[2][2], b2l[2][2], bm[2];
     {
-        float gl[40];
+        float gl[32];
 #pragma unroll
         for (int c = 0; c < 32; ++c)
             gl[c] = (inside && a.dL_dlang && c < C) ? a.dL_dlang[(size_t)c * HW + pid] : 0.0f;
-        gl[32] = g0; gl[33] = g1; gl[34] = g2; gl[35] = gD;
-#pragma unroll
-        for (int c = 36; c < 40; ++c) gl[c] = 0.0f;
 #pragma unroll
         for (int part = 0; part < 2; ++part) {
 #pragma unroll
-            for (int c8 = 0; c8 < 6; ++c8) {
+            for (int c8 = 0; c8 < 4; ++c8) {
                 bf16x8 v;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     __bf16 h, l;
-                    split_bf16(c8 < 5 ? gl[8 * c8 + j] : 0.0f, h, l);
+                    split_bf16(gl[8 * c8 + j], h, l);
                     v[j] = part == 0 ? h : l;
                 }
                 *reinterpret_cast<bf16x8*>(s_FR + lane * WGB + 8 * c8) = v;
@@ -135,7 +135,7 @@ k_render_bwd_wave(RenderBwdArgs a) {
 #pragma unroll
             for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-                for (int nb = 0; nb < 3; ++nb) {
+                for (int nb = 0; nb < 2; ++nb) {
                     const __bf16* p = s_FR + (32 * kb + 8 * g4 + (l16 >> 2)) * WGB + 16 * nb + 4 * (l16 & 3);
                     const bf16x4 lo4 = ds_read_tr16(p), hi4 = ds_read_tr16(p + 4 * WGB);
                     const bf16x8 v = __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7);
@@ -143,16 +143,31 @@ k_render_bwd_wave(RenderBwdArgs a) {
                 }
             wave_lds_sync();
         }
-        // pixel p = 32 kb + 8 g4 + j has local x = j, y = 4 kb + g4
+        // bm rows [p][n], pitch 16: pixel p = lane has local x = p & 7, y = p >> 3
+        {
+            const float x = (float)(lane & 7), y = (float)(lane >> 3);
+            const float gv[4] = {g0, g1, g2, gD};
+            bf16x8 r0, r1;
+            r0[0] = (__bf16)1.0f; r0[1] = (__bf16)x; r0[2] = (__bf16)y;
+            r0[3] = (__bf16)(x * x); r0[4] = (__bf16)(x * y); r0[5] = (__bf16)(y * y);
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float x = (float)j, y = (float)(4 * kb + g4);
-                const float m = l16 == 0 ? 1.0f : l16 == 1 ? x : l16 == 2 ? y : l16 == 3 ? x * x
-                              : l16 == 4 ? x * y : l16 == 5 ? y * y : 0.0f;
-                bm[kb][j] = (__bf16)m;
+            for (int c = 0; c < 4; ++c) {
+                __bf16 h, l;
+                split_bf16(gv[c], h, l);
+                if (c < 2) r0[6 + c] = h; else r1[c - 2] = h;
+                r1[2 + c] = l;
             }
+            r1[6] = (__bf16)0.0f; r1[7] = (__bf16)0.0f;
+            *reinterpret_cast<bf16x8*>(s_FR + lane * 16) = r0;
+            *reinterpret_cast<bf16x8*>(s_FR + lane * 16 + 8) = r1;
+            wave_lds_sync();
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) {
+                const __bf16* p = s_FR + (32 * kb + 8 * g4 + (l16 >> 2)) * 16 + 4 * (l16 & 3);
+                bm[kb] = __builtin_shufflevector(ds_read_tr16(p), ds_read_tr16(p + 4 * 16), 0, 1, 2, 3, 4, 5, 6, 7);
+            }
+            wave_lds_sync();
+        }
     }
     __bf16* s_Fh = s_FR;              // F rows [e][c] of the group (MFMA1 A), hi
     __bf16* s_Fl = s_FR + WG * WFP;   // lo
@@ -167,16 +182,16 @@ k_render_bwd_wave(RenderBwdArgs a) {
     int pos = (int)nrep;     // list positions [0, pos) not yet scanned
     int head = 0, tail = 0;  // FIFO counters (wave-uniform)
     // scan prefetch: point-list words (id | quadrant bits) of the round at positions
-    // [pos - 64, pos) and of the round after it
-    uint32_t sc_w = pos - 64 + lane >= 0 ? *at32(a.point_list, range.x + pos - 64 + lane) : 0u;
-    uint32_t sc_nw = pos - 128 + lane >= 0 ? *at32(a.point_list, range.x + pos - 128 + lane) : 0u;
+    // [pos - 64, pos), loaded at the end of the round before (one register, no rotation: a copy
+    // of a register whose load is in flight makes hipcc wait for every outstanding load and atomic)
+    // The loads are unconditional (positions clamped to 0, a valid entry; k < 0 is masked at use):
+    // a conditional load would also become a register copy.
+    uint32_t sc_w = *at32(a.point_list, range.x + max(pos - 64 + lane, 0));
     // scan rounds until `want` entries wait in the FIFO or the range is exhausted
     auto scan_fill = [&](int want) {
         while (tail - head < want && pos > 0) {
             const int k = pos - 64 + lane;       // this round's positions (k < 0: before the list)
             const uint32_t word = sc_w;
-            sc_w = sc_nw;
-            sc_nw = k - 128 >= 0 ? *at32(a.point_list, range.x + k - 128) : 0u;
             const uint32_t gid = word & PL_ID_MASK;
             const bool cand = k >= 0 && ((word >> (PL_QUAD_SHIFT + quad)) & 1u);
             const uint64_t m = __ballot(cand);
@@ -188,6 +203,7 @@ k_render_bwd_wave(RenderBwdArgs a) {
             }
             tail += __popcll(m);
             pos = max(pos - 64, 0);
+            sc_w = *at32(a.point_list, range.x + max(k - 64, 0));
         }
         wave_lds_sync();
     };
@@ -230,7 +246,7 @@ k_render_bwd_wave(RenderBwdArgs a) {
             s_gid[lane] = pf.gid;
             s_k[lane] = pf.k;
             s_X[lane] = pf.xy.x; s_Y[lane] = pf.xy.y;
-            s_A[lane] = pf.co.x; s_B[lane] = pf.co.y; s_C[lane] = pf.co.z; s_O[lane] = pf.co.w;
+            s_A[lane] = -0.5f * pf.co.x; s_B[lane] = -pf.co.y; s_C[lane] = -0.5f * pf.co.z; s_O[lane] = pf.co.w;
             s_R[lane] = pf.rgbd.x; s_Gc[lane] = pf.rgbd.y; s_Bc[lane] = pf.rgbd.z; s_D[lane] = pf.rgbd.w;
         }
         const int e = lane >> 2, c0 = 8 * (lane & 3);
@@ -273,6 +289,10 @@ k_render_bwd_wave(RenderBwdArgs a) {
             sv[r] = s_q[e][q];
             so[r] = s_agid[e] * (uint32_t)ACC_PITCH + q;
         }
+        // A branch-free variant (every lane, zeros for idle lanes, so that hipcc could count the
+        // atomics and skip them in its waits for later loads) measured 0.70 vs 0.50 ms: with no
+        // wait behind them a wave keeps several groups of atomics in flight and the memory
+        // system backs up.  The wait that follows each batch throttles them.
 #ifndef LSR_ABL_NOLANGATOM
         if (a.acc_lang) {   // 128-byte rows
 #pragma unroll
@@ -351,7 +371,7 @@ k_render_bwd_wave(RenderBwdArgs a) {
             const uint2 kk = *reinterpret_cast<const uint2*>(s_k + e0);
             // the forward's operation order per component (bit-identical alpha decisions)
             const lsr_f2 dx = X - px2, dy = Y - py2;
-            const lsr_f2 pw = -0.5f * (A * dx * dx + Cc * dy * dy) - B * dx * dy;
+            const lsr_f2 pw = gauss_power2(A, B, Cc, dx, dy);
 #ifdef LSR_ABL_NOEXP
             const lsr_f2 ge = {fmaxf(1.0f + pw.x, 0.0f), fmaxf(1.0f + pw.y, 0.0f)};   // timing ablation only
 #else
@@ -415,7 +435,8 @@ k_render_bwd_wave(RenderBwdArgs a) {
             ah = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
             al = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
         };
-        // MFMA-W: dacc[nb][i] at lane (g4, c) = sum_p w[p][4 g4 + i] Gx[p][16 nb + c]
+        // MFMA-W: dacc[nb][i] at lane (g4, c) = sum_p w[p][4 g4 + i] G[p][16 nb + c] (language);
+        //         dacc[2][i] at lane (g4, n) = sum_p w[p][4 g4 + i] bm[p][n] (n = 6..13: rgb / depth hi, lo)
         f32x4 dacc[3] = {f32x4{0.0f, 0.0f, 0.0f, 0.0f}, f32x4{0.0f, 0.0f, 0.0f, 0.0f}, f32x4{0.0f, 0.0f, 0.0f, 0.0f}};
         write_rows(wv);
 #pragma unroll
@@ -423,11 +444,13 @@ k_render_bwd_wave(RenderBwdArgs a) {
             bf16x8 ah, al;
             read_a(kb, ah, al);
 #pragma unroll
-            for (int nb = 0; nb < 3; ++nb) {
+            for (int nb = 0; nb < 2; ++nb) {
                 dacc[nb] = LSR_MFMA16(ah, b2h[kb][nb], dacc[nb]);
                 dacc[nb] = LSR_MFMA16(ah, b2l[kb][nb], dacc[nb]);
                 dacc[nb] = LSR_MFMA16(al, b2h[kb][nb], dacc[nb]);
             }
+            dacc[2] = LSR_MFMA16(ah, bm[kb], dacc[2]);   // w hi and lo times g hi (6..9) and lo (10..13)
+            dacc[2] = LSR_MFMA16(al, bm[kb], dacc[2]);
         }
         wave_lds_sync();   // W rows read before t overwrites them
         // MFMA-T: dmom[i] at lane (g4, n) = sum_p t[p][4 g4 + i] moment_n(p)
@@ -444,9 +467,14 @@ k_render_bwd_wave(RenderBwdArgs a) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) s_mom[4 * g4 + i][l16] = dmom[i];
         }
-        if (l16 < 4) {
+        {   // rgb 0-2, depth 3: hi column 6 + c plus lo column 10 + c
+            float v[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) s_q[4 * g4 + i][l16] = dacc[2][i];   // rgb 0-2, depth 3
+            for (int i = 0; i < 4; ++i) v[i] = dacc[2][i] + __shfl_down(dacc[2][i], 4, 16);
+            if (l16 >= 6 && l16 < 10) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) s_q[4 * g4 + i][l16 - 6] = v[i];
+            }
         }
         BWD_STAMP(7);
         // stage the group's results: language rows from the MFMA layout, gids
@@ -461,7 +489,7 @@ k_render_bwd_wave(RenderBwdArgs a) {
             const float M0 = s_mom[e][0], Mx = s_mom[e][1], My = s_mom[e][2];
             const float Mxx = s_mom[e][3], Mxy = s_mom[e][4], Myy = s_mom[e][5];
             const float2 xy = make_float2(s_X[e], s_Y[e]);
-            const float4 co = make_float4(s_A[e], s_B[e], s_C[e], s_O[e]);
+            const float4 co = make_float4(-2.0f * s_A[e], -s_B[e], -2.0f * s_C[e], s_O[e]);   // staged (-a/2, -b, -c/2)
             const float X = xy.x - bx0, Y = xy.y - by0;      // quadrant-local centre
             const float Sdx = X * M0 - Mx, Sdy = Y * M0 - My;
             const float Sdxdx = X * X * M0 - 2.0f * X * Mx + Mxx;

@@ -69,7 +69,7 @@ __global__ void __launch_bounds__(256) k_render_fwd(RenderFwdArgs a) {
             const float2 xy = s_xy[j];
             const float4 co = s_co[j];
             const float dx = xy.x - pxf, dy = xy.y - pyf;
-            const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+            const float power = gauss_power(-0.5f * co.x, -co.y, -0.5f * co.z, dx, dy);
             if (power > 0.0f || power < s_thr[j]) continue;   // the second test never changes a decision
             const float alpha = fminf(0.99f, co.w * expf_repro(power));
             if (alpha < 1.0f / 255.0f) continue;
@@ -224,7 +224,7 @@ __global__ void __launch_bounds__(256) k_render_fwd_mfma(RenderFwdArgs a) {
                     const float2 xy = s_xy[j];
                     const float4 co = s_co[j];
                     const float dx = xy.x - pxf, dy = xy.y - pyf;
-                    const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+                    const float power = gauss_power(-0.5f * co.x, -co.y, -0.5f * co.z, dx, dy);
                     if (!(power > 0.0f || power < s_thr[j])) {
                         const float alpha = fminf(0.99f, co.w * expf_repro(power));
                         if (alpha >= 1.0f / 255.0f) {

@@ -84,7 +84,7 @@ __global__ void __launch_bounds__(64) k_render_fwd_wave(RenderFwdArgs a) {
             const float4 co = ok ? a.conic_o[gid] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             s_k[lane] = ok ? s_fk[s] : 0u;
             s_xy[lane] = ok ? a.xy[gid] : make_float2(0.0f, 0.0f);
-            s_co[lane] = co;
+            s_co[lane] = stage_conic(co);   // (-a/2, -b, -c/2, o): gauss_power's operands
             s_rgbd[lane] = ok ? a.rgbd[gid] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         }
         if constexpr (CPAD > 0) {
@@ -127,7 +127,7 @@ __global__ void __launch_bounds__(64) k_render_fwd_wave(RenderFwdArgs a) {
                 const float2 xy = s_xy[e0 + u];
                 const float4 co = s_co[e0 + u];
                 const float dx = xy.x - pxf, dy = xy.y - pyf;
-                pw[u] = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+                pw[u] = gauss_power(co.x, co.y, co.z, dx, dy);
             }
 #pragma unroll
             for (int u = 0; u < FB; u += 2) {   // two entries per packed-fp32 exp

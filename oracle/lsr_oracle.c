@@ -38,9 +38,10 @@
  *
  * Floating point
  *   Compiled with -ffp-contract=off.  exp() of the Gaussian falloff uses orc_exp, a
- *   Cody-Waite + degree-7 Horner exp (<= 2 ulp) written only with IEEE *, fmaf, rint and exponent
- *   bit assembly, so that the product kernels can reproduce the contributor decisions
- *   (alpha < 1/255, T < 1e-4) bit for bit.  The CUDA original uses expf (<= 2 ulp as well).
+ *   Cody-Waite + degree-7 Horner exp (<= 2 ulp) written only with IEEE max, *, +, fmaf and
+ *   exponent bit assembly, and the falloff exponent is orc_power (two fmaf), so that the product
+ *   kernels reproduce the contributor decisions (alpha < 1/255, T < 1e-4) bit for bit.  The CUDA
+ *   original uses expf (<= 2 ulp as well) and nvcc's default fma contraction.
  */
 #include <math.h>
 #include <stdint.h>
@@ -65,11 +66,15 @@ typedef float real;
 #define RCEIL ceilf
 #define RMIN fminf
 #define RMAX fmaxf
-/* exp for x <= 0; bit-reproducible with the HIP kernels' expf_repro (fmaf is correctly rounded on
- * both sides, so the sequence of roundings is identical). */
+/* exp for x <= 0; bit-reproducible with the HIP kernels' expf_repro (lsr_common.h): the same
+ * sequence of correctly rounded operations (fmaxf, *, +, fmaf).  The argument is clamped at -87
+ * (every alpha from exp(-87) ~ 1.6e-38 is far below 1/255); rint(x log2 e) is computed as
+ * (t + 1.5 2^23) - 1.5 2^23 and 2^k assembled from the low bits of t + 1.5 2^23. */
 static inline float orc_exp(float x) {
-    if (!(x >= -87.0f)) return 0.0f;
-    const float kf = rintf(x * 1.44269504088896341f);
+    x = fmaxf(x, -87.0f);
+    const float t = x * 1.44269504088896341f;
+    const float y = t + 12582912.0f;
+    const float kf = y - 12582912.0f;
     float r = fmaf(kf, -0.693145751953125f, x);
     r = fmaf(kf, -1.428606765330187045e-06f, r);
     float p = 1.98412698412698413e-04f;  /* 1/5040 */
@@ -80,12 +85,24 @@ static inline float orc_exp(float x) {
     p = fmaf(p, r, 0.5f);
     p = fmaf(p, r, 1.0f);
     p = fmaf(p, r, 1.0f);
-    const int k = (int)kf;
-    union { uint32_t u; float f; } s;
-    s.u = (uint32_t)(k + 127) << 23;
+    union { uint32_t u; float f; } yb, s;
+    yb.f = y;
+    s.u = (yb.u << 23) + 0x3F800000u;
     return p * s.f;
 }
 #endif
+
+/* Gaussian falloff exponent at d = (dx, dy) = centre - pixel:
+ *   power = -(a dx^2 + c dy^2)/2 - b dx dy = dx (A dx + B dy) + (C dy) dy,  (A, B, C) = (-a/2, -b, -c/2)
+ * the HIP kernels' gauss_power (lsr_common.h) operation for operation (the scalings are exact). */
+static inline real orc_power(const real *co, real dx, real dy) {
+    const real A = R(-0.5) * co[0], B = -co[1], Cq = R(-0.5) * co[2];
+#ifdef ORC_DOUBLE
+    return fma(dx, fma(A, dx, B * dy), (Cq * dy) * dy);
+#else
+    return fmaf(dx, fmaf(A, dx, B * dy), (Cq * dy) * dy);
+#endif
+}
 
 #define BLOCK_X 16
 #define BLOCK_Y 16
@@ -383,7 +400,7 @@ orc_state *orc_forward(const orc_settings *s, int P, int M, int C,
                     const uint32_t g = st->point_list[k];
                     const real *xy = st->xy + 2 * (size_t)g, *co = st->conic_o + 4 * (size_t)g;
                     const real dx = xy[0] - (real)px, dy = xy[1] - (real)py;
-                    const real power = R(-0.5) * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                    const real power = orc_power(co, dx, dy);
                     if (power > R(0.0)) continue;
                     const real alpha = RMIN(R(0.99), co[3] * orc_exp(power));
                     if (alpha < R(1.0) / R(255.0)) continue;
@@ -636,7 +653,7 @@ void orc_backward(const orc_state *st, const orc_settings *s,
                     const uint32_t g = st->point_list[kk - 1];
                     const real *xy = st->xy + 2 * (size_t)g, *co = st->conic_o + 4 * (size_t)g;
                     const real dx = xy[0] - (real)px, dy = xy[1] - (real)py;
-                    const real power = R(-0.5) * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                    const real power = orc_power(co, dx, dy);
                     if (power > R(0.0)) continue;
                     const real G = orc_exp(power);
                     const real alpha = RMIN(R(0.99), co[3] * G);
