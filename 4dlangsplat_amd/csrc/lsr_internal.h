@@ -261,14 +261,19 @@ size_t radix_temp_bytes(size_t n);
 // stable LSD sort of (key, value) pairs on bits [begin_bit, end_bit); returns true when the result
 // is in (keys_b, vals_b).  err (device word, may be null) is set non-zero if a look-back timed out.
 // temp_zeroed: the caller already zeroed the first radix_temp_zero_bytes(n, begin, end) bytes of temp
+// kept (device word, may be null, reduce-then-scan build only): the first pass drops every key
+// equal to 0xFFFFFFFF and writes the number of kept keys here; the later passes sort only those,
+// so the output holds the kept pairs in [0, *kept) (the rest of the buffers is left as it was).
 bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b, size_t n,
-                      int begin_bit, int end_bit, void* temp, uint32_t* err, hipStream_t st, bool temp_zeroed = false);
+                      int begin_bit, int end_bit, void* temp, uint32_t* err, hipStream_t st, bool temp_zeroed = false,
+                      uint32_t* kept = nullptr);
 size_t radix_temp_zero_bytes(size_t n, int begin_bit, int end_bit);
 
 // binning (binning.hip)
 void launch_iota(int n, uint32_t* out, hipStream_t st);
-void launch_gather_tile_counts(int P, const uint32_t* order, const uint2* rect, uint32_t* counts, uint2* rect_sorted,
-                               hipStream_t st);
+// ranks r >= *nsorted (device word, may be null) get count 0 (the depth sort dropped culled keys)
+void launch_gather_tile_counts(int P, const uint32_t* nsorted, const uint32_t* order, const uint2* rect, uint32_t* counts,
+                               uint2* rect_sorted, hipStream_t st);
 // Point-list values: Gaussian id in the low 28 bits, in the top 4 the quadrants (bit 28 + q,
 // q = (y >= 8) * 2 + (x >= 8) inside the 16x16 tile) the splat may reach (quad_may_touch); an
 // instance reaching none gets tile key ntiles and sorts past every list.

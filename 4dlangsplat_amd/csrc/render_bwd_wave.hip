@@ -524,22 +524,35 @@ k_render_bwd_wave(RenderBwdArgs a) {
 // buckets the tiles by their replay bound (tile_max_contrib, written by the forward) in
 // descending order: a counting sort over 1024 buckets of 2 replay entries.  The order inside a
 // bucket is not fixed, which only permutes float atomic summation (this path is non-deterministic).
+// LSR_TILE_ORDER_BANDS: slot s runs on XCD s mod 8 (the compositors' block -> slot map), so the
+// tiles are cut into 8 contiguous raster bands, band x sorted longest-first onto the slots
+// s = x (mod 8): each XCD's L2 then serves one region of the image (neighbouring tiles share
+// Gaussians: their records and accumulator rows) instead of every XCD touching all of it.
 constexpr int ORDER_BUCKETS = 1024;
 __global__ void __launch_bounds__(1024) k_tile_order(int ntiles, const uint32_t* __restrict__ tile_max,
                                                      const uint2* __restrict__ ranges, uint32_t* __restrict__ order) {
     __shared__ uint32_t s_cnt[ORDER_BUCKETS];
     __shared__ uint32_t s_wave[16];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#ifdef LSR_TILE_ORDER_BANDS
+    // band x = blockIdx.x: its size is the number of slots s < ntiles with s = x (mod 8)
+    const int x = blockIdx.x;
+    int t0 = 0;
+    for (int y = 0; y < x; ++y) t0 += (ntiles - y + 7) / 8;
+    const int nb = (ntiles - x + 7) / 8, t1 = t0 + nb;
+#else
+    const int x = 0, t0 = 0, t1 = ntiles;
+#endif
     s_cnt[tid] = 0;
     __syncthreads();
     auto bucket = [&](int t) {
         const uint32_t cost = ranges ? (ranges[t].y - ranges[t].x) >> 2 : tile_max[t] >> 1;
         return ORDER_BUCKETS - 1 - (int)min(cost, (uint32_t)ORDER_BUCKETS - 1);
     };
-    for (int t = tid; t < ntiles; t += 1024) atomicAdd(&s_cnt[bucket(t)], 1u);
+    for (int t = t0 + tid; t < t1; t += 1024) atomicAdd(&s_cnt[bucket(t)], 1u);
     __syncthreads();
-    const uint32_t x = s_cnt[tid];
-    uint32_t inc = x;
+    const uint32_t v = s_cnt[tid];
+    uint32_t inc = v;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t y = __shfl_up(inc, o);
@@ -549,13 +562,22 @@ __global__ void __launch_bounds__(1024) k_tile_order(int ntiles, const uint32_t*
     __syncthreads();
     uint32_t off = 0;
     for (int w = 0; w < wave; ++w) off += s_wave[w];
-    s_cnt[tid] = off + inc - x;   // exclusive start of bucket tid
+    s_cnt[tid] = off + inc - v;   // exclusive start of bucket tid
     __syncthreads();
+#ifdef LSR_TILE_ORDER_BANDS
+    for (int t = t0 + tid; t < t1; t += 1024) order[8 * atomicAdd(&s_cnt[bucket(t)], 1u) + x] = (uint32_t)t;
+#else
+    (void)x;
     for (int t = tid; t < ntiles; t += 1024) order[atomicAdd(&s_cnt[bucket(t)], 1u)] = (uint32_t)t;
+#endif
 }
 
 void launch_tile_order(int ntiles, const uint32_t* tile_max, const uint2* ranges, uint32_t* order, hipStream_t st) {
+#ifdef LSR_TILE_ORDER_BANDS
+    hipLaunchKernelGGL(k_tile_order, dim3(8), dim3(1024), 0, st, ntiles, tile_max, ranges, order);
+#else
     hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, st, ntiles, tile_max, ranges, order);
+#endif
 }
 
 void launch_render_bwd_wave(const RenderBwdArgs& a, hipStream_t st) {

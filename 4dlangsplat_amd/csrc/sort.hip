@@ -341,12 +341,21 @@ __global__ void __launch_bounds__(256) k_radix_pass(const uint32_t* __restrict__
 // hop (each an agent-scope round trip through the fabric, ~0.5-1 us), which bounded a pass by
 // the chain length; here the keys are read once more (4 B / key) and two small launches are
 // added per pass.
-__global__ void __launch_bounds__(256) k_rts_count(const uint32_t* __restrict__ keys, size_t n, int shift, int nbits,
+//   drop (first pass of a sort with a kept-count word): keys equal to 0xFFFFFFFF are not counted
+//   and not placed; the scatter's block 0 writes the number of kept keys to *kept_out.
+//   n_dev (later passes): the number of keys is *n_dev (<= n); blocks past it write zero counts
+//   and place nothing.
+__device__ __forceinline__ size_t rts_n(size_t n, const uint32_t* n_dev) {
+    return n_dev ? min(n, (size_t)*n_dev) : n;
+}
+__global__ void __launch_bounds__(256) k_rts_count(const uint32_t* __restrict__ keys, size_t n,
+                                                   const uint32_t* __restrict__ n_dev, int drop, int shift, int nbits,
                                                    uint32_t* __restrict__ counts) {
     __shared__ uint32_t s_h[4][256];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
 #pragma unroll
     for (int w = 0; w < 4; ++w) s_h[w][tid] = 0;
+    n = rts_n(n, n_dev);
     __syncthreads();
     const uint32_t mask = (1u << nbits) - 1u;
     const uint64_t lt = lanemask_lt();
@@ -359,7 +368,7 @@ __global__ void __launch_bounds__(256) k_rts_count(const uint32_t* __restrict__ 
     }
 #pragma unroll
     for (int r = 0; r < OS_ITEMS; ++r) {
-        const bool valid = base + (size_t)r * 64 + lane < n;
+        const bool valid = base + (size_t)r * 64 + lane < n && !(drop && key[r] == 0xFFFFFFFFu);
         const uint32_t d = (key[r] >> shift) & mask;
         const uint64_t peers = match_digit(d, valid, nbits);
         if (valid && (peers & lt) == 0) s_h[wave][d] += (uint32_t)__popcll(peers);   // one leader per digit
@@ -397,7 +406,8 @@ __global__ void __launch_bounds__(256) k_rts_scan(uint32_t* __restrict__ counts,
 __global__ void __launch_bounds__(256) k_rts_scatter(const uint32_t* __restrict__ keys_in,
                                                      const uint32_t* __restrict__ vals_in,
                                                      uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
-                                                     size_t n, int shift, int nbits,
+                                                     size_t n, const uint32_t* __restrict__ n_dev, int drop,
+                                                     uint32_t* __restrict__ kept_out, int shift, int nbits,
                                                      const uint32_t* __restrict__ totals,
                                                      const uint32_t* __restrict__ offs) {
     __shared__ uint32_t s_key[OS_TILE];
@@ -410,6 +420,7 @@ __global__ void __launch_bounds__(256) k_rts_scatter(const uint32_t* __restrict_
     const uint32_t bid = blockIdx.x;
 #pragma unroll
     for (int w = 0; w < 4; ++w) s_wcnt[w][tid] = 0;
+    n = rts_n(n, n_dev);
     __syncthreads();
     const uint32_t mask = (1u << nbits) - 1u;
     const uint64_t lt = lanemask_lt();
@@ -427,7 +438,7 @@ __global__ void __launch_bounds__(256) k_rts_scatter(const uint32_t* __restrict_
     const uint32_t hcount = totals[tid];
 #pragma unroll
     for (int r = 0; r < OS_ITEMS; ++r) {
-        const bool valid = base + (size_t)r * 64 + lane < n;
+        const bool valid = base + (size_t)r * 64 + lane < n && !(drop && key[r] == 0xFFFFFFFFu);
         const uint32_t d = (key[r] >> shift) & mask;
         const uint64_t peers = match_digit(d, valid, nbits);
         const uint32_t before = s_wcnt[wave][d];
@@ -445,12 +456,15 @@ __global__ void __launch_bounds__(256) k_rts_scatter(const uint32_t* __restrict_
     const uint32_t lbase = block_excl_scan256(total, s_wave);        // local start of digit tid
     s_lbase[tid] = lbase;
     s_gbase[tid] = dstart + prefix - lbase;
+    if (tid == 255) {
+        s_wave[0] = lbase + total;                                    // keys this block places
+        if (kept_out && bid == 0) *kept_out = dstart + hcount;        // keys kept over all blocks
+    }
     __syncthreads();
-    const size_t tile0 = (size_t)bid * OS_TILE;
-    const int ntile = (int)min((size_t)OS_TILE, n - min(n, tile0));
+    const int ntile = (int)s_wave[0];
 #pragma unroll
     for (int r = 0; r < OS_ITEMS; ++r) {
-        const bool valid = base + (size_t)r * 64 + lane < n;
+        const bool valid = base + (size_t)r * 64 + lane < n && !(drop && key[r] == 0xFFFFFFFFu);
         if (valid) {
             const uint32_t d = (key[r] >> shift) & mask;
             const uint32_t pos = s_lbase[d] + s_wcnt[wave][d] + rank[r];
@@ -482,7 +496,8 @@ size_t radix_temp_zero_bytes(size_t n, int begin_bit, int end_bit) {
 }
 
 bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b, size_t n,
-                      int begin_bit, int end_bit, void* temp, uint32_t* err, hipStream_t st, bool temp_zeroed) {
+                      int begin_bit, int end_bit, void* temp, uint32_t* err, hipStream_t st, bool temp_zeroed,
+                      uint32_t* kept) {
     if (n == 0 || end_bit <= begin_bit) return false;
     const size_t nb = os_blocks(n);
     uint32_t* hist = reinterpret_cast<uint32_t*>(temp);
@@ -504,14 +519,18 @@ bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint
         uint32_t* kout = in_b ? keys_a : keys_b;
         uint32_t* vout = in_b ? vals_a : vals_b;
         uint32_t* cnt = status + (size_t)p_ * nb * 256;
-        hipLaunchKernelGGL(k_rts_count, dim3((unsigned)nb), dim3(256), 0, st, kin, n, shift, nbits, cnt);
+        const int drop = kept && p_ == 0;                       // first pass drops, later passes read
+        const uint32_t* n_dev = kept && p_ > 0 ? kept : nullptr;   // the kept count
+        hipLaunchKernelGGL(k_rts_count, dim3((unsigned)nb), dim3(256), 0, st, kin, n, n_dev, drop, shift, nbits, cnt);
         hipLaunchKernelGGL(k_rts_scan, dim3(256), dim3(256), 0, st, cnt, (int)nb, hist + p_ * 256);
-        hipLaunchKernelGGL(k_rts_scatter, dim3((unsigned)nb), dim3(256), 0, st, kin, vin, kout, vout, n, shift, nbits,
-                           (const uint32_t*)(hist + p_ * 256), (const uint32_t*)cnt);
+        hipLaunchKernelGGL(k_rts_scatter, dim3((unsigned)nb), dim3(256), 0, st, kin, vin, kout, vout, n, n_dev, drop,
+                           drop ? kept : (uint32_t*)nullptr, shift, nbits, (const uint32_t*)(hist + p_ * 256),
+                           (const uint32_t*)cnt);
         in_b = !in_b;
     }
     return in_b;
 #else
+    if (kept) (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(kept), (int)n, 1, st);   // no dropping here
     const unsigned hb = (unsigned)min((size_t)OS_HIST_BLOCKS, (n + 64 * HIST_ITEMS * 4 - 1) / (64 * HIST_ITEMS * 4));
     hipLaunchKernelGGL(k_radix_hist, dim3(hb), dim3(256), 0, st, (const uint32_t*)keys_a, n, begin_bit, end_bit, hist);
 #endif
