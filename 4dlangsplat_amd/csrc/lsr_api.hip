@@ -288,6 +288,7 @@ int lsr_forward_preprocess_async(const lsr_settings* s, const lsr_fwd_in* in, ls
     // accumulator rows of listed Gaussians, and clears the sort workspace and the counters
     // [0] K, [1] depth sort error word, [2] tile sort error word: no separate fill launches
     a.order = g.val_a;
+    a.rank_counts = lsr::radix_sort_fuses_gather() ? g.counts : nullptr;
     a.acc = g.acc;
     a.clear.p[0] = reinterpret_cast<uint32_t*>(g.sort_tmp);
     a.clear.n[0] = (uint32_t)(lsr::radix_temp_zero_bytes((size_t)P, 0, 32) / 4);
@@ -304,15 +305,19 @@ int lsr_forward_preprocess_async(const lsr_settings* s, const lsr_fwd_in* in, ls
         PhaseTimer t(LSR_PHASE_DEPTH_SORT, st);
         // culled Gaussians (key 0xFFFFFFFF) are dropped by the first pass: the visible count goes
         // to g.total[3] and only those are sorted (and gathered below)
+        // ... and its last pass writes the depth-ranked rectangles and instance counts (the ranks
+        // of culled Gaussians keep the zero counts the preprocess wrote)
+        const lsr::SortGather gather{g.rect, g.counts, g.rect_sorted};
         in_b = lsr::radix_sort_pairs(g.key_a, g.val_a, g.key_b, g.val_b, (size_t)P, 0, 32, g.sort_tmp, g.total + 1, st,
-                                     /*temp_zeroed=*/true, g.total + 3);
+                                     /*temp_zeroed=*/true, g.total + 3, &gather);
     }
     if (in_b != (bool)depth_sort_result_in_b()) return fail(LSR_EHIP, "internal: depth sort parity");
     if (g_inject_sort_fault.load() & 1u) LSR_HIP(hipMemsetAsync(g.total + 1, 1, 1, st));   // test hook
     LSR_LAUNCHED("depth sort", st, s->debug);
     {
         PhaseTimer t(LSR_PHASE_INSTANCE_SCAN, st);
-        lsr::launch_gather_tile_counts(P, g.total + 3, g.val_a, g.rect, g.counts, g.rect_sorted, st);
+        if (!lsr::radix_sort_fuses_gather())
+            lsr::launch_gather_tile_counts(P, g.total + 3, g.val_a, g.rect, g.counts, g.rect_sorted, st);
         lsr::exclusive_scan_u32(g.counts, g.offsets, (size_t)P, g.total, g.scan_tmp, st);
     }
     LSR_LAUNCHED("instance scan", st, s->debug);

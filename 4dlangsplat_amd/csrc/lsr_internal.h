@@ -65,6 +65,8 @@ struct PreprocessArgs {
     float4* rgbd;
     uint8_t* clamped;
     uint32_t* order;  // if set: order[i] = i (the depth sort's initial values)
+    uint32_t* rank_counts;   // if set: zeroed (per depth rank instance counts; the sort's last
+                             // pass fills the visible ranks, the culled ones stay 0)
     float4* acc;      // if set: [P, ACC_PITCH / 4] backward accumulators, zeroed for visible rows
     ClearList clear;  // zeroed on the side (sort workspace, counters)
 };
@@ -264,9 +266,17 @@ size_t radix_temp_bytes(size_t n);
 // kept (device word, may be null, reduce-then-scan build only): the first pass drops every key
 // equal to 0xFFFFFFFF and writes the number of kept keys here; the later passes sort only those,
 // so the output holds the kept pairs in [0, *kept) (the rest of the buffers is left as it was).
+// gather (reduce-then-scan build, radix_sort_fuses_gather()): the last pass also writes, per
+// output position, rect_sorted = rect[value] and counts = rect_count of it, and not the keys.
+struct SortGather {
+    const uint2* rect;
+    uint32_t* counts;
+    uint2* rect_sorted;
+};
+bool radix_sort_fuses_gather();
 bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b, size_t n,
                       int begin_bit, int end_bit, void* temp, uint32_t* err, hipStream_t st, bool temp_zeroed = false,
-                      uint32_t* kept = nullptr);
+                      uint32_t* kept = nullptr, const SortGather* gather = nullptr);
 size_t radix_temp_zero_bytes(size_t n, int begin_bit, int end_bit);
 
 // binning (binning.hip)

@@ -112,6 +112,7 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
     a.rect[i] = make_uint2(0u, 0u);
     a.clamped[i] = 0;
     if (a.order) a.order[i] = (uint32_t)i;
+    if (a.rank_counts) a.rank_counts[i] = 0u;
     if (a.key) a.key[i] = 0xFFFFFFFFu;
     const float3 p = make_float3(a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]);
     const float4 ph = xform4x4(a.proj, p);
@@ -238,7 +239,11 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
         for (int k = 0; k < ACC_PITCH / 4; ++k) r[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
     uint32_t qmap = 0;   // quadrant map of a rectangle of <= 2 x 2 tiles (the binning's emit_quad_mask)
+#ifdef LSR_ABL_NOQMAP
+    if (false) {   // timing ablation only (instances of small rectangles then reach no quadrant)
+#else
     if (ntiles > 0 && cmax.x - cmin.x <= 2 && cmax.y - cmin.y <= 2) {
+#endif
         const EmitSplat es = emit_splat(pix, conic);
         for (int ty = cmin.y; ty < cmax.y; ++ty)
             for (int tx = cmin.x; tx < cmax.x; ++tx) {

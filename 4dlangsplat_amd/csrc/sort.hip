@@ -409,7 +409,7 @@ __global__ void __launch_bounds__(256) k_rts_scatter(const uint32_t* __restrict_
                                                      size_t n, const uint32_t* __restrict__ n_dev, int drop,
                                                      uint32_t* __restrict__ kept_out, int shift, int nbits,
                                                      const uint32_t* __restrict__ totals,
-                                                     const uint32_t* __restrict__ offs) {
+                                                     const uint32_t* __restrict__ offs, SortGather gather) {
     __shared__ uint32_t s_key[OS_TILE];
     __shared__ uint32_t s_val[OS_TILE];
     __shared__ uint32_t s_wcnt[4][256];
@@ -473,6 +473,17 @@ __global__ void __launch_bounds__(256) k_rts_scatter(const uint32_t* __restrict_
         }
     }
     __syncthreads();
+    if (gather.rect) {   // last pass of the depth sort: the counts gather instead of the keys
+        for (int i = tid; i < ntile; i += 256) {
+            const uint32_t k = s_key[i], v = s_val[i];
+            const uint32_t dst = s_gbase[(k >> shift) & mask] + (uint32_t)i;
+            const uint2 rc = gather.rect[v];
+            vals_out[dst] = v;
+            gather.rect_sorted[dst] = rc;
+            gather.counts[dst] = rect_count(rc);
+        }
+        return;
+    }
     for (int i = tid; i < ntile; i += 256) {
         const uint32_t k = s_key[i];
         const uint32_t dst = s_gbase[(k >> shift) & mask] + (uint32_t)i;
@@ -480,6 +491,8 @@ __global__ void __launch_bounds__(256) k_rts_scatter(const uint32_t* __restrict_
         vals_out[dst] = s_val[i];
     }
 }
+
+bool radix_sort_fuses_gather() { return !LSR_SORT_LOOKBACK; }
 
 static size_t os_blocks(size_t n) { return (n + OS_TILE - 1) / OS_TILE; }
 
@@ -497,7 +510,7 @@ size_t radix_temp_zero_bytes(size_t n, int begin_bit, int end_bit) {
 
 bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b, size_t n,
                       int begin_bit, int end_bit, void* temp, uint32_t* err, hipStream_t st, bool temp_zeroed,
-                      uint32_t* kept) {
+                      uint32_t* kept, const SortGather* gather) {
     if (n == 0 || end_bit <= begin_bit) return false;
     const size_t nb = os_blocks(n);
     uint32_t* hist = reinterpret_cast<uint32_t*>(temp);
@@ -523,13 +536,16 @@ bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint
         const uint32_t* n_dev = kept && p_ > 0 ? kept : nullptr;   // the kept count
         hipLaunchKernelGGL(k_rts_count, dim3((unsigned)nb), dim3(256), 0, st, kin, n, n_dev, drop, shift, nbits, cnt);
         hipLaunchKernelGGL(k_rts_scan, dim3(256), dim3(256), 0, st, cnt, (int)nb, hist + p_ * 256);
+        const bool last = shift + 8 >= end_bit;
+        const SortGather g = last && gather ? *gather : SortGather{nullptr, nullptr, nullptr};
         hipLaunchKernelGGL(k_rts_scatter, dim3((unsigned)nb), dim3(256), 0, st, kin, vin, kout, vout, n, n_dev, drop,
                            drop ? kept : (uint32_t*)nullptr, shift, nbits, (const uint32_t*)(hist + p_ * 256),
-                           (const uint32_t*)cnt);
+                           (const uint32_t*)cnt, g);
         in_b = !in_b;
     }
     return in_b;
 #else
+    (void)gather;   // not fused here: the caller gathers (radix_sort_fuses_gather() is false)
     if (kept) (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(kept), (int)n, 1, st);   // no dropping here
     const unsigned hb = (unsigned)min((size_t)OS_HIST_BLOCKS, (n + 64 * HIST_ITEMS * 4 - 1) / (64 * HIST_ITEMS * 4));
     hipLaunchKernelGGL(k_radix_hist, dim3(hb), dim3(256), 0, st, (const uint32_t*)keys_a, n, begin_bit, end_bit, hist);

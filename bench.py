@@ -41,10 +41,12 @@ def phase_bytes(phase, P, Pvis, K, npix, ntiles, C, M=16, accumulate=True, V=1, 
     if phase == "preprocess":              # inputs; radii, radius, tiles, key, rect, sort ids; screen
         return (P * (12 + 12 + 16 + 4 + 4 * 3 * M) + P * (4 + 4 + 4 + 4 + 8 + 4)   # records; zeroed
                 + Pvis * (8 + 16 + 16 + 1 + 64))                                   # accumulator rows
-    if phase == "depth_sort":
-        return 4 * P * (4 + 16) + 4 * P     # 4 passes: count reads keys, scatter reads + writes pairs
-    if phase == "instance_scan":           # order + rect gather -> counts + depth-ordered rect; scan
-        return P * (4 + 8 + 4 + 8) + P * (4 + 4)
+    if phase == "depth_sort":              # pass 1 over all keys, passes 2-4 over the visible (culled
+        n = [P, Pvis, Pvis, Pvis]           # dropped); the last pass writes ids + the rect gather
+        return (sum(ni * (4 + 16) for ni in n) - Pvis * 4 + Pvis * (8 + 8 + 4)   # (rect, rect_sorted,
+                + P * 4)                    # counts) instead of keys; the culled ranks' zero counts
+    if phase == "instance_scan":           # exclusive scan of the depth-ranked counts
+        return P * (4 + 4)
     if phase == "emit":                    # order, offsets, counts, rect (depth order) -> keys, values
         return P * (4 + 4 + 4 + 8) + K * 8
     if phase == "tile_sort":
