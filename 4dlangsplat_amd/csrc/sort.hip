@@ -348,6 +348,7 @@ __global__ void __launch_bounds__(256) k_radix_pass(const uint32_t* __restrict__
 __device__ __forceinline__ size_t rts_n(size_t n, const uint32_t* n_dev) {
     return n_dev ? min(n, (size_t)*n_dev) : n;
 }
+template <int IT>
 __global__ void __launch_bounds__(256) k_rts_count(const uint32_t* __restrict__ keys, size_t n,
                                                    const uint32_t* __restrict__ n_dev, int drop, int shift, int nbits,
                                                    uint32_t* __restrict__ counts) {
@@ -359,15 +360,15 @@ __global__ void __launch_bounds__(256) k_rts_count(const uint32_t* __restrict__ 
     __syncthreads();
     const uint32_t mask = (1u << nbits) - 1u;
     const uint64_t lt = lanemask_lt();
-    const size_t base = (size_t)blockIdx.x * OS_TILE + (size_t)wave * (64 * OS_ITEMS);
-    uint32_t key[OS_ITEMS];
+    const size_t base = (size_t)blockIdx.x * (256 * IT) + (size_t)wave * (64 * IT);
+    uint32_t key[IT];
 #pragma unroll
-    for (int r = 0; r < OS_ITEMS; ++r) {
+    for (int r = 0; r < IT; ++r) {
         const size_t idx = base + (size_t)r * 64 + lane;
         key[r] = idx < n ? keys[idx] : 0u;
     }
 #pragma unroll
-    for (int r = 0; r < OS_ITEMS; ++r) {
+    for (int r = 0; r < IT; ++r) {
         const bool valid = base + (size_t)r * 64 + lane < n && !(drop && key[r] == 0xFFFFFFFFu);
         const uint32_t d = (key[r] >> shift) & mask;
         const uint64_t peers = match_digit(d, valid, nbits);
@@ -403,6 +404,7 @@ __global__ void __launch_bounds__(256) k_rts_scan(uint32_t* __restrict__ counts,
     if (tid == 0) totals[d] = carry;
 }
 
+template <int IT>
 __global__ void __launch_bounds__(256) k_rts_scatter(const uint32_t* __restrict__ keys_in,
                                                      const uint32_t* __restrict__ vals_in,
                                                      uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
@@ -410,8 +412,8 @@ __global__ void __launch_bounds__(256) k_rts_scatter(const uint32_t* __restrict_
                                                      uint32_t* __restrict__ kept_out, int shift, int nbits,
                                                      const uint32_t* __restrict__ totals,
                                                      const uint32_t* __restrict__ offs, SortGather gather) {
-    __shared__ uint32_t s_key[OS_TILE];
-    __shared__ uint32_t s_val[OS_TILE];
+    __shared__ uint32_t s_key[(256 * IT)];
+    __shared__ uint32_t s_val[(256 * IT)];
     __shared__ uint32_t s_wcnt[4][256];
     __shared__ uint32_t s_gbase[256];
     __shared__ uint32_t s_lbase[256];
@@ -424,10 +426,10 @@ __global__ void __launch_bounds__(256) k_rts_scatter(const uint32_t* __restrict_
     __syncthreads();
     const uint32_t mask = (1u << nbits) - 1u;
     const uint64_t lt = lanemask_lt();
-    const size_t base = (size_t)bid * OS_TILE + (size_t)wave * (64 * OS_ITEMS);
-    uint32_t key[OS_ITEMS], val[OS_ITEMS], rank[OS_ITEMS];
+    const size_t base = (size_t)bid * (256 * IT) + (size_t)wave * (64 * IT);
+    uint32_t key[IT], val[IT], rank[IT];
 #pragma unroll
-    for (int r = 0; r < OS_ITEMS; ++r) {
+    for (int r = 0; r < IT; ++r) {
         const size_t idx = base + (size_t)r * 64 + lane;
         const bool valid = idx < n;
         key[r] = valid ? keys_in[idx] : 0u;
@@ -437,7 +439,7 @@ __global__ void __launch_bounds__(256) k_rts_scatter(const uint32_t* __restrict_
     const uint32_t prefix = offs[(size_t)bid * 256 + tid];
     const uint32_t hcount = totals[tid];
 #pragma unroll
-    for (int r = 0; r < OS_ITEMS; ++r) {
+    for (int r = 0; r < IT; ++r) {
         const bool valid = base + (size_t)r * 64 + lane < n && !(drop && key[r] == 0xFFFFFFFFu);
         const uint32_t d = (key[r] >> shift) & mask;
         const uint64_t peers = match_digit(d, valid, nbits);
@@ -463,7 +465,7 @@ __global__ void __launch_bounds__(256) k_rts_scatter(const uint32_t* __restrict_
     __syncthreads();
     const int ntile = (int)s_wave[0];
 #pragma unroll
-    for (int r = 0; r < OS_ITEMS; ++r) {
+    for (int r = 0; r < IT; ++r) {
         const bool valid = base + (size_t)r * 64 + lane < n && !(drop && key[r] == 0xFFFFFFFFu);
         if (valid) {
             const uint32_t d = (key[r] >> shift) & mask;
@@ -525,22 +527,38 @@ bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint
     // no up-front histogram: each pass's scan kernel yields the digit totals (hist[pass] holds them)
     (void)err; (void)own_err;
     int p_ = 0;
-    for (int shift = begin_bit; shift < end_bit; shift += 8, ++p_) {
-        const int nbits = (end_bit - shift) < 8 ? (end_bit - shift) : 8;
+    // the bits spread evenly over the passes (13 bits: 7 + 6, not 8 + 5): fewer digits in a pass
+    // mean longer runs per digit in its scatter, i.e. fuller write segments
+    const int npass_ = (end_bit - begin_bit + 7) / 8;
+    // keys per thread: 8 (2M keys: more, shorter blocks), 12 above 4M keys (the 6M-instance
+    // tile sort: longer digit runs per block); swept 8 / 12 / 16 on both sorts
+    const int items = n > ((size_t)4 << 20) ? 12 : OS_ITEMS;
+    const size_t nbi = (n + 256 * items - 1) / (256 * items);   // <= nb: the count rows fit
+    for (int shift = begin_bit, nbits = 0; shift < end_bit; shift += nbits, ++p_) {
+        nbits = (end_bit - begin_bit) / npass_ + (p_ < (end_bit - begin_bit) % npass_ ? 1 : 0);
         const uint32_t* kin = in_b ? keys_b : keys_a;
         const uint32_t* vin = in_b ? vals_b : vals_a;
         uint32_t* kout = in_b ? keys_a : keys_b;
         uint32_t* vout = in_b ? vals_a : vals_b;
-        uint32_t* cnt = status + (size_t)p_ * nb * 256;
+        uint32_t* cnt = status + (size_t)p_ * nbi * 256;
         const int drop = kept && p_ == 0;                       // first pass drops, later passes read
         const uint32_t* n_dev = kept && p_ > 0 ? kept : nullptr;   // the kept count
-        hipLaunchKernelGGL(k_rts_count, dim3((unsigned)nb), dim3(256), 0, st, kin, n, n_dev, drop, shift, nbits, cnt);
-        hipLaunchKernelGGL(k_rts_scan, dim3(256), dim3(256), 0, st, cnt, (int)nb, hist + p_ * 256);
-        const bool last = shift + 8 >= end_bit;
+        if (items == 12)
+            hipLaunchKernelGGL(k_rts_count<12>, dim3((unsigned)nbi), dim3(256), 0, st, kin, n, n_dev, drop, shift, nbits, cnt);
+        else
+            hipLaunchKernelGGL(k_rts_count<OS_ITEMS>, dim3((unsigned)nbi), dim3(256), 0, st, kin, n, n_dev, drop, shift, nbits,
+                               cnt);
+        hipLaunchKernelGGL(k_rts_scan, dim3(256), dim3(256), 0, st, cnt, (int)nbi, hist + p_ * 256);
+        const bool last = shift + nbits >= end_bit;
         const SortGather g = last && gather ? *gather : SortGather{nullptr, nullptr, nullptr};
-        hipLaunchKernelGGL(k_rts_scatter, dim3((unsigned)nb), dim3(256), 0, st, kin, vin, kout, vout, n, n_dev, drop,
-                           drop ? kept : (uint32_t*)nullptr, shift, nbits, (const uint32_t*)(hist + p_ * 256),
-                           (const uint32_t*)cnt, g);
+        if (items == 12)
+            hipLaunchKernelGGL(k_rts_scatter<12>, dim3((unsigned)nbi), dim3(256), 0, st, kin, vin, kout, vout, n, n_dev,
+                               drop, drop ? kept : (uint32_t*)nullptr, shift, nbits,
+                               (const uint32_t*)(hist + p_ * 256), (const uint32_t*)cnt, g);
+        else
+            hipLaunchKernelGGL(k_rts_scatter<OS_ITEMS>, dim3((unsigned)nbi), dim3(256), 0, st, kin, vin, kout, vout, n,
+                               n_dev, drop, drop ? kept : (uint32_t*)nullptr, shift, nbits,
+                               (const uint32_t*)(hist + p_ * 256), (const uint32_t*)cnt, g);
         in_b = !in_b;
     }
     return in_b;
