@@ -16,24 +16,39 @@
 namespace lsr {
 
 // Falloff exp for x <= 0: the argument clamped at -87 (exp(-87) ~ 1.6e-38: every alpha built
-// from it is far below 1/255), Cody-Waite reduction + degree-7 Horner in fma, the exponent
-// assembled by bits.  <= 2 ulp above -87, like CUDA expf; made of correctly rounded operations
+// from it is far below 1/255), Cody-Waite reduction + a degree-6 minimax polynomial on
+// [-ln2/2, ln2/2] (relative error 1.9e-9 before rounding; Remez, float coefficients) in Horner
+// fma, the exponent assembled by bits.  <= 1.02 ulp above -87 (the degree-7 Taylor it replaced:
+// 0.94), like CUDA expf's 2 ulp bound; made of correctly rounded operations
 // only (max, mul, add, fma) so the host oracle reproduces it bit for bit.  round-to-nearest-even
 // of t = x log2(e) is (t + 1.5 2^23) - 1.5 2^23 (|t| < 2^22), and the low bits of t + 1.5 2^23
 // hold k, so 2^k = bits((t + 1.5 2^23) << 23 + 127 << 23).
 #define LSR_EXP_MAGIC 12582912.0f
+#ifdef LSR_EXP_DEG7_ABL   // timing ablation only: the previous degree-7 Taylor polynomial
+#define LSR_EXP_C7 1.98412698412698413e-04f
+#define LSR_EXP_C6 1.38888888888888889e-03f
+#define LSR_EXP_C5 8.33333333333333333e-03f
+#define LSR_EXP_C4 4.16666666666666667e-02f
+#define LSR_EXP_C3 1.66666666666666667e-01f
+#define LSR_EXP_C2 0.5f
+#else
+#define LSR_EXP_C6 0.0013836845755577087f   // minimax coefficients of r^6 .. r^2 (r^1, r^0: 1)
+#define LSR_EXP_C5 0.008374815806746483f
+#define LSR_EXP_C4 0.04166822507977486f
+#define LSR_EXP_C3 0.16666419804096222f
+#define LSR_EXP_C2 0.49999991059303284f
+#endif
 __device__ __forceinline__ float expf_repro(float x) {
     x = fmaxf(x, -87.0f);
     const float y = x * 1.44269504088896341f + LSR_EXP_MAGIC;
     const float kf = y - LSR_EXP_MAGIC;
     float r = __builtin_fmaf(kf, -0.693145751953125f, x);
     r = __builtin_fmaf(kf, -1.428606765330187045e-06f, r);
-    float p = 1.98412698412698413e-04f;
-    p = __builtin_fmaf(p, r, 1.38888888888888889e-03f);
-    p = __builtin_fmaf(p, r, 8.33333333333333333e-03f);
-    p = __builtin_fmaf(p, r, 4.16666666666666667e-02f);
-    p = __builtin_fmaf(p, r, 1.66666666666666667e-01f);
-    p = __builtin_fmaf(p, r, 0.5f);
+    float p = LSR_EXP_C6;
+    p = __builtin_fmaf(p, r, LSR_EXP_C5);
+    p = __builtin_fmaf(p, r, LSR_EXP_C4);
+    p = __builtin_fmaf(p, r, LSR_EXP_C3);
+    p = __builtin_fmaf(p, r, LSR_EXP_C2);
     p = __builtin_fmaf(p, r, 1.0f);
     p = __builtin_fmaf(p, r, 1.0f);
     return p * __uint_as_float((__float_as_uint(y) << 23) + 0x3F800000u);
@@ -50,12 +65,16 @@ __device__ __forceinline__ lsr_f2 expf_repro2(lsr_f2 x) {
     const lsr_f2 kf = y - lsr_f2{LSR_EXP_MAGIC, LSR_EXP_MAGIC};
     lsr_f2 r = __builtin_elementwise_fma(kf, lsr_f2{-0.693145751953125f, -0.693145751953125f}, x);
     r = __builtin_elementwise_fma(kf, lsr_f2{-1.428606765330187045e-06f, -1.428606765330187045e-06f}, r);
-    lsr_f2 p = {1.98412698412698413e-04f, 1.98412698412698413e-04f};
-    p = __builtin_elementwise_fma(p, r, lsr_f2{1.38888888888888889e-03f, 1.38888888888888889e-03f});
-    p = __builtin_elementwise_fma(p, r, lsr_f2{8.33333333333333333e-03f, 8.33333333333333333e-03f});
-    p = __builtin_elementwise_fma(p, r, lsr_f2{4.16666666666666667e-02f, 4.16666666666666667e-02f});
-    p = __builtin_elementwise_fma(p, r, lsr_f2{1.66666666666666667e-01f, 1.66666666666666667e-01f});
-    p = __builtin_elementwise_fma(p, r, lsr_f2{0.5f, 0.5f});
+#ifdef LSR_EXP_DEG7_ABL
+    lsr_f2 p = {LSR_EXP_C7, LSR_EXP_C7};
+    p = __builtin_elementwise_fma(p, r, lsr_f2{LSR_EXP_C6, LSR_EXP_C6});
+#else
+    lsr_f2 p = {LSR_EXP_C6, LSR_EXP_C6};
+#endif
+    p = __builtin_elementwise_fma(p, r, lsr_f2{LSR_EXP_C5, LSR_EXP_C5});
+    p = __builtin_elementwise_fma(p, r, lsr_f2{LSR_EXP_C4, LSR_EXP_C4});
+    p = __builtin_elementwise_fma(p, r, lsr_f2{LSR_EXP_C3, LSR_EXP_C3});
+    p = __builtin_elementwise_fma(p, r, lsr_f2{LSR_EXP_C2, LSR_EXP_C2});
     p = __builtin_elementwise_fma(p, r, lsr_f2{1.0f, 1.0f});
     p = __builtin_elementwise_fma(p, r, lsr_f2{1.0f, 1.0f});
     const lsr_f2 sc = {__uint_as_float((__float_as_uint(y.x) << 23) + 0x3F800000u),

@@ -147,7 +147,7 @@ k_render_fwd_wave_mfma(RenderFwdArgs a) {
     // X, Y; staged conic -a/2, -b, -c/2 (gauss_power); opacity (0 past the group: never blends); (r, g) and (b, depth) pairs
     __shared__ __attribute__((aligned(16))) float s_X[MG], s_Y[MG], s_A[MG], s_B[MG], s_C[MG], s_O[MG];
     __shared__ lsr_f2 s_RG[MG], s_BD[MG];
-    __shared__ uint32_t s_k[MG];
+    __shared__ uint32_t s_k[MG];   // list position + 1 (the n_contrib value of a blend)
     __shared__ __attribute__((aligned(16))) __bf16 s_Fh[DMA ? 8 : MG * MFP];
     __shared__ __attribute__((aligned(16))) __bf16 s_Fl[DMA ? 8 : MG * MFP];
     __shared__ uint32_t s_fk[MFIFO];
@@ -279,7 +279,7 @@ k_render_fwd_wave_mfma(RenderFwdArgs a) {
                     acc_bd = __builtin_elementwise_fma(s_BD[e], lsr_f2{w, w}, acc_bd);
                     w8[u] = w;
                     T = blend ? test_T : T;
-                    last = blend ? s_k[e] + 1 : last;
+                    last = blend ? s_k[e] : last;   // s_k holds the list position + 1
                 }
             }
             pack_octet(w8, oh[o], ol[o]);
@@ -378,7 +378,7 @@ k_render_fwd_wave_mfma(RenderFwdArgs a) {
                     *reinterpret_cast<bf16x8*>(s_Fl + e * MFP + c0 + 8 * h) = vl;
                 }
                 if (lane < MG) {
-                    s_k[lane] = g_k;
+                    s_k[lane] = g_k + 1u;
                     s_X[lane] = g_xy.x; s_Y[lane] = g_xy.y;
                     s_A[lane] = -0.5f * g_co.x; s_B[lane] = -g_co.y; s_C[lane] = -0.5f * g_co.z; s_O[lane] = g_co.w;
                     s_RG[lane] = lsr_f2{g_rgbd.x, g_rgbd.y};
@@ -428,7 +428,7 @@ k_render_fwd_wave_mfma(RenderFwdArgs a) {
                 const bool ok = lane < n;
                 const float4* geo = reinterpret_cast<const float4*>(s_stage + SG_GEO);
                 const float4 co = geo[lane], cd = geo[MG + lane];
-                s_k[lane] = ok ? s_fk[(head + lane) & (MFIFO - 1)] : 0u;
+                s_k[lane] = ok ? s_fk[(head + lane) & (MFIFO - 1)] + 1u : 0u;
                 s_X[lane] = s_stage[SG_XY + lane]; s_Y[lane] = s_stage[SG_XY + MG + lane];
                 s_A[lane] = -0.5f * co.x; s_B[lane] = -co.y; s_C[lane] = -0.5f * co.z; s_O[lane] = ok ? co.w : 0.0f;
                 s_RG[lane] = lsr_f2{cd.x, cd.y};

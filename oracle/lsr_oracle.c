@@ -38,7 +38,7 @@
  *
  * Floating point
  *   Compiled with -ffp-contract=off.  exp() of the Gaussian falloff uses orc_exp, a
- *   Cody-Waite + degree-7 Horner exp (<= 2 ulp) written only with IEEE max, *, +, fmaf and
+ *   Cody-Waite + degree-6 minimax exp (<= 1.02 ulp) written only with IEEE max, *, +, fmaf and
  *   exponent bit assembly, and the falloff exponent is orc_power (two fmaf), so that the product
  *   kernels reproduce the contributor decisions (alpha < 1/255, T < 1e-4) bit for bit.  The CUDA
  *   original uses expf (<= 2 ulp as well) and nvcc's default fma contraction.
@@ -69,7 +69,8 @@ typedef float real;
 /* exp for x <= 0; bit-reproducible with the HIP kernels' expf_repro (lsr_common.h): the same
  * sequence of correctly rounded operations (fmaxf, *, +, fmaf).  The argument is clamped at -87
  * (every alpha from exp(-87) ~ 1.6e-38 is far below 1/255); rint(x log2 e) is computed as
- * (t + 1.5 2^23) - 1.5 2^23 and 2^k assembled from the low bits of t + 1.5 2^23. */
+ * (t + 1.5 2^23) - 1.5 2^23, e^r by a degree-6 minimax polynomial on [-ln2/2, ln2/2] (Remez,
+ * float coefficients, <= 1.02 ulp overall) and 2^k assembled from the low bits of t + 1.5 2^23. */
 static inline float orc_exp(float x) {
     x = fmaxf(x, -87.0f);
     const float t = x * 1.44269504088896341f;
@@ -77,12 +78,11 @@ static inline float orc_exp(float x) {
     const float kf = y - 12582912.0f;
     float r = fmaf(kf, -0.693145751953125f, x);
     r = fmaf(kf, -1.428606765330187045e-06f, r);
-    float p = 1.98412698412698413e-04f;  /* 1/5040 */
-    p = fmaf(p, r, 1.38888888888888889e-03f); /* 1/720 */
-    p = fmaf(p, r, 8.33333333333333333e-03f); /* 1/120 */
-    p = fmaf(p, r, 4.16666666666666667e-02f); /* 1/24 */
-    p = fmaf(p, r, 1.66666666666666667e-01f); /* 1/6 */
-    p = fmaf(p, r, 0.5f);
+    float p = 0.0013836845755577087f;
+    p = fmaf(p, r, 0.008374815806746483f);
+    p = fmaf(p, r, 0.04166822507977486f);
+    p = fmaf(p, r, 0.16666419804096222f);
+    p = fmaf(p, r, 0.49999991059303284f);
     p = fmaf(p, r, 1.0f);
     p = fmaf(p, r, 1.0f);
     union { uint32_t u; float f; } yb, s;
