@@ -289,6 +289,7 @@ void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t
 // Backward.  g_* are the per-Gaussian screen-space gradients summed by the compositor backward.
 __device__ void cov2d_bwd(float3 mean, const float* c3, float fx, float fy, float tanfovx, float tanfovy,
                           const float* __restrict__ view, float3 dconic, float3& dmean, float* dcov) {
+#pragma clang fp contract(fast)   // gradients only (no decisions): fma contraction allowed
     float3 t = xform4x3(view, mean);
     const float limx = 1.3f * tanfovx, limy = 1.3f * tanfovy;
     const float txtz = t.x / t.z, tytz = t.y / t.z;
@@ -350,6 +351,7 @@ __device__ void cov2d_bwd(float3 mean, const float* c3, float fx, float fy, floa
 }
 
 __device__ void cov3d_bwd(float3 sc, float mod, float4 q, const float* dcov, float3& dscale, float4& drot) {
+#pragma clang fp contract(fast)   // gradients only (no decisions): fma contraction allowed
     const float r = q.x, x = q.y, y = q.z, z = q.w;
     const m3 Rm = quat_R(q);
     const float s[3] = {mod * sc.x, mod * sc.y, mod * sc.z};
@@ -388,6 +390,7 @@ __device__ void cov3d_bwd(float3 sc, float mod, float4 q, const float* dcov, flo
 // (assigned, not accumulated, into dRdx, dRdy, dRdz; left as given at degree 0).
 __device__ __forceinline__ void sh_bwd_channel(const float* __restrict__ sh, int ch, int deg, float x, float y, float z,
                                                float dRc, float (&g)[16], float& dRdx, float& dRdy, float& dRdz) {
+#pragma clang fp contract(fast)   // gradients only
 #define SHc(k) sh[(k) * 3 + ch]
 #pragma unroll
     for (int k = 0; k < 16; ++k) g[k] = 0.0f;
@@ -429,6 +432,7 @@ __device__ __forceinline__ void sh_bwd_channel(const float* __restrict__ sh, int
 // The direction-only factors of sh_bwd_channel's g[k] (g[k] = b[k] * dRc with the same operation
 // order), computed once for the three colour channels.
 __device__ __forceinline__ void sh_bwd_basis(int deg, float x, float y, float z, float (&b)[16]) {
+#pragma clang fp contract(fast)   // gradients only
 #pragma unroll
     for (int k = 0; k < 16; ++k) b[k] = 0.0f;
     b[0] = SH_C0;
@@ -454,6 +458,7 @@ __device__ __forceinline__ void sh_bwd_basis(int deg, float x, float y, float z,
 // The d colour / d direction partials of channel ch (the second half of sh_bwd_channel).
 __device__ __forceinline__ void sh_bwd_dir(const float* __restrict__ sh, int ch, int deg, float x, float y, float z,
                                           float& dRdx, float& dRdy, float& dRdz) {
+#pragma clang fp contract(fast)   // gradients only
 #define SHc(k) sh[(k) * 3 + ch]
     if (deg > 0) {
         dRdx = -SH_C1 * SHc(3); dRdy = -SH_C1 * SHc(1); dRdz = SH_C1 * SHc(2);
@@ -555,6 +560,7 @@ __device__ __forceinline__ void write_rows(float* __restrict__ dst, const float*
 
 template <bool ACC, int MS>
 __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
+#pragma clang fp contract(fast)   // backward: gradients only, fma contraction allowed
     constexpr int M3 = MS * 3, SP = M3 + 1;
     __shared__ float s_sh[MS > 0 ? 256 * SP : 1];
     __shared__ uint8_t s_vis[256];
@@ -699,6 +705,7 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
 // on the summed dL/dcov3D (it is linear in it); the gradient rows are written once.
 template <bool ACC, int MS>
 __global__ void __launch_bounds__(256) k_preprocess_bwd_views(PreprocessBwdViewsArgs a) {
+#pragma clang fp contract(fast)   // backward: gradients only, fma contraction allowed
     constexpr int M3 = MS * 3, SP = M3 + 1;
     __shared__ float s_sh[MS > 0 ? 256 * SP : 1];
     __shared__ uint8_t s_vis[256];
