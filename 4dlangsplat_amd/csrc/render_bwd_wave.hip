@@ -198,7 +198,11 @@ k_render_bwd_wave(RenderBwdArgs a) {
             if (cand) {   // back to front: higher list positions first
                 const int rank = lane == 63 ? 0 : __popcll(m >> (lane + 1));
                 const int s = (tail + rank) & (WFIFO - 1);
+#ifdef LSR_ABL_DEDUP   // timing ablation only: atomics only from the entry's lowest quadrant
+                s_fk[s] = (uint32_t)k | ((((word >> PL_QUAD_SHIFT) & ((1u << quad) - 1u)) == 0u ? 0u : 1u) << 31);
+#else
                 s_fk[s] = (uint32_t)k;
+#endif
                 s_fg[s] = gid;
             }
             tail += __popcll(m);
@@ -222,9 +226,16 @@ k_render_bwd_wave(RenderBwdArgs a) {
             const int s = (head + lane) & (WFIFO - 1);
             pf.gid = ok ? s_fg[s] : 0u;
             pf.k = ok ? s_fk[s] : 0xFFFFFFFFu;
+#ifdef LSR_ABL_DEDUP
+            const uint32_t dup = ok ? (pf.k & 0x80000000u) : 0u;
+            pf.k = ok ? (pf.k & 0x7FFFFFFFu) : 0xFFFFFFFFu;
+#endif
             pf.xy = *at32(a.xy, pf.gid);
             pf.co = *at32(a.conic_o, pf.gid);
             pf.rgbd = *at32(a.rgbd, pf.gid);
+#ifdef LSR_ABL_DEDUP
+            pf.gid |= dup;
+#endif
         }
         const int e = lane >> 2, c0 = 8 * (lane & 3);
         const uint32_t gid = e < n ? s_fg[(head + e) & (WFIFO - 1)] : 0u;
@@ -281,13 +292,19 @@ k_render_bwd_wave(RenderBwdArgs a) {
         for (int j = 0; j < WG / 2; ++j) {   // lane -> channel lane & 31 of entries (lane >> 5) + 2 j
             const int e = (lane >> 5) + 2 * j;
             lv[j] = s_lq[e][ch];
-            lo[j] = s_agid[e] * (uint32_t)C + ch;
+#ifdef LSR_ABL_DEDUP
+            if (s_agid[e] >> 31) lv[j] = 0.0f;
+#endif
+            lo[j] = (s_agid[e] & 0x7FFFFFFFu) * (uint32_t)C + ch;
         }
 #pragma unroll
         for (int r = 0; r < WG / 4; ++r) {   // lane -> field lane & 15 of entry (lane >> 4) + 4 r
             const int e = (lane >> 4) + 4 * r;
             sv[r] = s_q[e][q];
-            so[r] = s_agid[e] * (uint32_t)ACC_PITCH + q;
+#ifdef LSR_ABL_DEDUP
+            if (s_agid[e] >> 31) sv[r] = 0.0f;
+#endif
+            so[r] = (s_agid[e] & 0x7FFFFFFFu) * (uint32_t)ACC_PITCH + q;
         }
         // A branch-free variant (every lane, zeros for idle lanes, so that hipcc could count the
         // atomics and skip them in its waits for later loads) measured 0.70 vs 0.50 ms: with no
