@@ -76,6 +76,7 @@ k_render_bwd_wave(RenderBwdArgs a) {
     const int b = blockIdx.x;
     const int slot = (b >> 5) * 8 + (b & 7), quad = (b >> 3) & 3;   // a slot's 4 quadrants: one XCD
     if (slot >= a.grid_x * a.grid_y) return;
+    // longest-first order (k_tile_order); column-major measured 0.61 vs 0.49 ms here
     const int tile = a.tile_order ? (int)a.tile_order[slot] : slot;
     const int lane = threadIdx.x, g4 = lane >> 4, l16 = lane & 15;
     const int tx = tile % a.grid_x, ty = tile / a.grid_x;

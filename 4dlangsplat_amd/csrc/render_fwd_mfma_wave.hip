@@ -165,7 +165,10 @@ k_render_fwd_wave_mfma(RenderFwdArgs a) {
     const int b = blockIdx.x;
     const int slot = (b >> 5) * 8 + (b & 7), quad = (b >> 3) & 3;   // a slot's 4 quadrants: one XCD
     if (slot >= a.grid_x * a.grid_y) return;
-    const int tile = a.tile_order ? (int)a.tile_order[slot] : slot;
+    // Slots walk the tiles column by column (no order array): measured 0.250 -> 0.232 ms against
+    // raster order on the headline scene (either column direction; a per-quadrant makespan
+    // simulation from the frame's composited-entry counts also favours it, 1.20 vs 1.26 of ideal).
+    const int tile = a.tile_order ? (int)a.tile_order[slot] : (slot % a.grid_y) * a.grid_x + slot / a.grid_y;
     const int lane = threadIdx.x, g4 = lane >> 4, l16 = lane & 15;
     const int tx = tile % a.grid_x, ty = tile / a.grid_x;
     const int qx0 = tx * LSR_TILE_X + (quad & 1) * 8, qy0 = ty * LSR_TILE_Y + (quad >> 1) * 8;

@@ -31,7 +31,8 @@ __global__ void __launch_bounds__(64) k_render_fwd_wave(RenderFwdArgs a) {
     const int b = blockIdx.x;
     const int slot = (b >> 5) * 8 + (b & 7), quad = (b >> 3) & 3;   // a slot's 4 quadrants: one XCD
     if (slot >= a.grid_x * a.grid_y) return;
-    const int tile = a.tile_order ? (int)a.tile_order[slot] : slot;
+    // column by column, as k_render_fwd_wave_mfma (measured faster than raster order there)
+    const int tile = a.tile_order ? (int)a.tile_order[slot] : (slot % a.grid_y) * a.grid_x + slot / a.grid_y;
     const int lane = threadIdx.x;
     const int tx = tile % a.grid_x, ty = tile / a.grid_x;
     const int qx0 = tx * LSR_TILE_X + (quad & 1) * 8, qy0 = ty * LSR_TILE_Y + (quad >> 1) * 8;
