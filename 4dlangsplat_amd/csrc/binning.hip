@@ -95,15 +95,22 @@ __global__ void __launch_bounds__(256) k_emit(int P, const uint32_t* __restrict_
         rect_unpack(rc, x0, y0, x1, y1);
         const uint32_t wd = x1 - x0;
         const uint32_t loc = j - s_off[w][k];
-        const uint32_t dy = loc / wd;
-        const uint32_t dx = loc - dy * wd, tx = x0 + dx, ty = y0 + dy;
-        uint32_t quads;
-        if (wd <= 2 && y1 - y0 <= 2) {   // the preprocess's map
-            const uint32_t map = rect_quad_map(rc), sh = 8 * dy + 2 * dx;
+        uint32_t dx, dy, quads;
+        if (rect_small(x0, y0, x1, y1)) {   // the preprocess's map: the loc-th reachable tile
+            const uint32_t map = rect_quad_map(rc);
+            uint32_t m = rect_tile_mask(map);
+            for (uint32_t i = 0; i < loc; ++i) m &= m - 1u;
+            const uint32_t pos = (uint32_t)__builtin_ctz(m);
+            dx = pos & 1u;
+            dy = pos >> 1;
+            const uint32_t sh = 8 * dy + 2 * dx;
             quads = ((map >> sh) & 3u) | (((map >> (sh + 4)) & 3u) << 2);
         } else {
-            quads = emit_quad_mask(s_sp[w][k], (int)tx * LSR_TILE_X, (int)ty * LSR_TILE_Y, W, H);
+            dy = loc / wd;
+            dx = loc - dy * wd;
+            quads = emit_quad_mask(s_sp[w][k], (int)(x0 + dx) * LSR_TILE_X, (int)(y0 + dy) * LSR_TILE_Y, W, H);
         }
+        const uint32_t tx = x0 + dx, ty = y0 + dy;
         keys[j] = quads ? ty * (uint32_t)gx + tx : ntiles;
         vals[j] = s_id[w][k] | (quads << PL_QUAD_SHIFT);
     }

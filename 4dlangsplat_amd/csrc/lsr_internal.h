@@ -35,10 +35,29 @@ __host__ __device__ __forceinline__ void rect_unpack(uint2 r, uint32_t& x0, uint
     x0 = r.x & 0xFFFu; y0 = (r.x >> 12) & 0xFFFu; x1 = r.y & 0xFFFu; y1 = (r.y >> 12) & 0xFFFu;
 }
 __host__ __device__ __forceinline__ uint32_t rect_quad_map(uint2 r) { return (r.x >> 24) | (r.y >> 24) << 8; }
+// Rectangles of at most 2 x 2 tiles carry their quadrant map: only their tiles with a reachable
+// quadrant get an instance.  Bit 2 dy + dx of the mask: tile (x0 + dx, y0 + dy) has one.
+__host__ __device__ __forceinline__ bool rect_small(uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1) {
+    return x1 - x0 <= 2 && y1 - y0 <= 2;
+}
+__host__ __device__ __forceinline__ uint32_t rect_tile_mask(uint32_t map) {
+    return ((map & 0x33u) ? 1u : 0u) | ((map & 0xCCu) ? 2u : 0u) | ((map & 0x3300u) ? 4u : 0u) |
+           ((map & 0xCC00u) ? 8u : 0u);
+}
+// Instances a rectangle emits: its reachable tiles when small, else all its tiles.
 __host__ __device__ __forceinline__ uint32_t rect_count(uint2 r) {
     uint32_t x0, y0, x1, y1;
     rect_unpack(r, x0, y0, x1, y1);
+    if ((x1 - x0) * (y1 - y0) > 0 && rect_small(x0, y0, x1, y1)) return __builtin_popcount(rect_tile_mask(rect_quad_map(r)));
     return (x1 - x0) * (y1 - y0);
+}
+// Index of tile (tx, ty) among the rectangle's emitted instances (row-major order).
+__host__ __device__ __forceinline__ uint32_t rect_local_index(uint2 r, uint32_t tx, uint32_t ty) {
+    uint32_t x0, y0, x1, y1;
+    rect_unpack(r, x0, y0, x1, y1);
+    if (rect_small(x0, y0, x1, y1))
+        return __builtin_popcount(rect_tile_mask(rect_quad_map(r)) & ((1u << (2 * (ty - y0) + (tx - x0))) - 1u));
+    return (ty - y0) * (x1 - x0) + (tx - x0);
 }
 
 struct PreprocessArgs {

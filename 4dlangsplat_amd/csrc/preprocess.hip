@@ -232,8 +232,7 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
     }
     a.radii[i] = radius;
     a.radius[i] = radius;
-    a.tiles[i] = (uint32_t)ntiles;
-    if (a.acc && ntiles > 0) {   // only listed Gaussians receive backward atomics
+    if (a.acc && ntiles > 0) {   // only rectangles receive backward atomics (a superset of the listed)
         float4* r = a.acc + (size_t)i * (ACC_PITCH / 4);
 #pragma unroll
         for (int k = 0; k < ACC_PITCH / 4; ++k) r[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -252,7 +251,11 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
                 qmap |= ((m & 3u) << sh) | ((m >> 2) << (sh + 4));
             }
     }
-    a.rect[i] = rect_pack((uint32_t)cmin.x, (uint32_t)cmin.y, (uint32_t)cmax.x, (uint32_t)cmax.y, qmap);
+    const uint2 rc = rect_pack((uint32_t)cmin.x, (uint32_t)cmin.y, (uint32_t)cmax.x, (uint32_t)cmax.y, qmap);
+    a.rect[i] = rc;
+    // instances it will emit: a small rectangle's tiles with a reachable quadrant (none: the
+    // Gaussian blends no pixel and is not listed -- its gradient is exactly zero)
+    a.tiles[i] = rect_count(rc);
     if (a.key) a.key[i] = __float_as_uint(pv.z);
     a.xy[i] = pix;
     a.conic_o[i] = conic;

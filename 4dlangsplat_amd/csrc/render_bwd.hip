@@ -88,11 +88,8 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
             s_co[tid] = co;
             s_rgbd[tid] = a.rgbd[gid];
             s_thr[tid] = skip_power(co.w);
-            const uint2 rc = a.rect[gid];   // the binning rectangle (preprocess), packed 16-bit
-            uint32_t ux0, uy0, ux1, uy1;
-            rect_unpack(rc, ux0, uy0, ux1, uy1);
-            const int rx0 = (int)ux0, ry0 = (int)uy0, rx1 = (int)ux1;
-            s_inst[tid] = a.inst_off[gid] + (uint32_t)((ty - ry0) * (rx1 - rx0) + (tx - rx0));
+            // record slot: the Gaussian's first instance + this tile's index among its emitted ones
+            s_inst[tid] = a.inst_off[gid] + rect_local_index(a.rect[gid], (uint32_t)tx, (uint32_t)ty);
             s_act[tid] = 0;
         }
         for (int e = tid; e < NSLOT * BATCH * RECQ; e += 256) s_rec[e] = 0.0f;
