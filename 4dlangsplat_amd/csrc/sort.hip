@@ -76,6 +76,48 @@ __global__ void __launch_bounds__(256) k_scan_down(const uint32_t* __restrict__ 
     if (total && threadIdx.x == 0 && gridDim.x == 1) *total = block_total;
 }
 
+// Second pass of a two-kernel scan: block b sums the partials of blocks [0, b) itself (no
+// separate scan of the partials: one dependent launch less), then scans its tile.  Block 0 also
+// writes the grand total.
+__global__ void __launch_bounds__(256) k_scan_down_sum(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                       size_t n, const uint32_t* __restrict__ partials, int nb,
+                                                       uint32_t* __restrict__ total) {
+    __shared__ uint32_t s_wave[4];
+    __shared__ uint32_t s_base[2];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int b = blockIdx.x;
+    uint32_t pre = 0, all = 0;
+    for (int i = tid; i < nb; i += 256) {
+        const uint32_t v = partials[i];
+        pre += i < b ? v : 0u;
+        all += v;
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        pre += __shfl_xor(pre, o);
+        all += __shfl_xor(all, o);
+    }
+    if (lane == 0) s_wave[wave] = pre;
+    __syncthreads();
+    if (tid == 0) s_base[0] = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+    __syncthreads();
+    if (lane == 0) s_wave[wave] = all;
+    __syncthreads();
+    if (tid == 0) s_base[1] = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+    __syncthreads();
+    const uint32_t b0 = s_base[0];
+    if (total && b == 0 && tid == 0) *total = s_base[1];
+    const size_t base = (size_t)b * SCAN_TILE + (size_t)tid * SCAN_ITEMS;
+    uint32_t v[SCAN_ITEMS];
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) v[i] = (base + i < n) ? in[base + i] : 0u;
+    uint32_t block_total;
+    block_exclusive_scan8(v, s_wave, block_total);
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i)
+        if (base + i < n) out[base + i] = v[i] + b0;
+}
+
 size_t scan_temp_bytes(size_t n) {
     if (n <= (size_t)SCAN_TILE) return 0;
     const size_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
@@ -93,6 +135,12 @@ void exclusive_scan_u32(const uint32_t* in, uint32_t* out, size_t n, uint32_t* t
     }
     const size_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
     uint32_t* partials = reinterpret_cast<uint32_t*>(temp);
+    if (nb <= 4096) {   // up to 8M values: the scan of the partials is folded into the second pass
+        hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nb), dim3(256), 0, st, in, n, partials);
+        hipLaunchKernelGGL(k_scan_down_sum, dim3((unsigned)nb), dim3(256), 0, st, in, out, n, (const uint32_t*)partials,
+                           (int)nb, total);
+        return;
+    }
     uint32_t* scanned = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(temp) + align_up(nb * 4, 256));
     void* deeper = reinterpret_cast<char*>(temp) + 2 * align_up(nb * 4, 256);
     hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nb), dim3(256), 0, st, in, n, partials);
