@@ -101,11 +101,8 @@ __device__ __forceinline__ void stage_rows(float* __restrict__ lds, const float*
 }
 
 template <int MS>  // SH coefficients per Gaussian known at compile time (0 = any M, read from global)
-__global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
+__device__ __forceinline__ bool preprocess_one(const PreprocessArgs& a, int i) {   // true: rectangle
     constexpr int M3 = MS * 3;
-    clear_words(a.clear);
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.P) return;
     a.radii[i] = 0;
     a.radius[i] = 0;
     a.tiles[i] = 0;
@@ -117,7 +114,7 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
     const float3 p = make_float3(a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]);
     const float4 ph = xform4x4(a.proj, p);
     const float3 pv = xform4x3(a.view, p);
-    if (pv.z <= 0.2f) return;
+    if (pv.z <= 0.2f) return false;
     const float pw = 1.0f / (ph.w + 0.0000001f);
     const float3 pp = make_float3(ph.x * pw, ph.y * pw, ph.z * pw);
 
@@ -145,7 +142,7 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
     const m3 cv = mul(A, T);
     const float ca = cv.m[0][0] + 0.3f, cb = cv.m[0][1], cc = cv.m[1][1] + 0.3f;
     const float det = ca * cc - cb * cb;
-    if (det == 0.0f) return;
+    if (det == 0.0f) return false;
     const float det_inv = 1.0f / det;
     const float4 conic = make_float4(cc * det_inv, -cb * det_inv, ca * det_inv, a.opacities[i]);
     const float mid = 0.5f * (ca + cc);
@@ -155,7 +152,7 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
     const float2 pix = make_float2(ndc2pix(pp.x, a.W), ndc2pix(pp.y, a.H));
     int2 rmin, rmax;
     tile_rect(pix, radius, a.grid_x, a.grid_y, rmin, rmax);
-    if ((rmax.y - rmin.y) * (rmax.x - rmin.x) == 0) return;   // upstream: culled (radius 0)
+    if ((rmax.y - rmin.y) * (rmax.x - rmin.x) == 0) return false;   // upstream: culled (radius 0)
     // Binning rectangle: upstream's 3-sigma square intersected with the bounding box of the ellipse
     // where a pixel can pass the compositors' exact alpha prefilter (power >= skip_power(o), i.e.
     // q(d) <= -2 skip_power(o)).  Every dropped (Gaussian, tile) would be skipped at every pixel of
@@ -189,9 +186,17 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
         if constexpr (MS > 0) {
             const float* src = a.shs + (size_t)i * M3;
             if (M3 % 4 == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+#ifdef LSR_ABL_SHCOAL   // timing ablation only: the wave's rows read coalesced (wrong colours)
+                const int ln = threadIdx.x & 63;
+                const float4* w4 = reinterpret_cast<const float4*>(a.shs + (size_t)(i - ln) * M3);
+#endif
 #pragma unroll
                 for (int q = 0; q < M3 / 4; ++q) {
+#ifdef LSR_ABL_SHCOAL
+                    const float4 v = w4[q * 64 + ln];
+#else
                     const float4 v = reinterpret_cast<const float4*>(src)[q];
+#endif
                     shr[4 * q] = v.x; shr[4 * q + 1] = v.y; shr[4 * q + 2] = v.z; shr[4 * q + 3] = v.w;
                 }
             } else {
@@ -232,11 +237,6 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
     }
     a.radii[i] = radius;
     a.radius[i] = radius;
-    if (a.acc && ntiles > 0) {   // only rectangles receive backward atomics (a superset of the listed)
-        float4* r = a.acc + (size_t)i * (ACC_PITCH / 4);
-#pragma unroll
-        for (int k = 0; k < ACC_PITCH / 4; ++k) r[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    }
     uint32_t qmap = 0;   // quadrant map of a rectangle of <= 2 x 2 tiles (the binning's emit_quad_mask)
 #ifdef LSR_ABL_NOQMAP
     if (false) {   // timing ablation only (instances of small rectangles then reach no quadrant)
@@ -260,6 +260,30 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
     a.xy[i] = pix;
     a.conic_o[i] = conic;
     a.rgbd[i] = make_float4(rgb[0], rgb[1], rgb[2], pv.z);
+    return ntiles > 0;
+}
+
+template <int MS>
+__global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
+    clear_words(a.clear);
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool rect = i < a.P && preprocess_one<MS>(a, i);
+#ifdef LSR_ABL_NOACCZERO   // timing ablation only
+    if (true) return;
+#endif
+    if (!a.acc) return;
+    // Only rectangles receive backward atomics (a superset of the listed): zero their accumulator
+    // rows, the wave's 64 rows written as whole float4 runs (coalesced; a row per lane would
+    // write 64 strided partial lines per store).
+    const uint64_t m = __ballot(rect);
+    if (m == 0) return;
+    const int ln = threadIdx.x & 63;
+    float4* w = a.acc + (size_t)(i - ln) * (ACC_PITCH / 4);
+#pragma unroll
+    for (int q = 0; q < ACC_PITCH / 4; ++q) {
+        const int e = q * 64 + ln;
+        if ((m >> (e / (ACC_PITCH / 4))) & 1) w[e] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
 }
 
 void launch_preprocess(const PreprocessArgs& a, hipStream_t st) {
