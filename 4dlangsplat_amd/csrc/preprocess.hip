@@ -317,6 +317,9 @@ void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t
 __device__ void cov2d_bwd(float3 mean, const float* c3, float fx, float fy, float tanfovx, float tanfovy,
                           const float* __restrict__ view, float3 dconic, float3& dmean, float* dcov) {
 #pragma clang fp contract(fast)   // gradients only (no decisions): fma contraction allowed
+    // Upstream's chain (T = W J, cov2D = T^T V T, then dT -> dJ -> dt) restated on the two nonzero
+    // columns u0, u1 of T (J's third column is zero): W(r, c) = view[4r + c].  Reciprocals are the
+    // hardware rcp (gradients only); the clamp decisions use the same exact quotients as the forward.
     float3 t = xform4x3(view, mean);
     const float limx = 1.3f * tanfovx, limy = 1.3f * tanfovy;
     const float txtz = t.x / t.z, tytz = t.y / t.z;
@@ -324,51 +327,48 @@ __device__ void cov2d_bwd(float3 mean, const float* c3, float fx, float fy, floa
     t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
     const float x_grad_mul = (txtz < -limx || txtz > limx) ? 0.0f : 1.0f;
     const float y_grad_mul = (tytz < -limy || tytz > limy) ? 0.0f : 1.0f;
-    m3 J = zero3();
-    J.m[0][0] = fx / t.z; J.m[0][2] = -(fx * t.x) / (t.z * t.z);
-    J.m[1][1] = fy / t.z; J.m[1][2] = -(fy * t.y) / (t.z * t.z);
-    const m3 W = view_W(view);
-    const m3 V = sym3(c3);
-    const m3 T = mul(W, J);
-    const m3 cv = mul(mul(tr(T), tr(V)), T);
-    const float a = cv.m[0][0] + 0.3f, b = cv.m[0][1], c = cv.m[1][1] + 0.3f;
+    const float tz = __builtin_amdgcn_rcpf(t.z), tz2 = tz * tz, tz3 = tz2 * tz;
+    const float J00 = fx * tz, J11 = fy * tz, J02 = -(fx * t.x) * tz2, J12 = -(fy * t.y) * tz2;
+    float u0[3], u1[3], Vu0[3], Vu1[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        u0[r] = view[4 * r] * J00 + view[4 * r + 2] * J02;
+        u1[r] = view[4 * r + 1] * J11 + view[4 * r + 2] * J12;
+    }
+    const float V[3][3] = {{c3[0], c3[1], c3[2]}, {c3[1], c3[3], c3[4]}, {c3[2], c3[4], c3[5]}};
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        Vu0[r] = V[r][0] * u0[0] + V[r][1] * u0[1] + V[r][2] * u0[2];
+        Vu1[r] = V[r][0] * u1[0] + V[r][1] * u1[1] + V[r][2] * u1[2];
+    }
+    const float a = u0[0] * Vu0[0] + u0[1] * Vu0[1] + u0[2] * Vu0[2] + 0.3f;
+    const float b = u0[0] * Vu1[0] + u0[1] * Vu1[1] + u0[2] * Vu1[2];
+    const float c = u1[0] * Vu1[0] + u1[1] * Vu1[1] + u1[2] * Vu1[2] + 0.3f;
     const float denom = a * c - b * b;
     float dL_da = 0.0f, dL_db = 0.0f, dL_dc = 0.0f;
-    const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
-    const float (*Tm)[3] = T.m;
+    const float denom2inv = __builtin_amdgcn_rcpf((denom * denom) + 0.0000001f);
     if (denom2inv != 0.0f) {
         dL_da = denom2inv * (-c * c * dconic.x + 2.0f * b * c * dconic.y + (denom - a * c) * dconic.z);
         dL_dc = denom2inv * (-a * a * dconic.z + 2.0f * a * b * dconic.y + (denom - a * c) * dconic.x);
         dL_db = denom2inv * 2.0f * (b * c * dconic.x - (denom + 2.0f * b * b) * dconic.y + a * b * dconic.z);
-        dcov[0] = Tm[0][0] * Tm[0][0] * dL_da + Tm[0][0] * Tm[1][0] * dL_db + Tm[1][0] * Tm[1][0] * dL_dc;
-        dcov[3] = Tm[0][1] * Tm[0][1] * dL_da + Tm[0][1] * Tm[1][1] * dL_db + Tm[1][1] * Tm[1][1] * dL_dc;
-        dcov[5] = Tm[0][2] * Tm[0][2] * dL_da + Tm[0][2] * Tm[1][2] * dL_db + Tm[1][2] * Tm[1][2] * dL_dc;
-        dcov[1] = 2.0f * Tm[0][0] * Tm[0][1] * dL_da + (Tm[0][0] * Tm[1][1] + Tm[0][1] * Tm[1][0]) * dL_db + 2.0f * Tm[1][0] * Tm[1][1] * dL_dc;
-        dcov[2] = 2.0f * Tm[0][0] * Tm[0][2] * dL_da + (Tm[0][0] * Tm[1][2] + Tm[0][2] * Tm[1][0]) * dL_db + 2.0f * Tm[1][0] * Tm[1][2] * dL_dc;
-        dcov[4] = 2.0f * Tm[0][2] * Tm[0][1] * dL_da + (Tm[0][1] * Tm[1][2] + Tm[0][2] * Tm[1][1]) * dL_db + 2.0f * Tm[1][1] * Tm[1][2] * dL_dc;
-    } else {
-#pragma unroll
-        for (int k = 0; k < 6; ++k) dcov[k] = 0.0f;
     }
-    const float (*Vm)[3] = V.m;
-    const float dT00 = 2.0f * (Tm[0][0] * Vm[0][0] + Tm[0][1] * Vm[0][1] + Tm[0][2] * Vm[0][2]) * dL_da +
-                       (Tm[1][0] * Vm[0][0] + Tm[1][1] * Vm[0][1] + Tm[1][2] * Vm[0][2]) * dL_db;
-    const float dT01 = 2.0f * (Tm[0][0] * Vm[1][0] + Tm[0][1] * Vm[1][1] + Tm[0][2] * Vm[1][2]) * dL_da +
-                       (Tm[1][0] * Vm[1][0] + Tm[1][1] * Vm[1][1] + Tm[1][2] * Vm[1][2]) * dL_db;
-    const float dT02 = 2.0f * (Tm[0][0] * Vm[2][0] + Tm[0][1] * Vm[2][1] + Tm[0][2] * Vm[2][2]) * dL_da +
-                       (Tm[1][0] * Vm[2][0] + Tm[1][1] * Vm[2][1] + Tm[1][2] * Vm[2][2]) * dL_db;
-    const float dT10 = 2.0f * (Tm[1][0] * Vm[0][0] + Tm[1][1] * Vm[0][1] + Tm[1][2] * Vm[0][2]) * dL_dc +
-                       (Tm[0][0] * Vm[0][0] + Tm[0][1] * Vm[0][1] + Tm[0][2] * Vm[0][2]) * dL_db;
-    const float dT11 = 2.0f * (Tm[1][0] * Vm[1][0] + Tm[1][1] * Vm[1][1] + Tm[1][2] * Vm[1][2]) * dL_dc +
-                       (Tm[0][0] * Vm[1][0] + Tm[0][1] * Vm[1][1] + Tm[0][2] * Vm[1][2]) * dL_db;
-    const float dT12 = 2.0f * (Tm[1][0] * Vm[2][0] + Tm[1][1] * Vm[2][1] + Tm[1][2] * Vm[2][2]) * dL_dc +
-                       (Tm[0][0] * Vm[2][0] + Tm[0][1] * Vm[2][1] + Tm[0][2] * Vm[2][2]) * dL_db;
-    const float (*Wm)[3] = W.m;
-    const float dJ00 = Wm[0][0] * dT00 + Wm[0][1] * dT01 + Wm[0][2] * dT02;
-    const float dJ02 = Wm[2][0] * dT00 + Wm[2][1] * dT01 + Wm[2][2] * dT02;
-    const float dJ11 = Wm[1][0] * dT10 + Wm[1][1] * dT11 + Wm[1][2] * dT12;
-    const float dJ12 = Wm[2][0] * dT10 + Wm[2][1] * dT11 + Wm[2][2] * dT12;
-    const float tz = 1.0f / t.z, tz2 = tz * tz, tz3 = tz2 * tz;
+    dcov[0] = u0[0] * u0[0] * dL_da + u0[0] * u1[0] * dL_db + u1[0] * u1[0] * dL_dc;
+    dcov[3] = u0[1] * u0[1] * dL_da + u0[1] * u1[1] * dL_db + u1[1] * u1[1] * dL_dc;
+    dcov[5] = u0[2] * u0[2] * dL_da + u0[2] * u1[2] * dL_db + u1[2] * u1[2] * dL_dc;
+    dcov[1] = 2.0f * u0[0] * u0[1] * dL_da + (u0[0] * u1[1] + u0[1] * u1[0]) * dL_db + 2.0f * u1[0] * u1[1] * dL_dc;
+    dcov[2] = 2.0f * u0[0] * u0[2] * dL_da + (u0[0] * u1[2] + u0[2] * u1[0]) * dL_db + 2.0f * u1[0] * u1[2] * dL_dc;
+    dcov[4] = 2.0f * u0[2] * u0[1] * dL_da + (u0[1] * u1[2] + u0[2] * u1[1]) * dL_db + 2.0f * u1[1] * u1[2] * dL_dc;
+    // dT rows (upstream dL_dT00..dL_dT12) from the same V u products
+    float dT0[3], dT1[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        dT0[k] = 2.0f * Vu0[k] * dL_da + Vu1[k] * dL_db;
+        dT1[k] = 2.0f * Vu1[k] * dL_dc + Vu0[k] * dL_db;
+    }
+    const float dJ00 = view[0] * dT0[0] + view[4] * dT0[1] + view[8] * dT0[2];
+    const float dJ02 = view[2] * dT0[0] + view[6] * dT0[1] + view[10] * dT0[2];
+    const float dJ11 = view[1] * dT1[0] + view[5] * dT1[1] + view[9] * dT1[2];
+    const float dJ12 = view[2] * dT1[0] + view[6] * dT1[1] + view[10] * dT1[2];
     const float dtx = x_grad_mul * -fx * tz2 * dJ02;
     const float dty = y_grad_mul * -fy * tz2 * dJ12;
     const float dtz = -fx * tz2 * dJ00 - fy * tz2 * dJ11 + (2.0f * fx * t.x) * tz3 * dJ02 + (2.0f * fy * t.y) * tz3 * dJ12;
@@ -412,52 +412,8 @@ __device__ void cov3d_bwd(float3 sc, float mod, float4 q, const float* dcov, flo
              4.0f * z * (d.m[1][1] + d.m[0][0]);
 }
 
-// SH backward of colour channel ch (upstream computeColorFromSH backward): g[k] = dL/dsh[k][ch]
-// for k < 16 (zero past the active degree), and this channel's d colour / d direction partials
-// (assigned, not accumulated, into dRdx, dRdy, dRdz; left as given at degree 0).
-__device__ __forceinline__ void sh_bwd_channel(const float* __restrict__ sh, int ch, int deg, float x, float y, float z,
-                                               float dRc, float (&g)[16], float& dRdx, float& dRdy, float& dRdz) {
-#pragma clang fp contract(fast)   // gradients only
-#define SHc(k) sh[(k) * 3 + ch]
-#pragma unroll
-    for (int k = 0; k < 16; ++k) g[k] = 0.0f;
-    g[0] = SH_C0 * dRc;
-    if (deg > 0) {
-        g[1] = -SH_C1 * y * dRc; g[2] = SH_C1 * z * dRc; g[3] = -SH_C1 * x * dRc;
-        dRdx = -SH_C1 * SHc(3); dRdy = -SH_C1 * SHc(1); dRdz = SH_C1 * SHc(2);
-        if (deg > 1) {
-            const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-            g[4] = SH_C2[0] * xy * dRc; g[5] = SH_C2[1] * yz * dRc;
-            g[6] = SH_C2[2] * (2.0f * zz - xx - yy) * dRc; g[7] = SH_C2[3] * xz * dRc;
-            g[8] = SH_C2[4] * (xx - yy) * dRc;
-            dRdx += SH_C2[0] * y * SHc(4) + SH_C2[2] * 2.0f * -x * SHc(6) + SH_C2[3] * z * SHc(7) + SH_C2[4] * 2.0f * x * SHc(8);
-            dRdy += SH_C2[0] * x * SHc(4) + SH_C2[1] * z * SHc(5) + SH_C2[2] * 2.0f * -y * SHc(6) + SH_C2[4] * 2.0f * -y * SHc(8);
-            dRdz += SH_C2[1] * y * SHc(5) + SH_C2[2] * 2.0f * 2.0f * z * SHc(6) + SH_C2[3] * x * SHc(7);
-            if (deg > 2) {
-                g[9] = SH_C3[0] * y * (3.0f * xx - yy) * dRc;
-                g[10] = SH_C3[1] * xy * z * dRc;
-                g[11] = SH_C3[2] * y * (4.0f * zz - xx - yy) * dRc;
-                g[12] = SH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * dRc;
-                g[13] = SH_C3[4] * x * (4.0f * zz - xx - yy) * dRc;
-                g[14] = SH_C3[5] * z * (xx - yy) * dRc;
-                g[15] = SH_C3[6] * x * (xx - 3.0f * yy) * dRc;
-                dRdx += SH_C3[0] * SHc(9) * 3.0f * 2.0f * xy + SH_C3[1] * SHc(10) * yz + SH_C3[2] * SHc(11) * -2.0f * xy +
-                        SH_C3[3] * SHc(12) * -3.0f * 2.0f * xz + SH_C3[4] * SHc(13) * (-3.0f * xx + 4.0f * zz - yy) +
-                        SH_C3[5] * SHc(14) * 2.0f * xz + SH_C3[6] * SHc(15) * 3.0f * (xx - yy);
-                dRdy += SH_C3[0] * SHc(9) * 3.0f * (xx - yy) + SH_C3[1] * SHc(10) * xz +
-                        SH_C3[2] * SHc(11) * (-3.0f * yy + 4.0f * zz - xx) + SH_C3[3] * SHc(12) * -3.0f * 2.0f * yz +
-                        SH_C3[4] * SHc(13) * -2.0f * xy + SH_C3[5] * SHc(14) * -2.0f * yz + SH_C3[6] * SHc(15) * -3.0f * 2.0f * xy;
-                dRdz += SH_C3[1] * SHc(10) * xy + SH_C3[2] * SHc(11) * 4.0f * 2.0f * yz +
-                        SH_C3[3] * SHc(12) * 3.0f * (2.0f * zz - xx - yy) + SH_C3[4] * SHc(13) * 4.0f * 2.0f * xz +
-                        SH_C3[5] * SHc(14) * (xx - yy);
-            }
-        }
-    }
-#undef SHc
-}
-
-// The direction-only factors of sh_bwd_channel's g[k] (g[k] = b[k] * dRc with the same operation
-// order), computed once for the three colour channels.
+// SH backward (upstream computeColorFromSH backward): dL/dsh[k][ch] = b[k] * dR[ch] with b[k] the
+// direction-only basis factors, computed once for the three colour channels.
 __device__ __forceinline__ void sh_bwd_basis(int deg, float x, float y, float z, float (&b)[16]) {
 #pragma clang fp contract(fast)   // gradients only
 #pragma unroll
@@ -482,32 +438,37 @@ __device__ __forceinline__ void sh_bwd_basis(int deg, float x, float y, float z,
     }
 }
 
-// The d colour / d direction partials of channel ch (the second half of sh_bwd_channel).
-__device__ __forceinline__ void sh_bwd_dir(const float* __restrict__ sh, int ch, int deg, float x, float y, float z,
-                                          float& dRdx, float& dRdy, float& dRdz) {
+// Sum over the colour channels of dR[ch] * d colour_ch / d direction (the dL/dx, dL/dy, dL/dz that
+// upstream forms from its per-channel dRGBdx, dRGBdy, dRGBdz), contracted per coefficient first:
+// s_k = sum_ch SH[k][ch] dR[ch], then one pass of the basis derivatives over s_k.
+__device__ __forceinline__ void sh_bwd_dirsum(const float* __restrict__ sh, int deg, float x, float y, float z,
+                                              const float (&dR)[3], float& dLdx, float& dLdy, float& dLdz) {
 #pragma clang fp contract(fast)   // gradients only
-#define SHc(k) sh[(k) * 3 + ch]
+#define SK(k) (sh[(k) * 3] * dR[0] + sh[(k) * 3 + 1] * dR[1] + sh[(k) * 3 + 2] * dR[2])
+    dLdx = 0.0f; dLdy = 0.0f; dLdz = 0.0f;
     if (deg > 0) {
-        dRdx = -SH_C1 * SHc(3); dRdy = -SH_C1 * SHc(1); dRdz = SH_C1 * SHc(2);
+        dLdx = -SH_C1 * SK(3); dLdy = -SH_C1 * SK(1); dLdz = SH_C1 * SK(2);
         if (deg > 1) {
             const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-            dRdx += SH_C2[0] * y * SHc(4) + SH_C2[2] * 2.0f * -x * SHc(6) + SH_C2[3] * z * SHc(7) + SH_C2[4] * 2.0f * x * SHc(8);
-            dRdy += SH_C2[0] * x * SHc(4) + SH_C2[1] * z * SHc(5) + SH_C2[2] * 2.0f * -y * SHc(6) + SH_C2[4] * 2.0f * -y * SHc(8);
-            dRdz += SH_C2[1] * y * SHc(5) + SH_C2[2] * 2.0f * 2.0f * z * SHc(6) + SH_C2[3] * x * SHc(7);
+            const float s4 = SK(4), s5 = SK(5), s6 = SK(6), s7 = SK(7), s8 = SK(8);
+            dLdx += SH_C2[0] * y * s4 + SH_C2[2] * 2.0f * -x * s6 + SH_C2[3] * z * s7 + SH_C2[4] * 2.0f * x * s8;
+            dLdy += SH_C2[0] * x * s4 + SH_C2[1] * z * s5 + SH_C2[2] * 2.0f * -y * s6 + SH_C2[4] * 2.0f * -y * s8;
+            dLdz += SH_C2[1] * y * s5 + SH_C2[2] * 2.0f * 2.0f * z * s6 + SH_C2[3] * x * s7;
             if (deg > 2) {
-                dRdx += SH_C3[0] * SHc(9) * 3.0f * 2.0f * xy + SH_C3[1] * SHc(10) * yz + SH_C3[2] * SHc(11) * -2.0f * xy +
-                        SH_C3[3] * SHc(12) * -3.0f * 2.0f * xz + SH_C3[4] * SHc(13) * (-3.0f * xx + 4.0f * zz - yy) +
-                        SH_C3[5] * SHc(14) * 2.0f * xz + SH_C3[6] * SHc(15) * 3.0f * (xx - yy);
-                dRdy += SH_C3[0] * SHc(9) * 3.0f * (xx - yy) + SH_C3[1] * SHc(10) * xz +
-                        SH_C3[2] * SHc(11) * (-3.0f * yy + 4.0f * zz - xx) + SH_C3[3] * SHc(12) * -3.0f * 2.0f * yz +
-                        SH_C3[4] * SHc(13) * -2.0f * xy + SH_C3[5] * SHc(14) * -2.0f * yz + SH_C3[6] * SHc(15) * -3.0f * 2.0f * xy;
-                dRdz += SH_C3[1] * SHc(10) * xy + SH_C3[2] * SHc(11) * 4.0f * 2.0f * yz +
-                        SH_C3[3] * SHc(12) * 3.0f * (2.0f * zz - xx - yy) + SH_C3[4] * SHc(13) * 4.0f * 2.0f * xz +
-                        SH_C3[5] * SHc(14) * (xx - yy);
+                const float s9 = SK(9), s10 = SK(10), s11 = SK(11), s12 = SK(12), s13 = SK(13), s14 = SK(14), s15 = SK(15);
+                dLdx += SH_C3[0] * s9 * 3.0f * 2.0f * xy + SH_C3[1] * s10 * yz + SH_C3[2] * s11 * -2.0f * xy +
+                        SH_C3[3] * s12 * -3.0f * 2.0f * xz + SH_C3[4] * s13 * (-3.0f * xx + 4.0f * zz - yy) +
+                        SH_C3[5] * s14 * 2.0f * xz + SH_C3[6] * s15 * 3.0f * (xx - yy);
+                dLdy += SH_C3[0] * s9 * 3.0f * (xx - yy) + SH_C3[1] * s10 * xz +
+                        SH_C3[2] * s11 * (-3.0f * yy + 4.0f * zz - xx) + SH_C3[3] * s12 * -3.0f * 2.0f * yz +
+                        SH_C3[4] * s13 * -2.0f * xy + SH_C3[5] * s14 * -2.0f * yz + SH_C3[6] * s15 * -3.0f * 2.0f * xy;
+                dLdz += SH_C3[1] * s10 * xy + SH_C3[2] * s11 * 4.0f * 2.0f * yz +
+                        SH_C3[3] * s12 * 3.0f * (2.0f * zz - xx - yy) + SH_C3[4] * s13 * 4.0f * 2.0f * xz +
+                        SH_C3[5] * s14 * (xx - yy);
             }
         }
     }
-#undef SHc
+#undef SK
 }
 
 template <bool ACC>
@@ -657,9 +618,9 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
             // projection of the mean
             const float* pm = a.proj;
             const float4 mh = xform4x4(pm, p);
-            const float mw = 1.0f / (mh.w + 0.0000001f);
-            const float mul1 = (pm[0] * p.x + pm[4] * p.y + pm[8] * p.z + pm[12]) * mw * mw;
-            const float mul2 = (pm[1] * p.x + pm[5] * p.y + pm[9] * p.z + pm[13]) * mw * mw;
+            const float mw = __builtin_amdgcn_rcpf(mh.w + 0.0000001f);
+            const float mul1 = mh.x * mw * mw;
+            const float mul2 = mh.y * mw * mw;
             dm.x += (pm[0] * mw - pm[3] * mul1) * gx + (pm[1] * mw - pm[3] * mul2) * gy;
             dm.y += (pm[4] * mw - pm[7] * mul1) * gx + (pm[5] * mw - pm[7] * mul2) * gy;
             dm.z += (pm[8] * mw - pm[11] * mul1) * gx + (pm[9] * mw - pm[11] * mul2) * gy;
@@ -671,32 +632,30 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
             // SH
             if (a.shs) {
                 const float3 dir_orig = make_float3(p.x - a.campos[0], p.y - a.campos[1], p.z - a.campos[2]);
-                const float len = sqrtf(dir_orig.x * dir_orig.x + dir_orig.y * dir_orig.y + dir_orig.z * dir_orig.z);
-                const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
+                const float sum2 = dir_orig.x * dir_orig.x + dir_orig.y * dir_orig.y + dir_orig.z * dir_orig.z;
+                const float il = __builtin_amdgcn_rsqf(sum2);   // gradients only: hardware rsq
+                const float x = dir_orig.x * il, y = dir_orig.y * il, z = dir_orig.z * il;
                 const uint8_t cl = a.clamped[i];
                 const float dR[3] = {(cl & 1) ? 0.0f : gcol.x, (cl & 2) ? 0.0f : gcol.y, (cl & 4) ? 0.0f : gcol.z};
                 const float* sh = stage ? srow : a.shs + (size_t)i * M * 3;
                 float* dsh = stage ? srow : (a.dsh ? a.dsh + (size_t)i * M * 3 : nullptr);
                 const int deg = a.deg;
-                float dRdx[3] = {0, 0, 0}, dRdy[3] = {0, 0, 0}, dRdz[3] = {0, 0, 0};
-                float g[16];
+                float dLdx, dLdy, dLdz;
+                sh_bwd_dirsum(sh, deg, x, y, z, dR, dLdx, dLdy, dLdz);
+                // every coefficient has been read: overwrite the staged row with the gradient
+                float bs[16];
+                sh_bwd_basis(deg, x, y, z, bs);
 #pragma unroll
                 for (int ch = 0; ch < 3; ++ch) {
-                    sh_bwd_channel(sh, ch, deg, x, y, z, dR[ch], g, dRdx[ch], dRdy[ch], dRdz[ch]);
-                    // this channel's coefficients have all been read: overwrite them with the gradient
                     if (stage) {
 #pragma unroll
-                        for (int k = 0; k < MS; ++k) dsh[k * 3 + ch] = k < 16 ? g[k] : 0.0f;
+                        for (int k = 0; k < MS; ++k) dsh[k * 3 + ch] = k < 16 ? bs[k] * dR[ch] : 0.0f;
                     } else if (dsh) {
-                        for (int k = 0; k < M; ++k) put<ACC>(dsh + k * 3 + ch, k < 16 ? g[k] : 0.0f);
+                        for (int k = 0; k < M; ++k) put<ACC>(dsh + k * 3 + ch, k < 16 ? bs[k] * dR[ch] : 0.0f);
                     }
                 }
-                const float dLdx = dRdx[0] * dR[0] + dRdx[1] * dR[1] + dRdx[2] * dR[2];
-                const float dLdy = dRdy[0] * dR[0] + dRdy[1] * dR[1] + dRdy[2] * dR[2];
-                const float dLdz = dRdz[0] * dR[0] + dRdz[1] * dR[1] + dRdz[2] * dR[2];
                 const float3 v = dir_orig;
-                const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
-                const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+                const float invsum32 = il * il * il;
                 dm.x += ((sum2 - v.x * v.x) * dLdx - v.y * v.x * dLdy - v.z * v.x * dLdz) * invsum32;
                 dm.y += (-v.x * v.y * dLdx + (sum2 - v.y * v.y) * dLdy - v.z * v.y * dLdz) * invsum32;
                 dm.z += (-v.x * v.z * dLdx - v.y * v.z * dLdy + (sum2 - v.z * v.z) * dLdz) * invsum32;
@@ -799,9 +758,9 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd_views(PreprocessBwdViews
                 for (int k = 0; k < 6; ++k) dcov[k] += dcv[k];
                 const float* pm = cm.proj;
                 const float4 mh = xform4x4(pm, p);
-                const float mw = 1.0f / (mh.w + 0.0000001f);
-                const float mul1 = (pm[0] * p.x + pm[4] * p.y + pm[8] * p.z + pm[12]) * mw * mw;
-                const float mul2 = (pm[1] * p.x + pm[5] * p.y + pm[9] * p.z + pm[13]) * mw * mw;
+                const float mw = __builtin_amdgcn_rcpf(mh.w + 0.0000001f);
+                const float mul1 = mh.x * mw * mw;
+                const float mul2 = mh.y * mw * mw;
                 dmv.x += (pm[0] * mw - pm[3] * mul1) * gx + (pm[1] * mw - pm[3] * mul2) * gy;
                 dmv.y += (pm[4] * mw - pm[7] * mul1) * gx + (pm[5] * mw - pm[7] * mul2) * gy;
                 dmv.z += (pm[8] * mw - pm[11] * mul1) * gx + (pm[9] * mw - pm[11] * mul2) * gy;
@@ -811,25 +770,21 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd_views(PreprocessBwdViews
                 dmv.z += cm.view[10] * gd;
                 if (sh) {
                     const float3 dir_orig = make_float3(p.x - cm.campos[0], p.y - cm.campos[1], p.z - cm.campos[2]);
-                    const float len = sqrtf(dir_orig.x * dir_orig.x + dir_orig.y * dir_orig.y + dir_orig.z * dir_orig.z);
-                    const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
+                    const float sum2 = dir_orig.x * dir_orig.x + dir_orig.y * dir_orig.y + dir_orig.z * dir_orig.z;
+                    const float il = __builtin_amdgcn_rsqf(sum2);   // gradients only: hardware rsq
+                    const float x = dir_orig.x * il, y = dir_orig.y * il, z = dir_orig.z * il;
                     const uint8_t cl = cm.clamped[i];
                     const float dR[3] = {(cl & 1) ? 0.0f : rs[0], (cl & 2) ? 0.0f : rs[1], (cl & 4) ? 0.0f : rs[2]};
-                    float dRdx[3] = {0, 0, 0}, dRdy[3] = {0, 0, 0}, dRdz[3] = {0, 0, 0};
                     float bs[16];
                     sh_bwd_basis(cm.deg, x, y, z, bs);   // once for the three channels
 #pragma unroll
-                    for (int ch = 0; ch < 3; ++ch) {
-                        sh_bwd_dir(sh, ch, cm.deg, x, y, z, dRdx[ch], dRdy[ch], dRdz[ch]);
+                    for (int ch = 0; ch < 3; ++ch)
 #pragma unroll
                         for (int k = 0; k < 16; ++k) dsh[k * 3 + ch] += bs[k] * dR[ch];
-                    }
-                    const float dLdx = dRdx[0] * dR[0] + dRdx[1] * dR[1] + dRdx[2] * dR[2];
-                    const float dLdy = dRdy[0] * dR[0] + dRdy[1] * dR[1] + dRdy[2] * dR[2];
-                    const float dLdz = dRdz[0] * dR[0] + dRdz[1] * dR[1] + dRdz[2] * dR[2];
+                    float dLdx, dLdy, dLdz;
+                    sh_bwd_dirsum(sh, cm.deg, x, y, z, dR, dLdx, dLdy, dLdz);
                     const float3 w = dir_orig;
-                    const float sum2 = w.x * w.x + w.y * w.y + w.z * w.z;
-                    const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+                    const float invsum32 = il * il * il;
                     dmv.x += ((sum2 - w.x * w.x) * dLdx - w.y * w.x * dLdy - w.z * w.x * dLdz) * invsum32;
                     dmv.y += (-w.x * w.y * dLdx + (sum2 - w.y * w.y) * dLdy - w.z * w.y * dLdz) * invsum32;
                     dmv.z += (-w.x * w.z * dLdx - w.y * w.z * dLdy + (sum2 - w.z * w.z) * dLdz) * invsum32;

@@ -11,6 +11,7 @@ FLAGS="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -fhip-fp32-c
 for spec in "$@"; do
     name=${spec%%:*}; rest=${spec#*:}; src=${rest%%:*}; defs=${rest#*:}; defs=${defs//,/ }
     base=${src%.hip}
+    [ "$base" = preprocess ] && defs="$defs -fno-slp-vectorize"   # as in the Makefile
     /opt/rocm/bin/hipcc $FLAGS $defs -c -o $OUT/obj/${base}_$name.o $src
     objs=$(ls $OBJ/*.o | grep -v "/$base.o")
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/liblsr_$name.so $objs $OUT/obj/${base}_$name.o
