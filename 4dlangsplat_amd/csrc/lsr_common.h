@@ -279,7 +279,8 @@ __device__ __forceinline__ bool quad_may_touch(float2 xy, float4 co, float x0, f
 // end is convex in dy), and symmetrically on the right.  In real arithmetic this is exactly the
 // box test of quad_may_touch; in float, Q carries the same kind of margin (doubled) and the
 // extents are widened by 1e-4 hx + 1e-3 px, so a quadrant where some pixel passes the
-// compositors' prefilter is never dropped (tests/test_parity_gpu.py checks the bits).
+// compositors' prefilter is never dropped (tests/test_parity_gpu.py checks the bits).  The bits
+// only need to be conservative: the hardware sqrt / rcp (1 ulp) sit far inside those margins.
 struct EmitSplat {
     float X, Y;        // centre (pixels)
     float a, b;        // conic x^2 and xy terms (q = a dx^2 + 2 b dx dy + c dy^2)
@@ -293,20 +294,21 @@ __device__ __forceinline__ EmitSplat emit_splat(float2 xy, float4 co) {
     s.a = co.x; s.b = co.y;
     const float c = co.z;
     s.det = co.x * c - co.y * co.y;
-    s.inv_a = 1.0f / co.x;
+    s.inv_a = __builtin_amdgcn_rcpf(co.x);
     const float Q0 = -2.0f * skip_power(co.w);
     float hx = 0.0f, hy = -1.0f;
     s.Q = Q0;
     if (Q0 > 0.0f && s.det > 0.0f) {
-        hx = sqrtf(Q0 * c / s.det);
-        hy = sqrtf(Q0 * co.x / s.det);
+        const float rdet = __builtin_amdgcn_rcpf(s.det);
+        hx = __builtin_amdgcn_sqrtf(Q0 * c * rdet);
+        hy = __builtin_amdgcn_sqrtf(Q0 * co.x * rdet);
         const float M = co.x * hx * hx + c * hy * hy + 2.0f * fabsf(co.y) * hx * hy;
         s.Q = Q0 + 2e-5f * M + 2e-4f;
-        hx = sqrtf(s.Q * c / s.det);
-        hy = sqrtf(s.Q * co.x / s.det);
+        hx = __builtin_amdgcn_sqrtf(s.Q * c * rdet);
+        hy = __builtin_amdgcn_sqrtf(s.Q * co.x * rdet);
     }
     s.hx = hx; s.hy = hy;
-    s.dyl = co.y * hx / c;
+    s.dyl = co.y * hx * __builtin_amdgcn_rcpf(c);
     s.dyr = -s.dyl;
     return s;
 }
@@ -319,8 +321,8 @@ __device__ __forceinline__ uint32_t emit_quad_mask(const EmitSplat& s, int x0, i
         const int yb0 = y0 + 8 * band, yb1 = min(yb0 + 7, H - 1);
         // dy = Y - y over the band's pixel rows, clipped to R's y extent
         const float u0 = fmaxf(s.Y - (float)yb1, -s.hy - ex), u1 = fminf(s.Y - (float)yb0, s.hy + ex);
-        const float r0 = sqrtf(fmaxf(0.0f, s.a * s.Q - s.det * u0 * u0));
-        const float r1 = sqrtf(fmaxf(0.0f, s.a * s.Q - s.det * u1 * u1));
+        const float r0 = __builtin_amdgcn_sqrtf(fmaxf(0.0f, s.a * s.Q - s.det * u0 * u0));
+        const float r1 = __builtin_amdgcn_sqrtf(fmaxf(0.0f, s.a * s.Q - s.det * u1 * u1));
         const float l0 = (-s.b * u0 - r0) * s.inv_a, l1 = (-s.b * u1 - r1) * s.inv_a;
         const float g0 = (-s.b * u0 + r0) * s.inv_a, g1 = (-s.b * u1 + r1) * s.inv_a;
         const float xmin = (s.dyl >= u0 && s.dyl <= u1 ? -s.hx : fminf(l0, l1)) - ex;
