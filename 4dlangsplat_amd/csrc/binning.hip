@@ -51,18 +51,22 @@ void launch_gather_tile_counts(int P, const uint32_t* nsorted, const uint32_t* o
 // every list entry (quad_may_touch); once per instance here, so their scans read only the point
 // list (no centre / conic gathers).  An instance reaching no quadrant would be
 // skipped at every pixel of its tile: it gets the past-the-end tile key (dropped from the lists).
-__global__ void __launch_bounds__(256) k_emit(int P, const uint32_t* __restrict__ order,
-                                              const uint32_t* __restrict__ offsets,
-                                              const uint32_t* __restrict__ counts,
-                                              const uint2* __restrict__ rect_sorted, int gx, int gy, int W, int H,
-                                              const float2* __restrict__ xy, const float4* __restrict__ conic_o,
-                                              uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
-                                              ClearList clear) {
+__global__ void __launch_bounds__(256) k_emit(const EmitBatch eb) {
     __shared__ uint32_t s_off[4][64];
     __shared__ uint2 s_rc[4][64];
     __shared__ uint32_t s_id[4][64];
     __shared__ EmitSplat s_sp[4][64];
-    clear_words(clear);   // tile ranges, per-tile bounds, tile-sort workspace (used after this kernel)
+    const EmitView& ev = eb.v[blockIdx.y];   // one view of the batch per grid row
+    const int P = eb.P, gx = eb.grid_x, gy = eb.grid_y, W = eb.W, H = eb.H;
+    const uint32_t* __restrict__ order = ev.order;
+    const uint32_t* __restrict__ offsets = ev.offsets;
+    const uint32_t* __restrict__ counts = ev.counts;
+    const uint2* __restrict__ rect_sorted = ev.rect_sorted;
+    const float2* __restrict__ xy = ev.xy;
+    const float4* __restrict__ conic_o = ev.conic_o;
+    uint32_t* __restrict__ keys = ev.keys;
+    uint32_t* __restrict__ vals = ev.vals;
+    clear_words(ev.clear);   // tile ranges, per-tile bounds, tile-sort workspace (used after this kernel)
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int base = (blockIdx.x * 4 + w) * 64;
     if (base >= P) return;                                   // wave-uniform
@@ -116,13 +120,9 @@ __global__ void __launch_bounds__(256) k_emit(int P, const uint32_t* __restrict_
     }
 }
 
-void launch_emit_instances(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* counts,
-                           const uint2* rect_sorted, int grid_x, int grid_y, int W, int H, const float2* xy,
-                           const float4* conic_o, uint32_t* keys, uint32_t* vals, const ClearList& clear,
-                           hipStream_t st) {
-    if (P == 0) return;
-    hipLaunchKernelGGL(k_emit, dim3((P + 255) / 256), dim3(256), 0, st, P, order, offsets, counts, rect_sorted,
-                       grid_x, grid_y, W, H, xy, conic_o, keys, vals, clear);
+void launch_emit_instances(const EmitBatch& eb, int nv, hipStream_t st) {
+    if (eb.P == 0 || nv <= 0) return;
+    hipLaunchKernelGGL(k_emit, dim3((eb.P + 255) / 256, nv), dim3(256), 0, st, eb);
 }
 
 // inst_off[g] = first instance slot of Gaussian g: only the deterministic backward needs it (its
@@ -142,19 +142,26 @@ void launch_scatter_inst_off(int P, const uint32_t* order, const uint32_t* offse
                        inst_off);
 }
 
-__global__ void __launch_bounds__(256) k_tile_ranges(size_t K, const uint32_t* __restrict__ keys, uint32_t ntiles,
-                                                     uint2* __restrict__ ranges) {
+__global__ void __launch_bounds__(256) k_tile_ranges(const RangesBatch rb, uint32_t ntiles) {
+    const RangesSeg& sg = rb.s[blockIdx.y];
+    const size_t K = sg.K;
+    const uint32_t* __restrict__ keys = sg.keys;
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= K) return;
     const uint32_t t = keys[i];
     if (t >= ntiles) return;   // dropped instances (past-the-end key)
-    if (i == 0 || keys[i - 1] != t) ranges[t].x = (uint32_t)i;
-    if (i == K - 1 || keys[i + 1] != t) ranges[t].y = (uint32_t)(i + 1);
+    if (i == 0 || keys[i - 1] != t) sg.ranges[t].x = (uint32_t)i;
+    if (i == K - 1 || keys[i + 1] != t) sg.ranges[t].y = (uint32_t)(i + 1);
 }
 
-void launch_tile_ranges(size_t K, const uint32_t* keys, uint32_t ntiles, uint2* ranges, hipStream_t st) {
-    if (K == 0) return;
-    hipLaunchKernelGGL(k_tile_ranges, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, st, K, keys, ntiles, ranges);
+void launch_tile_ranges(const RangesSeg* segs, int nseg, uint32_t ntiles, hipStream_t st) {
+    RangesBatch rb{};
+    int ns = 0;
+    size_t kmax = 0;
+    for (int i = 0; i < nseg; ++i)
+        if (segs[i].K > 0) { rb.s[ns++] = segs[i]; kmax = std::max(kmax, segs[i].K); }
+    if (ns == 0) return;
+    hipLaunchKernelGGL(k_tile_ranges, dim3((unsigned)((kmax + 255) / 256), ns), dim3(256), 0, st, rb, ntiles);
 }
 
 }  // namespace lsr

@@ -230,6 +230,35 @@ int check_common(const lsr_settings* s, const lsr_fwd_in* in) {
     return LSR_OK;
 }
 
+// The Gaussians' side of a preprocess launch (shared by its views).
+void preprocess_shared(lsr::PreprocessArgs& a, const lsr_settings* s, const lsr_fwd_in* in) {
+    const int W = s->image_width, H = s->image_height;
+    a.P = in->P; a.M = in->M; a.deg = s->sh_degree; a.W = W; a.H = H;
+    a.grid_x = (W + LSR_TILE_X - 1) / LSR_TILE_X; a.grid_y = (H + LSR_TILE_Y - 1) / LSR_TILE_Y;
+    a.scale_modifier = s->scale_modifier;
+    a.means3D = in->means3D; a.scales = in->scales; a.rotations = in->rotations; a.opacities = in->opacities;
+    a.shs = in->shs; a.colors_precomp = in->colors_precomp; a.cov3D_precomp = in->cov3D_precomp;
+}
+// One view's camera and outputs.  The preprocess also writes the depth sort's initial values
+// (ids), zeroes the split-backward accumulator rows of listed Gaussians, and clears the sort
+// workspace and the counters [0] K, [1] depth sort error word, [2] tile sort error word: no
+// separate fill launches.
+void preprocess_view(lsr::PreprocessView& v, const lsr_settings* s, const Geom& g, int* radii, int P) {
+    v.tanfovx = s->tanfovx; v.tanfovy = s->tanfovy;
+    v.focal_x = (float)s->image_width / (2.0f * s->tanfovx);
+    v.focal_y = (float)s->image_height / (2.0f * s->tanfovy);
+    v.view = s->viewmatrix; v.proj = s->projmatrix; v.campos = s->campos;
+    v.radii = radii; v.radius = g.radius; v.tiles = g.tiles; v.rect = g.rect; v.key = g.key_a; v.xy = g.xy;
+    v.conic_o = g.conic_o; v.rgbd = g.rgbd; v.clamped = g.clamped;
+    v.order = g.val_a;
+    v.rank_counts = lsr::radix_sort_fuses_gather() ? g.counts : nullptr;
+    v.acc = g.acc;
+    v.clear.p[0] = reinterpret_cast<uint32_t*>(g.sort_tmp);
+    v.clear.n[0] = (uint32_t)(lsr::radix_temp_zero_bytes((size_t)P, 0, 32) / 4);
+    v.clear.p[1] = g.total;
+    v.clear.n[1] = 3;
+}
+
 }  // namespace
 
 extern "C" {
@@ -274,26 +303,9 @@ int lsr_forward_preprocess_async(const lsr_settings* s, const lsr_fwd_in* in, ls
         return LSR_OK;
     }
     lsr::PreprocessArgs a{};
-    a.P = P; a.M = in->M; a.deg = s->sh_degree; a.W = W; a.H = H; a.grid_x = gx; a.grid_y = gy;
-    a.tanfovx = s->tanfovx; a.tanfovy = s->tanfovy;
-    a.focal_x = (float)W / (2.0f * s->tanfovx);
-    a.focal_y = (float)H / (2.0f * s->tanfovy);
-    a.scale_modifier = s->scale_modifier;
-    a.means3D = in->means3D; a.scales = in->scales; a.rotations = in->rotations; a.opacities = in->opacities;
-    a.shs = in->shs; a.colors_precomp = in->colors_precomp; a.cov3D_precomp = in->cov3D_precomp;
-    a.view = s->viewmatrix; a.proj = s->projmatrix; a.campos = s->campos;
-    a.radii = out->radii; a.radius = g.radius; a.tiles = g.tiles; a.rect = g.rect; a.key = g.key_a; a.xy = g.xy; a.conic_o = g.conic_o; a.rgbd = g.rgbd;
-    a.clamped = g.clamped;
-    // the preprocess also writes the depth sort's initial values (ids), zeroes the split-backward
-    // accumulator rows of listed Gaussians, and clears the sort workspace and the counters
-    // [0] K, [1] depth sort error word, [2] tile sort error word: no separate fill launches
-    a.order = g.val_a;
-    a.rank_counts = lsr::radix_sort_fuses_gather() ? g.counts : nullptr;
-    a.acc = g.acc;
-    a.clear.p[0] = reinterpret_cast<uint32_t*>(g.sort_tmp);
-    a.clear.n[0] = (uint32_t)(lsr::radix_temp_zero_bytes((size_t)P, 0, 32) / 4);
-    a.clear.p[1] = g.total;
-    a.clear.n[1] = 3;
+    preprocess_shared(a, s, in);
+    a.nv = 1;
+    preprocess_view(a.v[0], s, g, out->radii, P);
     {
         PhaseTimer t(LSR_PHASE_PREPROCESS, st);
         lsr::launch_preprocess(a, st);
@@ -325,6 +337,75 @@ int lsr_forward_preprocess_async(const lsr_settings* s, const lsr_fwd_in* in, ls
     return LSR_OK;
 }
 
+int lsr_forward_preprocess_views_async(int32_t n_views, const lsr_settings* const* s, const lsr_fwd_in* in,
+                                       lsr_fwd_out* const* out, void* const* geom, uint32_t* host_counts,
+                                       lsr_stream_t stream) {
+    if (n_views < 1 || !s || !out || !geom || !host_counts)
+        return fail(LSR_EINVAL, "n_views >= 1 and the per-view arrays and host_counts are required");
+    if (!lsr::radix_sort_fuses_gather()) {   // look-back build: the per-view path
+        for (int v = 0; v < n_views; ++v) {
+            int rc = lsr_forward_preprocess_async(s[v], in, out[v], geom[v], host_counts + 2 * v, stream);
+            if (rc) return rc;
+        }
+        return LSR_OK;
+    }
+    for (int v = 0; v < n_views; ++v) {
+        int rc = check_common(s[v], in);
+        if (rc) return rc;
+        if (!out[v] || (!out[v]->radii && in->P > 0)) return fail(LSR_EINVAL, "radii output is required");
+        if (!geom[v]) return fail(LSR_EINVAL, "geom workspaces are required");
+        if (s[v]->image_width != s[0]->image_width || s[v]->image_height != s[0]->image_height ||
+            s[v]->sh_degree != s[0]->sh_degree || s[v]->scale_modifier != s[0]->scale_modifier)
+            return fail(LSR_EINVAL, "batched views must share the image size, sh_degree and scale_modifier");
+    }
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int P = in->P;
+    if (P == 0) {
+        for (int v = 0; v < 2 * n_views; ++v) host_counts[v] = 0;
+        return LSR_OK;
+    }
+    for (int v0 = 0; v0 < n_views; v0 += lsr::LSR_MAX_VIEWS) {
+        const int nv = std::min(n_views - v0, lsr::LSR_MAX_VIEWS);
+        lsr::PreprocessArgs a{};
+        preprocess_shared(a, s[v0], in);
+        a.nv = nv;
+        lsr::SortSeg ss[lsr::LSR_MAX_VIEWS] = {};
+        lsr::ScanSeg sc[lsr::LSR_MAX_VIEWS] = {};
+        for (int k = 0; k < nv; ++k) {
+            Geom g = carve_geom(geom[v0 + k], (size_t)P, nullptr);
+            preprocess_view(a.v[k], s[v0 + k], g, out[v0 + k]->radii, P);
+            // depth order of the visible Gaussians (the first pass drops culled keys, kept count in
+            // g.total[3]; the last pass writes the depth-ranked rectangles and instance counts)
+            ss[k] = lsr::SortSeg{g.key_a, g.val_a, g.key_b, g.val_b, g.sort_tmp, g.total + 3,
+                                 lsr::SortGather{g.rect, g.counts, g.rect_sorted}, (size_t)P};
+            sc[k] = lsr::ScanSeg{g.counts, g.offsets, g.total, reinterpret_cast<uint32_t*>(g.scan_tmp), (size_t)P};
+        }
+        {
+            PhaseTimer t(LSR_PHASE_PREPROCESS, st);
+            lsr::launch_preprocess(a, st);
+        }
+        LSR_LAUNCHED("preprocess", st, s[v0]->debug);
+        {
+            PhaseTimer t(LSR_PHASE_DEPTH_SORT, st);
+            if (lsr::radix_sort_batch(ss, nv, 0, 32, st) != (bool)depth_sort_result_in_b())
+                return fail(LSR_EHIP, "internal: depth sort parity");
+        }
+        LSR_LAUNCHED("depth sort", st, s[v0]->debug);
+        {
+            PhaseTimer t(LSR_PHASE_INSTANCE_SCAN, st);
+            lsr::exclusive_scan_batch(sc, nv, st);
+        }
+        LSR_LAUNCHED("instance scan", st, s[v0]->debug);
+        for (int k = 0; k < nv; ++k) {
+            Geom g = carve_geom(geom[v0 + k], (size_t)P, nullptr);
+            if (g_inject_sort_fault.load() & 1u) LSR_HIP(hipMemsetAsync(g.total + 1, 1, 1, st));   // test hook
+            LSR_HIP(hipMemcpyAsync(host_counts + 2 * (v0 + k), g.total, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                   st));
+        }
+    }
+    return LSR_OK;
+}
+
 int lsr_forward_preprocess(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_out* out, void* geom,
                            int64_t* num_rendered, lsr_stream_t stream) {
     if (!num_rendered) return fail(LSR_EINVAL, "geom workspace and num_rendered are required");
@@ -339,53 +420,89 @@ int lsr_forward_preprocess(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_
 
 int lsr_forward_binning(const lsr_settings* s, const lsr_fwd_in* in, void* geom, void* binning, void* img,
                         int64_t num_rendered, lsr_stream_t stream) {
-    int rc = check_common(s, in);
-    if (rc) return rc;
-    if (!geom || !img || (num_rendered > 0 && !binning)) return fail(LSR_EINVAL, "workspaces are required");
+    return lsr_forward_binning_views(1, &s, in, &geom, &binning, &img, &num_rendered, stream);
+}
+
+int lsr_forward_binning_views(int32_t n_views, const lsr_settings* const* s, const lsr_fwd_in* in, void* const* geom,
+                              void* const* binning, void* const* img, const int64_t* num_rendered,
+                              lsr_stream_t stream) {
+    if (n_views < 1 || !s || !geom || !binning || !img || !num_rendered)
+        return fail(LSR_EINVAL, "n_views >= 1 and the per-view arrays are required");
+    for (int v = 0; v < n_views; ++v) {
+        int rc = check_common(s[v], in);
+        if (rc) return rc;
+        if (s[v]->image_width != s[0]->image_width || s[v]->image_height != s[0]->image_height)
+            return fail(LSR_EINVAL, "batched views must share the image size");
+        if (!geom[v] || !img[v] || (num_rendered[v] > 0 && !binning[v])) return fail(LSR_EINVAL, "workspaces are required");
+    }
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const int P = in->P, W = s->image_width, H = s->image_height;
+    const int P = in->P, W = s[0]->image_width, H = s[0]->image_height;
     const int gx = (W + LSR_TILE_X - 1) / LSR_TILE_X, gy = (H + LSR_TILE_Y - 1) / LSR_TILE_Y;
-    const size_t K = (size_t)num_rendered;
-    Geom g = carve_geom(geom, (size_t)(P > 0 ? P : 1), nullptr);
-    Binning b = carve_binning(binning, K > 0 ? K : 1, nullptr);
-    Img m = carve_img(img, W, H, nullptr);
     const size_t ntiles = (size_t)gx * gy;
-    if (K == 0) {
-        LSR_HIP(hipMemsetAsync(m.ranges, 0, sizeof(uint2) * ntiles, st));
-        LSR_HIP(hipMemsetAsync(m.tile_max, 0, sizeof(uint32_t) * ntiles, st));
-    } else {
-        // the emission also clears the tile ranges, the per-tile replay bounds and the tile sort's
-        // workspace (no separate fill launches)
-        lsr::ClearList cl{};
-        cl.p[0] = reinterpret_cast<uint32_t*>(m.ranges);
-        cl.n[0] = (uint32_t)(2 * ntiles);
-        cl.p[1] = m.tile_max;
-        cl.n[1] = (uint32_t)ntiles;
-        cl.p[2] = reinterpret_cast<uint32_t*>(b.sort_tmp);
-        cl.n[2] = (uint32_t)(lsr::radix_temp_zero_bytes(K, 0, tile_bits((int)ntiles)) / 4);
+    const int tbits = tile_bits((int)ntiles);
+    for (int v0 = 0; v0 < n_views; v0 += lsr::LSR_MAX_VIEWS) {
+        const int nv = std::min(n_views - v0, lsr::LSR_MAX_VIEWS);
+        lsr::EmitBatch eb{};
+        eb.P = P; eb.grid_x = gx; eb.grid_y = gy; eb.W = W; eb.H = H;
+        lsr::SortSeg ss[lsr::LSR_MAX_VIEWS] = {};
+        lsr::RangesSeg rs[lsr::LSR_MAX_VIEWS] = {};
+        int ne = 0, ev_view[lsr::LSR_MAX_VIEWS];
+        for (int k = 0; k < nv; ++k) {
+            const int v = v0 + k;
+            const size_t K = (size_t)num_rendered[v];
+            Geom g = carve_geom(geom[v], (size_t)(P > 0 ? P : 1), nullptr);
+            Img m = carve_img(img[v], W, H, nullptr);
+            if (K == 0) {
+                LSR_HIP(hipMemsetAsync(m.ranges, 0, sizeof(uint2) * ntiles, st));
+                LSR_HIP(hipMemsetAsync(m.tile_max, 0, sizeof(uint32_t) * ntiles, st));
+                continue;
+            }
+            Binning b = carve_binning(binning[v], K, nullptr);
+            // the emission also clears the tile ranges, the per-tile replay bounds and the tile
+            // sort's workspace (no separate fill launches)
+            lsr::EmitView& e = eb.v[ne];
+            e.order = g.val_a; e.offsets = g.offsets; e.counts = g.counts; e.rect_sorted = g.rect_sorted;
+            e.xy = g.xy; e.conic_o = g.conic_o; e.keys = b.key_a; e.vals = b.val_a;
+            e.clear.p[0] = reinterpret_cast<uint32_t*>(m.ranges);
+            e.clear.n[0] = (uint32_t)(2 * ntiles);
+            e.clear.p[1] = m.tile_max;
+            e.clear.n[1] = (uint32_t)ntiles;
+            e.clear.p[2] = reinterpret_cast<uint32_t*>(b.sort_tmp);
+            e.clear.n[2] = (uint32_t)(lsr::radix_temp_zero_bytes(K, 0, tbits) / 4);
+            ss[ne] = lsr::SortSeg{b.key_a, b.val_a, b.key_b, b.val_b, b.sort_tmp, nullptr,
+                                  lsr::SortGather{nullptr, nullptr, nullptr}, K};
+            rs[ne] = lsr::RangesSeg{K, tile_sort_in_b((int)ntiles) ? b.key_b : b.key_a, m.ranges};
+            ev_view[ne++] = v;
+        }
+        if (ne == 0) continue;
         {
             PhaseTimer t(LSR_PHASE_EMIT, st);
-            lsr::launch_emit_instances(P, g.val_a, g.offsets, g.counts, g.rect_sorted, gx, gy, W, H, g.xy, g.conic_o,
-                                       b.key_a, b.val_a, cl, st);
+            lsr::launch_emit_instances(eb, ne, st);
         }
-        LSR_LAUNCHED("emit", st, s->debug);
-        bool in_b;
+        LSR_LAUNCHED("emit", st, s[0]->debug);
         {
             PhaseTimer t(LSR_PHASE_TILE_SORT, st);
-            // error word g.total[2] (cleared by the preprocess): the compositor poisons its outputs
-            // and lsr_forward_status reports it
-            in_b = lsr::radix_sort_pairs(b.key_a, b.val_a, b.key_b, b.val_b, K, 0, tile_bits(gx * gy), b.sort_tmp,
-                                         g.total + 2, st, /*temp_zeroed=*/true);
+            bool in_b = true;
+            if (lsr::radix_sort_fuses_gather()) {   // reduce-then-scan: one set of launches for all views
+                in_b = lsr::radix_sort_batch(ss, ne, 0, tbits, st);
+            } else {                                // look-back build: per view, error word g.total[2]
+                for (int k = 0; k < ne; ++k) {
+                    Geom g = carve_geom(geom[ev_view[k]], (size_t)P, nullptr);
+                    in_b = lsr::radix_sort_pairs(ss[k].keys_a, ss[k].vals_a, ss[k].keys_b, ss[k].vals_b, ss[k].n, 0,
+                                                 tbits, ss[k].temp, g.total + 2, st, /*temp_zeroed=*/true);
+                }
+            }
+            if (in_b != tile_sort_in_b((int)ntiles)) return fail(LSR_EHIP, "internal: tile sort parity");
         }
-        if (in_b != tile_sort_in_b(gx * gy)) return fail(LSR_EHIP, "internal: tile sort parity");
-        if (g_inject_sort_fault.load() & 2u) LSR_HIP(hipMemsetAsync(g.total + 2, 1, 1, st));   // test hook
-        const uint32_t* keys = in_b ? b.key_b : b.key_a;
-        LSR_LAUNCHED("tile sort", st, s->debug);
+        if (g_inject_sort_fault.load() & 2u)   // test hook: error word g.total[2] (cleared by the preprocess)
+            for (int k = 0; k < nv; ++k)
+                LSR_HIP(hipMemsetAsync(carve_geom(geom[v0 + k], (size_t)P, nullptr).total + 2, 1, 1, st));
+        LSR_LAUNCHED("tile sort", st, s[0]->debug);
         {
             PhaseTimer t(LSR_PHASE_TILE_RANGES, st);
-            lsr::launch_tile_ranges(K, keys, (uint32_t)ntiles, m.ranges, st);
+            lsr::launch_tile_ranges(rs, ne, (uint32_t)ntiles, st);
         }
-        LSR_LAUNCHED("tile ranges", st, s->debug);
+        LSR_LAUNCHED("tile ranges", st, s[0]->debug);
     }
     return LSR_OK;
 }

@@ -16,6 +16,8 @@ struct ClearList {
     uint32_t* p[4];
     uint32_t n[4];
 };
+
+constexpr int LSR_MAX_VIEWS = 8;   // views per launch; more are processed in chunks
 __device__ __forceinline__ void clear_words(const ClearList& c) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
 #pragma unroll
@@ -60,20 +62,12 @@ __host__ __device__ __forceinline__ uint32_t rect_local_index(uint2 r, uint32_t 
     return (ty - y0) * (x1 - x0) + (tx - x0);
 }
 
-struct PreprocessArgs {
-    int P, M, deg, W, H, grid_x, grid_y;
-    float tanfovx, tanfovy, focal_x, focal_y, scale_modifier;
-    const float* means3D;
-    const float* scales;
-    const float* rotations;
-    const float* opacities;
-    const float* shs;
-    const float* colors_precomp;
-    const float* cov3D_precomp;
+// One camera of a preprocess launch and its outputs.
+struct PreprocessView {
+    float tanfovx, tanfovy, focal_x, focal_y;
     const float* view;
     const float* proj;
     const float* campos;
-    // outputs
     int* radii;
     int* radius;      // internal copy of radii (the backward recomputes tile rectangles)
     uint32_t* tiles;
@@ -88,6 +82,20 @@ struct PreprocessArgs {
                              // pass fills the visible ranks, the culled ones stay 0)
     float4* acc;      // if set: [P, ACC_PITCH / 4] backward accumulators, zeroed for visible rows
     ClearList clear;  // zeroed on the side (sort workspace, counters)
+};
+// Preprocess of nv <= LSR_MAX_VIEWS cameras over the same Gaussians: with nv > 1 a Gaussian's
+// inputs are read (and its cov3D built) once for all of them.
+struct PreprocessArgs {
+    int P, M, deg, W, H, grid_x, grid_y, nv;
+    float scale_modifier;
+    const float* means3D;
+    const float* scales;
+    const float* rotations;
+    const float* opacities;
+    const float* shs;
+    const float* colors_precomp;
+    const float* cov3D_precomp;
+    PreprocessView v[LSR_MAX_VIEWS];
 };
 
 struct PreprocessBwdArgs {
@@ -126,7 +134,6 @@ struct PreprocessBwdArgs {
 // per Gaussian, the view-independent rows (mean, scale, rotation, SH) are read once, each view's
 // screen-space sums (acc_small of its compositor backward) are pushed through that view's camera,
 // and the summed gradient rows are written (or accumulated) once.
-constexpr int LSR_MAX_VIEWS = 8;   // views per launch; more are processed in chunks
 struct ViewCam {
     const float* view;
     const float* proj;
@@ -278,6 +285,18 @@ void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t
 size_t scan_temp_bytes(size_t n);
 // exclusive scan of n u32 values; writes the total to *total (device) if non-null
 void exclusive_scan_u32(const uint32_t* in, uint32_t* out, size_t n, uint32_t* total, void* temp, hipStream_t st);
+// Exclusive scans of a batch of independent segments (in, out, n; total and the scan workspace
+// scan_temp_bytes(n) as for exclusive_scan_u32): two launches for all segments of 2K..8M values.
+constexpr int SCAN_SEG_TILES = 4096;
+struct ScanSeg {
+    const uint32_t* in;
+    uint32_t* out;
+    uint32_t* total;
+    uint32_t* partials;   // the segment's scan workspace
+    size_t n;
+};
+struct ScanBatch { ScanSeg s[LSR_MAX_VIEWS]; };
+void exclusive_scan_batch(const ScanSeg* segs, int nseg, hipStream_t st);
 size_t radix_temp_bytes(size_t n);
 // stable LSD sort of (key, value) pairs on bits [begin_bit, end_bit); returns true when the result
 // is in (keys_b, vals_b).  err (device word, may be null) is set non-zero if a look-back timed out.
@@ -292,6 +311,19 @@ struct SortGather {
     uint32_t* counts;
     uint2* rect_sorted;
 };
+// One sort of a batch: its own arrays, workspace (radix_temp_bytes(n)), optional kept count (the
+// first pass drops 0xFFFFFFFF keys and counts the rest there) and last-pass gather.
+struct SortSeg {
+    uint32_t *keys_a, *vals_a, *keys_b, *vals_b;
+    void* temp;
+    uint32_t* kept;
+    SortGather gather;
+    size_t n;
+};
+struct SortBatch { SortSeg s[LSR_MAX_VIEWS]; };
+// Sorts up to LSR_MAX_VIEWS independent segments with one launch per kernel of each pass (every
+// segment the same key bits); returns whether the results are in the (b) buffers.
+bool radix_sort_batch(const SortSeg* segs, int nseg, int begin_bit, int end_bit, hipStream_t st);
 bool radix_sort_fuses_gather();
 bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b, size_t n,
                       int begin_bit, int end_bit, void* temp, uint32_t* err, hipStream_t st, bool temp_zeroed = false,
@@ -308,13 +340,33 @@ void launch_gather_tile_counts(int P, const uint32_t* nsorted, const uint32_t* o
 // instance reaching none gets tile key ntiles and sorts past every list.
 constexpr uint32_t PL_ID_MASK = 0x0FFFFFFFu;
 constexpr int PL_QUAD_SHIFT = 28;
-void launch_emit_instances(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* counts,
-                           const uint2* rect_sorted, int grid_x, int grid_y, int W, int H, const float2* xy,
-                           const float4* conic_o, uint32_t* keys, uint32_t* vals, const ClearList& clear,
-                           hipStream_t st);
+// Instance emission of nv <= LSR_MAX_VIEWS views (one grid row per view; same P and tile grid).
+struct EmitView {
+    const uint32_t* order;       // depth-ranked ids
+    const uint32_t* offsets;     // first instance slot per depth rank
+    const uint32_t* counts;      // instances per depth rank
+    const uint2* rect_sorted;    // rectangles per depth rank
+    const float2* xy;
+    const float4* conic_o;
+    uint32_t* keys;
+    uint32_t* vals;
+    ClearList clear;
+};
+struct EmitBatch {
+    int P, grid_x, grid_y, W, H;
+    EmitView v[LSR_MAX_VIEWS];
+};
+void launch_emit_instances(const EmitBatch& eb, int nv, hipStream_t st);
 void launch_scatter_inst_off(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* counts,
                              uint32_t* inst_off, hipStream_t st);
-void launch_tile_ranges(size_t K, const uint32_t* keys, uint32_t ntiles, uint2* ranges, hipStream_t st);
+// Per-tile [start, end) of a batch of tile-sorted instance lists (one grid row per list).
+struct RangesSeg {
+    size_t K;
+    const uint32_t* keys;
+    uint2* ranges;
+};
+struct RangesBatch { RangesSeg s[LSR_MAX_VIEWS]; };
+void launch_tile_ranges(const RangesSeg* segs, int nseg, uint32_t ntiles, hipStream_t st);
 
 // compositing (render_fwd.hip / render_bwd.hip)
 void launch_render_fwd(const RenderFwdArgs& a, hipStream_t st);

@@ -100,25 +100,20 @@ __device__ __forceinline__ void stage_rows(float* __restrict__ lds, const float*
     }
 }
 
-template <int MS>  // SH coefficients per Gaussian known at compile time (0 = any M, read from global)
-__device__ __forceinline__ bool preprocess_one(const PreprocessArgs& a, int i) {   // true: rectangle
-    constexpr int M3 = MS * 3;
-    a.radii[i] = 0;
-    a.radius[i] = 0;
-    a.tiles[i] = 0;
-    a.rect[i] = make_uint2(0u, 0u);
-    a.clamped[i] = 0;
-    if (a.order) a.order[i] = (uint32_t)i;
-    if (a.rank_counts) a.rank_counts[i] = 0u;
-    if (a.key) a.key[i] = 0xFFFFFFFFu;
-    const float3 p = make_float3(a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]);
-    const float4 ph = xform4x4(a.proj, p);
-    const float3 pv = xform4x3(a.view, p);
-    if (pv.z <= 0.2f) return false;
-    const float pw = 1.0f / (ph.w + 0.0000001f);
-    const float3 pp = make_float3(ph.x * pw, ph.y * pw, ph.z * pw);
-
+// A Gaussian's view-independent inputs.  One view: read where the projection first needs them
+// (culled Gaussians skip the scale / rotation / SH reads).  Several views: read once, cov3D built
+// once, kept in registers for every view.
+template <int MS>
+struct GaussIn {
+    float3 p;
+    float op;
     float c3[6];
+    float sh[MS > 0 ? 3 * MS : 1];
+};
+__device__ __forceinline__ float3 load_mean(const PreprocessArgs& a, int i) {
+    return make_float3(a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]);
+}
+__device__ __forceinline__ void load_cov3d(const PreprocessArgs& a, int i, float (&c3)[6]) {
     if (a.cov3D_precomp) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) c3[k] = a.cov3D_precomp[6 * (size_t)i + k];
@@ -127,16 +122,68 @@ __device__ __forceinline__ bool preprocess_one(const PreprocessArgs& a, int i) {
         const float4 q = reinterpret_cast<const float4*>(a.rotations)[i];
         cov3d(s, a.scale_modifier, q, c3);
     }
+}
+// the SH row in registers, every load in flight at once (float4 when 16-byte aligned)
+template <int MS, int N>
+__device__ __forceinline__ void load_sh(const PreprocessArgs& a, int i, float (&shr)[N]) {
+    constexpr int M3 = MS * 3;
+    const float* src = a.shs + (size_t)i * M3;
+    if (M3 % 4 == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+#pragma unroll
+        for (int q = 0; q < M3 / 4; ++q) {
+            const float4 t = reinterpret_cast<const float4*>(src)[q];
+            shr[4 * q] = t.x; shr[4 * q + 1] = t.y; shr[4 * q + 2] = t.z; shr[4 * q + 3] = t.w;
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < M3; ++q) shr[q] = src[q];
+    }
+}
+template <int MS>
+__device__ __forceinline__ void load_gauss(const PreprocessArgs& a, int i, GaussIn<MS>& g) {
+    g.p = load_mean(a, i);
+    g.op = a.opacities[i];
+    load_cov3d(a, i, g.c3);
+    if constexpr (MS > 0) {
+        if (a.shs && !a.colors_precomp) load_sh<MS>(a, i, g.sh);
+    }
+}
+
+template <int MS, bool PRE>  // MS: SH coefficients per Gaussian (0 = any M, read from global); PRE: g holds the inputs
+__device__ __forceinline__ bool preprocess_one(const PreprocessArgs& a, const PreprocessView& v, const GaussIn<MS>& g,
+                                               int i) {   // true: rectangle
+    v.radii[i] = 0;
+    v.radius[i] = 0;
+    v.tiles[i] = 0;
+    v.rect[i] = make_uint2(0u, 0u);
+    v.clamped[i] = 0;
+    if (v.order) v.order[i] = (uint32_t)i;
+    if (v.rank_counts) v.rank_counts[i] = 0u;
+    if (v.key) v.key[i] = 0xFFFFFFFFu;
+    const float3 p = PRE ? g.p : load_mean(a, i);
+    const float4 ph = xform4x4(v.proj, p);
+    const float3 pv = xform4x3(v.view, p);
+    if (pv.z <= 0.2f) return false;
+    const float pw = 1.0f / (ph.w + 0.0000001f);
+    const float3 pp = make_float3(ph.x * pw, ph.y * pw, ph.z * pw);
+
+    float c3[6];
+    if constexpr (PRE) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) c3[k] = g.c3[k];
+    } else {
+        load_cov3d(a, i, c3);
+    }
     // EWA projection (computeCov2D)
     float3 t = pv;
-    const float limx = 1.3f * a.tanfovx, limy = 1.3f * a.tanfovy;
+    const float limx = 1.3f * v.tanfovx, limy = 1.3f * v.tanfovy;
     const float txtz = t.x / t.z, tytz = t.y / t.z;
     t.x = fminf(limx, fmaxf(-limx, txtz)) * t.z;
     t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
     m3 J = zero3();
-    J.m[0][0] = a.focal_x / t.z; J.m[0][2] = -(a.focal_x * t.x) / (t.z * t.z);
-    J.m[1][1] = a.focal_y / t.z; J.m[1][2] = -(a.focal_y * t.y) / (t.z * t.z);
-    const m3 T = mul(view_W(a.view), J);
+    J.m[0][0] = v.focal_x / t.z; J.m[0][2] = -(v.focal_x * t.x) / (t.z * t.z);
+    J.m[1][1] = v.focal_y / t.z; J.m[1][2] = -(v.focal_y * t.y) / (t.z * t.z);
+    const m3 T = mul(view_W(v.view), J);
     const m3 V = sym3(c3);
     const m3 A = mul(tr(T), tr(V));
     const m3 cv = mul(A, T);
@@ -144,7 +191,7 @@ __device__ __forceinline__ bool preprocess_one(const PreprocessArgs& a, int i) {
     const float det = ca * cc - cb * cb;
     if (det == 0.0f) return false;
     const float det_inv = 1.0f / det;
-    const float4 conic = make_float4(cc * det_inv, -cb * det_inv, ca * det_inv, a.opacities[i]);
+    const float4 conic = make_float4(cc * det_inv, -cb * det_inv, ca * det_inv, PRE ? g.op : a.opacities[i]);
     const float mid = 0.5f * (ca + cc);
     const float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
     const float l2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
@@ -178,30 +225,16 @@ __device__ __forceinline__ bool preprocess_one(const PreprocessArgs& a, int i) {
     if (a.colors_precomp) {
         rgb[0] = a.colors_precomp[3 * i]; rgb[1] = a.colors_precomp[3 * i + 1]; rgb[2] = a.colors_precomp[3 * i + 2];
     } else {
-        float3 dir = make_float3(p.x - a.campos[0], p.y - a.campos[1], p.z - a.campos[2]);
+        float3 dir = make_float3(p.x - v.campos[0], p.y - v.campos[1], p.z - v.campos[2]);
         const float len = sqrtf(dir.x * dir.x + dir.y * dir.y + dir.z * dir.z);
         dir.x = dir.x / len; dir.y = dir.y / len; dir.z = dir.z / len;
-        // the row in registers, every load in flight at once (float4 when 16-byte aligned)
         float shr[48];   // static indices reach coefficient 15; only the first M3 are loaded (deg validated)
         if constexpr (MS > 0) {
-            const float* src = a.shs + (size_t)i * M3;
-            if (M3 % 4 == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
-#ifdef LSR_ABL_SHCOAL   // timing ablation only: the wave's rows read coalesced (wrong colours)
-                const int ln = threadIdx.x & 63;
-                const float4* w4 = reinterpret_cast<const float4*>(a.shs + (size_t)(i - ln) * M3);
-#endif
+            if constexpr (PRE) {
 #pragma unroll
-                for (int q = 0; q < M3 / 4; ++q) {
-#ifdef LSR_ABL_SHCOAL
-                    const float4 v = w4[q * 64 + ln];
-#else
-                    const float4 v = reinterpret_cast<const float4*>(src)[q];
-#endif
-                    shr[4 * q] = v.x; shr[4 * q + 1] = v.y; shr[4 * q + 2] = v.z; shr[4 * q + 3] = v.w;
-                }
+                for (int q = 0; q < 3 * MS; ++q) shr[q] = g.sh[q];
             } else {
-#pragma unroll
-                for (int q = 0; q < M3; ++q) shr[q] = src[q];
+                load_sh<MS>(a, i, shr);
             }
         }
         const float* sh = MS > 0 ? shr : a.shs + (size_t)i * a.M * 3;
@@ -233,10 +266,10 @@ __device__ __forceinline__ bool preprocess_one(const PreprocessArgs& a, int i) {
             cl |= (res < 0.0f ? 1 : 0) << ch;
             rgb[ch] = res < 0.0f ? 0.0f : res;
         }
-        a.clamped[i] = cl;
+        v.clamped[i] = cl;
     }
-    a.radii[i] = radius;
-    a.radius[i] = radius;
+    v.radii[i] = radius;
+    v.radius[i] = radius;
     uint32_t qmap = 0;   // quadrant map of a rectangle of <= 2 x 2 tiles (the binning's emit_quad_mask)
 #ifdef LSR_ABL_NOQMAP
     if (false) {   // timing ablation only (instances of small rectangles then reach no quadrant)
@@ -252,33 +285,29 @@ __device__ __forceinline__ bool preprocess_one(const PreprocessArgs& a, int i) {
             }
     }
     const uint2 rc = rect_pack((uint32_t)cmin.x, (uint32_t)cmin.y, (uint32_t)cmax.x, (uint32_t)cmax.y, qmap);
-    a.rect[i] = rc;
+    v.rect[i] = rc;
     // instances it will emit: a small rectangle's tiles with a reachable quadrant (none: the
     // Gaussian blends no pixel and is not listed -- its gradient is exactly zero)
-    a.tiles[i] = rect_count(rc);
-    if (a.key) a.key[i] = __float_as_uint(pv.z);
-    a.xy[i] = pix;
-    a.conic_o[i] = conic;
-    a.rgbd[i] = make_float4(rgb[0], rgb[1], rgb[2], pv.z);
+    v.tiles[i] = rect_count(rc);
+    if (v.key) v.key[i] = __float_as_uint(pv.z);
+    v.xy[i] = pix;
+    v.conic_o[i] = conic;
+    v.rgbd[i] = make_float4(rgb[0], rgb[1], rgb[2], pv.z);
     return ntiles > 0;
 }
 
-template <int MS>
-__global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
-    clear_words(a.clear);
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool rect = i < a.P && preprocess_one<MS>(a, i);
+// Only rectangles receive backward atomics (a superset of the listed): zero their accumulator
+// rows, the wave's 64 rows written as whole float4 runs (coalesced; a row per lane would write 64
+// strided partial lines per store).  Every lane of the wave calls this.
+__device__ __forceinline__ void zero_acc_rows(float4* acc, bool rect, int i) {
 #ifdef LSR_ABL_NOACCZERO   // timing ablation only
-    if (true) return;
+    return;
 #endif
-    if (!a.acc) return;
-    // Only rectangles receive backward atomics (a superset of the listed): zero their accumulator
-    // rows, the wave's 64 rows written as whole float4 runs (coalesced; a row per lane would
-    // write 64 strided partial lines per store).
+    if (!acc) return;
     const uint64_t m = __ballot(rect);
     if (m == 0) return;
     const int ln = threadIdx.x & 63;
-    float4* w = a.acc + (size_t)(i - ln) * (ACC_PITCH / 4);
+    float4* w = acc + (size_t)(i - ln) * (ACC_PITCH / 4);
 #pragma unroll
     for (int q = 0; q < ACC_PITCH / 4; ++q) {
         const int e = q * 64 + ln;
@@ -286,16 +315,42 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
     }
 }
 
-void launch_preprocess(const PreprocessArgs& a, hipStream_t st) {
-    if (a.P == 0) return;
-    const dim3 grid((a.P + 255) / 256), block(256);
-    switch ((a.shs && !a.colors_precomp) ? a.M : 0) {
-        case 1: hipLaunchKernelGGL(k_preprocess<1>, grid, block, 0, st, a); break;
-        case 4: hipLaunchKernelGGL(k_preprocess<4>, grid, block, 0, st, a); break;
-        case 9: hipLaunchKernelGGL(k_preprocess<9>, grid, block, 0, st, a); break;
-        case 16: hipLaunchKernelGGL(k_preprocess<16>, grid, block, 0, st, a); break;
-        default: hipLaunchKernelGGL(k_preprocess<0>, grid, block, 0, st, a); break;
+template <int MS, bool MULTI>
+__global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    GaussIn<MS> g;
+    if constexpr (!MULTI) {
+        clear_words(a.v[0].clear);
+        const bool rect = i < a.P && preprocess_one<MS, false>(a, a.v[0], g, i);
+        zero_acc_rows(a.v[0].acc, rect, i);
+    } else {
+        const bool ok = i < a.P;
+        if (ok) load_gauss<MS>(a, i, g);
+        for (int k = 0; k < a.nv; ++k) {   // uniform: the view's fields are scalar loads
+            const PreprocessView& v = a.v[k];
+            clear_words(v.clear);
+            const bool rect = ok && preprocess_one<MS, true>(a, v, g, i);
+            zero_acc_rows(v.acc, rect, i);
+        }
     }
+}
+
+void launch_preprocess(const PreprocessArgs& a, hipStream_t st) {
+    if (a.P == 0 || a.nv <= 0) return;
+    const dim3 grid((a.P + 255) / 256), block(256);
+#define LSR_PP(MS)                                                                   \
+    do {                                                                             \
+        if (a.nv > 1) hipLaunchKernelGGL((k_preprocess<MS, true>), grid, block, 0, st, a);  \
+        else hipLaunchKernelGGL((k_preprocess<MS, false>), grid, block, 0, st, a);          \
+    } while (0)
+    switch ((a.shs && !a.colors_precomp) ? a.M : 0) {
+        case 1: LSR_PP(1); break;
+        case 4: LSR_PP(4); break;
+        case 9: LSR_PP(9); break;
+        case 16: LSR_PP(16); break;
+        default: LSR_PP(0); break;
+    }
+#undef LSR_PP
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -76,19 +76,38 @@ __global__ void __launch_bounds__(256) k_scan_down(const uint32_t* __restrict__ 
     if (total && threadIdx.x == 0 && gridDim.x == 1) *total = block_total;
 }
 
-// Second pass of a two-kernel scan: block b sums the partials of blocks [0, b) itself (no
+// Two-kernel scan of up to 4096 tiles, for a batch of segments (blockIdx.y): the first kernel
+// writes every tile's sum; in the second, block b sums the partials of blocks [0, b) itself (no
 // separate scan of the partials: one dependent launch less), then scans its tile.  Block 0 also
-// writes the grand total.
-__global__ void __launch_bounds__(256) k_scan_down_sum(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
-                                                       size_t n, const uint32_t* __restrict__ partials, int nb,
-                                                       uint32_t* __restrict__ total) {
+// writes the grand total.  Blocks past a segment's own tile count return at once.
+__global__ void __launch_bounds__(256) k_scan_reduce_seg(const ScanBatch bt) {
+    __shared__ uint32_t s_wave[4];
+    const ScanSeg& sg = bt.s[blockIdx.y];
+    const size_t n = sg.n;
+    if ((size_t)blockIdx.x * SCAN_TILE >= n) return;                  // block-uniform
+    const size_t base = (size_t)blockIdx.x * SCAN_TILE + (size_t)threadIdx.x * SCAN_ITEMS;
+    uint32_t s = 0;
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) s += (base + i < n) ? sg.in[base + i] : 0u;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) s += __shfl_xor(s, o);
+    if ((threadIdx.x & 63) == 0) s_wave[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) sg.partials[blockIdx.x] = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+}
+
+__global__ void __launch_bounds__(256) k_scan_down_sum(const ScanBatch bt) {
     __shared__ uint32_t s_wave[4];
     __shared__ uint32_t s_base[2];
+    const ScanSeg& sg = bt.s[blockIdx.y];
+    const size_t n = sg.n;
+    const int nb = (int)((n + SCAN_TILE - 1) / SCAN_TILE);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int b = blockIdx.x;
+    if (b >= nb) return;                                               // block-uniform
     uint32_t pre = 0, all = 0;
     for (int i = tid; i < nb; i += 256) {
-        const uint32_t v = partials[i];
+        const uint32_t v = sg.partials[i];
         pre += i < b ? v : 0u;
         all += v;
     }
@@ -106,16 +125,16 @@ __global__ void __launch_bounds__(256) k_scan_down_sum(const uint32_t* __restric
     if (tid == 0) s_base[1] = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
     __syncthreads();
     const uint32_t b0 = s_base[0];
-    if (total && b == 0 && tid == 0) *total = s_base[1];
+    if (sg.total && b == 0 && tid == 0) *sg.total = s_base[1];
     const size_t base = (size_t)b * SCAN_TILE + (size_t)tid * SCAN_ITEMS;
     uint32_t v[SCAN_ITEMS];
 #pragma unroll
-    for (int i = 0; i < SCAN_ITEMS; ++i) v[i] = (base + i < n) ? in[base + i] : 0u;
+    for (int i = 0; i < SCAN_ITEMS; ++i) v[i] = (base + i < n) ? sg.in[base + i] : 0u;
     uint32_t block_total;
     block_exclusive_scan8(v, s_wave, block_total);
 #pragma unroll
     for (int i = 0; i < SCAN_ITEMS; ++i)
-        if (base + i < n) out[base + i] = v[i] + b0;
+        if (base + i < n) sg.out[base + i] = v[i] + b0;
 }
 
 size_t scan_temp_bytes(size_t n) {
@@ -135,10 +154,9 @@ void exclusive_scan_u32(const uint32_t* in, uint32_t* out, size_t n, uint32_t* t
     }
     const size_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
     uint32_t* partials = reinterpret_cast<uint32_t*>(temp);
-    if (nb <= 4096) {   // up to 8M values: the scan of the partials is folded into the second pass
-        hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nb), dim3(256), 0, st, in, n, partials);
-        hipLaunchKernelGGL(k_scan_down_sum, dim3((unsigned)nb), dim3(256), 0, st, in, out, n, (const uint32_t*)partials,
-                           (int)nb, total);
+    if (nb <= (size_t)SCAN_SEG_TILES) {   // up to 8M values: the scan of the partials is folded into the second pass
+        const ScanSeg sg{in, out, total, partials, n};
+        exclusive_scan_batch(&sg, 1, st);
         return;
     }
     uint32_t* scanned = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(temp) + align_up(nb * 4, 256));
@@ -147,6 +165,25 @@ void exclusive_scan_u32(const uint32_t* in, uint32_t* out, size_t n, uint32_t* t
     exclusive_scan_u32(partials, scanned, nb, total, deeper, st);
     hipLaunchKernelGGL(k_scan_down, dim3((unsigned)nb), dim3(256), 0, st, in, out, n, (const uint32_t*)scanned,
                        (uint32_t*)nullptr);
+}
+
+void exclusive_scan_batch(const ScanSeg* segs, int nseg, hipStream_t st) {
+    ScanBatch bt{};
+    int ns = 0;
+    size_t nbmax = 0;
+    for (int i = 0; i < nseg; ++i) {
+        const ScanSeg& g = segs[i];
+        const size_t nb = (g.n + SCAN_TILE - 1) / SCAN_TILE;
+        if (g.n > (size_t)SCAN_TILE && nb <= (size_t)SCAN_SEG_TILES) {
+            bt.s[ns++] = g;
+            nbmax = std::max(nbmax, nb);
+        } else {
+            exclusive_scan_u32(g.in, g.out, g.n, g.total, g.partials, st);   // one tile, or beyond 8M values
+        }
+    }
+    if (ns == 0) return;
+    hipLaunchKernelGGL(k_scan_reduce_seg, dim3((unsigned)nbmax, ns), dim3(256), 0, st, bt);
+    hipLaunchKernelGGL(k_scan_down_sum, dim3((unsigned)nbmax, ns), dim3(256), 0, st, bt);
 }
 
 // ---- radix sort ---------------------------------------------------------------------------------
@@ -396,15 +433,32 @@ __global__ void __launch_bounds__(256) k_radix_pass(const uint32_t* __restrict__
 __device__ __forceinline__ size_t rts_n(size_t n, const uint32_t* n_dev) {
     return n_dev ? min(n, (size_t)*n_dev) : n;
 }
+// A segment's workspace: digit totals [pass][256] at the front (the look-back layout's histogram
+// area), then the per-pass count rows [pass][block][256].
+constexpr size_t RTS_ROWS_OFF = (HIST_COPIES * HIST_WORDS * 4 + 64 + 255) / 256 * 256;
+__device__ __forceinline__ size_t rts_blocks(size_t n, int it) { return (n + 256 * (size_t)it - 1) / (256 * (size_t)it); }
+__device__ __forceinline__ uint32_t* rts_rows(const SortSeg& g, int pass, size_t nbi) {
+    return reinterpret_cast<uint32_t*>(static_cast<char*>(g.temp) + RTS_ROWS_OFF) + (size_t)pass * nbi * 256;
+}
+__device__ __forceinline__ uint32_t* rts_totals(const SortSeg& g, int pass) {
+    return static_cast<uint32_t*>(g.temp) + pass * 256;
+}
+
+// Every kernel of a pass serves all segments of a batch: blockIdx.y is the segment, blocks past
+// a segment's own count return at once (the grid is sized for the largest segment).
 template <int IT>
-__global__ void __launch_bounds__(256) k_rts_count(const uint32_t* __restrict__ keys, size_t n,
-                                                   const uint32_t* __restrict__ n_dev, int drop, int shift, int nbits,
-                                                   uint32_t* __restrict__ counts) {
+__global__ void __launch_bounds__(256) k_rts_count(const SortBatch b, int pass, int in_b, int shift, int nbits) {
     __shared__ uint32_t s_h[4][256];
+    const SortSeg& sg = b.s[blockIdx.y];
+    const size_t nbi = rts_blocks(sg.n, IT);
+    if (blockIdx.x >= nbi) return;                                   // block-uniform
+    const uint32_t* __restrict__ keys = in_b ? sg.keys_b : sg.keys_a;
+    const int drop = sg.kept && pass == 0;                         // first pass drops, later passes read
+    const size_t n = rts_n(sg.n, sg.kept && pass > 0 ? sg.kept : nullptr);
+    uint32_t* __restrict__ counts = rts_rows(sg, pass, nbi);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
 #pragma unroll
     for (int w = 0; w < 4; ++w) s_h[w][tid] = 0;
-    n = rts_n(n, n_dev);
     __syncthreads();
     const uint32_t mask = (1u << nbits) - 1u;
     const uint64_t lt = lanemask_lt();
@@ -427,50 +481,61 @@ __global__ void __launch_bounds__(256) k_rts_count(const uint32_t* __restrict__ 
     counts[(size_t)blockIdx.x * 256 + tid] = s_h[0][tid] + s_h[1][tid] + s_h[2][tid] + s_h[3][tid];
 }
 
-// block d: exclusive scan of counts[b][d] over the blocks b, in place; totals[d] = digit d's count
-__global__ void __launch_bounds__(256) k_rts_scan(uint32_t* __restrict__ counts, int nb, uint32_t* __restrict__ totals) {
+// One block per (digit, segment): the digit's count row over the segment's blocks becomes each
+// block's offset within the digit; the digit total goes to the segment's totals.
+__global__ void __launch_bounds__(256) k_rts_scan(const SortBatch b, int pass, int it) {
     __shared__ uint32_t s_wave[4];
+    const SortSeg& sg = b.s[blockIdx.y];
+    const int nb = (int)rts_blocks(sg.n, it);
+    uint32_t* __restrict__ counts = rts_rows(sg, pass, (size_t)nb);
     const int d = blockIdx.x, tid = threadIdx.x;
     uint32_t carry = 0;
     for (int b0 = 0; b0 < nb; b0 += SCAN_TILE) {
         uint32_t v[SCAN_ITEMS];
 #pragma unroll
         for (int i = 0; i < SCAN_ITEMS; ++i) {
-            const int b = b0 + tid * SCAN_ITEMS + i;
-            v[i] = b < nb ? counts[(size_t)b * 256 + d] : 0u;
+            const int bb = b0 + tid * SCAN_ITEMS + i;
+            v[i] = bb < nb ? counts[(size_t)bb * 256 + d] : 0u;
         }
         uint32_t total;
         block_exclusive_scan8(v, s_wave, total);
 #pragma unroll
         for (int i = 0; i < SCAN_ITEMS; ++i) {
-            const int b = b0 + tid * SCAN_ITEMS + i;
-            if (b < nb) counts[(size_t)b * 256 + d] = v[i] + carry;
+            const int bb = b0 + tid * SCAN_ITEMS + i;
+            if (bb < nb) counts[(size_t)bb * 256 + d] = v[i] + carry;
         }
         carry += total;
         __syncthreads();   // s_wave reused by the next chunk
     }
-    if (tid == 0) totals[d] = carry;
+    if (tid == 0) rts_totals(sg, pass)[d] = carry;
 }
 
 template <int IT>
-__global__ void __launch_bounds__(256) k_rts_scatter(const uint32_t* __restrict__ keys_in,
-                                                     const uint32_t* __restrict__ vals_in,
-                                                     uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
-                                                     size_t n, const uint32_t* __restrict__ n_dev, int drop,
-                                                     uint32_t* __restrict__ kept_out, int shift, int nbits,
-                                                     const uint32_t* __restrict__ totals,
-                                                     const uint32_t* __restrict__ offs, SortGather gather) {
+__global__ void __launch_bounds__(256) k_rts_scatter(const SortBatch b, int pass, int in_b, int shift, int nbits,
+                                                     int last) {
     __shared__ uint32_t s_key[(256 * IT)];
     __shared__ uint32_t s_val[(256 * IT)];
     __shared__ uint32_t s_wcnt[4][256];
     __shared__ uint32_t s_gbase[256];
     __shared__ uint32_t s_lbase[256];
     __shared__ uint32_t s_wave[4];
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const SortSeg& sg = b.s[blockIdx.y];
+    const size_t nbi = rts_blocks(sg.n, IT);
     const uint32_t bid = blockIdx.x;
+    if (bid >= nbi) return;                                          // block-uniform
+    const uint32_t* __restrict__ keys_in = in_b ? sg.keys_b : sg.keys_a;
+    const uint32_t* __restrict__ vals_in = in_b ? sg.vals_b : sg.vals_a;
+    uint32_t* __restrict__ keys_out = in_b ? sg.keys_a : sg.keys_b;
+    uint32_t* __restrict__ vals_out = in_b ? sg.vals_a : sg.vals_b;
+    const int drop = sg.kept && pass == 0;
+    uint32_t* kept_out = drop ? sg.kept : nullptr;
+    const uint32_t* __restrict__ totals = rts_totals(sg, pass);
+    const uint32_t* __restrict__ offs = rts_rows(sg, pass, nbi);
+    const SortGather gather = last ? sg.gather : SortGather{nullptr, nullptr, nullptr};
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
 #pragma unroll
     for (int w = 0; w < 4; ++w) s_wcnt[w][tid] = 0;
-    n = rts_n(n, n_dev);
+    const size_t n = rts_n(sg.n, sg.kept && pass > 0 ? sg.kept : nullptr);
     __syncthreads();
     const uint32_t mask = (1u << nbits) - 1u;
     const uint64_t lt = lanemask_lt();
@@ -558,10 +623,50 @@ size_t radix_temp_zero_bytes(size_t n, int begin_bit, int end_bit) {
     return align_up(HIST_COPIES * HIST_WORDS * 4 + 64, 256) + (size_t)npass * os_blocks(n) * 256 * 4;
 }
 
+bool radix_sort_batch(const SortSeg* segs, int nseg, int begin_bit, int end_bit, hipStream_t st) {
+    SortBatch bt{};
+    int ns = 0;
+    size_t nmax = 0;
+    for (int i = 0; i < nseg; ++i)
+        if (segs[i].n > 0) { bt.s[ns++] = segs[i]; nmax = std::max(nmax, segs[i].n); }
+    if (ns == 0 || end_bit <= begin_bit) return false;
+    bool in_b = false;
+    // the bits spread evenly over the passes (13 bits: 7 + 6, not 8 + 5): fewer digits in a pass
+    // mean longer runs per digit in its scatter, i.e. fuller write segments
+    const int npass = (end_bit - begin_bit + 7) / 8;
+    // keys per thread: 8 (2M keys: more, shorter blocks), 12 above 4M keys (the 6M-instance
+    // tile sort: longer digit runs per block); swept 8 / 12 / 16 on both sorts
+    const int items = nmax > ((size_t)4 << 20) ? 12 : OS_ITEMS;
+    const unsigned nbi = (unsigned)((nmax + 256 * items - 1) / (256 * items));   // <= os_blocks: rows fit
+    for (int shift = begin_bit, nbits = 0, p = 0; shift < end_bit; shift += nbits, ++p) {
+        nbits = (end_bit - begin_bit) / npass + (p < (end_bit - begin_bit) % npass ? 1 : 0);
+        const int last = shift + nbits >= end_bit;
+        if (items == 12)
+            hipLaunchKernelGGL(k_rts_count<12>, dim3(nbi, ns), dim3(256), 0, st, bt, p, (int)in_b, shift, nbits);
+        else
+            hipLaunchKernelGGL(k_rts_count<OS_ITEMS>, dim3(nbi, ns), dim3(256), 0, st, bt, p, (int)in_b, shift, nbits);
+        hipLaunchKernelGGL(k_rts_scan, dim3(256, ns), dim3(256), 0, st, bt, p, items);
+        if (items == 12)
+            hipLaunchKernelGGL(k_rts_scatter<12>, dim3(nbi, ns), dim3(256), 0, st, bt, p, (int)in_b, shift, nbits, last);
+        else
+            hipLaunchKernelGGL(k_rts_scatter<OS_ITEMS>, dim3(nbi, ns), dim3(256), 0, st, bt, p, (int)in_b, shift, nbits,
+                               last);
+        in_b = !in_b;
+    }
+    return in_b;
+}
+
 bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b, size_t n,
                       int begin_bit, int end_bit, void* temp, uint32_t* err, hipStream_t st, bool temp_zeroed,
                       uint32_t* kept, const SortGather* gather) {
     if (n == 0 || end_bit <= begin_bit) return false;
+#if !LSR_SORT_LOOKBACK
+    // reduce-then-scan: no up-front histogram (each pass's scan kernel yields the digit totals)
+    // and no timeouts (err unused)
+    (void)err; (void)temp_zeroed;
+    SortSeg sg{keys_a, vals_a, keys_b, vals_b, temp, kept, gather ? *gather : SortGather{nullptr, nullptr, nullptr}, n};
+    return radix_sort_batch(&sg, 1, begin_bit, end_bit, st);
+#else
     const size_t nb = os_blocks(n);
     uint32_t* hist = reinterpret_cast<uint32_t*>(temp);
     uint32_t* tickets = hist + HIST_COPIES * HIST_WORDS;
@@ -571,51 +676,10 @@ bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint
     const size_t zb = radix_temp_zero_bytes(n, begin_bit, end_bit);
     if (!temp_zeroed && zb) (void)hipMemsetAsync(temp, 0, zb, st);
     bool in_b = false;
-#if !LSR_SORT_LOOKBACK
-    // no up-front histogram: each pass's scan kernel yields the digit totals (hist[pass] holds them)
-    (void)err; (void)own_err;
-    int p_ = 0;
-    // the bits spread evenly over the passes (13 bits: 7 + 6, not 8 + 5): fewer digits in a pass
-    // mean longer runs per digit in its scatter, i.e. fuller write segments
-    const int npass_ = (end_bit - begin_bit + 7) / 8;
-    // keys per thread: 8 (2M keys: more, shorter blocks), 12 above 4M keys (the 6M-instance
-    // tile sort: longer digit runs per block); swept 8 / 12 / 16 on both sorts
-    const int items = n > ((size_t)4 << 20) ? 12 : OS_ITEMS;
-    const size_t nbi = (n + 256 * items - 1) / (256 * items);   // <= nb: the count rows fit
-    for (int shift = begin_bit, nbits = 0; shift < end_bit; shift += nbits, ++p_) {
-        nbits = (end_bit - begin_bit) / npass_ + (p_ < (end_bit - begin_bit) % npass_ ? 1 : 0);
-        const uint32_t* kin = in_b ? keys_b : keys_a;
-        const uint32_t* vin = in_b ? vals_b : vals_a;
-        uint32_t* kout = in_b ? keys_a : keys_b;
-        uint32_t* vout = in_b ? vals_a : vals_b;
-        uint32_t* cnt = status + (size_t)p_ * nbi * 256;
-        const int drop = kept && p_ == 0;                       // first pass drops, later passes read
-        const uint32_t* n_dev = kept && p_ > 0 ? kept : nullptr;   // the kept count
-        if (items == 12)
-            hipLaunchKernelGGL(k_rts_count<12>, dim3((unsigned)nbi), dim3(256), 0, st, kin, n, n_dev, drop, shift, nbits, cnt);
-        else
-            hipLaunchKernelGGL(k_rts_count<OS_ITEMS>, dim3((unsigned)nbi), dim3(256), 0, st, kin, n, n_dev, drop, shift, nbits,
-                               cnt);
-        hipLaunchKernelGGL(k_rts_scan, dim3(256), dim3(256), 0, st, cnt, (int)nbi, hist + p_ * 256);
-        const bool last = shift + nbits >= end_bit;
-        const SortGather g = last && gather ? *gather : SortGather{nullptr, nullptr, nullptr};
-        if (items == 12)
-            hipLaunchKernelGGL(k_rts_scatter<12>, dim3((unsigned)nbi), dim3(256), 0, st, kin, vin, kout, vout, n, n_dev,
-                               drop, drop ? kept : (uint32_t*)nullptr, shift, nbits,
-                               (const uint32_t*)(hist + p_ * 256), (const uint32_t*)cnt, g);
-        else
-            hipLaunchKernelGGL(k_rts_scatter<OS_ITEMS>, dim3((unsigned)nbi), dim3(256), 0, st, kin, vin, kout, vout, n,
-                               n_dev, drop, drop ? kept : (uint32_t*)nullptr, shift, nbits,
-                               (const uint32_t*)(hist + p_ * 256), (const uint32_t*)cnt, g);
-        in_b = !in_b;
-    }
-    return in_b;
-#else
     (void)gather;   // not fused here: the caller gathers (radix_sort_fuses_gather() is false)
     if (kept) (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(kept), (int)n, 1, st);   // no dropping here
     const unsigned hb = (unsigned)min((size_t)OS_HIST_BLOCKS, (n + 64 * HIST_ITEMS * 4 - 1) / (64 * HIST_ITEMS * 4));
     hipLaunchKernelGGL(k_radix_hist, dim3(hb), dim3(256), 0, st, (const uint32_t*)keys_a, n, begin_bit, end_bit, hist);
-#endif
     int p = 0;
     for (int shift = begin_bit; shift < end_bit; shift += 8, ++p) {
         const int nbits = (end_bit - shift) < 8 ? (end_bit - shift) : 8;
@@ -629,6 +693,7 @@ bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint
         in_b = !in_b;
     }
     return in_b;
+#endif
 }
 
 }  // namespace lsr

@@ -156,24 +156,15 @@ def _dump_forward(raster_settings, inputs):
         print("\nAn error occured in forward. Writing snapshot_fw.dump for debugging.")
 
 
-def preprocess_native(raster_settings, means3D, opacities, shs=None, colors_precomp=None, language_feature=None,
-                      scales=None, rotations=None, cov3D_precomp=None, stream=None, binning=False,
-                      defer_count=False):
-    """Forward phase 1 through liblsr.so (lsr_forward_preprocess) on `stream` (a torch stream,
-    default: the current one).  Synchronises that stream once to read num_rendered (as upstream).
-    binning=True also runs the tile binning there (lsr_forward_binning), so that render_native
-    only composites.  Workspaces are allocated on `stream`; render_native may run on another
-    stream.
+def _check_device(t):
+    if t.device.type != "cuda":
+        raise RuntimeError("the rasterizer runs on the GPU only (no CPU fallback); got tensors on " + str(t.device))
+    return t.device
 
-    defer_count=True (lsr_forward_preprocess_async) does not synchronise: the count lands in pinned
-    host memory and PendingForward.resolve(binning) reads it later (render_native resolves too),
-    so a caller can enqueue this view's preprocess ahead of another view's work on the same stream."""
-    device = means3D.device
-    if device.type != "cuda":
-        raise RuntimeError("the rasterizer runs on the GPU only (no CPU fallback); got tensors on " + str(device))
-    L = _lib.load()
-    stream = stream or torch.cuda.current_stream(device)
-    st = _NativeSettings(raster_settings, device)
+
+def _fwd_inputs(means3D, opacities, shs, colors_precomp, language_feature, scales, rotations, cov3D_precomp):
+    """fp32 contiguous device inputs and their lsr_fwd_in; returns (fin, inputs, P)."""
+    device = _check_device(means3D)
     P = means3D.shape[0]
     means3D = _f32(means3D, device)
     opacities = _f32(opacities, device)
@@ -194,9 +185,30 @@ def preprocess_native(raster_settings, means3D, opacities, shs=None, colors_prec
     fin.means3D, fin.shs, fin.colors_precomp = means3D.data_ptr(), _ptr(shs), _ptr(colors_precomp)
     fin.language_feature, fin.opacities = _ptr(language_feature), opacities.data_ptr()
     fin.scales, fin.rotations, fin.cov3D_precomp = _ptr(scales), _ptr(rotations), _ptr(cov3D_precomp)
-    H, W = int(raster_settings.image_height), int(raster_settings.image_width)
     inputs = dict(means3D=means3D, opacities=opacities, shs=shs, colors_precomp=colors_precomp,
                   language_feature=language_feature, scales=scales, rotations=rotations, cov3D_precomp=cov3D_precomp)
+    return fin, inputs, P
+
+
+def preprocess_native(raster_settings, means3D, opacities, shs=None, colors_precomp=None, language_feature=None,
+                      scales=None, rotations=None, cov3D_precomp=None, stream=None, binning=False,
+                      defer_count=False):
+    """Forward phase 1 through liblsr.so (lsr_forward_preprocess) on `stream` (a torch stream,
+    default: the current one).  Synchronises that stream once to read num_rendered (as upstream).
+    binning=True also runs the tile binning there (lsr_forward_binning), so that render_native
+    only composites.  Workspaces are allocated on `stream`; render_native may run on another
+    stream.
+
+    defer_count=True (lsr_forward_preprocess_async) does not synchronise: the count lands in pinned
+    host memory and PendingForward.resolve(binning) reads it later (render_native resolves too),
+    so a caller can enqueue this view's preprocess ahead of another view's work on the same stream."""
+    device = _check_device(means3D)
+    L = _lib.load()
+    stream = stream or torch.cuda.current_stream(device)
+    st = _NativeSettings(raster_settings, device)
+    fin, inputs, P = _fwd_inputs(means3D, opacities, shs, colors_precomp, language_feature, scales, rotations,
+                                 cov3D_precomp)
+    H, W = int(raster_settings.image_height), int(raster_settings.image_width)
     with torch.cuda.stream(stream):
         radii = torch.empty(P, dtype=torch.int32, device=device)
         geom = torch.empty(int(L.lsr_geom_bytes(P)), dtype=torch.uint8, device=device)
@@ -252,6 +264,82 @@ def _run_binning(pf, stream):
         raise
     pf.ready = torch.cuda.Event()
     pf.ready.record(stream)               # render_native's stream waits for the binning
+
+
+def preprocess_views_native(raster_settings_list, means3D, opacities, shs=None, colors_precomp=None,
+                            language_feature=None, scales=None, rotations=None, cov3D_precomp=None, stream=None):
+    """Forward phase 1 of several views of the same Gaussians as one batch
+    (lsr_forward_preprocess_views_async: one preprocess launch per 8 views reads each Gaussian once,
+    the views' depth sorts and instance scans share their launches) on `stream`.  No host
+    synchronisation: returns one deferred-count PendingForward per view; binning_views_native
+    resolves them all with one wait.  Same results as preprocess_native per view."""
+    device = _check_device(means3D)
+    L = _lib.load()
+    stream = stream or torch.cuda.current_stream(device)
+    fin, inputs, P = _fwd_inputs(means3D, opacities, shs, colors_precomp, language_feature, scales, rotations,
+                                 cov3D_precomp)
+    n = len(raster_settings_list)
+    sts = [_NativeSettings(rs, device) for rs in raster_settings_list]
+    with torch.cuda.stream(stream):
+        radii = [torch.empty(P, dtype=torch.int32, device=device) for _ in range(n)]
+        geoms = [torch.empty(int(L.lsr_geom_bytes(P)), dtype=torch.uint8, device=device) for _ in range(n)]
+    fouts = [_lib.FwdOut() for _ in range(n)]
+    for fo, r in zip(fouts, radii):
+        fo.radii = r.data_ptr()
+    counts = torch.zeros(n, 2, dtype=torch.int32, pin_memory=True)
+    s_arr = (ctypes.POINTER(_lib.Settings) * n)(*[ctypes.pointer(x.c) for x in sts])
+    o_arr = (ctypes.POINTER(_lib.FwdOut) * n)(*[ctypes.pointer(fo) for fo in fouts])
+    g_arr = (ctypes.c_void_p * n)(*[g.data_ptr() for g in geoms])
+    try:
+        _lib.check(L.lsr_forward_preprocess_views_async(n, s_arr, ctypes.byref(fin), o_arr, g_arr,
+                                                        ctypes.c_void_p(counts.data_ptr()),
+                                                        ctypes.c_void_p(stream.cuda_stream)),
+                   "lsr_forward_preprocess_views_async")
+    except RuntimeError:
+        _dump_forward(raster_settings_list[0], inputs)
+        raise
+    ev = torch.cuda.Event()
+    ev.record(stream)
+    out = []
+    for v, rs in enumerate(raster_settings_list):
+        H, W = int(rs.image_height), int(rs.image_width)
+        pf = PendingForward(rs, sts[v], fin, inputs, geoms[v], radii[v], None, device, H, W)
+        pf.count_host, pf.stream, pf.counted = counts[v], stream, ev
+        out.append(pf)
+    return out
+
+
+def binning_views_native(pendings, stream=None):
+    """Resolve the deferred counts of preprocess_views_native's views (one host wait) and run their
+    tile binning as one batch (lsr_forward_binning_views) on `stream` (default: theirs), so that
+    render_native only composites each view."""
+    if not pendings:
+        return
+    L = _lib.load()
+    stream = stream or pendings[0].stream
+    for pf in pendings:
+        pf.resolve()
+    n = len(pendings)
+    device = pendings[0].device
+    with torch.cuda.stream(stream):
+        for pf in pendings:
+            pf.binning = torch.empty(int(L.lsr_binning_bytes(pf.num_rendered)), dtype=torch.uint8, device=device)
+            pf.img = torch.empty(int(L.lsr_img_bytes(pf.W, pf.H)), dtype=torch.uint8, device=device)
+    s_arr = (ctypes.POINTER(_lib.Settings) * n)(*[ctypes.pointer(pf.settings.c) for pf in pendings])
+    g_arr = (ctypes.c_void_p * n)(*[pf.geom.data_ptr() for pf in pendings])
+    b_arr = (ctypes.c_void_p * n)(*[pf.binning.data_ptr() for pf in pendings])
+    i_arr = (ctypes.c_void_p * n)(*[pf.img.data_ptr() for pf in pendings])
+    k_arr = (ctypes.c_int64 * n)(*[pf.num_rendered for pf in pendings])
+    try:
+        _lib.check(L.lsr_forward_binning_views(n, s_arr, ctypes.byref(pendings[0].fin), g_arr, b_arr, i_arr, k_arr,
+                                               ctypes.c_void_p(stream.cuda_stream)), "lsr_forward_binning_views")
+    except RuntimeError:
+        _dump_forward(pendings[0].raster_settings, pendings[0].inputs)
+        raise
+    ev = torch.cuda.Event()
+    ev.record(stream)
+    for pf in pendings:
+        pf.ready = ev
 
 
 def render_native(pending: PendingForward):

@@ -110,6 +110,14 @@ SIGNATURES = {
     "lsr_forward_preprocess_async": (ctypes.c_int, [ctypes.POINTER(Settings), ctypes.POINTER(FwdIn),
                                                     ctypes.POINTER(FwdOut), ctypes.c_void_p, ctypes.c_void_p,
                                                     ctypes.c_void_p]),
+    "lsr_forward_preprocess_views_async": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(ctypes.POINTER(Settings)),
+                                                          ctypes.POINTER(FwdIn), ctypes.POINTER(ctypes.POINTER(FwdOut)),
+                                                          ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p,
+                                                          ctypes.c_void_p]),
+    "lsr_forward_binning_views": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(ctypes.POINTER(Settings)),
+                                                 ctypes.POINTER(FwdIn), ctypes.POINTER(ctypes.c_void_p),
+                                                 ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
+                                                 ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
     "lsr_forward_render": (ctypes.c_int, [ctypes.POINTER(Settings), ctypes.POINTER(FwdIn), ctypes.POINTER(FwdOut),
                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                           ctypes.c_void_p]),
@@ -152,6 +160,14 @@ SIGNATURES = {
                                         ctypes.c_int32]),
 }
 
+# entry points newer builds add; callers check has() (variant libraries of older revisions lack them)
+OPTIONAL = {"lsr_forward_preprocess_views_async", "lsr_forward_binning_views"}
+
+
+def has(name):
+    return hasattr(load(), name)
+
+
 PHASES = ["preprocess", "depth_sort", "instance_scan", "emit", "tile_sort", "tile_ranges", "render_fwd",
           "render_bwd", "preprocess_bwd", "preprocess_bwd_views"]
 
@@ -184,6 +200,8 @@ def load():
                               "(or __graft_entry__.build()).  There is no CPU fallback.")
         lib = ctypes.CDLL(path)
         for name, (res, args) in SIGNATURES.items():
+            if name in OPTIONAL and not hasattr(lib, name):   # an older build (A/B runs): has() says so
+                continue
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

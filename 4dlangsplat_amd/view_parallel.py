@@ -177,6 +177,12 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
     the sequential order (preprocess and binning only read the Gaussians and write their own
     workspaces).
 
+    overlap="batched" runs the forward phase 1 and the binning of ALL of the step's views (from
+    the first one rendered) as one batch when the step starts (lsr_forward_preprocess_views_async,
+    lsr_forward_binning_views: a Gaussian's inputs read once per 8 views, one set of sort launches
+    for all views, one host wait for their counts); each view then only composites.  Needs the
+    step's views (begin_step, as ViewParallelStep.run calls it); without them, views batch alone.
+
     overlap="lookahead" keeps ONE stream: view v+1's preprocess is enqueued ahead of view v's
     compositing with its instance count copied to pinned memory (lsr_forward_preprocess_async);
     the host waits for that count only (an event), while view v's compositing is still queued,
@@ -185,7 +191,9 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
     import diff_gaussian_rasterization as dgr
 
     lookahead = overlap == "lookahead"
-    side = torch.cuda.Stream(device=scene.means3D.device) if (overlap and not lookahead) else None
+    batch_fwd = overlap == "batched"
+    side = (torch.cuda.Stream(device=scene.means3D.device) if (overlap and not lookahead and not batch_fwd)
+            else None)
     pending = {}
     params_ready = torch.cuda.Event() if side is not None else None
     step_views = [None]                   # this rank's views of the current step (begin_step)
@@ -205,7 +213,20 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
     batched = batch_backward and not deterministic
     held = []                             # (state, dL_dcolor, dL_dlang, dL_ddepth) awaiting flush
 
+    def batch_preprocess(v):
+        """The step's views from v on, as one batch: preprocess + depth sorts + instance scans, one
+        host wait for their counts, then their binning (lsr_forward_*_views)."""
+        views = [w for w in step_views[0] if w >= v] if step_views[0] is not None else [v]
+        views = [w for w in views if has_view(w)] or [v]
+        pfs = dgr.preprocess_views_native([settings[w] for w in views], scene.means3D, scene.opacities,
+                                          shs=scene.shs, language_feature=scene.lang, scales=scene.scales,
+                                          rotations=scene.rotations)
+        dgr.binning_views_native(pfs)
+        pending.update(zip(views, pfs))
+
     def render_view(v: int, bucket: GradBucket):
+        if batch_fwd and v not in pending:
+            batch_preprocess(v)
         pf = pending.pop(v, None)
         if pf is None:                    # first view of a step: the Gaussians are final here
             pf = preprocess(v)

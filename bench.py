@@ -108,8 +108,9 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=3, help="headline frames timed on the CPU oracle")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-overlap", action="store_true", help="diagnostic: no side stream (uncontended phase times)")
-    ap.add_argument("--pipeline", choices=("lookahead", "side"), default="lookahead",
-                    help="view pipelining: next view's preprocess queued ahead on one stream with a deferred count "
+    ap.add_argument("--pipeline", choices=("batched", "lookahead", "side"), default=None,
+                    help="view pipelining: the step's forward phase 1 + binning of all views as one batch (batched, "
+                         "default), next view's preprocess queued ahead on one stream with a deferred count "
                          "(lookahead), or run on a side stream (side)")
     args = ap.parse_args()
 
@@ -126,6 +127,8 @@ def main():
     import diff_gaussian_rasterization as dgr
     from diff_gaussian_rasterization import _lib
     import synthetic
+    if args.pipeline is None:   # variant libraries of older revisions (A/B runs) lack the batched entry points
+        args.pipeline = "batched" if _lib.has("lsr_forward_preprocess_views_async") else "lookahead"
 
     P, C, W, H, V = args.gaussians, args.channels, args.width, args.height, args.views
     tanfovx = 0.6
@@ -145,8 +148,8 @@ def main():
     gcol = (torch.randn(3, H, W, generator=g) * 1e-3).to(dev)
     glang = (torch.randn(C, H, W, generator=g) * 1e-3).to(dev)
     render = native_view_renderer(scene, settings, lambda v, color, lang, depth: (gcol, glang, None),
-                                  overlap=False if args.no_overlap else ("lookahead" if args.pipeline == "lookahead"
-                                                                         else True))
+                                  overlap=False if args.no_overlap else (True if args.pipeline == "side"
+                                                                         else args.pipeline))
     Ks = []
 
     def render_view(v, b):
@@ -156,6 +159,7 @@ def main():
 
     if hasattr(render, "flush"):                           # batched backward of the step's views
         render_view.flush = render.flush
+    render_view.begin_step, render_view.end_step = render.begin_step, render.end_step   # the step's views
 
     def step():
         dp.run(render_view)                                # fwd+bwd per view, SUM all-reduce (RCCL) if world > 1
@@ -219,9 +223,10 @@ def main():
         phases = {}
         if prof:
             for k, (ms, n) in prof_all.items():   # the untimed all-phase step
-                if n:
-                    phases[k] = dict(mean_ms=ms / n, launches=n, gbs=phase_bytes(k, P, Pvis, Kmean, W * H, ntiles, C, M, **pb)
-                                     / (ms / n * 1e-3) / 1e9)
+                if n:   # per view (a batched launch serves several); preprocess_bwd_views: per launch
+                    per = ms / n if k == "preprocess_bwd_views" else ms / len(dp.views)
+                    phases[k] = dict(mean_ms=per, launches=n, gbs=phase_bytes(k, P, Pvis, Kmean, W * H, ntiles, C, M, **pb)
+                                     / (per * 1e-3) / 1e9)
             ms, n = prof[dom]                      # live, over the timed region
             byts = phase_bytes(dom, P, Pvis, Kmean, W * H, ntiles, C, M, **pb)
             ach = byts / (ms / n * 1e-3) / 1e9

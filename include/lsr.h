@@ -133,6 +133,19 @@ int lsr_forward_preprocess(const lsr_settings *s, const lsr_fwd_in *in, lsr_fwd_
 int lsr_forward_preprocess_async(const lsr_settings *s, const lsr_fwd_in *in, lsr_fwd_out *out, void *geom,
                                  uint32_t *host_count, lsr_stream_t stream);
 
+/* lsr_forward_preprocess_async for n_views >= 1 cameras of the same Gaussians `in` (one training
+ * batch), batched: ONE preprocess launch per 8 views reads each Gaussian's inputs (and builds its
+ * 3D covariance) once for all of them, and the depth sorts and instance scans of those views run
+ * as one set of launches (every kernel serves all the views).  s[v], out[v], geom[v] are view v's
+ * (workspaces as for lsr_forward_preprocess_async); `host_counts` (page-locked, 2 * n_views words)
+ * receives [2v] num_rendered and [2v + 1] the depth sort error word of view v, valid once the
+ * stream has passed this point.  The views must share the image size, sh_degree and
+ * scale_modifier.  Results equal lsr_forward_preprocess_async per view.  The pointer arrays are
+ * HOST arrays. */
+int lsr_forward_preprocess_views_async(int32_t n_views, const lsr_settings *const *s, const lsr_fwd_in *in,
+                                       lsr_fwd_out *const *out, void *const *geom, uint32_t *host_counts,
+                                       lsr_stream_t stream);
+
 /* Forward, phase 2: tile binning and compositing of RGB + C language channels + depth.
  * `geom` is the buffer phase 1 filled; `binning` holds >= lsr_binning_bytes(num_rendered) bytes. */
 int lsr_forward_render(const lsr_settings *s, const lsr_fwd_in *in, lsr_fwd_out *out, void *geom,
@@ -147,6 +160,13 @@ int lsr_forward_binning(const lsr_settings *s, const lsr_fwd_in *in, void *geom,
                         int64_t num_rendered, lsr_stream_t stream);
 int lsr_forward_composite(const lsr_settings *s, const lsr_fwd_in *in, lsr_fwd_out *out, const void *geom,
                           const void *binning, void *img, int64_t num_rendered, lsr_stream_t stream);
+/* lsr_forward_binning of n_views >= 1 views of the same Gaussians (phase 1 done, by either entry
+ * point): the emissions, tile sorts and tile ranges of all of them as one set of launches per 8
+ * views.  geom[v], binning[v], img[v], num_rendered[v] are view v's; the views must share the
+ * image size.  Results equal lsr_forward_binning per view.  HOST pointer arrays. */
+int lsr_forward_binning_views(int32_t n_views, const lsr_settings *const *s, const lsr_fwd_in *in,
+                              void *const *geom, void *const *binning, void *const *img,
+                              const int64_t *num_rendered, lsr_stream_t stream);
 
 /* Sort status of the forward whose phase 1 filled `geom` (P Gaussians): an asynchronous copy of two
  * words to `host_status` (valid once the stream has passed this point): [0] nonzero if the depth
