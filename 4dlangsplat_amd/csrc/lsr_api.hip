@@ -295,8 +295,7 @@ int lsr_forward_preprocess_async(const lsr_settings* s, const lsr_fwd_in* in, ls
     if (!out || (!out->radii && in->P > 0)) return fail(LSR_EINVAL, "radii output is required");
     if (!geom || !host_count) return fail(LSR_EINVAL, "geom workspace and host_count are required");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const int P = in->P, W = s->image_width, H = s->image_height;
-    const int gx = (W + LSR_TILE_X - 1) / LSR_TILE_X, gy = (H + LSR_TILE_Y - 1) / LSR_TILE_Y;
+    const int P = in->P;
     Geom g = carve_geom(geom, (size_t)(P > 0 ? P : 1), nullptr);
     if (P == 0) {
         host_count[0] = host_count[1] = 0;

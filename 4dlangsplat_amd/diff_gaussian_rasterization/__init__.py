@@ -546,15 +546,21 @@ class CompositeGrad:
 
 
 def backward_composite_native(state: RasterizerState, grad_color, grad_lang=None, grad_depth=None,
-                              dL_dlanguage=None) -> CompositeGrad:
+                              dL_dlanguage=None, defer_sort_check=False) -> CompositeGrad:
     """First half of backward_views_native for ONE view (lsr_backward_composite), on the current
     stream: the compositor backward; the language gradient is ADDED to dL_dlanguage [P,C] (the
-    caller zeroes it once per batch).  Finish a batch with backward_preprocess_views_native."""
+    caller zeroes it once per batch).  Finish a batch with backward_preprocess_views_native.
+
+    defer_sort_check=True leaves the forward's sort-status check to backward_preprocess_views_native
+    (which raises before the batch's gradients are complete): checking here would make the host wait
+    for the forward that was enqueued just before, and the device would idle until this call's
+    launches arrive."""
     L = _lib.load()
     if state.composited:
         raise RuntimeError("backward_composite_native already ran on this forward: its screen-space sums are "
                            "accumulated in the forward's workspace, so a second run would double them")
-    state.check_sorts()
+    if not defer_sort_check:
+        state.check_sorts()
     device = state.inputs["means3D"].device
     P, C = state.fin.P, state.fin.C
     H, W = state.settings.c.image_height, state.settings.c.image_width
@@ -589,6 +595,8 @@ def backward_preprocess_views_native(parts, out=None, accumulate=False, need=Non
     for p_ in parts[1:]:
         if p_.state.inputs["means3D"].data_ptr() != inp["means3D"].data_ptr():
             raise ValueError("all views must render the same Gaussians")
+    for p_ in parts:                      # deferred checks (backward_composite_native(defer_sort_check))
+        p_.state.check_sorts()
     device = inp["means3D"].device
     need = dict(need or {})
     need["language_feature"] = False

@@ -239,7 +239,8 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
         color, lang, radii, depth, st = dgr.render_native(pf)
         gc, gl, gd = grad_fn(v, color, lang, depth)
         if batched:                   # compositor backward now, preprocess backward at flush
-            held.append(dgr.backward_composite_native(st, gc, gl, gd, dL_dlanguage=bucket.views["language_feature"]))
+            held.append(dgr.backward_composite_native(st, gc, gl, gd, dL_dlanguage=bucket.views["language_feature"],
+                                                      defer_sort_check=True))   # checked at flush
         else:
             dgr.backward_native(st, gc, gl, gd, out=bucket.views, accumulate=True, need=bucket.need(),
                                 deterministic=deterministic)

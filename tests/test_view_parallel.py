@@ -167,11 +167,12 @@ class _FakePending:
         return self
 
 
-def _lookahead_worker(rank, world, port, outdir):
-    """native_view_renderer's one-stream lookahead with LIST settings (every view of the batch
-    visible to every rank): each rank must preprocess exactly its own views, never the next rank's
-    first view, and leave nothing pending after the step.  The native calls are replaced by
-    recorders (no GPU here); the control flow is the product's."""
+def _lookahead_worker(rank, world, port, outdir, mode="lookahead"):
+    """native_view_renderer's one-stream lookahead (or the batched forward) with LIST settings
+    (every view of the batch visible to every rank): each rank must preprocess exactly its own
+    views, never the next rank's first view, and leave nothing pending after the step; batched:
+    in ONE preprocess + binning batch per step.  The native calls are replaced by recorders (no
+    GPU here); the control flow is the product's."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -189,9 +190,16 @@ def _lookahead_worker(rank, world, port, outdir):
             z = torch.zeros(3, 4, 4)
             return z, torch.zeros(2, 4, 4), torch.full((Pn,), pf.v + 1, dtype=torch.int32), z[:1], pf
 
-        def backward_composite_native(st, gc, gl, gd, dL_dlanguage=None):
+        def backward_composite_native(st, gc, gl, gd, dL_dlanguage=None, defer_sort_check=False):
             log.append(("composite_bwd", st.v))
             return st
+
+        def preprocess_views_native(settings_list, *a, **k):
+            log.append(("preprocess_views", list(settings_list)))
+            return [_FakePending(v, log) for v in settings_list]
+
+        def binning_views_native(pfs):
+            log.append(("binning_views", [pf.v for pf in pfs]))
 
         def backward_preprocess_views_native(held, out=None, accumulate=False, need=None):
             log.append(("flush", [h.v for h in held]))
@@ -202,21 +210,27 @@ def _lookahead_worker(rank, world, port, outdir):
         dgr.preprocess_native, dgr.render_native = preprocess_native, render_native
         dgr.backward_composite_native = backward_composite_native
         dgr.backward_preprocess_views_native = backward_preprocess_views_native
+        dgr.preprocess_views_native, dgr.binning_views_native = preprocess_views_native, binning_views_native
 
         class S:
             means3D = opacities = shs = lang = scales = rotations = torch.zeros(Pn, 3)
 
         n_views = 5
         settings = list(range(n_views))          # "settings" of view v is just v here
-        render = native_view_renderer(S(), settings, lambda v, c, l, d: (c, l, d), overlap="lookahead")
+        render = native_view_renderer(S(), settings, lambda v, c, l, d: (c, l, d), overlap=mode)
         b = GradBucket(Pn, 1, 2, "cpu", densify_stats=True)
         step = ViewParallelStep(b, n_views)
         for _ in range(2):                       # two steps: nothing carried over
             step.run(render)
             assert not render.pending
         mine = list(step.views)
-        pre = [s for k, s in log if k == "preprocess"]
-        assert pre == mine * 2, (rank, pre, mine)
+        if mode == "batched":
+            assert [s for k, s in log if k == "preprocess_views"] == [mine] * 2, (rank, log)
+            assert [s for k, s in log if k == "binning_views"] == [mine] * 2, (rank, log)
+            assert not [s for k, s in log if k == "preprocess"]
+        else:
+            pre = [s for k, s in log if k == "preprocess"]
+            assert pre == mine * 2, (rank, pre, mine)
         assert [s for k, s in log if k == "render"] == mine * 2
         assert [s for k, s in log if k == "flush"] == [mine] * 2
         torch.save(dict(radii=b.radii.clone()), os.path.join(outdir, f"rank{rank}.pt"))
@@ -224,9 +238,10 @@ def _lookahead_worker(rank, world, port, outdir):
         dist.destroy_process_group()
 
 
-def test_two_rank_lookahead_stays_in_rank_slice():
+@pytest.mark.parametrize("mode", ["lookahead", "batched"])
+def test_two_rank_lookahead_stays_in_rank_slice(mode):
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_lookahead_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        mp.spawn(_lookahead_worker, args=(2, _free_port(), d, mode), nprocs=2, join=True)
         outs = [torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(2)]
     # radii MAX over all 5 views (the fake radius of view v is v + 1)
     assert torch.equal(outs[0]["radii"], torch.full((16,), 5, dtype=torch.int32))
