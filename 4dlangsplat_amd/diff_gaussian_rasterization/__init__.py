@@ -102,10 +102,15 @@ class RasterizerState:
         self.sort_status = sort_status    # (pinned int32 [2], event) or None
         self.composited = False           # backward_composite_native ran (it may run once)
 
-    def check_sorts(self):
+    def check_sorts(self, event=None):
+        """event: one recorded after this forward on its stream, for forwards rendered with
+        render_native(status_event=False) (ignored when the forward recorded its own)."""
         if self.sort_status is None:
             return self
         words, ev = self.sort_status
+        ev = ev or event
+        if ev is None:
+            raise RuntimeError("check_sorts: this forward recorded no status event; pass one recorded after it")
         ev.synchronize()
         self.sort_status = None
         bad = [name for name, w in zip(("depth sort", "tile sort"), words.tolist()) if w]
@@ -128,6 +133,7 @@ class PendingForward:
         self.geom, self.radii, self.num_rendered, self.device, self.H, self.W = geom, radii, K, device, H, W
         self.binning = self.img = None     # set when the binning already ran (preprocess_native(binning=True))
         self.ready = None                  # event recorded after that binning
+        self.ready_stream = None           # the stream `ready` was recorded on
         self.count_host = None             # deferred count (preprocess_native(defer_count=True)): pinned
         self.counted = None                # [K, error word], valid once `counted` (an event) has passed
         self.stream = None
@@ -264,6 +270,7 @@ def _run_binning(pf, stream):
         raise
     pf.ready = torch.cuda.Event()
     pf.ready.record(stream)               # render_native's stream waits for the binning
+    pf.ready_stream = stream
 
 
 def preprocess_views_native(raster_settings_list, means3D, opacities, shs=None, colors_precomp=None,
@@ -339,12 +346,16 @@ def binning_views_native(pendings, stream=None):
     ev = torch.cuda.Event()
     ev.record(stream)
     for pf in pendings:
-        pf.ready = ev
+        pf.ready, pf.ready_stream = ev, stream
 
 
-def render_native(pending: PendingForward):
+def render_native(pending: PendingForward, status_event=True):
     """Forward phase 2 (binning unless preprocess_native already did it, then compositing) on the
-    current stream.  Returns (color, language_feature, radii, depth, state)."""
+    current stream.  Returns (color, language_feature, radii, depth, state).
+
+    status_event=False records no event for the sort status words (an event record between two
+    launches idles the device ~15 us): the caller then checks them with check_sorts(event) on an
+    event recorded later on the same stream (backward_preprocess_views_native does)."""
     L = _lib.load()
     pending.resolve()
     device, H, W, C = pending.device, pending.H, pending.W, pending.fin.C
@@ -363,7 +374,8 @@ def render_native(pending: PendingForward):
     binned = pending.binning is not None
     if binned:
         binning, img = pending.binning, pending.img
-        stream.wait_event(pending.ready)
+        if pending.ready_stream != stream:   # same stream: already ordered (a wait idles the device)
+            stream.wait_event(pending.ready)
         binning.record_stream(stream)
         img.record_stream(stream)
     else:
@@ -378,12 +390,17 @@ def render_native(pending: PendingForward):
     except RuntimeError:
         _dump_forward(pending.raster_settings, pending.inputs)
         raise
-    ev = torch.cuda.Event()
-    ev.record(stream)
+    ev = None
+    if status_event:
+        ev = torch.cuda.Event()
+        ev.record(stream)
     state = RasterizerState(pending.settings, pending.inputs, pending.fin, pending.geom, binning, img, K, pending.radii,
                             sort_status=(status, ev))
     if pending.raster_settings.debug:
-        state.check_sorts()
+        if ev is None:
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        state.check_sorts(ev)
     return color, lang_out, pending.radii, depth, state
 
 
@@ -552,7 +569,7 @@ def backward_composite_native(state: RasterizerState, grad_color, grad_lang=None
     caller zeroes it once per batch).  Finish a batch with backward_preprocess_views_native.
 
     defer_sort_check=True leaves the forward's sort-status check to backward_preprocess_views_native
-    (which raises before the batch's gradients are complete): checking here would make the host wait
+    (which raises before it returns the batch's gradients): checking here would make the host wait
     for the forward that was enqueued just before, and the device would idle until this call's
     launches arrive."""
     L = _lib.load()
@@ -595,9 +612,12 @@ def backward_preprocess_views_native(parts, out=None, accumulate=False, need=Non
     for p_ in parts[1:]:
         if p_.state.inputs["means3D"].data_ptr() != inp["means3D"].data_ptr():
             raise ValueError("all views must render the same Gaussians")
-    for p_ in parts:                      # deferred checks (backward_composite_native(defer_sort_check))
-        p_.state.check_sorts()
     device = inp["means3D"].device
+    # deferred sort checks (backward_composite_native(defer_sort_check)): one event before this
+    # launch covers every view's forward; the host waits on it only after the launch is enqueued,
+    # so the device runs this batch while the host checks (a failed check still raises here)
+    covered = torch.cuda.Event()
+    covered.record(torch.cuda.current_stream(device))
     need = dict(need or {})
     need["language_feature"] = False
     g = _grad_buffers(st0, out, accumulate, need)
@@ -609,6 +629,8 @@ def backward_preprocess_views_native(parts, out=None, accumulate=False, need=Non
                                                vp(*[p_.state.geom.data_ptr() for p_ in parts]),
                                                1 if accumulate else 0, _stream(device)),
                "lsr_backward_preprocess_views")
+    for p_ in parts:
+        p_.state.check_sorts(covered)
     return g
 
 

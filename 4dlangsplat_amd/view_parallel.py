@@ -236,7 +236,7 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
             pf.resolve(binning=True)      # count of view v (enqueued a view earlier), then its binning
             if has_view(v + 1):           # view v+1's preprocess ahead of view v's compositing
                 pending[v + 1] = preprocess(v + 1, defer=True)
-        color, lang, radii, depth, st = dgr.render_native(pf)
+        color, lang, radii, depth, st = dgr.render_native(pf, status_event=not batched)   # batched: checked at flush
         gc, gl, gd = grad_fn(v, color, lang, depth)
         if batched:                   # compositor backward now, preprocess backward at flush
             held.append(dgr.backward_composite_native(st, gc, gl, gd, dL_dlanguage=bucket.views["language_feature"],

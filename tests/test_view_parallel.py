@@ -185,7 +185,7 @@ def _lookahead_worker(rank, world, port, outdir, mode="lookahead"):
             log.append(("preprocess", settings))
             return _FakePending(settings, log)
 
-        def render_native(pf):
+        def render_native(pf, status_event=True):
             log.append(("render", pf.v))
             z = torch.zeros(3, 4, 4)
             return z, torch.zeros(2, 4, 4), torch.full((Pn,), pf.v + 1, dtype=torch.int32), z[:1], pf
