@@ -12,6 +12,9 @@
 
 namespace lsr {
 
+#ifndef LSR_SORT_SCAN_DIGIT
+#define LSR_SORT_SCAN_DIGIT 0   // 1: the per-digit count-row scan (k_rts_scan), for A/B
+#endif
 constexpr int SCAN_ITEMS = 8;
 constexpr int SCAN_TILE = 256 * SCAN_ITEMS;
 
@@ -510,6 +513,95 @@ __global__ void __launch_bounds__(256) k_rts_scan(const SortBatch b, int pass, i
     if (tid == 0) rts_totals(sg, pass)[d] = carry;
 }
 
+// The same scan, one block per (16-digit group, segment) instead of per digit: thread t owns
+// SCAN16_ROWS consecutive block rows of a chunk and reads each row's 16 counts as one 64-byte
+// piece (four 16-byte loads, all in flight at once), so the count table is read once in whole
+// pieces instead of one 4-byte word per (row, digit block) -- the per-digit kernel touched every
+// line of the table from 256 blocks (33 us per depth pass, 58 us per tile pass on 8 views).
+// Digit groups past 2^nbits (the tile sort's 7- and 6-bit passes) only zero their totals.
+constexpr int SCAN16_ROWS = 8;
+__global__ void __launch_bounds__(256) k_rts_scan16(const SortBatch b, int pass, int it, int nbits) {
+    __shared__ uint32_t s_part[4][16];
+    const SortSeg& sg = b.s[blockIdx.y];
+    const int d0 = 16 * (int)blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t* __restrict__ totals = rts_totals(sg, pass);
+    if (d0 >= (1 << nbits)) {                                        // block-uniform
+        if (tid < 16) totals[d0 + tid] = 0u;
+        return;
+    }
+    const int nb = (int)rts_blocks(sg.n, it);
+    uint32_t* __restrict__ counts = rts_rows(sg, pass, (size_t)nb);
+    uint32_t carry[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) carry[j] = 0u;
+    for (int c0 = 0; c0 < nb; c0 += 256 * SCAN16_ROWS) {
+        const int r0 = c0 + tid * SCAN16_ROWS;
+        uint4 v[SCAN16_ROWS][4];
+#pragma unroll
+        for (int r = 0; r < SCAN16_ROWS; ++r) {
+            const uint4* p = reinterpret_cast<const uint4*>(counts + (size_t)(r0 + r) * 256 + d0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[r][q] = r0 + r < nb ? p[q] : make_uint4(0u, 0u, 0u, 0u);
+        }
+        uint32_t sum[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            sum[4 * q] = 0u; sum[4 * q + 1] = 0u; sum[4 * q + 2] = 0u; sum[4 * q + 3] = 0u;
+#pragma unroll
+            for (int r = 0; r < SCAN16_ROWS; ++r) {
+                sum[4 * q] += v[r][q].x; sum[4 * q + 1] += v[r][q].y;
+                sum[4 * q + 2] += v[r][q].z; sum[4 * q + 3] += v[r][q].w;
+            }
+        }
+        // exclusive scan of the 16 per-thread sums over the block's threads (rows in order)
+        uint32_t off[16], tot[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            uint32_t inc = sum[j];
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t t = __shfl_up(inc, o);
+                if (lane >= o) inc += t;
+            }
+            off[j] = inc - sum[j];
+            if (lane == 63) s_part[wave][j] = inc;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            uint32_t before = 0u, all = 0u;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const uint32_t x = s_part[w][j];
+                before += w < wave ? x : 0u;
+                all += x;
+            }
+            off[j] += before + carry[j];
+            tot[j] = all;
+        }
+#pragma unroll
+        for (int r = 0; r < SCAN16_ROWS; ++r) {
+            if (r0 + r >= nb) break;
+            uint4* p = reinterpret_cast<uint4*>(counts + (size_t)(r0 + r) * 256 + d0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint4 x = v[r][q];
+                p[q] = make_uint4(off[4 * q], off[4 * q + 1], off[4 * q + 2], off[4 * q + 3]);
+                off[4 * q] += x.x; off[4 * q + 1] += x.y; off[4 * q + 2] += x.z; off[4 * q + 3] += x.w;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) carry[j] += tot[j];
+        __syncthreads();   // s_part reused by the next chunk
+    }
+    if (tid < 16) {
+        uint32_t t = 0u;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) t = tid == j ? carry[j] : t;
+        totals[d0 + tid] = t;
+    }
+}
+
 template <int IT>
 __global__ void __launch_bounds__(256) k_rts_scatter(const SortBatch b, int pass, int in_b, int shift, int nbits,
                                                      int last) {
@@ -645,7 +737,11 @@ bool radix_sort_batch(const SortSeg* segs, int nseg, int begin_bit, int end_bit,
             hipLaunchKernelGGL(k_rts_count<12>, dim3(nbi, ns), dim3(256), 0, st, bt, p, (int)in_b, shift, nbits);
         else
             hipLaunchKernelGGL(k_rts_count<OS_ITEMS>, dim3(nbi, ns), dim3(256), 0, st, bt, p, (int)in_b, shift, nbits);
+#if LSR_SORT_SCAN_DIGIT
         hipLaunchKernelGGL(k_rts_scan, dim3(256, ns), dim3(256), 0, st, bt, p, items);
+#else
+        hipLaunchKernelGGL(k_rts_scan16, dim3(16, ns), dim3(256), 0, st, bt, p, items, nbits);
+#endif
         if (items == 12)
             hipLaunchKernelGGL(k_rts_scatter<12>, dim3(nbi, ns), dim3(256), 0, st, bt, p, (int)in_b, shift, nbits, last);
         else
