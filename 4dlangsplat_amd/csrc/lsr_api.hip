@@ -363,6 +363,14 @@ int lsr_forward_preprocess_views_async(int32_t n_views, const lsr_settings* cons
         for (int v = 0; v < 2 * n_views; ++v) host_counts[v] = 0;
         return LSR_OK;
     }
+    // page-locked host_counts: the instance scan writes the counts into them itself (no copy
+    // launches); pageable memory gets the copies
+    uint32_t* mapped = nullptr;
+    {
+        void* dptr = nullptr;
+        if (hipHostGetDevicePointer(&dptr, host_counts, 0) == hipSuccess && dptr) mapped = static_cast<uint32_t*>(dptr);
+        else (void)hipGetLastError();   // clear the sticky error of the failed query
+    }
     for (int v0 = 0; v0 < n_views; v0 += lsr::LSR_MAX_VIEWS) {
         const int nv = std::min(n_views - v0, lsr::LSR_MAX_VIEWS);
         lsr::PreprocessArgs a{};
@@ -378,6 +386,10 @@ int lsr_forward_preprocess_views_async(int32_t n_views, const lsr_settings* cons
             ss[k] = lsr::SortSeg{g.key_a, g.val_a, g.key_b, g.val_b, g.sort_tmp, g.total + 3,
                                  lsr::SortGather{g.rect, g.counts, g.rect_sorted}, (size_t)P};
             sc[k] = lsr::ScanSeg{g.counts, g.offsets, g.total, reinterpret_cast<uint32_t*>(g.scan_tmp), (size_t)P};
+            if (mapped) {   // the scan writes {K, error word} straight to the caller's pinned words
+                sc[k].host_total = mapped + 2 * (v0 + k);
+                sc[k].err = g.total + 1;
+            }
         }
         {
             PhaseTimer t(LSR_PHASE_PREPROCESS, st);
@@ -390,14 +402,18 @@ int lsr_forward_preprocess_views_async(int32_t n_views, const lsr_settings* cons
                 return fail(LSR_EHIP, "internal: depth sort parity");
         }
         LSR_LAUNCHED("depth sort", st, s[v0]->debug);
+        if (g_inject_sort_fault.load() & 1u)   // test hook (error word g.total[1], read by the scan below)
+            for (int k = 0; k < nv; ++k)
+                LSR_HIP(hipMemsetAsync(carve_geom(geom[v0 + k], (size_t)P, nullptr).total + 1, 1, 1, st));
+        uint32_t wrote;
         {
             PhaseTimer t(LSR_PHASE_INSTANCE_SCAN, st);
-            lsr::exclusive_scan_batch(sc, nv, st);
+            wrote = lsr::exclusive_scan_batch(sc, nv, st);
         }
         LSR_LAUNCHED("instance scan", st, s[v0]->debug);
         for (int k = 0; k < nv; ++k) {
+            if ((wrote >> k) & 1u) continue;
             Geom g = carve_geom(geom[v0 + k], (size_t)P, nullptr);
-            if (g_inject_sort_fault.load() & 1u) LSR_HIP(hipMemsetAsync(g.total + 1, 1, 1, st));   // test hook
             LSR_HIP(hipMemcpyAsync(host_counts + 2 * (v0 + k), g.total, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                    st));
         }

@@ -294,9 +294,14 @@ struct ScanSeg {
     uint32_t* total;
     uint32_t* partials;   // the segment's scan workspace
     size_t n;
+    // optional: host-mapped pinned words {total, *err} written by the scan itself (no copy launch)
+    uint32_t* host_total = nullptr;
+    const uint32_t* err = nullptr;
 };
 struct ScanBatch { ScanSeg s[LSR_MAX_VIEWS]; };
-void exclusive_scan_batch(const ScanSeg* segs, int nseg, hipStream_t st);
+// Returns the segments (bit i = segs[i]) whose host_total the scan wrote; the caller copies the
+// others' totals itself (single-tile segments and those beyond 8M values take another path).
+uint32_t exclusive_scan_batch(const ScanSeg* segs, int nseg, hipStream_t st);
 size_t radix_temp_bytes(size_t n);
 // stable LSD sort of (key, value) pairs on bits [begin_bit, end_bit); returns true when the result
 // is in (keys_b, vals_b).  err (device word, may be null) is set non-zero if a look-back timed out.

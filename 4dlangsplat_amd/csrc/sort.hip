@@ -79,6 +79,19 @@ __global__ void __launch_bounds__(256) k_scan_down(const uint32_t* __restrict__ 
     if (total && threadIdx.x == 0 && gridDim.x == 1) *total = block_total;
 }
 
+// SCAN_ITEMS consecutive values from `base` (zeros past n): two 16-byte loads when aligned
+static_assert(SCAN_ITEMS == 8, "load_items reads two uint4");
+__device__ __forceinline__ void load_items(const uint32_t* __restrict__ in, size_t base, size_t n,
+                                           uint32_t (&v)[SCAN_ITEMS]) {
+    if (base + SCAN_ITEMS <= n && (reinterpret_cast<uintptr_t>(in + base) & 15u) == 0) {
+        const uint4 a = reinterpret_cast<const uint4*>(in + base)[0], c = reinterpret_cast<const uint4*>(in + base)[1];
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = c.x; v[5] = c.y; v[6] = c.z; v[7] = c.w;
+    } else {
+#pragma unroll
+        for (int i = 0; i < SCAN_ITEMS; ++i) v[i] = (base + i < n) ? in[base + i] : 0u;
+    }
+}
+
 // Two-kernel scan of up to 4096 tiles, for a batch of segments (blockIdx.y): the first kernel
 // writes every tile's sum; in the second, block b sums the partials of blocks [0, b) itself (no
 // separate scan of the partials: one dependent launch less), then scans its tile.  Block 0 also
@@ -89,9 +102,11 @@ __global__ void __launch_bounds__(256) k_scan_reduce_seg(const ScanBatch bt) {
     const size_t n = sg.n;
     if ((size_t)blockIdx.x * SCAN_TILE >= n) return;                  // block-uniform
     const size_t base = (size_t)blockIdx.x * SCAN_TILE + (size_t)threadIdx.x * SCAN_ITEMS;
+    uint32_t v[SCAN_ITEMS];
+    load_items(sg.in, base, n, v);
     uint32_t s = 0;
 #pragma unroll
-    for (int i = 0; i < SCAN_ITEMS; ++i) s += (base + i < n) ? sg.in[base + i] : 0u;
+    for (int i = 0; i < SCAN_ITEMS; ++i) s += v[i];
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) s += __shfl_xor(s, o);
     if ((threadIdx.x & 63) == 0) s_wave[threadIdx.x >> 6] = s;
@@ -108,11 +123,16 @@ __global__ void __launch_bounds__(256) k_scan_down_sum(const ScanBatch bt) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int b = blockIdx.x;
     if (b >= nb) return;                                               // block-uniform
+    // this tile's items are loaded first: their latency overlaps the partials' sum
+    const size_t base = (size_t)b * SCAN_TILE + (size_t)tid * SCAN_ITEMS;
+    uint32_t v[SCAN_ITEMS];
+    load_items(sg.in, base, n, v);
     uint32_t pre = 0, all = 0;
-    for (int i = tid; i < nb; i += 256) {
-        const uint32_t v = sg.partials[i];
-        pre += i < b ? v : 0u;
-        all += v;
+    const int upto = b == 0 ? nb : b;   // block 0 also sums them all for the grand total
+    for (int i = tid; i < upto; i += 256) {
+        const uint32_t x = sg.partials[i];
+        pre += i < b ? x : 0u;
+        all += x;
     }
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -128,16 +148,26 @@ __global__ void __launch_bounds__(256) k_scan_down_sum(const ScanBatch bt) {
     if (tid == 0) s_base[1] = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
     __syncthreads();
     const uint32_t b0 = s_base[0];
-    if (sg.total && b == 0 && tid == 0) *sg.total = s_base[1];
-    const size_t base = (size_t)b * SCAN_TILE + (size_t)tid * SCAN_ITEMS;
-    uint32_t v[SCAN_ITEMS];
-#pragma unroll
-    for (int i = 0; i < SCAN_ITEMS; ++i) v[i] = (base + i < n) ? sg.in[base + i] : 0u;
+    if (b == 0 && tid == 0) {
+        if (sg.total) *sg.total = s_base[1];
+        if (sg.host_total) {   // host-mapped: visible to the host once the kernel has completed
+            sg.host_total[0] = s_base[1];
+            sg.host_total[1] = sg.err ? *sg.err : 0u;
+        }
+    }
     uint32_t block_total;
     block_exclusive_scan8(v, s_wave, block_total);
 #pragma unroll
-    for (int i = 0; i < SCAN_ITEMS; ++i)
-        if (base + i < n) sg.out[base + i] = v[i] + b0;
+    for (int i = 0; i < SCAN_ITEMS; ++i) v[i] += b0;
+    if (base + SCAN_ITEMS <= n && (reinterpret_cast<uintptr_t>(sg.out + base) & 15u) == 0) {
+        uint4* o = reinterpret_cast<uint4*>(sg.out + base);
+        o[0] = make_uint4(v[0], v[1], v[2], v[3]);
+        o[1] = make_uint4(v[4], v[5], v[6], v[7]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < SCAN_ITEMS; ++i)
+            if (base + i < n) sg.out[base + i] = v[i];
+    }
 }
 
 size_t scan_temp_bytes(size_t n) {
@@ -170,23 +200,26 @@ void exclusive_scan_u32(const uint32_t* in, uint32_t* out, size_t n, uint32_t* t
                        (uint32_t*)nullptr);
 }
 
-void exclusive_scan_batch(const ScanSeg* segs, int nseg, hipStream_t st) {
+uint32_t exclusive_scan_batch(const ScanSeg* segs, int nseg, hipStream_t st) {
     ScanBatch bt{};
     int ns = 0;
     size_t nbmax = 0;
+    uint32_t wrote = 0;
     for (int i = 0; i < nseg; ++i) {
         const ScanSeg& g = segs[i];
         const size_t nb = (g.n + SCAN_TILE - 1) / SCAN_TILE;
         if (g.n > (size_t)SCAN_TILE && nb <= (size_t)SCAN_SEG_TILES) {
             bt.s[ns++] = g;
             nbmax = std::max(nbmax, nb);
+            if (g.host_total) wrote |= 1u << i;
         } else {
             exclusive_scan_u32(g.in, g.out, g.n, g.total, g.partials, st);   // one tile, or beyond 8M values
         }
     }
-    if (ns == 0) return;
+    if (ns == 0) return wrote;
     hipLaunchKernelGGL(k_scan_reduce_seg, dim3((unsigned)nbmax, ns), dim3(256), 0, st, bt);
     hipLaunchKernelGGL(k_scan_down_sum, dim3((unsigned)nbmax, ns), dim3(256), 0, st, bt);
+    return wrote;
 }
 
 // ---- radix sort ---------------------------------------------------------------------------------

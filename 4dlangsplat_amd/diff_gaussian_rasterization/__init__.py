@@ -137,6 +137,7 @@ class PendingForward:
         self.count_host = None             # deferred count (preprocess_native(defer_count=True)): pinned
         self.counted = None                # [K, error word], valid once `counted` (an event) has passed
         self.stream = None
+        self.count_batch = None            # (pinned [n, 2] counts of a batch, this view's row)
 
     def resolve(self, binning=False):
         """Deferred-count forwards: wait for the instance count (host waits on the event only, not
@@ -312,8 +313,13 @@ def preprocess_views_native(raster_settings_list, means3D, opacities, shs=None, 
         H, W = int(rs.image_height), int(rs.image_width)
         pf = PendingForward(rs, sts[v], fin, inputs, geoms[v], radii[v], None, device, H, W)
         pf.count_host, pf.stream, pf.counted = counts[v], stream, ev
+        pf.count_batch = (counts, v)      # binning_views_native reads the whole batch at once
         out.append(pf)
     return out
+
+
+def _align(nbytes, a=256):
+    return (nbytes + a - 1) // a * a
 
 
 def binning_views_native(pendings, stream=None):
@@ -324,14 +330,33 @@ def binning_views_native(pendings, stream=None):
         return
     L = _lib.load()
     stream = stream or pendings[0].stream
-    for pf in pendings:
-        pf.resolve()
+    # the device idles from the counts' arrival to the emission launch, so this stretch is kept
+    # short: one wait and one read for a batch's counts, one allocation for all workspaces
+    batch = pendings[0].count_batch
+    if batch is not None and all(pf.count_batch is not None and pf.count_batch[0] is batch[0] for pf in pendings):
+        pendings[0].counted.synchronize()
+        rows = batch[0].tolist()
+        for pf in pendings:
+            K, err = rows[pf.count_batch[1]]
+            if err:
+                raise RuntimeError("lsr_forward_preprocess: depth sort: look-back timed out")
+            pf.num_rendered, pf.counted = K, None
+    else:
+        for pf in pendings:
+            pf.resolve()
     n = len(pendings)
     device = pendings[0].device
+    sizes = []
+    for pf in pendings:
+        sizes += [_align(int(L.lsr_binning_bytes(pf.num_rendered))), _align(int(L.lsr_img_bytes(pf.W, pf.H)))]
     with torch.cuda.stream(stream):
-        for pf in pendings:
-            pf.binning = torch.empty(int(L.lsr_binning_bytes(pf.num_rendered)), dtype=torch.uint8, device=device)
-            pf.img = torch.empty(int(L.lsr_img_bytes(pf.W, pf.H)), dtype=torch.uint8, device=device)
+        ws = torch.empty(sum(sizes), dtype=torch.uint8, device=device)
+    off = 0
+    for i, pf in enumerate(pendings):
+        pf.binning = ws[off:off + sizes[2 * i]]
+        off += sizes[2 * i]
+        pf.img = ws[off:off + sizes[2 * i + 1]]
+        off += sizes[2 * i + 1]
     s_arr = (ctypes.POINTER(_lib.Settings) * n)(*[ctypes.pointer(pf.settings.c) for pf in pendings])
     g_arr = (ctypes.c_void_p * n)(*[pf.geom.data_ptr() for pf in pendings])
     b_arr = (ctypes.c_void_p * n)(*[pf.binning.data_ptr() for pf in pendings])
