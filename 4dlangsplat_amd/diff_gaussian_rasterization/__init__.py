@@ -400,7 +400,13 @@ def render_native(pending: PendingForward, status_event=True):
     if binned:
         binning, img = pending.binning, pending.img
         if pending.ready_stream != stream:   # same stream: already ordered (a wait idles the device)
-            stream.wait_event(pending.ready)
+            waited = getattr(pending.ready, "_lsr_waited_by", None)
+            if waited is None or stream.cuda_stream not in waited:   # views binned together share one event
+                stream.wait_event(pending.ready)
+                try:
+                    pending.ready._lsr_waited_by = (waited or set()) | {stream.cuda_stream}
+                except AttributeError:
+                    pass
         binning.record_stream(stream)
         img.record_stream(stream)
     else:

@@ -156,7 +156,7 @@ class ViewParallelStep:
 
 
 def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool = False, overlap: bool = True,
-                         batch_backward: bool = True):
+                         batch_backward: bool = True, early_views: int = 2):
     """render_view callback for ViewParallelStep on the HIP rasterizer (the product path).
 
     scene    : object with means3D, opacities, shs, lang, scales, rotations device tensors
@@ -183,6 +183,11 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
     for all views, one host wait for their counts); each view then only composites.  Needs the
     step's views (begin_step, as ViewParallelStep.run calls it); without them, views batch alone.
 
+    With more than `early_views` views in the batch, only the first `early_views` are binned on
+    the current stream; the others' binning (emission, tile sort, tile ranges: chains of short,
+    dependent launches that leave most of the GPU idle) runs on a side stream while those first
+    views composite, and each later view's compositing waits for it (an event).
+
     overlap="lookahead" keeps ONE stream: view v+1's preprocess is enqueued ahead of view v's
     compositing with its instance count copied to pinned memory (lsr_forward_preprocess_async);
     the host waits for that count only (an event), while view v's compositing is still queued,
@@ -194,6 +199,7 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
     batch_fwd = overlap == "batched"
     side = (torch.cuda.Stream(device=scene.means3D.device) if (overlap and not lookahead and not batch_fwd)
             else None)
+    bin_side = [None]                     # created at the first split batch (CUDA tensors only)
     pending = {}
     params_ready = torch.cuda.Event() if side is not None else None
     step_views = [None]                   # this rank's views of the current step (begin_step)
@@ -221,7 +227,18 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
         pfs = dgr.preprocess_views_native([settings[w] for w in views], scene.means3D, scene.opacities,
                                           shs=scene.shs, language_feature=scene.lang, scales=scene.scales,
                                           rotations=scene.rotations)
-        dgr.binning_views_native(pfs)
+        if 0 < early_views < len(pfs) and scene.means3D.is_cuda:
+            dev = scene.means3D.device
+            if bin_side[0] is None:
+                bin_side[0] = torch.cuda.Stream(device=dev)   # priorities -1 / +1 measured no better
+            side_b = bin_side[0]
+            dgr.binning_views_native(pfs[:early_views])      # waits for the batch's counts
+            side_b.wait_stream(torch.cuda.current_stream(dev))   # after the preprocess batch
+            for pf in pfs[early_views:]:
+                pf.geom.record_stream(side_b)
+            dgr.binning_views_native(pfs[early_views:], stream=side_b)
+        else:
+            dgr.binning_views_native(pfs)
         pending.update(zip(views, pfs))
 
     def render_view(v: int, bucket: GradBucket):

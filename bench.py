@@ -107,6 +107,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=3, help="headline frames timed on the CPU oracle")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--early-views", type=int, default=2,
+                    help="batched pipeline: views binned before compositing starts; the rest bin on a side stream "
+                         "while they composite (0: all binned first)")
     ap.add_argument("--no-overlap", action="store_true", help="diagnostic: no side stream (uncontended phase times)")
     ap.add_argument("--pipeline", choices=("batched", "lookahead", "side"), default=None,
                     help="view pipelining: the step's forward phase 1 + binning of all views as one batch (batched, "
@@ -149,7 +152,8 @@ def main():
     glang = (torch.randn(C, H, W, generator=g) * 1e-3).to(dev)
     render = native_view_renderer(scene, settings, lambda v, color, lang, depth: (gcol, glang, None),
                                   overlap=False if args.no_overlap else (True if args.pipeline == "side"
-                                                                         else args.pipeline))
+                                                                         else args.pipeline),
+                                  early_views=args.early_views)
     Ks = []
 
     def render_view(v, b):
