@@ -540,7 +540,8 @@ int lsr_forward_composite(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_o
     lsr::RenderFwdArgs r{};
     r.W = W; r.H = H; r.grid_x = gx; r.grid_y = gy; r.C = C; r.include_feature = s->include_feature;
     r.ranges = m.ranges; r.point_list = point_list; r.xy = g.xy; r.conic_o = g.conic_o; r.rgbd = g.rgbd;
-    r.lang = in->language_feature; r.bg = s->bg; r.final_T = m.final_T; r.n_contrib = m.n_contrib;
+    r.lang = in->language_feature;
+    r.lang_split = in->C == 32 ? in->language_feature_split : nullptr; r.bg = s->bg; r.final_T = m.final_T; r.n_contrib = m.n_contrib;
     r.tile_max_contrib = m.tile_max; r.tile_order = m.tile_order;
     r.sort_err = P > 0 ? g.total + 1 : nullptr;
     if (out->host_sort_status) {
@@ -570,6 +571,16 @@ int lsr_forward_status(int32_t P, const void* geom, uint32_t* host_status, lsr_s
     Geom g = carve_geom(const_cast<void*>(geom), (size_t)P, nullptr);
     LSR_HIP(hipMemcpyAsync(host_status, g.total + 1, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost,
                            reinterpret_cast<hipStream_t>(stream)));
+    return LSR_OK;
+}
+
+int lsr_language_split(int32_t P, int32_t C, const float* language_feature, uint16_t* out, lsr_stream_t stream) {
+    if (P < 0 || C != 32 || (P > 0 && (!language_feature || !out)))
+        return fail(LSR_EINVAL, "lsr_language_split: P >= 0, C == 32 and both buffers are required");
+    if ((size_t)P * 32 * 4 >= (size_t)1 << 32) return fail(LSR_EINVAL, "lsr_language_split: P * C * 4 must be < 2^32");
+    if (P == 0) return LSR_OK;
+    lsr::launch_language_split(P, language_feature, out, reinterpret_cast<hipStream_t>(stream));
+    LSR_LAUNCHED("language split", reinterpret_cast<hipStream_t>(stream), false);
     return LSR_OK;
 }
 
@@ -621,7 +632,8 @@ int lsr_backward(const lsr_settings* s, const lsr_fwd_in* in, const lsr_bwd_in* 
         r.W = W; r.H = H; r.grid_x = gx; r.grid_y = gy; r.C = C; r.include_feature = s->include_feature;
         r.ranges = m.ranges; r.point_list = point_list; r.xy = g.xy; r.conic_o = g.conic_o; r.rgbd = g.rgbd;
         r.rect = g.rect; r.inst_off = g.inst_off;
-        r.lang = in->language_feature; r.bg = s->bg; r.final_T = m.final_T; r.n_contrib = m.n_contrib;
+        r.lang = in->language_feature;
+    r.lang_split = in->C == 32 ? in->language_feature_split : nullptr; r.bg = s->bg; r.final_T = m.final_T; r.n_contrib = m.n_contrib;
         r.tile_max_contrib = m.tile_max; r.tile_order = m.tile_order;
         r.dL_dcolor = gin->dL_dout_color; r.dL_dlang = gin->dL_dout_language_feature; r.dL_ddepth = gin->dL_dout_depth;
         r.rec = sc.rec; r.flags = sc.flags; r.recq = recq; r.deterministic = det;
@@ -684,7 +696,8 @@ int lsr_backward_composite(const lsr_settings* s, const lsr_fwd_in* in, const ls
     r.ranges = m.ranges; r.point_list = tile_sort_in_b(gx * gy) ? b.val_b : b.val_a;
     r.xy = g.xy; r.conic_o = g.conic_o; r.rgbd = g.rgbd;
     r.rect = g.rect; r.inst_off = g.inst_off;
-    r.lang = in->language_feature; r.bg = s->bg; r.final_T = m.final_T; r.n_contrib = m.n_contrib;
+    r.lang = in->language_feature;
+    r.lang_split = in->C == 32 ? in->language_feature_split : nullptr; r.bg = s->bg; r.final_T = m.final_T; r.n_contrib = m.n_contrib;
     r.tile_max_contrib = m.tile_max; r.tile_order = m.tile_order;
     r.dL_dcolor = gin->dL_dout_color; r.dL_dlang = gin->dL_dout_language_feature; r.dL_ddepth = gin->dL_dout_depth;
     r.recq = recq; r.deterministic = 0;

@@ -164,6 +164,8 @@ struct PreprocessBwdViewsArgs {
 };
 void launch_preprocess_bwd_views(const PreprocessBwdViewsArgs& a, bool accumulate, hipStream_t st);
 
+void launch_language_split(int P, const float* lang, uint16_t* out, hipStream_t st);
+
 struct RenderFwdArgs {
     int W, H, grid_x, grid_y, C, include_feature;
     const uint2* ranges;
@@ -172,6 +174,7 @@ struct RenderFwdArgs {
     const float4* conic_o;
     const float4* rgbd;
     const float* lang;
+    const uint16_t* lang_split;   // [P][64] bf16 hi | lo (lsr_language_split; C == 32) or null
     const float* bg;
     float* final_T;
     uint32_t* n_contrib;
@@ -195,6 +198,7 @@ struct RenderBwdArgs {
     const uint2* rect;        // binning rectangles (deterministic records are indexed within them)
     const uint32_t* inst_off;
     const float* lang;
+    const uint16_t* lang_split;   // [P][64] bf16 hi | lo (lsr_language_split; C == 32) or null
     const float* bg;
     const float* final_T;
     const uint32_t* n_contrib;

@@ -54,7 +54,7 @@ constexpr int WFIFO = 128;   // compacted entries waiting (list positions and id
 #ifndef LSR_BWD_WAVES
 #define LSR_BWD_WAVES 2   // waves per SIMD the register budget targets
 #endif
-template <bool C32>
+template <bool C32, bool PRE>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LSR_BWD_WAVES, LSR_BWD_WAVES)))
 k_render_bwd_wave(RenderBwdArgs a) {
     __shared__ __attribute__((aligned(16))) __bf16 s_FR[64 * WGB];       // G rows (build), then F / W / t rows
@@ -241,9 +241,15 @@ k_render_bwd_wave(RenderBwdArgs a) {
         const int e = lane >> 2, c0 = 8 * (lane & 3);
         const uint32_t gid = e < n ? s_fg[(head + e) & (WFIFO - 1)] : 0u;
         if constexpr (C32) {
-            const float4* r = reinterpret_cast<const float4*>(at32(a.lang, gid * 32u + c0));
-            pf.f0 = r[0];
-            pf.f1 = r[1];
+            if constexpr (PRE) {   // hi / lo made once per batch (lsr_language_split): bits in f0 / f1
+                const uint4* q = reinterpret_cast<const uint4*>(a.lang_split);
+                pf.f0 = __builtin_bit_cast(float4, *at32(q, gid * 8u + (uint32_t)(c0 >> 3)));
+                pf.f1 = __builtin_bit_cast(float4, *at32(q, gid * 8u + 4u + (uint32_t)(c0 >> 3)));
+            } else {
+                const float4* r = reinterpret_cast<const float4*>(at32(a.lang, gid * 32u + c0));
+                pf.f0 = r[0];
+                pf.f1 = r[1];
+            }
         } else {
             float f[8];
 #pragma unroll
@@ -262,16 +268,21 @@ k_render_bwd_wave(RenderBwdArgs a) {
             s_R[lane] = pf.rgbd.x; s_Gc[lane] = pf.rgbd.y; s_Bc[lane] = pf.rgbd.z; s_D[lane] = pf.rgbd.w;
         }
         const int e = lane >> 2, c0 = 8 * (lane & 3);
-        const float f[8] = {pf.f0.x, pf.f0.y, pf.f0.z, pf.f0.w, pf.f1.x, pf.f1.y, pf.f1.z, pf.f1.w};
-        bf16x8 h8, l8;
+        if constexpr (C32 && PRE) {
+            *reinterpret_cast<uint4*>(s_Fh + e * WFP + c0) = __builtin_bit_cast(uint4, pf.f0);
+            *reinterpret_cast<uint4*>(s_Fl + e * WFP + c0) = __builtin_bit_cast(uint4, pf.f1);
+        } else {
+            const float f[8] = {pf.f0.x, pf.f0.y, pf.f0.z, pf.f0.w, pf.f1.x, pf.f1.y, pf.f1.z, pf.f1.w};
+            bf16x8 h8, l8;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            __bf16 h, l;
-            split_bf16(f[j], h, l);
-            h8[j] = h; l8[j] = l;
+            for (int j = 0; j < 8; ++j) {
+                __bf16 h, l;
+                split_bf16(f[j], h, l);
+                h8[j] = h; l8[j] = l;
+            }
+            *reinterpret_cast<bf16x8*>(s_Fh + e * WFP + c0) = h8;
+            *reinterpret_cast<bf16x8*>(s_Fl + e * WFP + c0) = l8;
         }
-        *reinterpret_cast<bf16x8*>(s_Fh + e * WFP + c0) = h8;
-        *reinterpret_cast<bf16x8*>(s_Fl + e * WFP + c0) = l8;
         wave_lds_sync();
     };
 
@@ -602,8 +613,10 @@ void launch_render_bwd_wave(const RenderBwdArgs& a, hipStream_t st) {
     const int ntiles = a.grid_x * a.grid_y;
     if (a.tile_order) launch_tile_order(ntiles, a.tile_max_contrib, nullptr, a.tile_order, st);
     const bool c32 = a.include_feature && a.C == 32;
-    if (c32) hipLaunchKernelGGL(k_render_bwd_wave<true>, dim3(((ntiles + 7) / 8) * 32), dim3(64), 0, st, a);
-    else hipLaunchKernelGGL(k_render_bwd_wave<false>, dim3(((ntiles + 7) / 8) * 32), dim3(64), 0, st, a);
+    const dim3 grid(((ntiles + 7) / 8) * 32);
+    if (c32 && a.lang_split) hipLaunchKernelGGL((k_render_bwd_wave<true, true>), grid, dim3(64), 0, st, a);
+    else if (c32) hipLaunchKernelGGL((k_render_bwd_wave<true, false>), grid, dim3(64), 0, st, a);
+    else hipLaunchKernelGGL((k_render_bwd_wave<false, false>), grid, dim3(64), 0, st, a);
 }
 
 }  // namespace lsr

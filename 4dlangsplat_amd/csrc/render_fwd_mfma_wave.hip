@@ -139,7 +139,7 @@ __device__ unsigned long long g_fwd_stamps[8];
 // targets one batch (vm_wait_upto with the count of instructions issued after it).  The MFMA A
 // operand is read straight from the staged fp32 rows (no bf16 row copies): 8.6 KB of LDS per
 // wave, so 4 waves per SIMD as the register-staged version.
-template <bool DMA>
+template <bool DMA, bool PRE>
 __global__ void __launch_bounds__(64)
 __attribute__((amdgpu_waves_per_eu(DMA ? LSR_FWD_DMA_WAVES : LSR_FWD_WAVES, DMA ? LSR_FWD_DMA_WAVES : LSR_FWD_WAVES)))
 k_render_fwd_wave_mfma(RenderFwdArgs a) {
@@ -340,8 +340,16 @@ k_render_fwd_wave_mfma(RenderFwdArgs a) {
                 const int e = lane >> 1, c0 = 16 * (lane & 1);
                 const bool ok = e < cnt;
                 const uint32_t gid = ok ? s_fg[(head + e) & (MFIFO - 1)] : 0u;
-                float f[16];
-                if (C == 32) {
+                constexpr bool pre = PRE;   // C == 32, hi / lo made once per batch (a.lang_split)
+                float f[16];   // pre: the bits of hi channels c0 .. +15 in f[0..7], lo in f[8..15]
+                if constexpr (pre) {     // hi at [gid][c0], lo at [gid][32 + c0] (a uint4 holds 8 bf16)
+                    const float4* q = reinterpret_cast<const float4*>(a.lang_split);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const float4 v = *at32(q, gid * 8u + (uint32_t)(c0 >> 3) + (u & 1) + 4u * (u >> 1));
+                        f[4 * u] = v.x; f[4 * u + 1] = v.y; f[4 * u + 2] = v.z; f[4 * u + 3] = v.w;
+                    }
+                } else if (C == 32) {
                     const float4* r = reinterpret_cast<const float4*>(a.lang + (size_t)gid * 32 + c0);
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {   // unmasked (gid 0 is a valid row), zeroed after
@@ -363,22 +371,34 @@ k_render_fwd_wave_mfma(RenderFwdArgs a) {
                     g_co = a.conic_o[gid];
                     g_rgbd = a.rgbd[gid];
                 }
-                if (C == 32) {
+                if constexpr (pre) {
 #pragma unroll
-                    for (int j = 0; j < 16; ++j) f[j] = ok ? f[j] : 0.0f;
-                }
+                    for (int j = 0; j < 16; ++j) f[j] = ok ? f[j] : 0.0f;   // +0.0 = bf16 zeros
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    bf16x8 vh, vl;
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        __bf16 hh, ll;
-                        split_bf16(f[8 * h + j], hh, ll);
-                        vh[j] = hh;
-                        vl[j] = ll;
+                    for (int h = 0; h < 2; ++h) {
+                        *reinterpret_cast<float4*>(s_Fh + e * MFP + c0 + 8 * h) =
+                            make_float4(f[4 * h], f[4 * h + 1], f[4 * h + 2], f[4 * h + 3]);
+                        *reinterpret_cast<float4*>(s_Fl + e * MFP + c0 + 8 * h) =
+                            make_float4(f[8 + 4 * h], f[8 + 4 * h + 1], f[8 + 4 * h + 2], f[8 + 4 * h + 3]);
                     }
-                    *reinterpret_cast<bf16x8*>(s_Fh + e * MFP + c0 + 8 * h) = vh;
-                    *reinterpret_cast<bf16x8*>(s_Fl + e * MFP + c0 + 8 * h) = vl;
+                } else {
+                    if (C == 32) {
+#pragma unroll
+                        for (int j = 0; j < 16; ++j) f[j] = ok ? f[j] : 0.0f;
+                    }
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        bf16x8 vh, vl;
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            __bf16 hh, ll;
+                            split_bf16(f[8 * h + j], hh, ll);
+                            vh[j] = hh;
+                            vl[j] = ll;
+                        }
+                        *reinterpret_cast<bf16x8*>(s_Fh + e * MFP + c0 + 8 * h) = vh;
+                        *reinterpret_cast<bf16x8*>(s_Fl + e * MFP + c0 + 8 * h) = vl;
+                    }
                 }
                 if (lane < MG) {
                     s_k[lane] = g_k + 1u;
@@ -518,15 +538,44 @@ k_render_fwd_wave_mfma(RenderFwdArgs a) {
     if (lane == 0 && m > 0) atomicMax(a.tile_max_contrib + tile, m);
 }
 
+// lsr_language_split: per Gaussian the 32 channels' bf16 hi then lo (split_bf16), one thread per
+// 8 channels (two 16-byte loads, two 16-byte stores)
+__global__ void __launch_bounds__(256) k_language_split(int P, const float* __restrict__ lang, uint16_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= 4u * (uint32_t)P) return;
+    const uint32_t g = i >> 2, c8 = i & 3u;
+    const float4* src = reinterpret_cast<const float4*>(lang);
+    const float4 x = *at32(src, g * 8u + 2u * c8), y = *at32(src, g * 8u + 2u * c8 + 1u);
+    const float f[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+    bf16x8 h, l;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        __bf16 hh, ll;
+        split_bf16(f[j], hh, ll);
+        h[j] = hh;
+        l[j] = ll;
+    }
+    bf16x8* dst = reinterpret_cast<bf16x8*>(out);
+    dst[g * 8u + c8] = h;
+    dst[g * 8u + 4u + c8] = l;
+}
+
+void launch_language_split(int P, const float* lang, uint16_t* out, hipStream_t st) {
+    if (P > 0) hipLaunchKernelGGL(k_language_split, dim3((unsigned)((4u * (uint32_t)P + 255u) / 256u)), dim3(256), 0, st, P, lang, out);
+}
+
 void launch_render_fwd_wave_mfma(const RenderFwdArgs& a, hipStream_t st) {
     const int ntiles = a.grid_x * a.grid_y;
 #if LSR_FWD_DMA
     if (a.C == 32) {
-        hipLaunchKernelGGL(k_render_fwd_wave_mfma<true>, dim3(((ntiles + 7) / 8) * 32), dim3(64), 0, st, a);
+        hipLaunchKernelGGL((k_render_fwd_wave_mfma<true, false>), dim3(((ntiles + 7) / 8) * 32), dim3(64), 0, st, a);
         return;
     }
 #endif
-    hipLaunchKernelGGL(k_render_fwd_wave_mfma<false>, dim3(((ntiles + 7) / 8) * 32), dim3(64), 0, st, a);
+    if (a.lang_split && a.C == 32)
+        hipLaunchKernelGGL((k_render_fwd_wave_mfma<false, true>), dim3(((ntiles + 7) / 8) * 32), dim3(64), 0, st, a);
+    else
+        hipLaunchKernelGGL((k_render_fwd_wave_mfma<false, false>), dim3(((ntiles + 7) / 8) * 32), dim3(64), 0, st, a);
 }
 
 }  // namespace lsr

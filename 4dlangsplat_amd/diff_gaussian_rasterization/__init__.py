@@ -274,18 +274,41 @@ def _run_binning(pf, stream):
     pf.ready_stream = stream
 
 
+def language_split_native(language_feature, stream=None):
+    """lsr_language_split: [P,32] fp32 -> [P,64] int16 holding the bf16 bit patterns (hi channels,
+    then lo) that the compositors' matrix-core operands use; lsr_fwd_in.language_feature_split."""
+    L = _lib.load()
+    device = _check_device(language_feature)
+    P, C = language_feature.shape
+    stream = stream or torch.cuda.current_stream(device)
+    lang = language_feature.detach().to(torch.float32).contiguous()
+    with torch.cuda.stream(stream):
+        out = torch.empty(P, 2 * C, dtype=torch.int16, device=device)
+    _lib.check(L.lsr_language_split(P, C, ctypes.c_void_p(lang.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                    ctypes.c_void_p(stream.cuda_stream)), "lsr_language_split")
+    return out
+
+
 def preprocess_views_native(raster_settings_list, means3D, opacities, shs=None, colors_precomp=None,
-                            language_feature=None, scales=None, rotations=None, cov3D_precomp=None, stream=None):
+                            language_feature=None, scales=None, rotations=None, cov3D_precomp=None, stream=None,
+                            split_language=True):
     """Forward phase 1 of several views of the same Gaussians as one batch
     (lsr_forward_preprocess_views_async: one preprocess launch per 8 views reads each Gaussian once,
     the views' depth sorts and instance scans share their launches) on `stream`.  No host
     synchronisation: returns one deferred-count PendingForward per view; binning_views_native
-    resolves them all with one wait.  Same results as preprocess_native per view."""
+    resolves them all with one wait.  Same results as preprocess_native per view.
+
+    split_language (C == 32): the language rows' bf16 hi / lo operands are made once here for all
+    the batch's views (lsr_language_split) instead of per entry in every compositor wave (same
+    bits, same results)."""
     device = _check_device(means3D)
     L = _lib.load()
     stream = stream or torch.cuda.current_stream(device)
     fin, inputs, P = _fwd_inputs(means3D, opacities, shs, colors_precomp, language_feature, scales, rotations,
                                  cov3D_precomp)
+    if split_language and fin.C == 32 and P > 0 and _lib.has("lsr_language_split"):
+        inputs["language_feature_split"] = language_split_native(inputs["language_feature"], stream=stream)
+        fin.language_feature_split = inputs["language_feature_split"].data_ptr()
     n = len(raster_settings_list)
     sts = [_NativeSettings(rs, device) for rs in raster_settings_list]
     with torch.cuda.stream(stream):

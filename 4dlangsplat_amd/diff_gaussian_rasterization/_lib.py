@@ -32,6 +32,7 @@ class FwdIn(ctypes.Structure):
         ("means3D", ctypes.c_void_p), ("shs", ctypes.c_void_p), ("colors_precomp", ctypes.c_void_p),
         ("language_feature", ctypes.c_void_p), ("opacities", ctypes.c_void_p), ("scales", ctypes.c_void_p),
         ("rotations", ctypes.c_void_p), ("cov3D_precomp", ctypes.c_void_p),
+        ("language_feature_split", ctypes.c_void_p),   # API 3 (older libraries ignore the trailing field)
     ]
 
 
@@ -142,6 +143,8 @@ SIGNATURES = {
     "lsr_backward_preprocess_views": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(ctypes.POINTER(Settings)),
                                                      ctypes.POINTER(FwdIn), ctypes.POINTER(BwdOut),
                                                      ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32, ctypes.c_void_p]),
+    "lsr_language_split": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p]),
     "lsr_mark_visible": (ctypes.c_int, [ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p]),
     "lsr_profile_enable": (ctypes.c_int, [ctypes.c_int32]),
@@ -161,7 +164,7 @@ SIGNATURES = {
 }
 
 # entry points newer builds add; callers check has() (variant libraries of older revisions lack them)
-OPTIONAL = {"lsr_forward_preprocess_views_async", "lsr_forward_binning_views"}
+OPTIONAL = {"lsr_forward_preprocess_views_async", "lsr_forward_binning_views", "lsr_language_split"}
 
 
 def has(name):

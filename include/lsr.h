@@ -38,7 +38,8 @@
 extern "C" {
 #endif
 
-#define LSR_API_VERSION 2   /* 2: lsr_fwd_out.host_sort_status, lsr_forward_status */
+#define LSR_API_VERSION 3   /* 2: lsr_fwd_out.host_sort_status, lsr_forward_status;
+                               3: lsr_fwd_in.language_feature_split, lsr_language_split */
 
 #define LSR_OK 0
 #define LSR_EINVAL 1     /* bad argument (null pointer, exactly-one-of violation, size) */
@@ -75,6 +76,12 @@ typedef struct lsr_fwd_in {
     const float *scales;              /* [P,3]  activated; with rotations, or cov3D_precomp */
     const float *rotations;           /* [P,4]  activated (normalised) */
     const float *cov3D_precomp;       /* [P,6] */
+    const uint16_t *language_feature_split; /* optional, C == 32 only: [P,64] bf16 bit patterns, per
+                                         Gaussian the 32 channels' bf16(x) then bf16(x - bf16(x)),
+                                         as lsr_language_split writes them (the compositors' matrix-
+                                         core operands, made once for all views of a batch instead
+                                         of per entry in every quadrant wave: same bits, same
+                                         results).  NULL: split in the compositors. */
 } lsr_fwd_in;
 
 typedef struct lsr_fwd_out {
@@ -222,6 +229,11 @@ int lsr_backward_preprocess_views(int32_t n_views, const lsr_settings *const *s,
                                   lsr_stream_t stream);
 
 /* markVisible: present[i] = (view-space z of means3D[i]) > 0.2 */
+/* language_feature [P,C] fp32 -> out [P,2C] bf16 bit patterns (hi channels then lo channels) for
+ * lsr_fwd_in.language_feature_split.  C must be 32.  No reference counterpart (an MI355X operand
+ * layout); on the caller's stream. */
+int lsr_language_split(int32_t P, int32_t C, const float *language_feature, uint16_t *out, lsr_stream_t stream);
+
 int lsr_mark_visible(int32_t P, const float *means3D, const float *viewmatrix, const float *projmatrix,
                      uint8_t *present, lsr_stream_t stream);
 

@@ -52,7 +52,7 @@ def test_library_is_built_for_gfx950():
 def test_size_queries():
     from diff_gaussian_rasterization import _lib
     lib = _lib.load()
-    assert lib.lsr_version() == 2
+    assert lib.lsr_version() == 3
     g1, g2 = lib.lsr_geom_bytes(1000), lib.lsr_geom_bytes(2_000_000)
     assert 0 < g1 < g2 and g2 >= 2_000_000 * 60
     assert lib.lsr_binning_bytes(8_600_000) >= 8_600_000 * 16

@@ -85,3 +85,38 @@ def test_bucket_is_sum_of_views(mode):
     scale = float(ref.abs().max())
     assert float((flat - ref).abs().max()) <= 1e-4 * scale
     assert torch.equal(radii, rmax)
+
+
+def test_language_split_bits():
+    """lsr_language_split writes, per Gaussian, bf16(x) for the 32 channels then bf16(x - bf16(x))
+    (round to nearest even, as torch's conversion)."""
+    g = torch.Generator(device="cpu").manual_seed(3)
+    lang = torch.randn(1001, 32, generator=g).cuda()
+    lang[0, :4] = torch.tensor([0.0, -0.0, 1e-30, 3.0e38])
+    out = dgr.language_split_native(lang)
+    hi = lang.to(torch.bfloat16)
+    lo = (lang - hi.float()).to(torch.bfloat16)
+    torch.cuda.synchronize()
+    assert torch.equal(out[:, :32], hi.view(torch.int16)) and torch.equal(out[:, 32:], lo.view(torch.int16))
+
+
+def test_batched_forward_with_language_split_is_bit_identical():
+    """The batched preprocess + binning with the precomputed bf16 operands (split_language) renders
+    every view bit for bit as the single-view forward, whose compositors split the rows themselves;
+    the compositor backward's language gradient agrees within float-atomic reordering."""
+    sc, settings, grads = _setup(n_views=3)
+    args = dict(shs=sc.shs, language_feature=sc.lang, scales=sc.scales, rotations=sc.rotations)
+    pfs = dgr.preprocess_views_native(settings, sc.means3D, sc.opacities, **args)
+    assert "language_feature_split" in pfs[0].inputs
+    dgr.binning_views_native(pfs)
+    for v, (rs, pf) in enumerate(zip(settings, pfs)):
+        c1, l1, r1, d1, st1 = dgr.render_native(pf)
+        c0, l0, r0, d0, st0 = dgr.forward_native(rs, sc.means3D, sc.opacities, **args)
+        assert torch.equal(c0, c1) and torch.equal(l0, l1) and torch.equal(r0, r1) and torch.equal(d0, d1)
+        g0 = torch.zeros_like(sc.lang)
+        g1 = torch.zeros_like(sc.lang)
+        dgr.backward_composite_native(st0, grads[v][0], grads[v][1], None, dL_dlanguage=g0)
+        dgr.backward_composite_native(st1, grads[v][0], grads[v][1], None, dL_dlanguage=g1)
+        torch.cuda.synchronize()
+        scale = float(g0.abs().max())
+        assert scale > 0 and float((g0 - g1).abs().max()) <= 1e-5 * scale
