@@ -428,7 +428,8 @@ k_render_bwd_wave(RenderBwdArgs a) {
             const bool on = act[u];
             const float alpha = alv[u], rom = romv[u], dot = dotv[u];
             T = on ? T * rom : T;
-            const float acc_new = __builtin_fmaf(last_alpha, last_dot, (1.0f - last_alpha) * acc_dot);
+            // upstream's last_alpha * last_c + (1 - last_alpha) * accum_rec, as one fma on the difference
+            const float acc_new = __builtin_fmaf(last_alpha, last_dot - acc_dot, acc_dot);
             acc_dot = on ? acc_new : acc_dot;
             last_dot = on ? dot : last_dot;
             last_alpha = on ? alpha : last_alpha;
