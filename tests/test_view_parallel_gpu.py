@@ -25,11 +25,11 @@ def _setup(n_views=4, P=20000, W=160, H=120, C=32):
     return sc, settings, grads
 
 
-def _run(sc, settings, grads, overlap, deterministic, prefill=None):
+def _run(sc, settings, grads, overlap, deterministic, prefill=None, **kw):
     b = GradBucket(sc.means3D.shape[0], sc.shs.shape[1], sc.lang.shape[1], "cuda", densify_stats=True)
     step = ViewParallelStep(b, len(settings))
     r = native_view_renderer(sc, settings, lambda v, c, l, d: (grads[v][0], grads[v][1], None),
-                             deterministic=deterministic, overlap=overlap)
+                             deterministic=deterministic, overlap=overlap, **kw)
     for _ in range(2):   # second step exercises the pipeline with warm streams and caches
         if prefill is not None:   # whatever the step does not zero or write shows up
             b.flat.fill_(prefill)
@@ -120,3 +120,16 @@ def test_batched_forward_with_language_split_is_bit_identical():
         torch.cuda.synchronize()
         scale = float(g0.abs().max())
         assert scale > 0 and float((g0 - g1).abs().max()) <= 1e-5 * scale
+
+
+@pytest.mark.parametrize("early", [1, 2])
+def test_batched_side_binning_agrees(early):
+    """The batched forward with the later views binned on a side stream (early_views) gives the
+    one-stream result: radii exactly, the float-atomic bucket within 1e-5."""
+    kw = dict(early_views=early)
+    sc, settings, grads = _setup(n_views=4)
+    f0, r0 = _run(sc, settings, grads, overlap="batched", deterministic=False, early_views=0)
+    f1, r1 = _run(sc, settings, grads, overlap="batched", deterministic=False, prefill=float("nan"), **kw)
+    assert not torch.isnan(f1).any() and torch.equal(r0, r1)
+    scale = float(f0.abs().max())
+    assert scale > 0 and float((f0 - f1).abs().max()) <= 1e-5 * scale
