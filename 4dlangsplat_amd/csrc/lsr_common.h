@@ -312,29 +312,39 @@ __device__ __forceinline__ EmitSplat emit_splat(float2 xy, float4 co) {
     s.dyr = -s.dyl;
     return s;
 }
+// R's dx extent [xmin, xmax] over the pixel rows [yb0, min(yb0 + 7, H - 1)] of one 8-row band
+// (ok: the band is inside the image and meets R); shared by every tile column of a tile row
+__device__ __forceinline__ void emit_band(const EmitSplat& s, int yb0, int H, float ex, bool& ok, float& xmin,
+                                          float& xmax) {
+    const int yb1 = min(yb0 + 7, H - 1);
+    // dy = Y - y over the band's pixel rows, clipped to R's y extent
+    const float u0 = fmaxf(s.Y - (float)yb1, -s.hy - ex), u1 = fminf(s.Y - (float)yb0, s.hy + ex);
+    const float r0 = __builtin_amdgcn_sqrtf(fmaxf(0.0f, s.a * s.Q - s.det * u0 * u0));
+    const float r1 = __builtin_amdgcn_sqrtf(fmaxf(0.0f, s.a * s.Q - s.det * u1 * u1));
+    const float l0 = (-s.b * u0 - r0) * s.inv_a, l1 = (-s.b * u1 - r1) * s.inv_a;
+    const float g0 = (-s.b * u0 + r0) * s.inv_a, g1 = (-s.b * u1 + r1) * s.inv_a;
+    xmin = (s.dyl >= u0 && s.dyl <= u1 ? -s.hx : fminf(l0, l1)) - ex;
+    xmax = (s.dyr >= u0 && s.dyr <= u1 ? s.hx : fmaxf(g0, g1)) + ex;
+    ok = yb0 < H && u0 <= u1 && s.hy >= 0.0f;
+}
+// does the band's extent meet the 8 pixel columns from xa (dx = X - x over them)?
+__device__ __forceinline__ bool emit_col_hit(const EmitSplat& s, bool band_ok, float xmin, float xmax, int xa, int W) {
+    const int xb = min(xa + 7, W - 1);
+    return band_ok && xa < W && s.X - (float)xb <= xmax && s.X - (float)xa >= xmin;
+}
+__device__ __forceinline__ float emit_margin(const EmitSplat& s) { return 1e-4f * s.hx + 1e-3f; }
 // mask bit (q = (band) * 2 + (column)) for the four quadrants of the tile at pixel origin (x0, y0)
 __device__ __forceinline__ uint32_t emit_quad_mask(const EmitSplat& s, int x0, int y0, int W, int H) {
-    const float ex = 1e-4f * s.hx + 1e-3f;
+    const float ex = emit_margin(s);
     uint32_t mask = 0;
 #pragma unroll
     for (int band = 0; band < 2; ++band) {
-        const int yb0 = y0 + 8 * band, yb1 = min(yb0 + 7, H - 1);
-        // dy = Y - y over the band's pixel rows, clipped to R's y extent
-        const float u0 = fmaxf(s.Y - (float)yb1, -s.hy - ex), u1 = fminf(s.Y - (float)yb0, s.hy + ex);
-        const float r0 = __builtin_amdgcn_sqrtf(fmaxf(0.0f, s.a * s.Q - s.det * u0 * u0));
-        const float r1 = __builtin_amdgcn_sqrtf(fmaxf(0.0f, s.a * s.Q - s.det * u1 * u1));
-        const float l0 = (-s.b * u0 - r0) * s.inv_a, l1 = (-s.b * u1 - r1) * s.inv_a;
-        const float g0 = (-s.b * u0 + r0) * s.inv_a, g1 = (-s.b * u1 + r1) * s.inv_a;
-        const float xmin = (s.dyl >= u0 && s.dyl <= u1 ? -s.hx : fminf(l0, l1)) - ex;
-        const float xmax = (s.dyr >= u0 && s.dyr <= u1 ? s.hx : fmaxf(g0, g1)) + ex;
-        const bool band_ok = yb0 < H && u0 <= u1 && s.hy >= 0.0f;
+        bool ok;
+        float xmin, xmax;
+        emit_band(s, y0 + 8 * band, H, ex, ok, xmin, xmax);
 #pragma unroll
-        for (int col = 0; col < 2; ++col) {
-            const int xa = x0 + 8 * col, xb = min(xa + 7, W - 1);
-            // dx = X - x over the column's pixels
-            const bool hit = band_ok && xa < W && s.X - (float)xb <= xmax && s.X - (float)xa >= xmin;
-            mask |= hit ? 1u << (band * 2 + col) : 0u;
-        }
+        for (int col = 0; col < 2; ++col)
+            mask |= emit_col_hit(s, ok, xmin, xmax, x0 + 8 * col, W) ? 1u << (band * 2 + col) : 0u;
     }
     return mask;
 }

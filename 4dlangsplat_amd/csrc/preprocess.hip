@@ -276,12 +276,21 @@ __device__ __forceinline__ bool preprocess_one(const PreprocessArgs& a, const Pr
 #else
     if (ntiles > 0 && cmax.x - cmin.x <= 2 && cmax.y - cmin.y <= 2) {
 #endif
+        // emit_quad_mask per tile, with each 8-row band's extent computed once for the tile row
+        // (bit 8 (ty - y0) + 4 band + 2 (tx - x0) + column; the same arithmetic and bits)
         const EmitSplat es = emit_splat(pix, conic);
+        const float ex = emit_margin(es);
         for (int ty = cmin.y; ty < cmax.y; ++ty)
-            for (int tx = cmin.x; tx < cmax.x; ++tx) {
-                const uint32_t m = emit_quad_mask(es, tx * LSR_TILE_X, ty * LSR_TILE_Y, a.W, a.H);
-                const uint32_t sh = (uint32_t)(2 * (ty - cmin.y)) * 4 + 2 * (tx - cmin.x);
-                qmap |= ((m & 3u) << sh) | ((m >> 2) << (sh + 4));
+#pragma unroll
+            for (int band = 0; band < 2; ++band) {
+                bool ok;
+                float xmin, xmax;
+                emit_band(es, ty * LSR_TILE_Y + 8 * band, a.H, ex, ok, xmin, xmax);
+                for (int tx = cmin.x; tx < cmax.x; ++tx)
+#pragma unroll
+                    for (int col = 0; col < 2; ++col)
+                        qmap |= emit_col_hit(es, ok, xmin, xmax, tx * LSR_TILE_X + 8 * col, a.W)
+                                    ? 1u << (8 * (ty - cmin.y) + 4 * band + 2 * (tx - cmin.x) + col) : 0u;
             }
     }
     const uint2 rc = rect_pack((uint32_t)cmin.x, (uint32_t)cmin.y, (uint32_t)cmax.x, (uint32_t)cmax.y, qmap);
