@@ -20,6 +20,7 @@ means2D's values are ignored; its .grad receives the screen-space gradient (NDC 
 from __future__ import annotations
 
 import ctypes
+import functools
 from typing import NamedTuple, Optional
 
 import torch
@@ -345,6 +346,16 @@ def _align(nbytes, a=256):
     return (nbytes + a - 1) // a * a
 
 
+@functools.lru_cache(maxsize=4096)
+def _binning_bytes(K):   # pure size queries, asked on the device's critical path (the count wait)
+    return _align(int(_lib.load().lsr_binning_bytes(K)))
+
+
+@functools.lru_cache(maxsize=64)
+def _img_bytes(W, H):
+    return _align(int(_lib.load().lsr_img_bytes(W, H)))
+
+
 def binning_views_native(pendings, stream=None):
     """Resolve the deferred counts of preprocess_views_native's views (one host wait) and run their
     tile binning as one batch (lsr_forward_binning_views) on `stream` (default: theirs), so that
@@ -371,7 +382,7 @@ def binning_views_native(pendings, stream=None):
     device = pendings[0].device
     sizes = []
     for pf in pendings:
-        sizes += [_align(int(L.lsr_binning_bytes(pf.num_rendered))), _align(int(L.lsr_img_bytes(pf.W, pf.H)))]
+        sizes += [_binning_bytes(pf.num_rendered), _img_bytes(pf.W, pf.H)]
     with torch.cuda.stream(stream):
         ws = torch.empty(sum(sizes), dtype=torch.uint8, device=device)
     off = 0
