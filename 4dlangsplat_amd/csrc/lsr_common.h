@@ -16,36 +16,26 @@
 namespace lsr {
 
 // Falloff exp for x <= 0: the argument clamped at -87 (exp(-87) ~ 1.6e-38: every alpha built
-// from it is far below 1/255), Cody-Waite reduction + a degree-6 minimax polynomial on
-// [-ln2/2, ln2/2] (relative error 1.9e-9 before rounding; Remez, float coefficients) in Horner
-// fma, the exponent assembled by bits.  <= 1.02 ulp above -87 (the degree-7 Taylor it replaced:
-// 0.94), like CUDA expf's 2 ulp bound; made of correctly rounded operations
-// only (max, mul, add, fma) so the host oracle reproduces it bit for bit.  round-to-nearest-even
-// of t = x log2(e) is (t + 1.5 2^23) - 1.5 2^23 (|t| < 2^22), and the low bits of t + 1.5 2^23
-// hold k, so 2^k = bits((t + 1.5 2^23) << 23 + 127 << 23).
+// from it is far below 1/255), k = rint(x log2 e) as fma(x, log2 e, 1.5 2^23) - 1.5 2^23 (one
+// rounding of the exact product: the nearest integer), two-constant Cody-Waite reduction, a
+// degree-5 polynomial 1 + r (1 + r (c2 + r (c3 + r (c4 + r c5)))) minimax in relative error on
+// [-ln2/2, ln2/2] (1.03e-7 before rounding; tools/exp_minimax.py: LP fit, float coefficients) in
+// Horner fma, and 2^k assembled from the low bits of that fma's result (bits(y) << 23 + 127 << 23).
+// <= 2.16 ulp above -87 (the degree-6 polynomial it replaced: 1.02 with one fma more and an
+// unfused rounding step; CUDA's expf: 2 ulp); made of correctly rounded operations only (max,
+// mul, add, fma), so the host oracle (orc_exp) reproduces it bit for bit.
 #define LSR_EXP_MAGIC 12582912.0f
-#ifdef LSR_EXP_DEG7_ABL   // timing ablation only: the previous degree-7 Taylor polynomial
-#define LSR_EXP_C7 1.98412698412698413e-04f
-#define LSR_EXP_C6 1.38888888888888889e-03f
-#define LSR_EXP_C5 8.33333333333333333e-03f
-#define LSR_EXP_C4 4.16666666666666667e-02f
-#define LSR_EXP_C3 1.66666666666666667e-01f
-#define LSR_EXP_C2 0.5f
-#else
-#define LSR_EXP_C6 0.0013836845755577087f   // minimax coefficients of r^6 .. r^2 (r^1, r^0: 1)
-#define LSR_EXP_C5 0.008374815806746483f
-#define LSR_EXP_C4 0.04166822507977486f
-#define LSR_EXP_C3 0.16666419804096222f
-#define LSR_EXP_C2 0.49999991059303284f
-#endif
+#define LSR_EXP_C5 0.008314719423651695f
+#define LSR_EXP_C4 0.041890207678079605f
+#define LSR_EXP_C3 0.16667090356349945f
+#define LSR_EXP_C2 0.499992311000824f
 __device__ __forceinline__ float expf_repro(float x) {
     x = fmaxf(x, -87.0f);
-    const float y = x * 1.44269504088896341f + LSR_EXP_MAGIC;
+    const float y = __builtin_fmaf(x, 1.44269504088896341f, LSR_EXP_MAGIC);
     const float kf = y - LSR_EXP_MAGIC;
     float r = __builtin_fmaf(kf, -0.693145751953125f, x);
     r = __builtin_fmaf(kf, -1.428606765330187045e-06f, r);
-    float p = LSR_EXP_C6;
-    p = __builtin_fmaf(p, r, LSR_EXP_C5);
+    float p = LSR_EXP_C5;
     p = __builtin_fmaf(p, r, LSR_EXP_C4);
     p = __builtin_fmaf(p, r, LSR_EXP_C3);
     p = __builtin_fmaf(p, r, LSR_EXP_C2);
@@ -60,18 +50,12 @@ __device__ __forceinline__ float expf_repro(float x) {
 typedef float lsr_f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ lsr_f2 expf_repro2(lsr_f2 x) {
     x = lsr_f2{fmaxf(x.x, -87.0f), fmaxf(x.y, -87.0f)};
-    const lsr_f2 t = x * lsr_f2{1.44269504088896341f, 1.44269504088896341f};
-    const lsr_f2 y = t + lsr_f2{LSR_EXP_MAGIC, LSR_EXP_MAGIC};
+    const lsr_f2 y = __builtin_elementwise_fma(x, lsr_f2{1.44269504088896341f, 1.44269504088896341f},
+                                               lsr_f2{LSR_EXP_MAGIC, LSR_EXP_MAGIC});
     const lsr_f2 kf = y - lsr_f2{LSR_EXP_MAGIC, LSR_EXP_MAGIC};
     lsr_f2 r = __builtin_elementwise_fma(kf, lsr_f2{-0.693145751953125f, -0.693145751953125f}, x);
     r = __builtin_elementwise_fma(kf, lsr_f2{-1.428606765330187045e-06f, -1.428606765330187045e-06f}, r);
-#ifdef LSR_EXP_DEG7_ABL
-    lsr_f2 p = {LSR_EXP_C7, LSR_EXP_C7};
-    p = __builtin_elementwise_fma(p, r, lsr_f2{LSR_EXP_C6, LSR_EXP_C6});
-#else
-    lsr_f2 p = {LSR_EXP_C6, LSR_EXP_C6};
-#endif
-    p = __builtin_elementwise_fma(p, r, lsr_f2{LSR_EXP_C5, LSR_EXP_C5});
+    lsr_f2 p = {LSR_EXP_C5, LSR_EXP_C5};
     p = __builtin_elementwise_fma(p, r, lsr_f2{LSR_EXP_C4, LSR_EXP_C4});
     p = __builtin_elementwise_fma(p, r, lsr_f2{LSR_EXP_C3, LSR_EXP_C3});
     p = __builtin_elementwise_fma(p, r, lsr_f2{LSR_EXP_C2, LSR_EXP_C2});

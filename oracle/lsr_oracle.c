@@ -38,10 +38,10 @@
  *
  * Floating point
  *   Compiled with -ffp-contract=off.  exp() of the Gaussian falloff uses orc_exp, a
- *   Cody-Waite + degree-6 minimax exp (<= 1.02 ulp) written only with IEEE max, *, +, fmaf and
+ *   Cody-Waite + degree-5 minimax exp (<= 2.16 ulp) written only with IEEE max, *, +, fmaf and
  *   exponent bit assembly, and the falloff exponent is orc_power (two fmaf), so that the product
  *   kernels reproduce the contributor decisions (alpha < 1/255, T < 1e-4) bit for bit.  The CUDA
- *   original uses expf (<= 2 ulp as well) and nvcc's default fma contraction.
+ *   original uses expf (<= 2 ulp) and nvcc's default fma contraction.
  */
 #include <math.h>
 #include <stdint.h>
@@ -67,22 +67,21 @@ typedef float real;
 #define RMIN fminf
 #define RMAX fmaxf
 /* exp for x <= 0; bit-reproducible with the HIP kernels' expf_repro (lsr_common.h): the same
- * sequence of correctly rounded operations (fmaxf, *, +, fmaf).  The argument is clamped at -87
- * (every alpha from exp(-87) ~ 1.6e-38 is far below 1/255); rint(x log2 e) is computed as
- * (t + 1.5 2^23) - 1.5 2^23, e^r by a degree-6 minimax polynomial on [-ln2/2, ln2/2] (Remez,
- * float coefficients, <= 1.02 ulp overall) and 2^k assembled from the low bits of t + 1.5 2^23. */
+ * sequence of correctly rounded operations (fmaxf, fmaf, +, *).  The argument is clamped at -87
+ * (every alpha from exp(-87) ~ 1.6e-38 is far below 1/255); k = rint(x log2 e) is
+ * fmaf(x, log2 e, 1.5 2^23) - 1.5 2^23, e^r by a degree-5 minimax polynomial on [-ln2/2, ln2/2]
+ * (tools/exp_minimax.py, float coefficients, <= 2.16 ulp overall) and 2^k assembled from the low
+ * bits of that fmaf's result. */
 static inline float orc_exp(float x) {
     x = fmaxf(x, -87.0f);
-    const float t = x * 1.44269504088896341f;
-    const float y = t + 12582912.0f;
+    const float y = fmaf(x, 1.44269504088896341f, 12582912.0f);
     const float kf = y - 12582912.0f;
     float r = fmaf(kf, -0.693145751953125f, x);
     r = fmaf(kf, -1.428606765330187045e-06f, r);
-    float p = 0.0013836845755577087f;
-    p = fmaf(p, r, 0.008374815806746483f);
-    p = fmaf(p, r, 0.04166822507977486f);
-    p = fmaf(p, r, 0.16666419804096222f);
-    p = fmaf(p, r, 0.49999991059303284f);
+    float p = 0.008314719423651695f;
+    p = fmaf(p, r, 0.041890207678079605f);
+    p = fmaf(p, r, 0.16667090356349945f);
+    p = fmaf(p, r, 0.499992311000824f);
     p = fmaf(p, r, 1.0f);
     p = fmaf(p, r, 1.0f);
     union { uint32_t u; float f; } yb, s;
