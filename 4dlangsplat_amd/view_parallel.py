@@ -156,7 +156,7 @@ class ViewParallelStep:
 
 
 def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool = False, overlap: bool = True,
-                         batch_backward: bool = True, early_views: int = 2):
+                         batch_backward: bool = True, early_views: int = 3):
     """render_view callback for ViewParallelStep on the HIP rasterizer (the product path).
 
     scene    : object with means3D, opacities, shs, lang, scales, rotations device tensors

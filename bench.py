@@ -107,7 +107,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=3, help="headline frames timed on the CPU oracle")
     ap.add_argument("--no-profile", action="store_true")
-    ap.add_argument("--early-views", type=int, default=2,
+    ap.add_argument("--early-views", type=int, default=3,
                     help="batched pipeline: views binned before compositing starts; the rest bin on a side stream "
                          "while they composite (0: all binned first)")
     ap.add_argument("--no-overlap", action="store_true", help="diagnostic: no side stream (uncontended phase times)")
