@@ -10,37 +10,6 @@
 
 namespace lsr {
 
-__global__ void __launch_bounds__(256) k_iota(int n, uint32_t* __restrict__ out) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) out[i] = (uint32_t)i;
-}
-void launch_iota(int n, uint32_t* out, hipStream_t st) {
-    if (n > 0) hipLaunchKernelGGL(k_iota, dim3((n + 255) / 256), dim3(256), 0, st, n, out);
-}
-
-// Depth-order pass: the one random gather of the binning's counts (8 B per Gaussian), after which
-// the emission reads coalesced depth-ordered arrays (and gathers the splats of listed Gaussians).
-// Ranks past the sorted count (culled Gaussians, dropped by the depth sort) get an empty rectangle.
-__global__ void __launch_bounds__(256) k_gather_tile_counts(int P, const uint32_t* __restrict__ nsorted,
-                                                            const uint32_t* __restrict__ order,
-                                                            const uint2* __restrict__ rect,
-                                                            uint32_t* __restrict__ counts,
-                                                            uint2* __restrict__ rect_sorted) {
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= P) return;
-    const uint32_t ns = nsorted ? *nsorted : (uint32_t)P;
-    const uint2 rc = (uint32_t)r < ns ? rect[order[r]] : make_uint2(0u, 0u);
-    rect_sorted[r] = rc;
-    counts[r] = rect_count(rc);
-}
-
-void launch_gather_tile_counts(int P, const uint32_t* nsorted, const uint32_t* order, const uint2* rect,
-                               uint32_t* counts, uint2* rect_sorted, hipStream_t st) {
-    if (P == 0) return;
-    hipLaunchKernelGGL(k_gather_tile_counts, dim3((P + 255) / 256), dim3(256), 0, st, P, nsorted, order, rect, counts,
-                       rect_sorted);
-}
-
 // Instance emission, one wave per 64 consecutive depth ranks.  Their instances occupy one
 // contiguous slot range [offsets[r0], offsets[r0+63] + counts[r0+63]), so the wave walks that
 // range with consecutive lanes on consecutive slots (fully coalesced key/value stores); a lane

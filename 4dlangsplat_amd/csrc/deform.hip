@@ -1,14 +1,18 @@
-// deform.hip -- the 4D deformation field forward: HexPlane sampling + MLP heads, fused, one block
-// per 64 Gaussians (include/lsr_deform.h; reference scene/hexplane.py, scene/deformation.py).
+// deform.hip -- the 4D deformation field: HexPlane sampling + MLP heads, fused, one block per 64
+// Gaussians (include/lsr_deform.h; reference scene/hexplane.py, scene/deformation.py).
 //
 // Stage 1 (features): 4 threads per Gaussian, each owning 4 of the 16 channels of every plane.
 //   Planes are packed channel-last ([H][W][16], lsr_deform_prepare), so a bilinear tap is one
-//   float4 per thread; the 6 planes of a scale multiply, the scales concatenate (32 features).
+//   float4 per thread; the 6 planes of a scale multiply, the S scales concatenate (16 S features).
 // Stage 2 (MLP): Y = X W^T on v_mfma_f32_32x32x16_bf16 with fp32 accuracy from a bf16 hi/lo split
 //   of both operands (hi*hi + hi*lo + lo*hi).  A comes from the block's activation rows in LDS,
 //   B straight from the packed bf16 weights ([N][K] rows = the torch layout), which stay
-//   L2-resident (94K weights).  Bias, ReLU and the residual adds of the heads are fused into the
-//   epilogues; nothing but the deformed parameters leaves the block.
+//   L2-resident.  feature_out is a chain of max(defor_depth, 1) layers (ReLU between, and before
+//   every head: the heads' first module is a ReLU); bias, ReLU and the residual adds of the heads
+//   are fused into the epilogues.  The rotation head's quaternion product (apply_rotation) and the
+//   discrete language combination (coff head) are per-Gaussian epilogues through LDS.  lang_deform
+//   (the time-varying language field) reads only the language rows and the time: its own kernels
+//   below, on the same MFMA helpers.
 #include "lsr_common.h"
 #include "lsr_internal.h"
 
@@ -19,17 +23,17 @@ typedef float df32x16 __attribute__((ext_vector_type(16)));
 #define DMFMA(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
 
 constexpr int DN = 64;            // Gaussians per block
-constexpr int DFEAT = 32;         // 2 scales x 16 channels
 constexpr int DWID = 128;         // MLP width
-constexpr int DXP = DFEAT + 8;    // LDS row pitch (bf16) of the feature rows
 constexpr int DAP = DWID + 8;     // LDS row pitch (bf16) of the hidden rows
-constexpr int DW2ROWS = 64;       // output rows of every head's last layer, zero padded
+constexpr int DLP = 64 + 8;       // LDS row pitch (bf16) of rows of up to 64 entries
 __constant__ int kHeadOut[5] = {3, 3, 4, 1, 48};
 
 __device__ __forceinline__ void dsplit(float x, __bf16& hi, __bf16& lo) {
     hi = (__bf16)x;
     lo = (__bf16)(x - (float)hi);
 }
+__device__ __forceinline__ int head_out(const DeformArgs& a, int hd) { return hd < 5 ? kHeadOut[hd] : a.centers; }
+__device__ __forceinline__ int row_of(int mt, int q, int hh) { return 32 * mt + (q & 3) + 8 * (q >> 2) + 4 * hh; }
 
 // Y[64 x 32] (+)= X[64 x K] W^T for N tile `nt`: both M tiles (the block's 64 Gaussians) share
 // every weight fragment, so a block reads each weight once per layer.
@@ -59,6 +63,16 @@ __device__ __forceinline__ void mlp_ntile(df32x16 (&acc)[2], const __bf16* __res
         }
     }
 }
+// the same with K a runtime multiple of 16 in [16, 64] (the lang_deform input width)
+__device__ __forceinline__ void mlp_ntile_k(int K, df32x16 (&acc)[2], const __bf16* xh, const __bf16* xl, int xp, int nt,
+                                            const __bf16* wh, const __bf16* wl) {
+    switch (K) {
+        case 16: mlp_ntile<16>(acc, xh, xl, xp, nt, wh, wl); break;
+        case 32: mlp_ntile<32>(acc, xh, xl, xp, nt, wh, wl); break;
+        case 48: mlp_ntile<48>(acc, xh, xl, xp, nt, wh, wl); break;
+        default: mlp_ntile<64>(acc, xh, xl, xp, nt, wh, wl); break;
+    }
+}
 
 // epilogue to LDS rows: relu(acc + bias) as bf16 hi/lo, N tile `nt`, both M tiles
 __device__ __forceinline__ void store_hidden(const df32x16 (&acc)[2], int nt, const float* __restrict__ bias,
@@ -70,7 +84,7 @@ __device__ __forceinline__ void store_hidden(const df32x16 (&acc)[2], int nt, co
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-            const int row = 32 * mt + (q & 3) + 8 * (q >> 2) + 4 * h;
+            const int row = row_of(mt, q, h);
             const float v = fmaxf(acc[mt][q] + b, 0.0f);
             __bf16 hi, lo;
             dsplit(v, hi, lo);
@@ -79,71 +93,220 @@ __device__ __forceinline__ void store_hidden(const df32x16 (&acc)[2], int nt, co
         }
 }
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) k_deform_fwd(DeformArgs a) {
-    __shared__ __attribute__((aligned(16))) __bf16 s_xh[DN * DXP];
-    __shared__ __attribute__((aligned(16))) __bf16 s_xl[DN * DXP];
-    __shared__ __attribute__((aligned(16))) __bf16 s_ah[DN * DAP];
-    __shared__ __attribute__((aligned(16))) __bf16 s_al[DN * DAP];
-    __shared__ __attribute__((aligned(16))) __bf16 s_bh[DN * DAP];
-    __shared__ __attribute__((aligned(16))) __bf16 s_bl[DN * DAP];
+// normalised aabb coordinates + time of Gaussian g (normalize_aabb: (p - aabb[0]) * (2 / (aabb[1] -
+// aabb[0])) - 1, aabb = [xyz_max, xyz_min])
+__device__ __forceinline__ void coords(const DeformArgs& a, int g, float (&crd)[4]) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+        crd[c] = (a.means3D[3 * g + c] - a.aabb[c]) * (2.0f / (a.aabb[3 + c] - a.aabb[c])) - 1.0f;
+    crd[3] = a.time[g];
+}
+// coordinate pair (c0, c1) of plane combo ci: xy, xz, xt, yz, yt, zt.  Functions, not a table: the
+// unrolled loops index the coordinate arrays with compile-time constants (a table in constant
+// memory would send those arrays to scratch).
+__device__ constexpr int kC0(int ci) { return ci < 3 ? 0 : (ci < 5 ? 1 : 2); }
+__device__ constexpr int kC1(int ci) { return ci == 0 ? 1 : (ci == 1 || ci == 3) ? 2 : 3; }
+
+struct Tap {
+    int x0, x1, y0, y1;
+    float fx, fy;
+};
+// bilinear tap of plane pi at the coordinate pair of combo ci (grid_sample, align_corners, border)
+__device__ __forceinline__ Tap tap_of(const DeformArgs& a, int pi, int ci, const float (&crd)[4]) {
+    const int W = a.pw[pi], H = a.ph[pi];
+    const float ix = fminf(fmaxf((crd[kC0(ci)] + 1.0f) * 0.5f * (float)(W - 1), 0.0f), (float)(W - 1));
+    const float iy = fminf(fmaxf((crd[kC1(ci)] + 1.0f) * 0.5f * (float)(H - 1), 0.0f), (float)(H - 1));
+    Tap t;
+    t.x0 = (int)floorf(ix); t.y0 = (int)floorf(iy);
+    t.x1 = min(t.x0 + 1, W - 1); t.y1 = min(t.y0 + 1, H - 1);
+    t.fx = ix - (float)t.x0; t.fy = iy - (float)t.y0;
+    return t;
+}
+__device__ __forceinline__ float4 sample4(const DeformArgs& a, int pi, const Tap& t, int q) {
+    const int W = a.pw[pi];
+    const float4* pl = reinterpret_cast<const float4*>(a.planes + a.poff[pi]) + q;
+    const float4 v00 = pl[(t.y0 * W + t.x0) * 4], v01 = pl[(t.y0 * W + t.x1) * 4];
+    const float4 v10 = pl[(t.y1 * W + t.x0) * 4], v11 = pl[(t.y1 * W + t.x1) * 4];
+    const float w00 = (1.0f - t.fx) * (1.0f - t.fy), w01 = t.fx * (1.0f - t.fy), w10 = (1.0f - t.fx) * t.fy,
+                w11 = t.fx * t.fy;
+    return make_float4(v00.x * w00 + v01.x * w01 + v10.x * w10 + v11.x * w11,
+                       v00.y * w00 + v01.y * w01 + v10.y * w10 + v11.y * w11,
+                       v00.z * w00 + v01.z * w01 + v10.z * w10 + v11.z * w11,
+                       v00.w * w00 + v01.w * w01 + v10.w * w10 + v11.w * w11);
+}
+
+// Stage 1 of both passes: the block's features into LDS rows (bf16 hi/lo, pitch XP), optionally
+// saved as fp32 [P, 16 S]
+template <int S>
+__device__ __forceinline__ void features_to_lds(const DeformArgs& a, int g0, __bf16* xh, __bf16* xl, int xp, float* save) {
+    const int tid = threadIdx.x, gl = tid >> 2, q = tid & 3;
+    const int g = min(g0 + gl, a.P - 1);
+    float crd[4];
+    coords(a, g, crd);
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        float4 prod = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+#pragma unroll
+        for (int ci = 0; ci < 6; ++ci) {
+            const int pi = 6 * s + ci;
+            const float4 v = sample4(a, pi, tap_of(a, pi, ci, crd), q);
+            prod.x *= v.x; prod.y *= v.y; prod.z *= v.z; prod.w *= v.w;
+        }
+        const float f[4] = {prod.x, prod.y, prod.z, prod.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            __bf16 hi, lo;
+            dsplit(f[i], hi, lo);
+            xh[gl * xp + 16 * s + 4 * q + i] = hi;
+            xl[gl * xp + 16 * s + 4 * q + i] = lo;
+        }
+        if (save && g0 + gl < a.P)
+            *reinterpret_cast<float4*>(save + (size_t)(g0 + gl) * (16 * S) + 16 * s + 4 * q) = prod;
+    }
+}
+
+// The quaternion product of batch_quaternion_multiply (utils/graphics_utils.py:121-124)
+__device__ __forceinline__ float4 quat_mul(const float4 a, const float4 b) {
+    return make_float4(a.x * b.x - a.y * b.y - a.z * b.z - a.w * b.w, a.x * b.y + a.y * b.x + a.z * b.w - a.w * b.z,
+                       a.x * b.z - a.y * b.w + a.z * b.x + a.w * b.y, a.x * b.w + a.y * b.z - a.z * b.y + a.w * b.x);
+}
+
+// Discrete language combination of one Gaussian (deformation.py:156-163): centres e_c = lang rows
+// [c][lang_dim] each normalised (no epsilon), m = sum_c coff_c e_c / |e_c|, out = m / (|m| + 1e-9)
+__device__ __forceinline__ void discrete_combine(const DeformArgs& a, int g, const float* coff, float* out) {
+    const int C = a.lang_dim, K = a.centers;
+    const float* e = a.lang + (size_t)g * a.lang_in;
+    float m[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) m[j] = 0.0f;
+    for (int c = 0; c < K; ++c) {
+        float n2 = 0.0f;
+        for (int j = 0; j < C; ++j) n2 += e[c * C + j] * e[c * C + j];
+        const float w = coff[c] / sqrtf(n2);
+#pragma unroll
+        for (int j = 0; j < 32; ++j)
+            if (j < C) m[j] += w * e[c * C + j];
+    }
+    float n2 = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) n2 += m[j] * m[j];
+    const float inv = 1.0f / (sqrtf(n2) + 1e-9f);
+#pragma unroll
+    for (int j = 0; j < 32; ++j)
+        if (j < C) out[(size_t)g * C + j] = m[j] * inv;
+}
+
+// Gradient of the rotation head's output under apply_rotation, Gaussian g: out = p / |p|,
+// p = q1 (x) q2 with q2 = d_rot; dp = (d - out (out . d)) / |p|; d/dq1_k of sum(p dp) =
+// quat_mul(e_k, q2) . dp, likewise q2.  Writes d_rotations (the input's gradient) and the head
+// output's gradient (sG_rot, the upstream of the head's backward).
+__device__ __forceinline__ void quat_grad(const DeformBwdArgs& b, int g, const float* dr) {
+    const float4 q1 = reinterpret_cast<const float4*>(b.f.in[2])[g];
+    const float4 q2 = make_float4(dr[0], dr[1], dr[2], dr[3]);
+    const float4 p = quat_mul(q1, q2);
+    const float inv = 1.0f / sqrtf(p.x * p.x + p.y * p.y + p.z * p.z + p.w * p.w);
+    const float4 d = reinterpret_cast<const float4*>(b.up[2])[g];
+    const float4 o = make_float4(p.x * inv, p.y * inv, p.z * inv, p.w * inv);
+    const float od = o.x * d.x + o.y * d.y + o.z * d.z + o.w * d.w;
+    const float4 dp = make_float4((d.x - o.x * od) * inv, (d.y - o.y * od) * inv, (d.z - o.z * od) * inv,
+                                  (d.w - o.w * od) * inv);
+    float d1[4], d2[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float4 ek = make_float4(k == 0, k == 1, k == 2, k == 3);
+        const float4 u = quat_mul(ek, q2), w = quat_mul(q1, ek);
+        d1[k] = u.x * dp.x + u.y * dp.y + u.z * dp.z + u.w * dp.w;
+        d2[k] = w.x * dp.x + w.y * dp.y + w.z * dp.z + w.w * dp.w;
+    }
+    reinterpret_cast<float4*>(b.d_rotations)[g] = make_float4(d1[0], d1[1], d1[2], d1[3]);
+    reinterpret_cast<float4*>(b.sG_rot)[g] = make_float4(d2[0], d2[1], d2[2], d2[3]);
+}
+
+// Gradient of the discrete combination (deformation.py:156-163), Gaussian g, coff = the head's
+// output: dm from out = m / (|m| + eps); dcoff_c = u_c . dm (+ the upstream of coff itself);
+// du_c = coff_c dm; de_c = (du_c - u_c (u_c . du_c)) / |e_c|.  m_j and dm_j are recomputed per
+// pass (<= 8 terms) instead of held in registers.  Writes d_lang and sG_coff.
+__device__ __forceinline__ void discrete_grad(const DeformBwdArgs& b, int g, const float* coff) {
+    const DeformArgs& a = b.f;
+    const int C = a.lang_dim, K = a.centers;
+    const float* e = a.lang + (size_t)g * a.lang_in;
+    const float* up = b.up_lang ? b.up_lang + (size_t)g * C : nullptr;
+    float w[8], en[8];
+    for (int c = 0; c < K; ++c) {
+        float n2 = 0.0f;
+        for (int j = 0; j < C; ++j) n2 += e[c * C + j] * e[c * C + j];
+        en[c] = sqrtf(n2);
+        w[c] = coff[c] / en[c];
+    }
+    auto m_at = [&](int j) {
+        float m = 0.0f;
+        for (int c = 0; c < K; ++c) m += w[c] * e[c * C + j];
+        return m;
+    };
+    float n2 = 0.0f, md = 0.0f;
+    for (int j = 0; j < C; ++j) {
+        const float m = m_at(j);
+        n2 += m * m;
+        md += m * (up ? up[j] : 0.0f);
+    }
+    const float n = sqrtf(n2), ne = n + 1e-9f, f = md / (n * ne * ne);
+    auto dm_at = [&](int j) { return (up ? up[j] : 0.0f) / ne - m_at(j) * f; };
+    for (int c = 0; c < K; ++c) {
+        float ud = 0.0f;
+        for (int j = 0; j < C; ++j) ud += e[c * C + j] / en[c] * dm_at(j);
+        b.sG_coff[(size_t)g * K + c] = ud + (b.up_coff ? b.up_coff[(size_t)g * K + c] : 0.0f);
+        const float cc = coff[c];   // du_c . u_c = cc (dm . u_c) = cc ud
+        for (int j = 0; j < C; ++j)
+            b.d_lang[(size_t)g * a.lang_in + c * C + j] = (cc * dm_at(j) - e[c * C + j] / en[c] * (cc * ud)) / en[c];
+    }
+}
+
+// GRAD = false: the forward.  GRAD = true (backward, apply_rotation / discrete only): the same
+// recompute, but only the heads whose output feeds a nonlinear epilogue run, and that epilogue is
+// the gradient (quat_grad, discrete_grad) the backward kernel then reads as the head's upstream.
+template <int S, bool GRAD>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) k_deform_fwd(const DeformBwdArgs b) {
+    const DeformArgs& a = b.f;
+    constexpr int F = 16 * S, XP = F + 8;
+    static_assert(XP <= DAP, "feature rows live in the second hidden buffer");
+    __shared__ __attribute__((aligned(16))) __bf16 s_hh[2][DN * DAP];   // hidden rows, ping-pong
+    __shared__ __attribute__((aligned(16))) __bf16 s_hl[2][DN * DAP];
+    __shared__ float s_q[DN][9];                                         // per-Gaussian head outputs
+    // the features are read by the first layer only, which writes buffer 0: they use buffer 1 (72 KB
+    // of LDS in all: two blocks per CU)
+    __bf16* const s_xh = s_hh[1];
+    __bf16* const s_xl = s_hl[1];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int g0 = blockIdx.x * DN;
 
-    // ---- stage 1: HexPlane features, 4 threads per Gaussian ------------------------------------
-    {
-        const int gl = tid >> 2, q = tid & 3;
-        const int g = min(g0 + gl, a.P - 1);
-        float crd[4];
-        // normalize_aabb: (p - aabb[0]) * (2 / (aabb[1] - aabb[0])) - 1, aabb = [xyz_max, xyz_min]
-#pragma unroll
-        for (int c = 0; c < 3; ++c)
-            crd[c] = (__builtin_nontemporal_load(a.means3D + 3 * g + c) - a.aabb[c]) * (2.0f / (a.aabb[3 + c] - a.aabb[c])) - 1.0f;
-        crd[3] = __builtin_nontemporal_load(a.time + g);
-        const int c0s[6] = {0, 0, 0, 1, 1, 2}, c1s[6] = {1, 2, 3, 2, 3, 3};
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            float4 prod = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
-#pragma unroll
-            for (int ci = 0; ci < 6; ++ci) {
-                const int pi = 6 * s + ci;
-                const int W = a.pw[pi], H = a.ph[pi];
-                const float ix = fminf(fmaxf((crd[c0s[ci]] + 1.0f) * 0.5f * (float)(W - 1), 0.0f), (float)(W - 1));
-                const float iy = fminf(fmaxf((crd[c1s[ci]] + 1.0f) * 0.5f * (float)(H - 1), 0.0f), (float)(H - 1));
-                const int x0 = (int)floorf(ix), y0 = (int)floorf(iy);
-                const int x1 = min(x0 + 1, W - 1), y1 = min(y0 + 1, H - 1);
-                const float fx = ix - (float)x0, fy = iy - (float)y0;
-                const float4* pl = reinterpret_cast<const float4*>(a.planes + a.poff[pi]) + q;
-                const float4 v00 = pl[(y0 * W + x0) * 4], v01 = pl[(y0 * W + x1) * 4];
-                const float4 v10 = pl[(y1 * W + x0) * 4], v11 = pl[(y1 * W + x1) * 4];
-                const float w00 = (1.0f - fx) * (1.0f - fy), w01 = fx * (1.0f - fy), w10 = (1.0f - fx) * fy, w11 = fx * fy;
-                prod.x *= v00.x * w00 + v01.x * w01 + v10.x * w10 + v11.x * w11;
-                prod.y *= v00.y * w00 + v01.y * w01 + v10.y * w10 + v11.y * w11;
-                prod.z *= v00.z * w00 + v01.z * w01 + v10.z * w10 + v11.z * w11;
-                prod.w *= v00.w * w00 + v01.w * w01 + v10.w * w10 + v11.w * w11;
-            }
-            const float f[4] = {prod.x, prod.y, prod.z, prod.w};
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                __bf16 hi, lo;
-                dsplit(f[i], hi, lo);
-                s_xh[gl * DXP + 16 * s + 4 * q + i] = hi;
-                s_xl[gl * DXP + 16 * s + 4 * q + i] = lo;
-            }
-        }
-    }
+    features_to_lds<S>(a, g0, s_xh, s_xl, XP, nullptr);
     __syncthreads();
 
-    // ---- stage 2: hidden = relu(feat W_f^T + b_f); wave w owns hidden columns 32 w .. 32 w + 31 ----
+    // ---- feature_out chain: hidden = relu(... relu(feat W_0^T + b_0) ... W_k^T + b_k) ------------
+    int cur = 0;
     {
         df32x16 acc[2] = {df32x16{}, df32x16{}};
-        mlp_ntile<DFEAT>(acc, s_xh, s_xl, DXP, wave, a.wf_h, a.wf_l);
-        store_hidden(acc, wave, a.b_feat, s_ah, s_al);
+        mlp_ntile<F>(acc, s_xh, s_xl, XP, wave, a.wf_h[0], a.wf_l[0]);
+        store_hidden(acc, wave, a.b_feat[0], s_hh[0], s_hl[0]);
     }
     __syncthreads();
+    for (int k = 1; k < a.nlayers; ++k) {
+        df32x16 acc[2] = {df32x16{}, df32x16{}};
+        mlp_ntile<DWID>(acc, s_hh[cur], s_hl[cur], DAP, wave, a.wf_h[k], a.wf_l[k]);
+        store_hidden(acc, wave, a.b_feat[k], s_hh[cur ^ 1], s_hl[cur ^ 1]);
+        __syncthreads();
+        cur ^= 1;
+    }
+    const __bf16 *ah = s_hh[cur], *al = s_hl[cur];
+    __bf16 *bh = s_hh[cur ^ 1], *bl = s_hl[cur ^ 1];
 
-    // ---- heads: out = in + (relu(hidden W1^T + b1) W2^T + b2) -------------------------------------
-    for (int hd = 0; hd < 5; ++hd) {
-        const int nout = kHeadOut[hd];
+    // ---- heads: out = in + (relu(hidden W1^T + b1) W2^T + b2) ---------------------------------------
+    for (int hd = 0; hd < DEF_HEADS; ++hd) {
+        if (!((a.heads >> hd) & 1u)) continue;                       // block-uniform
+        const int nout = head_out(a, hd);
+        const bool quat = hd == 2 && a.apply_rotation, coff = hd == 5;
+        const bool resid_add = !quat && !coff;
+        if (GRAD && resid_add) continue;
         const bool owner = wave < (nout + 31) / 32;     // 1 N tile, or 2 for the 48 SH coefficients
         const int col = 32 * wave + (lane & 31), h = lane >> 5;
         // the residual inputs of this wave's outputs, loaded now so the head's first layer hides
@@ -153,206 +316,233 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
         for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
-                const int g = g0 + 32 * mt + (q & 3) + 8 * (q >> 2) + 4 * h;
-                resid[mt][q] = (owner && col < nout && g < a.P)
+                const int g = g0 + row_of(mt, q, h);
+                resid[mt][q] = (resid_add && owner && col < nout && g < a.P)
                                    ? __builtin_nontemporal_load(a.in[hd] + (size_t)g * nout + col) : 0.0f;
             }
         {
             df32x16 acc[2] = {df32x16{}, df32x16{}};
-            mlp_ntile<DWID>(acc, s_ah, s_al, DAP, wave, a.w1_h + (size_t)hd * DWID * DWID,
-                            a.w1_l + (size_t)hd * DWID * DWID);
-            store_hidden(acc, wave, a.b1[hd], s_bh, s_bl);
+            mlp_ntile<DWID>(acc, ah, al, DAP, wave, a.w1_h[hd], a.w1_l[hd]);
+            store_hidden(acc, wave, a.b1[hd], bh, bl);
         }
         __syncthreads();
         if (owner) {
             df32x16 acc[2] = {df32x16{}, df32x16{}};
-            mlp_ntile<DWID>(acc, s_bh, s_bl, DAP, wave, a.w2_h + (size_t)hd * DW2ROWS * DWID,
-                            a.w2_l + (size_t)hd * DW2ROWS * DWID);
+            mlp_ntile<DWID>(acc, bh, bl, DAP, wave, a.w2_h[hd], a.w2_l[hd]);
             if (col < nout) {
                 const float b = a.b2[hd][col];
-                float* out = a.out[hd];
 #pragma unroll
                 for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
                     for (int q = 0; q < 16; ++q) {
-                        const int g = g0 + 32 * mt + (q & 3) + 8 * (q >> 2) + 4 * h;
-                        if (g < a.P) __builtin_nontemporal_store(resid[mt][q] + (acc[mt][q] + b), out + (size_t)g * nout + col);
+                        const int r = row_of(mt, q, h), g = g0 + r;
+                        const float v = acc[mt][q] + b;
+                        if (resid_add) {
+                            if (g < a.P) __builtin_nontemporal_store(resid[mt][q] + v, a.out[hd] + (size_t)g * nout + col);
+                        } else {
+                            s_q[r][col] = v;
+                            if (!GRAD && coff && a.out_coff && g < a.P) a.out_coff[(size_t)g * nout + col] = v;
+                        }
                     }
+            }
+            if (!resid_add) {                                        // wave 0: one Gaussian per lane
+                wave_lds_sync();
+                const int g = g0 + lane;
+                if (GRAD && g < a.P) {
+                    if (quat) quat_grad(b, g, s_q[lane]);
+                    else discrete_grad(b, g, s_q[lane]);
+                } else if (g < a.P) {
+                    if (quat) {   // rotations = normalize(rotations (x) d_rot)  (deformation.py:135-136)
+                        const float4 q1 = reinterpret_cast<const float4*>(a.in[2])[g];
+                        const float4 p = quat_mul(q1, make_float4(s_q[lane][0], s_q[lane][1], s_q[lane][2], s_q[lane][3]));
+                        const float inv = 1.0f / sqrtf(p.x * p.x + p.y * p.y + p.z * p.z + p.w * p.w);
+                        reinterpret_cast<float4*>(a.out[2])[g] = make_float4(p.x * inv, p.y * inv, p.z * inv, p.w * inv);
+                    } else {
+                        discrete_combine(a, g, s_q[lane], a.out_lang);
+                    }
+                }
             }
         }
         __syncthreads();
     }
 }
 
+template <int S, bool GRAD>
+static void go_fwd(const DeformBwdArgs& b, hipStream_t st) {
+    hipLaunchKernelGGL((k_deform_fwd<S, GRAD>), dim3((b.f.P + DN - 1) / DN), dim3(256), 0, st, b);
+}
+template <bool GRAD>
+static void go_fwd_s(const DeformBwdArgs& b, hipStream_t st) {
+    switch (b.f.n_scales) {
+        case 1: go_fwd<1, GRAD>(b, st); break;
+        case 2: go_fwd<2, GRAD>(b, st); break;
+        case 3: go_fwd<3, GRAD>(b, st); break;
+        default: go_fwd<4, GRAD>(b, st); break;
+    }
+}
 void launch_deform_fwd(const DeformArgs& a, hipStream_t st) {
     if (a.P <= 0) return;
-    hipLaunchKernelGGL(k_deform_fwd, dim3((a.P + DN - 1) / DN), dim3(256), 0, st, a);
+    DeformBwdArgs b{};
+    b.f = a;
+    go_fwd_s<false>(b, st);
 }
 
 // ==== backward ====================================================================================
 // Phase A, one block per 64 Gaussians (the forward's tiling): recompute the features X and the
-// hidden rows A0 = relu(X Wf^T + bf); per head, Z1 = A0 W1^T + b1 (A1 = relu(Z1) saved), the
-// upstream gradient G of the head's outputs through the last layer, dZ1 = (G W2) * [Z1 > 0] (saved),
-// and dA0 += dZ1 W1, all on the bf16 hi/lo MFMA of the forward with transposed weight packs; then
-// dH0 = dA0 * [H0 > 0] (saved), dX = dH0 Wf, and per Gaussian the HexPlane backward: each plane's
-// sample gets dX times the product of the other five planes of its scale, scattered to the 4 bilinear
-// taps (float atomics into a channel-last gradient copy: the 16 channels of a tap are one 64-byte
-// segment), and the coordinate gradient (zero where border padding clips) goes to d_means3D.
+// chain A_k = relu(H_k) (saved); per head, Z1 = A W1^T + b1 (A1 = relu(Z1) saved), the gradient G
+// of the head's output (the upstream gradient, or for the quaternion product / the discrete
+// combination their per-Gaussian backward from the recomputed output), dZ1 = (G W2) * [Z1 > 0]
+// (saved), and dA += dZ1 W1, all on the bf16 hi/lo MFMA of the forward with transposed weight
+// packs; then back through the chain, dH_k = dA_k * [H_k > 0] (saved), dA_{k-1} = dH_k W_k, and
+// dX = dH_0 W_0; and per Gaussian the HexPlane backward: each plane's sample gets dX times the
+// product of the other five planes of its scale, scattered to the 4 bilinear taps (float atomics
+// into a channel-last gradient copy: the 16 channels of a tap are one 64-byte segment), and the
+// coordinate gradient (zero where border padding clips) goes to d_means3D.
 constexpr int DGP = 64 + 8;   // LDS row pitch (bf16) of the upstream-gradient rows (K padded to 64)
 
+// DEEP: a feature_out chain of more than one layer (defor_depth >= 2; runtime length).  The
+// one-layer chain of every reference config gets its own instantiation: the runtime-length loops
+// cost registers (spills) even when they run once.
+template <int S, bool DEEP>
 __global__ void __launch_bounds__(256) k_deform_bwd_a(DeformBwdArgs b) {
-    __shared__ __attribute__((aligned(16))) __bf16 s_xh[DN * DXP];
-    __shared__ __attribute__((aligned(16))) __bf16 s_xl[DN * DXP];
-    __shared__ __attribute__((aligned(16))) __bf16 s_ah[DN * DAP];
-    __shared__ __attribute__((aligned(16))) __bf16 s_al[DN * DAP];
-    __shared__ __attribute__((aligned(16))) __bf16 s_bh[DN * DAP];
-    __shared__ __attribute__((aligned(16))) __bf16 s_bl[DN * DAP];
+    constexpr int F = 16 * S, XP = F + 8;
+    static_assert(XP <= DAP, "feature rows live in the second hidden buffer");
+    __shared__ __attribute__((aligned(16))) __bf16 s_hh[2][DN * DAP];
+    __shared__ __attribute__((aligned(16))) __bf16 s_hl[2][DN * DAP];
+    __bf16* const s_xh = s_hh[1];   // read by the first layer only, which writes buffer 0
+    __bf16* const s_xl = s_hl[1];
     __shared__ __attribute__((aligned(16))) __bf16 s_gh[DN * DGP];
     __shared__ __attribute__((aligned(16))) __bf16 s_gl[DN * DGP];
-    __shared__ float s_dx[DN][DFEAT + 1];
+    __shared__ float s_dx[DN][F + 1];
     __shared__ float s_sdv[4][16][17];   // plane scatter staging, per wave: dv of 16 Gaussians
     __shared__ int s_soff[4][16][4];     //   their 4 tap offsets
     __shared__ float s_sw[4][16][4];     //   and bilinear weights
     const DeformArgs& a = b.f;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int g0 = blockIdx.x * DN;
-    const int c0s[6] = {0, 0, 0, 1, 1, 2}, c1s[6] = {1, 2, 3, 2, 3, 3};
+    const int col = 32 * wave + (lane & 31), hh = lane >> 5;
+    const int L = DEEP ? a.nlayers : 1;
 
-    // ---- features (as the forward), saved as fp32 for the feature_out weight gradient ----------
-    {
-        const int gl = tid >> 2, q = tid & 3;
-        const int g = min(g0 + gl, a.P - 1);
-        float crd[4];
-#pragma unroll
-        for (int c = 0; c < 3; ++c)
-            crd[c] = (a.means3D[3 * g + c] - a.aabb[c]) * (2.0f / (a.aabb[3 + c] - a.aabb[c])) - 1.0f;
-        crd[3] = a.time[g];
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            float4 prod = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
-#pragma unroll
-            for (int ci = 0; ci < 6; ++ci) {
-                const int pi = 6 * s + ci;
-                const int W = a.pw[pi], H = a.ph[pi];
-                const float ix = fminf(fmaxf((crd[c0s[ci]] + 1.0f) * 0.5f * (float)(W - 1), 0.0f), (float)(W - 1));
-                const float iy = fminf(fmaxf((crd[c1s[ci]] + 1.0f) * 0.5f * (float)(H - 1), 0.0f), (float)(H - 1));
-                const int x0 = (int)floorf(ix), y0 = (int)floorf(iy);
-                const int x1 = min(x0 + 1, W - 1), y1 = min(y0 + 1, H - 1);
-                const float fx = ix - (float)x0, fy = iy - (float)y0;
-                const float4* pl = reinterpret_cast<const float4*>(a.planes + a.poff[pi]) + q;
-                const float4 v00 = pl[(y0 * W + x0) * 4], v01 = pl[(y0 * W + x1) * 4];
-                const float4 v10 = pl[(y1 * W + x0) * 4], v11 = pl[(y1 * W + x1) * 4];
-                const float w00 = (1.0f - fx) * (1.0f - fy), w01 = fx * (1.0f - fy), w10 = (1.0f - fx) * fy, w11 = fx * fy;
-                prod.x *= v00.x * w00 + v01.x * w01 + v10.x * w10 + v11.x * w11;
-                prod.y *= v00.y * w00 + v01.y * w01 + v10.y * w10 + v11.y * w11;
-                prod.z *= v00.z * w00 + v01.z * w01 + v10.z * w10 + v11.z * w11;
-                prod.w *= v00.w * w00 + v01.w * w01 + v10.w * w10 + v11.w * w11;
-            }
-            const float f[4] = {prod.x, prod.y, prod.z, prod.w};
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                __bf16 hi, lo;
-                dsplit(f[i], hi, lo);
-                s_xh[gl * DXP + 16 * s + 4 * q + i] = hi;
-                s_xl[gl * DXP + 16 * s + 4 * q + i] = lo;
-            }
-            if (g0 + gl < a.P)
-                *reinterpret_cast<float4*>(b.sX + (size_t)(g0 + gl) * DFEAT + 16 * s + 4 * q) = prod;
-        }
-    }
+    // ---- features (as the forward), saved as fp32 for the first layer's weight gradient ---------
+    features_to_lds<S>(a, g0, s_xh, s_xl, XP, b.sX);
     __syncthreads();
 
-    const int col = 32 * wave + (lane & 31), hh = lane >> 5;
-    auto row_of = [&](int mt, int q) { return 32 * mt + (q & 3) + 8 * (q >> 2) + 4 * hh; };
-    // ---- A0 = relu(X Wf^T + bf), saved -------------------------------------------------------------
-    {
+    // ---- chain forward, A_k = relu(H_k) saved ------------------------------------------------------
+    int cur = 0;
+    for (int k = 0; k < L; ++k) {
         df32x16 acc[2] = {df32x16{}, df32x16{}};
-        mlp_ntile<DFEAT>(acc, s_xh, s_xl, DXP, wave, a.wf_h, a.wf_l);
-        store_hidden(acc, wave, a.b_feat, s_ah, s_al);
-        const float bias = a.b_feat[col];
+        if (k == 0) mlp_ntile<F>(acc, s_xh, s_xl, XP, wave, a.wf_h[0], a.wf_l[0]);
+        else mlp_ntile<DWID>(acc, s_hh[cur], s_hl[cur], DAP, wave, a.wf_h[k], a.wf_l[k]);
+        const int dst = k == 0 ? 0 : cur ^ 1;
+        store_hidden(acc, wave, a.b_feat[k], s_hh[dst], s_hl[dst]);
+        const float bias = a.b_feat[k][col];
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
-                const int g = g0 + row_of(mt, q);
-                if (g < a.P) b.sA0[(size_t)g * DWID + col] = fmaxf(acc[mt][q] + bias, 0.0f);
+                const int g = g0 + row_of(mt, q, hh);
+                if (g < a.P) b.sA[k][(size_t)g * DWID + col] = fmaxf(acc[mt][q] + bias, 0.0f);
             }
+        __syncthreads();
+        cur = dst;
     }
-    __syncthreads();
+    const __bf16 *ah = s_hh[cur], *al = s_hl[cur];
+    __bf16 *bh = s_hh[cur ^ 1], *bl = s_hl[cur ^ 1];
 
-    df32x16 dA0[2] = {df32x16{}, df32x16{}};
-    for (int hd = 0; hd < 5; ++hd) {
-        const int nout = kHeadOut[hd];
-        // upstream gradient rows of this head, K padded to 64
+    df32x16 dA[2] = {df32x16{}, df32x16{}};
+    int slot = 0;
+    for (int hd = 0; hd < DEF_HEADS; ++hd) {
+        if (!((a.heads >> hd) & 1u)) continue;                       // block-uniform
+        const int nout = head_out(a, hd);
+        const bool quat = hd == 2 && a.apply_rotation, coff = hd == 5;
+        // Z1 for this wave's 32 columns (its rows finish before the sync below)
+        uint32_t zpos = 0;   // bit 16 mt + q: Z1 > 0 (the ReLU mask of dZ1; Z1 itself dies here)
+        {
+            df32x16 z[2] = {df32x16{}, df32x16{}};
+            mlp_ntile<DWID>(z, ah, al, DAP, wave, a.w1_h[hd], a.w1_l[hd]);
+            const float bias = a.b1[hd][col];
+            float* sA1 = b.sA1[slot];
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const float zz = z[mt][q] + bias;
+                    zpos |= zz > 0.0f ? 1u << (16 * mt + q) : 0u;
+                    const int r = row_of(mt, q, hh), g = g0 + r;
+                    if (g < a.P) sA1[(size_t)g * DWID + col] = fmaxf(zz, 0.0f);
+                }
+        }
+        // gradient rows of this head's output, K padded to 64
+        const float* G = coff ? b.sG_coff : quat ? b.sG_rot : b.up[hd];   // saved by the GRAD pass
         for (int i = tid; i < DN * 64; i += 256) {
             const int r = i >> 6, k = i & 63, g = g0 + r;
-            const float v = (k < nout && g < a.P) ? b.up[hd][(size_t)g * nout + k] : 0.0f;
+            float v = 0.0f;
+            if (k < nout && g < a.P) v = G[(size_t)g * nout + k];
             __bf16 hi, lo;
             dsplit(v, hi, lo);
             s_gh[r * DGP + k] = hi;
             s_gl[r * DGP + k] = lo;
         }
-        // Z1 for this wave's 32 columns (its rows finish before the sync below)
-        df32x16 z[2] = {df32x16{}, df32x16{}};
-        mlp_ntile<DWID>(z, s_ah, s_al, DAP, wave, a.w1_h + (size_t)hd * DWID * DWID, a.w1_l + (size_t)hd * DWID * DWID);
-        {
-            const float bias = a.b1[hd][col];
-            float* sA1 = b.sA1 + (size_t)hd * a.P * DWID;
-#pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    z[mt][q] += bias;
-                    const int g = g0 + row_of(mt, q);
-                    if (g < a.P) sA1[(size_t)g * DWID + col] = fmaxf(z[mt][q], 0.0f);
-                }
-        }
-        __syncthreads();   // G rows complete
+        __syncthreads();   // G rows complete (and the A1 rows consumed)
         df32x16 d[2] = {df32x16{}, df32x16{}};
-        mlp_ntile<64>(d, s_gh, s_gl, DGP, wave, b.w2t_h + (size_t)hd * DWID * 64, b.w2t_l + (size_t)hd * DWID * 64);
+        mlp_ntile<64>(d, s_gh, s_gl, DGP, wave, b.w2t_h[hd], b.w2t_l[hd]);
         {
-            float* sdZ1 = b.sdZ1 + (size_t)hd * a.P * DWID;
+            float* sdZ1 = b.sdZ1[slot];
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
                 for (int q = 0; q < 16; ++q) {
-                    const int r = row_of(mt, q), g = g0 + r;
-                    const float v = z[mt][q] > 0.0f ? d[mt][q] : 0.0f;
+                    const int r = row_of(mt, q, hh), g = g0 + r;
+                    const float v = (zpos >> (16 * mt + q)) & 1u ? d[mt][q] : 0.0f;
                     __bf16 hi, lo;
                     dsplit(v, hi, lo);
-                    s_bh[r * DAP + col] = hi;
-                    s_bl[r * DAP + col] = lo;
+                    bh[r * DAP + col] = hi;
+                    bl[r * DAP + col] = lo;
                     if (g < a.P) sdZ1[(size_t)g * DWID + col] = v;
                 }
         }
         __syncthreads();   // dZ1 rows complete
-        mlp_ntile<DWID>(dA0, s_bh, s_bl, DAP, wave, b.w1t_h + (size_t)hd * DWID * DWID,
-                        b.w1t_l + (size_t)hd * DWID * DWID);
+        mlp_ntile<DWID>(dA, bh, bl, DAP, wave, b.w1t_h[hd], b.w1t_l[hd]);
         __syncthreads();   // dZ1 / G rows consumed before the next head rewrites them
+        ++slot;
     }
 
-    // ---- dH0 = dA0 * [H0 > 0] (saved), then dX = dH0 Wf --------------------------------------------
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const int r = row_of(mt, q), g = g0 + r;
-            const bool on = (float)s_ah[r * DAP + col] + (float)s_al[r * DAP + col] > 0.0f;
-            const float v = on ? dA0[mt][q] : 0.0f;
-            __bf16 hi, lo;
-            dsplit(v, hi, lo);
-            s_bh[r * DAP + col] = hi;
-            s_bl[r * DAP + col] = lo;
-            if (g < a.P) b.sdH0[(size_t)g * DWID + col] = v;
-        }
-    __syncthreads();
-    if (wave == 0) {
-        df32x16 acc[2] = {df32x16{}, df32x16{}};
-        mlp_ntile<DWID>(acc, s_bh, s_bl, DAP, 0, b.wft_h, b.wft_l);
+    // ---- back through the chain: dH_k = dA_k * [H_k > 0] (saved), dA_{k-1} = dH_k W_k -------------
+    for (int k = L - 1; k >= 0; --k) {
+        // dH_k rows into the buffer that does not hold what the MFMA below still reads
+        __bf16 *dh_h = s_hh[cur ^ 1], *dh_l = s_hl[cur ^ 1];
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-            for (int q = 0; q < 16; ++q) s_dx[row_of(mt, q)][lane & 31] = acc[mt][q];
+            for (int q = 0; q < 16; ++q) {
+                const int r = row_of(mt, q, hh), g = g0 + r;
+                const float av = g < a.P ? b.sA[k][(size_t)g * DWID + col] : 0.0f;   // this block wrote it
+                const float v = av > 0.0f ? dA[mt][q] : 0.0f;
+                __bf16 hi, lo;
+                dsplit(v, hi, lo);
+                dh_h[r * DAP + col] = hi;
+                dh_l[r * DAP + col] = lo;
+                if (g < a.P) b.sdH[k][(size_t)g * DWID + col] = v;
+            }
+        __syncthreads();
+        cur ^= 1;
+        if (k > 0) {
+            df32x16 acc[2] = {df32x16{}, df32x16{}};
+            mlp_ntile<DWID>(acc, dh_h, dh_l, DAP, wave, b.wft_h[k], b.wft_l[k]);
+            dA[0] = acc[0];
+            dA[1] = acc[1];
+            __syncthreads();   // the dH rows read before the next iteration overwrites the other buffer
+        } else if (wave < (F + 31) / 32) {
+            df32x16 acc[2] = {df32x16{}, df32x16{}};
+            mlp_ntile<DWID>(acc, dh_h, dh_l, DAP, wave, b.wft_h[0], b.wft_l[0]);
+            const int c = 32 * wave + (lane & 31);
+            if (c < F) {
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) s_dx[row_of(mt, q, hh)][c] = acc[mt][q];
+            }
+        }
     }
     __syncthreads();
 
@@ -362,32 +552,13 @@ __global__ void __launch_bounds__(256) k_deform_bwd_a(DeformBwdArgs b) {
         const bool ok = g0 + gl < a.P;
         const int g = min(g0 + gl, a.P - 1);
         float crd[4];
-#pragma unroll
-        for (int c = 0; c < 3; ++c)
-            crd[c] = (a.means3D[3 * g + c] - a.aabb[c]) * (2.0f / (a.aabb[3 + c] - a.aabb[c])) - 1.0f;
-        crd[3] = a.time[g];
+        coords(a, g, crd);
         float dq[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
+        for (int s = 0; s < S; ++s) {
             float4 v[6];
 #pragma unroll
-            for (int ci = 0; ci < 6; ++ci) {   // the six samples of this scale
-                const int pi = 6 * s + ci;
-                const int W = a.pw[pi], H = a.ph[pi];
-                const float ix = fminf(fmaxf((crd[c0s[ci]] + 1.0f) * 0.5f * (float)(W - 1), 0.0f), (float)(W - 1));
-                const float iy = fminf(fmaxf((crd[c1s[ci]] + 1.0f) * 0.5f * (float)(H - 1), 0.0f), (float)(H - 1));
-                const int x0 = (int)floorf(ix), y0 = (int)floorf(iy);
-                const int x1 = min(x0 + 1, W - 1), y1 = min(y0 + 1, H - 1);
-                const float fx = ix - (float)x0, fy = iy - (float)y0;
-                const float4* pl = reinterpret_cast<const float4*>(a.planes + a.poff[pi]) + q;
-                const float4 v00 = pl[(y0 * W + x0) * 4], v01 = pl[(y0 * W + x1) * 4];
-                const float4 v10 = pl[(y1 * W + x0) * 4], v11 = pl[(y1 * W + x1) * 4];
-                const float w00 = (1.0f - fx) * (1.0f - fy), w01 = fx * (1.0f - fy), w10 = (1.0f - fx) * fy, w11 = fx * fy;
-                v[ci] = make_float4(v00.x * w00 + v01.x * w01 + v10.x * w10 + v11.x * w11,
-                                    v00.y * w00 + v01.y * w01 + v10.y * w10 + v11.y * w11,
-                                    v00.z * w00 + v01.z * w01 + v10.z * w10 + v11.z * w11,
-                                    v00.w * w00 + v01.w * w01 + v10.w * w10 + v11.w * w11);
-            }
+            for (int ci = 0; ci < 6; ++ci) v[ci] = sample4(a, 6 * s + ci, tap_of(a, 6 * s + ci, ci, crd), q);
             const float dxv[4] = {s_dx[gl][16 * s + 4 * q], s_dx[gl][16 * s + 4 * q + 1], s_dx[gl][16 * s + 4 * q + 2],
                                   s_dx[gl][16 * s + 4 * q + 3]};
 #pragma unroll
@@ -401,17 +572,14 @@ __global__ void __launch_bounds__(256) k_deform_bwd_a(DeformBwdArgs b) {
                 const float dv[4] = {dxv[0] * oth.x, dxv[1] * oth.y, dxv[2] * oth.z, dxv[3] * oth.w};
                 const int pi = 6 * s + ci;
                 const int W = a.pw[pi], H = a.ph[pi];
-                const float rx = (crd[c0s[ci]] + 1.0f) * 0.5f * (float)(W - 1);
-                const float ry = (crd[c1s[ci]] + 1.0f) * 0.5f * (float)(H - 1);
-                const float ix = fminf(fmaxf(rx, 0.0f), (float)(W - 1));
-                const float iy = fminf(fmaxf(ry, 0.0f), (float)(H - 1));
-                const int x0 = (int)floorf(ix), y0 = (int)floorf(iy);
-                const int x1 = min(x0 + 1, W - 1), y1 = min(y0 + 1, H - 1);
-                const float fx = ix - (float)x0, fy = iy - (float)y0;
+                const float rx = (crd[kC0(ci)] + 1.0f) * 0.5f * (float)(W - 1);
+                const float ry = (crd[kC1(ci)] + 1.0f) * 0.5f * (float)(H - 1);
+                const Tap t = tap_of(a, pi, ci, crd);
                 const float4* pl = reinterpret_cast<const float4*>(a.planes + a.poff[pi]) + q;
-                const float4 t00 = pl[(y0 * W + x0) * 4], t01 = pl[(y0 * W + x1) * 4];
-                const float4 t10 = pl[(y1 * W + x0) * 4], t11 = pl[(y1 * W + x1) * 4];
-                const float w00 = (1.0f - fx) * (1.0f - fy), w01 = fx * (1.0f - fy), w10 = (1.0f - fx) * fy, w11 = fx * fy;
+                const float4 t00 = pl[(t.y0 * W + t.x0) * 4], t01 = pl[(t.y0 * W + t.x1) * 4];
+                const float4 t10 = pl[(t.y1 * W + t.x0) * 4], t11 = pl[(t.y1 * W + t.x1) * 4];
+                const float w00 = (1.0f - t.fx) * (1.0f - t.fy), w01 = t.fx * (1.0f - t.fy),
+                            w10 = (1.0f - t.fx) * t.fy, w11 = t.fx * t.fy;
                 // scatter: stage the wave's 16 Gaussians (16 channels, 4 taps each) in LDS, then one
                 // atomic instruction per Gaussian covers its 4 taps x 16 channels = four full
                 // 64-byte segments (lane = 16 tap + channel) instead of 16 partial ones; blocks add
@@ -422,8 +590,8 @@ __global__ void __launch_bounds__(256) k_deform_bwd_a(DeformBwdArgs b) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) s_sdv[wave][wl][4 * q + i] = ok ? dv[i] : 0.0f;
                     if (q == 0) {
-                        s_soff[wave][wl][0] = (y0 * W + x0) * 16; s_soff[wave][wl][1] = (y0 * W + x1) * 16;
-                        s_soff[wave][wl][2] = (y1 * W + x0) * 16; s_soff[wave][wl][3] = (y1 * W + x1) * 16;
+                        s_soff[wave][wl][0] = (t.y0 * W + t.x0) * 16; s_soff[wave][wl][1] = (t.y0 * W + t.x1) * 16;
+                        s_soff[wave][wl][2] = (t.y1 * W + t.x0) * 16; s_soff[wave][wl][3] = (t.y1 * W + t.x1) * 16;
                         s_sw[wave][wl][0] = w00; s_sw[wave][wl][1] = w01; s_sw[wave][wl][2] = w10; s_sw[wave][wl][3] = w11;
                     }
                     wave_lds_sync();
@@ -431,12 +599,8 @@ __global__ void __launch_bounds__(256) k_deform_bwd_a(DeformBwdArgs b) {
                     const int tap = lane >> 4, ch = lane & 15;
 #pragma unroll 4
                     for (int j = 0; j < 16; ++j) {
-                        const float v = s_sdv[wave][j][ch] * s_sw[wave][j][tap];
-#ifndef LSR_ABL_NOSCATTER
-                        if (v != 0.0f) atomicAdd(gp + s_soff[wave][j][tap] + ch, v);
-#else
-                        if (v == 12345.0f) gp[0] = v;   // timing ablation only
-#endif
+                        const float val = s_sdv[wave][j][ch] * s_sw[wave][j][tap];
+                        if (val != 0.0f) atomicAdd(gp + s_soff[wave][j][tap] + ch, val);
                     }
                     wave_lds_sync();   // staging read before the next plane rewrites it
                 }
@@ -445,11 +609,11 @@ __global__ void __launch_bounds__(256) k_deform_bwd_a(DeformBwdArgs b) {
                 float dix = 0.0f, diy = 0.0f;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    dix += dv[i] * ((a01[i] - a00[i]) * (1.0f - fy) + (a11[i] - a10[i]) * fy);
-                    diy += dv[i] * ((a10[i] - a00[i]) * (1.0f - fx) + (a11[i] - a01[i]) * fx);
+                    dix += dv[i] * ((a01[i] - a00[i]) * (1.0f - t.fy) + (a11[i] - a10[i]) * t.fy);
+                    diy += dv[i] * ((a10[i] - a00[i]) * (1.0f - t.fx) + (a11[i] - a01[i]) * t.fx);
                 }
-                if (rx > 0.0f && rx < (float)(W - 1)) dq[c0s[ci]] += dix * 0.5f * (float)(W - 1);
-                if (ry > 0.0f && ry < (float)(H - 1)) dq[c1s[ci]] += diy * 0.5f * (float)(H - 1);
+                if (rx > 0.0f && rx < (float)(W - 1)) dq[kC0(ci)] += dix * 0.5f * (float)(W - 1);
+                if (ry > 0.0f && ry < (float)(H - 1)) dq[kC1(ci)] += diy * 0.5f * (float)(H - 1);
             }
         }
 #pragma unroll
@@ -466,9 +630,198 @@ __global__ void __launch_bounds__(256) k_deform_bwd_a(DeformBwdArgs b) {
     }
 }
 
-void launch_deform_bwd_a(const DeformBwdArgs& a, hipStream_t st) {
-    if (a.f.P <= 0) return;
-    hipLaunchKernelGGL(k_deform_bwd_a, dim3((a.f.P + DN - 1) / DN), dim3(256), 0, st, a);
+template <int S>
+static void go_bwd(const DeformBwdArgs& b, hipStream_t st) {
+    if (b.f.nlayers > 1) hipLaunchKernelGGL((k_deform_bwd_a<S, true>), dim3((b.f.P + DN - 1) / DN), dim3(256), 0, st, b);
+    else hipLaunchKernelGGL((k_deform_bwd_a<S, false>), dim3((b.f.P + DN - 1) / DN), dim3(256), 0, st, b);
+}
+void launch_deform_bwd_a(const DeformBwdArgs& b, hipStream_t st) {
+    if (b.f.P <= 0) return;
+    if (b.f.apply_rotation || (b.f.heads >> 5) & 1u) go_fwd_s<true>(b, st);   // the nonlinear heads' gradients
+    switch (b.f.n_scales) {
+        case 1: go_bwd<1>(b, st); break;
+        case 2: go_bwd<2>(b, st); break;
+        case 3: go_bwd<3>(b, st); break;
+        default: go_bwd<4>(b, st); break;
+    }
+}
+
+// ==== lang_deform (deformation.py:68, 172-180) ====================================================
+// relu([lang, t, sin(2^i t), cos(2^i t)]) -> Linear(kin, 128), ReLU, Linear(128, 128), ReLU,
+// Linear(128, lang_dim); lang_out = normalize((lang +) dl).  One block per 64 Gaussians; the input
+// rows are K-padded to a multiple of 16 (<= 64).
+__device__ __forceinline__ float lang_in_value(const LangDeformArgs& a, int g, int k) {
+    const int C = a.lang_dim;
+    if (k < C) return a.lang[(size_t)g * C + k];
+    const float t = a.time[g];
+    if (k == C) return t;
+    const int j = k - C - 1;                                          // poc_fre: sin block, cos block
+    if (j < a.time_pe) return sinf(t * (float)(1 << j));
+    if (j < 2 * a.time_pe) return cosf(t * (float)(1 << (j - a.time_pe)));
+    return 0.0f;
+}
+
+// forward of the MLP for the block's 64 rows; leaves v = (lang +) dl in s_v[64][33] (and with
+// `save`, the saved activations).  kpad = 16-padded input width.
+__device__ __forceinline__ void lang_mlp_fwd(const LangDeformArgs& a, int g0, int kpad, __bf16* xh, __bf16* xl,
+                                             __bf16 (*hh)[DN * DAP], __bf16 (*hl)[DN * DAP], float (*s_v)[33], bool save) {
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hh_ = lane >> 5;
+    for (int i = tid; i < DN * 64; i += 256) {
+        const int r = i >> 6, k = i & 63, g = g0 + r;
+        const float v = (g < a.P && k < a.kin) ? fmaxf(lang_in_value(a, g, k), 0.0f) : 0.0f;
+        if (k < kpad) {
+            __bf16 hi, lo;
+            dsplit(v, hi, lo);
+            xh[r * DLP + k] = hi;
+            xl[r * DLP + k] = lo;
+        }
+        if (save && g < a.P && k < a.kin) a.sU0[(size_t)g * a.kin + k] = v;
+    }
+    __syncthreads();
+    const int col = 32 * wave + (lane & 31);
+    for (int layer = 0; layer < 2; ++layer) {
+        df32x16 acc[2] = {df32x16{}, df32x16{}};
+        if (layer == 0) mlp_ntile_k(kpad, acc, xh, xl, DLP, wave, a.w_h[0], a.w_l[0]);
+        else mlp_ntile<DWID>(acc, hh[0], hl[0], DAP, wave, a.w_h[1], a.w_l[1]);
+        store_hidden(acc, wave, a.b[layer], hh[layer], hl[layer]);
+        if (save) {
+            const float bias = a.b[layer][col];
+            float* dst = layer == 0 ? a.sU1 : a.sU2;
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const int g = g0 + row_of(mt, q, hh_);
+                    if (g < a.P) dst[(size_t)g * DWID + col] = fmaxf(acc[mt][q] + bias, 0.0f);
+                }
+        }
+        __syncthreads();
+    }
+    if (wave == 0) {
+        df32x16 acc[2] = {df32x16{}, df32x16{}};
+        mlp_ntile<DWID>(acc, hh[1], hl[1], DAP, 0, a.w_h[2], a.w_l[2]);
+        const int c = lane & 31;
+        if (c < a.lang_dim) {
+            const float bias = a.b[2][c];
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const int r = row_of(mt, q, hh_), g = g0 + r;
+                    float v = acc[mt][q] + bias;
+                    if (a.residual && g < a.P) v += a.lang[(size_t)g * a.lang_dim + c];
+                    s_v[r][c] = v;
+                }
+        }
+    }
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) k_lang_deform_fwd(LangDeformArgs a) {
+    __shared__ __attribute__((aligned(16))) __bf16 s_xh[DN * DLP];
+    __shared__ __attribute__((aligned(16))) __bf16 s_xl[DN * DLP];
+    __shared__ __attribute__((aligned(16))) __bf16 s_hh[2][DN * DAP];
+    __shared__ __attribute__((aligned(16))) __bf16 s_hl[2][DN * DAP];
+    __shared__ float s_v[DN][33];
+    const int g0 = blockIdx.x * DN, tid = threadIdx.x;
+    const int kpad = (a.kin + 15) / 16 * 16;
+    lang_mlp_fwd(a, g0, kpad, s_xh, s_xl, s_hh, s_hl, s_v, false);
+    if (tid < DN && g0 + tid < a.P) {   // out = v / (|v| + 1e-9)
+        float n2 = 0.0f;
+        for (int c = 0; c < a.lang_dim; ++c) n2 += s_v[tid][c] * s_v[tid][c];
+        const float inv = 1.0f / (sqrtf(n2) + 1e-9f);
+        for (int c = 0; c < a.lang_dim; ++c) a.out_lang[(size_t)(g0 + tid) * a.lang_dim + c] = s_v[tid][c] * inv;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_lang_deform_bwd(LangDeformArgs a) {
+    __shared__ __attribute__((aligned(16))) __bf16 s_xh[DN * DLP];
+    __shared__ __attribute__((aligned(16))) __bf16 s_xl[DN * DLP];
+    __shared__ __attribute__((aligned(16))) __bf16 s_hh[2][DN * DAP];
+    __shared__ __attribute__((aligned(16))) __bf16 s_hl[2][DN * DAP];
+    __shared__ __attribute__((aligned(16))) __bf16 s_gh[DN * DLP];
+    __shared__ __attribute__((aligned(16))) __bf16 s_gl[DN * DLP];
+    __shared__ float s_v[DN][33];
+    const int g0 = blockIdx.x * DN, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hh = lane >> 5;
+    const int col = 32 * wave + (lane & 31);
+    const int C = a.lang_dim, kpad = (a.kin + 15) / 16 * 16;
+    lang_mlp_fwd(a, g0, kpad, s_xh, s_xl, s_hh, s_hl, s_v, true);
+    // dv = d / (|v| + eps) - v (v . d) / (|v| (|v| + eps)^2), d = the upstream language gradient
+    if (tid < DN) {
+        const int g = g0 + tid;
+        float n2 = 0.0f, vd = 0.0f;
+        for (int c = 0; c < C; ++c) {
+            const float up = (g < a.P && a.up_lang) ? a.up_lang[(size_t)g * C + c] : 0.0f;
+            n2 += s_v[tid][c] * s_v[tid][c];
+            vd += s_v[tid][c] * up;
+        }
+        const float n = sqrtf(n2), ne = n + 1e-9f, f = n > 0.0f ? vd / (n * ne * ne) : 0.0f;
+        for (int c = 0; c < 32; ++c) {
+            float dv = 0.0f;
+            if (c < C && g < a.P) dv = (a.up_lang ? a.up_lang[(size_t)g * C + c] : 0.0f) / ne - s_v[tid][c] * f;
+            s_v[tid][c] = dv;
+            __bf16 hi, lo;
+            dsplit(dv, hi, lo);
+            s_gh[tid * DLP + c] = hi;
+            s_gl[tid * DLP + c] = lo;
+            if (c < C && g < a.P) a.sdv[(size_t)g * C + c] = dv;
+        }
+    }
+    __syncthreads();
+    // dZ2 = (dv W3) * [U2 > 0]; dZ1 = (dZ2 W2) * [U1 > 0]   (U_k > 0 <=> Z_k > 0)
+    for (int layer = 1; layer >= 0; --layer) {
+        df32x16 acc[2] = {df32x16{}, df32x16{}};
+        if (layer == 1) mlp_ntile<32>(acc, s_gh, s_gl, DLP, wave, a.wt_h[2], a.wt_l[2]);
+        else mlp_ntile<DWID>(acc, s_hh[1], s_hl[1], DAP, wave, a.wt_h[1], a.wt_l[1]);
+        const __bf16 *uh = s_hh[layer], *ul = s_hl[layer];
+        float dz[2][16];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int r = row_of(mt, q, hh);
+                const bool on = (float)uh[r * DAP + col] + (float)ul[r * DAP + col] > 0.0f;
+                dz[mt][q] = on ? acc[mt][q] : 0.0f;
+            }
+        float* save = layer == 1 ? a.sdZ2 : a.sdZ1;
+        __syncthreads();   // U rows (and, for layer 0, the dZ2 rows in buffer 1) read
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int r = row_of(mt, q, hh), g = g0 + r;
+                __bf16 hi, lo;
+                dsplit(dz[mt][q], hi, lo);
+                s_hh[1][r * DAP + col] = hi;   // dZ rows replace U2 (the next step's A operand)
+                s_hl[1][r * DAP + col] = lo;
+                if (g < a.P) save[(size_t)g * DWID + col] = dz[mt][q];
+            }
+        __syncthreads();
+    }
+    // dU0 = dZ1 W1 (waves owning input columns), d_lang = (dv if residual) + dU0 * [U0 > 0]
+    if (wave < (kpad + 31) / 32) {
+        df32x16 acc[2] = {df32x16{}, df32x16{}};
+        mlp_ntile<DWID>(acc, s_hh[1], s_hl[1], DAP, wave, a.wt_h[0], a.wt_l[0]);
+        const int c = 32 * wave + (lane & 31);
+        if (c < C) {
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const int r = row_of(mt, q, hh), g = g0 + r;
+                    if (g >= a.P) continue;
+                    const bool on = (float)s_xh[r * DLP + c] + (float)s_xl[r * DLP + c] > 0.0f;
+                    a.d_lang[(size_t)g * C + c] = (a.residual ? s_v[r][c] : 0.0f) + (on ? acc[mt][q] : 0.0f);
+                }
+        }
+    }
+}
+
+void launch_lang_deform_fwd(const LangDeformArgs& a, hipStream_t st) {
+    if (a.P > 0) hipLaunchKernelGGL(k_lang_deform_fwd, dim3((a.P + DN - 1) / DN), dim3(256), 0, st, a);
+}
+void launch_lang_deform_bwd(const LangDeformArgs& a, hipStream_t st) {
+    if (a.P > 0) hipLaunchKernelGGL(k_lang_deform_bwd, dim3((a.P + DN - 1) / DN), dim3(256), 0, st, a);
 }
 
 // Phase B: C[M][N] += sum_g L[g][m] R[g][n] (M, N <= 128), bias[m] += sum_g L[g][m]; split-K over
@@ -588,42 +941,45 @@ __global__ void k_pack_plane(const float* __restrict__ src, float* __restrict__ 
     dst[i] = src[(size_t)c * H * W + hw];
 }
 
-// fp32 [rows][cols] -> bf16 hi / lo [rows_pad][cols], zero rows past `rows`
+// fp32 [rows][cols] -> bf16 hi / lo [rows_pad][cols_pad], zero past `rows` / `cols`
 __global__ void k_pack_weight(const float* __restrict__ src, __bf16* __restrict__ hi, __bf16* __restrict__ lo,
-                              int rows, int rows_pad, int cols) {
+                              int rows, int rows_pad, int cols, int cols_pad) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= rows_pad * cols) return;
-    const float v = (i / cols) < rows ? src[i] : 0.0f;
+    if (i >= rows_pad * cols_pad) return;
+    const int r = i / cols_pad, c = i - r * cols_pad;
+    const float v = (r < rows && c < cols) ? src[(size_t)r * cols + c] : 0.0f;
     __bf16 h, l;
     dsplit(v, h, l);
     hi[i] = h;
     lo[i] = l;
 }
 
-// fp32 [rows][cols] -> bf16 hi / lo [cols][k_pad], dst[c][r] = src[r][c], zero for r >= rows
+// fp32 [rows][cols] -> bf16 hi / lo [cols_pad][k_pad], dst[c][r] = src[r][c], zero for r >= rows, c >= cols
 __global__ void k_pack_weight_t(const float* __restrict__ src, __bf16* __restrict__ hi, __bf16* __restrict__ lo,
-                                int rows, int cols, int k_pad) {
+                                int rows, int cols, int k_pad, int cols_pad) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= cols * k_pad) return;
+    if (i >= cols_pad * k_pad) return;
     const int c = i / k_pad, r = i - c * k_pad;
-    const float v = r < rows ? src[(size_t)r * cols + c] : 0.0f;
+    const float v = (r < rows && c < cols) ? src[(size_t)r * cols + c] : 0.0f;
     __bf16 h, l;
     dsplit(v, h, l);
     hi[i] = h;
     lo[i] = l;
 }
 
-void launch_pack_weight_t(const float* src, __bf16* hi, __bf16* lo, int rows, int cols, int k_pad, hipStream_t st) {
-    hipLaunchKernelGGL(k_pack_weight_t, dim3((cols * k_pad + 255) / 256), dim3(256), 0, st, src, hi, lo, rows, cols,
-                       k_pad);
+void launch_pack_weight_t(const float* src, __bf16* hi, __bf16* lo, int rows, int cols, int k_pad, int cols_pad,
+                          hipStream_t st) {
+    hipLaunchKernelGGL(k_pack_weight_t, dim3((cols_pad * k_pad + 255) / 256), dim3(256), 0, st, src, hi, lo, rows, cols,
+                       k_pad, cols_pad);
 }
 
 void launch_pack_plane(const float* src, float* dst, int H, int W, hipStream_t st) {
     hipLaunchKernelGGL(k_pack_plane, dim3((H * W * 16 + 255) / 256), dim3(256), 0, st, src, dst, H, W);
 }
-void launch_pack_weight(const float* src, __bf16* hi, __bf16* lo, int rows, int rows_pad, int cols, hipStream_t st) {
-    hipLaunchKernelGGL(k_pack_weight, dim3((rows_pad * cols + 255) / 256), dim3(256), 0, st, src, hi, lo, rows,
-                       rows_pad, cols);
+void launch_pack_weight(const float* src, __bf16* hi, __bf16* lo, int rows, int rows_pad, int cols, int cols_pad,
+                        hipStream_t st) {
+    hipLaunchKernelGGL(k_pack_weight, dim3((rows_pad * cols_pad + 255) / 256), dim3(256), 0, st, src, hi, lo, rows,
+                       rows_pad, cols, cols_pad);
 }
 
 }  // namespace lsr

@@ -16,9 +16,21 @@ namespace {
 
 constexpr int kCombos[6][2] = {{0, 1}, {0, 2}, {0, 3}, {1, 2}, {1, 3}, {2, 3}};
 constexpr int kHeadOut[5] = {3, 3, 4, 1, 48};
-constexpr int kW2Rows = 64;
+constexpr int kW = 128;   // MLP width
 
 size_t align256(size_t x) { return (x + 255) / 256 * 256; }
+int nlayers(const lsr_deform_net* n) { return std::max(n->depth, 1); }
+int head_out(const lsr_deform_net* n, int hd) { return hd < 5 ? kHeadOut[hd] : n->centers; }
+bool head_on(const lsr_deform_net* n, int hd) { return (n->heads >> hd) & 1u; }
+int feat_dim(const lsr_deform_net* n) { return 16 * n->n_scales; }
+int lang_kin(const lsr_deform_net* n) { return n->lang_dim + 1 + 2 * n->time_pe; }
+int lang_kpad(const lsr_deform_net* n) { return (lang_kin(n) + 15) / 16 * 16; }
+bool lang_mlp(const lsr_deform_net* n) {
+    return n->lang_mode == LSR_DEFORM_LANG_RESIDUAL || n->lang_mode == LSR_DEFORM_LANG_NORESNET;
+}
+int lang_in(const lsr_deform_net* n) {
+    return n->lang_mode == LSR_DEFORM_LANG_DISCRETE ? n->lang_dim * n->centers : n->lang_dim;
+}
 
 // plane 6 s + ci: width (along coordinate c0) and height (along c1)
 void plane_dims(const lsr_deform_net* n, int s, int ci, int& W, int& H) {
@@ -27,11 +39,16 @@ void plane_dims(const lsr_deform_net* n, int s, int ci, int& W, int& H) {
     H = res(kCombos[ci][1]);
 }
 
+// one packed bf16 hi / lo pair of `count` elements
+struct Pack {
+    size_t off = 0, count = 0;
+};
 struct Layout {
-    size_t plane_off[12];   // bytes
+    size_t plane_off[24];   // bytes
     size_t planes_end;      // bytes of the packed planes
-    size_t wf, w1, w2;      // bytes: hi arrays, lo right after each
-    size_t wft, w1t, w2t;   // transposed packs for the backward: [32][128], [5][128][128], [5][128][64]
+    Pack wf[LSR_DEFORM_MAX_DEPTH], wft[LSR_DEFORM_MAX_DEPTH];
+    Pack w1[LSR_DEFORM_HEADS], w2[LSR_DEFORM_HEADS], w1t[LSR_DEFORM_HEADS], w2t[LSR_DEFORM_HEADS];
+    Pack wl[3], wlt[3];
     size_t total;
 };
 
@@ -46,21 +63,41 @@ Layout layout(const lsr_deform_net* n) {
             o += align256((size_t)W * H * 16 * sizeof(float));
         }
     L.planes_end = o;
-    const size_t bf = sizeof(__bf16);
-    L.wf = o; o += align256((size_t)128 * 32 * bf) * 2;
-    L.w1 = o; o += align256((size_t)5 * 128 * 128 * bf) * 2;
-    L.w2 = o; o += align256((size_t)5 * kW2Rows * 128 * bf) * 2;
-    L.wft = o; o += align256((size_t)32 * 128 * bf) * 2;
-    L.w1t = o; o += align256((size_t)5 * 128 * 128 * bf) * 2;
-    L.w2t = o; o += align256((size_t)5 * 128 * 64 * bf) * 2;
+    auto take = [&](Pack& p, size_t count) {
+        p.off = o;
+        p.count = count;
+        o += align256(count * sizeof(__bf16)) * 2;
+    };
+    const int F = feat_dim(n), Fpad = (F + 31) / 32 * 32;
+    for (int k = 0; k < nlayers(n); ++k) {
+        take(L.wf[k], (size_t)kW * (k == 0 ? F : kW));          // [128][K_k]
+        take(L.wft[k], (size_t)(k == 0 ? Fpad : kW) * kW);     // [K_k pad 32][128]
+    }
+    for (int hd = 0; hd < LSR_DEFORM_HEADS; ++hd) {
+        if (!head_on(n, hd)) continue;
+        take(L.w1[hd], (size_t)kW * kW);
+        take(L.w2[hd], (size_t)lsr::DEF_W2ROWS * kW);
+        take(L.w1t[hd], (size_t)kW * kW);
+        take(L.w2t[hd], (size_t)kW * 64);
+    }
+    if (lang_mlp(n)) {
+        const int kp = lang_kpad(n);
+        take(L.wl[0], (size_t)kW * kp);
+        take(L.wl[1], (size_t)kW * kW);
+        take(L.wl[2], (size_t)32 * kW);
+        take(L.wlt[0], (size_t)((kp + 31) / 32 * 32) * kW);
+        take(L.wlt[1], (size_t)kW * kW);
+        take(L.wlt[2], (size_t)kW * 32);
+    }
     L.total = o;
     return L;
 }
 
 int check(const lsr_deform_net* n) {
     if (!n) return lsr::fail(LSR_EINVAL, "null deformation net");
-    if (n->n_scales != 2 || n->channels != 16 || n->width != 128)
-        return lsr::fail(LSR_EINVAL, "this build supports the Neu3D structure: 2 scales x 16 channels, width 128");
+    if (n->n_scales < 1 || n->n_scales > LSR_DEFORM_MAX_SCALES || n->channels != 16 || n->width != kW)
+        return lsr::fail(LSR_EINVAL, "supported: 1..4 scales x 16 channels, width 128 (every HyperNeRF / Neu3D config)");
+    if (n->depth < 0 || n->depth > LSR_DEFORM_MAX_DEPTH) return lsr::fail(LSR_EINVAL, "defor_depth must be in [0, 4]");
     for (int c = 0; c < 4; ++c)
         if (n->res[c] < 2) return lsr::fail(LSR_EINVAL, "plane resolutions must be >= 2");
     for (int s = 0; s < n->n_scales; ++s) {
@@ -68,9 +105,26 @@ int check(const lsr_deform_net* n) {
         for (int ci = 0; ci < 6; ++ci)
             if (!n->planes[s][ci]) return lsr::fail(LSR_EINVAL, "missing plane");
     }
-    if (!n->aabb || !n->w_feat || !n->b_feat) return lsr::fail(LSR_EINVAL, "missing aabb / feature_out");
+    if (!n->aabb) return lsr::fail(LSR_EINVAL, "missing aabb");
+    for (int k = 0; k < nlayers(n); ++k)
+        if (!n->w_feat[k] || !n->b_feat[k]) return lsr::fail(LSR_EINVAL, "missing feature_out layer");
+    if (n->lang_mode < LSR_DEFORM_LANG_PASS || n->lang_mode > LSR_DEFORM_LANG_DISCRETE)
+        return lsr::fail(LSR_EINVAL, "unknown language mode");
+    if (n->heads >> LSR_DEFORM_HEADS) return lsr::fail(LSR_EINVAL, "head mask has bits past the 6 heads");
+    if (head_on(n, 5) != (n->lang_mode == LSR_DEFORM_LANG_DISCRETE))
+        return lsr::fail(LSR_EINVAL, "the coff head (bit 5) runs exactly in the discrete language mode");
+    if (n->lang_dim < 0 || n->lang_dim > 32) return lsr::fail(LSR_EINVAL, "lang_dim must be in [0, 32]");
+    if (n->lang_mode == LSR_DEFORM_LANG_DISCRETE && (n->centers < 1 || n->centers > 8 || n->lang_dim < 1))
+        return lsr::fail(LSR_EINVAL, "discrete mode: centers in [1, 8], lang_dim >= 1");
+    if (lang_mlp(n) && (n->lang_dim < 1 || n->time_pe < 0 || lang_kin(n) > 64))
+        return lsr::fail(LSR_EINVAL, "lang_deform: lang_dim >= 1 and 2 time_pe + 1 + lang_dim <= 64");
+    if (n->apply_rotation && !head_on(n, 2)) return lsr::fail(LSR_EINVAL, "apply_rotation needs the rotation head");
     for (int h = 0; h < LSR_DEFORM_HEADS; ++h)
-        if (!n->w1[h] || !n->b1[h] || !n->w2[h] || !n->b2[h]) return lsr::fail(LSR_EINVAL, "missing head weights");
+        if (head_on(n, h) && (!n->w1[h] || !n->b1[h] || !n->w2[h] || !n->b2[h]))
+            return lsr::fail(LSR_EINVAL, "missing head weights");
+    if (lang_mlp(n))
+        for (int k = 0; k < 3; ++k)
+            if (!n->w_lang[k] || !n->b_lang[k]) return lsr::fail(LSR_EINVAL, "missing lang_deform weights");
     return LSR_OK;
 }
 
@@ -94,35 +148,43 @@ extern "C" int lsr_deform_prepare(const lsr_deform_net* net, void* workspace, vo
             plane_dims(net, s, ci, W, H);
             lsr::launch_pack_plane(net->planes[s][ci], reinterpret_cast<float*>(ws + L.plane_off[6 * s + ci]), H, W, st);
         }
-    auto hi_lo = [&](size_t off, size_t count, __bf16*& hi, __bf16*& lo) {
-        hi = reinterpret_cast<__bf16*>(ws + off);
-        lo = reinterpret_cast<__bf16*>(ws + off + align256(count * sizeof(__bf16)));
-    };
-    __bf16 *h, *l;
-    hi_lo(L.wf, 128 * 32, h, l);
-    lsr::launch_pack_weight(net->w_feat, h, l, 128, 128, 32, st);
-    hi_lo(L.w1, 5 * 128 * 128, h, l);
-    for (int hd = 0; hd < 5; ++hd)
-        lsr::launch_pack_weight(net->w1[hd], h + (size_t)hd * 128 * 128, l + (size_t)hd * 128 * 128, 128, 128, 128, st);
-    hi_lo(L.w2, 5 * kW2Rows * 128, h, l);
-    for (int hd = 0; hd < 5; ++hd)
-        lsr::launch_pack_weight(net->w2[hd], h + (size_t)hd * kW2Rows * 128, l + (size_t)hd * kW2Rows * 128,
-                                kHeadOut[hd], kW2Rows, 128, st);
-    // transposed packs (B operands of the backward's data gradients)
-    hi_lo(L.wft, 32 * 128, h, l);
-    lsr::launch_pack_weight_t(net->w_feat, h, l, 128, 32, 128, st);
-    hi_lo(L.w1t, 5 * 128 * 128, h, l);
-    for (int hd = 0; hd < 5; ++hd)
-        lsr::launch_pack_weight_t(net->w1[hd], h + (size_t)hd * 128 * 128, l + (size_t)hd * 128 * 128, 128, 128, 128, st);
-    hi_lo(L.w2t, 5 * 128 * 64, h, l);
-    for (int hd = 0; hd < 5; ++hd)
-        lsr::launch_pack_weight_t(net->w2[hd], h + (size_t)hd * 128 * 64, l + (size_t)hd * 128 * 64, kHeadOut[hd], 128,
-                                  64, st);
+    auto hi = [&](const Pack& p) { return reinterpret_cast<__bf16*>(ws + p.off); };
+    auto lo = [&](const Pack& p) { return reinterpret_cast<__bf16*>(ws + p.off + align256(p.count * sizeof(__bf16))); };
+    const int F = feat_dim(net), Fpad = (F + 31) / 32 * 32;
+    for (int k = 0; k < nlayers(net); ++k) {
+        const int K = k == 0 ? F : kW;
+        lsr::launch_pack_weight(net->w_feat[k], hi(L.wf[k]), lo(L.wf[k]), kW, kW, K, K, st);
+        lsr::launch_pack_weight_t(net->w_feat[k], hi(L.wft[k]), lo(L.wft[k]), kW, K, kW, k == 0 ? Fpad : kW, st);
+    }
+    for (int hd = 0; hd < LSR_DEFORM_HEADS; ++hd) {
+        if (!head_on(net, hd)) continue;
+        const int nout = head_out(net, hd);
+        lsr::launch_pack_weight(net->w1[hd], hi(L.w1[hd]), lo(L.w1[hd]), kW, kW, kW, kW, st);
+        lsr::launch_pack_weight(net->w2[hd], hi(L.w2[hd]), lo(L.w2[hd]), nout, lsr::DEF_W2ROWS, kW, kW, st);
+        lsr::launch_pack_weight_t(net->w1[hd], hi(L.w1t[hd]), lo(L.w1t[hd]), kW, kW, kW, kW, st);
+        lsr::launch_pack_weight_t(net->w2[hd], hi(L.w2t[hd]), lo(L.w2t[hd]), nout, kW, 64, kW, st);
+    }
+    if (lang_mlp(net)) {
+        const int kin = lang_kin(net), kp = lang_kpad(net), C = net->lang_dim;
+        lsr::launch_pack_weight(net->w_lang[0], hi(L.wl[0]), lo(L.wl[0]), kW, kW, kin, kp, st);
+        lsr::launch_pack_weight(net->w_lang[1], hi(L.wl[1]), lo(L.wl[1]), kW, kW, kW, kW, st);
+        lsr::launch_pack_weight(net->w_lang[2], hi(L.wl[2]), lo(L.wl[2]), C, 32, kW, kW, st);
+        lsr::launch_pack_weight_t(net->w_lang[0], hi(L.wlt[0]), lo(L.wlt[0]), kW, kin, kW, (kp + 31) / 32 * 32, st);
+        lsr::launch_pack_weight_t(net->w_lang[1], hi(L.wlt[1]), lo(L.wlt[1]), kW, kW, kW, kW, st);
+        lsr::launch_pack_weight_t(net->w_lang[2], hi(L.wlt[2]), lo(L.wlt[2]), C, kW, 32, kW, st);
+    }
     if (hipGetLastError() != hipSuccess) return lsr::fail(LSR_EHIP, "deformation packing launch failed");
     return LSR_OK;
 }
 
 namespace {
+
+template <typename T>
+const T* chi(const char* ws, const Pack& p) { return reinterpret_cast<const T*>(ws + p.off); }
+template <typename T>
+const T* clo(const char* ws, const Pack& p) {
+    return reinterpret_cast<const T*>(ws + p.off + align256(p.count * sizeof(__bf16)));
+}
 
 // forward kernel arguments common to the forward and the backward (planes, packed weights, biases)
 lsr::DeformArgs forward_args(const lsr_deform_net* net, const void* workspace, int32_t P) {
@@ -130,9 +192,17 @@ lsr::DeformArgs forward_args(const lsr_deform_net* net, const void* workspace, i
     const char* ws = reinterpret_cast<const char*>(workspace);
     lsr::DeformArgs a{};
     a.P = P;
+    a.n_scales = net->n_scales;
+    a.nlayers = nlayers(net);
+    a.heads = net->heads;
+    a.apply_rotation = net->apply_rotation;
+    a.lang_mode = net->lang_mode;
+    a.lang_dim = net->lang_dim;
+    a.centers = net->centers;
+    a.lang_in = lang_in(net);
     a.aabb = net->aabb;
     a.planes = reinterpret_cast<const float*>(ws);
-    for (int s = 0; s < 2; ++s)
+    for (int s = 0; s < net->n_scales; ++s)
         for (int ci = 0; ci < 6; ++ci) {
             int W, H;
             plane_dims(net, s, ci, W, H);
@@ -140,17 +210,34 @@ lsr::DeformArgs forward_args(const lsr_deform_net* net, const void* workspace, i
             a.pw[6 * s + ci] = W;
             a.ph[6 * s + ci] = H;
         }
-    auto hi_lo = [&](size_t off, size_t count, const __bf16*& hi, const __bf16*& lo) {
-        hi = reinterpret_cast<const __bf16*>(ws + off);
-        lo = reinterpret_cast<const __bf16*>(ws + off + align256(count * sizeof(__bf16)));
-    };
-    hi_lo(L.wf, 128 * 32, a.wf_h, a.wf_l);
-    hi_lo(L.w1, 5 * 128 * 128, a.w1_h, a.w1_l);
-    hi_lo(L.w2, 5 * kW2Rows * 128, a.w2_h, a.w2_l);
-    a.b_feat = net->b_feat;
-    for (int hd = 0; hd < 5; ++hd) {
+    for (int k = 0; k < a.nlayers; ++k) {
+        a.wf_h[k] = chi<__bf16>(ws, L.wf[k]);
+        a.wf_l[k] = clo<__bf16>(ws, L.wf[k]);
+        a.b_feat[k] = net->b_feat[k];
+    }
+    for (int hd = 0; hd < LSR_DEFORM_HEADS; ++hd) {
+        if (!head_on(net, hd)) continue;
+        a.w1_h[hd] = chi<__bf16>(ws, L.w1[hd]); a.w1_l[hd] = clo<__bf16>(ws, L.w1[hd]);
+        a.w2_h[hd] = chi<__bf16>(ws, L.w2[hd]); a.w2_l[hd] = clo<__bf16>(ws, L.w2[hd]);
         a.b1[hd] = net->b1[hd];
         a.b2[hd] = net->b2[hd];
+    }
+    return a;
+}
+
+lsr::LangDeformArgs lang_args(const lsr_deform_net* net, const void* workspace, int32_t P) {
+    const Layout L = layout(net);
+    const char* ws = reinterpret_cast<const char*>(workspace);
+    lsr::LangDeformArgs a{};
+    a.P = P;
+    a.lang_dim = net->lang_dim;
+    a.time_pe = net->time_pe;
+    a.kin = lang_kin(net);
+    a.residual = net->lang_mode == LSR_DEFORM_LANG_RESIDUAL;
+    for (int k = 0; k < 3; ++k) {
+        a.w_h[k] = chi<__bf16>(ws, L.wl[k]); a.w_l[k] = clo<__bf16>(ws, L.wl[k]);
+        a.wt_h[k] = chi<__bf16>(ws, L.wlt[k]); a.wt_l[k] = clo<__bf16>(ws, L.wlt[k]);
+        a.b[k] = net->b_lang[k];
     }
     return a;
 }
@@ -158,18 +245,42 @@ lsr::DeformArgs forward_args(const lsr_deform_net* net, const void* workspace, i
 // backward scratch: saved activations, then kGradReplicas copies of the packed gradient planes
 constexpr int kGradReplicas = 16;
 struct BwdScratch {
-    size_t X, A0, dH0, A1, dZ1, dplanes, total;
+    size_t X, A[LSR_DEFORM_MAX_DEPTH], dH[LSR_DEFORM_MAX_DEPTH], A1[LSR_DEFORM_HEADS], dZ1[LSR_DEFORM_HEADS];
+    size_t Grot, Gcoff, U0, U1, U2, dv, dZ2l, dZ1l, dplanes, total;
 };
 BwdScratch bwd_scratch(const lsr_deform_net* net, size_t P) {
     BwdScratch s{};
     size_t o = 0;
     const size_t f = sizeof(float);
-    s.X = o; o += align256(P * 32 * f);
-    s.A0 = o; o += align256(P * 128 * f);
-    s.dH0 = o; o += align256(P * 128 * f);
-    s.A1 = o; o += align256(5 * P * 128 * f);
-    s.dZ1 = o; o += align256(5 * P * 128 * f);
-    s.dplanes = o; o += kGradReplicas * layout(net).planes_end;
+    auto take = [&](size_t floats) {
+        const size_t at = o;
+        o += align256(floats * f);
+        return at;
+    };
+    s.X = take(P * feat_dim(net));
+    for (int k = 0; k < nlayers(net); ++k) {
+        s.A[k] = take(P * kW);
+        s.dH[k] = take(P * kW);
+    }
+    int slot = 0;
+    for (int hd = 0; hd < LSR_DEFORM_HEADS; ++hd) {
+        if (!head_on(net, hd)) continue;
+        s.A1[slot] = take(P * kW);
+        s.dZ1[slot] = take(P * kW);
+        ++slot;
+    }
+    s.Grot = take(net->apply_rotation ? P * 4 : 1);
+    s.Gcoff = take(net->lang_mode == LSR_DEFORM_LANG_DISCRETE ? P * net->centers : 1);
+    if (lang_mlp(net)) {
+        s.U0 = take(P * lang_kin(net));
+        s.U1 = take(P * kW);
+        s.U2 = take(P * kW);
+        s.dv = take(P * net->lang_dim);
+        s.dZ2l = take(P * kW);
+        s.dZ1l = take(P * kW);
+    }
+    s.dplanes = o;
+    o += kGradReplicas * layout(net).planes_end;
     s.total = o;
     return s;
 }
@@ -178,21 +289,40 @@ BwdScratch bwd_scratch(const lsr_deform_net* net, size_t P) {
 
 extern "C" int lsr_deform_forward(const lsr_deform_net* net, const void* workspace, int32_t P, const float* means3D,
                                   const float* scales, const float* rotations, const float* opacity,
-                                  const float* shs, const float* time, float* out_means3D, float* out_scales,
-                                  float* out_rotations, float* out_opacity, float* out_shs, void* stream) {
+                                  const float* shs, const float* lang, const float* time, float* out_means3D,
+                                  float* out_scales, float* out_rotations, float* out_opacity, float* out_shs,
+                                  float* out_lang, float* out_coff, void* stream) {
     int rc = check(net);
     if (rc) return rc;
     if (P < 0) return lsr::fail(LSR_EINVAL, "P must be >= 0");
     if (P == 0) return LSR_OK;
-    if (!workspace || !means3D || !scales || !rotations || !opacity || !shs || !time || !out_means3D ||
-        !out_scales || !out_rotations || !out_opacity || !out_shs)
-        return lsr::fail(LSR_EINVAL, "all inputs, outputs and the workspace are required");
+    const float* ins[5] = {means3D, scales, rotations, opacity, shs};
+    float* outs[5] = {out_means3D, out_scales, out_rotations, out_opacity, out_shs};
+    if (!workspace || !means3D || !time) return lsr::fail(LSR_EINVAL, "workspace, means3D and time are required");
+    for (int hd = 0; hd < 5; ++hd)
+        if (head_on(net, hd) && (!ins[hd] || !outs[hd]))
+            return lsr::fail(LSR_EINVAL, "the input and output of every computed head are required");
+    if (net->lang_mode != LSR_DEFORM_LANG_PASS && (!lang || !out_lang))
+        return lsr::fail(LSR_EINVAL, "lang and out_lang are required unless the language passes through");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     lsr::DeformArgs a = forward_args(net, workspace, P);
     a.means3D = means3D;
     a.time = time;
-    a.in[0] = means3D; a.in[1] = scales; a.in[2] = rotations; a.in[3] = opacity; a.in[4] = shs;
-    a.out[0] = out_means3D; a.out[1] = out_scales; a.out[2] = out_rotations; a.out[3] = out_opacity; a.out[4] = out_shs;
-    lsr::launch_deform_fwd(a, reinterpret_cast<hipStream_t>(stream));
+    a.lang = lang;
+    for (int hd = 0; hd < 5; ++hd) {
+        a.in[hd] = ins[hd];
+        a.out[hd] = outs[hd];
+    }
+    a.out_lang = out_lang;
+    a.out_coff = out_coff;
+    lsr::launch_deform_fwd(a, st);
+    if (lang_mlp(net)) {
+        lsr::LangDeformArgs la = lang_args(net, workspace, P);
+        la.lang = lang;
+        la.time = time;
+        la.out_lang = out_lang;
+        lsr::launch_lang_deform_fwd(la, st);
+    }
     if (hipGetLastError() != hipSuccess) return lsr::fail(LSR_EHIP, "deformation forward launch failed");
     return LSR_OK;
 }
@@ -203,20 +333,33 @@ extern "C" int64_t lsr_deform_backward_scratch_bytes(const lsr_deform_net* net, 
 }
 
 extern "C" int lsr_deform_backward(const lsr_deform_net* net, const void* workspace, int32_t P, const float* means3D,
-                                   const float* time, const float* d_out_means3D, const float* d_out_scales,
-                                   const float* d_out_rotations, const float* d_out_opacity, const float* d_out_shs,
-                                   float* d_means3D, const lsr_deform_grads* grads, void* scratch, void* stream) {
+                                   const float* rotations, const float* lang, const float* time,
+                                   const float* d_out_means3D, const float* d_out_scales, const float* d_out_rotations,
+                                   const float* d_out_opacity, const float* d_out_shs, const float* d_out_lang,
+                                   const float* d_out_coff, float* d_means3D, float* d_rotations, float* d_lang,
+                                   const lsr_deform_grads* grads, void* scratch, void* stream) {
     int rc = check(net);
     if (rc) return rc;
     if (P < 0) return lsr::fail(LSR_EINVAL, "P must be >= 0");
     if (P == 0) return LSR_OK;
-    if (!workspace || !means3D || !time || !d_out_means3D || !d_out_scales || !d_out_rotations || !d_out_opacity ||
-        !d_out_shs || !d_means3D || !grads || !scratch)
-        return lsr::fail(LSR_EINVAL, "inputs, upstream gradients, d_means3D, grads and scratch are required");
-    if (!grads->w_feat || !grads->b_feat) return lsr::fail(LSR_EINVAL, "missing feature_out gradients");
+    const float* ups[5] = {d_out_means3D, d_out_scales, d_out_rotations, d_out_opacity, d_out_shs};
+    if (!workspace || !means3D || !time || !d_out_means3D || !d_means3D || !grads || !scratch)
+        return lsr::fail(LSR_EINVAL, "means3D, time, d_out_means3D, d_means3D, grads, scratch and the workspace are "
+                                     "required");
+    for (int hd = 0; hd < 5; ++hd)
+        if (head_on(net, hd) && !ups[hd]) return lsr::fail(LSR_EINVAL, "the gradient of every computed head's output is required");
+    if (net->apply_rotation && (!rotations || !d_rotations))
+        return lsr::fail(LSR_EINVAL, "apply_rotation: rotations and d_rotations are required");
+    if (net->lang_mode != LSR_DEFORM_LANG_PASS && (!lang || !d_lang))
+        return lsr::fail(LSR_EINVAL, "lang and d_lang are required unless the language passes through");
+    for (int k = 0; k < nlayers(net); ++k)
+        if (!grads->w_feat[k] || !grads->b_feat[k]) return lsr::fail(LSR_EINVAL, "missing feature_out gradients");
     for (int h = 0; h < LSR_DEFORM_HEADS; ++h)
-        if (!grads->w1[h] || !grads->b1[h] || !grads->w2[h] || !grads->b2[h])
+        if (head_on(net, h) && (!grads->w1[h] || !grads->b1[h] || !grads->w2[h] || !grads->b2[h]))
             return lsr::fail(LSR_EINVAL, "missing head gradients");
+    if (lang_mlp(net))
+        for (int k = 0; k < 3; ++k)
+            if (!grads->w_lang[k] || !grads->b_lang[k]) return lsr::fail(LSR_EINVAL, "missing lang_deform gradients");
     for (int s = 0; s < net->n_scales; ++s)
         for (int ci = 0; ci < 6; ++ci)
             if (!grads->planes[s][ci]) return lsr::fail(LSR_EINVAL, "missing plane gradient");
@@ -225,42 +368,78 @@ extern "C" int lsr_deform_backward(const lsr_deform_net* net, const void* worksp
     const BwdScratch S = bwd_scratch(net, (size_t)P);
     char* sc = reinterpret_cast<char*>(scratch);
     const char* ws = reinterpret_cast<const char*>(workspace);
+    auto fp = [&](size_t off) { return reinterpret_cast<float*>(sc + off); };
     lsr::DeformBwdArgs b{};
     b.f = forward_args(net, workspace, P);
     b.f.means3D = means3D;
     b.f.time = time;
-    auto hi_lo = [&](size_t off, size_t count, const __bf16*& hi, const __bf16*& lo) {
-        hi = reinterpret_cast<const __bf16*>(ws + off);
-        lo = reinterpret_cast<const __bf16*>(ws + off + align256(count * sizeof(__bf16)));
-    };
-    hi_lo(L.wft, 32 * 128, b.wft_h, b.wft_l);
-    hi_lo(L.w1t, 5 * 128 * 128, b.w1t_h, b.w1t_l);
-    hi_lo(L.w2t, 5 * 128 * 64, b.w2t_h, b.w2t_l);
-    b.up[0] = d_out_means3D; b.up[1] = d_out_scales; b.up[2] = d_out_rotations; b.up[3] = d_out_opacity;
-    b.up[4] = d_out_shs;
+    b.f.lang = lang;
+    b.f.in[2] = rotations;
+    for (int k = 0; k < b.f.nlayers; ++k) {
+        b.wft_h[k] = chi<__bf16>(ws, L.wft[k]); b.wft_l[k] = clo<__bf16>(ws, L.wft[k]);
+        b.sA[k] = fp(S.A[k]);
+        b.sdH[k] = fp(S.dH[k]);
+    }
+    int slot = 0;
+    for (int hd = 0; hd < LSR_DEFORM_HEADS; ++hd) {
+        if (!head_on(net, hd)) continue;
+        b.w1t_h[hd] = chi<__bf16>(ws, L.w1t[hd]); b.w1t_l[hd] = clo<__bf16>(ws, L.w1t[hd]);
+        b.w2t_h[hd] = chi<__bf16>(ws, L.w2t[hd]); b.w2t_l[hd] = clo<__bf16>(ws, L.w2t[hd]);
+        b.sA1[slot] = fp(S.A1[slot]);
+        b.sdZ1[slot] = fp(S.dZ1[slot]);
+        ++slot;
+    }
+    for (int hd = 0; hd < 5; ++hd) b.up[hd] = ups[hd];
+    b.up_lang = d_out_lang;
+    b.up_coff = d_out_coff;
     b.d_means3D = d_means3D;
-    b.dplanes = reinterpret_cast<float*>(sc + S.dplanes);
-    b.sX = reinterpret_cast<float*>(sc + S.X);
-    b.sA0 = reinterpret_cast<float*>(sc + S.A0);
-    b.sdH0 = reinterpret_cast<float*>(sc + S.dH0);
-    b.sA1 = reinterpret_cast<float*>(sc + S.A1);
-    b.sdZ1 = reinterpret_cast<float*>(sc + S.dZ1);
+    b.d_rotations = d_rotations;
+    b.d_lang = d_lang;
+    b.sX = fp(S.X);
+    b.sG_rot = fp(S.Grot);
+    b.sG_coff = fp(S.Gcoff);
+    b.dplanes = fp(S.dplanes);
     b.replicas = kGradReplicas;
     b.plane_stride = (int64_t)(L.planes_end / sizeof(float));
     if (hipMemsetAsync(b.dplanes, 0, kGradReplicas * L.planes_end, st) != hipSuccess) return lsr::fail(LSR_EHIP, "memset");
     lsr::launch_deform_bwd_a(b, st);
-    // weight gradients: 5 x (dW1, dW2) + feature_out, split-K over ~256 row blocks
+    lsr::LangDeformArgs la{};
+    if (lang_mlp(net)) {
+        la = lang_args(net, workspace, P);
+        la.lang = lang;
+        la.time = time;
+        la.up_lang = d_out_lang;
+        la.d_lang = d_lang;
+        la.sU0 = fp(S.U0); la.sU1 = fp(S.U1); la.sU2 = fp(S.U2);
+        la.sdv = fp(S.dv); la.sdZ2 = fp(S.dZ2l); la.sdZ1 = fp(S.dZ1l);
+        lsr::launch_lang_deform_bwd(la, st);
+    }
+    // weight gradients, split-K over ~256 row blocks: the feature_out chain, every computed head,
+    // and lang_deform
     lsr::AtbArgs g{};
     g.P = P;
     const int64_t per = ((int64_t)P + 255) / 256;
     g.rows_per_block = (int)std::max<int64_t>(64, (per + 63) / 64 * 64);
-    const size_t PW = (size_t)P * 128;
-    for (int hd = 0; hd < 5; ++hd) {
-        g.job[hd] = lsr::AtbJob{b.sdZ1 + hd * PW, b.sA0, grads->w1[hd], grads->b1[hd], 128, 128};
-        g.job[5 + hd] = lsr::AtbJob{b.up[hd], b.sA1 + hd * PW, grads->w2[hd], grads->b2[hd], kHeadOut[hd], 128};
+    int nj = 0;
+    const int F = feat_dim(net);
+    for (int k = 0; k < b.f.nlayers; ++k)
+        g.job[nj++] = lsr::AtbJob{b.sdH[k], k == 0 ? b.sX : b.sA[k - 1], grads->w_feat[k], grads->b_feat[k], kW,
+                                  k == 0 ? F : kW};
+    slot = 0;
+    const float* last = b.sA[b.f.nlayers - 1];
+    for (int hd = 0; hd < LSR_DEFORM_HEADS; ++hd) {
+        if (!head_on(net, hd)) continue;
+        const float* G = hd == 5 ? b.sG_coff : (hd == 2 && net->apply_rotation) ? b.sG_rot : ups[hd];
+        g.job[nj++] = lsr::AtbJob{b.sdZ1[slot], last, grads->w1[hd], grads->b1[hd], kW, kW};
+        g.job[nj++] = lsr::AtbJob{G, b.sA1[slot], grads->w2[hd], grads->b2[hd], head_out(net, hd), kW};
+        ++slot;
     }
-    g.job[10] = lsr::AtbJob{b.sdH0, b.sX, grads->w_feat, grads->b_feat, 128, 32};
-    lsr::launch_atb(g, 11, st);
+    if (lang_mlp(net)) {
+        g.job[nj++] = lsr::AtbJob{la.sdZ1, la.sU0, grads->w_lang[0], grads->b_lang[0], kW, la.kin};
+        g.job[nj++] = lsr::AtbJob{la.sdZ2, la.sU1, grads->w_lang[1], grads->b_lang[1], kW, kW};
+        g.job[nj++] = lsr::AtbJob{la.sdv, la.sU2, grads->w_lang[2], grads->b_lang[2], net->lang_dim, kW};
+    }
+    lsr::launch_atb(g, nj, st);
     for (int s = 0; s < net->n_scales; ++s)
         for (int ci = 0; ci < 6; ++ci) {
             int W, H;

@@ -224,8 +224,7 @@ int lsr_knn_mean_dist(int32_t P, const float* points, float* mean_dist, void* wo
     hipLaunchKernelGGL(k_bbox_partial, dim3(nred), dim3(256), 0, st, P, points, w.partial);
     hipLaunchKernelGGL(k_bbox_final, dim3(1), dim3(256), 0, st, nred, (const Bounds*)w.partial, w.bbox);
     hipLaunchKernelGGL(k_morton, dim3(nblk), dim3(256), 0, st, P, points, (const Bounds*)w.bbox, w.code_a, w.idx_a);
-    const bool in_b = lsr::radix_sort_pairs(w.code_a, w.idx_a, w.code_b, w.idx_b, (size_t)P, 0, 30, w.sort_tmp,
-                                            nullptr, st);
+    const bool in_b = lsr::radix_sort_pairs(w.code_a, w.idx_a, w.code_b, w.idx_b, (size_t)P, 0, 30, w.sort_tmp, st);
     const uint32_t* idx = in_b ? w.idx_b : w.idx_a;
     hipLaunchKernelGGL(k_gather_sorted, dim3(nblk), dim3(256), 0, st, P, points, idx, w.sp);
     hipLaunchKernelGGL(k_box_bounds, dim3(nbox), dim3(256), 0, st, P, (const float4*)w.sp, w.boxes);

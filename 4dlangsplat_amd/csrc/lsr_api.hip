@@ -19,7 +19,7 @@
 namespace {
 
 thread_local std::string g_err;
-std::atomic<uint32_t> g_inject_sort_fault{0};   // lsr_test_inject_sort_fault
+std::atomic<int32_t> g_caller_api{0};   // lsr_require_api: the lsr.h version the caller was built against
 
 int fail(int code, const std::string& msg) {
     g_err = msg;
@@ -203,6 +203,9 @@ bool tile_sort_in_b(int ntiles) { return ((tile_bits(ntiles) + 7) / 8) % 2 == 1;
 int depth_sort_result_in_b() { return 0; }  // 32 key bits = 4 passes: result back in the (a) buffers
 
 int check_common(const lsr_settings* s, const lsr_fwd_in* in) {
+    if (g_caller_api.load() != LSR_API_VERSION)   // the structs' layout is that of this lsr.h only
+        return fail(LSR_EINVAL, "call lsr_require_api(LSR_API_VERSION) first: the caller must be built against lsr.h "
+                                "version " + std::to_string(LSR_API_VERSION));
     if (!s || !in) return fail(LSR_EINVAL, "null settings or inputs");
     if (s->image_width <= 0 || s->image_height <= 0) return fail(LSR_EINVAL, "image size must be positive");
     if (s->image_width > 4095 * LSR_TILE_X || s->image_height > 4095 * LSR_TILE_Y)
@@ -240,10 +243,9 @@ void preprocess_shared(lsr::PreprocessArgs& a, const lsr_settings* s, const lsr_
     a.shs = in->shs; a.colors_precomp = in->colors_precomp; a.cov3D_precomp = in->cov3D_precomp;
 }
 // One view's camera and outputs.  The preprocess also writes the depth sort's initial values
-// (ids), zeroes the split-backward accumulator rows of listed Gaussians, and clears the sort
-// workspace and the counters [0] K, [1] depth sort error word, [2] tile sort error word: no
-// separate fill launches.
-void preprocess_view(lsr::PreprocessView& v, const lsr_settings* s, const Geom& g, int* radii, int P) {
+// (ids), zeroes the split-backward accumulator rows of listed Gaussians, and clears the counters
+// [0] K, [1..2] reserved (reported as 0), [3] visible count: no separate fill launches.
+void preprocess_view(lsr::PreprocessView& v, const lsr_settings* s, const Geom& g, int* radii) {
     v.tanfovx = s->tanfovx; v.tanfovy = s->tanfovy;
     v.focal_x = (float)s->image_width / (2.0f * s->tanfovx);
     v.focal_y = (float)s->image_height / (2.0f * s->tanfovy);
@@ -251,12 +253,10 @@ void preprocess_view(lsr::PreprocessView& v, const lsr_settings* s, const Geom& 
     v.radii = radii; v.radius = g.radius; v.tiles = g.tiles; v.rect = g.rect; v.key = g.key_a; v.xy = g.xy;
     v.conic_o = g.conic_o; v.rgbd = g.rgbd; v.clamped = g.clamped;
     v.order = g.val_a;
-    v.rank_counts = lsr::radix_sort_fuses_gather() ? g.counts : nullptr;
+    v.rank_counts = g.counts;
     v.acc = g.acc;
-    v.clear.p[0] = reinterpret_cast<uint32_t*>(g.sort_tmp);
-    v.clear.n[0] = (uint32_t)(lsr::radix_temp_zero_bytes((size_t)P, 0, 32) / 4);
-    v.clear.p[1] = g.total;
-    v.clear.n[1] = 3;
+    v.clear.p[0] = g.total;
+    v.clear.n[0] = 4;
 }
 
 }  // namespace
@@ -264,6 +264,13 @@ void preprocess_view(lsr::PreprocessView& v, const lsr_settings* s, const Geom& 
 extern "C" {
 
 int lsr_version(void) { return LSR_API_VERSION; }
+int lsr_require_api(int32_t caller_version) {
+    if (caller_version != LSR_API_VERSION)
+        return fail(LSR_EINVAL, "lsr.h version mismatch: caller " + std::to_string(caller_version) + ", library " +
+                                    std::to_string(LSR_API_VERSION));
+    g_caller_api.store(caller_version);
+    return LSR_OK;
+}
 const char* lsr_last_error(void) { return g_err.c_str(); }
 
 int64_t lsr_geom_bytes(int32_t P) {
@@ -304,7 +311,7 @@ int lsr_forward_preprocess_async(const lsr_settings* s, const lsr_fwd_in* in, ls
     lsr::PreprocessArgs a{};
     preprocess_shared(a, s, in);
     a.nv = 1;
-    preprocess_view(a.v[0], s, g, out->radii, P);
+    preprocess_view(a.v[0], s, g, out->radii);
     {
         PhaseTimer t(LSR_PHASE_PREPROCESS, st);
         lsr::launch_preprocess(a, st);
@@ -319,16 +326,13 @@ int lsr_forward_preprocess_async(const lsr_settings* s, const lsr_fwd_in* in, ls
         // ... and its last pass writes the depth-ranked rectangles and instance counts (the ranks
         // of culled Gaussians keep the zero counts the preprocess wrote)
         const lsr::SortGather gather{g.rect, g.counts, g.rect_sorted};
-        in_b = lsr::radix_sort_pairs(g.key_a, g.val_a, g.key_b, g.val_b, (size_t)P, 0, 32, g.sort_tmp, g.total + 1, st,
-                                     /*temp_zeroed=*/true, g.total + 3, &gather);
+        in_b = lsr::radix_sort_pairs(g.key_a, g.val_a, g.key_b, g.val_b, (size_t)P, 0, 32, g.sort_tmp, st, g.total + 3,
+                                     &gather);
     }
     if (in_b != (bool)depth_sort_result_in_b()) return fail(LSR_EHIP, "internal: depth sort parity");
-    if (g_inject_sort_fault.load() & 1u) LSR_HIP(hipMemsetAsync(g.total + 1, 1, 1, st));   // test hook
     LSR_LAUNCHED("depth sort", st, s->debug);
     {
         PhaseTimer t(LSR_PHASE_INSTANCE_SCAN, st);
-        if (!lsr::radix_sort_fuses_gather())
-            lsr::launch_gather_tile_counts(P, g.total + 3, g.val_a, g.rect, g.counts, g.rect_sorted, st);
         lsr::exclusive_scan_u32(g.counts, g.offsets, (size_t)P, g.total, g.scan_tmp, st);
     }
     LSR_LAUNCHED("instance scan", st, s->debug);
@@ -341,13 +345,6 @@ int lsr_forward_preprocess_views_async(int32_t n_views, const lsr_settings* cons
                                        lsr_stream_t stream) {
     if (n_views < 1 || !s || !out || !geom || !host_counts)
         return fail(LSR_EINVAL, "n_views >= 1 and the per-view arrays and host_counts are required");
-    if (!lsr::radix_sort_fuses_gather()) {   // look-back build: the per-view path
-        for (int v = 0; v < n_views; ++v) {
-            int rc = lsr_forward_preprocess_async(s[v], in, out[v], geom[v], host_counts + 2 * v, stream);
-            if (rc) return rc;
-        }
-        return LSR_OK;
-    }
     for (int v = 0; v < n_views; ++v) {
         int rc = check_common(s[v], in);
         if (rc) return rc;
@@ -380,15 +377,15 @@ int lsr_forward_preprocess_views_async(int32_t n_views, const lsr_settings* cons
         lsr::ScanSeg sc[lsr::LSR_MAX_VIEWS] = {};
         for (int k = 0; k < nv; ++k) {
             Geom g = carve_geom(geom[v0 + k], (size_t)P, nullptr);
-            preprocess_view(a.v[k], s[v0 + k], g, out[v0 + k]->radii, P);
+            preprocess_view(a.v[k], s[v0 + k], g, out[v0 + k]->radii);
             // depth order of the visible Gaussians (the first pass drops culled keys, kept count in
             // g.total[3]; the last pass writes the depth-ranked rectangles and instance counts)
             ss[k] = lsr::SortSeg{g.key_a, g.val_a, g.key_b, g.val_b, g.sort_tmp, g.total + 3,
                                  lsr::SortGather{g.rect, g.counts, g.rect_sorted}, (size_t)P};
             sc[k] = lsr::ScanSeg{g.counts, g.offsets, g.total, reinterpret_cast<uint32_t*>(g.scan_tmp), (size_t)P};
-            if (mapped) {   // the scan writes {K, error word} straight to the caller's pinned words
-                sc[k].host_total = mapped + 2 * (v0 + k);
-                sc[k].err = g.total + 1;
+            if (mapped) {   // the scan writes K straight to the caller's pinned word (the preprocess
+                sc[k].host_total = mapped + 2 * (v0 + k);   // zeroed a view's reserved word only on the
+                host_counts[2 * (v0 + k) + 1] = 0;           // device: the host clears it here)
             }
         }
         {
@@ -402,9 +399,6 @@ int lsr_forward_preprocess_views_async(int32_t n_views, const lsr_settings* cons
                 return fail(LSR_EHIP, "internal: depth sort parity");
         }
         LSR_LAUNCHED("depth sort", st, s[v0]->debug);
-        if (g_inject_sort_fault.load() & 1u)   // test hook (error word g.total[1], read by the scan below)
-            for (int k = 0; k < nv; ++k)
-                LSR_HIP(hipMemsetAsync(carve_geom(geom[v0 + k], (size_t)P, nullptr).total + 1, 1, 1, st));
         uint32_t wrote;
         {
             PhaseTimer t(LSR_PHASE_INSTANCE_SCAN, st);
@@ -428,7 +422,6 @@ int lsr_forward_preprocess(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_
     int rc = lsr_forward_preprocess_async(s, in, out, geom, tot, stream);
     if (rc) return rc;
     LSR_HIP(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
-    if (tot[1]) return fail(LSR_EHIP, "depth sort: look-back timed out");
     *num_rendered = (int64_t)tot[0];
     return LSR_OK;
 }
@@ -461,7 +454,7 @@ int lsr_forward_binning_views(int32_t n_views, const lsr_settings* const* s, con
         eb.P = P; eb.grid_x = gx; eb.grid_y = gy; eb.W = W; eb.H = H;
         lsr::SortSeg ss[lsr::LSR_MAX_VIEWS] = {};
         lsr::RangesSeg rs[lsr::LSR_MAX_VIEWS] = {};
-        int ne = 0, ev_view[lsr::LSR_MAX_VIEWS];
+        int ne = 0;
         for (int k = 0; k < nv; ++k) {
             const int v = v0 + k;
             const size_t K = (size_t)num_rendered[v];
@@ -473,8 +466,8 @@ int lsr_forward_binning_views(int32_t n_views, const lsr_settings* const* s, con
                 continue;
             }
             Binning b = carve_binning(binning[v], K, nullptr);
-            // the emission also clears the tile ranges, the per-tile replay bounds and the tile
-            // sort's workspace (no separate fill launches)
+            // the emission also clears the tile ranges and the per-tile replay bounds (no separate
+            // fill launches)
             lsr::EmitView& e = eb.v[ne];
             e.order = g.val_a; e.offsets = g.offsets; e.counts = g.counts; e.rect_sorted = g.rect_sorted;
             e.xy = g.xy; e.conic_o = g.conic_o; e.keys = b.key_a; e.vals = b.val_a;
@@ -482,12 +475,9 @@ int lsr_forward_binning_views(int32_t n_views, const lsr_settings* const* s, con
             e.clear.n[0] = (uint32_t)(2 * ntiles);
             e.clear.p[1] = m.tile_max;
             e.clear.n[1] = (uint32_t)ntiles;
-            e.clear.p[2] = reinterpret_cast<uint32_t*>(b.sort_tmp);
-            e.clear.n[2] = (uint32_t)(lsr::radix_temp_zero_bytes(K, 0, tbits) / 4);
             ss[ne] = lsr::SortSeg{b.key_a, b.val_a, b.key_b, b.val_b, b.sort_tmp, nullptr,
                                   lsr::SortGather{nullptr, nullptr, nullptr}, K};
-            rs[ne] = lsr::RangesSeg{K, tile_sort_in_b((int)ntiles) ? b.key_b : b.key_a, m.ranges};
-            ev_view[ne++] = v;
+            rs[ne++] = lsr::RangesSeg{K, tile_sort_in_b((int)ntiles) ? b.key_b : b.key_a, m.ranges};
         }
         if (ne == 0) continue;
         {
@@ -497,21 +487,9 @@ int lsr_forward_binning_views(int32_t n_views, const lsr_settings* const* s, con
         LSR_LAUNCHED("emit", st, s[0]->debug);
         {
             PhaseTimer t(LSR_PHASE_TILE_SORT, st);
-            bool in_b = true;
-            if (lsr::radix_sort_fuses_gather()) {   // reduce-then-scan: one set of launches for all views
-                in_b = lsr::radix_sort_batch(ss, ne, 0, tbits, st);
-            } else {                                // look-back build: per view, error word g.total[2]
-                for (int k = 0; k < ne; ++k) {
-                    Geom g = carve_geom(geom[ev_view[k]], (size_t)P, nullptr);
-                    in_b = lsr::radix_sort_pairs(ss[k].keys_a, ss[k].vals_a, ss[k].keys_b, ss[k].vals_b, ss[k].n, 0,
-                                                 tbits, ss[k].temp, g.total + 2, st, /*temp_zeroed=*/true);
-                }
-            }
+            const bool in_b = lsr::radix_sort_batch(ss, ne, 0, tbits, st);   // one set of launches for all views
             if (in_b != tile_sort_in_b((int)ntiles)) return fail(LSR_EHIP, "internal: tile sort parity");
         }
-        if (g_inject_sort_fault.load() & 2u)   // test hook: error word g.total[2] (cleared by the preprocess)
-            for (int k = 0; k < nv; ++k)
-                LSR_HIP(hipMemsetAsync(carve_geom(geom[v0 + k], (size_t)P, nullptr).total + 2, 1, 1, st));
         LSR_LAUNCHED("tile sort", st, s[0]->debug);
         {
             PhaseTimer t(LSR_PHASE_TILE_RANGES, st);
@@ -543,13 +521,6 @@ int lsr_forward_composite(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_o
     r.lang = in->language_feature;
     r.lang_split = in->C == 32 ? in->language_feature_split : nullptr; r.bg = s->bg; r.final_T = m.final_T; r.n_contrib = m.n_contrib;
     r.tile_max_contrib = m.tile_max; r.tile_order = m.tile_order;
-    r.sort_err = P > 0 ? g.total + 1 : nullptr;
-    if (out->host_sort_status) {
-        void* dptr = nullptr;
-        if (hipHostGetDevicePointer(&dptr, out->host_sort_status, 0) != hipSuccess || !dptr)
-            return fail(LSR_EINVAL, "host_sort_status must be page-locked host memory");
-        r.status_out = static_cast<uint32_t*>(dptr);
-    }
     r.out_color = out->out_color; r.out_lang = out->out_language_feature;
     r.out_depth = out->out_depth;
     if (C > 0 && !s->include_feature)
@@ -562,18 +533,6 @@ int lsr_forward_composite(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_o
     return LSR_OK;
 }
 
-int lsr_forward_status(int32_t P, const void* geom, uint32_t* host_status, lsr_stream_t stream) {
-    if (P < 0 || !geom || !host_status) return fail(LSR_EINVAL, "bad lsr_forward_status arguments");
-    if (P == 0) {
-        host_status[0] = host_status[1] = 0;
-        return LSR_OK;
-    }
-    Geom g = carve_geom(const_cast<void*>(geom), (size_t)P, nullptr);
-    LSR_HIP(hipMemcpyAsync(host_status, g.total + 1, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                           reinterpret_cast<hipStream_t>(stream)));
-    return LSR_OK;
-}
-
 int lsr_language_split(int32_t P, int32_t C, const float* language_feature, uint16_t* out, lsr_stream_t stream) {
     if (P < 0 || C != 32 || (P > 0 && (!language_feature || !out)))
         return fail(LSR_EINVAL, "lsr_language_split: P >= 0, C == 32 and both buffers are required");
@@ -581,11 +540,6 @@ int lsr_language_split(int32_t P, int32_t C, const float* language_feature, uint
     if (P == 0) return LSR_OK;
     lsr::launch_language_split(P, language_feature, out, reinterpret_cast<hipStream_t>(stream));
     LSR_LAUNCHED("language split", reinterpret_cast<hipStream_t>(stream), false);
-    return LSR_OK;
-}
-
-int lsr_test_inject_sort_fault(uint32_t mask) {
-    g_inject_sort_fault.store(mask & 3u);
     return LSR_OK;
 }
 
@@ -713,6 +667,13 @@ int lsr_backward_composite(const lsr_settings* s, const lsr_fwd_in* in, const ls
 int lsr_backward_preprocess_views(int32_t n_views, const lsr_settings* const* s, const lsr_fwd_in* in,
                                   lsr_bwd_out* gout, const void* const* geom, int32_t accumulate,
                                   lsr_stream_t stream) {
+    if (!in) return fail(LSR_EINVAL, "null argument");
+    return lsr_backward_preprocess_views_rows(n_views, s, in, gout, geom, accumulate, 0, in->P, stream);
+}
+
+int lsr_backward_preprocess_views_rows(int32_t n_views, const lsr_settings* const* s, const lsr_fwd_in* in,
+                                       lsr_bwd_out* gout, const void* const* geom, int32_t accumulate,
+                                       int32_t row_begin, int32_t row_count, lsr_stream_t stream) {
     if (n_views < 1) return fail(LSR_EINVAL, "n_views must be >= 1");
     if (!s || !in || !gout || !geom) return fail(LSR_EINVAL, "null argument");
     for (int v = 0; v < n_views; ++v) {
@@ -721,16 +682,25 @@ int lsr_backward_preprocess_views(int32_t n_views, const lsr_settings* const* s,
         if (!geom[v]) return fail(LSR_EINVAL, "the geom workspace is required for every view");
         if (s[v]->scale_modifier != s[0]->scale_modifier) return fail(LSR_EINVAL, "all views must share scale_modifier");
     }
+    if (row_begin < 0 || row_count < 0 || (int64_t)row_begin + row_count > in->P)
+        return fail(LSR_EINVAL, "rows [row_begin, row_begin + row_count) must lie inside [0, P)");
+    if (row_begin % 256 != 0) return fail(LSR_EINVAL, "row_begin must be a multiple of 256");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const int P = in->P;
-    if (P == 0) return LSR_OK;
-    // one launch per LSR_MAX_VIEWS views: Gaussian rows read and gradient rows written once
+    const int P = in->P, n = row_count;
+    const size_t r0 = (size_t)row_begin;
+    if (n == 0) return LSR_OK;
+    const int M = in->M;
+    // one launch per LSR_MAX_VIEWS views: Gaussian rows read and gradient rows written once; a row
+    // range is the same kernel over pointers advanced to row_begin (gout already addresses it)
     for (int v0 = 0; v0 < n_views; v0 += lsr::LSR_MAX_VIEWS) {
         const int nv = std::min(lsr::LSR_MAX_VIEWS, n_views - v0);
         lsr::PreprocessBwdViewsArgs a{};
-        a.P = P; a.M = in->M; a.nv = nv; a.scale_modifier = s[0]->scale_modifier;
-        a.means3D = in->means3D; a.scales = in->scales; a.rotations = in->rotations; a.shs = in->shs;
-        a.cov3D_precomp = in->cov3D_precomp;
+        a.P = n; a.M = M; a.nv = nv; a.scale_modifier = s[0]->scale_modifier;
+        a.means3D = in->means3D + 3 * r0;
+        a.scales = in->scales ? in->scales + 3 * r0 : nullptr;
+        a.rotations = in->rotations ? in->rotations + 4 * r0 : nullptr;
+        a.shs = in->shs ? in->shs + (size_t)M * 3 * r0 : nullptr;
+        a.cov3D_precomp = in->cov3D_precomp ? in->cov3D_precomp + 6 * r0 : nullptr;
         for (int j = 0; j < nv; ++j) {
             const int v = v0 + j;
             const lsr_settings* sv = s[v];
@@ -741,7 +711,8 @@ int lsr_backward_preprocess_views(int32_t n_views, const lsr_settings* const* s,
             c.focal_x = (float)sv->image_width / (2.0f * sv->tanfovx);
             c.focal_y = (float)sv->image_height / (2.0f * sv->tanfovy);
             c.deg = sv->sh_degree;
-            c.tiles = g.tiles; c.clamped = g.clamped; c.acc_small = reinterpret_cast<const float*>(g.acc);
+            c.tiles = g.tiles + r0; c.clamped = g.clamped + r0;
+            c.acc_small = reinterpret_cast<const float*>(g.acc) + lsr::ACC_PITCH * r0;
         }
         a.dopacity = gout->dL_dopacity;
         a.dmeans3D = gout->dL_dmeans3D; a.dmeans2D = gout->dL_dmeans2D; a.dcolors = gout->dL_dcolors;

@@ -180,9 +180,6 @@ struct RenderFwdArgs {
     uint32_t* n_contrib;
     uint32_t* tile_max_contrib;   // per tile: max n_contrib over its pixels (bounds the backward replay)
     uint32_t* tile_order;         // [tiles] scratch: longest-list-first launch order (null: tile order)
-    const uint32_t* sort_err;     // [2] depth / tile sort look-back timeouts (null: none): NaN outputs
-    uint32_t* status_out;         // [2] host-mapped (device address of pinned memory) or null: block 0
-                                  //     stores sort_err there
     float* out_color;
     float* out_lang;
     float* out_depth;
@@ -223,43 +220,67 @@ struct RenderBwdArgs {
 inline int lang_pad(int C) { return C == 0 ? 0 : C <= 4 ? 4 : C <= 8 ? 8 : C <= 16 ? 16 : C <= 32 ? 32 : 64; }
 inline int record_floats(int C) { return 12 + lang_pad(C); }
 
-// deformation field forward (deform.hip)
+// deformation field (deform.hip; include/lsr_deform.h)
+constexpr int DEF_MAX_LAYERS = 4;     // feature_out Linear layers
+constexpr int DEF_HEADS = 6;          // pos, scales, rotations, opacity, shs, coff
+constexpr int DEF_W2ROWS = 64;        // output rows of every head's last layer, zero padded
+constexpr int DEF_LANG_MODE_PASS = 0, DEF_LANG_MODE_RESIDUAL = 1, DEF_LANG_MODE_NORESNET = 2,
+              DEF_LANG_MODE_DISCRETE = 3;
 struct DeformArgs {
     int P;
+    int n_scales, nlayers;
+    uint32_t heads;                   // bit h: head h computed
+    int apply_rotation, lang_mode, lang_dim, centers, lang_in;   // lang_in: input lang channels
     const float* means3D;
     const float* time;
     const float* aabb;                // [2][3] device: xyz_max, xyz_min
     const float* planes;              // packed channel-last planes
-    int64_t poff[12];                 // float offset of plane 6 s + ci
-    int pw[12], ph[12];               // its width / height
-    const __bf16 *wf_h, *wf_l;        // [128][32]
-    const __bf16 *w1_h, *w1_l;        // [5][128][128]
-    const __bf16 *w2_h, *w2_l;        // [5][64][128] (rows past the head's outputs are zero)
-    const float* b_feat;
-    const float* b1[5];
-    const float* b2[5];
+    int64_t poff[24];                 // float offset of plane 6 s + ci
+    int pw[24], ph[24];               // its width / height
+    const __bf16 *wf_h[DEF_MAX_LAYERS], *wf_l[DEF_MAX_LAYERS];   // layer k: [128][K_k], K_0 = 16 n_scales
+    const __bf16 *w1_h[DEF_HEADS], *w1_l[DEF_HEADS];             // [128][128]
+    const __bf16 *w2_h[DEF_HEADS], *w2_l[DEF_HEADS];             // [DEF_W2ROWS][128]
+    const float* b_feat[DEF_MAX_LAYERS];
+    const float* b1[DEF_HEADS];
+    const float* b2[DEF_HEADS];
     const float* in[5];               // means3D, scales, rotations, opacity, shs
+    const float* lang;                // [P, lang_in]
     float* out[5];
+    float* out_lang;                  // DISCRETE: [P, lang_dim]
+    float* out_coff;                  // DISCRETE: [P, centers] or null
 };
 void launch_deform_fwd(const DeformArgs& a, hipStream_t st);
 void launch_pack_plane(const float* src, float* dst, int H, int W, hipStream_t st);
-void launch_pack_weight(const float* src, __bf16* hi, __bf16* lo, int rows, int rows_pad, int cols, hipStream_t st);
-// transposed packing: src fp32 [rows][cols] -> hi / lo [cols][k_pad] with dst[c][r] = src[r][c], zero for r >= rows
-void launch_pack_weight_t(const float* src, __bf16* hi, __bf16* lo, int rows, int cols, int k_pad, hipStream_t st);
+void launch_pack_weight(const float* src, __bf16* hi, __bf16* lo, int rows, int rows_pad, int cols, int cols_pad,
+                        hipStream_t st);
+// transposed packing: src fp32 [rows][cols] -> hi / lo [cols_pad][k_pad] with dst[c][r] = src[r][c],
+// zero for r >= rows or c >= cols
+void launch_pack_weight_t(const float* src, __bf16* hi, __bf16* lo, int rows, int cols, int k_pad, int cols_pad,
+                          hipStream_t st);
 
 // deformation backward (deform.hip): phase A per 64 Gaussians (recompute, data gradients, plane
 // scatter, saved activations), phase B the weight gradients as split-K A^T B products
 struct DeformBwdArgs {
-    DeformArgs f;                     // planes, packed weights, biases, means3D, time, aabb
-    const __bf16 *w1t_h, *w1t_l;      // [5][128 in][128 out]
-    const __bf16 *w2t_h, *w2t_l;      // [5][128 in][64 out, zero padded]
-    const __bf16 *wft_h, *wft_l;      // [32 feat][128 hidden]
-    const float* up[5];               // gradients of the five outputs
+    DeformArgs f;                     // planes, packed weights, biases, means3D, time, aabb, lang, in[2]
+    const __bf16 *wft_h[DEF_MAX_LAYERS], *wft_l[DEF_MAX_LAYERS];   // layer k transposed: [K_k pad 32][128]
+    const __bf16 *w1t_h[DEF_HEADS], *w1t_l[DEF_HEADS];             // [128 in][128 out]
+    const __bf16 *w2t_h[DEF_HEADS], *w2t_l[DEF_HEADS];             // [128 in][64 out, zero padded]
+    const float* up[5];               // gradients of the five outputs (null: head off)
+    const float* up_lang;             // DISCRETE: [P, lang_dim] or null
+    const float* up_coff;             // DISCRETE: [P, centers] or null
     float* d_means3D;
+    float* d_rotations;               // apply_rotation: [P, 4]
+    float* d_lang;                    // DISCRETE: [P, lang_in]
     float* dplanes;                   // packed channel-last gradient planes (same offsets as f.planes),
     int64_t plane_stride;             //   `replicas` copies plane_stride floats apart (block b adds
     int replicas;                     //   into copy b % replicas; the unpack sums them)
-    float *sX, *sA0, *sdH0, *sA1, *sdZ1;   // saved: [P,32], [P,128], [P,128], [5][P,128], [5][P,128]
+    float* sX;                        // saved [P, 16 n_scales] features
+    float* sA[DEF_MAX_LAYERS];        // saved [P,128] relu(H_k)
+    float* sdH[DEF_MAX_LAYERS];       // saved [P,128] gradients of H_k
+    float* sA1[DEF_HEADS];            // per computed head: [P,128] relu(Z1)
+    float* sdZ1[DEF_HEADS];           //                    [P,128] gradient of Z1
+    float* sG_rot;                    // apply_rotation: [P,4] gradient of the rotation head's output
+    float* sG_coff;                   // DISCRETE: [P, centers] gradient of coff
 };
 void launch_deform_bwd_a(const DeformBwdArgs& a, hipStream_t st);
 struct AtbJob {                        // C[M][N] += sum_g L[g][m] R[g][n]; bias[m] += sum_g L[g][m]
@@ -269,7 +290,7 @@ struct AtbJob {                        // C[M][N] += sum_g L[g][m] R[g][n]; bias
     float* bias;
     int M, N;
 };
-constexpr int LSR_ATB_MAX_JOBS = 12;
+constexpr int LSR_ATB_MAX_JOBS = 20;
 struct AtbArgs {
     AtbJob job[LSR_ATB_MAX_JOBS];
     int P;
@@ -278,6 +299,25 @@ struct AtbArgs {
 void launch_atb(const AtbArgs& a, int njobs, hipStream_t st);
 void launch_unpack_plane_grad(const float* src, float* dst, int H, int W, int replicas, int64_t stride,
                               hipStream_t st);
+
+// lang_deform (RESIDUAL / NORESNET): relu([lang, poc_fre(t)]) -> Linear, ReLU, Linear, ReLU, Linear,
+// (+ lang), normalised.  Separate kernels: the MLP reads only the language rows and the time.
+struct LangDeformArgs {
+    int P, lang_dim, time_pe, kin, residual;   // kin = lang_dim + 1 + 2 time_pe
+    const float* lang;                // [P, lang_dim]
+    const float* time;
+    const __bf16 *w_h[3], *w_l[3];    // [128][kpad], [128][128], [32][128] (rows past lang_dim zero)
+    const float* b[3];
+    float* out_lang;
+    // backward only
+    const __bf16 *wt_h[3], *wt_l[3];  // transposed: [kpad 32][128], [128][128], [128][32]
+    const float* up_lang;             // [P, lang_dim] or null
+    float* d_lang;                    // [P, lang_dim]
+    float *sU0, *sU1, *sU2;           // saved [P, kin], [P,128], [P,128]
+    float *sdv, *sdZ2, *sdZ1;         // saved [P, lang_dim], [P,128], [P,128]
+};
+void launch_lang_deform_fwd(const LangDeformArgs& a, hipStream_t st);
+void launch_lang_deform_bwd(const LangDeformArgs& a, hipStream_t st);
 
 void launch_preprocess(const PreprocessArgs& a, hipStream_t st);
 void launch_preprocess_bwd(const PreprocessBwdArgs& a, bool accumulate, hipStream_t st);
@@ -298,9 +338,8 @@ struct ScanSeg {
     uint32_t* total;
     uint32_t* partials;   // the segment's scan workspace
     size_t n;
-    // optional: host-mapped pinned words {total, *err} written by the scan itself (no copy launch)
+    // optional: host-mapped pinned word the scan writes the total to itself (no copy launch)
     uint32_t* host_total = nullptr;
-    const uint32_t* err = nullptr;
 };
 struct ScanBatch { ScanSeg s[LSR_MAX_VIEWS]; };
 // Returns the segments (bit i = segs[i]) whose host_total the scan wrote; the caller copies the
@@ -308,13 +347,12 @@ struct ScanBatch { ScanSeg s[LSR_MAX_VIEWS]; };
 uint32_t exclusive_scan_batch(const ScanSeg* segs, int nseg, hipStream_t st);
 size_t radix_temp_bytes(size_t n);
 // stable LSD sort of (key, value) pairs on bits [begin_bit, end_bit); returns true when the result
-// is in (keys_b, vals_b).  err (device word, may be null) is set non-zero if a look-back timed out.
-// temp_zeroed: the caller already zeroed the first radix_temp_zero_bytes(n, begin, end) bytes of temp
-// kept (device word, may be null, reduce-then-scan build only): the first pass drops every key
-// equal to 0xFFFFFFFF and writes the number of kept keys here; the later passes sort only those,
-// so the output holds the kept pairs in [0, *kept) (the rest of the buffers is left as it was).
-// gather (reduce-then-scan build, radix_sort_fuses_gather()): the last pass also writes, per
-// output position, rect_sorted = rect[value] and counts = rect_count of it, and not the keys.
+// is in (keys_b, vals_b).  Every word of temp it reads it has written (no zeroing needed).
+// kept (device word, may be null): the first pass drops every key equal to 0xFFFFFFFF and writes
+// the number of kept keys here; the later passes sort only those, so the output holds the kept
+// pairs in [0, *kept) (the rest of the buffers is left as it was).
+// gather (may be null): the last pass also writes, per output position, rect_sorted = rect[value]
+// and counts = rect_count of it, and not the keys.
 struct SortGather {
     const uint2* rect;
     uint32_t* counts;
@@ -333,17 +371,11 @@ struct SortBatch { SortSeg s[LSR_MAX_VIEWS]; };
 // Sorts up to LSR_MAX_VIEWS independent segments with one launch per kernel of each pass (every
 // segment the same key bits); returns whether the results are in the (b) buffers.
 bool radix_sort_batch(const SortSeg* segs, int nseg, int begin_bit, int end_bit, hipStream_t st);
-bool radix_sort_fuses_gather();
 bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b, size_t n,
-                      int begin_bit, int end_bit, void* temp, uint32_t* err, hipStream_t st, bool temp_zeroed = false,
-                      uint32_t* kept = nullptr, const SortGather* gather = nullptr);
-size_t radix_temp_zero_bytes(size_t n, int begin_bit, int end_bit);
+                      int begin_bit, int end_bit, void* temp, hipStream_t st, uint32_t* kept = nullptr,
+                      const SortGather* gather = nullptr);
 
 // binning (binning.hip)
-void launch_iota(int n, uint32_t* out, hipStream_t st);
-// ranks r >= *nsorted (device word, may be null) get count 0 (the depth sort dropped culled keys)
-void launch_gather_tile_counts(int P, const uint32_t* nsorted, const uint32_t* order, const uint2* rect, uint32_t* counts,
-                               uint2* rect_sorted, hipStream_t st);
 // Point-list values: Gaussian id in the low 28 bits, in the top 4 the quadrants (bit 28 + q,
 // q = (y >= 8) * 2 + (x >= 8) inside the 16x16 tile) the splat may reach (quad_may_touch); an
 // instance reaching none gets tile key ntiles and sorts past every list.

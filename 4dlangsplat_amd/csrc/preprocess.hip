@@ -271,11 +271,7 @@ __device__ __forceinline__ bool preprocess_one(const PreprocessArgs& a, const Pr
     v.radii[i] = radius;
     v.radius[i] = radius;
     uint32_t qmap = 0;   // quadrant map of a rectangle of <= 2 x 2 tiles (the binning's emit_quad_mask)
-#ifdef LSR_ABL_NOQMAP
-    if (false) {   // timing ablation only (instances of small rectangles then reach no quadrant)
-#else
     if (ntiles > 0 && cmax.x - cmin.x <= 2 && cmax.y - cmin.y <= 2) {
-#endif
         // emit_quad_mask per tile, with each 8-row band's extent computed once for the tile row
         // (bit 8 (ty - y0) + 4 band + 2 (tx - x0) + column; the same arithmetic and bits)
         const EmitSplat es = emit_splat(pix, conic);
@@ -309,9 +305,6 @@ __device__ __forceinline__ bool preprocess_one(const PreprocessArgs& a, const Pr
 // rows, the wave's 64 rows written as whole float4 runs (coalesced; a row per lane would write 64
 // strided partial lines per store).  Every lane of the wave calls this.
 __device__ __forceinline__ void zero_acc_rows(float4* acc, bool rect, int i) {
-#ifdef LSR_ABL_NOACCZERO   // timing ablation only
-    return;
-#endif
     if (!acc) return;
     const uint64_t m = __ballot(rect);
     if (m == 0) return;

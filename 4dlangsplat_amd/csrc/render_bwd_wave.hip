@@ -199,11 +199,7 @@ k_render_bwd_wave(RenderBwdArgs a) {
             if (cand) {   // back to front: higher list positions first
                 const int rank = lane == 63 ? 0 : __popcll(m >> (lane + 1));
                 const int s = (tail + rank) & (WFIFO - 1);
-#ifdef LSR_ABL_DEDUP   // timing ablation only: atomics only from the entry's lowest quadrant
-                s_fk[s] = (uint32_t)k | ((((word >> PL_QUAD_SHIFT) & ((1u << quad) - 1u)) == 0u ? 0u : 1u) << 31);
-#else
                 s_fk[s] = (uint32_t)k;
-#endif
                 s_fg[s] = gid;
             }
             tail += __popcll(m);
@@ -227,16 +223,9 @@ k_render_bwd_wave(RenderBwdArgs a) {
             const int s = (head + lane) & (WFIFO - 1);
             pf.gid = ok ? s_fg[s] : 0u;
             pf.k = ok ? s_fk[s] : 0xFFFFFFFFu;
-#ifdef LSR_ABL_DEDUP
-            const uint32_t dup = ok ? (pf.k & 0x80000000u) : 0u;
-            pf.k = ok ? (pf.k & 0x7FFFFFFFu) : 0xFFFFFFFFu;
-#endif
             pf.xy = *at32(a.xy, pf.gid);
             pf.co = *at32(a.conic_o, pf.gid);
             pf.rgbd = *at32(a.rgbd, pf.gid);
-#ifdef LSR_ABL_DEDUP
-            pf.gid |= dup;
-#endif
         }
         const int e = lane >> 2, c0 = 8 * (lane & 3);
         const uint32_t gid = e < n ? s_fg[(head + e) & (WFIFO - 1)] : 0u;
@@ -304,36 +293,26 @@ k_render_bwd_wave(RenderBwdArgs a) {
         for (int j = 0; j < WG / 2; ++j) {   // lane -> channel lane & 31 of entries (lane >> 5) + 2 j
             const int e = (lane >> 5) + 2 * j;
             lv[j] = s_lq[e][ch];
-#ifdef LSR_ABL_DEDUP
-            if (s_agid[e] >> 31) lv[j] = 0.0f;
-#endif
-            lo[j] = (s_agid[e] & 0x7FFFFFFFu) * (uint32_t)C + ch;
+            lo[j] = s_agid[e] * (uint32_t)C + ch;
         }
 #pragma unroll
         for (int r = 0; r < WG / 4; ++r) {   // lane -> field lane & 15 of entry (lane >> 4) + 4 r
             const int e = (lane >> 4) + 4 * r;
             sv[r] = s_q[e][q];
-#ifdef LSR_ABL_DEDUP
-            if (s_agid[e] >> 31) sv[r] = 0.0f;
-#endif
-            so[r] = (s_agid[e] & 0x7FFFFFFFu) * (uint32_t)ACC_PITCH + q;
+            so[r] = s_agid[e] * (uint32_t)ACC_PITCH + q;
         }
         // A branch-free variant (every lane, zeros for idle lanes, so that hipcc could count the
         // atomics and skip them in its waits for later loads) measured 0.70 vs 0.50 ms: with no
         // wait behind them a wave keeps several groups of atomics in flight and the memory
         // system backs up.  The wait that follows each batch throttles them.
-#ifndef LSR_ABL_NOLANGATOM
         if (a.acc_lang) {   // 128-byte rows
 #pragma unroll
             for (int j = 0; j < WG / 2; ++j)
                 if ((lane >> 5) + 2 * j < acnt && ch < C && lv[j] != 0.0f) atomicAdd(at32(a.acc_lang, lo[j]), lv[j]);
         }
-#endif
-#ifndef LSR_ABL_NOSMALLATOM
 #pragma unroll
         for (int r = 0; r < WG / 4; ++r)
             if ((lane >> 4) + 4 * r < acnt && q < 10 && sv[r] != 0.0f) atomicAdd(at32(a.acc_small, so[r]), sv[r]);
-#endif
         acnt = 0;
     };
 
@@ -401,11 +380,7 @@ k_render_bwd_wave(RenderBwdArgs a) {
             // the forward's operation order per component (bit-identical alpha decisions)
             const lsr_f2 dx = X - px2, dy = Y - py2;
             const lsr_f2 pw = gauss_power2(A, B, Cc, dx, dy);
-#ifdef LSR_ABL_NOEXP
-            const lsr_f2 ge = {fmaxf(1.0f + pw.x, 0.0f), fmaxf(1.0f + pw.y, 0.0f)};   // timing ablation only
-#else
             const lsr_f2 ge = expf_repro2(pw);
-#endif
             const lsr_f2 og = O * ge;
             lsr_f2 dot = ld2(s_R) * g0;
             dot = __builtin_elementwise_fma(ld2(s_Gc), lsr_f2{g1, g1}, dot);
@@ -554,32 +529,19 @@ k_render_bwd_wave(RenderBwdArgs a) {
 // buckets the tiles by their replay bound (tile_max_contrib, written by the forward) in
 // descending order: a counting sort over 1024 buckets of 2 replay entries.  The order inside a
 // bucket is not fixed, which only permutes float atomic summation (this path is non-deterministic).
-// LSR_TILE_ORDER_BANDS: slot s runs on XCD s mod 8 (the compositors' block -> slot map), so the
-// tiles are cut into 8 contiguous raster bands, band x sorted longest-first onto the slots
-// s = x (mod 8): each XCD's L2 then serves one region of the image (neighbouring tiles share
-// Gaussians: their records and accumulator rows) instead of every XCD touching all of it.
 constexpr int ORDER_BUCKETS = 1024;
 __global__ void __launch_bounds__(1024) k_tile_order(int ntiles, const uint32_t* __restrict__ tile_max,
                                                      const uint2* __restrict__ ranges, uint32_t* __restrict__ order) {
     __shared__ uint32_t s_cnt[ORDER_BUCKETS];
     __shared__ uint32_t s_wave[16];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-#ifdef LSR_TILE_ORDER_BANDS
-    // band x = blockIdx.x: its size is the number of slots s < ntiles with s = x (mod 8)
-    const int x = blockIdx.x;
-    int t0 = 0;
-    for (int y = 0; y < x; ++y) t0 += (ntiles - y + 7) / 8;
-    const int nb = (ntiles - x + 7) / 8, t1 = t0 + nb;
-#else
-    const int x = 0, t0 = 0, t1 = ntiles;
-#endif
     s_cnt[tid] = 0;
     __syncthreads();
     auto bucket = [&](int t) {
         const uint32_t cost = ranges ? (ranges[t].y - ranges[t].x) >> 2 : tile_max[t] >> 1;
         return ORDER_BUCKETS - 1 - (int)min(cost, (uint32_t)ORDER_BUCKETS - 1);
     };
-    for (int t = t0 + tid; t < t1; t += 1024) atomicAdd(&s_cnt[bucket(t)], 1u);
+    for (int t = tid; t < ntiles; t += 1024) atomicAdd(&s_cnt[bucket(t)], 1u);
     __syncthreads();
     const uint32_t v = s_cnt[tid];
     uint32_t inc = v;
@@ -594,20 +556,11 @@ __global__ void __launch_bounds__(1024) k_tile_order(int ntiles, const uint32_t*
     for (int w = 0; w < wave; ++w) off += s_wave[w];
     s_cnt[tid] = off + inc - v;   // exclusive start of bucket tid
     __syncthreads();
-#ifdef LSR_TILE_ORDER_BANDS
-    for (int t = t0 + tid; t < t1; t += 1024) order[8 * atomicAdd(&s_cnt[bucket(t)], 1u) + x] = (uint32_t)t;
-#else
-    (void)x;
     for (int t = tid; t < ntiles; t += 1024) order[atomicAdd(&s_cnt[bucket(t)], 1u)] = (uint32_t)t;
-#endif
 }
 
 void launch_tile_order(int ntiles, const uint32_t* tile_max, const uint2* ranges, uint32_t* order, hipStream_t st) {
-#ifdef LSR_TILE_ORDER_BANDS
-    hipLaunchKernelGGL(k_tile_order, dim3(8), dim3(1024), 0, st, ntiles, tile_max, ranges, order);
-#else
     hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, st, ntiles, tile_max, ranges, order);
-#endif
 }
 
 void launch_render_bwd_wave(const RenderBwdArgs& a, hipStream_t st) {

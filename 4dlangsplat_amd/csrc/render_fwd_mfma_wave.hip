@@ -36,51 +36,6 @@ __device__ __forceinline__ void pack_octet(const float (&w)[8], bf16x8& h, bf16x
     }
 }
 
-// LDS-DMA gather (global_load_lds): 16 or 4 bytes from this lane's global address to
-// lds_base + lane * size.  Inline asm, M0 written in the same statement (cdna_hip_programming.md,
-// LDS-DMA recipe): issued through the builtin, hipcc cannot tell the DMA's LDS image from the
-// compositing arrays and waits vmcnt(0) before every later ds_read, serialising the prefetch.
-// hipcc does not count these loads: relayout() waits vmcnt(0) itself before reading the image
-// (an untracked VMEM op can only make hipcc's own counted waits wait longer, never too little).
-__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)reinterpret_cast<uintptr_t>(p); }
-__device__ __forceinline__ void lds_dma16(const float* g, uint32_t lds_base) {
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(g), "s"(lds_base) : "memory");
-}
-__device__ __forceinline__ void lds_dma4(const float* g, uint32_t lds_base) {
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(g), "s"(lds_base) : "memory");
-}
-// The same from a wave-uniform base (SGPR pair) + this lane's 32-bit byte offset: one VGPR of
-// address per lane instead of two.
-__device__ __forceinline__ void lds_dma16_s(const void* base, uint32_t off, uint32_t lds_base) {
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(off), "s"(base), "s"(lds_base) : "memory");
-}
-__device__ __forceinline__ void lds_dma4_s(const void* base, uint32_t off, uint32_t lds_base) {
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(off), "s"(base), "s"(lds_base) : "memory");
-}
-// Wait until at most n (clamped to 0..7) of this wave's vector memory instructions are in flight.
-// Completion is in issue order, so n = the number of instructions issued after a batch waits for
-// that batch and nothing later.  Inline asm: hipcc neither moves nor drops it.
-__device__ __forceinline__ void vm_wait_upto(int n) {
-    switch (n < 0 ? 0 : n > 7 ? 7 : n) {
-        case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    }
-}
-
 // lane group g holds octets x[0..3] (one per entry octet o) of its own pixel; afterwards it holds
 // in x[nb] the octet g of pixel 16 nb + (lane & 15): the MFMA B fragments, nb = pixel block
 __device__ __forceinline__ void octets_to_b(bf16x8 (&x)[4]) {
@@ -121,46 +76,21 @@ __device__ unsigned long long g_fwd_stamps[8];
 #ifndef LSR_FWD_WAVES
 #define LSR_FWD_WAVES 4   // waves per SIMD the register budget targets (3: 0.293 ms, 4: 0.268 ms)
 #endif
-#ifndef LSR_FWD_DMA
-// 1: the LDS-DMA pipeline below for 32 channels.  It runs a wave's loop in 0.85x the cycles of
-// the register-staged path at the same 4 waves per SIMD (tools/fwd_stamps.py), yet measured
-// 0.257-0.271 vs 0.249-0.264 ms same-box: with the gathers hidden the waves contend for issue
-// (PMC: 35 % of wave cycles waiting for issue), so it stays off.
-#define LSR_FWD_DMA 0
-#endif
-#ifndef LSR_FWD_DMA_WAVES
-#define LSR_FWD_DMA_WAVES 4
-#endif
-// DMA (32 channels): every global read of the group loop -- the point-list words of the scan,
-// the group's geometry and its language rows -- is an LDS-DMA gather (global_load_lds) issued
-// one step ahead: the next scan round's words after a round, the next group's geometry before
-// this group composites, its rows once this group's channel sums have read theirs.  The gathers
-// stalled the register-staged loop (52 % of its cycles, tools/fwd_stamps.py); here each wait
-// targets one batch (vm_wait_upto with the count of instructions issued after it).  The MFMA A
-// operand is read straight from the staged fp32 rows (no bf16 row copies): 8.6 KB of LDS per
-// wave, so 4 waves per SIMD as the register-staged version.
-template <bool DMA, bool PRE>
-__global__ void __launch_bounds__(64)
-__attribute__((amdgpu_waves_per_eu(DMA ? LSR_FWD_DMA_WAVES : LSR_FWD_WAVES, DMA ? LSR_FWD_DMA_WAVES : LSR_FWD_WAVES)))
+// PRE: C == 32 with the language rows' bf16 hi / lo made once per batch (a.lang_split).  A variant
+// that gathered every read of the group loop by LDS-DMA ran a wave's loop in 0.85x the cycles but
+// was no faster (the waves then contend for issue); it was removed in round 3.
+template <bool PRE>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LSR_FWD_WAVES, LSR_FWD_WAVES)))
 k_render_fwd_wave_mfma(RenderFwdArgs a) {
     // group entries, one array per field (a b64 read of a pair = one packed-fp32 operand): centre
     // X, Y; staged conic -a/2, -b, -c/2 (gauss_power); opacity (0 past the group: never blends); (r, g) and (b, depth) pairs
     __shared__ __attribute__((aligned(16))) float s_X[MG], s_Y[MG], s_A[MG], s_B[MG], s_C[MG], s_O[MG];
     __shared__ lsr_f2 s_RG[MG], s_BD[MG];
     __shared__ uint32_t s_k[MG];   // list position + 1 (the n_contrib value of a blend)
-    __shared__ __attribute__((aligned(16))) __bf16 s_Fh[DMA ? 8 : MG * MFP];
-    __shared__ __attribute__((aligned(16))) __bf16 s_Fl[DMA ? 8 : MG * MFP];
+    __shared__ __attribute__((aligned(16))) __bf16 s_Fh[MG * MFP];
+    __shared__ __attribute__((aligned(16))) __bf16 s_Fl[MG * MFP];
     __shared__ uint32_t s_fk[MFIFO];
     __shared__ uint32_t s_fg[MFIFO];
-    // DMA staging (wave-instruction images, lane-linear), one array: language rows of entries
-    // 8 i .. 8 i + 7 at SG_LANG + i SG_IMG (rows of 32 floats; the 16-float pad between images
-    // makes the A-operand reads conflict-free), conic_o [0, MG) then rgbd [MG, 2 MG) as float4
-    // at SG_GEO, X [0, MG) then Y [MG, 2 MG) at SG_XY, two rounds of point-list words at SG_SCAN.
-    // (Separate __shared__ arrays as LDS-DMA targets crash hipcc 7.2's SIFixSGPRCopies; float
-    // pointers into one array do not.)
-    constexpr int SG_LANG = 0, SG_IMG = 8 * 32 + 16, SG_GEO = SG_LANG + 4 * SG_IMG, SG_XY = SG_GEO + 2 * MG * 4,
-                  SG_SCAN = SG_XY + 2 * MG, SG_END = SG_SCAN + 128;
-    __shared__ __attribute__((aligned(16))) float s_stage[DMA ? SG_END : 4];
 
     const int b = blockIdx.x;
     const int slot = (b >> 5) * 8 + (b & 7), quad = (b >> 3) & 3;   // a slot's 4 quadrants: one XCD
@@ -176,8 +106,6 @@ k_render_fwd_wave_mfma(RenderFwdArgs a) {
     const bool inside = px < a.W && py < a.H;
     const float pxf = (float)px, pyf = (float)py;
     const uint2 range = a.ranges[tile];
-    const uint32_t sort_err = a.sort_err ? (a.sort_err[0] | a.sort_err[1]) : 0u;
-    if (a.status_out && b == 0 && lane < 2) a.status_out[lane] = a.sort_err ? a.sort_err[lane] : 0u;
     const int C = a.C;
 
     float T = 1.0f;
@@ -194,39 +122,18 @@ k_render_fwd_wave_mfma(RenderFwdArgs a) {
     uint32_t pos = range.x;  // list entries [pos, range.y) not yet scanned
     int head = 0, tail = 0;  // FIFO counters (wave-uniform)
     // scan prefetch: point-list words (id | quadrant bits, k_emit) of the next two rounds
-    uint32_t w_c = !DMA && pos + lane < range.y ? *at32(a.point_list, pos + lane) : 0u;
-    uint32_t w_n = !DMA && pos + 64 + lane < range.y ? *at32(a.point_list, pos + 64 + lane) : 0u;
+    uint32_t w_c = pos + lane < range.y ? *at32(a.point_list, pos + lane) : 0u;
+    uint32_t w_n = pos + 64 + lane < range.y ? *at32(a.point_list, pos + 64 + lane) : 0u;
 #ifdef LSR_FWD_STAMPS
     unsigned long long st_sum[4] = {0, 0, 0, 0}, st_prev = 0;
 #endif
-    // DMA bookkeeping (wave-uniform): LDS-DMA instructions issued so far, and the count right
-    // after the outstanding scan / geometry / language batch
-    int issued = 0, mark_scan = 0, mark_geo = 0, mark_lang = 0, rslot = 0;
-    uint32_t* const ring = reinterpret_cast<uint32_t*>(s_stage + (DMA ? SG_SCAN : 0));
-    // point-list words [p0, p0 + 64) (clamped into the list; masked at use) -> ring slot sl
-    auto issue_scan = [&](uint32_t p0, int sl) __attribute__((always_inline)) {
-        const uint32_t idx = min(p0 + (uint32_t)lane, range.y - 1u);
-        lds_dma4_s(a.point_list, 4u * idx, lds_addr(ring + 64 * sl));
-        mark_scan = ++issued;
-    };
-    if constexpr (DMA) {
-        if (range.x < range.y) issue_scan(range.x, 0);
-    }
     // scan rounds until `want` entries wait in the FIFO or the list is exhausted
     auto scan_fill = [&](int want) __attribute__((always_inline)) {
         while (tail - head < want && pos < range.y) {
             const uint32_t idx = pos + lane;
-            uint32_t word;
-            if constexpr (DMA) {   // this round's words landed in the ring; the next round's go out
-                vm_wait_upto(issued - mark_scan);
-                word = ring[64 * rslot + lane];
-                if (pos + 64 < range.y) issue_scan(pos + 64, rslot ^ 1);
-                rslot ^= 1;
-            } else {
-                word = w_c;
-                w_c = w_n;
-                w_n = idx + 128 < range.y ? *at32(a.point_list, idx + 128) : 0u;
-            }
+            const uint32_t word = w_c;
+            w_c = w_n;
+            w_n = idx + 128 < range.y ? *at32(a.point_list, idx + 128) : 0u;
             const uint32_t gid = word & PL_ID_MASK;
             const bool cand = idx < range.y && ((word >> (PL_QUAD_SHIFT + quad)) & 1u);
             const uint64_t m = __ballot(cand);
@@ -259,11 +166,7 @@ k_render_fwd_wave_mfma(RenderFwdArgs a) {
                     const lsr_f2 X = ld2(s_X), Y = ld2(s_Y), A = ld2(s_A), B = ld2(s_B), Cc = ld2(s_C), O = ld2(s_O);
                     const lsr_f2 dx = X - px2, dy = Y - py2;
                     const lsr_f2 pw = gauss_power2(A, B, Cc, dx, dy);
-#ifdef LSR_ABL_FWD_NOEXP
-                    const lsr_f2 og = O * lsr_f2{fmaxf(1.0f + pw.x, 0.0f), fmaxf(1.0f + pw.y, 0.0f)};   // timing ablation only
-#else
                     const lsr_f2 og = O * expf_repro2(pw);
-#endif
                     al[u] = fminf(0.99f, og.x);
                     al[u + 1] = fminf(0.99f, og.y);
                     ok[u] = pw.x <= 0.0f && al[u] >= 1.0f / 255.0f;        // padding entries: O = 0
@@ -289,33 +192,16 @@ k_render_fwd_wave_mfma(RenderFwdArgs a) {
         }
         FWD_STAMP(3);
         // ---- 4. language channels on matrix cores -----------------------------------------------
-#ifdef LSR_ABL_FWD_NOMFMA
-        if (cnt > 0) return;   // timing ablation only
-#endif
         octets_to_b(oh);
         octets_to_b(ol);
-        if constexpr (DMA) vm_wait_upto(issued - mark_lang);   // this group's rows landed
 #pragma unroll
         for (int mb = 0; mb < 2; ++mb) {
             // A[m = channel 16 mb + l16][k = entry 8 g4 + j] from the rows [e][c]
-            bf16x8 ah, alo;
-            if constexpr (DMA) {   // fp32 rows of the stage, split here (rows past the group: 0)
-                const float* F = s_stage + SG_LANG + SG_IMG * g4 + 16 * mb + l16;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const float f = 8 * g4 + j < cnt ? F[32 * j] : 0.0f;
-                    __bf16 hh, ll;
-                    split_bf16(f, hh, ll);
-                    ah[j] = hh;
-                    alo[j] = ll;
-                }
-            } else {
-                const int off = (8 * g4 + (l16 >> 2)) * MFP + 16 * mb + 4 * (l16 & 3);
-                ah = __builtin_shufflevector(ds_read_tr16(s_Fh + off), ds_read_tr16(s_Fh + off + 4 * MFP),
-                                             0, 1, 2, 3, 4, 5, 6, 7);
-                alo = __builtin_shufflevector(ds_read_tr16(s_Fl + off), ds_read_tr16(s_Fl + off + 4 * MFP),
-                                              0, 1, 2, 3, 4, 5, 6, 7);
-            }
+            const int off = (8 * g4 + (l16 >> 2)) * MFP + 16 * mb + 4 * (l16 & 3);
+            const bf16x8 ah = __builtin_shufflevector(ds_read_tr16(s_Fh + off), ds_read_tr16(s_Fh + off + 4 * MFP),
+                                                      0, 1, 2, 3, 4, 5, 6, 7);
+            const bf16x8 alo = __builtin_shufflevector(ds_read_tr16(s_Fl + off), ds_read_tr16(s_Fl + off + 4 * MFP),
+                                                       0, 1, 2, 3, 4, 5, 6, 7);
 #pragma unroll
             for (int nb = 0; nb < 4; ++nb) {
                 L[mb][nb] = LSR_MFMA16(ah, oh[nb], L[mb][nb]);
@@ -324,7 +210,7 @@ k_render_fwd_wave_mfma(RenderFwdArgs a) {
             }
         }
     };
-    if constexpr (!DMA) {
+    {
         while (!__all(done)) {
             FWD_STAMP(0);
             scan_fill(MG);
@@ -415,79 +301,6 @@ k_render_fwd_wave_mfma(RenderFwdArgs a) {
             wave_lds_sync();   // the group's LDS rows are read before the next staging
             FWD_STAMP(4);
         }
-    } else {
-        // geometry of FIFO group [head, head + n): lanes < MG conic + opacity, lanes >= MG rgb +
-        // depth; x for lanes < MG, y for the others (entries past the group read Gaussian 0)
-        auto issue_geo = [&](int n) __attribute__((always_inline)) {
-            const int e = lane & (MG - 1);
-            const uint32_t gid = e < n ? s_fg[(head + e) & (MFIFO - 1)] : 0u;
-            // one uniform base for both arrays (carved from one workspace: 32-bit offsets)
-            const char* co = reinterpret_cast<const char*>(a.conic_o);
-            const char* cd = reinterpret_cast<const char*>(a.rgbd);
-            const char* gb = co < cd ? co : cd;
-            uint32_t hi = (uint32_t)lane >> 5;   // 0: conic, 1: rgbd
-            asm volatile("" : "+v"(hi));          // recomputed here, not hoisted into a live register
-            const uint32_t off = (hi ? (uint32_t)(cd - gb) : (uint32_t)(co - gb)) + 16u * gid;
-            lds_dma16_s(gb, off, lds_addr(s_stage + SG_GEO));
-            lds_dma4_s(a.xy, 8u * gid + 4u * (uint32_t)(lane >> 5), lds_addr(s_stage + SG_XY));
-            issued += 2;
-            mark_geo = issued;
-        };
-        // language rows of FIFO group [h, h + n): image i = entries 8 i + lane / 8, 16-byte chunk lane % 8
-        auto issue_lang = [&](int h, int n) __attribute__((always_inline)) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int e = 8 * i + (lane >> 3);
-                const uint32_t gid = e < n ? s_fg[(h + e) & (MFIFO - 1)] : 0u;
-                lds_dma16_s(a.lang, 128u * gid + 16u * (uint32_t)(lane & 7), lds_addr(s_stage + SG_LANG + SG_IMG * i));
-            }
-            issued += 4;
-            mark_lang = issued;
-        };
-        // staged geometry of the group (count n) -> SoA arrays; frees the geometry stage
-        auto relayout = [&](int n) __attribute__((always_inline)) {
-            vm_wait_upto(issued - mark_geo);
-            if (lane < MG) {
-                const bool ok = lane < n;
-                const float4* geo = reinterpret_cast<const float4*>(s_stage + SG_GEO);
-                const float4 co = geo[lane], cd = geo[MG + lane];
-                s_k[lane] = ok ? s_fk[(head + lane) & (MFIFO - 1)] + 1u : 0u;
-                s_X[lane] = s_stage[SG_XY + lane]; s_Y[lane] = s_stage[SG_XY + MG + lane];
-                s_A[lane] = -0.5f * co.x; s_B[lane] = -co.y; s_C[lane] = -0.5f * co.z; s_O[lane] = ok ? co.w : 0.0f;
-                s_RG[lane] = lsr_f2{cd.x, cd.y};
-                s_BD[lane] = lsr_f2{cd.z, cd.w};
-            }
-        };
-        scan_fill(MG);
-        int cnt = min(MG, tail - head);
-        if (cnt > 0) {
-            wave_lds_sync();
-            issue_geo(cnt);
-            issue_lang(head, cnt);
-        }
-        while (cnt > 0) {
-            FWD_STAMP(0);
-            relayout(cnt);
-            head += cnt;
-            wave_lds_sync();
-            FWD_STAMP(1);
-            int next = 0;
-            if (!__all(done)) {   // the next group's geometry flies while this one composites
-                scan_fill(MG);
-                next = min(MG, tail - head);
-                if (next > 0) {
-                    wave_lds_sync();
-                    issue_geo(next);
-                }
-            }
-            FWD_STAMP(2);
-            composite(cnt);   // waits for this group's rows before its channel sums
-            wave_lds_sync();
-            if (next > 0) issue_lang(head, next);   // the rows were read: the stage is free
-            FWD_STAMP(4);
-            cnt = __all(done) ? 0 : next;
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA left in flight when the wave ends
     }
 #ifdef LSR_FWD_STAMPS
     if (lane < 4) {
@@ -498,15 +311,6 @@ k_render_fwd_wave_mfma(RenderFwdArgs a) {
     }
     if (lane == 4) atomicAdd(&g_fwd_stamps[4], 1ull);
 #endif
-    if (sort_err) {   // a sort's look-back timed out: the lists are invalid, make every output NaN
-        const float nan = __builtin_nanf("");
-        T = nan;
-        acc_rg = acc_bd = lsr_f2{nan, nan};
-#pragma unroll
-        for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-            for (int nb = 0; nb < 4; ++nb) L[mb][nb] = f32x4{nan, nan, nan, nan};
-    }
     if (inside) {
         const size_t HW = (size_t)a.H * a.W, pid = (size_t)py * a.W + px;
         a.final_T[pid] = T;
@@ -566,16 +370,10 @@ void launch_language_split(int P, const float* lang, uint16_t* out, hipStream_t 
 
 void launch_render_fwd_wave_mfma(const RenderFwdArgs& a, hipStream_t st) {
     const int ntiles = a.grid_x * a.grid_y;
-#if LSR_FWD_DMA
-    if (a.C == 32) {
-        hipLaunchKernelGGL((k_render_fwd_wave_mfma<true, false>), dim3(((ntiles + 7) / 8) * 32), dim3(64), 0, st, a);
-        return;
-    }
-#endif
     if (a.lang_split && a.C == 32)
-        hipLaunchKernelGGL((k_render_fwd_wave_mfma<false, true>), dim3(((ntiles + 7) / 8) * 32), dim3(64), 0, st, a);
+        hipLaunchKernelGGL((k_render_fwd_wave_mfma<true>), dim3(((ntiles + 7) / 8) * 32), dim3(64), 0, st, a);
     else
-        hipLaunchKernelGGL((k_render_fwd_wave_mfma<false, false>), dim3(((ntiles + 7) / 8) * 32), dim3(64), 0, st, a);
+        hipLaunchKernelGGL((k_render_fwd_wave_mfma<false>), dim3(((ntiles + 7) / 8) * 32), dim3(64), 0, st, a);
 }
 
 }  // namespace lsr

@@ -40,8 +40,6 @@ __global__ void __launch_bounds__(64) k_render_fwd_wave(RenderFwdArgs a) {
     const bool inside = px < a.W && py < a.H;
     const float pxf = (float)px, pyf = (float)py;
     const uint2 range = a.ranges[tile];
-    const uint32_t sort_err = a.sort_err ? (a.sort_err[0] | a.sort_err[1]) : 0u;
-    if (a.status_out && b == 0 && lane < 2) a.status_out[lane] = a.sort_err ? a.sort_err[lane] : 0u;
     const int C = a.C;
 
     float T = 1.0f;
@@ -153,11 +151,7 @@ __global__ void __launch_bounds__(64) k_render_fwd_wave(RenderFwdArgs a) {
                 acc[1] = __builtin_fmaf(cd.y, w, acc[1]);
                 acc[2] = __builtin_fmaf(cd.z, w, acc[2]);
                 accD = __builtin_fmaf(cd.w, w, accD);
-#ifdef LSR_ABL_NOLANGACC
-                if constexpr (false) {
-#else
                 if constexpr (CPAD > 0) {
-#endif
                     const float4* f4 = reinterpret_cast<const float4*>(s_lang + e * CPAD);
 #pragma unroll
                     for (int c4 = 0; c4 < CPAD / 4; ++c4) {
@@ -174,12 +168,6 @@ __global__ void __launch_bounds__(64) k_render_fwd_wave(RenderFwdArgs a) {
             if (__all(done)) break;
         }
         wave_lds_sync();
-    }
-    if (sort_err) {   // a sort's look-back timed out: the lists are invalid, make every output NaN
-        const float nan = __builtin_nanf("");
-        T = accD = acc[0] = acc[1] = acc[2] = nan;
-#pragma unroll
-        for (int c = 0; c < LP; ++c) accL[c] = nan;
     }
     if (inside) {
         const size_t HW = (size_t)a.H * a.W, pid = (size_t)py * a.W + px;
@@ -215,11 +203,7 @@ void launch_render_fwd_wave(const RenderFwdArgs& a, hipStream_t st) {
         case 4: go_fwd_wave<4>(a, st); break;
         case 8: go_fwd_wave<8>(a, st); break;
         case 16: go_fwd_wave<16>(a, st); break;
-#ifdef LSR_FWD_VALU32
-        case 32: go_fwd_wave<32>(a, st); break;
-#else
         case 32: launch_render_fwd_wave_mfma(a, st); break;   // channel sums on matrix cores
-#endif
         default: go_fwd_wave<64>(a, st); break;
     }
 }

@@ -12,9 +12,6 @@
 
 namespace lsr {
 
-#ifndef LSR_SORT_SCAN_DIGIT
-#define LSR_SORT_SCAN_DIGIT 0   // 1: the per-digit count-row scan (k_rts_scan), for A/B
-#endif
 constexpr int SCAN_ITEMS = 8;
 constexpr int SCAN_TILE = 256 * SCAN_ITEMS;
 
@@ -150,10 +147,7 @@ __global__ void __launch_bounds__(256) k_scan_down_sum(const ScanBatch bt) {
     const uint32_t b0 = s_base[0];
     if (b == 0 && tid == 0) {
         if (sg.total) *sg.total = s_base[1];
-        if (sg.host_total) {   // host-mapped: visible to the host once the kernel has completed
-            sg.host_total[0] = s_base[1];
-            sg.host_total[1] = sg.err ? *sg.err : 0u;
-        }
+        if (sg.host_total) sg.host_total[0] = s_base[1];   // host-mapped: visible once the kernel completed
     }
     uint32_t block_total;
     block_exclusive_scan8(v, s_wave, block_total);
@@ -223,37 +217,15 @@ uint32_t exclusive_scan_batch(const ScanSeg* segs, int nseg, hipStream_t st) {
 }
 
 // ---- radix sort ---------------------------------------------------------------------------------
-// One histogram kernel for all passes (a pass permutes keys, it does not change the digit counts),
-// then ONE kernel per 8-bit pass with decoupled look-back:
-//   * blocks take tickets in launch order, so a block only ever waits for blocks already running;
-//   * each wave ranks its 1024 keys (16 rounds of 64) against its own digit counters in LDS with
-//     ballot digit matching -- stable, no block barriers while ranking;
-//   * thread d of the block publishes the block's count of digit d, sums predecessors' counts
-//     (status words {flag, count}: the data is the flag, agent-scope relaxed atomics = sc1, so
-//     no fences; MI355X_MICROARCH.md, inter-workgroup visibility) until an inclusive prefix, and
-//     publishes its own inclusive prefix;
-//   * the tile is placed digit-sorted in LDS and written out in runs (coalesced stores).
-// A look-back spin is bounded: on timeout the pass sets the caller's error word and finishes
-// (results invalid, never a hang).
-#ifndef LSR_SORT_LOOKBACK
-#define LSR_SORT_LOOKBACK 0   // 1: one pass kernel with decoupled look-back; 0: reduce-then-scan
-#endif
-#ifndef LSR_OS_ITEMS
-#if LSR_SORT_LOOKBACK
-#define LSR_OS_ITEMS 16   // look-back: 4..48 swept, 16 best (smaller tiles lengthen the chain)
-#else
-#define LSR_OS_ITEMS 8    // reduce-then-scan: 4 / 8 / 16 swept, 8 best
-#endif
-#endif
-constexpr int OS_ITEMS = LSR_OS_ITEMS;   // keys per thread per pass
-#ifndef LSR_LOOKBACK
-#define LSR_LOOKBACK 4   // predecessors read per look-back round trip (1..32 swept: 4 best)
-#endif
-
+// Reduce-then-scan LSD passes, 8 keys per thread (12 above 4M keys): per pass a count kernel writes
+// every block's 256 digit counts, a scan kernel turns them into each block's offset inside its
+// digit and the digit totals, and the scatter kernel ranks the block's keys again (ballot digit
+// matching per wave, stable), places them digit-sorted in LDS and writes runs (coalesced stores).
+// There is no inter-block chain: a decoupled look-back (one pass kernel, blocks waiting on their
+// predecessors' published counts) crossed the 8 XCDs' non-coherent L2s at every hop and bounded a
+// pass by the chain length; it was removed in round 3.
+constexpr int OS_ITEMS = 8;                   // keys per thread per pass (4 / 8 / 16 swept)
 constexpr int OS_TILE = 256 * OS_ITEMS;       // keys per block
-constexpr uint32_t OS_AGG = 1u << 30, OS_PRE = 2u << 30, OS_CNT = (1u << 30) - 1u;
-
-typedef __attribute__((address_space(1))) uint32_t gu32;
 
 // Peers of this lane's digit inside the wave (lanes with the same digit among the valid lanes).
 __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid, int nbits) {
@@ -284,184 +256,7 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t x, uint32_t* s_w
     return off + inc - x;
 }
 
-// Digit counts of every pass in one read of the keys (a pass permutes keys, it does not change
-// the counts).  The grid strides over the keys, 4 per thread per round, up to 4096 blocks
-// (blocks x keys-per-thread swept: the digit matching is latency-bound, so more, shorter blocks
-// win; 2M keys 153 -> 143 us per sort, 7.8M keys 192 -> 168 us), so each global counter takes
-// at most one atomic per block.  The counters are kept in HIST_COPIES
-// copies, one per XCD (block b runs on XCD b mod 8): each address then takes 1/8 of the blocks'
-// atomics (same-address device atomics serialise), and the pass kernel sums the copies.
-#ifndef LSR_HIST_BLOCKS
-#define LSR_HIST_BLOCKS 4096
-#endif
-[[maybe_unused]] constexpr int OS_HIST_BLOCKS = LSR_HIST_BLOCKS;
-#ifndef LSR_HIST_ITEMS
-#define LSR_HIST_ITEMS 4
-#endif
-constexpr int HIST_ITEMS = LSR_HIST_ITEMS;   // keys per thread per histogram round
-constexpr int HIST_COPIES = 8;
-constexpr int HIST_WORDS = 4 * 256;   // one copy: [pass][digit]
-__global__ void __launch_bounds__(256) k_radix_hist(const uint32_t* __restrict__ keys, size_t n, int begin_bit,
-                                                    int end_bit, uint32_t* __restrict__ hist) {
-    __shared__ uint32_t s_h[4][256];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) s_h[p][tid] = 0;
-    __syncthreads();
-    const uint64_t lt = lanemask_lt();
-    for (size_t base = ((size_t)blockIdx.x * 4 + wave) * (64 * HIST_ITEMS); base < n;
-         base += (size_t)gridDim.x * 4 * (64 * HIST_ITEMS)) {
-        uint32_t key[HIST_ITEMS];
-#pragma unroll
-        for (int r = 0; r < HIST_ITEMS; ++r) {
-            const size_t idx = base + (size_t)r * 64 + lane;
-            key[r] = idx < n ? keys[idx] : 0u;
-        }
-#pragma unroll
-        for (int r = 0; r < HIST_ITEMS; ++r) {
-            const bool valid = base + (size_t)r * 64 + lane < n;
-            int p = 0;
-            for (int shift = begin_bit; shift < end_bit; shift += 8, ++p) {
-                const int nbits = min(8, end_bit - shift);
-                const uint32_t d = (key[r] >> shift) & ((1u << nbits) - 1u);
-                const uint64_t peers = match_digit(d, valid, nbits);
-                if (valid && (peers & lt) == 0) atomicAdd(&s_h[p][d], (uint32_t)__popcll(peers));
-            }
-        }
-    }
-    __syncthreads();
-    int p = 0;
-    for (int shift = begin_bit; shift < end_bit; shift += 8, ++p)
-        if (s_h[p][tid]) atomicAdd(hist + (blockIdx.x % HIST_COPIES) * HIST_WORDS + p * 256 + tid, s_h[p][tid]);
-}
-
-__global__ void __launch_bounds__(256) k_radix_pass(const uint32_t* __restrict__ keys_in,
-                                                    const uint32_t* __restrict__ vals_in,
-                                                    uint32_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
-                                                    size_t n, int shift, int nbits,
-                                                    const uint32_t* __restrict__ hist, uint32_t* status,
-                                                    uint32_t* ticket, uint32_t* err) {
-    __shared__ uint32_t s_key[OS_TILE];
-    __shared__ uint32_t s_val[OS_TILE];
-    __shared__ uint32_t s_wcnt[4][256];
-    __shared__ uint32_t s_gbase[256];
-    __shared__ uint32_t s_lbase[256];
-    __shared__ uint32_t s_wave[4];
-    __shared__ uint32_t s_bid;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    if (tid == 0) s_bid = atomicAdd(ticket, 1u);
-#pragma unroll
-    for (int w = 0; w < 4; ++w) s_wcnt[w][tid] = 0;
-
-    __syncthreads();
-    const uint32_t bid = s_bid;
-    const uint32_t mask = (1u << nbits) - 1u;
-    const uint64_t lt = lanemask_lt();
-    const size_t base = (size_t)bid * OS_TILE + (size_t)wave * (64 * OS_ITEMS);
-    uint32_t key[OS_ITEMS], val[OS_ITEMS], rank[OS_ITEMS];
-#pragma unroll
-    for (int r = 0; r < OS_ITEMS; ++r) {
-        const size_t idx = base + (size_t)r * 64 + lane;
-        const bool valid = idx < n;
-        key[r] = valid ? keys_in[idx] : 0u;
-        val[r] = valid ? vals_in[idx] : 0u;
-    }
-#pragma unroll
-    for (int r = 0; r < OS_ITEMS; ++r) {
-        const bool valid = base + (size_t)r * 64 + lane < n;
-        const uint32_t d = (key[r] >> shift) & mask;
-        const uint64_t peers = match_digit(d, valid, nbits);
-        const uint32_t before = s_wcnt[wave][d];
-        const uint32_t pr = (uint32_t)__popcll(peers & lt);
-        rank[r] = before + pr;
-        __builtin_amdgcn_wave_barrier();
-        if (valid && pr == 0) s_wcnt[wave][d] = before + (uint32_t)__popcll(peers);
-        __builtin_amdgcn_wave_barrier();
-    }
-    __syncthreads();
-
-    // thread tid = digit: block count, per-wave offsets, look-back, local and global bases
-    const uint32_t c0 = s_wcnt[0][tid], c1 = s_wcnt[1][tid], c2 = s_wcnt[2][tid], c3 = s_wcnt[3][tid];
-    const uint32_t total = c0 + c1 + c2 + c3;
-    s_wcnt[0][tid] = 0; s_wcnt[1][tid] = c0; s_wcnt[2][tid] = c0 + c1; s_wcnt[3][tid] = c0 + c1 + c2;
-    gu32* st = (gu32*)status;   // global address space: agent-scope atomics compile to global_* sc1
-    uint32_t prefix = 0;
-#ifdef LSR_ABL_NOLOOKBACK
-    if (true) {
-#else
-    if (bid == 0) {
-#endif
-        __hip_atomic_store(st + tid, OS_PRE | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-        __hip_atomic_store(st + (size_t)bid * 256 + tid, OS_AGG | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // window of LSR_LOOKBACK predecessors per round trip, nearest first; stop at an inclusive prefix,
-        // resume at the first one not published yet.  Block 0 always publishes a prefix.
-        uint32_t p = bid;   // predecessors p-1, p-2, ... not consumed yet
-        uint32_t spins = 0;
-        while (true) {
-            constexpr int LB = LSR_LOOKBACK;
-            uint32_t v[LB];
-#pragma unroll
-            for (int j = 0; j < LB; ++j)
-                v[j] = (uint32_t)j < p ? __hip_atomic_load(st + (size_t)(p - 1 - j) * 256 + tid, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT)
-                                       : 0u;
-            bool found = false;
-            uint32_t used = 0;
-#pragma unroll
-            for (int j = 0; j < LB; ++j) {
-                if (found || used != (uint32_t)j || (uint32_t)j >= p) continue;
-                if (v[j] & OS_PRE) { prefix += v[j] & OS_CNT; found = true; }
-                else if (v[j] & OS_AGG) { prefix += v[j] & OS_CNT; ++used; }
-            }
-            if (found) break;
-            p -= used;
-            if (used == 0) {
-                if (++spins > (1u << 22)) { atomicOr(err, 1u); break; }
-                __builtin_amdgcn_s_sleep(1);
-            }
-        }
-        __hip_atomic_store(st + (size_t)bid * 256 + tid, OS_PRE | (prefix + total), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
-    uint32_t hcount = 0;
-#pragma unroll
-    for (int c = 0; c < HIST_COPIES; ++c) hcount += hist[c * HIST_WORDS + tid];
-    const uint32_t dstart = block_excl_scan256(hcount, s_wave);      // global start of digit tid
-    const uint32_t lbase = block_excl_scan256(total, s_wave);        // local start of digit tid
-    s_lbase[tid] = lbase;
-    s_gbase[tid] = dstart + prefix - lbase;
-    __syncthreads();
-    // digit-sorted placement in LDS, then runs to global
-    const size_t tile0 = (size_t)bid * OS_TILE;
-    const int ntile = (int)min((size_t)OS_TILE, n - min(n, tile0));
-#pragma unroll
-    for (int r = 0; r < OS_ITEMS; ++r) {
-        const bool valid = base + (size_t)r * 64 + lane < n;
-        if (valid) {
-            const uint32_t d = (key[r] >> shift) & mask;
-            const uint32_t pos = s_lbase[d] + s_wcnt[wave][d] + rank[r];
-            s_key[pos] = key[r];
-            s_val[pos] = val[r];
-        }
-    }
-    __syncthreads();
-    for (int i = tid; i < ntile; i += 256) {
-        const uint32_t k = s_key[i];
-        const uint32_t dst = s_gbase[(k >> shift) & mask] + (uint32_t)i;
-        keys_out[dst] = k;
-        vals_out[dst] = s_val[i];
-    }
-}
-
-// ---- reduce-then-scan passes (LSR_SORT_LOOKBACK=0) ---------------------------------------------
-// The same stable pass without the decoupled look-back: a count kernel writes every block's 256
-// digit counts, a scan kernel (one block per digit) turns them into each block's offset inside
-// the digit, and the scatter kernel ranks and places exactly as k_radix_pass, its global base
-// read instead of chained.  The look-back chain crosses the 8 XCDs' non-coherent L2s at every
-// hop (each an agent-scope round trip through the fabric, ~0.5-1 us), which bounded a pass by
-// the chain length; here the keys are read once more (4 B / key) and two small launches are
-// added per pass.
+// ---- reduce-then-scan passes ------------------------------------------------------------------
 //   drop (first pass of a sort with a kept-count word): keys equal to 0xFFFFFFFF are not counted
 //   and not placed; the scatter's block 0 writes the number of kept keys to *kept_out.
 //   n_dev (later passes): the number of keys is *n_dev (<= n); blocks past it write zero counts
@@ -469,9 +264,9 @@ __global__ void __launch_bounds__(256) k_radix_pass(const uint32_t* __restrict__
 __device__ __forceinline__ size_t rts_n(size_t n, const uint32_t* n_dev) {
     return n_dev ? min(n, (size_t)*n_dev) : n;
 }
-// A segment's workspace: digit totals [pass][256] at the front (the look-back layout's histogram
-// area), then the per-pass count rows [pass][block][256].
-constexpr size_t RTS_ROWS_OFF = (HIST_COPIES * HIST_WORDS * 4 + 64 + 255) / 256 * 256;
+// A segment's workspace: digit totals [pass][256] at the front, then the per-pass count rows
+// [pass][block][256].
+constexpr size_t RTS_ROWS_OFF = 4 * 256 * 4;
 __device__ __forceinline__ size_t rts_blocks(size_t n, int it) { return (n + 256 * (size_t)it - 1) / (256 * (size_t)it); }
 __device__ __forceinline__ uint32_t* rts_rows(const SortSeg& g, int pass, size_t nbi) {
     return reinterpret_cast<uint32_t*>(static_cast<char*>(g.temp) + RTS_ROWS_OFF) + (size_t)pass * nbi * 256;
@@ -517,39 +312,10 @@ __global__ void __launch_bounds__(256) k_rts_count(const SortBatch b, int pass, 
     counts[(size_t)blockIdx.x * 256 + tid] = s_h[0][tid] + s_h[1][tid] + s_h[2][tid] + s_h[3][tid];
 }
 
-// One block per (digit, segment): the digit's count row over the segment's blocks becomes each
-// block's offset within the digit; the digit total goes to the segment's totals.
-__global__ void __launch_bounds__(256) k_rts_scan(const SortBatch b, int pass, int it) {
-    __shared__ uint32_t s_wave[4];
-    const SortSeg& sg = b.s[blockIdx.y];
-    const int nb = (int)rts_blocks(sg.n, it);
-    uint32_t* __restrict__ counts = rts_rows(sg, pass, (size_t)nb);
-    const int d = blockIdx.x, tid = threadIdx.x;
-    uint32_t carry = 0;
-    for (int b0 = 0; b0 < nb; b0 += SCAN_TILE) {
-        uint32_t v[SCAN_ITEMS];
-#pragma unroll
-        for (int i = 0; i < SCAN_ITEMS; ++i) {
-            const int bb = b0 + tid * SCAN_ITEMS + i;
-            v[i] = bb < nb ? counts[(size_t)bb * 256 + d] : 0u;
-        }
-        uint32_t total;
-        block_exclusive_scan8(v, s_wave, total);
-#pragma unroll
-        for (int i = 0; i < SCAN_ITEMS; ++i) {
-            const int bb = b0 + tid * SCAN_ITEMS + i;
-            if (bb < nb) counts[(size_t)bb * 256 + d] = v[i] + carry;
-        }
-        carry += total;
-        __syncthreads();   // s_wave reused by the next chunk
-    }
-    if (tid == 0) rts_totals(sg, pass)[d] = carry;
-}
-
-// The same scan, one block per (16-digit group, segment) instead of per digit: thread t owns
+// The scan, one block per (16-digit group, segment): thread t owns
 // SCAN16_ROWS consecutive block rows of a chunk and reads each row's 16 counts as one 64-byte
 // piece (four 16-byte loads, all in flight at once), so the count table is read once in whole
-// pieces instead of one 4-byte word per (row, digit block) -- the per-digit kernel touched every
+// pieces instead of one 4-byte word per (row, digit block) -- a per-digit scan kernel touched every
 // line of the table from 256 blocks (33 us per depth pass, 58 us per tile pass on 8 views).
 // Digit groups past 2^nbits (the tile sort's 7- and 6-bit passes) only zero their totals.
 constexpr int SCAN16_ROWS = 8;
@@ -732,20 +498,11 @@ __global__ void __launch_bounds__(256) k_rts_scatter(const SortBatch b, int pass
     }
 }
 
-bool radix_sort_fuses_gather() { return !LSR_SORT_LOOKBACK; }
-
 static size_t os_blocks(size_t n) { return (n + OS_TILE - 1) / OS_TILE; }
 
 size_t radix_temp_bytes(size_t n) {
-    // hist [HIST_COPIES][4][256] | tickets [4] | err [1] (padded) | status [4][blocks][256]
-    return align_up(HIST_COPIES * HIST_WORDS * 4 + 64, 256) + align_up(4 * os_blocks(n) * 256 * 4, 256);
-}
-
-size_t radix_temp_zero_bytes(size_t n, int begin_bit, int end_bit) {
-    if (n == 0 || end_bit <= begin_bit) return 0;
-    if (!LSR_SORT_LOOKBACK) return 0;   // reduce-then-scan writes every word it reads
-    const int npass = (end_bit - begin_bit + 7) / 8;
-    return align_up(HIST_COPIES * HIST_WORDS * 4 + 64, 256) + (size_t)npass * os_blocks(n) * 256 * 4;
+    // digit totals [4][256] | count rows [4][blocks][256] (blocks of OS_TILE keys: the most rows)
+    return RTS_ROWS_OFF + align_up(4 * os_blocks(n) * 256 * 4, 256);
 }
 
 bool radix_sort_batch(const SortSeg* segs, int nseg, int begin_bit, int end_bit, hipStream_t st) {
@@ -770,11 +527,7 @@ bool radix_sort_batch(const SortSeg* segs, int nseg, int begin_bit, int end_bit,
             hipLaunchKernelGGL(k_rts_count<12>, dim3(nbi, ns), dim3(256), 0, st, bt, p, (int)in_b, shift, nbits);
         else
             hipLaunchKernelGGL(k_rts_count<OS_ITEMS>, dim3(nbi, ns), dim3(256), 0, st, bt, p, (int)in_b, shift, nbits);
-#if LSR_SORT_SCAN_DIGIT
-        hipLaunchKernelGGL(k_rts_scan, dim3(256, ns), dim3(256), 0, st, bt, p, items);
-#else
         hipLaunchKernelGGL(k_rts_scan16, dim3(16, ns), dim3(256), 0, st, bt, p, items, nbits);
-#endif
         if (items == 12)
             hipLaunchKernelGGL(k_rts_scatter<12>, dim3(nbi, ns), dim3(256), 0, st, bt, p, (int)in_b, shift, nbits, last);
         else
@@ -786,43 +539,10 @@ bool radix_sort_batch(const SortSeg* segs, int nseg, int begin_bit, int end_bit,
 }
 
 bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b, size_t n,
-                      int begin_bit, int end_bit, void* temp, uint32_t* err, hipStream_t st, bool temp_zeroed,
-                      uint32_t* kept, const SortGather* gather) {
+                      int begin_bit, int end_bit, void* temp, hipStream_t st, uint32_t* kept, const SortGather* gather) {
     if (n == 0 || end_bit <= begin_bit) return false;
-#if !LSR_SORT_LOOKBACK
-    // reduce-then-scan: no up-front histogram (each pass's scan kernel yields the digit totals)
-    // and no timeouts (err unused)
-    (void)err; (void)temp_zeroed;
     SortSeg sg{keys_a, vals_a, keys_b, vals_b, temp, kept, gather ? *gather : SortGather{nullptr, nullptr, nullptr}, n};
     return radix_sort_batch(&sg, 1, begin_bit, end_bit, st);
-#else
-    const size_t nb = os_blocks(n);
-    uint32_t* hist = reinterpret_cast<uint32_t*>(temp);
-    uint32_t* tickets = hist + HIST_COPIES * HIST_WORDS;
-    uint32_t* own_err = tickets + 4;
-    uint32_t* status =
-        reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(temp) + align_up(HIST_COPIES * HIST_WORDS * 4 + 64, 256));
-    const size_t zb = radix_temp_zero_bytes(n, begin_bit, end_bit);
-    if (!temp_zeroed && zb) (void)hipMemsetAsync(temp, 0, zb, st);
-    bool in_b = false;
-    (void)gather;   // not fused here: the caller gathers (radix_sort_fuses_gather() is false)
-    if (kept) (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(kept), (int)n, 1, st);   // no dropping here
-    const unsigned hb = (unsigned)min((size_t)OS_HIST_BLOCKS, (n + 64 * HIST_ITEMS * 4 - 1) / (64 * HIST_ITEMS * 4));
-    hipLaunchKernelGGL(k_radix_hist, dim3(hb), dim3(256), 0, st, (const uint32_t*)keys_a, n, begin_bit, end_bit, hist);
-    int p = 0;
-    for (int shift = begin_bit; shift < end_bit; shift += 8, ++p) {
-        const int nbits = (end_bit - shift) < 8 ? (end_bit - shift) : 8;
-        const uint32_t* kin = in_b ? keys_b : keys_a;
-        const uint32_t* vin = in_b ? vals_b : vals_a;
-        uint32_t* kout = in_b ? keys_a : keys_b;
-        uint32_t* vout = in_b ? vals_a : vals_b;
-        hipLaunchKernelGGL(k_radix_pass, dim3((unsigned)nb), dim3(256), 0, st, kin, vin, kout, vout, n, shift, nbits,
-                           (const uint32_t*)(hist + p * 256), status + (size_t)p * nb * 256, tickets + p,
-                           err ? err : own_err);
-        in_b = !in_b;
-    }
-    return in_b;
-#endif
 }
 
 }  // namespace lsr

@@ -89,36 +89,13 @@ class _NativeSettings:
 
 
 class RasterizerState:
-    """What the forward leaves for the backward (upstream: num_rendered + geom/binning/img buffers).
+    """What the forward leaves for the backward (upstream: num_rendered + geom/binning/img buffers)."""
 
-    sort_status: the forward's sort status words (lsr_forward_status, pinned host memory) and the
-    event after which they are valid; check_sorts() raises if a sort's look-back timed out (the
-    compositor has then already written NaN outputs).  Every backward entry point checks it, which
-    costs no wait: the forward finished long before its backward is enqueued behind it."""
-
-    def __init__(self, settings, inputs, fin, geom, binning, img, num_rendered, radii, sort_status=None):
+    def __init__(self, settings, inputs, fin, geom, binning, img, num_rendered, radii):
         self.settings, self.inputs, self.fin = settings, inputs, fin
         self.geom, self.binning, self.img = geom, binning, img
         self.num_rendered, self.radii = num_rendered, radii
-        self.sort_status = sort_status    # (pinned int32 [2], event) or None
         self.composited = False           # backward_composite_native ran (it may run once)
-
-    def check_sorts(self, event=None):
-        """event: one recorded after this forward on its stream, for forwards rendered with
-        render_native(status_event=False) (ignored when the forward recorded its own)."""
-        if self.sort_status is None:
-            return self
-        words, ev = self.sort_status
-        ev = ev or event
-        if ev is None:
-            raise RuntimeError("check_sorts: this forward recorded no status event; pass one recorded after it")
-        ev.synchronize()
-        self.sort_status = None
-        bad = [name for name, w in zip(("depth sort", "tile sort"), words.tolist()) if w]
-        if bad:
-            raise RuntimeError("rasterizer forward: " + " and ".join(bad) + " look-back timed out "
-                               "(outputs are NaN; this forward cannot be backpropagated)")
-        return self
 
 
 def _stream(device):
@@ -136,7 +113,7 @@ class PendingForward:
         self.ready = None                  # event recorded after that binning
         self.ready_stream = None           # the stream `ready` was recorded on
         self.count_host = None             # deferred count (preprocess_native(defer_count=True)): pinned
-        self.counted = None                # [K, error word], valid once `counted` (an event) has passed
+        self.counted = None                # [K, reserved], valid once `counted` (an event) has passed
         self.stream = None
         self.count_batch = None            # (pinned [n, 2] counts of a batch, this view's row)
 
@@ -147,10 +124,7 @@ class PendingForward:
             return self
         self.counted.synchronize()
         self.counted = None
-        K, err = int(self.count_host[0]), int(self.count_host[1])
-        if err:
-            raise RuntimeError("lsr_forward_preprocess: depth sort: look-back timed out")
-        self.num_rendered = K
+        self.num_rendered = int(self.count_host[0])
         if binning:
             _run_binning(self, self.stream)
         return self
@@ -307,7 +281,7 @@ def preprocess_views_native(raster_settings_list, means3D, opacities, shs=None, 
     stream = stream or torch.cuda.current_stream(device)
     fin, inputs, P = _fwd_inputs(means3D, opacities, shs, colors_precomp, language_feature, scales, rotations,
                                  cov3D_precomp)
-    if split_language and fin.C == 32 and P > 0 and _lib.has("lsr_language_split"):
+    if split_language and fin.C == 32 and P > 0:
         inputs["language_feature_split"] = language_split_native(inputs["language_feature"], stream=stream)
         fin.language_feature_split = inputs["language_feature_split"].data_ptr()
     n = len(raster_settings_list)
@@ -371,10 +345,7 @@ def binning_views_native(pendings, stream=None):
         pendings[0].counted.synchronize()
         rows = batch[0].tolist()
         for pf in pendings:
-            K, err = rows[pf.count_batch[1]]
-            if err:
-                raise RuntimeError("lsr_forward_preprocess: depth sort: look-back timed out")
-            pf.num_rendered, pf.counted = K, None
+            pf.num_rendered, pf.counted = rows[pf.count_batch[1]][0], None
     else:
         for pf in pendings:
             pf.resolve()
@@ -408,13 +379,9 @@ def binning_views_native(pendings, stream=None):
         pf.ready, pf.ready_stream = ev, stream
 
 
-def render_native(pending: PendingForward, status_event=True):
+def render_native(pending: PendingForward):
     """Forward phase 2 (binning unless preprocess_native already did it, then compositing) on the
-    current stream.  Returns (color, language_feature, radii, depth, state).
-
-    status_event=False records no event for the sort status words (an event record between two
-    launches idles the device ~15 us): the caller then checks them with check_sorts(event) on an
-    event recorded later on the same stream (backward_preprocess_views_native does)."""
+    current stream.  Returns (color, language_feature, radii, depth, state)."""
     L = _lib.load()
     pending.resolve()
     device, H, W, C = pending.device, pending.H, pending.W, pending.fin.C
@@ -427,8 +394,6 @@ def render_native(pending: PendingForward, status_event=True):
     fout = _lib.FwdOut()
     fout.out_color, fout.out_language_feature = color.data_ptr(), _ptr(lang_out) if C > 0 else None
     fout.radii, fout.out_depth = pending.radii.data_ptr(), depth.data_ptr()
-    status = torch.zeros(2, dtype=torch.int32, pin_memory=True)   # the compositor writes the sort status here
-    fout.host_sort_status = status.data_ptr()
     K = pending.num_rendered
     binned = pending.binning is not None
     if binned:
@@ -455,17 +420,7 @@ def render_native(pending: PendingForward, status_event=True):
     except RuntimeError:
         _dump_forward(pending.raster_settings, pending.inputs)
         raise
-    ev = None
-    if status_event:
-        ev = torch.cuda.Event()
-        ev.record(stream)
-    state = RasterizerState(pending.settings, pending.inputs, pending.fin, pending.geom, binning, img, K, pending.radii,
-                            sort_status=(status, ev))
-    if pending.raster_settings.debug:
-        if ev is None:
-            ev = torch.cuda.Event()
-            ev.record(stream)
-        state.check_sorts(ev)
+    state = RasterizerState(pending.settings, pending.inputs, pending.fin, pending.geom, binning, img, K, pending.radii)
     return color, lang_out, pending.radii, depth, state
 
 
@@ -484,7 +439,6 @@ def backward_native(state: RasterizerState, grad_color, grad_lang=None, grad_dep
     accumulate=True they are added to.  deterministic=True selects the fixed-order reduction
     (bitwise reproducible gradients).  Returns the dict of gradient tensors."""
     L = _lib.load()
-    state.check_sorts()
     inp = state.inputs
     means3D = inp["means3D"]
     device = means3D.device
@@ -553,7 +507,6 @@ def backward_views_native(states, grad_colors, grad_langs=None, grad_depths=None
         if s.composited:
             raise RuntimeError("a view's forward was already backpropagated through its workspace accumulators "
                                "(backward_composite_native / backward_views_native run once per forward)")
-        s.check_sorts()
     st0 = states[0]
     inp = st0.inputs
     for s in states[1:]:
@@ -628,21 +581,14 @@ class CompositeGrad:
 
 
 def backward_composite_native(state: RasterizerState, grad_color, grad_lang=None, grad_depth=None,
-                              dL_dlanguage=None, defer_sort_check=False) -> CompositeGrad:
+                              dL_dlanguage=None) -> CompositeGrad:
     """First half of backward_views_native for ONE view (lsr_backward_composite), on the current
     stream: the compositor backward; the language gradient is ADDED to dL_dlanguage [P,C] (the
-    caller zeroes it once per batch).  Finish a batch with backward_preprocess_views_native.
-
-    defer_sort_check=True leaves the forward's sort-status check to backward_preprocess_views_native
-    (which raises before it returns the batch's gradients): checking here would make the host wait
-    for the forward that was enqueued just before, and the device would idle until this call's
-    launches arrive."""
+    caller zeroes it once per batch).  Finish a batch with backward_preprocess_views_native."""
     L = _lib.load()
     if state.composited:
         raise RuntimeError("backward_composite_native already ran on this forward: its screen-space sums are "
                            "accumulated in the forward's workspace, so a second run would double them")
-    if not defer_sort_check:
-        state.check_sorts()
     device = state.inputs["means3D"].device
     P, C = state.fin.P, state.fin.C
     H, W = state.settings.c.image_height, state.settings.c.image_width
@@ -664,10 +610,15 @@ def backward_composite_native(state: RasterizerState, grad_color, grad_lang=None
     return CompositeGrad(state, (gc, gl, gd))
 
 
-def backward_preprocess_views_native(parts, out=None, accumulate=False, need=None):
+def backward_preprocess_views_native(parts, out=None, accumulate=False, need=None, row_chunks=None, on_rows=None):
     """Second half of backward_views_native (lsr_backward_preprocess_views): the preprocess backward
     of every view in `parts` (CompositeGrad), summed into one set of gradient rows.  The language
-    gradient is not touched here (the composite halves added it).  Returns the dict of gradients."""
+    gradient is not touched here (the composite halves added it).  Returns the dict of gradients.
+
+    row_chunks: [(r0, r1), ...] covering [0, P) in order (r0 multiples of 256): one launch per chunk
+    (lsr_backward_preprocess_views_rows), and on_rows(r0, r1) is called right after each chunk's
+    launch is enqueued, so a data-parallel caller can start that chunk's all-reduce while the next
+    chunk computes."""
     L = _lib.load()
     n = len(parts)
     if n == 0:
@@ -678,24 +629,34 @@ def backward_preprocess_views_native(parts, out=None, accumulate=False, need=Non
         if p_.state.inputs["means3D"].data_ptr() != inp["means3D"].data_ptr():
             raise ValueError("all views must render the same Gaussians")
     device = inp["means3D"].device
-    # deferred sort checks (backward_composite_native(defer_sort_check)): one event before this
-    # launch covers every view's forward; the host waits on it only after the launch is enqueued,
-    # so the device runs this batch while the host checks (a failed check still raises here)
-    covered = torch.cuda.Event()
-    covered.record(torch.cuda.current_stream(device))
     need = dict(need or {})
     need["language_feature"] = False
     g = _grad_buffers(st0, out, accumulate, need)
     gout = _bwd_out(g)
     SP = ctypes.POINTER(_lib.Settings)
     vp = ctypes.c_void_p * n
-    _lib.check(L.lsr_backward_preprocess_views(n, (SP * n)(*[ctypes.pointer(p_.state.settings.c) for p_ in parts]),
-                                               ctypes.byref(st0.fin), ctypes.byref(gout),
-                                               vp(*[p_.state.geom.data_ptr() for p_ in parts]),
-                                               1 if accumulate else 0, _stream(device)),
-               "lsr_backward_preprocess_views")
-    for p_ in parts:
-        p_.state.check_sorts(covered)
+    s_arr = (SP * n)(*[ctypes.pointer(p_.state.settings.c) for p_ in parts])
+    geoms = vp(*[p_.state.geom.data_ptr() for p_ in parts])
+    if row_chunks is None:
+        _lib.check(L.lsr_backward_preprocess_views(n, s_arr, ctypes.byref(st0.fin), ctypes.byref(gout), geoms,
+                                                   1 if accumulate else 0, _stream(device)),
+                   "lsr_backward_preprocess_views")
+    else:
+        P = st0.fin.P
+        expect = 0
+        for r0, r1 in row_chunks:
+            if r0 != expect or r1 < r0 or r1 > P:
+                raise ValueError(f"row_chunks must tile [0, {P}) in order, got {list(row_chunks)}")
+            expect = r1
+            part = {k: (v[r0:r1] if v is not None else None) for k, v in g.items()}
+            gc = _bwd_out(part)
+            _lib.check(L.lsr_backward_preprocess_views_rows(n, s_arr, ctypes.byref(st0.fin), ctypes.byref(gc), geoms,
+                                                            1 if accumulate else 0, r0, r1 - r0, _stream(device)),
+                       "lsr_backward_preprocess_views_rows")
+            if on_rows is not None:
+                on_rows(r0, r1)
+        if expect != P:
+            raise ValueError(f"row_chunks must tile [0, {P}) in order, got {list(row_chunks)}")
     return g
 
 

@@ -13,6 +13,7 @@ _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("LSR_LIBRARY", os.path.join(_PKG, "build", "liblsr.so"))
 
 c_float_p = ctypes.c_void_p  # device pointers are passed as opaque addresses
+API_VERSION = 4               # LSR_API_VERSION of the include/lsr.h these structs mirror
 
 
 class Settings(ctypes.Structure):
@@ -32,13 +33,13 @@ class FwdIn(ctypes.Structure):
         ("means3D", ctypes.c_void_p), ("shs", ctypes.c_void_p), ("colors_precomp", ctypes.c_void_p),
         ("language_feature", ctypes.c_void_p), ("opacities", ctypes.c_void_p), ("scales", ctypes.c_void_p),
         ("rotations", ctypes.c_void_p), ("cov3D_precomp", ctypes.c_void_p),
-        ("language_feature_split", ctypes.c_void_p),   # API 3 (older libraries ignore the trailing field)
+        ("language_feature_split", ctypes.c_void_p),
     ]
 
 
 class FwdOut(ctypes.Structure):
     _fields_ = [("out_color", ctypes.c_void_p), ("out_language_feature", ctypes.c_void_p),
-                ("radii", ctypes.c_void_p), ("out_depth", ctypes.c_void_p), ("host_sort_status", ctypes.c_void_p)]
+                ("radii", ctypes.c_void_p), ("out_depth", ctypes.c_void_p)]
 
 
 class BwdIn(ctypes.Structure):
@@ -55,19 +56,22 @@ class BwdOut(ctypes.Structure):
 
 # every symbol include/lsr.h declares, with its ctypes signature
 class DeformNet(ctypes.Structure):
-    """include/lsr_deform.h lsr_deform_net"""
+    """include/lsr_deform.h lsr_deform_net (LSR_DEFORM_API_VERSION 2)"""
     _fields_ = [("n_scales", ctypes.c_int32), ("channels", ctypes.c_int32), ("width", ctypes.c_int32),
-                ("res", ctypes.c_int32 * 4), ("multires", ctypes.c_int32 * 4), ("aabb", ctypes.c_void_p),
-                ("planes", (ctypes.c_void_p * 6) * 4), ("w_feat", ctypes.c_void_p), ("b_feat", ctypes.c_void_p),
-                ("w1", ctypes.c_void_p * 5), ("b1", ctypes.c_void_p * 5), ("w2", ctypes.c_void_p * 5),
-                ("b2", ctypes.c_void_p * 5)]
+                ("res", ctypes.c_int32 * 4), ("multires", ctypes.c_int32 * 4), ("depth", ctypes.c_int32),
+                ("heads", ctypes.c_uint32), ("apply_rotation", ctypes.c_int32), ("lang_mode", ctypes.c_int32),
+                ("lang_dim", ctypes.c_int32), ("centers", ctypes.c_int32), ("time_pe", ctypes.c_int32),
+                ("aabb", ctypes.c_void_p), ("planes", (ctypes.c_void_p * 6) * 4),
+                ("w_feat", ctypes.c_void_p * 4), ("b_feat", ctypes.c_void_p * 4),
+                ("w1", ctypes.c_void_p * 6), ("b1", ctypes.c_void_p * 6), ("w2", ctypes.c_void_p * 6),
+                ("b2", ctypes.c_void_p * 6), ("w_lang", ctypes.c_void_p * 3), ("b_lang", ctypes.c_void_p * 3)]
 
 
 class DeformGrads(ctypes.Structure):
     """include/lsr_deform.h lsr_deform_grads"""
-    _fields_ = [("planes", (ctypes.c_void_p * 6) * 4), ("w_feat", ctypes.c_void_p), ("b_feat", ctypes.c_void_p),
-                ("w1", ctypes.c_void_p * 5), ("b1", ctypes.c_void_p * 5), ("w2", ctypes.c_void_p * 5),
-                ("b2", ctypes.c_void_p * 5)]
+    _fields_ = [("planes", (ctypes.c_void_p * 6) * 4), ("w_feat", ctypes.c_void_p * 4), ("b_feat", ctypes.c_void_p * 4),
+                ("w1", ctypes.c_void_p * 6), ("b1", ctypes.c_void_p * 6), ("w2", ctypes.c_void_p * 6),
+                ("b2", ctypes.c_void_p * 6), ("w_lang", ctypes.c_void_p * 3), ("b_lang", ctypes.c_void_p * 3)]
 
 
 class AdamGroup(ctypes.Structure):
@@ -101,6 +105,7 @@ SIGNATURES = {
                                        _vp, _vp]),
     "lsr_reset_opacity": (ctypes.c_int, [ctypes.c_int32, _vp, _vp, _vp, _vp]),
     "lsr_version": (ctypes.c_int, []),
+    "lsr_require_api": (ctypes.c_int, [ctypes.c_int32]),
     "lsr_last_error": (ctypes.c_char_p, []),
     "lsr_geom_bytes": (ctypes.c_int64, [ctypes.c_int32]),
     "lsr_binning_bytes": (ctypes.c_int64, [ctypes.c_int64]),
@@ -127,8 +132,6 @@ SIGNATURES = {
     "lsr_forward_composite": (ctypes.c_int, [ctypes.POINTER(Settings), ctypes.POINTER(FwdIn), ctypes.POINTER(FwdOut),
                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                              ctypes.c_void_p]),
-    "lsr_forward_status": (ctypes.c_int, [ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
-    "lsr_test_inject_sort_fault": (ctypes.c_int, [ctypes.c_uint32]),
     "lsr_backward": (ctypes.c_int, [ctypes.POINTER(Settings), ctypes.POINTER(FwdIn), ctypes.POINTER(BwdIn),
                                     ctypes.POINTER(BwdOut), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p]),
@@ -143,6 +146,10 @@ SIGNATURES = {
     "lsr_backward_preprocess_views": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(ctypes.POINTER(Settings)),
                                                      ctypes.POINTER(FwdIn), ctypes.POINTER(BwdOut),
                                                      ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32, ctypes.c_void_p]),
+    "lsr_backward_preprocess_views_rows": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(ctypes.POINTER(Settings)),
+                                                          ctypes.POINTER(FwdIn), ctypes.POINTER(BwdOut),
+                                                          ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32,
+                                                          ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]),
     "lsr_language_split": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_void_p]),
     "lsr_mark_visible": (ctypes.c_int, [ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -155,21 +162,13 @@ SIGNATURES = {
     "lsr_deform_workspace_bytes": (ctypes.c_int64, [ctypes.POINTER(DeformNet)]),
     "lsr_deform_prepare": (ctypes.c_int, [ctypes.POINTER(DeformNet), ctypes.c_void_p, ctypes.c_void_p]),
     "lsr_deform_forward": (ctypes.c_int, [ctypes.POINTER(DeformNet), ctypes.c_void_p, ctypes.c_int32]
-                           + [ctypes.c_void_p] * 11 + [ctypes.c_void_p]),
+                           + [ctypes.c_void_p] * 14 + [ctypes.c_void_p]),
     "lsr_deform_backward_scratch_bytes": (ctypes.c_int64, [ctypes.POINTER(DeformNet), ctypes.c_int32]),
     "lsr_deform_backward": (ctypes.c_int, [ctypes.POINTER(DeformNet), ctypes.c_void_p, ctypes.c_int32]
-                            + [ctypes.c_void_p] * 8 + [ctypes.POINTER(DeformGrads), ctypes.c_void_p, ctypes.c_void_p]),
+                            + [ctypes.c_void_p] * 14 + [ctypes.POINTER(DeformGrads), ctypes.c_void_p, ctypes.c_void_p]),
     "lsr_profile_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64),
                                         ctypes.c_int32]),
 }
-
-# entry points newer builds add; callers check has() (variant libraries of older revisions lack them)
-OPTIONAL = {"lsr_forward_preprocess_views_async", "lsr_forward_binning_views", "lsr_language_split"}
-
-
-def has(name):
-    return hasattr(load(), name)
-
 
 PHASES = ["preprocess", "depth_sort", "instance_scan", "emit", "tile_sort", "tile_ranges", "render_fwd",
           "render_bwd", "preprocess_bwd", "preprocess_bwd_views"]
@@ -203,11 +202,11 @@ def load():
                               "(or __graft_entry__.build()).  There is no CPU fallback.")
         lib = ctypes.CDLL(path)
         for name, (res, args) in SIGNATURES.items():
-            if name in OPTIONAL and not hasattr(lib, name):   # an older build (A/B runs): has() says so
-                continue
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        if lib.lsr_require_api(API_VERSION) != 0:
+            raise ImportError(f"{path}: {lib.lsr_last_error().decode()} (rebuild it: make -C 4dlangsplat_amd/csrc)")
         _LIB = lib
     return _LIB
 

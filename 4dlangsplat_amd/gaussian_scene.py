@@ -239,7 +239,10 @@ def render(viewpoint_camera, pc: GaussianScene, bg_color: torch.Tensor, scaling_
         # inside autograd (training) the field's backward runs (DeformationField.apply)
         deform = pc.deformation.apply if (torch.is_grad_enabled() and hasattr(pc.deformation, "apply")) \
             else pc.deformation
-        m3, s3, r3, o3, sh3, l3, coff = deform(means3D, scales, rotations, opacity, shs, lang, t)
+        # 'base' stages pass the language through (the reference sets no_dlang = 1 there,
+        # gaussian_renderer/__init__.py:121-124)
+        m3, s3, r3, o3, sh3, l3, coff = deform(means3D, scales, rotations, opacity, shs, lang, t,
+                                               no_dlang=True if "base" in stage else None)
     else:
         raise NotImplementedError(stage)
     s3 = torch.exp(s3) if s3 is not None else None

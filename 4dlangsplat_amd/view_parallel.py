@@ -19,6 +19,7 @@ data-path collective: views are independent (SURVEY.md 8(e) "Shards naturally? Y
 The per-view work is a callback so that the same step runs the native HIP rasterizer
 (native_view_renderer, the product path) or, in tests only, the CPU oracle.
 """
+import os
 from typing import Callable, Dict, Optional, Tuple
 
 import torch
@@ -27,6 +28,34 @@ import torch.distributed as dist
 # gradient fields of the flat bucket, in order; None = width depends on M (SH) or C (language)
 GRAD_FIELDS = (("means3D", 3), ("scales", 3), ("rotations", 4), ("opacities", 1), ("sh", None),
                ("language_feature", None))
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_child(rank: int, fn: Callable, world: int, fn_args: tuple):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_WORLD_SIZE=str(world))
+    fn(rank, world, *fn_args)
+
+
+def launch_ranks(world: int, fn: Callable, fn_args: tuple = ()) -> None:
+    """One process per rank on this node without torchrun: spawns `world` children (fresh
+    interpreters, so call this before the parent touches the GPU) with the torchrun environment
+    (RANK, LOCAL_RANK, WORLD_SIZE; MASTER_ADDR 127.0.0.1 and a free MASTER_PORT unless set) and
+    runs fn(rank, world, *fn_args) in each; raises if any rank fails.  The children initialise
+    their own process group ("nccl" = RCCL on the GPU, "gloo" in the CPU tests)."""
+    import torch.multiprocessing as mp
+    if world < 1:
+        raise ValueError(f"world size {world}")
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", str(_free_port()))
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC only on this host driver
+    mp.spawn(_rank_child, args=(fn, world, tuple(fn_args)), nprocs=world, join=True)
 
 
 def view_slice(n_views: int, world: int, rank: int) -> Tuple[int, int]:
@@ -92,6 +121,15 @@ class GradBucket:
         return self.flat.numel() * 4
 
 
+def row_chunks(P: int, n: int, align: int = 256):
+    """[(r0, r1), ...]: [0, P) in at most n contiguous chunks, every r0 a multiple of `align`."""
+    if P <= 0:
+        return [(0, 0)]
+    step = -(-P // max(1, n))
+    step = -(-step // align) * align
+    return [(r0, min(P, r0 + step)) for r0 in range(0, P, step)]
+
+
 class ViewParallelStep:
     """One data-parallel step over a batch of `n_views` views.
 
@@ -100,10 +138,11 @@ class ViewParallelStep:
     Afterwards the bucket holds the SUM over ALL views of the batch on every rank, and
     bucket.radii the MAX over all views (when densify_stats)."""
 
-    def __init__(self, bucket: GradBucket, n_views: int, group=None):
+    def __init__(self, bucket: GradBucket, n_views: int, group=None, flush_chunks: int = 4):
         self.bucket = bucket
         self.n_views = n_views
         self.group = group
+        self.flush_chunks = flush_chunks   # world > 1: the flush in row chunks, each all-reduced as it ends
         self.distributed = dist.is_available() and dist.is_initialized()
         self.world = dist.get_world_size(group) if self.distributed else 1
         self.rank = dist.get_rank(group) if self.distributed else 0
@@ -123,28 +162,43 @@ class ViewParallelStep:
             radii = render_view(v, b)
             if b.radii is not None and radii is not None:
                 torch.maximum(b.radii, radii.to(torch.int32), out=b.radii)
-        early = None
+        pending = []
         lo, hi = b.ranges["language_feature"]
+        if self.world > 1 and b.radii is not None:   # final once the last view's forward ran
+            pending.append(dist.all_reduce(b.radii, op=dist.ReduceOp.MAX, group=self.group, async_op=True))
         if self.world > 1 and flush is not None and hi > lo:
             # with the batched backward the language gradients are final once the last view's
             # compositor backward ran; their SUM runs during the flush (the preprocess backward,
             # which writes every other field) instead of after it
-            early = dist.all_reduce(b.flat[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-        if flush is not None:        # renderers that batch the backward over the rank's views
+            pending.append(dist.all_reduce(b.flat[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+        chunked = self.world > 1 and getattr(flush, "chunked", False) and self.flush_chunks > 1
+        if chunked:
+            # the flush in Gaussian-row chunks: each chunk's rows of every other field are SUMmed
+            # (asynchronously, behind that chunk's launch) while the next chunk is computed
+            def on_rows(r0, r1):
+                for name, (f0, f1) in b.ranges.items():
+                    w = (f1 - f0) // b.P if b.P else 0
+                    if name == "language_feature" or w == 0 or r1 <= r0:
+                        continue
+                    pending.append(dist.all_reduce(b.flat[f0 + r0 * w:f0 + r1 * w], op=dist.ReduceOp.SUM,
+                                                   group=self.group, async_op=True))
+            flush(b, row_chunks=row_chunks(b.P, self.flush_chunks), on_rows=on_rows)
+        elif flush is not None:      # renderers that batch the backward over the rank's views
             flush(b)
         end = getattr(render_view, "end_step", None)
         if end is not None:
             end()
         if self.world > 1:
-            if early is None:
-                dist.all_reduce(b.flat, op=dist.ReduceOp.SUM, group=self.group)
-            else:
-                for seg in (b.flat[:lo], b.flat[hi:]):
+            if not chunked:
+                if flush is not None and hi > lo:
+                    segs = (b.flat[:lo], b.flat[hi:])
+                else:
+                    segs = (b.flat,)
+                for seg in segs:
                     if seg.numel():
                         dist.all_reduce(seg, op=dist.ReduceOp.SUM, group=self.group)
-                early.wait()
-            if b.radii is not None:
-                dist.all_reduce(b.radii, op=dist.ReduceOp.MAX, group=self.group)
+            for h in pending:
+                h.wait()
         return b
 
     def visibility(self) -> torch.Tensor:
@@ -253,11 +307,10 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
             pf.resolve(binning=True)      # count of view v (enqueued a view earlier), then its binning
             if has_view(v + 1):           # view v+1's preprocess ahead of view v's compositing
                 pending[v + 1] = preprocess(v + 1, defer=True)
-        color, lang, radii, depth, st = dgr.render_native(pf, status_event=not batched)   # batched: checked at flush
+        color, lang, radii, depth, st = dgr.render_native(pf)
         gc, gl, gd = grad_fn(v, color, lang, depth)
         if batched:                   # compositor backward now, preprocess backward at flush
-            held.append(dgr.backward_composite_native(st, gc, gl, gd, dL_dlanguage=bucket.views["language_feature"],
-                                                      defer_sort_check=True))   # checked at flush
+            held.append(dgr.backward_composite_native(st, gc, gl, gd, dL_dlanguage=bucket.views["language_feature"]))
         else:
             dgr.backward_native(st, gc, gl, gd, out=bucket.views, accumulate=True, need=bucket.need(),
                                 deterministic=deterministic)
@@ -267,18 +320,23 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
             pending[v + 1] = preprocess(v + 1, stream=side)
         return radii
 
-    def flush(bucket: GradBucket):
+    def flush(bucket: GradBucket, row_chunks=None, on_rows=None):
         # overwrites every field but the language gradients (all P rows, culled ones with zeros), so
         # ViewParallelStep zeroes only the accumulated fields before the views
         if held:
-            dgr.backward_preprocess_views_native(held, out=bucket.views, accumulate=False, need=bucket.need())
+            dgr.backward_preprocess_views_native(held, out=bucket.views, accumulate=False, need=bucket.need(),
+                                                 row_chunks=row_chunks, on_rows=on_rows)
             held.clear()
         else:                             # no views on this rank this step
             lo, hi = bucket.ranges["language_feature"]
             bucket.flat[:lo].zero_()
             bucket.flat[hi:].zero_()
+            for r0, r1 in (row_chunks or []):
+                if on_rows is not None:
+                    on_rows(r0, r1)
 
     flush.overwrites = True
+    flush.chunked = True
 
     def begin_step(views):
         pending.clear()

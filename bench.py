@@ -6,8 +6,10 @@ SURVEY.md 8(d) (seeded; the Neu3D checkpoints are not available offline), replic
 rank; each rank renders V views per step (default 8 = the 64-view batch of configs[3] over 8
 GPUs), forward + full backward of the rasterizer for each view, accumulating all Gaussian
 gradients in one flat fp32 buffer (means3D, scales, rotations, opacities, SH, language
-features = 59 + C floats per Gaussian); with N > 1 ranks the buffer is SUM all-reduced (RCCL)
-once per step.  Upstream gradients dL/dcolor, dL/dlanguage are fixed seeded tensors, so the
+features and the means2D gradient train.py:352-354 feeds to densification = 62 + C floats per
+Gaussian) and the per-Gaussian radii MAX; with N > 1 ranks the buffer is SUM all-reduced (RCCL)
+and the radii MAX all-reduced once per step.  `--gpus N` without torchrun starts the N ranks
+itself (view_parallel.launch_ranks).  Upstream gradients dL/dcolor, dL/dlanguage are fixed seeded tensors, so the
 step is the rasterizer alone.  Inputs are resident in HBM before the timed region.
 
 value = frames (views) rendered fwd+bwd by all ranks / max over ranks of the timed wall time.
@@ -33,10 +35,11 @@ import torch.distributed as dist  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-def phase_bytes(phase, P, Pvis, K, npix, ntiles, C, M=16, accumulate=True, V=1, Pvis_sum=None, Pany=None):
+def phase_bytes(phase, P, Pvis, K, npix, ntiles, C, M=16, accumulate=True, V=1, Pvis_sum=None, Pany=None,
+                means2D=False):
     """Algorithmic HBM bytes of one launch of each phase (each byte counted once).
     preprocess_bwd_views covers V views: Pvis_sum = visible Gaussians summed over them, Pany =
-    Gaussians visible in at least one."""
+    Gaussians visible in at least one; means2D: the screen-space gradient rows are written too."""
     rec = 4 + 8 + 16 + 16 + 4 * C          # id + xy + conic/opacity + rgb/depth + language row
     if phase == "preprocess":              # inputs; radii, radius, tiles, key, rect, sort ids; screen
         return (P * (12 + 12 + 16 + 4 + 4 * 3 * M) + P * (4 + 4 + 4 + 4 + 8 + 4)   # records; zeroed
@@ -61,7 +64,7 @@ def phase_bytes(phase, P, Pvis, K, npix, ntiles, C, M=16, accumulate=True, V=1, 
         grads = 4 * (3 + 3 + 4 + 1 + 3 * M)
         return P * 4 + Pvis * (12 + 12 + 16 + 4 * 3 * M + 1 + 48) + (2 * Pvis * grads if accumulate else P * grads)
     if phase == "preprocess_bwd_views":    # per view: tiles, and for its visible rows clamped + screen sums;
-        grads = 4 * (3 + 3 + 4 + 1 + 3 * M)  # once: Gaussian rows of the visible-anywhere set; gradient rows
+        grads = 4 * (3 + 3 + 4 + 1 + 3 * M + (3 if means2D else 0))  # once: rows of the visible-anywhere set; grads
         return (V * P * 4 + Pvis_sum * (1 + 48) + Pany * (12 + 12 + 16 + 4 * 3 * M)   # RMW, or all P written
                 + (2 * Pany * grads if accumulate else P * grads))
     return 0
@@ -93,7 +96,31 @@ def cpu_baseline(scene, cams, C, threads):
     return tf + tb, tf, tb
 
 
-def main():
+def host_cpu():
+    """Host cores the CPU baseline may use (the process's affinity, capped by a cgroup CPU quota)
+    and the host's description: os.cpu_count(), lscpu model, threads per core."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except Exception:
+        pass
+    info = dict(os_cpu_count=os.cpu_count(), affinity=n, cgroup_quota=quota)
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in ("Model name", "Thread(s) per core", "Socket(s)", "Core(s) per socket"):
+                info[k.strip().lower().replace("(s)", "s").replace(" ", "_")] = v.strip()
+    except Exception:
+        pass
+    return min(n, quota) if quota else n, info
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -103,7 +130,8 @@ def main():
     ap.add_argument("--channels", type=int, default=32)
     ap.add_argument("--width", type=int, default=1352)
     ap.add_argument("--height", type=int, default=1014)
-    ap.add_argument("--cpu-threads", type=int, default=0, help="oracle threads (0 = min(16, cpus))")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="oracle threads (0 = every core available to the process)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=3, help="headline frames timed on the CPU oracle")
     ap.add_argument("--no-profile", action="store_true")
@@ -115,8 +143,26 @@ def main():
                     help="view pipelining: the step's forward phase 1 + binning of all views as one batch (batched, "
                          "default), next view's preprocess queued ahead on one stream with a deferred count "
                          "(lookahead), or run on a side stream (side)")
-    args = ap.parse_args()
+    ap.add_argument("--single-view-steps", type=int, default=10,
+                    help="secondary figure: single-view forward_native + backward_native frames timed (0: skip)")
+    return ap.parse_args(argv)
 
+
+def main():
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no torchrun: start one rank per GPU here, before this process touches the GPU
+        from view_parallel import launch_ranks
+        launch_ranks(args.gpus, _rank_main, (args,))
+        return
+    run(args)
+
+
+def _rank_main(rank, world, args):
+    run(args)
+
+
+def run(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -124,14 +170,16 @@ def main():
         print(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
+    pg_ranks = 1
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+        pg_ranks = dist.get_world_size()
 
     import diff_gaussian_rasterization as dgr
     from diff_gaussian_rasterization import _lib
     import synthetic
-    if args.pipeline is None:   # variant libraries of older revisions (A/B runs) lack the batched entry points
-        args.pipeline = "batched" if _lib.has("lsr_forward_preprocess_views_async") else "lookahead"
+    if args.pipeline is None:
+        args.pipeline = "batched"
 
     P, C, W, H, V = args.gaussians, args.channels, args.width, args.height, args.views
     tanfovx = 0.6
@@ -139,7 +187,8 @@ def main():
     scene = scene_cpu.to(dev)
     from view_parallel import GradBucket, ViewParallelStep, native_view_renderer
     M = scene.shs.shape[1]
-    bucket = GradBucket(P, M, C, dev)                      # flat grads, 59 + C floats per Gaussian
+    bucket = GradBucket(P, M, C, dev, densify_stats=True)  # flat grads, 62 + C floats per Gaussian (means2D
+                                                           # for the densification statistics), radii MAX
     dp = ViewParallelStep(bucket, world * V)               # this rank's slice of the world*V batch
     all_cams = synthetic.camera_batch(world * V, W, H, tanfovx=tanfovx, seed=1)
     bg = torch.ones(3, device=dev)
@@ -207,6 +256,28 @@ def main():
     frames = world * V * args.steps
     value = frames / elapsed
 
+    single = None
+    if args.single_view_steps > 0:
+        # secondary figure: BASELINE configs[2] literally, one view at a time through the per-view
+        # entry points (forward_native + backward_native, workspaces allocated per call), no batching
+        v0 = dp.views[0]
+        kw = dict(shs=scene.shs, language_feature=scene.lang, scales=scene.scales, rotations=scene.rotations)
+
+        def one_view():
+            *_, st = dgr.forward_native(settings[v0], scene.means3D, scene.opacities, **kw)
+            dgr.backward_native(st, gcol, glang, None, out=bucket.views, accumulate=True, need=bucket.need())
+
+        one_view()
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for _ in range(args.single_view_steps):
+            one_view()
+        torch.cuda.synchronize(dev)
+        dt = (time.perf_counter() - t1) / args.single_view_steps
+        single = dict(value=round(1.0 / dt, 3), unit="frames/s", ms_per_frame=round(dt * 1e3, 3),
+                      frames=args.single_view_steps,
+                      path="forward_native + backward_native per view (configs[2]: one view fwd+bwd, no batching)")
+
     if rank == 0:
         Kmean = float(np.mean(Ks)) if Ks else 0.0
         with torch.no_grad():
@@ -220,7 +291,7 @@ def main():
                 if v == dp.views[0]:
                     Pvis = int((radii > 0).sum())
             Pany = int(any_vis.sum())
-        pb = dict(V=len(dp.views), Pvis_sum=vis_sum, Pany=Pany,
+        pb = dict(V=len(dp.views), Pvis_sum=vis_sum, Pany=Pany, means2D=bucket.densify_stats,
                   accumulate=not getattr(getattr(render, "flush", None), "overwrites", False))
         ntiles = ((W + 15) // 16) * ((H + 15) // 16)
         roof = None
@@ -234,34 +305,42 @@ def main():
             ms, n = prof[dom]                      # live, over the timed region
             byts = phase_bytes(dom, P, Pvis, Kmean, W * H, ntiles, C, M, **pb)
             ach = byts / (ms / n * 1e-3) / 1e9
-            traffic = None
+            pmc_rec = {}
             pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
             if os.path.exists(pmc):
                 try:
-                    traffic = json.load(open(pmc)).get(dom, {}).get("hbm_bytes_per_launch")
+                    pmc_rec = json.load(open(pmc)).get(dom, {})
                 except Exception:
-                    traffic = None
+                    pmc_rec = {}
+            # the HBM roofline is the contract's; the compositors are bound by VALU issue and atomics
+            # (DESIGN.md 4), so the PMC VALU-issue share and matrix-core busy fraction ride along
             roof = dict(kernel=dom, bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                        frac=round(ach / HBM_PEAK_GBS, 4), traffic=traffic, algorithmic_bytes=int(byts),
-                        mean_launch_ms=round(ms / n, 4))
+                        frac=round(ach / HBM_PEAK_GBS, 4), traffic=pmc_rec.get("hbm_bytes_per_launch"),
+                        traffic_source="profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes)",
+                        algorithmic_bytes=int(byts), mean_launch_ms=round(ms / n, 4),
+                        limiter="valu-issue+atomics" if dom.startswith("render") else "hbm",
+                        valu_issue_per_wave=pmc_rec.get("valu_issue_per_wave"),
+                        mfma_busy_frac=pmc_rec.get("mfma_busy_frac"))
         cpu = None
         if not args.no_cpu_baseline:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            avail, host = host_cpu()
+            threads = args.cpu_threads or avail
             nf = args.cpu_frames
             tot, tf, tb = cpu_baseline(scene_cpu, all_cams[:nf], C, threads)
             cpu = dict(value=round(nf / tot, 5), unit="frames/s", cores=threads, kind="port",
                        sample=f"{nf} headline frames (P={P}, {W}x{H}, C={C}, the first cameras of the batch) "
-                              f"fwd {tf:.2f}s + bwd {tb:.2f}s, C oracle oracle/lsr_oracle.c, OpenMP {threads} threads")
+                              f"fwd {tf:.2f}s + bwd {tb:.2f}s, C oracle oracle/lsr_oracle.c, OpenMP {threads} threads",
+                       host=host)
         line = dict(
             metric="rasterizer fwd+bwd frames/sec @ 2M Gaussians, 1352x1014, 32-ch features",
-            value=round(value, 3), unit="frames/s", n_gpus=world, steps=args.steps, warmup=args.warmup,
+            value=round(value, 3), unit="frames/s", n_gpus=world, ranks=pg_ranks, steps=args.steps, warmup=args.warmup,
             ms_per_step=round(elapsed / args.steps * 1e3, 3), higher_is_better=True, scaling="weak",
             vs_baseline=None, dtype="f32", data="synthetic",
             config=dict(workload="S2M synthetic (BASELINE configs[2] per GPU; configs[3] batch split)",
                         gaussians=P, width=W, height=H, channels=C, views_per_gpu_per_step=V,
                         global_batch=world * V, parallelism=f"dp{world}", pipeline="none" if args.no_overlap else args.pipeline, num_rendered_mean=int(Kmean),
                         visible=Pvis, visible_any_view=Pany, grad_bucket_mb=round(bucket.nbytes / 2**20, 1)),
-            roofline=roof, cpu_baseline=cpu,
+            roofline=roof, cpu_baseline=cpu, single_view=single,
             phases={k: dict(mean_ms=round(v["mean_ms"], 4), gbs=round(v["gbs"], 1)) for k, v in phases.items()},
         )
         print(json.dumps(line))

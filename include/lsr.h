@@ -38,8 +38,10 @@
 extern "C" {
 #endif
 
-#define LSR_API_VERSION 3   /* 2: lsr_fwd_out.host_sort_status, lsr_forward_status;
-                               3: lsr_fwd_in.language_feature_split, lsr_language_split */
+#define LSR_API_VERSION 4   /* 3: lsr_fwd_in.language_feature_split, lsr_language_split;
+                               4: lsr_require_api; the sort status words are gone (lsr_fwd_out
+                                  .host_sort_status, lsr_forward_status, lsr_test_inject_sort_fault:
+                                  the radix sorts have no look-back that could time out) */
 
 #define LSR_OK 0
 #define LSR_EINVAL 1     /* bad argument (null pointer, exactly-one-of violation, size) */
@@ -89,11 +91,6 @@ typedef struct lsr_fwd_out {
     float *out_language_feature;      /* [C,H,W] (may be NULL when C == 0) */
     int32_t *radii;                   /* [P] */
     float *out_depth;                 /* [1,H,W] */
-    uint32_t *host_sort_status;       /* optional, [2] PAGE-LOCKED HOST memory (hipHostMalloc /
-                                         torch pin_memory): the compositor writes the sort status
-                                         words of lsr_forward_status there itself (no copy, no
-                                         launch); valid once the stream has passed the composite.
-                                         NULL: not reported. */
 } lsr_fwd_out;
 
 typedef struct lsr_bwd_in {
@@ -118,6 +115,10 @@ typedef struct lsr_bwd_out {                 /* any pointer may be NULL if that 
 
 int lsr_version(void);
 const char *lsr_last_error(void);
+/* Call once before any other entry point with LSR_API_VERSION from the lsr.h the caller was built
+ * against: the structs above are read with THIS header's layout, so a caller built against another
+ * version is refused (LSR_EINVAL, every entry point) instead of having trailing fields misread. */
+int lsr_require_api(int32_t caller_version);
 
 /* Workspace sizes in bytes (upstream geomBuffer / binningBuffer / imgBuffer + backward scratch). */
 int64_t lsr_geom_bytes(int32_t P);
@@ -133,7 +134,7 @@ int lsr_forward_preprocess(const lsr_settings *s, const lsr_fwd_in *in, lsr_fwd_
 
 /* lsr_forward_preprocess without the host synchronisation: the same launches, then an
  * asynchronous copy of two words to `host_count` (page-locked host memory): [0] num_rendered,
- * [1] nonzero if the depth sort's look-back timed out (results invalid).  Valid once the stream
+ * [1] reserved (0).  Valid once the stream
  * has passed this point (an event recorded after the call).  Lets a caller enqueue the next
  * view's preprocess ahead of the current view's compositing on ONE stream and read the count
  * later, so the device never idles on the host between views. */
@@ -145,7 +146,7 @@ int lsr_forward_preprocess_async(const lsr_settings *s, const lsr_fwd_in *in, ls
  * 3D covariance) once for all of them, and the depth sorts and instance scans of those views run
  * as one set of launches (every kernel serves all the views).  s[v], out[v], geom[v] are view v's
  * (workspaces as for lsr_forward_preprocess_async); `host_counts` (page-locked, 2 * n_views words)
- * receives [2v] num_rendered and [2v + 1] the depth sort error word of view v, valid once the
+ * receives [2v] num_rendered of view v ([2v + 1] reserved, 0), valid once the
  * stream has passed this point.  The views must share the image size, sh_degree and
  * scale_modifier.  Results equal lsr_forward_preprocess_async per view.  The pointer arrays are
  * HOST arrays. */
@@ -174,19 +175,6 @@ int lsr_forward_composite(const lsr_settings *s, const lsr_fwd_in *in, lsr_fwd_o
 int lsr_forward_binning_views(int32_t n_views, const lsr_settings *const *s, const lsr_fwd_in *in,
                               void *const *geom, void *const *binning, void *const *img,
                               const int64_t *num_rendered, lsr_stream_t stream);
-
-/* Sort status of the forward whose phase 1 filled `geom` (P Gaussians): an asynchronous copy of two
- * words to `host_status` (valid once the stream has passed this point): [0] nonzero if the depth
- * sort's look-back timed out, [1] the same for the tile sort.  A bounded look-back spin never
- * hangs; on a timeout the sorted lists are invalid, and the compositor then writes NaN to every
- * output pixel (colour, language, depth, final T) so that the failure cannot pass silently.
- * lsr_forward_preprocess reports [0] itself.  The same words reach the host without a copy through
- * lsr_fwd_out.host_sort_status (a stream-ordered copy per view costs ~25 us on MI355X). */
-int lsr_forward_status(int32_t P, const void *geom, uint32_t *host_status, lsr_stream_t stream);
-
-/* Test hook: the next forwards' sorts report a look-back timeout as if their spin had run out
- * (bit 0: depth sort, bit 1: tile sort; 0 restores normal operation).  Per process. */
-int lsr_test_inject_sort_fault(uint32_t mask);
 
 /* Backward through compositing and preprocess.  accumulate != 0 adds into the outputs instead of
  * overwriting them (multi-view gradient accumulation).  `scratch` holds >= lsr_backward_bytes. */
@@ -227,6 +215,12 @@ int lsr_backward_composite(const lsr_settings *s, const lsr_fwd_in *in, const ls
 int lsr_backward_preprocess_views(int32_t n_views, const lsr_settings *const *s, const lsr_fwd_in *in,
                                   lsr_bwd_out *gout, const void *const *geom, int32_t accumulate,
                                   lsr_stream_t stream);
+/* lsr_backward_preprocess_views over the Gaussian rows [row_begin, row_begin + row_count) only
+ * (row_begin a multiple of 256); every gout pointer addresses row row_begin of its array.  Lets a
+ * data-parallel caller start the all-reduce of finished rows while the next rows are computed. */
+int lsr_backward_preprocess_views_rows(int32_t n_views, const lsr_settings *const *s, const lsr_fwd_in *in,
+                                       lsr_bwd_out *gout, const void *const *geom, int32_t accumulate,
+                                       int32_t row_begin, int32_t row_count, lsr_stream_t stream);
 
 /* markVisible: present[i] = (view-space z of means3D[i]) > 0.2 */
 /* language_feature [P,C] fp32 -> out [P,2C] bf16 bit patterns (hi channels then lo channels) for

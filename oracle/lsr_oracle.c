@@ -66,6 +66,15 @@ typedef float real;
 #define RCEIL ceilf
 #define RMIN fminf
 #define RMAX fmaxf
+#endif
+
+#if !defined(ORC_DOUBLE) && defined(ORC_UPSTREAM_ARITH)
+/* Upstream-arithmetic float build (liborc_f32_up.so, compiled with -ffp-contract=fast -mfma):
+ * libm expf and the upstream falloff expression, every a*b+c free to contract as nvcc's default
+ * does.  It stands in for the CUDA build's rounding, so that tests can bound how far the
+ * reproducible build's contributor decisions (orc_exp / orc_power below) drift from it. */
+static inline float orc_exp(float x) { return expf(x); }
+#elif !defined(ORC_DOUBLE)
 /* exp for x <= 0; bit-reproducible with the HIP kernels' expf_repro (lsr_common.h): the same
  * sequence of correctly rounded operations (fmaxf, fmaf, +, *).  The argument is clamped at -87
  * (every alpha from exp(-87) ~ 1.6e-38 is far below 1/255); k = rint(x log2 e) is
@@ -95,11 +104,15 @@ static inline float orc_exp(float x) {
  *   power = -(a dx^2 + c dy^2)/2 - b dx dy = dx (A dx + B dy) + (C dy) dy,  (A, B, C) = (-a/2, -b, -c/2)
  * the HIP kernels' gauss_power (lsr_common.h) operation for operation (the scalings are exact). */
 static inline real orc_power(const real *co, real dx, real dy) {
+#if defined(ORC_UPSTREAM_ARITH) && !defined(ORC_DOUBLE)
+    return R(-0.5) * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;   /* upstream renderCUDA */
+#else
     const real A = R(-0.5) * co[0], B = -co[1], Cq = R(-0.5) * co[2];
 #ifdef ORC_DOUBLE
     return fma(dx, fma(A, dx, B * dy), (Cq * dy) * dy);
 #else
     return fmaf(dx, fmaf(A, dx, B * dy), (Cq * dy) * dy);
+#endif
 #endif
 }
 

@@ -22,7 +22,7 @@ _BUILD = os.path.join(_HERE, "build")
 
 
 def build(force: bool = False) -> None:
-    libs = [os.path.join(_BUILD, n) for n in ("liborc_f32.so", "liborc_f64.so")]
+    libs = [os.path.join(_BUILD, n) for n in ("liborc_f32.so", "liborc_f64.so", "liborc_f32_up.so")]
     src = os.path.join(_HERE, "lsr_oracle.c")
     if not force and all(os.path.exists(p) and os.path.getmtime(p) >= os.path.getmtime(src) for p in libs):
         return
@@ -32,8 +32,10 @@ def build(force: bool = False) -> None:
 _LIBS: dict = {}
 
 
-def _lib(double: bool):
-    key = "f64" if double else "f32"
+def _lib(double: bool, upstream: bool = False):
+    """double: the fp64 build (libm exp); upstream: the float build with libm expf and fma
+    contraction (liborc_f32_up.so, the stand-in for the CUDA original's rounding)."""
+    key = "f64" if double else ("f32_up" if upstream else "f32")
     if key not in _LIBS:
         build()
         lib = ctypes.CDLL(os.path.join(_BUILD, f"liborc_{key}.so"))
@@ -177,10 +179,13 @@ class OracleResult:
 
 
 def forward(settings: OracleSettings, means3D, opacities, shs=None, colors_precomp=None, lang=None,
-            scales=None, rotations=None, cov3D_precomp=None, double=False, nthreads=0) -> OracleResult:
+            scales=None, rotations=None, cov3D_precomp=None, double=False, nthreads=0,
+            upstream_arith=False) -> OracleResult:
     """Restated forward.  Inputs are numpy (or anything np.asarray accepts); activated values,
-    exactly what GaussianRasterizer receives (gaussian_renderer/__init__.py:191-228)."""
-    lib = _lib(double)
+    exactly what GaussianRasterizer receives (gaussian_renderer/__init__.py:191-228).
+    upstream_arith: float build with libm expf + fma contraction instead of the reproducible
+    orc_exp / orc_power (drift bound tests only; the parity checks use the default build)."""
+    lib = _lib(double, upstream_arith and not double)
     dt = np.float64 if double else np.float32
     means3D = _arr(means3D, dt, (-1, 3))
     P = means3D.shape[0]

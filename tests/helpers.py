@@ -24,3 +24,11 @@ def small_case(P=2000, W=128, H=96, C=8, seed=0, tanfovx=0.6, big_frac=0.01, log
 
 def axis_camera(W=33, H=33, tanfov=0.5):
     return synthetic.make_camera(np.eye(3), np.zeros(3), 2 * math.atan(tanfov), 2 * math.atan(tanfov), W, H)
+
+
+def image_drift(a, b):
+    """Per-pixel max |a - b| over channels ([C,H,W] images): (max, 99.99th percentile, fraction of
+    pixels above 1e-4 and above 1e-3)."""
+    d = np.abs(np.asarray(a, np.float64) - np.asarray(b, np.float64))
+    d = d.reshape(d.shape[0], -1).max(0) if d.size else np.zeros(1)
+    return float(d.max()), float(np.quantile(d, 0.9999)), float((d > 1e-4).mean()), float((d > 1e-3).mean())

@@ -52,7 +52,7 @@ def test_library_is_built_for_gfx950():
 def test_size_queries():
     from diff_gaussian_rasterization import _lib
     lib = _lib.load()
-    assert lib.lsr_version() == 3
+    assert lib.lsr_version() == _lib.API_VERSION == 4
     g1, g2 = lib.lsr_geom_bytes(1000), lib.lsr_geom_bytes(2_000_000)
     assert 0 < g1 < g2 and g2 >= 2_000_000 * 60
     assert lib.lsr_binning_bytes(8_600_000) >= 8_600_000 * 16
@@ -77,3 +77,28 @@ def test_settings_validation_messages():
     with pytest.raises(RuntimeError, match="GPU only"):
         r(means3D=m, means2D=m, opacities=torch.ones(4, 1), shs=torch.zeros(4, 16, 3), scales=m,
           rotations=torch.zeros(4, 4))
+
+
+def test_callers_of_another_header_version_are_refused():
+    """lsr_require_api: until a caller has declared the lsr.h version it was built against, every
+    entry point that reads the structs refuses (no misread trailing fields); a mismatched
+    declaration is refused too.  Fresh process: the handshake is per process."""
+    import sys
+    from diff_gaussian_rasterization import _lib
+    code = f"""
+import ctypes
+L = ctypes.CDLL({_lib.LIB_PATH!r})
+L.lsr_last_error.restype = ctypes.c_char_p
+k = ctypes.c_int64(0)
+rc = L.lsr_forward_preprocess(None, None, None, None, ctypes.byref(k), None)
+assert rc == 1 and b"lsr_require_api" in L.lsr_last_error(), (rc, L.lsr_last_error())
+assert L.lsr_require_api(3) == 1 and b"mismatch" in L.lsr_last_error()
+rc = L.lsr_forward_preprocess(None, None, None, None, ctypes.byref(k), None)
+assert rc == 1 and b"lsr_require_api" in L.lsr_last_error()
+assert L.lsr_require_api(4) == 0
+rc = L.lsr_forward_preprocess(None, None, None, None, ctypes.byref(k), None)
+assert rc == 1 and b"null settings" in L.lsr_last_error(), L.lsr_last_error()
+print("ok")
+"""
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and "ok" in out.stdout, out.stderr

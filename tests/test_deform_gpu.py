@@ -155,3 +155,112 @@ def test_apply_autograd_path():
     (outs[0].sum() + 2.0 * outs[4].sum()).backward()
     assert torch.equal(xs[4].grad, torch.full_like(xs[4], 2.0)) and torch.equal(xs[1].grad, torch.zeros_like(xs[1]))
     assert xs[0].grad.abs().sum() > 0 and f.grads["pos_deform.3.bias"][0].item() == pytest.approx(500.0)
+
+
+# ---- every switch of scene/deformation.py (tests/golden/deform_variants.npz) ----------------------
+VARIANTS = ("hypernerf", "lang", "noresnet", "discrete", "deep")
+
+
+def _variant_field(name):
+    import ast
+    from deformation import LANG_DISCRETE, LANG_NORESNET, LANG_PASS, LANG_RESIDUAL
+    z = np.load(os.path.join(ROOT, "tests", "golden", "deform_variants.npz"))
+    pre = name + "/"
+    cfg = ast.literal_eval(str(z[pre + "config"]))
+    d = {k[len(pre):]: z[k] for k in z.files if k.startswith(pre)}
+    params = {k[len("param/"):]: torch.tensor(v).cuda() for k, v in d.items() if k.startswith("param/")}
+    params["grid.aabb"] = torch.tensor(d["aabb"]).cuda()
+    mode = LANG_PASS if cfg["no_dlang"] else (LANG_DISCRETE if cfg["discrete"] else
+                                              (LANG_NORESNET if cfg["no_resnet"] else LANG_RESIDUAL))
+    f = DeformationField(params, cfg["res"], cfg["multires"], depth=cfg["depth"], no_dx=cfg["no_dx"],
+                         no_ds=cfg["no_ds"], no_dr=cfg["no_dr"], no_do=cfg["no_do"], no_dshs=cfg["no_dshs"],
+                         apply_rotation=cfg["apply_rotation"], lang_mode=mode, lang_dim=cfg["lang_dim"],
+                         centers=cfg["centers"], time_pe=cfg["time_pe"])
+    return f, cfg, d
+
+
+@pytest.mark.parametrize("name", VARIANTS)
+def test_variant_forward_matches_reference(name):
+    """HyperNeRF structure (3 scales, 3 heads), lang_deform with / without the residual, the discrete
+    centres + coff head, apply_rotation, no_ds / no_dx, defor_depth 2: every output vs the
+    reference module (residual outputs compared as offsets, what the kernels compute)."""
+    f, cfg, d = _variant_field(name)
+    t = lambda k: torch.tensor(d[k]).cuda()   # noqa: E731
+    out = f.forward(t("means3D"), t("scales"), t("rotations"), t("opacity"), t("shs"), t("lang"), t("time")[:, 0])
+    names = ("means3D", "scales", "rotations", "opacity", "shs", "lang", "coff")
+    for k, o in zip(names, out):
+        if "out_" + k not in d:
+            assert o is None, k
+            continue
+        ref = d["out_" + k].astype(np.float64)
+        got = o.cpu().numpy().astype(np.float64).reshape(ref.shape)
+        if k in ("lang", "coff") or (k == "rotations" and cfg["apply_rotation"]):
+            assert _rel(got, ref) < 1e-4, k
+        else:
+            base = d[k].astype(np.float64).reshape(ref.shape)
+            if np.abs(ref - base).max() == 0:           # head off: the input itself
+                assert np.array_equal(got, base), k
+            else:
+                assert _rel(got - base, ref - base) < 1e-4, k
+
+
+@pytest.mark.parametrize("name", VARIANTS)
+def test_variant_backward_matches_reference(name):
+    """Input gradients (means3D through the HexPlane coordinates, rotations through the quaternion
+    product, the language input through lang_deform / the discrete combination) and every
+    parameter gradient vs the reference's autograd."""
+    f, cfg, d = _variant_field(name)
+    t = lambda k: torch.tensor(d[k]).cuda() if k in d else None   # noqa: E731
+    f.zero_grad()
+    got = f.backward(t("means3D"), t("time")[:, 0], t("up_means3D"), t("up_scales"), t("up_rotations"),
+                     t("up_opacity"), t("up_shs"), rotations=t("rotations"), lang=t("lang"), d_lang=t("up_lang"),
+                     d_coff=t("up_coff"))
+    torch.cuda.synchronize()
+    for k, g in zip(("means3D", "scales", "rotations", "opacity", "shs", "lang"), got):
+        ref = d["grad_" + k]
+        assert _rel(g.cpu().numpy().reshape(ref.shape), ref) < 1e-4, k
+    grads = {k[len("grad/"):]: v for k, v in d.items() if k.startswith("grad/")}
+    assert set(f.grads) == set(grads)
+    for k, v in grads.items():
+        assert _rel(f.grads[k].cpu().numpy().reshape(v.shape), v) < 1e-4, k
+
+
+def test_variant_apply_autograd():
+    """apply() with the discrete language and apply_rotation variants inside autograd: the same
+    gradients as backward()."""
+    for name in ("discrete", "noresnet"):
+        f, cfg, d = _variant_field(name)
+        xs = [torch.tensor(d[k]).cuda().requires_grad_(True) for k in ("means3D", "scales", "rotations", "opacity",
+                                                                        "shs", "lang")]
+        outs = f.apply(*xs, torch.tensor(d["time"][:, 0]).cuda())
+        loss = sum((o * torch.tensor(d["up_" + k]).cuda()).sum() for o, k in
+                   zip(outs, ("means3D", "scales", "rotations", "opacity", "shs", "lang", "coff")) if o is not None)
+        f.zero_grad()
+        loss.backward()
+        for x, k in zip(xs, ("means3D", "scales", "rotations", "opacity", "shs", "lang")):
+            assert _rel(x.grad.cpu().numpy(), d["grad_" + k]) < 1e-4, (name, k)
+
+
+def test_from_reference_is_strict():
+    """deform_network.state_dict() + ModelHiddenParams + env: the unused modules the reference always
+    builds are skipped; a key the configuration does not compute raises (a defor_depth 2 state dict
+    loaded as depth 1), as do unsupported switches."""
+    f, cfg, d = _variant_field("hypernerf")
+    sd = {"deformation_net." + k: v for k, v in f.p.items()}
+    W = 128
+    for h, n in (("opacity_deform", 1), ("shs_deform", 48)):   # built but not computed (no_do, no_dshs)
+        sd[f"deformation_net.{h}.1.weight"], sd[f"deformation_net.{h}.1.bias"] = torch.zeros(W, W), torch.zeros(W)
+        sd[f"deformation_net.{h}.3.weight"], sd[f"deformation_net.{h}.3.bias"] = torch.zeros(n, W), torch.zeros(n)
+    sd["timenet.0.weight"], sd["time_poc"] = torch.zeros(64, 9), torch.zeros(4)
+    hidden = dict(kplanes_config={"resolution": cfg["res"], "output_coordinate_dim": 16}, multires=cfg["multires"],
+                  defor_depth=1, no_dlang=1)
+    g = DeformationField.from_reference(sd, hidden, env={"language_feature_hiddendim": "3"})
+    assert g.heads_computed() == ["pos_deform", "scales_deform", "rotations_deform"]
+    sd2 = dict(sd, **{"deformation_net.feature_out.2.weight": torch.zeros(W, W)})
+    with pytest.raises(ValueError, match="feature_out.2.weight"):
+        DeformationField.from_reference(sd2, hidden, env={})
+    with pytest.raises(ValueError, match="static_mlp"):
+        DeformationField.from_reference(sd, dict(hidden, static_mlp=True), env={})
+    with pytest.raises(ValueError, match="unexpected"):
+        DeformationField({**f.p, "feature_out.2.weight": torch.zeros(W, W).cuda()}, cfg["res"], cfg["multires"],
+                         depth=1, no_do=True, no_dshs=True)

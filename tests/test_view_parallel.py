@@ -64,9 +64,10 @@ def _view_grads(v):
     return g.normal(size=(3, H, W)).astype(np.float32), g.normal(size=(C, H, W)).astype(np.float32)
 
 
-def oracle_renderer(sc, cams, batched=False):
+def oracle_renderer(sc, cams, batched=False, chunked=False):
     """batched: like native_view_renderer(batch_backward=True), the language gradient goes into
-    the bucket per view and every other field only at flush (the batched preprocess backward)."""
+    the bucket per view and every other field only at flush (the batched preprocess backward);
+    chunked: the flush writes row chunks and reports each (flush(bucket, row_chunks, on_rows))."""
     names = dict(means3D="means3D", scales="scales", rotations="rotations", opacity="opacities", sh="sh",
                  lang="language_feature", means2D="means2D")
     held = []
@@ -86,13 +87,17 @@ def oracle_renderer(sc, cams, batched=False):
         r.close()
         return radii
 
-    def flush(bucket):
-        for name, t in held:
-            bucket.views[name] += t
+    def flush(bucket, row_chunks=None, on_rows=None):
+        for r0, r1 in (row_chunks or [(0, bucket.P)]):
+            for name, t in held:
+                bucket.views[name][r0:r1] += t[r0:r1]
+            if on_rows is not None:
+                on_rows(r0, r1)
         held.clear()
 
     if batched:
         render_view.flush = flush
+        flush.chunked = chunked
     return render_view
 
 
@@ -105,16 +110,16 @@ def _serial_reference(densify):
     return b
 
 
-def _worker(rank, world, port, outdir, densify, batched=False):
+def _worker(rank, world, port, outdir, densify, batched=False, chunked=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         sc, cams = _scene_and_cams()
         b = GradBucket(P, sc.shs.shape[1], C, "cpu", densify_stats=densify)
-        step = ViewParallelStep(b, N_VIEWS)
+        step = ViewParallelStep(b, N_VIEWS, flush_chunks=3)
         assert step.world == world and step.rank == rank
         calls = []
-        render = oracle_renderer(sc, cams, batched)
+        render = oracle_renderer(sc, cams, batched, chunked)
 
         def counted(v, bucket):
             calls.append(v)
@@ -138,12 +143,15 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("densify,batched", [(False, False), (True, False), (True, True)])
-def test_two_rank_step_equals_serial_batch(densify, batched):
-    """batched: the language field's SUM is issued before the flush and overlaps it."""
+@pytest.mark.parametrize("densify,batched,chunked", [(False, False, False), (True, False, False),
+                                                     (True, True, False), (True, True, True)])
+def test_two_rank_step_equals_serial_batch(densify, batched, chunked):
+    """batched: the language field's SUM is issued before the flush and overlaps it; chunked: the
+    flush runs in row chunks (P = 1500 -> 512-row chunks) and each chunk's rows of every other
+    field are SUMmed asynchronously as the chunk ends."""
     ref = _serial_reference(densify)
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(2, _free_port(), d, densify, batched), nprocs=2, join=True)
+        mp.spawn(_worker, args=(2, _free_port(), d, densify, batched, chunked), nprocs=2, join=True)
         outs = [torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(2)]
     assert sorted(outs[0]["calls"] + outs[1]["calls"]) == list(range(N_VIEWS))
     # both ranks hold the same reduced bucket, equal to the serial sum up to fp32 reassociation
@@ -185,12 +193,12 @@ def _lookahead_worker(rank, world, port, outdir, mode="lookahead"):
             log.append(("preprocess", settings))
             return _FakePending(settings, log)
 
-        def render_native(pf, status_event=True):
+        def render_native(pf):
             log.append(("render", pf.v))
             z = torch.zeros(3, 4, 4)
             return z, torch.zeros(2, 4, 4), torch.full((Pn,), pf.v + 1, dtype=torch.int32), z[:1], pf
 
-        def backward_composite_native(st, gc, gl, gd, dL_dlanguage=None, defer_sort_check=False):
+        def backward_composite_native(st, gc, gl, gd, dL_dlanguage=None):
             log.append(("composite_bwd", st.v))
             return st
 
@@ -201,11 +209,14 @@ def _lookahead_worker(rank, world, port, outdir, mode="lookahead"):
         def binning_views_native(pfs):
             log.append(("binning_views", [pf.v for pf in pfs]))
 
-        def backward_preprocess_views_native(held, out=None, accumulate=False, need=None):
+        def backward_preprocess_views_native(held, out=None, accumulate=False, need=None, row_chunks=None,
+                                             on_rows=None):
             log.append(("flush", [h.v for h in held]))
             for t in out.values():
                 if t is not None:
                     t.zero_()
+            for r0, r1 in (row_chunks or []):
+                on_rows(r0, r1)
 
         dgr.preprocess_native, dgr.render_native = preprocess_native, render_native
         dgr.backward_composite_native = backward_composite_native
@@ -246,3 +257,50 @@ def test_two_rank_lookahead_stays_in_rank_slice(mode):
     # radii MAX over all 5 views (the fake radius of view v is v + 1)
     assert torch.equal(outs[0]["radii"], torch.full((16,), 5, dtype=torch.int32))
     assert torch.equal(outs[1]["radii"], outs[0]["radii"])
+
+
+def test_row_chunks_tile_rows():
+    from view_parallel import row_chunks
+    for P, n in ((1500, 3), (2_000_000, 4), (100, 8), (256, 1), (0, 4), (257, 2)):
+        ch = row_chunks(P, n)
+        assert ch[0][0] == 0 and ch[-1][1] == P and len(ch) <= max(n, 1)
+        assert all(a % 256 == 0 for a, _ in ch)
+        assert all(ch[i][1] == ch[i + 1][0] for i in range(len(ch) - 1))
+
+
+def _launched(rank, world, outdir):
+    """A rank started by view_parallel.launch_ranks: the torchrun environment is set, the gloo
+    group forms from it, and a step with a stub renderer (view v adds v + 1 to every gradient,
+    radius v + 1) reduces over all ranks."""
+    assert os.environ["RANK"] == str(rank) and os.environ["WORLD_SIZE"] == str(world)
+    assert os.environ["MASTER_ADDR"] == "127.0.0.1"
+    dist.init_process_group("gloo")
+    try:
+        b = GradBucket(8, 1, 2, "cpu", densify_stats=True)
+        step = ViewParallelStep(b, 6)
+
+        def stub(v, bucket):
+            bucket.flat += float(v + 1)
+            return torch.full((8,), v + 1, dtype=torch.int32)
+
+        step.run(stub)
+        torch.save(dict(world=dist.get_world_size(), flat=b.flat.clone(), radii=b.radii.clone(),
+                        views=list(step.views)), os.path.join(outdir, f"rank{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_launch_ranks_starts_world_ranks(world, monkeypatch):
+    """bench.py --gpus N without torchrun: launch_ranks starts N ranks that form one group."""
+    from view_parallel import launch_ranks
+    monkeypatch.delenv("MASTER_PORT", raising=False)
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    with tempfile.TemporaryDirectory() as d:
+        launch_ranks(world, _launched, (d,))
+        outs = [torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(world)]
+    assert all(o["world"] == world for o in outs)
+    assert sorted(v for o in outs for v in o["views"]) == list(range(6))
+    for o in outs:
+        assert torch.equal(o["flat"], torch.full_like(o["flat"], 21.0))   # 1 + 2 + ... + 6
+        assert torch.equal(o["radii"], torch.full((8,), 6, dtype=torch.int32))

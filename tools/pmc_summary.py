@@ -74,6 +74,9 @@ def main(d, json_out=None):
                               dispatches=len(f["FETCH_SIZE"]))
             if "SQ_VALU_MFMA_BUSY_CYCLES" in f and "GRBM_GUI_ACTIVE" in f:
                 res[phase]["mfma_busy_frac"] = round(mfma_frac(f), 4)
+            if "SQ_ACTIVE_INST_VALU" in f and "SQ_WAVE_CYCLES" in f:
+                # both count quad-cycles: the share of a resident wave's cycles that issue VALU
+                res[phase]["valu_issue_per_wave"] = round(sum(f["SQ_ACTIVE_INST_VALU"]) / max(sum(f["SQ_WAVE_CYCLES"]), 1), 4)
         res["_note"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, bench.py --steps 1 (8 views); "
                         "hbm = (2*FETCH_SIZE + WRITE_SIZE)*1024 per MI355X_MICROARCH.md HBM section")
         with open(json_out, "w") as fh:
