@@ -196,16 +196,17 @@ class DeformationField:
             linear("lang_deform.5", lang_dim, width)
         return p
 
-    @classmethod
-    def from_reference(cls, state_dict: Mapping[str, torch.Tensor], hidden, env: Optional[Mapping[str, str]] = None,
-                       device="cuda", prefix="deformation_net."):
-        """A trained `deform_network` (`deformation.pth`, scene/gaussian_model.py:352-364): its state
-        dict, the ModelHiddenParams it was built with (a dict or an object with the attributes:
-        kplanes_config, multires, defor_depth, no_dx .. no_dshs, no_dlang, apply_rotation,
-        timebase_pe, net_width, static_mlp, empty_voxel, no_grid, grid_pe) and the environment
-        (language_feature_hiddendim, use_discrete_lang_f, centers_num, no_resnet,
+    @staticmethod
+    def config_from_reference(state_dict: Mapping[str, torch.Tensor], hidden, env: Optional[Mapping[str, str]] = None,
+                              prefix="deformation_net."):
+        """(params, config kwargs) of a trained `deform_network` (`deformation.pth`,
+        scene/gaussian_model.py:352-364): its state dict, the ModelHiddenParams it was built with (a
+        dict or an object with the attributes: kplanes_config, multires, defor_depth, no_dx ..
+        no_dshs, no_dlang, apply_rotation, timebase_pe, net_width, static_mlp, empty_voxel,
+        no_grid, grid_pe; the reference's defaults where absent, arguments/__init__.py:84-113) and
+        the environment (language_feature_hiddendim, use_discrete_lang_f, centers_num, no_resnet,
         use_tribute_dlang; default os.environ).  Modules the reference always builds but this
-        configuration does not compute are skipped; any other key raises."""
+        configuration does not compute are skipped; any other key raises.  CPU only (no device)."""
         env = os.environ if env is None else env
         h = hidden if isinstance(hidden, Mapping) else vars(hidden)
         get = lambda k, d=None: h.get(k, d)   # noqa: E731
@@ -217,7 +218,8 @@ class DeformationField:
         if env.get("use_tribute_dlang", "f") == "t":
             raise ValueError("use_tribute_dlang is not supported (the reference's lang_deform input width "
                              "does not admit it)")
-        if get("net_width", 128) != 128 or get("kplanes_config")["output_coordinate_dim"] != 16:
+        kp = get("kplanes_config")
+        if get("net_width", 64) != 128 or kp.get("output_coordinate_dim", 32) != 16:
             raise ValueError("supported: net_width 128, output_coordinate_dim 16 (every HyperNeRF / Neu3D config)")
         lang_dim = int(env.get("language_feature_hiddendim", 3))
         if env.get("use_discrete_lang_f", "f") == "t":
@@ -226,39 +228,59 @@ class DeformationField:
             mode = LANG_PASS
         else:
             mode = LANG_NORESNET if env.get("no_resnet", "f") == "t" else LANG_RESIDUAL
+        cfg = dict(resolution=list(kp["resolution"]), multires=list(get("multires", [1, 2, 4, 8])),
+                   depth=int(get("defor_depth", 1)), no_dx=bool(get("no_dx", False)), no_ds=bool(get("no_ds", False)),
+                   no_dr=bool(get("no_dr", False)), no_do=bool(get("no_do", True)), no_dshs=bool(get("no_dshs", True)),
+                   apply_rotation=bool(get("apply_rotation", False)), lang_mode=mode, lang_dim=lang_dim,
+                   centers=int(env.get("centers_num", 3)) if mode == LANG_DISCRETE else 0,
+                   time_pe=int(get("timebase_pe", 4)))
+        probe = DeformationField.__new__(DeformationField)   # the parameter set the configuration computes
+        probe.multires, probe.depth, probe.lang_mode = cfg["multires"], cfg["depth"], mode
+        probe.head_on = tuple(not cfg[f] for f in ("no_dx", "no_ds", "no_dr", "no_do", "no_dshs"))
+        probe.discrete = mode == LANG_DISCRETE
+        want = probe.param_names()
         params = {}
         for k, v in state_dict.items():
             if not k.startswith(prefix):
                 if _ALWAYS_BUILT.match(k):   # deform_network-level buffers and the time net
                     continue
                 raise ValueError(f"unexpected key {k!r} outside {prefix!r}")
-            params[k[len(prefix):]] = v
-        field = dict(resolution=get("kplanes_config")["resolution"], multires=get("multires"),
-                     depth=int(get("defor_depth", 1)), no_dx=bool(get("no_dx", False)), no_ds=bool(get("no_ds", False)),
-                     no_dr=bool(get("no_dr", False)), no_do=bool(get("no_do", True)),
-                     no_dshs=bool(get("no_dshs", True)), apply_rotation=bool(get("apply_rotation", False)),
-                     lang_mode=mode, lang_dim=lang_dim, centers=int(env.get("centers_num", 3)) if mode == LANG_DISCRETE
-                     else 0, time_pe=int(get("timebase_pe", 4)))
-        probe = cls.__new__(cls)   # the parameter set the configuration computes
-        probe.multires, probe.depth, probe.lang_mode = list(field["multires"]), field["depth"], mode
-        probe.head_on = tuple(not field[f] for f in ("no_dx", "no_ds", "no_dr", "no_do", "no_dshs"))
-        probe.discrete = mode == LANG_DISCRETE
-        want = probe.param_names()
-        for k in list(params):
-            if k not in want:
-                if _ALWAYS_BUILT.match(k):
-                    del params[k]
-                else:
-                    raise ValueError(f"state-dict key {prefix + k!r} is not computed by this configuration "
-                                     f"(defor_depth {field['depth']}, multires {field['multires']})")
-        return cls(params, device=device, **field)
+            name = k[len(prefix):]
+            if name in want:
+                params[name] = v
+            elif not _ALWAYS_BUILT.match(name):
+                raise ValueError(f"state-dict key {k!r} is not computed by this configuration "
+                                 f"(defor_depth {cfg['depth']}, multires {cfg['multires']})")
+        return params, cfg
+
+    @classmethod
+    def from_reference(cls, state_dict: Mapping[str, torch.Tensor], hidden, env: Optional[Mapping[str, str]] = None,
+                       device="cuda", prefix="deformation_net."):
+        """The field of a trained `deform_network` (config_from_reference), on `device`."""
+        params, cfg = cls.config_from_reference(state_dict, hidden, env, prefix)
+        return cls(params, device=device, **cfg)
+
+    def state_dict(self, prefix="deformation_net.") -> Dict[str, torch.Tensor]:
+        """The parameters under the reference's names (deform_network.state_dict() keys; the
+        modules this configuration does not compute are absent -- the reference loads with
+        strict=False, scene/gaussian_model.py:355)."""
+        return {prefix + k: v.detach().clone() for k, v in self.p.items()}
+
+    def hidden_params(self) -> dict:
+        """The ModelHiddenParams entries this field was built from (config_from_reference's input)."""
+        return dict(kplanes_config={"resolution": list(self.resolution), "output_coordinate_dim": 16,
+                                    "grid_dimensions": 2, "input_coordinate_dim": 4},
+                    multires=list(self.multires), defor_depth=self.depth, net_width=128,
+                    no_dx=not self.head_on[0], no_ds=not self.head_on[1], no_dr=not self.head_on[2],
+                    no_do=not self.head_on[3], no_dshs=not self.head_on[4], apply_rotation=self.apply_rotation,
+                    no_dlang=int(self.lang_mode == LANG_PASS), timebase_pe=self.time_pe)
 
     @classmethod
     def from_reference_state_dict(cls, state_dict, resolution, multires, prefix="deformation_net.", device="cuda"):
         """The Neu3D structure (arguments/neu3d/default.py): defor_depth 0, every head, language
         pass-through."""
         hidden = dict(kplanes_config={"resolution": list(resolution), "output_coordinate_dim": 16},
-                      multires=list(multires), defor_depth=0, no_do=False, no_dshs=False, no_dlang=1)
+                      multires=list(multires), defor_depth=0, no_do=False, no_dshs=False, no_dlang=1, net_width=128)
         return cls.from_reference(state_dict, hidden, env={}, device=device, prefix=prefix)
 
     def prepare(self):

@@ -80,7 +80,8 @@ class GaussianScene:
         t = lambda x: x.to(device)   # noqa: E731
         return GaussianScene(t(self.xyz), t(self.features_dc), t(self.features_rest), t(self.language_feature),
                              t(self.opacity), t(self.scaling), t(self.rotation), self.max_sh_degree,
-                             self.active_sh_degree, self.deformation, dict(self.extra))
+                             self.active_sh_degree, self.deformation,
+                             {k: (v.to(device) if torch.is_tensor(v) else v) for k, v in self.extra.items()})
 
     # ---- PLY (gaussian_model.py:331-345 attribute list, :370-389 save, :396-444 load) ---------
     def attribute_names(self) -> List[str]:
@@ -127,6 +128,67 @@ class GaussianScene:
                    features_rest=t(rest).transpose(1, 2).contiguous(), language_feature=t(group("f_lang_")),
                    opacity=t(col("opacity"))[:, None], scaling=t(group("scale_")), rotation=t(group("rot")),
                    max_sh_degree=max_sh_degree, active_sh_degree=max_sh_degree)
+
+
+# ---- trained model directories (scene/__init__.py:35-37,85-101; gaussian_model.py:352-370) -------
+def search_for_max_iteration(folder: str, stage: str) -> int:
+    """utils/system_utils.py:26-28: the largest N of the `{stage}_iteration_N` entries in folder."""
+    iters = [int(f.split("_")[-1]) for f in os.listdir(folder) if f.split("_")[0] == stage]
+    if not iters:
+        raise FileNotFoundError(f"no {stage}_iteration_* in {folder}")
+    return max(iters)
+
+
+def _load_pth(path: str, device):
+    """torch.load of a tensor file the reference wrote, without unpickling code (weights_only)."""
+    return torch.load(path, map_location=device, weights_only=True)
+
+
+def read_model_dir(model_path: str, load_iteration: int = -1, load_stage: str = "fine-lang", max_sh_degree: int = 3,
+                   device="cpu"):
+    """What Scene(load_iteration=...) reads (scene/__init__.py:35-37,85-93; gaussian_model.py:352-364):
+    model_path/point_cloud/{load_stage}_iteration_{N}/point_cloud.ply (N = the largest if -1),
+    deformation.pth (the deform_network state dict), deformation_table.pth (default all True) and
+    deformation_accum.pth (default zeros [P, 3]).  Returns (scene, deformation state dict, iteration);
+    the scene's `extra` holds the table and accumulator.  CPU; build the field with load_model_dir."""
+    root = os.path.join(model_path, "point_cloud")
+    it = search_for_max_iteration(root, load_stage) if load_iteration == -1 else int(load_iteration)
+    d = os.path.join(root, f"{load_stage}_iteration_{it}")
+    scene = GaussianScene.load_ply(os.path.join(d, "point_cloud.ply"), max_sh_degree=max_sh_degree, device=device)
+    state = _load_pth(os.path.join(d, "deformation.pth"), device)
+    P = scene.P
+    table = os.path.join(d, "deformation_table.pth")
+    accum = os.path.join(d, "deformation_accum.pth")
+    scene.extra["deformation_table"] = _load_pth(table, device) if os.path.exists(table) else \
+        torch.ones(P, dtype=torch.bool, device=device)
+    scene.extra["deformation_accum"] = _load_pth(accum, device) if os.path.exists(accum) else \
+        torch.zeros(P, 3, device=device)
+    return scene, state, it
+
+
+def load_model_dir(model_path: str, hidden, env=None, load_iteration: int = -1, load_stage: str = "fine-lang",
+                   max_sh_degree: int = 3, device="cuda"):
+    """read_model_dir + the deformation field on the GPU (DeformationField.from_reference with the
+    ModelHiddenParams and env the model was trained with).  Returns (scene, iteration)."""
+    from deformation import DeformationField
+    scene, state, it = read_model_dir(model_path, load_iteration, load_stage, max_sh_degree, device="cpu")
+    scene = scene.to(device)
+    scene.deformation = DeformationField.from_reference(state, hidden, env=env, device=device)
+    return scene, it
+
+
+def save_model_dir(scene: "GaussianScene", model_path: str, iteration: int, stage: str) -> str:
+    """Scene.save (scene/__init__.py:98-101): point_cloud.ply + deformation.pth (+ the table and
+    accumulator when the scene carries them) under model_path/point_cloud/{stage}_iteration_{N}."""
+    d = os.path.join(model_path, "point_cloud", f"{stage}_iteration_{iteration}")
+    os.makedirs(d, exist_ok=True)
+    scene.save_ply(os.path.join(d, "point_cloud.ply"))
+    if scene.deformation is not None:
+        torch.save({k: v.cpu() for k, v in scene.deformation.state_dict().items()}, os.path.join(d, "deformation.pth"))
+    for k in ("deformation_table", "deformation_accum"):
+        if k in scene.extra:
+            torch.save(torch.as_tensor(scene.extra[k]).cpu(), os.path.join(d, f"{k}.pth"))
+    return d
 
 
 def write_ply_vertices(path: str, names: List[str], cols: np.ndarray) -> None:

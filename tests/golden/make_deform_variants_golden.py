@@ -22,7 +22,8 @@ kernels see exactly what the reference saw), the forward outputs (pts, scales, r
 shs, lang, coff) and the float64 autograd gradients of a seeded linear loss over all outputs
 w.r.t. the inputs and the parameters.
 
-    python tests/golden/make_deform_variants_golden.py
+    python tests/golden/make_deform_variants_golden.py            # deform_variants.npz
+    python tests/golden/make_deform_variants_golden.py --layout   # deform_state_dict_layout.json
 """
 import os
 import sys
@@ -147,8 +148,35 @@ def make_variant(deform_network, name, spec, seed):
     return {f"{name}/{k}": v for k, v in data.items()}, used
 
 
+def state_dict_layout(deform_network):
+    """Keys and shapes of deform_network(...).state_dict() for the HyperNeRF and Neu3D configs (what
+    a trained model directory's deformation.pth holds: every module the reference builds, computed
+    or not) -> tests/golden/deform_state_dict_layout.json."""
+    import json
+    out = {}
+    for name, args in (("hypernerf", VARIANTS["hypernerf"]["args"]),
+                       ("neu3d", dict(multires=[1, 2], defor_depth=0, no_do=False, no_dshs=False, no_dlang=1))):
+        os.environ["language_feature_hiddendim"] = "3"
+        base = dict(net_width=128, timebase_pe=4, defor_depth=0, posebase_pe=10, scale_rotation_pe=2, opacity_pe=2,
+                    timenet_width=64, timenet_output=32, bounds=1.6,
+                    kplanes_config={"grid_dimensions": 2, "input_coordinate_dim": 4, "output_coordinate_dim": 16,
+                                    "resolution": [64, 64, 64, 150]},
+                    multires=[1, 2], no_dx=False, no_grid=False, no_ds=False, no_dr=False, no_do=True, no_dshs=True,
+                    no_dlang=1, empty_voxel=False, grid_pe=0, static_mlp=False, apply_rotation=False)
+        base.update(args)
+        net = deform_network(Namespace(**base))
+        out[name] = {k: list(v.shape) for k, v in net.state_dict().items()}
+    path = os.path.join(os.path.dirname(OUT), "deform_state_dict_layout.json")
+    with open(path, "w") as f:
+        json.dump(out, f, indent=0)
+    print("wrote", path)
+
+
 def main():
     deform_network = _import_reference()
+    if "--layout" in sys.argv:
+        state_dict_layout(deform_network)
+        return
     out = {}
     for i, (name, spec) in enumerate(VARIANTS.items()):
         d, used = make_variant(deform_network, name, spec, seed=10 * i)

@@ -253,7 +253,7 @@ def test_from_reference_is_strict():
         sd[f"deformation_net.{h}.3.weight"], sd[f"deformation_net.{h}.3.bias"] = torch.zeros(n, W), torch.zeros(n)
     sd["timenet.0.weight"], sd["time_poc"] = torch.zeros(64, 9), torch.zeros(4)
     hidden = dict(kplanes_config={"resolution": cfg["res"], "output_coordinate_dim": 16}, multires=cfg["multires"],
-                  defor_depth=1, no_dlang=1)
+                  defor_depth=1, no_dlang=1, net_width=128)
     g = DeformationField.from_reference(sd, hidden, env={"language_feature_hiddendim": "3"})
     assert g.heads_computed() == ["pos_deform", "scales_deform", "rotations_deform"]
     sd2 = dict(sd, **{"deformation_net.feature_out.2.weight": torch.zeros(W, W)})

@@ -103,3 +103,31 @@ def test_render_set_writes_eval_inputs(tmp_path):
         assert a.shape == (H, W, 6) and a.dtype == np.float32
         assert (base / "renders" / f"{i:05d}.png").stat().st_size > 0
     assert fps > 0
+
+
+def test_model_directory_load_and_render(tmp_path):
+    """A model directory in the reference's layout (save_model_dir: point_cloud.ply, deformation.pth
+    with the reference's keys, deformation_table / accum) loads back through load_model_dir (the
+    HyperNeRF field from the ModelHiddenParams, render.py's Scene(load_iteration=-1)) and renders
+    exactly what the in-memory model renders, in the fine-lang and fine-base stages."""
+    P = 2500
+    s = _scene(P=P, C=3)
+    hidden = dict(kplanes_config={"output_coordinate_dim": 16, "resolution": [12, 10, 9, 7]}, multires=[1, 2, 4],
+                  defor_depth=1, net_width=128, no_dlang=1)
+    params, cfg = DeformationField.config_from_reference(
+        {"deformation_net." + k: v for k, v in DeformationField.init_params(
+            [12, 10, 9, 7], [1, 2, 4], torch.stack([s.xyz.max(0).values, s.xyz.min(0).values]).cpu(), depth=1,
+            heads=("pos_deform", "scales_deform", "rotations_deform"), seed=5).items()}, hidden, env={})
+    s.deformation = DeformationField(params, device="cuda", **cfg)
+    s.extra["deformation_table"] = torch.ones(P, dtype=torch.bool)
+    for it in (3000, 9000):
+        gs.save_model_dir(s, str(tmp_path), it, "fine-lang")
+    m, it = gs.load_model_dir(str(tmp_path), hidden, env={"language_feature_hiddendim": "3"})
+    assert it == 9000 and m.deformation.heads_computed() == ["pos_deform", "scales_deform", "rotations_deform"]
+    bg = torch.ones(3, device="cuda")
+    for stage in ("fine-lang", "fine-base"):
+        a, b = gs.render(_cam(0.6), s, bg, stage=stage), gs.render(_cam(0.6), m, bg, stage=stage)
+        assert torch.equal(a["render"], b["render"]), stage
+        assert torch.equal(a["radii"], b["radii"]), stage
+    assert not torch.equal(gs.render(_cam(0.6), m, bg, stage="fine-lang")["render"],
+                           gs.render(_cam(0.6), m, bg, stage="coarse-lang")["render"])
