@@ -96,3 +96,37 @@ def test_densify_callback_runs_before_the_step():
     assert tr.steps["f_dc"] == 5 and tr.steps["xyz"] == 5   # iteration 3 skipped
     assert tr.steps["opacity"] == 4                          # iterations 3 and 5 skipped
     assert all(p.grad is None for p in tr.params.values())
+
+
+def test_reference_schedule_loop_fits_teacher():
+    """The configs[4] loop in miniature (tools/bench_train_loop.py at full size): create_from_pcd
+    init, the reference's learning-rate schedules, ReferenceSchedule densify / prune on a shortened
+    schedule; the mean loss falls window over window."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "bench_train_loop", os.path.join(os.path.dirname(__file__), "..", "tools", "bench_train_loop.py"))
+    btl = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(btl)
+    from train_step import ReferenceSchedule
+    args = type("A", (), dict(gaussians=3000, width=160, height=120, cameras=4, frames=2, point_noise=0.02,
+                              densify_until_iter=10_000))()
+    dev = torch.device("cuda")
+    step, _, pool, gts, extent = btl.build(args, dev)
+    sched = ReferenceSchedule(extent, densify_from_iter=10, densification_interval=10, pruning_from_iter=10,
+                              pruning_interval=20, densify_until_iter=60, min_points=3000)
+    step.densify = sched
+    g = torch.Generator().manual_seed(1)
+    windows, acc = [], 0.0
+    for it in range(1, 81):
+        idx = torch.randperm(len(pool), generator=g)[:2].tolist()
+        acc += float(step([pool[i] for i in idx], gts[idx], iteration=it))
+        if it % 20 == 0:
+            windows.append(acc / 20)
+            acc = 0.0
+    kinds = [(e[0], e[1]) for e in sched.events]
+    assert kinds[:3] == [(20, "densify"), (20, "prune"), (30, "densify")], sched.events
+    assert all(e[0] < 60 for e in sched.events)          # nothing past densify_until_iter
+    assert all(b < a for a, b in zip(windows, windows[1:])), windows
+    assert step.trainer.denom.shape[0] == step.trainer.P
+    assert step.trainer.lrs["xyz"] < 1.6e-4 * extent     # the xyz schedule decays
