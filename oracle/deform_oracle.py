@@ -183,7 +183,7 @@ class DeformOracle:
             res["rotations"] = rotations + outs["rotations_deform"]
         lc = None
         if c.lang_mode == "pass":
-            res["lang"] = lang[:, :c.lang_dim].copy()
+            res["lang"] = None if lang is None else lang[:, :c.lang_dim].copy()
         elif c.lang_mode == "discrete":
             e = lang[:, :c.lang_dim * c.centers].reshape(P, c.centers, c.lang_dim)
             en = np.linalg.norm(e, axis=2, keepdims=True)
@@ -226,6 +226,8 @@ class DeformOracle:
         g_in = dict(means3D=up_means3D.copy(), scales=up_scales.copy(), rotations=up_rotations.copy(),
                     opacity=up_opacity.copy(), shs=up_shs.copy())
         lang = f["lang"]
+        if lang is None:   # pass-through with no language rows: nothing to differentiate
+            lang = np.zeros((P, c.lang_dim))
         dlang_in = np.zeros_like(lang)
         ups = dict(pos_deform=up_means3D, scales_deform=up_scales, rotations_deform=up_rotations,
                    opacity_deform=up_opacity, shs_deform=up_shs.reshape(P, 48))
