@@ -407,16 +407,17 @@ void launch_deform_fwd(const DeformArgs& a, hipStream_t st) {
 // coordinate gradient (zero where border padding clips) goes to d_means3D.
 constexpr int DGP = 64 + 8;   // LDS row pitch (bf16) of the upstream-gradient rows (K padded to 64)
 
-// The block's 64 rows of a saved [P, DWID] fp32 activation as a buffer resource whose base is the
+// The block's rows of a saved [P, DWID] fp32 activation as a buffer resource whose base is the
 // block's first row: a row's offset is then a scalar constant (soffset), so the 32 rows a lane
 // stores share one address register (per-row 64-bit addresses, hoisted across the kernel, cost
-// ~64 VGPRs).  soffset is outside the hardware range check, so rows past P (the last block) are
-// skipped by a scalar branch on the block's row count.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(float* base, int g0) {
-    return __builtin_amdgcn_make_buffer_rsrc(base + (size_t)g0 * DWID, 0, DN * DWID * 4, 0x00020000);
+// ~64 VGPRs).  The hardware range check does not cover soffset, so a lane skips rows at or past
+// the block's row count itself (`lim` = the count minus the lane's row offset 4 hh in voff); the
+// resource's size is the block's rows as well.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(float* base, int g0, int nrows) {
+    return __builtin_amdgcn_make_buffer_rsrc(base + (size_t)g0 * DWID, 0, nrows * DWID * 4, 0x00020000);
 }
-__device__ __forceinline__ void store_row(__amdgpu_buffer_rsrc_t r, int voff, int row, int nrows, float v) {
-    if (row < nrows) __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(v), r, voff, row * DWID * 4, 0);
+__device__ __forceinline__ void store_row(__amdgpu_buffer_rsrc_t r, int voff, int row, int lim, float v) {
+    if (row < lim) __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(v), r, voff, row * DWID * 4, 0);
 }
 
 // DEEP: a feature_out chain of more than one layer (defor_depth >= 2; runtime length).  The
@@ -452,6 +453,7 @@ k_deform_bwd_a(DeformBwdArgs b) {
     // ---- chain forward, A_k = relu(H_k) saved ------------------------------------------------------
     const int voff = (4 * hh * DWID + col) * 4;   // this lane's byte offset in the saved rows (row 0)
     const int nrows = min(a.P - g0, DN);          // the block's rows (scalar)
+    const int rlim = nrows - 4 * hh;              // row_of(mt, q, 0) < rlim: this lane's row is one of them
     int cur = 0;
     for (int k = 0; k < L; ++k) {
         df32x16 acc[2] = {df32x16{}, df32x16{}};
@@ -464,7 +466,7 @@ k_deform_bwd_a(DeformBwdArgs b) {
         for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
             for (int q = 0; q < 16; ++q)
-                store_row(rows_rsrc(b.sA[k], g0), voff, row_of(mt, q, 0), nrows, fmaxf(acc[mt][q] + bias, 0.0f));
+                store_row(rows_rsrc(b.sA[k], g0, nrows), voff, row_of(mt, q, 0), rlim, fmaxf(acc[mt][q] + bias, 0.0f));
         __syncthreads();
         cur = dst;
     }
@@ -483,14 +485,14 @@ k_deform_bwd_a(DeformBwdArgs b) {
             df32x16 z[2] = {df32x16{}, df32x16{}};
             mlp_ntile<DWID>(z, ah, al, DAP, wave, a.w1_h[hd], a.w1_l[hd]);
             const float bias = a.b1[hd][col];
-            const __amdgpu_buffer_rsrc_t rA1 = rows_rsrc(b.sA1[slot], g0);
+            const __amdgpu_buffer_rsrc_t rA1 = rows_rsrc(b.sA1[slot], g0, nrows);
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
                 for (int q = 0; q < 16; ++q) {
                     const float zz = z[mt][q] + bias;
                     zpos |= zz > 0.0f ? 1u << (16 * mt + q) : 0u;
-                    store_row(rA1, voff, row_of(mt, q, 0), nrows, fmaxf(zz, 0.0f));
+                    store_row(rA1, voff, row_of(mt, q, 0), rlim, fmaxf(zz, 0.0f));
                 }
         }
         // gradient rows of this head's output, K padded to 64 (in the dZ1 buffer: free until below)
@@ -511,7 +513,7 @@ k_deform_bwd_a(DeformBwdArgs b) {
         mlp_ntile<64>(d, s_gh, s_gl, DGP, wave, b.w2t_h[hd], b.w2t_l[hd]);
         __syncthreads();   // every wave's G reads done before the dZ1 rows overwrite them
         {
-            const __amdgpu_buffer_rsrc_t rdZ1 = rows_rsrc(b.sdZ1[slot], g0);
+            const __amdgpu_buffer_rsrc_t rdZ1 = rows_rsrc(b.sdZ1[slot], g0, nrows);
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
@@ -522,7 +524,7 @@ k_deform_bwd_a(DeformBwdArgs b) {
                     dsplit(v, hi, lo);
                     bh[r * DAP + col] = hi;
                     bl[r * DAP + col] = lo;
-                    store_row(rdZ1, voff, row_of(mt, q, 0), nrows, v);
+                    store_row(rdZ1, voff, row_of(mt, q, 0), rlim, v);
                 }
         }
         __syncthreads();   // dZ1 rows complete
@@ -540,19 +542,18 @@ k_deform_bwd_a(DeformBwdArgs b) {
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const int r = row_of(mt, q, hh);
-                // [H_k > 0]: the last layer's A rows are still the heads' LDS input (relu >= 0, so
-                // positive iff its hi or lo part is); earlier layers' come back from the saved rows
-                const bool pos = k == L - 1
-                                     ? ((float)s_hh[cur][r * DAP + col] > 0.0f || (float)s_hl[cur][r * DAP + col] > 0.0f)
-                                     : row_of(mt, q, 0) < nrows &&
-                                           __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                                               rows_rsrc(b.sA[k], g0), voff, row_of(mt, q, 0) * DWID * 4, 0)) > 0.0f;
+                // [H_k > 0] from the saved rows (this block wrote them).  Reading it from the bf16
+                // hi / lo LDS rows the heads used instead (16-bit LDS loads) gave rare wrong rows
+                // at two blocks per CU (tools/deform_race.py): not kept.
+                const bool pos = row_of(mt, q, 0) < rlim &&
+                                 __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                                     rows_rsrc(b.sA[k], g0, nrows), voff, row_of(mt, q, 0) * DWID * 4, 0)) > 0.0f;
                 const float v = pos ? dA[mt][q] : 0.0f;
                 __bf16 hi, lo;
                 dsplit(v, hi, lo);
                 dh_h[r * DAP + col] = hi;
                 dh_l[r * DAP + col] = lo;
-                store_row(rows_rsrc(b.sdH[k], g0), voff, row_of(mt, q, 0), nrows, v);
+                store_row(rows_rsrc(b.sdH[k], g0, nrows), voff, row_of(mt, q, 0), rlim, v);
             }
         __syncthreads();
         cur ^= 1;
@@ -591,9 +592,23 @@ k_deform_bwd_a(DeformBwdArgs b) {
         float dq[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-            float4 v[6];
+            // the 4 taps of every plane loaded once: the sample (forward value) and, below, its
+            // coordinate derivative both come from them
+            float4 tp[6][4], v[6];
 #pragma unroll
-            for (int ci = 0; ci < 6; ++ci) v[ci] = sample4(a, 6 * s + ci, tap_of(a, 6 * s + ci, ci, crd), q);
+            for (int ci = 0; ci < 6; ++ci) {
+                const int pi = 6 * s + ci, W = a.pw[pi];
+                const Tap t = tap_of(a, pi, ci, crd);
+                const float4* pl = reinterpret_cast<const float4*>(a.planes + a.poff[pi]) + q;
+                tp[ci][0] = pl[(t.y0 * W + t.x0) * 4]; tp[ci][1] = pl[(t.y0 * W + t.x1) * 4];
+                tp[ci][2] = pl[(t.y1 * W + t.x0) * 4]; tp[ci][3] = pl[(t.y1 * W + t.x1) * 4];
+                const float w00 = (1.0f - t.fx) * (1.0f - t.fy), w01 = t.fx * (1.0f - t.fy), w10 = (1.0f - t.fx) * t.fy,
+                            w11 = t.fx * t.fy;
+                v[ci] = make_float4(tp[ci][0].x * w00 + tp[ci][1].x * w01 + tp[ci][2].x * w10 + tp[ci][3].x * w11,
+                                    tp[ci][0].y * w00 + tp[ci][1].y * w01 + tp[ci][2].y * w10 + tp[ci][3].y * w11,
+                                    tp[ci][0].z * w00 + tp[ci][1].z * w01 + tp[ci][2].z * w10 + tp[ci][3].z * w11,
+                                    tp[ci][0].w * w00 + tp[ci][1].w * w01 + tp[ci][2].w * w10 + tp[ci][3].w * w11);
+            }
             const float dxv[4] = {s_dx[gl][16 * s + 4 * q], s_dx[gl][16 * s + 4 * q + 1], s_dx[gl][16 * s + 4 * q + 2],
                                   s_dx[gl][16 * s + 4 * q + 3]};
 #pragma unroll
@@ -610,9 +625,7 @@ k_deform_bwd_a(DeformBwdArgs b) {
                 const float rx = (crd[kC0(ci)] + 1.0f) * 0.5f * (float)(W - 1);
                 const float ry = (crd[kC1(ci)] + 1.0f) * 0.5f * (float)(H - 1);
                 const Tap t = tap_of(a, pi, ci, crd);
-                const float4* pl = reinterpret_cast<const float4*>(a.planes + a.poff[pi]) + q;
-                const float4 t00 = pl[(t.y0 * W + t.x0) * 4], t01 = pl[(t.y0 * W + t.x1) * 4];
-                const float4 t10 = pl[(t.y1 * W + t.x0) * 4], t11 = pl[(t.y1 * W + t.x1) * 4];
+                const float4 t00 = tp[ci][0], t01 = tp[ci][1], t10 = tp[ci][2], t11 = tp[ci][3];
                 const float w00 = (1.0f - t.fx) * (1.0f - t.fy), w01 = t.fx * (1.0f - t.fy),
                             w10 = (1.0f - t.fx) * t.fy, w11 = t.fx * t.fy;
                 // scatter: stage the wave's 16 Gaussians (16 channels, 4 taps each) in LDS, then one

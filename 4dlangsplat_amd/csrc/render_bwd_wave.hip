@@ -49,76 +49,36 @@ constexpr int WGB = 48;      // G row pitch in bf16 at the one-off build: 32 lan
 constexpr int WWP = 20;      // W / t row pitch in bf16 (16 entries + 4): 40-byte rows, 8-byte aligned
 constexpr int WFIFO = 128;   // compacted entries waiting (list positions and ids); power of two
 
-// Per-wave LDS (one quadrant wave's staging; MERGE blocks hold four)
-struct BwdWaveLds {
-    __attribute__((aligned(16))) __bf16 FR[64 * WGB];   // G rows (build), then F / W / t rows
-    // group entries' screen-space data, one array per field (a b128 read gives 4 entries, a b64
-    // pair the operand of a packed-fp32 instruction): centre X, Y; staged conic -a/2, -b, -c/2
-    // (gauss_power); opacity; rgb, depth; list position k (0xFFFFFFFF past the group: never active)
-    __attribute__((aligned(16))) float X[WG], Y[WG], A[WG], B[WG], Cq[WG], O[WG];
-    __attribute__((aligned(16))) float R[WG], Gc[WG], Bc[WG], D[WG];
-    uint32_t gid[WG];
-    __attribute__((aligned(16))) uint32_t k[WG];
-    float mom[WG][8];
-    // results of the previous group, staged for its atomics / ring adds (issued one iteration late)
-    float q[WG][16];    // per-entry scalar gradients in acc_small record order (0..9)
-    float lq[WG][33];   // dL/dlanguage rows [e][c] (pitch 33: conflict-free stores)
-    uint32_t agid[WG], ak[WG];
-    uint32_t fk[WFIFO], fg[WFIFO];
-};
-
-// MERGE: the four quadrant waves of a tile in one 256-thread block add their per-entry partial
-// sums into an LDS ring keyed by list position (RCH-position chunks, NCH of them); a chunk is
-// flushed to the global accumulators, one atomic per (entry, quantity), once every wave has
-// passed it.  Protocol (all LDS, no block barrier after the start):
-//   prog[q]   positions >= prog[q] of quadrant q are merged into the ring (published before a
-//             wave waits and after each merge; a finished wave publishes 0)
-//   claim     chunks >= claim are claimed for flushing (atomicMin: disjoint, decreasing claims)
-//   owner[s]  the chunk that may use ring slot s; a flush of chunk c hands slot c % NCH to c - NCH
-// A wave merges a group only into owned chunks, and load_group never spans more than NCH chunks
-// from its top entry, so a waiting wave has always passed the chunks it waits for (no cycle).
-constexpr int RCH = 32, NCH = 4, RING = RCH * NCH;
-constexpr int RP = 44;   // ring row pitch (floats): language 0..31, records 32..41, gid 42
-constexpr uint32_t RING_EMPTY = 0xFFFFFFFFu;
-template <int NR>
-struct BwdRing {
-    float row[NR][RP];
-    int prog[4];
-    int claim;
-    int owner[NCH];
-};
-
 // C32: the 32-channel instantiation (headline), whose language rows are two float4 loads per lane
 // with no per-channel predication
 #ifndef LSR_BWD_WAVES
 #define LSR_BWD_WAVES 2   // waves per SIMD the register budget targets
 #endif
-template <bool C32, bool PRE, bool MERGE>
-__global__ void __launch_bounds__(MERGE ? 256 : 64) __attribute__((amdgpu_waves_per_eu(LSR_BWD_WAVES, LSR_BWD_WAVES)))
+template <bool C32, bool PRE>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LSR_BWD_WAVES, LSR_BWD_WAVES)))
 k_render_bwd_wave(RenderBwdArgs a) {
-    __shared__ BwdWaveLds s_w[MERGE ? 4 : 1];
-    __shared__ BwdRing<MERGE ? RING : 1> ring;
-    const int wave = MERGE ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
-    BwdWaveLds& L = s_w[wave];
-    __bf16* const s_FR = L.FR;
-    auto& s_X = L.X; auto& s_Y = L.Y; auto& s_A = L.A; auto& s_B = L.B; auto& s_C = L.Cq; auto& s_O = L.O;
-    auto& s_R = L.R; auto& s_Gc = L.Gc; auto& s_Bc = L.Bc; auto& s_D = L.D;
-    auto& s_gid = L.gid; auto& s_k = L.k; auto& s_mom = L.mom; auto& s_q = L.q; auto& s_lq = L.lq;
-    auto& s_agid = L.agid; auto& s_ak = L.ak; auto& s_fk = L.fk; auto& s_fg = L.fg;
+    __shared__ __attribute__((aligned(16))) __bf16 s_FR[64 * WGB];       // G rows (build), then F / W / t rows
+    // group entries' screen-space data, one array per field (a b128 read gives 4 entries, a b64
+    // pair the operand of a packed-fp32 instruction): centre X, Y; staged conic -a/2, -b, -c/2 (gauss_power); opacity; rgb,
+    // depth; list position k (0xFFFFFFFF past the group: never active)
+    __shared__ __attribute__((aligned(16))) float s_X[WG], s_Y[WG], s_A[WG], s_B[WG], s_C[WG], s_O[WG];
+    __shared__ __attribute__((aligned(16))) float s_R[WG], s_Gc[WG], s_Bc[WG], s_D[WG];
+    __shared__ uint32_t s_gid[WG];
+    __shared__ __attribute__((aligned(16))) uint32_t s_k[WG];
+    __shared__ float s_mom[WG][8];
+    // results of the previous group, staged for its atomics (issued one iteration late, see 6.)
+    __shared__ float s_q[WG][16];   // per-entry scalar gradients in acc_small record order (0..9)
+    __shared__ float s_lq[WG][33];  // dL/dlanguage rows [e][c] (pitch 33: conflict-free stores)
+    __shared__ uint32_t s_agid[WG];
+    __shared__ uint32_t s_fk[WFIFO];
+    __shared__ uint32_t s_fg[WFIFO];
 
     const int b = blockIdx.x;
-    int slot, quad;
-    if constexpr (MERGE) {
-        slot = b;
-        quad = wave;
-    } else {
-        slot = (b >> 5) * 8 + (b & 7);   // a slot's 4 quadrants: one XCD
-        quad = (b >> 3) & 3;
-    }
+    const int slot = (b >> 5) * 8 + (b & 7), quad = (b >> 3) & 3;   // a slot's 4 quadrants: one XCD
     if (slot >= a.grid_x * a.grid_y) return;
     // longest-first order (k_tile_order); column-major measured 0.61 vs 0.49 ms here
     const int tile = a.tile_order ? (int)a.tile_order[slot] : slot;
-    const int lane = threadIdx.x & 63, g4 = lane >> 4, l16 = lane & 15;
+    const int lane = threadIdx.x, g4 = lane >> 4, l16 = lane & 15;
     const int tx = tile % a.grid_x, ty = tile / a.grid_x;
     const int qx0 = tx * LSR_TILE_X + (quad & 1) * 8, qy0 = ty * LSR_TILE_Y + (quad >> 1) * 8;
     const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
@@ -129,20 +89,6 @@ k_render_bwd_wave(RenderBwdArgs a) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) nrep = max(nrep, (uint32_t)__shfl_xor((int)nrep, off));
     nrep = __builtin_amdgcn_readfirstlane(nrep);
-    if constexpr (MERGE) {   // ring: every row empty, progress = the quadrant's replay bound
-        for (int i = threadIdx.x; i < RING * RP; i += 256)
-            (&ring.row[0][0])[i] = (i % RP) == 42 ? __uint_as_float(RING_EMPTY) : 0.0f;
-        if (lane == 0) ring.prog[wave] = (int)nrep;
-        __syncthreads();
-        const int nmax = max(max(ring.prog[0], ring.prog[1]), max(ring.prog[2], ring.prog[3]));
-        const int nch = (nmax + RCH - 1) / RCH;
-        if (threadIdx.x < NCH) {   // slot s first holds the highest chunk c < nch with c % NCH == s
-            const int s0 = threadIdx.x;
-            ring.owner[s0] = nch - 1 >= s0 ? s0 + NCH * ((nch - 1 - s0) / NCH) : s0 - NCH;
-        }
-        if (threadIdx.x == 0) ring.claim = nch;
-        __syncthreads();
-    }
     if (nrep == 0) return;                                           // wave-uniform
     const uint2 range = a.ranges[tile];
     const int C = C32 ? 32 : (a.include_feature ? a.C : 0);   // language channels in play
@@ -271,15 +217,7 @@ k_render_bwd_wave(RenderBwdArgs a) {
         float2 xy;
         float4 co, rgbd, f0, f1;
     };
-    // FIFO entries [head, head + n) for n <= navail; returns n (MERGE: cut at NCH chunks below the
-    // top entry's chunk, see BwdRing)
-    auto load_group = [&](Pf& pf, int n) __attribute__((always_inline)) -> int {
-        if constexpr (MERGE) {
-            const uint32_t kk = lane < n ? s_fk[(head + lane) & (WFIFO - 1)] : 0u;
-            const int ktop = (int)__builtin_amdgcn_readfirstlane(kk);
-            const int lim = (ktop / RCH - NCH + 1) * RCH;
-            n = (int)__popcll(__ballot(lane < n && (int)kk >= lim));
-        }
+    auto load_group = [&](Pf& pf, int n) __attribute__((always_inline)) {   // FIFO entries [head, head + n)
         {
             const bool ok = lane < n;
             const int s = (head + lane) & (WFIFO - 1);
@@ -309,7 +247,6 @@ k_render_bwd_wave(RenderBwdArgs a) {
             pf.f1 = make_float4(f[4], f[5], f[6], f[7]);
         }
         head += n;
-        return n;
     };
     auto store_group = [&](const Pf& pf) __attribute__((always_inline)) {   // prefetched group -> LDS
         if (lane < WG) {
@@ -346,93 +283,7 @@ k_render_bwd_wave(RenderBwdArgs a) {
     //      the following iteration's, a whole group of compute later.  Offsets are 32-bit (P * 32
     //      floats < 2^32 bytes) so the addresses are SGPR base + VGPR offset. ---------------------
     int acnt = 0;   // entries staged
-    int dhead = 0;  // MERGE: FIFO entries before dhead are merged into the ring
-    // MERGE: flush chunk c (claimed by this wave) once it owns its slot: one atomic per nonzero
-    // (entry, quantity), rows re-zeroed, the slot handed to chunk c - NCH
-    auto flush_chunk = [&](int c) {
-        const int sl = c % NCH, r0 = sl * RCH;
-        while (__builtin_amdgcn_readfirstlane(*(volatile int*)&ring.owner[sl]) != c) __builtin_amdgcn_s_sleep(1);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        const uint32_t g = lane < RCH ? __float_as_uint(ring.row[r0 + lane][42]) : RING_EMPTY;
-        uint64_t m = __ballot(g != RING_EMPTY);
-        const int h = lane >> 5, ch = lane & 31;
-        while (m) {   // two entries per pass: lanes 0-31 the first, 32-63 the second
-            const int e0 = (int)__builtin_ctzll(m);
-            m &= m - 1;
-            const int e1 = m ? (int)__builtin_ctzll(m) : -1;
-            if (m) m &= m - 1;
-            const int e = h ? e1 : e0;
-            if (e >= 0) {
-                float* row = ring.row[r0 + e];
-                const uint32_t gid = __float_as_uint(row[42]);
-                const float v = row[ch];
-                const float w = ch < 10 ? row[32 + ch] : 0.0f;
-                if (a.acc_lang && ch < C && v != 0.0f) atomicAdd(at32(a.acc_lang, gid * (uint32_t)C + ch), v);
-                if (w != 0.0f) atomicAdd(at32(a.acc_small, gid * (uint32_t)ACC_PITCH + ch), w);
-                row[ch] = 0.0f;
-                if (ch < 10) row[32 + ch] = 0.0f;
-                if (ch == 10) row[42] = __uint_as_float(RING_EMPTY);
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane == 0) ring.owner[sl] = c - NCH;
-    };
-    // MERGE: publish this wave's progress, then claim and flush the chunks every wave has passed
-    auto publish = [&](int p) {
-        if (lane == 0) ring.prog[wave] = p;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        const volatile int* vp = ring.prog;
-        const int m = __builtin_amdgcn_readfirstlane(max(max(vp[0], vp[1]), max(vp[2], vp[3])));
-        const int mcc = (m + RCH - 1) / RCH;
-        if (mcc >= __builtin_amdgcn_readfirstlane(*(volatile int*)&ring.claim)) return;
-        int old = 0;
-        if (lane == 0) old = atomicMin(&ring.claim, mcc);
-        old = __builtin_amdgcn_readfirstlane(old);
-        for (int c = old - 1; c >= mcc; --c) flush_chunk(c);
-    };
-    auto merge_group = [&]() {
-        if (acnt == 0) return;
-        const int ktop = (int)s_ak[0], klast = (int)s_ak[acnt - 1];
-        publish(ktop + 1);   // every entry above the group is merged
-        const int ctop = ktop / RCH, clast = klast / RCH;
-        for (;;) {   // the group's chunks (at most NCH: load_group) must own their slots
-            bool wait = false;
-            if (lane < NCH) {
-                const int c = ctop - lane;
-                wait = c >= clast && *(volatile int*)&ring.owner[c % NCH] != c;
-            }
-            if (__ballot(wait) == 0) break;
-            __builtin_amdgcn_s_sleep(1);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        const int ch = lane & 31, q = lane & 15;
-#pragma unroll
-        for (int j = 0; j < WG / 2; ++j) {   // lane -> channel lane & 31 of entries (lane >> 5) + 2 j
-            const int e = (lane >> 5) + 2 * j;
-            if (e < acnt && ch < C) {
-                const float v = s_lq[e][ch];
-                if (v != 0.0f) atomicAdd(&ring.row[s_ak[e] & (RING - 1)][ch], v);
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < WG / 4; ++r) {   // lane -> field lane & 15 of entry (lane >> 4) + 4 r
-            const int e = (lane >> 4) + 4 * r;
-            if (e < acnt && q < 10) {
-                const float v = s_q[e][q];
-                if (v != 0.0f) atomicAdd(&ring.row[s_ak[e] & (RING - 1)][32 + q], v);
-            }
-        }
-        if (lane < acnt) ring.row[s_ak[lane] & (RING - 1)][42] = __uint_as_float(s_agid[lane]);
-        dhead += acnt;
-        acnt = 0;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        publish(dhead != tail ? (int)s_fk[dhead & (WFIFO - 1)] + 1 : pos);
-    };
     auto issue_atomics = [&]() {
-        if constexpr (MERGE) {
-            merge_group();
-            return;
-        }
         if (acnt == 0) return;
         // every staged value and row offset read from LDS first (one wait), then the atomics
         const int ch = lane & 31, q = lane & 15;
@@ -468,7 +319,7 @@ k_render_bwd_wave(RenderBwdArgs a) {
     scan_fill(WG);
     int cnt = min(WG, tail - head);
     Pf pf;
-    if (cnt > 0) cnt = load_group(pf, cnt);
+    if (cnt > 0) load_group(pf, cnt);
 #ifdef LSR_BWD_STAMPS
     unsigned long long st_sum[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_prev = 0;
 #endif
@@ -481,8 +332,8 @@ k_render_bwd_wave(RenderBwdArgs a) {
         issue_atomics();   // the previous group's (staging is rewritten only at this group's end)
         BWD_STAMP(3);
         // next group's loads in flight while this one computes
-        int next_cnt = min(WG, tail - head);
-        if (next_cnt > 0) next_cnt = load_group(pf, next_cnt);
+        const int next_cnt = min(WG, tail - head);
+        if (next_cnt > 0) load_group(pf, next_cnt);
         BWD_STAMP(4);
 
         // ---- 3. MFMA1: S[e][p], then to one pixel per lane -------------------------------------
@@ -636,10 +487,7 @@ k_render_bwd_wave(RenderBwdArgs a) {
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int nb = 0; nb < 2; ++nb) s_lq[4 * g4 + i][16 * nb + l16] = dacc[nb][i];
-        if (lane < WG) {
-            s_agid[lane] = s_gid[lane];
-            s_ak[lane] = s_k[lane];
-        }
+        if (lane < WG) s_agid[lane] = s_gid[lane];
         wave_lds_sync();
         if (lane < cnt) {   // moments -> mean2D (4-5), conic (6-8), opacity (9)
             const int e = lane;
@@ -665,7 +513,6 @@ k_render_bwd_wave(RenderBwdArgs a) {
         BWD_STAMP(8);
     }
     issue_atomics();   // the last group's
-    if constexpr (MERGE) publish(0);   // done: the last wave to finish flushes what is left
 #ifdef LSR_BWD_STAMPS
     if (lane < 8) {   // segments 0..7 (a vector atomic per lane)
         unsigned long long v = 0;
@@ -720,21 +567,10 @@ void launch_render_bwd_wave(const RenderBwdArgs& a, hipStream_t st) {
     const int ntiles = a.grid_x * a.grid_y;
     if (a.tile_order) launch_tile_order(ntiles, a.tile_max_contrib, nullptr, a.tile_order, st);
     const bool c32 = a.include_feature && a.C == 32;
-    static const bool merge = [] {
-        const char* e = getenv("LSR_BWD_MERGE");
-        return !(e && e[0] == '0');
-    }();
-    if (merge) {
-        const dim3 grid(ntiles);
-        if (c32 && a.lang_split) hipLaunchKernelGGL((k_render_bwd_wave<true, true, true>), grid, dim3(256), 0, st, a);
-        else if (c32) hipLaunchKernelGGL((k_render_bwd_wave<true, false, true>), grid, dim3(256), 0, st, a);
-        else hipLaunchKernelGGL((k_render_bwd_wave<false, false, true>), grid, dim3(256), 0, st, a);
-        return;
-    }
     const dim3 grid(((ntiles + 7) / 8) * 32);
-    if (c32 && a.lang_split) hipLaunchKernelGGL((k_render_bwd_wave<true, true, false>), grid, dim3(64), 0, st, a);
-    else if (c32) hipLaunchKernelGGL((k_render_bwd_wave<true, false, false>), grid, dim3(64), 0, st, a);
-    else hipLaunchKernelGGL((k_render_bwd_wave<false, false, false>), grid, dim3(64), 0, st, a);
+    if (c32 && a.lang_split) hipLaunchKernelGGL((k_render_bwd_wave<true, true>), grid, dim3(64), 0, st, a);
+    else if (c32) hipLaunchKernelGGL((k_render_bwd_wave<true, false>), grid, dim3(64), 0, st, a);
+    else hipLaunchKernelGGL((k_render_bwd_wave<false, false>), grid, dim3(64), 0, st, a);
 }
 
 }  // namespace lsr

@@ -204,30 +204,76 @@ def test_variant_forward_matches_reference(name):
                 assert _rel(got - base, ref - base) < 1e-4, k
 
 
+def _kink_masked_oracle(name, d, cfg):
+    """The float64 oracle (pinned to the reference's autograd by test_deform_oracle.py) on the
+    variant's inputs, with the upstream gradients of every Gaussian that has a ReLU input within
+    1e-4 of zero set to zero, and its backward.  Random 128-wide layers put ~1/3 of the golden's
+    300 Gaussians that close to a kink somewhere; there float32 / bf16-split pre-activations (error
+    ~1e-5) may fall on the other side than float64 and legitimately change that Gaussian's
+    gradients (the same masking as test_backward_matches_oracle_at_neu3d_resolution).  The language
+    inputs reach the kernel exactly (their ReLU decisions cannot differ) and are not masked on."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_deform_oracle import variant
+    _, dc, params, _, _ = variant(np.load(os.path.join(ROOT, "tests", "golden", "deform_variants.npz")), name)
+    o = DeformOracle(params, d["aabb"], cfg=dc)
+    f64 = lambda k: d[k].astype(np.float64)   # noqa: E731
+    o.forward(*[f64(k) for k in ("means3D", "scales", "rotations", "opacity", "shs", "lang", "time")])
+    zs = o.preactivations()
+    if dc.lang_mode in ("residual", "noresnet"):
+        zs[-3] = zs[-3][:, dc.lang_dim:]
+    amb = np.zeros(d["means3D"].shape[0], bool)
+    for v in zs:
+        amb |= (np.abs(v) < 1e-4).any(axis=1)
+    ups = {k: d["up_" + k].copy() for k in ("means3D", "scales", "rotations", "opacity", "shs", "lang", "coff")
+           if "up_" + k in d}
+    for v in ups.values():
+        v[amb] = 0.0
+    g_in, g_p = o.backward(*[ups[k].astype(np.float64) for k in KEYS], up_lang=ups["lang"].astype(np.float64),
+                           up_coff=ups["coff"].astype(np.float64) if "coff" in ups else None)
+    return ups, g_in, g_p, amb
+
+
 @pytest.mark.parametrize("name", VARIANTS)
 def test_variant_backward_matches_reference(name):
     """Input gradients (means3D through the HexPlane coordinates, rotations through the quaternion
     product, the language input through lang_deform / the discrete combination) and every
-    parameter gradient vs the reference's autograd."""
+    parameter gradient: within 1e-4 against the reference-pinned oracle once the kink-ambiguous
+    Gaussians' upstream is zeroed, and against the reference's autograd on the golden's full
+    upstream within 5e-2 of each tensor's range (kink flips, see _kink_masked_oracle)."""
     f, cfg, d = _variant_field(name)
-    t = lambda k: torch.tensor(d[k]).cuda() if k in d else None   # noqa: E731
-    f.zero_grad()
-    got = f.backward(t("means3D"), t("time")[:, 0], t("up_means3D"), t("up_scales"), t("up_rotations"),
-                     t("up_opacity"), t("up_shs"), rotations=t("rotations"), lang=t("lang"), d_lang=t("up_lang"),
-                     d_coff=t("up_coff"))
-    torch.cuda.synchronize()
-    for k, g in zip(("means3D", "scales", "rotations", "opacity", "shs", "lang"), got):
-        ref = d["grad_" + k]
-        assert _rel(g.cpu().numpy().reshape(ref.shape), ref) < 1e-4, k
-    grads = {k[len("grad/"):]: v for k, v in d.items() if k.startswith("grad/")}
-    assert set(f.grads) == set(grads)
-    for k, v in grads.items():
-        assert _rel(f.grads[k].cpu().numpy().reshape(v.shape), v) < 1e-4, k
+    t = lambda a: torch.tensor(a).cuda() if a is not None else None   # noqa: E731
+    names = ("means3D", "scales", "rotations", "opacity", "shs", "lang")
+
+    def run(ups):
+        f.zero_grad()
+        got = f.backward(t(d["means3D"]), t(d["time"][:, 0]), t(ups["up_means3D"]), t(ups["up_scales"]),
+                         t(ups["up_rotations"]), t(ups["up_opacity"]), t(ups["up_shs"]), rotations=t(d["rotations"]),
+                         lang=t(d["lang"]), d_lang=t(ups.get("up_lang")), d_coff=t(ups.get("up_coff")))
+        torch.cuda.synchronize()
+        return [g.cpu().numpy() for g in got], {k: v.cpu().numpy() for k, v in f.grads.items()}
+
+    ups, g_in, g_p, amb = _kink_masked_oracle(name, d, cfg)
+    assert amb.mean() < 0.5
+    got, grads = run({"up_" + k: v for k, v in ups.items()})
+    for k, g in zip(names, got):
+        assert _rel(g.reshape(g_in[k].shape), g_in[k]) < 1e-4, k
+    for k, v in g_p.items():
+        assert _rel(grads[k].reshape(v.shape), v) < 1e-4, k
+    # every Gaussian: the reference's own gradients, up to the kink flips (a flipped Gaussian moves
+    # whole rows of a weight gradient)
+    got, grads = run(d)
+    ref_grads = {k[len("grad/"):]: v for k, v in d.items() if k.startswith("grad/")}
+    assert set(grads) == set(ref_grads)
+    for k, g in zip(names, got):
+        assert _rel(g.reshape(d["grad_" + k].shape), d["grad_" + k]) < 5e-2, k
+    for k, v in ref_grads.items():
+        assert _rel(grads[k].reshape(v.shape), v) < 5e-2, k
 
 
 def test_variant_apply_autograd():
     """apply() with the discrete language and apply_rotation variants inside autograd: the same
-    gradients as backward()."""
+    gradients as backward() on the same upstream."""
     for name in ("discrete", "noresnet"):
         f, cfg, d = _variant_field(name)
         xs = [torch.tensor(d[k]).cuda().requires_grad_(True) for k in ("means3D", "scales", "rotations", "opacity",
@@ -237,8 +283,12 @@ def test_variant_apply_autograd():
                    zip(outs, ("means3D", "scales", "rotations", "opacity", "shs", "lang", "coff")) if o is not None)
         f.zero_grad()
         loss.backward()
-        for x, k in zip(xs, ("means3D", "scales", "rotations", "opacity", "shs", "lang")):
-            assert _rel(x.grad.cpu().numpy(), d["grad_" + k]) < 1e-4, (name, k)
+        t = lambda k: torch.tensor(d[k]).cuda() if k in d else None   # noqa: E731
+        ref = f.backward(t("means3D"), t("time")[:, 0], t("up_means3D"), t("up_scales"), t("up_rotations"),
+                         t("up_opacity"), t("up_shs"), rotations=t("rotations"), lang=t("lang"), d_lang=t("up_lang"),
+                         d_coff=t("up_coff"))
+        for x, r, k in zip(xs, ref, ("means3D", "scales", "rotations", "opacity", "shs", "lang")):
+            assert _rel(x.grad.cpu().numpy(), r.cpu().numpy().reshape(x.shape)) < 1e-6, (name, k)
 
 
 def test_from_reference_is_strict():

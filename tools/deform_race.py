@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Deformation backward repeatability and oracle agreement (diagnostic): the Neu3D-resolution case of
+tests/test_deform_gpu.py (P Gaussians, kink-ambiguous ones masked) run R times; d_means3D involves
+no atomics, so any run-to-run difference is a race.  LSR_LIBRARY selects a variant build."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in ("4dlangsplat_amd", "oracle", "tests"):
+    sys.path.insert(0, os.path.join(ROOT, p))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import test_deform_gpu as T  # noqa: E402
+from deform_oracle import DeformOracle  # noqa: E402
+
+
+def main():
+    P0 = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
+    R = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+    time = 0.37
+    params, res, multires, inp = T._neu3d_case(P0, seed=3)
+    a0, a1 = params["grid.aabb"][0], params["grid.aabb"][1]
+    crd = (inp["means3D"] - a0) * (2.0 / (a1 - a0)) - 1.0
+    keep = np.ones(P0, bool)
+    for m in multires:
+        for c in range(3):
+            u = (crd[:, c] + 1.0) * 0.5 * (res[c] * m - 1)
+            keep &= np.abs(u - np.round(u)) > 1e-3
+    inp = {k: v[keep] for k, v in inp.items()}
+    P = int(keep.sum())
+    rng = np.random.default_rng(5)
+    ups = dict(means3D=rng.normal(size=(P, 3)), scales=rng.normal(size=(P, 3)), rotations=rng.normal(size=(P, 4)),
+               opacity=rng.normal(size=(P, 1)), shs=rng.normal(size=(P, 16, 3)) * 0.1)
+    o = DeformOracle({k: v for k, v in params.items() if k != "grid.aabb"}, params["grid.aabb"])
+    o.forward(inp["means3D"], inp["scales"], inp["rotations"], inp["opacity"], inp["shs"], None, np.full((P, 1), time))
+    _, _, h, _, cache, _ = o._cache
+    amb = (np.abs(h) < 1e-4).any(axis=1)
+    for z, _ in cache.values():
+        amb |= (np.abs(z) < 1e-4).any(axis=1)
+    for k in T.KEYS:
+        ups[k][amb] = 0.0
+    g_in, g_p = o.backward(*[np.asarray(ups[k], np.float32).astype(np.float64) for k in T.KEYS])
+    f = T._field(params, res, multires)
+    t = lambda a: torch.tensor(np.asarray(a, np.float32)).cuda()   # noqa: E731
+    first = None
+    for r in range(R):
+        f.zero_grad()
+        got = f.backward(t(inp["means3D"]), time, *[t(ups[k]) for k in T.KEYS])
+        torch.cuda.synchronize()
+        dm = got[0].cpu().numpy()
+        err = T._rel(dm, g_in["means3D"])
+        perr = max(T._rel(g.cpu().numpy(), g_p[n].reshape(g.shape)) for n, g in f.grads.items())
+        bad = np.abs(dm - g_in["means3D"]).max(axis=1) > 1e-3 * np.abs(g_in["means3D"]).max()
+        same = "first" if first is None else ("identical" if np.array_equal(dm, first) else
+                                              f"DIFFERS at {int((dm != first).any(axis=1).sum())} rows")
+        first = dm if first is None else first
+        rows = np.nonzero(bad)[0]
+        print(f"run {r}: d_means3D rel {err:.2e} (bad rows {len(rows)}: {rows[:8].tolist()} blocks "
+              f"{sorted(set((rows // 64).tolist()))[:8]}), params rel {perr:.2e}, vs run 0: {same}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
