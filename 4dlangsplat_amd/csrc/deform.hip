@@ -37,36 +37,29 @@ __device__ __forceinline__ int row_of(int mt, int q, int hh) { return 32 * mt + 
 
 // Y[64 x 32] (+)= X[64 x K] W^T for N tile `nt`: both M tiles (the block's 64 Gaussians) share
 // every weight fragment, so a block reads each weight once per layer.
-// KC: weight fragments in flight per round (all of them by default: L2-resident, one round trip;
-// fewer where registers are short)
-template <int K, int KC = K / 16>
+template <int K>
 __device__ __forceinline__ void mlp_ntile(df32x16 (&acc)[2], const __bf16* __restrict__ xh, const __bf16* __restrict__ xl,
                                           int xp, int nt, const __bf16* __restrict__ wh, const __bf16* __restrict__ wl) {
     const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-    constexpr int NK = K / 16, C = KC < NK ? KC : NK;
+    // every weight fragment of the tile in flight at once (L2-resident, one round trip)
+    dbf16x8 bh[K / 16], bl[K / 16];
 #pragma unroll
-    for (int k0s = 0; k0s < NK; k0s += C) {
-        dbf16x8 bh[C], bl[C];
+    for (int ks = 0; ks < K / 16; ++ks) {
+        const size_t wo = (size_t)(32 * nt + r) * K + 16 * ks + 8 * h;
+        bh[ks] = *reinterpret_cast<const dbf16x8*>(wh + wo);
+        bl[ks] = *reinterpret_cast<const dbf16x8*>(wl + wo);
+    }
+    __builtin_amdgcn_sched_barrier(0);   // keep the loads issued here, ahead of the MFMAs
 #pragma unroll
-        for (int i = 0; i < C; ++i) {
-            if (k0s + i >= NK) break;
-            const size_t wo = (size_t)(32 * nt + r) * K + 16 * (k0s + i) + 8 * h;
-            bh[i] = *reinterpret_cast<const dbf16x8*>(wh + wo);
-            bl[i] = *reinterpret_cast<const dbf16x8*>(wl + wo);
-        }
-        __builtin_amdgcn_sched_barrier(0);   // keep the loads issued here, ahead of the MFMAs
+    for (int ks = 0; ks < K / 16; ++ks) {
+        const int k0 = 16 * ks + 8 * h;
 #pragma unroll
-        for (int i = 0; i < C; ++i) {
-            if (k0s + i >= NK) break;
-            const int k0 = 16 * (k0s + i) + 8 * h;
-#pragma unroll
-            for (int mt = 0; mt < 2; ++mt) {
-                const dbf16x8 ah = *reinterpret_cast<const dbf16x8*>(xh + (32 * mt + r) * xp + k0);
-                const dbf16x8 al = *reinterpret_cast<const dbf16x8*>(xl + (32 * mt + r) * xp + k0);
-                acc[mt] = DMFMA(ah, bh[i], acc[mt]);
-                acc[mt] = DMFMA(ah, bl[i], acc[mt]);
-                acc[mt] = DMFMA(al, bh[i], acc[mt]);
-            }
+        for (int mt = 0; mt < 2; ++mt) {
+            const dbf16x8 ah = *reinterpret_cast<const dbf16x8*>(xh + (32 * mt + r) * xp + k0);
+            const dbf16x8 al = *reinterpret_cast<const dbf16x8*>(xl + (32 * mt + r) * xp + k0);
+            acc[mt] = DMFMA(ah, bh[ks], acc[mt]);
+            acc[mt] = DMFMA(ah, bl[ks], acc[mt]);
+            acc[mt] = DMFMA(al, bh[ks], acc[mt]);
         }
     }
 }
@@ -407,39 +400,23 @@ void launch_deform_fwd(const DeformArgs& a, hipStream_t st) {
 // coordinate gradient (zero where border padding clips) goes to d_means3D.
 constexpr int DGP = 64 + 8;   // LDS row pitch (bf16) of the upstream-gradient rows (K padded to 64)
 
-// The block's rows of a saved [P, DWID] fp32 activation as a buffer resource whose base is the
-// block's first row: a row's offset is then a scalar constant (soffset), so the 32 rows a lane
-// stores share one address register (per-row 64-bit addresses, hoisted across the kernel, cost
-// ~64 VGPRs).  The hardware range check does not cover soffset, so a lane skips rows at or past
-// the block's row count itself (`lim` = the count minus the lane's row offset 4 hh in voff); the
-// resource's size is the block's rows as well.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(float* base, int g0, int nrows) {
-    return __builtin_amdgcn_make_buffer_rsrc(base + (size_t)g0 * DWID, 0, nrows * DWID * 4, 0x00020000);
-}
-__device__ __forceinline__ void store_row(__amdgpu_buffer_rsrc_t r, int voff, int row, int lim, float v) {
-    if (row < lim) __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(v), r, voff, row * DWID * 4, 0);
-}
-
 // DEEP: a feature_out chain of more than one layer (defor_depth >= 2; runtime length).  The
 // one-layer chain of every reference config gets its own instantiation: the runtime-length loops
 // cost registers (spills) even when they run once.
 template <int S, bool DEEP>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? 1 : 2, DEEP ? 1 : 2)))
-k_deform_bwd_a(DeformBwdArgs b) {
+__global__ void __launch_bounds__(256) k_deform_bwd_a(DeformBwdArgs b) {
     constexpr int F = 16 * S, XP = F + 8;
     static_assert(XP <= DAP, "feature rows live in the second hidden buffer");
-    // LDS: the two hidden-row buffers only (70 KB: two blocks per CU).  Everything else is carved
-    // from the buffer that is dead at the time: the features from buffer 1 (read by the first
-    // layer only, which writes buffer 0); a head's upstream-gradient rows G from the buffer its
-    // dZ1 rows then overwrite (a barrier between); dX and the plane-scatter staging from the
-    // chain's input buffer once the chain backward no longer reads it.
     __shared__ __attribute__((aligned(16))) __bf16 s_hh[2][DN * DAP];
     __shared__ __attribute__((aligned(16))) __bf16 s_hl[2][DN * DAP];
-    __bf16* const s_xh = s_hh[1];
+    __bf16* const s_xh = s_hh[1];   // read by the first layer only, which writes buffer 0
     __bf16* const s_xl = s_hl[1];
-    static_assert(DN * DGP <= DN * DAP, "G rows fit a hidden buffer");
-    static_assert(DN * (F + 1) * 4 <= DN * DAP * 2, "dX rows fit a hidden buffer");
-    static_assert((4 * 16 * 17 + 2 * 4 * 16 * 4) * 4 <= DN * DAP * 2, "scatter staging fits a hidden buffer");
+    __shared__ __attribute__((aligned(16))) __bf16 s_gh[DN * DGP];
+    __shared__ __attribute__((aligned(16))) __bf16 s_gl[DN * DGP];
+    __shared__ float s_dx[DN][F + 1];
+    __shared__ float s_sdv[4][16][17];   // plane scatter staging, per wave: dv of 16 Gaussians
+    __shared__ int s_soff[4][16][4];     //   their 4 tap offsets
+    __shared__ float s_sw[4][16][4];     //   and bilinear weights
     const DeformArgs& a = b.f;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int g0 = blockIdx.x * DN;
@@ -451,9 +428,6 @@ k_deform_bwd_a(DeformBwdArgs b) {
     __syncthreads();
 
     // ---- chain forward, A_k = relu(H_k) saved ------------------------------------------------------
-    const int voff = (4 * hh * DWID + col) * 4;   // this lane's byte offset in the saved rows (row 0)
-    const int nrows = min(a.P - g0, DN);          // the block's rows (scalar)
-    const int rlim = nrows - 4 * hh;              // row_of(mt, q, 0) < rlim: this lane's row is one of them
     int cur = 0;
     for (int k = 0; k < L; ++k) {
         df32x16 acc[2] = {df32x16{}, df32x16{}};
@@ -465,8 +439,10 @@ k_deform_bwd_a(DeformBwdArgs b) {
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-            for (int q = 0; q < 16; ++q)
-                store_row(rows_rsrc(b.sA[k], g0, nrows), voff, row_of(mt, q, 0), rlim, fmaxf(acc[mt][q] + bias, 0.0f));
+            for (int q = 0; q < 16; ++q) {
+                const int g = g0 + row_of(mt, q, hh);
+                if (g < a.P) b.sA[k][(size_t)g * DWID + col] = fmaxf(acc[mt][q] + bias, 0.0f);
+            }
         __syncthreads();
         cur = dst;
     }
@@ -485,19 +461,18 @@ k_deform_bwd_a(DeformBwdArgs b) {
             df32x16 z[2] = {df32x16{}, df32x16{}};
             mlp_ntile<DWID>(z, ah, al, DAP, wave, a.w1_h[hd], a.w1_l[hd]);
             const float bias = a.b1[hd][col];
-            const __amdgpu_buffer_rsrc_t rA1 = rows_rsrc(b.sA1[slot], g0, nrows);
+            float* sA1 = b.sA1[slot];
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
                 for (int q = 0; q < 16; ++q) {
                     const float zz = z[mt][q] + bias;
                     zpos |= zz > 0.0f ? 1u << (16 * mt + q) : 0u;
-                    store_row(rA1, voff, row_of(mt, q, 0), rlim, fmaxf(zz, 0.0f));
+                    const int r = row_of(mt, q, hh), g = g0 + r;
+                    if (g < a.P) sA1[(size_t)g * DWID + col] = fmaxf(zz, 0.0f);
                 }
         }
-        // gradient rows of this head's output, K padded to 64 (in the dZ1 buffer: free until below)
-        __bf16* const s_gh = bh;
-        __bf16* const s_gl = bl;
+        // gradient rows of this head's output, K padded to 64
         const float* G = coff ? b.sG_coff : quat ? b.sG_rot : b.up[hd];   // saved by the GRAD pass
         for (int i = tid; i < DN * 64; i += 256) {
             const int r = i >> 6, k = i & 63, g = g0 + r;
@@ -511,20 +486,19 @@ k_deform_bwd_a(DeformBwdArgs b) {
         __syncthreads();   // G rows complete (and the A1 rows consumed)
         df32x16 d[2] = {df32x16{}, df32x16{}};
         mlp_ntile<64>(d, s_gh, s_gl, DGP, wave, b.w2t_h[hd], b.w2t_l[hd]);
-        __syncthreads();   // every wave's G reads done before the dZ1 rows overwrite them
         {
-            const __amdgpu_buffer_rsrc_t rdZ1 = rows_rsrc(b.sdZ1[slot], g0, nrows);
+            float* sdZ1 = b.sdZ1[slot];
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
                 for (int q = 0; q < 16; ++q) {
-                    const int r = row_of(mt, q, hh);
+                    const int r = row_of(mt, q, hh), g = g0 + r;
                     const float v = (zpos >> (16 * mt + q)) & 1u ? d[mt][q] : 0.0f;
                     __bf16 hi, lo;
                     dsplit(v, hi, lo);
                     bh[r * DAP + col] = hi;
                     bl[r * DAP + col] = lo;
-                    store_row(rdZ1, voff, row_of(mt, q, 0), rlim, v);
+                    if (g < a.P) sdZ1[(size_t)g * DWID + col] = v;
                 }
         }
         __syncthreads();   // dZ1 rows complete
@@ -541,19 +515,14 @@ k_deform_bwd_a(DeformBwdArgs b) {
         for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
-                const int r = row_of(mt, q, hh);
-                // [H_k > 0] from the saved rows (this block wrote them).  Reading it from the bf16
-                // hi / lo LDS rows the heads used instead (16-bit LDS loads) gave rare wrong rows
-                // at two blocks per CU (tools/deform_race.py): not kept.
-                const bool pos = row_of(mt, q, 0) < rlim &&
-                                 __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                                     rows_rsrc(b.sA[k], g0, nrows), voff, row_of(mt, q, 0) * DWID * 4, 0)) > 0.0f;
-                const float v = pos ? dA[mt][q] : 0.0f;
+                const int r = row_of(mt, q, hh), g = g0 + r;
+                const float av = g < a.P ? b.sA[k][(size_t)g * DWID + col] : 0.0f;   // this block wrote it
+                const float v = av > 0.0f ? dA[mt][q] : 0.0f;
                 __bf16 hi, lo;
                 dsplit(v, hi, lo);
                 dh_h[r * DAP + col] = hi;
                 dh_l[r * DAP + col] = lo;
-                store_row(rows_rsrc(b.sdH[k], g0, nrows), voff, row_of(mt, q, 0), rlim, v);
+                if (g < a.P) b.sdH[k][(size_t)g * DWID + col] = v;
             }
         __syncthreads();
         cur ^= 1;
@@ -567,20 +536,15 @@ k_deform_bwd_a(DeformBwdArgs b) {
             df32x16 acc[2] = {df32x16{}, df32x16{}};
             mlp_ntile<DWID>(acc, dh_h, dh_l, DAP, wave, b.wft_h[0], b.wft_l[0]);
             const int c = 32 * wave + (lane & 31);
-            float* const dxr = reinterpret_cast<float*>(s_hh[cur ^ 1]);   // the chain's input rows: dead
             if (c < F) {
 #pragma unroll
                 for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-                    for (int q = 0; q < 16; ++q) dxr[row_of(mt, q, hh) * (F + 1) + c] = acc[mt][q];
+                    for (int q = 0; q < 16; ++q) s_dx[row_of(mt, q, hh)][c] = acc[mt][q];
             }
         }
     }
     __syncthreads();
-    float (*const s_dx)[F + 1] = reinterpret_cast<float (*)[F + 1]>(s_hh[cur ^ 1]);
-    float (*const s_sdv)[16][17] = reinterpret_cast<float (*)[16][17]>(s_hl[cur ^ 1]);   // per wave: dv of 16 Gaussians
-    int (*const s_soff)[16][4] = reinterpret_cast<int (*)[16][4]>(s_hl[cur ^ 1] + 2 * 4 * 16 * 17);   // their tap offsets
-    float (*const s_sw)[16][4] = reinterpret_cast<float (*)[16][4]>(s_hl[cur ^ 1] + 2 * (4 * 16 * 17 + 4 * 16 * 4));   // weights
 
     // ---- HexPlane backward: 4 threads per Gaussian, 4 channels each ----------------------------------
     {
@@ -592,23 +556,9 @@ k_deform_bwd_a(DeformBwdArgs b) {
         float dq[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-            // the 4 taps of every plane loaded once: the sample (forward value) and, below, its
-            // coordinate derivative both come from them
-            float4 tp[6][4], v[6];
+            float4 v[6];
 #pragma unroll
-            for (int ci = 0; ci < 6; ++ci) {
-                const int pi = 6 * s + ci, W = a.pw[pi];
-                const Tap t = tap_of(a, pi, ci, crd);
-                const float4* pl = reinterpret_cast<const float4*>(a.planes + a.poff[pi]) + q;
-                tp[ci][0] = pl[(t.y0 * W + t.x0) * 4]; tp[ci][1] = pl[(t.y0 * W + t.x1) * 4];
-                tp[ci][2] = pl[(t.y1 * W + t.x0) * 4]; tp[ci][3] = pl[(t.y1 * W + t.x1) * 4];
-                const float w00 = (1.0f - t.fx) * (1.0f - t.fy), w01 = t.fx * (1.0f - t.fy), w10 = (1.0f - t.fx) * t.fy,
-                            w11 = t.fx * t.fy;
-                v[ci] = make_float4(tp[ci][0].x * w00 + tp[ci][1].x * w01 + tp[ci][2].x * w10 + tp[ci][3].x * w11,
-                                    tp[ci][0].y * w00 + tp[ci][1].y * w01 + tp[ci][2].y * w10 + tp[ci][3].y * w11,
-                                    tp[ci][0].z * w00 + tp[ci][1].z * w01 + tp[ci][2].z * w10 + tp[ci][3].z * w11,
-                                    tp[ci][0].w * w00 + tp[ci][1].w * w01 + tp[ci][2].w * w10 + tp[ci][3].w * w11);
-            }
+            for (int ci = 0; ci < 6; ++ci) v[ci] = sample4(a, 6 * s + ci, tap_of(a, 6 * s + ci, ci, crd), q);
             const float dxv[4] = {s_dx[gl][16 * s + 4 * q], s_dx[gl][16 * s + 4 * q + 1], s_dx[gl][16 * s + 4 * q + 2],
                                   s_dx[gl][16 * s + 4 * q + 3]};
 #pragma unroll
@@ -625,7 +575,9 @@ k_deform_bwd_a(DeformBwdArgs b) {
                 const float rx = (crd[kC0(ci)] + 1.0f) * 0.5f * (float)(W - 1);
                 const float ry = (crd[kC1(ci)] + 1.0f) * 0.5f * (float)(H - 1);
                 const Tap t = tap_of(a, pi, ci, crd);
-                const float4 t00 = tp[ci][0], t01 = tp[ci][1], t10 = tp[ci][2], t11 = tp[ci][3];
+                const float4* pl = reinterpret_cast<const float4*>(a.planes + a.poff[pi]) + q;
+                const float4 t00 = pl[(t.y0 * W + t.x0) * 4], t01 = pl[(t.y0 * W + t.x1) * 4];
+                const float4 t10 = pl[(t.y1 * W + t.x0) * 4], t11 = pl[(t.y1 * W + t.x1) * 4];
                 const float w00 = (1.0f - t.fx) * (1.0f - t.fy), w01 = t.fx * (1.0f - t.fy),
                             w10 = (1.0f - t.fx) * t.fy, w11 = t.fx * t.fy;
                 // scatter: stage the wave's 16 Gaussians (16 channels, 4 taps each) in LDS, then one
@@ -879,12 +831,11 @@ void launch_lang_deform_bwd(const LangDeformArgs& a, hipStream_t st) {
 // splits it into bf16 hi / lo in registers; no LDS.  A wave owns a strip of 32x32 output tiles (one
 // M tile and every N tile when M = 128, else one N tile and every M tile), accumulates it over the
 // block's rows and adds it to C with one atomic per element.
-__device__ __forceinline__ void atb_load(const float* __restrict__ src, int ld, int col, int64_t g, int64_t row1,
-                                         float (&v)[8]) {
+__device__ __forceinline__ void atb_frag(const float* __restrict__ src, int ld, int col, int64_t g, int64_t row1,
+                                         dbf16x8& h8, dbf16x8& l8, float& sum) {
+    float v[8];
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) v[jj] = (g + jj < row1 && col < ld) ? src[(g + jj) * ld + col] : 0.0f;
-}
-__device__ __forceinline__ void atb_split(const float (&v)[8], dbf16x8& h8, dbf16x8& l8, float& sum) {
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
         __bf16 hi, lo;
@@ -903,49 +854,30 @@ __device__ __forceinline__ void atb_body(const AtbJob& j, int64_t row0, int64_t 
     if (ntile == 0) return;
     df32x16 acc[4] = {df32x16{}, df32x16{}, df32x16{}, df32x16{}};
     float bsum = 0.0f, dummy = 0.0f;
-    // software pipeline: the next 16 rows' operands are loaded while this 16 rows' MFMAs run
-    float vx[8], vy[4][8];   // STRIP_M: vx = the L strip, vy = the R tiles; else vx = R, vy = L tiles
-    auto load = [&](int64_t k0) {
-        const int64_t g = k0 + 8 * hh;
-        if (STRIP_M) {
-            atb_load(j.L, M, 32 * wave + r, g, row1, vx);
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-                if (t < ntile) atb_load(j.R, N, 32 * t + r, g, row1, vy[t]);
-        } else {
-            atb_load(j.R, N, 32 * wave + r, g, row1, vx);
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-                if (t < ntile) atb_load(j.L, M, 32 * t + r, g, row1, vy[t]);
-        }
-    };
-    load(row0);
     for (int64_t k0 = row0; k0 < row1; k0 += 16) {
-        dbf16x8 xh, xl, yh[4], yl[4];
+        const int64_t g = k0 + 8 * hh;
+        dbf16x8 ah[4], al[4], bh[4], bl[4];
         if (STRIP_M) {
-            atb_split(vx, xh, xl, bsum);
+            atb_frag(j.L, M, 32 * wave + r, g, row1, ah[0], al[0], bsum);
 #pragma unroll
             for (int t = 0; t < 4; ++t)
-                if (t < ntile) atb_split(vy[t], yh[t], yl[t], dummy);
+                if (t < ntile) atb_frag(j.R, N, 32 * t + r, g, row1, bh[t], bl[t], dummy);
         } else {
-            atb_split(vx, xh, xl, dummy);
 #pragma unroll
             for (int t = 0; t < 4; ++t)
-                if (t < ntile) atb_split(vy[t], yh[t], yl[t], t == wave ? bsum : dummy);
+                if (t < ntile) atb_frag(j.L, M, 32 * t + r, g, row1, ah[t], al[t], t == wave ? bsum : dummy);
+            atb_frag(j.R, N, 32 * wave + r, g, row1, bh[0], bl[0], dummy);
         }
-        if (k0 + 16 < row1) load(k0 + 16);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             if (t >= ntile) break;
-            if (STRIP_M) {   // A = L strip (M tile = wave), B = R tile t
-                acc[t] = DMFMA(xh, yh[t], acc[t]);
-                acc[t] = DMFMA(xh, yl[t], acc[t]);
-                acc[t] = DMFMA(xl, yh[t], acc[t]);
-            } else {         // A = L tile t, B = R strip (N tile = wave)
-                acc[t] = DMFMA(yh[t], xh, acc[t]);
-                acc[t] = DMFMA(yh[t], xl, acc[t]);
-                acc[t] = DMFMA(yl[t], xh, acc[t]);
-            }
+            const dbf16x8& xh = STRIP_M ? ah[0] : ah[t];
+            const dbf16x8& xl = STRIP_M ? al[0] : al[t];
+            const dbf16x8& yh = STRIP_M ? bh[t] : bh[0];
+            const dbf16x8& yl = STRIP_M ? bl[t] : bl[0];
+            acc[t] = DMFMA(xh, yh, acc[t]);
+            acc[t] = DMFMA(xh, yl, acc[t]);
+            acc[t] = DMFMA(xl, yh, acc[t]);
         }
     }
 #pragma unroll

@@ -158,10 +158,14 @@ class ViewParallelStep:
             b.zero_accumulated_()        # the flush writes every other field (HBM write saved)
         else:
             b.zero_()
+        radii_views = []
         for v in self.views:
             radii = render_view(v, b)
             if b.radii is not None and radii is not None:
-                torch.maximum(b.radii, radii.to(torch.int32), out=b.radii)
+                radii_views.append(radii)
+        # radii MAX over the views (train.py:270) after the views' launches, not between them
+        for radii in radii_views:
+            torch.maximum(b.radii, radii.to(torch.int32), out=b.radii)
         pending = []
         lo, hi = b.ranges["language_feature"]
         if self.world > 1 and b.radii is not None:   # final once the last view's forward ran

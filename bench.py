@@ -135,6 +135,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=3, help="headline frames timed on the CPU oracle")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-densify-stats", action="store_true",
+                    help="diagnostic: no means2D gradient / radii MAX in the step (train.py:350-352 needs them)")
     ap.add_argument("--early-views", type=int, default=3,
                     help="batched pipeline: views binned before compositing starts; the rest bin on a side stream "
                          "while they composite (0: all binned first)")
@@ -187,7 +189,7 @@ def run(args):
     scene = scene_cpu.to(dev)
     from view_parallel import GradBucket, ViewParallelStep, native_view_renderer
     M = scene.shs.shape[1]
-    bucket = GradBucket(P, M, C, dev, densify_stats=True)  # flat grads, 62 + C floats per Gaussian (means2D
+    bucket = GradBucket(P, M, C, dev, densify_stats=not args.no_densify_stats)  # flat grads, 62 + C floats (means2D
                                                            # for the densification statistics), radii MAX
     dp = ViewParallelStep(bucket, world * V)               # this rank's slice of the world*V batch
     all_cams = synthetic.camera_batch(world * V, W, H, tanfovx=tanfovx, seed=1)

@@ -45,10 +45,23 @@ def main():
     f = T._field(params, res, multires)
     t = lambda a: torch.tensor(np.asarray(a, np.float32)).cuda()   # noqa: E731
     first = None
+    first_dx = None
+    F = 16 * len(multires)
+    dx_off = ((P * F * 4 + 255) // 256) * 256          # deform_api.hip bwd_scratch: X, then dX
     for r in range(R):
         f.zero_grad()
         got = f.backward(t(inp["means3D"]), time, *[t(ups[k]) for k in T.KEYS])
         torch.cuda.synchronize()
+        dx = f._scratch[dx_off:dx_off + P * F * 4].view(torch.float32).reshape(P, F).cpu().numpy()
+        if first_dx is None:
+            first_dx = dx.copy()
+        elif not np.array_equal(dx, first_dx):
+            rows = np.nonzero((dx != first_dx).any(axis=1))[0]
+            print(f"run {r}: dX DIFFERS at rows {rows[:12].tolist()}", flush=True)
+            for rr in rows[:2]:
+                cols = np.nonzero(dx[rr] != first_dx[rr])[0]
+                print(f"   row {rr} cols {cols.tolist()}\n   got  {np.round(dx[rr][cols][:8], 5).tolist()}\n"
+                      f"   want {np.round(first_dx[rr][cols][:8], 5).tolist()}", flush=True)
         dm = got[0].cpu().numpy()
         err = T._rel(dm, g_in["means3D"])
         perr = max(T._rel(g.cpu().numpy(), g_p[n].reshape(g.shape)) for n, g in f.grads.items())

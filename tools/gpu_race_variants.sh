@@ -2,7 +2,7 @@
 # Deformation backward repeatability for each variant library (tools/deform_race.py).
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/race
-for v in cur ${VARIANTS:-base}; do
+for v in cur ${VARIANTS:-}; do
     lib=$PWD/4dlangsplat_amd/build/liblsr.so
     [ "$v" != cur ] && lib=$PWD/4dlangsplat_amd/build/variants/liblsr_$v.so
     LSR_LIBRARY=$lib timeout -k 10 200 python -u tools/deform_race.py ${P:-20000} ${R:-6} > gpurun_out/race/$v.log 2>&1
