@@ -50,13 +50,21 @@ constexpr int WWP = 20;      // W / t row pitch in bf16 (16 entries + 4): 40-byt
 constexpr int WFIFO = 128;   // compacted entries waiting (list positions and ids); power of two
 
 // C32: the 32-channel instantiation (headline), whose language rows are two float4 loads per lane
-// with no per-channel predication
+// with no per-channel predication.  NOL: no language channels in play (include_feature off or
+// C = 0: the RGB-only training and render.py passes): the F rows, MFMA1, the language half of
+// MFMA-W and its staging and atomics are compiled out, and the 64 VGPRs of B fragments they hold
+// with them, so the instantiation targets twice the occupancy.
 #ifndef LSR_BWD_WAVES
 #define LSR_BWD_WAVES 2   // waves per SIMD the register budget targets
 #endif
-template <bool C32, bool PRE>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LSR_BWD_WAVES, LSR_BWD_WAVES)))
+#ifndef LSR_BWD_WAVES_NOL
+#define LSR_BWD_WAVES_NOL 3
+#endif
+template <bool C32, bool PRE, bool NOL>
+__global__ void __launch_bounds__(64)
+__attribute__((amdgpu_waves_per_eu(NOL ? LSR_BWD_WAVES_NOL : LSR_BWD_WAVES, NOL ? LSR_BWD_WAVES_NOL : LSR_BWD_WAVES)))
 k_render_bwd_wave(RenderBwdArgs a) {
+    static_assert(!(NOL && C32), "NOL has no language channels");
     __shared__ __attribute__((aligned(16))) __bf16 s_FR[64 * WGB];       // G rows (build), then F / W / t rows
     // group entries' screen-space data, one array per field (a b128 read gives 4 entries, a b64
     // pair the operand of a packed-fp32 instruction): centre X, Y; staged conic -a/2, -b, -c/2 (gauss_power); opacity; rgb,
@@ -91,7 +99,7 @@ k_render_bwd_wave(RenderBwdArgs a) {
     nrep = __builtin_amdgcn_readfirstlane(nrep);
     if (nrep == 0) return;                                           // wave-uniform
     const uint2 range = a.ranges[tile];
-    const int C = C32 ? 32 : (a.include_feature ? a.C : 0);   // language channels in play
+    const int C = C32 ? 32 : (NOL ? 0 : (a.include_feature ? a.C : 0));   // language channels in play
     const float bx0 = (float)qx0, by0 = (float)qy0;
 
     const float T_final = inside ? a.final_T[pid] : 0.0f;
@@ -111,6 +119,7 @@ k_render_bwd_wave(RenderBwdArgs a) {
     //              (one fragment for both products: each reads only its own columns)
     bf16x8 b1h[4], b1l[4], b2h[2][2], b2l[2][2], bm[2];
     {
+        if constexpr (!NOL) {
         float gl[32];
 #pragma unroll
         for (int c = 0; c < 32; ++c)
@@ -143,6 +152,7 @@ k_render_bwd_wave(RenderBwdArgs a) {
                     if (part == 0) b2h[kb][nb] = v; else b2l[kb][nb] = v;
                 }
             wave_lds_sync();
+        }
         }
         // bm rows [p][n], pitch 16: pixel p = lane has local x = p & 7, y = p >> 3
         {
@@ -229,7 +239,9 @@ k_render_bwd_wave(RenderBwdArgs a) {
         }
         const int e = lane >> 2, c0 = 8 * (lane & 3);
         const uint32_t gid = e < n ? s_fg[(head + e) & (WFIFO - 1)] : 0u;
-        if constexpr (C32) {
+        if constexpr (NOL) {
+            (void)gid; (void)c0;
+        } else if constexpr (C32) {
             if constexpr (PRE) {   // hi / lo made once per batch (lsr_language_split): bits in f0 / f1
                 const uint4* q = reinterpret_cast<const uint4*>(a.lang_split);
                 pf.f0 = __builtin_bit_cast(float4, *at32(q, gid * 8u + (uint32_t)(c0 >> 3)));
@@ -257,7 +269,9 @@ k_render_bwd_wave(RenderBwdArgs a) {
             s_R[lane] = pf.rgbd.x; s_Gc[lane] = pf.rgbd.y; s_Bc[lane] = pf.rgbd.z; s_D[lane] = pf.rgbd.w;
         }
         const int e = lane >> 2, c0 = 8 * (lane & 3);
-        if constexpr (C32 && PRE) {
+        if constexpr (NOL) {
+            (void)e; (void)c0;
+        } else if constexpr (C32 && PRE) {
             *reinterpret_cast<uint4*>(s_Fh + e * WFP + c0) = __builtin_bit_cast(uint4, pf.f0);
             *reinterpret_cast<uint4*>(s_Fl + e * WFP + c0) = __builtin_bit_cast(uint4, pf.f1);
         } else {
@@ -289,11 +303,13 @@ k_render_bwd_wave(RenderBwdArgs a) {
         const int ch = lane & 31, q = lane & 15;
         float lv[WG / 2], sv[WG / 4];
         uint32_t lo[WG / 2], so[WG / 4];
+        if constexpr (!NOL) {
 #pragma unroll
-        for (int j = 0; j < WG / 2; ++j) {   // lane -> channel lane & 31 of entries (lane >> 5) + 2 j
-            const int e = (lane >> 5) + 2 * j;
-            lv[j] = s_lq[e][ch];
-            lo[j] = s_agid[e] * (uint32_t)C + ch;
+            for (int j = 0; j < WG / 2; ++j) {   // lane -> channel lane & 31 of entries (lane >> 5) + 2 j
+                const int e = (lane >> 5) + 2 * j;
+                lv[j] = s_lq[e][ch];
+                lo[j] = s_agid[e] * (uint32_t)C + ch;
+            }
         }
 #pragma unroll
         for (int r = 0; r < WG / 4; ++r) {   // lane -> field lane & 15 of entry (lane >> 4) + 4 r
@@ -305,7 +321,7 @@ k_render_bwd_wave(RenderBwdArgs a) {
         // atomics and skip them in its waits for later loads) measured 0.70 vs 0.50 ms: with no
         // wait behind them a wave keeps several groups of atomics in flight and the memory
         // system backs up.  The wait that follows each batch throttles them.
-        if (a.acc_lang) {   // 128-byte rows
+        if (!NOL && a.acc_lang) {   // 128-byte rows
 #pragma unroll
             for (int j = 0; j < WG / 2; ++j)
                 if ((lane >> 5) + 2 * j < acnt && ch < C && lv[j] != 0.0f) atomicAdd(at32(a.acc_lang, lo[j]), lv[j]);
@@ -338,7 +354,10 @@ k_render_bwd_wave(RenderBwdArgs a) {
 
         // ---- 3. MFMA1: S[e][p], then to one pixel per lane -------------------------------------
         float S[WG];
-        {
+        if constexpr (NOL) {
+#pragma unroll
+            for (int e = 0; e < WG; ++e) S[e] = 0.0f;
+        } else {
             const bf16x8 ah = *reinterpret_cast<const bf16x8*>(s_Fh + l16 * WFP + 8 * g4);
             const bf16x8 al = *reinterpret_cast<const bf16x8*>(s_Fl + l16 * WFP + 8 * g4);
             f32x4 d[4];
@@ -448,11 +467,13 @@ k_render_bwd_wave(RenderBwdArgs a) {
         for (int kb = 0; kb < 2; ++kb) {
             bf16x8 ah, al;
             read_a(kb, ah, al);
+            if constexpr (!NOL) {
 #pragma unroll
-            for (int nb = 0; nb < 2; ++nb) {
-                dacc[nb] = LSR_MFMA16(ah, b2h[kb][nb], dacc[nb]);
-                dacc[nb] = LSR_MFMA16(ah, b2l[kb][nb], dacc[nb]);
-                dacc[nb] = LSR_MFMA16(al, b2h[kb][nb], dacc[nb]);
+                for (int nb = 0; nb < 2; ++nb) {
+                    dacc[nb] = LSR_MFMA16(ah, b2h[kb][nb], dacc[nb]);
+                    dacc[nb] = LSR_MFMA16(ah, b2l[kb][nb], dacc[nb]);
+                    dacc[nb] = LSR_MFMA16(al, b2h[kb][nb], dacc[nb]);
+                }
             }
             dacc[2] = LSR_MFMA16(ah, bm[kb], dacc[2]);   // w hi and lo times g hi (6..9) and lo (10..13)
             dacc[2] = LSR_MFMA16(al, bm[kb], dacc[2]);
@@ -483,10 +504,12 @@ k_render_bwd_wave(RenderBwdArgs a) {
         }
         BWD_STAMP(7);
         // stage the group's results: language rows from the MFMA layout, gids
+        if constexpr (!NOL) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int nb = 0; nb < 2; ++nb) s_lq[4 * g4 + i][16 * nb + l16] = dacc[nb][i];
+                for (int nb = 0; nb < 2; ++nb) s_lq[4 * g4 + i][16 * nb + l16] = dacc[nb][i];
+        }
         if (lane < WG) s_agid[lane] = s_gid[lane];
         wave_lds_sync();
         if (lane < cnt) {   // moments -> mean2D (4-5), conic (6-8), opacity (9)
@@ -567,10 +590,12 @@ void launch_render_bwd_wave(const RenderBwdArgs& a, hipStream_t st) {
     const int ntiles = a.grid_x * a.grid_y;
     if (a.tile_order) launch_tile_order(ntiles, a.tile_max_contrib, nullptr, a.tile_order, st);
     const bool c32 = a.include_feature && a.C == 32;
+    const bool nol = !a.include_feature || a.C == 0;
     const dim3 grid(((ntiles + 7) / 8) * 32);
-    if (c32 && a.lang_split) hipLaunchKernelGGL((k_render_bwd_wave<true, true>), grid, dim3(64), 0, st, a);
-    else if (c32) hipLaunchKernelGGL((k_render_bwd_wave<true, false>), grid, dim3(64), 0, st, a);
-    else hipLaunchKernelGGL((k_render_bwd_wave<false, false>), grid, dim3(64), 0, st, a);
+    if (c32 && a.lang_split) hipLaunchKernelGGL((k_render_bwd_wave<true, true, false>), grid, dim3(64), 0, st, a);
+    else if (c32) hipLaunchKernelGGL((k_render_bwd_wave<true, false, false>), grid, dim3(64), 0, st, a);
+    else if (nol) hipLaunchKernelGGL((k_render_bwd_wave<false, false, true>), grid, dim3(64), 0, st, a);
+    else hipLaunchKernelGGL((k_render_bwd_wave<false, false, false>), grid, dim3(64), 0, st, a);
 }
 
 }  // namespace lsr
