@@ -21,7 +21,7 @@ import time as _time
 import zlib
 import struct
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 import torch
@@ -253,11 +253,12 @@ def read_ply_vertices(path: str) -> Dict[str, np.ndarray]:
 def render(viewpoint_camera, pc: GaussianScene, bg_color: torch.Tensor, scaling_modifier: float = 1.0,
            override_color=None, stage: str = "fine-lang", compute_cov3D_python: bool = False,
            convert_SHs_python: bool = False, debug: bool = False, nonormalized: bool = False,
-           language_feature_hiddendim: int = 3):
+           language_feature_hiddendim: int = 3, _deformed=None):
     """The reference's render() on this build's rasterizer.  viewpoint_camera: FoVx, FoVy,
     image_width, image_height, world_view_transform, full_proj_transform, camera_center, time
     (synthetic.Camera or the reference Camera).  Environment switches of the reference
-    (nonormalized, language_feature_hiddendim) are arguments here."""
+    (nonormalized, language_feature_hiddendim) are arguments here.  _deformed: this view's
+    deformation outputs, already evaluated (render_views); the field is then not called."""
     from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
 
     dev = pc.xyz.device
@@ -291,7 +292,9 @@ def render(viewpoint_camera, pc: GaussianScene, bg_color: torch.Tensor, scaling_
     else:
         scales, rotations = pc.scaling, pc.rotation
     coff = None
-    if "coarse" in stage:
+    if _deformed is not None:
+        m3, s3, r3, o3, sh3, l3, coff = _deformed
+    elif "coarse" in stage:
         m3, s3, r3, o3, sh3, l3 = means3D, scales, rotations, opacity, shs, lang
     elif "fine" in stage:
         if pc.deformation is None:
@@ -327,6 +330,39 @@ def render(viewpoint_camera, pc: GaussianScene, bg_color: torch.Tensor, scaling_
         lang_img = None
     return {"render": image, "language_feature_image": lang_img, "viewspace_points": screenspace_points,
             "visibility_filter": radii > 0, "radii": radii, "depth": depth, "coff": coff}
+
+
+def render_views(cams: Sequence, pc: GaussianScene, bg_color: torch.Tensor, stage: str = "fine-lang",
+                 nonormalized: bool = False, language_feature_hiddendim: int = 3, **kw):
+    """render() for each camera of a batch, the deformation field evaluated ONCE for all of them.
+    train.py:242-268 renders the batch's views one after the other, each with its own
+    deform_network call at that view's time; here the Gaussians are repeated once per view and
+    the field runs one launch over V * P rows (row block v at cams[v].time), then each view
+    rasterizes its block.  Same values as the per-view loop (the field is per-row); the
+    field's backward then runs once per iteration, not once per view (its plane-gradient
+    replicas are cleared and folded once).  Falls back to per-view render() outside the 'fine'
+    stages or for one view."""
+    if "fine" not in stage or pc.deformation is None or len(cams) < 2 or kw.get("compute_cov3D_python"):
+        return [render(c, pc, bg_color, stage=stage, nonormalized=nonormalized,
+                       language_feature_hiddendim=language_feature_hiddendim, **kw) for c in cams]
+    dev = pc.xyz.device
+    V, P = len(cams), pc.P
+    if "base" not in stage:
+        lang = pc.get_language_feature
+        if not nonormalized:
+            lang = lang / (lang.norm(dim=-1, keepdim=True) + 1e-9)
+    else:
+        lang = torch.zeros((P, language_feature_hiddendim), dtype=pc.opacity.dtype, device=dev)
+    rep = lambda x: x.repeat(V, *([1] * (x.dim() - 1)))   # noqa: E731
+    t = torch.cat([torch.full((P,), float(c.time), device=dev) for c in cams])
+    deform = pc.deformation.apply if (torch.is_grad_enabled() and hasattr(pc.deformation, "apply")) \
+        else pc.deformation
+    outs = deform(rep(pc.get_xyz), rep(pc.scaling), rep(pc.rotation), rep(pc.opacity), rep(pc.get_features),
+                  rep(lang), t, no_dlang=True if "base" in stage else None)
+    parts = [o.split(P) if o is not None else (None,) * V for o in outs]
+    return [render(c, pc, bg_color, stage=stage, nonormalized=nonormalized,
+                   language_feature_hiddendim=language_feature_hiddendim,
+                   _deformed=tuple(p[v] for p in parts), **kw) for v, c in enumerate(cams)]
 
 
 _SH_C0 = 0.28209479177387814

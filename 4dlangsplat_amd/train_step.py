@@ -27,7 +27,7 @@ from typing import Callable, Optional, Sequence
 
 import torch
 
-from gaussian_scene import GaussianScene, render
+from gaussian_scene import GaussianScene, render, render_views
 from gaussian_train import GaussianTrainer, TensorAdam, get_expon_lr_func
 
 
@@ -87,10 +87,15 @@ class TrainStep:
 
     def __init__(self, trainer: GaussianTrainer, field=None, deform_lr: float = 1.6e-4, grid_lr: float = 1.6e-3,
                  bg: Optional[torch.Tensor] = None, stage: str = "fine-base", sh_degree: int = 3,
-                 densify: Optional[Callable[[GaussianTrainer, int], None]] = None):
+                 densify: Optional[Callable[[GaussianTrainer, int], None]] = None, batch_views: bool = False):
         """densify(trainer, iteration): optional densify / prune / reset_opacity schedule, run
-        between the densification statistics and the optimizer step (train.py:388-421)."""
+        between the densification statistics and the optimizer step (train.py:388-421).
+        batch_views: the batch's views share one deformation-field launch (render_views)
+        instead of one per view (render); same values.  Off by default: at configs[4] size
+        the repeat / split copies around the one launch cost more than the per-call fixed work
+        saved (127.8 vs 140.5 iterations/s)."""
         self.trainer, self.field, self.stage = trainer, field, stage
+        self.batch_views = batch_views
         self.densify = densify
         self.iteration = 0
         self.sh_degree = sh_degree
@@ -141,7 +146,10 @@ class TrainStep:
         if self.field is not None:
             self.field.zero_grad()
         sc = self.scene()
-        outs = [render(cam, sc, self.bg, stage=self.stage) for cam in cams]
+        if self.batch_views:
+            outs = render_views(cams, sc, self.bg, stage=self.stage)
+        else:
+            outs = [render(cam, sc, self.bg, stage=self.stage) for cam in cams]
         images = torch.stack([o["render"] for o in outs])
         loss = (images - gts).abs().mean()
         loss.backward()

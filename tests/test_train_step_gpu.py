@@ -3,6 +3,7 @@ through lsr_deform_backward) -> rasterizer for 2 views -> L1 -> backward -> dens
 statistics -> Adam on the Gaussians (lsr_adam_step) and on the field (TensorAdam), densify and
 prune between iterations.  No oracle: the check is that the pieces compose (shapes, gradient
 flow, every parameter moves) and that the loss falls when fitting renders of a teacher scene."""
+import dataclasses
 import math
 
 import numpy as np
@@ -11,7 +12,7 @@ import torch
 
 import synthetic
 from deformation import DeformationField
-from gaussian_scene import render
+from gaussian_scene import render, render_views
 from gaussian_train import GaussianTrainer
 from train_step import TrainStep
 
@@ -130,3 +131,42 @@ def test_reference_schedule_loop_fits_teacher():
     assert all(b < a for a, b in zip(windows, windows[1:])), windows
     assert step.trainer.denom.shape[0] == step.trainer.P
     assert step.trainer.lrs["xyz"] < 1.6e-4 * extent     # the xyz schedule decays
+
+
+def test_render_views_matches_per_view_render():
+    """render_views (one deformation launch over V * P rows) against render() per view: the field
+    is per row, so images and radii are bit-identical; the Gaussians' and the field's gradients
+    agree up to the summation order of the atomics and of the views."""
+    P, W, H = 3000, 128, 96
+    dev = torch.device("cuda")
+    sc = synthetic.make_scene(P, C=3, tanfovx=0.6, tanfovy=0.6 * H / W, seed=5, logscale_mean=-3.0).to(dev)
+    cams = synthetic.camera_batch(3, W, H, tanfovx=0.6, seed=2)
+    cams = [dataclasses.replace(c, time=0.2 + 0.3 * i) for i, c in enumerate(cams)]
+    field_p = DeformationField.init_params(RES, MULTIRES, AABB, seed=1)
+    gts = torch.rand(len(cams), 3, H, W, device=dev)
+    res = []
+    for batched in (False, True):
+        field = DeformationField({k: v.to(dev) for k, v in field_p.items()}, RES, MULTIRES)
+        tr = GaussianTrainer(_raw(sc, P), LRS)
+        step = TrainStep(tr, field, batch_views=batched)
+        field.zero_grad()
+        scene = step.scene()
+        outs = render_views(cams, scene, step.bg, stage="fine-base") if batched else \
+            [render(c, scene, step.bg, stage="fine-base") for c in cams]
+        images = torch.stack([o["render"] for o in outs])
+        (images - gts).abs().mean().backward()
+        torch.cuda.synchronize()
+        res.append(dict(images=images.detach(), radii=torch.stack([o["radii"] for o in outs]),
+                        vs=torch.stack([o["viewspace_points"].grad for o in outs]),
+                        g={k: v.grad.clone() for k, v in tr.params.items()},
+                        f={k: v.clone() for k, v in field.grads.items()}))
+    a, b = res
+    assert torch.equal(a["images"], b["images"]) and torch.equal(a["radii"], b["radii"])
+    torch.testing.assert_close(b["vs"], a["vs"], rtol=1e-4, atol=1e-9)
+    for k in a["g"]:
+        torch.testing.assert_close(b["g"][k], a["g"][k], rtol=1e-4, atol=1e-8 * float(a["g"][k].abs().max()) + 1e-12,
+                                   msg=k)
+    for k in a["f"]:
+        scale = float(a["f"][k].abs().max())
+        err = float((b["f"][k] - a["f"][k]).abs().max())
+        assert err <= 1e-4 * scale + 1e-12, (k, err, scale)

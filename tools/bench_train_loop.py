@@ -115,13 +115,17 @@ def build(args, dev):
 
 
 def deformation_ms(step, views, reps=10):
-    """The field's share of one iteration at the current size: forward + backward per view (as
-    render() calls it) and its Adam + repack, event-timed on the current stream."""
+    """The field's share of one iteration at the current size: forward + backward for the views
+    (one call over views * P rows as render_views makes it, or one per view as render() does
+    when step.batch_views is off) and its Adam + repack, event-timed on the current stream."""
     tr, field = step.trainer, step.field
     sc = step.scene()
     P = tr.P
     args = (sc.xyz.detach(), sc.scaling.detach(), sc.rotation.detach(), sc.opacity.detach(),
             sc.get_features.detach(), None)
+    if step.batch_views and views > 1:
+        args = tuple(a.repeat(views, *([1] * (a.dim() - 1))) for a in args[:5]) + (None,)
+        P, views = P * views, 1
     ups = [torch.randn(P, 3, device=tr.device) * 1e-3, torch.randn(P, 3, device=tr.device) * 1e-3,
            torch.randn(P, 4, device=tr.device) * 1e-3, torch.randn(P, 1, device=tr.device) * 1e-3,
            torch.randn(P, 16, 3, device=tr.device) * 1e-3]
@@ -164,11 +168,14 @@ def main():
     ap.add_argument("--window", type=int, default=100)
     ap.add_argument("--point-noise", type=float, default=0.02)
     ap.add_argument("--densify-until-iter", type=int, default=10_000)
+    ap.add_argument("--batched-deform", action="store_true",
+                    help="one deformation launch per iteration over all views (render_views) instead of one per view")
     args = ap.parse_args()
     dev = torch.device("cuda")
     torch.manual_seed(0)
     t_setup = time.perf_counter()
     step, sched, pool, gts, extent = build(args, dev)
+    step.batch_views = args.batched_deform
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t_setup
     P0 = step.trainer.P
@@ -204,13 +211,15 @@ def main():
                 gaussians_initial=P0, gaussians_final=step.trainer.P,
                 schedule_events=[list(e) for e in sched.events],
                 deformation=dict(forward_ms=round(f_ms, 3), backward_ms=round(b_ms, 3), adam_repack_ms=round(o_ms, 3),
+                                 batched_views=step.batch_views,
                                  ms_per_iteration=round(deform, 3),
                                  share_of_last_window=round(deform / last, 3) if last > 0 else None,
                                  note="forward/backward are per iteration (all views), at the final size"),
                 setup_s=round(setup_s, 1), cameras_extent=round(extent, 4),
                 config=dict(workload="configs[4] stand-in: synthetic teacher, Neu3D field, fine-base",
                             gaussians=args.gaussians, views_per_iteration=args.views, width=args.width,
-                            height=args.height, pool=len(pool), resolution=NEU3D_RES, multires=NEU3D_MULTIRES),
+                            height=args.height, pool=len(pool), resolution=NEU3D_RES, multires=NEU3D_MULTIRES,
+                            deformation_launches="one per iteration" if args.batched_deform else "per view"),
                 data="synthetic")
     print(json.dumps(line))
 
