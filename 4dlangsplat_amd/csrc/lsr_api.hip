@@ -502,34 +502,57 @@ int lsr_forward_binning_views(int32_t n_views, const lsr_settings* const* s, con
 
 int lsr_forward_composite(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_out* out, const void* geom,
                           const void* binning, void* img, int64_t num_rendered, lsr_stream_t stream) {
-    int rc = check_common(s, in);
-    if (rc) return rc;
-    if (!out || !out->out_color || !out->out_depth) return fail(LSR_EINVAL, "color and depth outputs are required");
-    if (in->C > 0 && !out->out_language_feature) return fail(LSR_EINVAL, "language feature output is required when C > 0");
-    if (!geom || !img || (num_rendered > 0 && !binning)) return fail(LSR_EINVAL, "workspaces are required");
-    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const int P = in->P, W = s->image_width, H = s->image_height, C = in->C;
-    const int gx = (W + LSR_TILE_X - 1) / LSR_TILE_X, gy = (H + LSR_TILE_Y - 1) / LSR_TILE_Y;
-    const size_t K = (size_t)num_rendered;
-    Geom g = carve_geom(const_cast<void*>(geom), (size_t)(P > 0 ? P : 1), nullptr);
-    Binning b = carve_binning(const_cast<void*>(binning), K > 0 ? K : 1, nullptr);
-    Img m = carve_img(img, W, H, nullptr);   // tile_max was zeroed by the binning (atomicMax: idempotent)
-    const uint32_t* point_list = K > 0 ? (tile_sort_in_b(gx * gy) ? b.val_b : b.val_a) : nullptr;
-    lsr::RenderFwdArgs r{};
-    r.W = W; r.H = H; r.grid_x = gx; r.grid_y = gy; r.C = C; r.include_feature = s->include_feature;
-    r.ranges = m.ranges; r.point_list = point_list; r.xy = g.xy; r.conic_o = g.conic_o; r.rgbd = g.rgbd;
-    r.lang = in->language_feature;
-    r.lang_split = in->C == 32 ? in->language_feature_split : nullptr; r.bg = s->bg; r.final_T = m.final_T; r.n_contrib = m.n_contrib;
-    r.tile_max_contrib = m.tile_max; r.tile_order = m.tile_order;
-    r.out_color = out->out_color; r.out_lang = out->out_language_feature;
-    r.out_depth = out->out_depth;
-    if (C > 0 && !s->include_feature)
-        LSR_HIP(hipMemsetAsync(out->out_language_feature, 0, sizeof(float) * (size_t)C * W * H, st));
-    {
-        PhaseTimer t(LSR_PHASE_RENDER_FWD, st);
-        lsr::launch_render_fwd(r, st);
+    lsr_fwd_out* o[1] = {out};
+    return lsr_forward_composite_views(1, &s, in, o, &geom, &binning, &img, &num_rendered, stream);
+}
+
+int lsr_forward_composite_views(int32_t n_views, const lsr_settings* const* s, const lsr_fwd_in* in,
+                                lsr_fwd_out* const* out, const void* const* geom, const void* const* binning,
+                                void* const* img, const int64_t* num_rendered, lsr_stream_t stream) {
+    if (n_views < 1 || !s || !out || !geom || !binning || !img || !num_rendered)
+        return fail(LSR_EINVAL, "n_views >= 1 and the per-view arrays are required");
+    for (int v = 0; v < n_views; ++v) {   // every view validated before anything is launched
+        int rc = check_common(s[v], in);
+        if (rc) return rc;
+        if (!out[v] || !out[v]->out_color || !out[v]->out_depth) return fail(LSR_EINVAL, "color and depth outputs are required");
+        if (in->C > 0 && !out[v]->out_language_feature)
+            return fail(LSR_EINVAL, "language feature output is required when C > 0");
+        if (!geom[v] || !img[v] || (num_rendered[v] > 0 && !binning[v])) return fail(LSR_EINVAL, "workspaces are required");
+        if (s[v]->image_width != s[0]->image_width || s[v]->image_height != s[0]->image_height ||
+            (s[v]->include_feature != 0) != (s[0]->include_feature != 0))
+            return fail(LSR_EINVAL, "batched views must share the image size and include_feature");
     }
-    LSR_LAUNCHED("render forward", st, s->debug);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int P = in->P, W = s[0]->image_width, H = s[0]->image_height, C = in->C;
+    const int gx = (W + LSR_TILE_X - 1) / LSR_TILE_X, gy = (H + LSR_TILE_Y - 1) / LSR_TILE_Y;
+    for (int v0 = 0; v0 < n_views; v0 += lsr::LSR_MAX_VIEWS) {
+        const int nv = std::min(n_views - v0, lsr::LSR_MAX_VIEWS);
+        lsr::RenderFwdArgs r[lsr::LSR_MAX_VIEWS] = {};
+        for (int k = 0; k < nv; ++k) {
+            const int v = v0 + k;
+            const size_t K = (size_t)num_rendered[v];
+            Geom g = carve_geom(const_cast<void*>(geom[v]), (size_t)(P > 0 ? P : 1), nullptr);
+            Binning b = carve_binning(const_cast<void*>(binning[v]), K > 0 ? K : 1, nullptr);
+            Img m = carve_img(img[v], W, H, nullptr);   // tile_max was zeroed by the binning (atomicMax: idempotent)
+            lsr::RenderFwdArgs& a = r[k];
+            a.W = W; a.H = H; a.grid_x = gx; a.grid_y = gy; a.C = C; a.include_feature = s[v]->include_feature;
+            a.ranges = m.ranges; a.point_list = K > 0 ? (tile_sort_in_b(gx * gy) ? b.val_b : b.val_a) : nullptr;
+            a.xy = g.xy; a.conic_o = g.conic_o; a.rgbd = g.rgbd;
+            a.lang = in->language_feature;
+            a.lang_split = in->C == 32 ? in->language_feature_split : nullptr;
+            a.bg = s[v]->bg; a.final_T = m.final_T; a.n_contrib = m.n_contrib;
+            a.tile_max_contrib = m.tile_max; a.tile_order = m.tile_order;
+            a.out_color = out[v]->out_color; a.out_lang = out[v]->out_language_feature;
+            a.out_depth = out[v]->out_depth;
+            if (C > 0 && !s[v]->include_feature)
+                LSR_HIP(hipMemsetAsync(out[v]->out_language_feature, 0, sizeof(float) * (size_t)C * W * H, st));
+        }
+        {
+            PhaseTimer t(LSR_PHASE_RENDER_FWD, st);
+            lsr::launch_render_fwd_views(r, nv, st);
+        }
+        LSR_LAUNCHED("render forward", st, s[0]->debug);
+    }
     return LSR_OK;
 }
 
@@ -628,39 +651,67 @@ int lsr_backward(const lsr_settings* s, const lsr_fwd_in* in, const lsr_bwd_in* 
 int lsr_backward_composite(const lsr_settings* s, const lsr_fwd_in* in, const lsr_bwd_in* gin, float* dL_dlanguage,
                            void* geom, const void* binning, const void* img, int64_t num_rendered,
                            lsr_stream_t stream) {
-    int rc = check_common(s, in);
-    if (rc) return rc;
-    if (!gin || !gin->dL_dout_color) return fail(LSR_EINVAL, "dL_dout_color is required");
-    if (gin->deterministic)
-        return fail(LSR_EINVAL, "the split backward reduces with float atomics; use lsr_backward for deterministic "
-                                "gradients");
-    if (!geom || !img || (num_rendered > 0 && !binning)) return fail(LSR_EINVAL, "workspaces are required");
+    return lsr_backward_composite_views(1, &s, in, &gin, dL_dlanguage, &geom, &binning, &img, &num_rendered, stream);
+}
+
+int lsr_backward_composite_views(int32_t n_views, const lsr_settings* const* s, const lsr_fwd_in* in,
+                                 const lsr_bwd_in* const* gin, float* dL_dlanguage, void* const* geom,
+                                 const void* const* binning, const void* const* img, const int64_t* num_rendered,
+                                 lsr_stream_t stream) {
+    if (n_views < 1 || !s || !gin || !geom || !binning || !img || !num_rendered)
+        return fail(LSR_EINVAL, "n_views >= 1 and the per-view arrays are required");
+    for (int v = 0; v < n_views; ++v) {   // every view validated before anything is launched
+        int rc = check_common(s[v], in);
+        if (rc) return rc;
+        if (!gin[v] || !gin[v]->dL_dout_color) return fail(LSR_EINVAL, "dL_dout_color is required");
+        if (gin[v]->deterministic)
+            return fail(LSR_EINVAL, "the split backward reduces with float atomics; use lsr_backward for deterministic "
+                                    "gradients");
+        if (!geom[v] || !img[v] || (num_rendered[v] > 0 && !binning[v])) return fail(LSR_EINVAL, "workspaces are required");
+        if (s[v]->image_width != s[0]->image_width || s[v]->image_height != s[0]->image_height ||
+            (s[v]->include_feature != 0) != (s[0]->include_feature != 0))
+            return fail(LSR_EINVAL, "batched views must share the image size and include_feature");
+    }
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    const int P = in->P, C = in->C, W = s->image_width, H = s->image_height;
+    const int P = in->P, C = in->C, W = s[0]->image_width, H = s[0]->image_height;
     if (P == 0) return LSR_OK;
     const int gx = (W + LSR_TILE_X - 1) / LSR_TILE_X, gy = (H + LSR_TILE_Y - 1) / LSR_TILE_Y;
-    const size_t K = (size_t)num_rendered;
-    Geom g = carve_geom(geom, (size_t)P, nullptr);   // g.acc: rows of listed Gaussians zeroed by the preprocess
-    Binning b = carve_binning(const_cast<void*>(binning), K > 0 ? K : 1, nullptr);
-    Img m = carve_img(const_cast<void*>(img), W, H, nullptr);
-    const int recq = lsr::record_floats(s->include_feature ? C : 0);
-    if (K == 0) return LSR_OK;
-    lsr::RenderBwdArgs r{};
-    r.W = W; r.H = H; r.grid_x = gx; r.grid_y = gy; r.C = C; r.include_feature = s->include_feature;
-    r.ranges = m.ranges; r.point_list = tile_sort_in_b(gx * gy) ? b.val_b : b.val_a;
-    r.xy = g.xy; r.conic_o = g.conic_o; r.rgbd = g.rgbd;
-    r.rect = g.rect; r.inst_off = g.inst_off;
-    r.lang = in->language_feature;
-    r.lang_split = in->C == 32 ? in->language_feature_split : nullptr; r.bg = s->bg; r.final_T = m.final_T; r.n_contrib = m.n_contrib;
-    r.tile_max_contrib = m.tile_max; r.tile_order = m.tile_order;
-    r.dL_dcolor = gin->dL_dout_color; r.dL_dlang = gin->dL_dout_language_feature; r.dL_ddepth = gin->dL_dout_depth;
-    r.recq = recq; r.deterministic = 0;
-    r.acc_small = reinterpret_cast<float*>(g.acc); r.acc_lang = dL_dlanguage;
-    {
-        PhaseTimer t(LSR_PHASE_RENDER_BWD, st);
-        lsr::launch_render_bwd(r, st);
+    const int recq = lsr::record_floats(s[0]->include_feature ? C : 0);
+    lsr::RenderBwdArgs r[lsr::LSR_MAX_VIEWS] = {};
+    int nr = 0;
+    auto launch = [&]() {
+        if (nr == 0) return;
+        {
+            PhaseTimer t(LSR_PHASE_RENDER_BWD, st);
+            if (C <= 32) lsr::launch_render_bwd_wave_views(r, nr, st);
+            else
+                for (int k = 0; k < nr; ++k) lsr::launch_render_bwd(r[k], st);   // 64 channels: per-tile kernel
+        }
+        nr = 0;
+    };
+    for (int v = 0; v < n_views; ++v) {
+        const size_t K = (size_t)num_rendered[v];
+        if (K == 0) continue;   // nothing listed: no compositor work
+        Geom g = carve_geom(geom[v], (size_t)P, nullptr);   // g.acc: rows of listed Gaussians zeroed by the preprocess
+        Binning b = carve_binning(const_cast<void*>(binning[v]), K, nullptr);
+        Img m = carve_img(const_cast<void*>(img[v]), W, H, nullptr);
+        lsr::RenderBwdArgs& a = r[nr++];
+        a.W = W; a.H = H; a.grid_x = gx; a.grid_y = gy; a.C = C; a.include_feature = s[v]->include_feature;
+        a.ranges = m.ranges; a.point_list = tile_sort_in_b(gx * gy) ? b.val_b : b.val_a;
+        a.xy = g.xy; a.conic_o = g.conic_o; a.rgbd = g.rgbd;
+        a.rect = g.rect; a.inst_off = g.inst_off;
+        a.lang = in->language_feature;
+        a.lang_split = in->C == 32 ? in->language_feature_split : nullptr;
+        a.bg = s[v]->bg; a.final_T = m.final_T; a.n_contrib = m.n_contrib;
+        a.tile_max_contrib = m.tile_max; a.tile_order = m.tile_order;
+        a.dL_dcolor = gin[v]->dL_dout_color; a.dL_dlang = gin[v]->dL_dout_language_feature;
+        a.dL_ddepth = gin[v]->dL_dout_depth;
+        a.recq = recq; a.deterministic = 0;
+        a.acc_small = reinterpret_cast<float*>(g.acc); a.acc_lang = dL_dlanguage;
+        if (nr == lsr::LSR_MAX_VIEWS) launch();
     }
-    LSR_LAUNCHED("render backward", st, s->debug);
+    launch();
+    LSR_LAUNCHED("render backward", st, s[0]->debug);
     return LSR_OK;
 }
 
@@ -748,11 +799,9 @@ int lsr_backward_views(int32_t n_views, const lsr_settings* const* s, const lsr_
     if (P == 0) return LSR_OK;
     if (!accumulate && C > 0 && gout->dL_dlanguage_feature)
         LSR_HIP(hipMemsetAsync(gout->dL_dlanguage_feature, 0, sizeof(float) * (size_t)P * C, st));
-    for (int v = 0; v < n_views; ++v) {
-        int rc = lsr_backward_composite(s[v], in, gin[v], gout->dL_dlanguage_feature, geom[v], binning[v], img[v],
-                                        num_rendered[v], stream);
-        if (rc) return rc;
-    }
+    int rc = lsr_backward_composite_views(n_views, s, in, gin, gout->dL_dlanguage_feature, geom, binning, img,
+                                          num_rendered, stream);
+    if (rc) return rc;
     return lsr_backward_preprocess_views(n_views, s, in, gout, const_cast<const void* const*>(geom), accumulate,
                                          stream);
 }

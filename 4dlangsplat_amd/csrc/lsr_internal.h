@@ -216,6 +216,15 @@ struct RenderBwdArgs {
     float* acc_lang;          // [P,C] (the caller's dL/dlanguage buffer), may be null
 };
 
+// The compacted-wave compositors take up to LSR_MAX_VIEWS views of one image size per launch
+// (grid row = view; blocks dispatch row by row, so a view's tail waves overlap the next view's
+// first ones instead of draining the chip between launches).  A single view is a batch of one.
+struct RenderFwdBatch { RenderFwdArgs v[LSR_MAX_VIEWS]; };
+struct RenderBwdBatch { RenderBwdArgs v[LSR_MAX_VIEWS]; };
+void launch_render_fwd_views(const RenderFwdArgs* a, int n, hipStream_t st);
+// non-deterministic views with C <= 32 only (the wave backward); tile orders built in one launch
+void launch_render_bwd_wave_views(const RenderBwdArgs* a, int n, hipStream_t st);
+
 // record width for C language channels (multiple of 4 floats)
 inline int lang_pad(int C) { return C == 0 ? 0 : C <= 4 ? 4 : C <= 8 ? 8 : C <= 16 ? 16 : C <= 32 ? 32 : 64; }
 inline int record_floats(int C) { return 12 + lang_pad(C); }
@@ -411,12 +420,8 @@ void launch_tile_ranges(const RangesSeg* segs, int nseg, uint32_t ntiles, hipStr
 
 // compositing (render_fwd.hip / render_bwd.hip)
 void launch_render_fwd(const RenderFwdArgs& a, hipStream_t st);
-// Longest-first launch order of the tiles into order[]: by ranges' list lengths (forward) when
-// ranges is given, else by the forward's replay bounds tile_max (backward).  render_bwd_wave.hip.
-void launch_tile_order(int ntiles, const uint32_t* tile_max, const uint2* ranges, uint32_t* order, hipStream_t st);
 void launch_render_bwd(const RenderBwdArgs& a, hipStream_t st);
-void launch_render_fwd_wave(const RenderFwdArgs& a, hipStream_t st);
-void launch_render_fwd_wave_mfma(const RenderFwdArgs& a, hipStream_t st);   // 17..32 channels
-void launch_render_bwd_wave(const RenderBwdArgs& a, hipStream_t st);
+void launch_render_fwd_wave_views(const RenderFwdArgs* a, int n, hipStream_t st);
+void launch_render_fwd_wave_mfma_views(const RenderFwdArgs* a, int n, hipStream_t st);   // 17..32 channels
 
 }  // namespace lsr

@@ -220,7 +220,7 @@ static void go_bwd(const RenderBwdArgs& a, hipStream_t st) {
 void launch_render_bwd(const RenderBwdArgs& a, hipStream_t st) {
     const int C = a.include_feature ? a.C : 0;
     if (!a.deterministic && C <= 32) {
-        launch_render_bwd_wave(a, st);   // compacted per-quadrant waves, pixel sums on matrix cores
+        launch_render_bwd_wave_views(&a, 1, st);   // compacted per-quadrant waves, pixel sums on matrix cores
         return;
     }
     switch (lang_pad(C)) {               // deterministic records, or 64 channels

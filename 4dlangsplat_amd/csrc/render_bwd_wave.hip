@@ -63,7 +63,8 @@ constexpr int WFIFO = 128;   // compacted entries waiting (list positions and id
 template <bool C32, bool PRE, bool NOL>
 __global__ void __launch_bounds__(64)
 __attribute__((amdgpu_waves_per_eu(NOL ? LSR_BWD_WAVES_NOL : LSR_BWD_WAVES, NOL ? LSR_BWD_WAVES_NOL : LSR_BWD_WAVES)))
-k_render_bwd_wave(RenderBwdArgs a) {
+k_render_bwd_wave(RenderBwdBatch ab) {
+    const RenderBwdArgs& a = ab.v[blockIdx.y];   // grid row = view
     static_assert(!(NOL && C32), "NOL has no language channels");
     __shared__ __attribute__((aligned(16))) __bf16 s_FR[64 * WGB];       // G rows (build), then F / W / t rows
     // group entries' screen-space data, one array per field (a b128 read gives 4 entries, a b64
@@ -552,16 +553,22 @@ k_render_bwd_wave(RenderBwdArgs a) {
 // buckets the tiles by their replay bound (tile_max_contrib, written by the forward) in
 // descending order: a counting sort over 1024 buckets of 2 replay entries.  The order inside a
 // bucket is not fixed, which only permutes float atomic summation (this path is non-deterministic).
+// One block per view of a batch.
 constexpr int ORDER_BUCKETS = 1024;
-__global__ void __launch_bounds__(1024) k_tile_order(int ntiles, const uint32_t* __restrict__ tile_max,
-                                                     const uint2* __restrict__ ranges, uint32_t* __restrict__ order) {
+struct TileOrderBatch {
+    const uint32_t* tile_max[LSR_MAX_VIEWS];
+    uint32_t* order[LSR_MAX_VIEWS];
+};
+__global__ void __launch_bounds__(1024) k_tile_order(int ntiles, TileOrderBatch tb) {
     __shared__ uint32_t s_cnt[ORDER_BUCKETS];
     __shared__ uint32_t s_wave[16];
+    const uint32_t* __restrict__ tile_max = tb.tile_max[blockIdx.x];
+    uint32_t* __restrict__ order = tb.order[blockIdx.x];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     s_cnt[tid] = 0;
     __syncthreads();
     auto bucket = [&](int t) {
-        const uint32_t cost = ranges ? (ranges[t].y - ranges[t].x) >> 2 : tile_max[t] >> 1;
+        const uint32_t cost = tile_max[t] >> 1;
         return ORDER_BUCKETS - 1 - (int)min(cost, (uint32_t)ORDER_BUCKETS - 1);
     };
     for (int t = tid; t < ntiles; t += 1024) atomicAdd(&s_cnt[bucket(t)], 1u);
@@ -582,20 +589,31 @@ __global__ void __launch_bounds__(1024) k_tile_order(int ntiles, const uint32_t*
     for (int t = tid; t < ntiles; t += 1024) order[atomicAdd(&s_cnt[bucket(t)], 1u)] = (uint32_t)t;
 }
 
-void launch_tile_order(int ntiles, const uint32_t* tile_max, const uint2* ranges, uint32_t* order, hipStream_t st) {
-    hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, st, ntiles, tile_max, ranges, order);
-}
-
-void launch_render_bwd_wave(const RenderBwdArgs& a, hipStream_t st) {
-    const int ntiles = a.grid_x * a.grid_y;
-    if (a.tile_order) launch_tile_order(ntiles, a.tile_max_contrib, nullptr, a.tile_order, st);
-    const bool c32 = a.include_feature && a.C == 32;
-    const bool nol = !a.include_feature || a.C == 0;
-    const dim3 grid(((ntiles + 7) / 8) * 32);
-    if (c32 && a.lang_split) hipLaunchKernelGGL((k_render_bwd_wave<true, true, false>), grid, dim3(64), 0, st, a);
-    else if (c32) hipLaunchKernelGGL((k_render_bwd_wave<true, false, false>), grid, dim3(64), 0, st, a);
-    else if (nol) hipLaunchKernelGGL((k_render_bwd_wave<false, false, true>), grid, dim3(64), 0, st, a);
-    else hipLaunchKernelGGL((k_render_bwd_wave<false, false, false>), grid, dim3(64), 0, st, a);
+// n <= LSR_MAX_VIEWS views sharing the image size, C, include_feature and the language operands'
+// form; the tile orders of all of them in one launch, then one compositor launch
+void launch_render_bwd_wave_views(const RenderBwdArgs* a, int n, hipStream_t st) {
+    const int ntiles = a[0].grid_x * a[0].grid_y;
+    RenderBwdBatch ab{};
+    TileOrderBatch tb{};
+    bool order = false;
+    for (int v = 0; v < n; ++v) {
+        ab.v[v] = a[v];
+        tb.tile_max[v] = a[v].tile_max_contrib;
+        tb.order[v] = a[v].tile_order;
+        order = order || a[v].tile_order;
+    }
+    if (order) {
+        for (int v = 0; v < n; ++v)
+            if (!a[v].tile_order) { ab.v[v].tile_order = nullptr; tb.order[v] = nullptr; }
+        hipLaunchKernelGGL(k_tile_order, dim3(n), dim3(1024), 0, st, ntiles, tb);
+    }
+    const bool c32 = a[0].include_feature && a[0].C == 32;
+    const bool nol = !a[0].include_feature || a[0].C == 0;
+    const dim3 grid(((ntiles + 7) / 8) * 32, n);
+    if (c32 && a[0].lang_split) hipLaunchKernelGGL((k_render_bwd_wave<true, true, false>), grid, dim3(64), 0, st, ab);
+    else if (c32) hipLaunchKernelGGL((k_render_bwd_wave<true, false, false>), grid, dim3(64), 0, st, ab);
+    else if (nol) hipLaunchKernelGGL((k_render_bwd_wave<false, false, true>), grid, dim3(64), 0, st, ab);
+    else hipLaunchKernelGGL((k_render_bwd_wave<false, false, false>), grid, dim3(64), 0, st, ab);
 }
 
 }  // namespace lsr

@@ -11,10 +11,15 @@
 
 namespace lsr {
 
-void launch_render_fwd(const RenderFwdArgs& a, hipStream_t st) {
-    RenderFwdArgs f = a;
-    f.tile_order = nullptr;   // the forward takes no cost order: its scratch is not written
-    launch_render_fwd_wave(f, st);
+void launch_render_fwd(const RenderFwdArgs& a, hipStream_t st) { launch_render_fwd_views(&a, 1, st); }
+
+void launch_render_fwd_views(const RenderFwdArgs* a, int n, hipStream_t st) {
+    RenderFwdArgs f[LSR_MAX_VIEWS];
+    for (int v = 0; v < n; ++v) {
+        f[v] = a[v];
+        f[v].tile_order = nullptr;   // the forward takes no cost order: its scratch is not written
+    }
+    launch_render_fwd_wave_views(f, n, st);
 }
 
 }  // namespace lsr

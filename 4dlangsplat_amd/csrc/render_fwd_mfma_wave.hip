@@ -81,7 +81,8 @@ __device__ unsigned long long g_fwd_stamps[8];
 // was no faster (the waves then contend for issue); it was removed in round 3.
 template <bool PRE>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LSR_FWD_WAVES, LSR_FWD_WAVES)))
-k_render_fwd_wave_mfma(RenderFwdArgs a) {
+k_render_fwd_wave_mfma(RenderFwdBatch ab) {
+    const RenderFwdArgs& a = ab.v[blockIdx.y];   // grid row = view
     // group entries, one array per field (a b64 read of a pair = one packed-fp32 operand): centre
     // X, Y; staged conic -a/2, -b, -c/2 (gauss_power); opacity (0 past the group: never blends); (r, g) and (b, depth) pairs
     __shared__ __attribute__((aligned(16))) float s_X[MG], s_Y[MG], s_A[MG], s_B[MG], s_C[MG], s_O[MG];
@@ -368,12 +369,15 @@ void launch_language_split(int P, const float* lang, uint16_t* out, hipStream_t 
     if (P > 0) hipLaunchKernelGGL(k_language_split, dim3((unsigned)((4u * (uint32_t)P + 255u) / 256u)), dim3(256), 0, st, P, lang, out);
 }
 
-void launch_render_fwd_wave_mfma(const RenderFwdArgs& a, hipStream_t st) {
-    const int ntiles = a.grid_x * a.grid_y;
-    if (a.lang_split && a.C == 32)
-        hipLaunchKernelGGL((k_render_fwd_wave_mfma<true>), dim3(((ntiles + 7) / 8) * 32), dim3(64), 0, st, a);
+void launch_render_fwd_wave_mfma_views(const RenderFwdArgs* a, int n, hipStream_t st) {
+    RenderFwdBatch ab{};
+    for (int v = 0; v < n; ++v) ab.v[v] = a[v];
+    const int ntiles = a[0].grid_x * a[0].grid_y;
+    const dim3 grid(((ntiles + 7) / 8) * 32, n);
+    if (a[0].lang_split && a[0].C == 32)
+        hipLaunchKernelGGL((k_render_fwd_wave_mfma<true>), grid, dim3(64), 0, st, ab);
     else
-        hipLaunchKernelGGL((k_render_fwd_wave_mfma<false>), dim3(((ntiles + 7) / 8) * 32), dim3(64), 0, st, a);
+        hipLaunchKernelGGL((k_render_fwd_wave_mfma<false>), grid, dim3(64), 0, st, ab);
 }
 
 }  // namespace lsr

@@ -18,7 +18,8 @@
 namespace lsr {
 
 template <int CPAD>
-__global__ void __launch_bounds__(64) k_render_fwd_wave(RenderFwdArgs a) {
+__global__ void __launch_bounds__(64) k_render_fwd_wave(RenderFwdBatch ab) {
+    const RenderFwdArgs& a = ab.v[blockIdx.y];   // grid row = view
     constexpr int GF = 32, FIFO = 128, LP = CPAD > 0 ? CPAD : 1;
     __shared__ float4 s_co[GF];
     __shared__ float4 s_rgbd[GF];
@@ -191,20 +192,26 @@ __global__ void __launch_bounds__(64) k_render_fwd_wave(RenderFwdArgs a) {
 }
 
 template <int CPAD>
-static void go_fwd_wave(const RenderFwdArgs& a, hipStream_t st) {
-    const int ntiles = a.grid_x * a.grid_y;
-    hipLaunchKernelGGL(k_render_fwd_wave<CPAD>, dim3(((ntiles + 7) / 8) * 32), dim3(64), 0, st, a);
+static void go_fwd_wave(const RenderFwdBatch& ab, int n, hipStream_t st) {
+    const int ntiles = ab.v[0].grid_x * ab.v[0].grid_y;
+    hipLaunchKernelGGL(k_render_fwd_wave<CPAD>, dim3(((ntiles + 7) / 8) * 32, n), dim3(64), 0, st, ab);
 }
 
-void launch_render_fwd_wave(const RenderFwdArgs& a, hipStream_t st) {
-    const int C = a.include_feature ? a.C : 0;
+// n <= LSR_MAX_VIEWS views sharing the image size, C and include_feature
+void launch_render_fwd_wave_views(const RenderFwdArgs* a, int n, hipStream_t st) {
+    const int C = a[0].include_feature ? a[0].C : 0;
+    if (lang_pad(C) == 32) {   // channel sums on matrix cores
+        launch_render_fwd_wave_mfma_views(a, n, st);
+        return;
+    }
+    RenderFwdBatch ab{};
+    for (int v = 0; v < n; ++v) ab.v[v] = a[v];
     switch (lang_pad(C)) {
-        case 0: go_fwd_wave<0>(a, st); break;
-        case 4: go_fwd_wave<4>(a, st); break;
-        case 8: go_fwd_wave<8>(a, st); break;
-        case 16: go_fwd_wave<16>(a, st); break;
-        case 32: launch_render_fwd_wave_mfma(a, st); break;   // channel sums on matrix cores
-        default: go_fwd_wave<64>(a, st); break;
+        case 0: go_fwd_wave<0>(ab, n, st); break;
+        case 4: go_fwd_wave<4>(ab, n, st); break;
+        case 8: go_fwd_wave<8>(ab, n, st); break;
+        case 16: go_fwd_wave<16>(ab, n, st); break;
+        default: go_fwd_wave<64>(ab, n, st); break;
     }
 }
 

@@ -424,6 +424,59 @@ def render_native(pending: PendingForward):
     return color, lang_out, pending.radii, depth, state
 
 
+def render_views_native(pendings):
+    """render_native for several views of the same Gaussians and image size, their compositing as
+    ONE launch per 8 views (lsr_forward_composite_views: a view's last waves run beside the next
+    view's first ones).  Views not binned yet are binned first, as one batch.  Same results as
+    render_native per view.  Returns a list of (color, language_feature, radii, depth, state)."""
+    if not pendings:
+        return []
+    L = _lib.load()
+    unbinned = [pf for pf in pendings if pf.binning is None]
+    if unbinned:
+        binning_views_native(unbinned, stream=torch.cuda.current_stream(unbinned[0].device))
+    device = pendings[0].device
+    stream = torch.cuda.current_stream(device)
+    waited = set()
+    outs, fouts = [], []
+    for pf in pendings:
+        if pf.device != device or (pf.H, pf.W) != (pendings[0].H, pendings[0].W):
+            raise ValueError("render_views_native: the views must share the device and image size")
+        if pf.ready_stream is not None and pf.ready_stream != stream and id(pf.ready) not in waited:
+            stream.wait_event(pf.ready)   # one wait per binning batch (a wait idles the device)
+            waited.add(id(pf.ready))
+        for t in (pf.geom, pf.radii, pf.binning, pf.img):
+            t.record_stream(stream)
+        H, W, C = pf.H, pf.W, pf.fin.C
+        color = torch.empty(3, H, W, dtype=torch.float32, device=device)
+        lang_out = torch.empty(C, H, W, dtype=torch.float32, device=device)
+        depth = torch.empty(1, H, W, dtype=torch.float32, device=device)
+        fout = _lib.FwdOut()
+        fout.out_color, fout.out_language_feature = color.data_ptr(), _ptr(lang_out) if C > 0 else None
+        fout.radii, fout.out_depth = pf.radii.data_ptr(), depth.data_ptr()
+        outs.append((color, lang_out, depth))
+        fouts.append(fout)
+    n = len(pendings)
+    s_arr = (ctypes.POINTER(_lib.Settings) * n)(*[ctypes.pointer(pf.settings.c) for pf in pendings])
+    o_arr = (ctypes.POINTER(_lib.FwdOut) * n)(*[ctypes.pointer(f) for f in fouts])
+    vp = ctypes.c_void_p * n
+    try:
+        _lib.check(L.lsr_forward_composite_views(n, s_arr, ctypes.byref(pendings[0].fin), o_arr,
+                                                 vp(*[pf.geom.data_ptr() for pf in pendings]),
+                                                 vp(*[pf.binning.data_ptr() for pf in pendings]),
+                                                 vp(*[pf.img.data_ptr() for pf in pendings]),
+                                                 (ctypes.c_int64 * n)(*[pf.num_rendered for pf in pendings]),
+                                                 _stream(device)), "lsr_forward_composite_views")
+    except RuntimeError:
+        _dump_forward(pendings[0].raster_settings, pendings[0].inputs)
+        raise
+    res = []
+    for pf, (color, lang_out, depth) in zip(pendings, outs):
+        state = RasterizerState(pf.settings, pf.inputs, pf.fin, pf.geom, pf.binning, pf.img, pf.num_rendered, pf.radii)
+        res.append((color, lang_out, pf.radii, depth, state))
+    return res
+
+
 def forward_native(raster_settings, means3D, opacities, shs=None, colors_precomp=None, language_feature=None,
                    scales=None, rotations=None, cov3D_precomp=None):
     """Forward through liblsr.so on the current stream.  Returns (color, language_feature, radii,
@@ -608,6 +661,56 @@ def backward_composite_native(state: RasterizerState, grad_color, grad_lang=None
                                         ctypes.c_int64(state.num_rendered), _stream(device)), "lsr_backward_composite")
     state.composited = True
     return CompositeGrad(state, (gc, gl, gd))
+
+
+def backward_composite_views_native(states, grad_colors, grad_langs=None, grad_depths=None,
+                                    dL_dlanguage=None):
+    """backward_composite_native for several views of the same Gaussians and image size, their
+    compositor backward as ONE launch per 8 views (lsr_backward_composite_views; one launch for
+    their tile orders too).  grad_* are per-view lists (entries may be None).  Returns a list of
+    CompositeGrad for backward_preprocess_views_native."""
+    if not states:
+        return []
+    L = _lib.load()
+    for s in states:
+        if s.composited:
+            raise RuntimeError("backward_composite_native already ran on this forward: its screen-space sums are "
+                               "accumulated in the forward's workspace, so a second run would double them")
+    st0 = states[0]
+    device = st0.inputs["means3D"].device
+    P, C = st0.fin.P, st0.fin.C
+    n = len(states)
+    grad_langs = grad_langs or [None] * n
+    grad_depths = grad_depths or [None] * n
+    if dL_dlanguage is not None and (dL_dlanguage.shape != (P, C) or not dL_dlanguage.is_contiguous()):
+        raise ValueError("dL_dlanguage must be a contiguous [P, C] tensor")
+    gins, keeps = [], []
+    for v, s in enumerate(states):
+        if s.inputs["means3D"].data_ptr() != st0.inputs["means3D"].data_ptr():
+            raise ValueError("all views must render the same Gaussians")
+        H, W = s.settings.c.image_height, s.settings.c.image_width
+        gc = grad_colors[v].detach().to(torch.float32).contiguous() if grad_colors[v] is not None else \
+            torch.zeros(3, H, W, dtype=torch.float32, device=device)
+        gl = grad_langs[v].detach().to(torch.float32).contiguous() if (grad_langs[v] is not None and C > 0) else None
+        gd = grad_depths[v].detach().to(torch.float32).contiguous() if grad_depths[v] is not None else None
+        gi = _lib.BwdIn()
+        gi.dL_dout_color, gi.dL_dout_language_feature, gi.dL_dout_depth = gc.data_ptr(), _ptr(gl), _ptr(gd)
+        gi.deterministic = 0
+        gins.append(gi)
+        keeps.append((gc, gl, gd))
+    s_arr = (ctypes.POINTER(_lib.Settings) * n)(*[ctypes.pointer(s.settings.c) for s in states])
+    g_arr = (ctypes.POINTER(_lib.BwdIn) * n)(*[ctypes.pointer(gi) for gi in gins])
+    vp = ctypes.c_void_p * n
+    _lib.check(L.lsr_backward_composite_views(n, s_arr, ctypes.byref(st0.fin), g_arr,
+                                              _ptr(dL_dlanguage if C > 0 else None),
+                                              vp(*[s.geom.data_ptr() for s in states]),
+                                              vp(*[s.binning.data_ptr() for s in states]),
+                                              vp(*[s.img.data_ptr() for s in states]),
+                                              (ctypes.c_int64 * n)(*[s.num_rendered for s in states]),
+                                              _stream(device)), "lsr_backward_composite_views")
+    for s in states:
+        s.composited = True
+    return [CompositeGrad(s, k) for s, k in zip(states, keeps)]
 
 
 def backward_preprocess_views_native(parts, out=None, accumulate=False, need=None, row_chunks=None, on_rows=None):

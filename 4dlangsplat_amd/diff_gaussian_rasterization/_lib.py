@@ -132,6 +132,16 @@ SIGNATURES = {
     "lsr_forward_composite": (ctypes.c_int, [ctypes.POINTER(Settings), ctypes.POINTER(FwdIn), ctypes.POINTER(FwdOut),
                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                              ctypes.c_void_p]),
+    "lsr_forward_composite_views": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(ctypes.POINTER(Settings)),
+                                                   ctypes.POINTER(FwdIn), ctypes.POINTER(ctypes.POINTER(FwdOut)),
+                                                   ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
+                                                   ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int64),
+                                                   ctypes.c_void_p]),
+    "lsr_backward_composite_views": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(ctypes.POINTER(Settings)),
+                                                    ctypes.POINTER(FwdIn), ctypes.POINTER(ctypes.POINTER(BwdIn)),
+                                                    ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
+                                                    ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
+                                                    ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
     "lsr_backward": (ctypes.c_int, [ctypes.POINTER(Settings), ctypes.POINTER(FwdIn), ctypes.POINTER(BwdIn),
                                     ctypes.POINTER(BwdOut), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p]),

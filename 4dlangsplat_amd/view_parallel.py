@@ -135,6 +135,8 @@ class ViewParallelStep:
 
     run(render_view) calls render_view(v, bucket) for every view v this rank owns; the callback
     adds view v's gradients into bucket.views (and returns view v's int32 radii [P], or None).
+    A callback with a `render_batch(views, bucket)` attribute is called once with all of them
+    instead (and returns their radii).
     Afterwards the bucket holds the SUM over ALL views of the batch on every rank, and
     bucket.radii the MAX over all views (when densify_stats)."""
 
@@ -158,11 +160,17 @@ class ViewParallelStep:
             b.zero_accumulated_()        # the flush writes every other field (HBM write saved)
         else:
             b.zero_()
-        radii_views = []
-        for v in self.views:
-            radii = render_view(v, b)
-            if b.radii is not None and radii is not None:
-                radii_views.append(radii)
+        batch = getattr(render_view, "render_batch", None)
+        if batch is not None:             # every view of the rank at once (batched compositor launches)
+            radii_views = [r for r in batch(self.views, b) if r is not None]
+            if b.radii is None:
+                radii_views = []
+        else:
+            radii_views = []
+            for v in self.views:
+                radii = render_view(v, b)
+                if b.radii is not None and radii is not None:
+                    radii_views.append(radii)
         # radii MAX over the views (train.py:270) after the views' launches, not between them
         for radii in radii_views:
             torch.maximum(b.radii, radii.to(torch.int32), out=b.radii)
@@ -214,7 +222,7 @@ class ViewParallelStep:
 
 
 def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool = False, overlap: bool = True,
-                         batch_backward: bool = True, early_views: int = 3):
+                         batch_backward: bool = True, early_views: int = 3, composite_batch: bool = True):
     """render_view callback for ViewParallelStep on the HIP rasterizer (the product path).
 
     scene    : object with means3D, opacities, shs, lang, scales, rotations device tensors
@@ -244,7 +252,9 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
     With more than `early_views` views in the batch, only the first `early_views` are binned on
     the current stream; the others' binning (emission, tile sort, tile ranges: chains of short,
     dependent launches that leave most of the GPU idle) runs on a side stream while those first
-    views composite, and each later view's compositing waits for it (an event).
+    views composite, and each later view's compositing waits for it (an event).  With
+    composite_batch (batched only) the step runs through render_batch: one compositor forward and
+    one compositor backward launch per binning batch instead of per view.
 
     overlap="lookahead" keeps ONE stream: view v+1's preprocess is enqueued ahead of view v's
     compositing with its instance count copied to pinned memory (lsr_forward_preprocess_async);
@@ -324,6 +334,41 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
             pending[v + 1] = preprocess(v + 1, stream=side)
         return radii
 
+    def render_batch(views, bucket: GradBucket):
+        """Every view of the step at once (ViewParallelStep.run prefers this to per-view calls):
+        forward phase 1 and binning as one batch, then per binning batch (the early views binned
+        on this stream, the rest on the side stream) ONE compositor forward launch for its views,
+        their upstream gradients (grad_fn, as train.py computes the loss on the stacked renders
+        before backward), and ONE compositor backward launch.  Two launches per group instead of
+        two per view: the chip no longer drains at every view's last waves.  Returns the radii."""
+        views = list(views)
+        if not views:
+            return []
+        if views[0] not in pending:
+            batch_preprocess(views[0])
+        pfs = [pending.pop(v) for v in views]
+        groups = []                        # consecutive views binned by one launch set (one event)
+        for v, pf in zip(views, pfs):
+            if groups and groups[-1][0][1].ready is pf.ready:
+                groups[-1].append((v, pf))
+            else:
+                groups.append([(v, pf)])
+        radii, ks = [], []
+        for grp in groups:
+            res = dgr.render_views_native([pf for _, pf in grp])
+            gcs, gls, gds = [], [], []
+            for (v, _), (color, lang, r, depth, st) in zip(grp, res):
+                gc, gl, gd = grad_fn(v, color, lang, depth)
+                gcs.append(gc)
+                gls.append(gl)
+                gds.append(gd)
+                radii.append(r)
+                ks.append(st.num_rendered)
+            held.extend(dgr.backward_composite_views_native([x[4] for x in res], gcs, gls, gds,
+                                                            dL_dlanguage=bucket.views["language_feature"]))
+        render_batch.last_num_rendered = ks
+        return radii
+
     def flush(bucket: GradBucket, row_chunks=None, on_rows=None):
         # overwrites every field but the language gradients (all P rows, culled ones with zeros), so
         # ViewParallelStep zeroes only the accumulated fields before the views
@@ -356,4 +401,7 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
     render_view.last_num_rendered = 0
     if batched:
         render_view.flush = flush
+        if batch_fwd and composite_batch:
+            render_batch.last_num_rendered = []
+            render_view.render_batch = render_batch
     return render_view

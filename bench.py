@@ -141,6 +141,8 @@ def parse_args(argv=None):
                     help="batched pipeline: views binned before compositing starts; the rest bin on a side stream "
                          "while they composite (0: all binned first)")
     ap.add_argument("--no-overlap", action="store_true", help="diagnostic: no side stream (uncontended phase times)")
+    ap.add_argument("--per-view-composite", action="store_true",
+                    help="one compositor launch per view instead of one per binning batch of views")
     ap.add_argument("--pipeline", choices=("batched", "lookahead", "side"), default=None,
                     help="view pipelining: the step's forward phase 1 + binning of all views as one batch (batched, "
                          "default), next view's preprocess queued ahead on one stream with a deferred count "
@@ -204,7 +206,7 @@ def run(args):
     render = native_view_renderer(scene, settings, lambda v, color, lang, depth: (gcol, glang, None),
                                   overlap=False if args.no_overlap else (True if args.pipeline == "side"
                                                                          else args.pipeline),
-                                  early_views=args.early_views)
+                                  early_views=args.early_views, composite_batch=not args.per_view_composite)
     Ks = []
 
     def render_view(v, b):
@@ -212,6 +214,13 @@ def run(args):
         Ks.append(render.last_num_rendered)
         return r
 
+    if hasattr(render, "render_batch"):                    # one compositor launch per binning batch
+
+        def render_batch(views, b):
+            r = render.render_batch(views, b)
+            Ks.extend(render.render_batch.last_num_rendered)
+            return r
+        render_view.render_batch = render_batch
     if hasattr(render, "flush"):                           # batched backward of the step's views
         render_view.flush = render.flush
     render_view.begin_step, render_view.end_step = render.begin_step, render.end_step   # the step's views
@@ -249,8 +258,13 @@ def run(args):
     elapsed = time.perf_counter() - t0
     prof = _lib.profile_read() if not args.no_profile else {}
     _lib.profile_enable(False)
-    if dom == "render_bwd" and prof["render_bwd"][1] != V * args.steps:   # every view's backward ran, timed
-        raise RuntimeError(f"expected {V * args.steps} backward launches, profiled {prof['render_bwd'][1]}")
+    # every view's backward ran, timed (a batched launch serves a binning batch of views)
+    if hasattr(render, "render_batch"):
+        want = 2 if 0 < args.early_views < V else 1
+    else:
+        want = V
+    if dom == "render_bwd" and prof["render_bwd"][1] != want * args.steps:
+        raise RuntimeError(f"expected {want * args.steps} backward launches, profiled {prof['render_bwd'][1]}")
     el = torch.tensor([elapsed], device=dev, dtype=torch.float64)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -306,6 +320,8 @@ def run(args):
                                      / (per * 1e-3) / 1e9)
             ms, n = prof[dom]                      # live, over the timed region
             byts = phase_bytes(dom, P, Pvis, Kmean, W * H, ntiles, C, M, **pb)
+            if dom.startswith("render"):           # per view; a batched launch composites several views
+                byts *= V * args.steps / n
             ach = byts / (ms / n * 1e-3) / 1e9
             pmc_rec = {}
             pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")

@@ -175,6 +175,14 @@ int lsr_forward_composite(const lsr_settings *s, const lsr_fwd_in *in, lsr_fwd_o
 int lsr_forward_binning_views(int32_t n_views, const lsr_settings *const *s, const lsr_fwd_in *in,
                               void *const *geom, void *const *binning, void *const *img,
                               const int64_t *num_rendered, lsr_stream_t stream);
+/* lsr_forward_composite of n_views >= 1 binned views of the same Gaussians in ONE compositor
+ * launch per 8 views (grid row = view: a view's last waves run beside the next view's first ones
+ * instead of the chip draining between per-view launches).  out[v], geom[v], binning[v], img[v],
+ * num_rendered[v] are view v's; the views must share the image size and include_feature.  Results
+ * equal lsr_forward_composite per view.  HOST pointer arrays. */
+int lsr_forward_composite_views(int32_t n_views, const lsr_settings *const *s, const lsr_fwd_in *in,
+                                lsr_fwd_out *const *out, const void *const *geom, const void *const *binning,
+                                void *const *img, const int64_t *num_rendered, lsr_stream_t stream);
 
 /* Backward through compositing and preprocess.  accumulate != 0 adds into the outputs instead of
  * overwriting them (multi-view gradient accumulation).  `scratch` holds >= lsr_backward_bytes. */
@@ -212,6 +220,13 @@ int lsr_backward_views(int32_t n_views, const lsr_settings *const *s, const lsr_
 int lsr_backward_composite(const lsr_settings *s, const lsr_fwd_in *in, const lsr_bwd_in *gin, float *dL_dlanguage,
                            void *geom, const void *binning, const void *img, int64_t num_rendered,
                            lsr_stream_t stream);
+/* lsr_backward_composite of n_views >= 1 views in one compositor launch per 8 views (and one
+ * launch for their tile orders); same image size and include_feature; the same once-per-forward
+ * rule per view.  Equals lsr_backward_composite per view up to the order of float atomics. */
+int lsr_backward_composite_views(int32_t n_views, const lsr_settings *const *s, const lsr_fwd_in *in,
+                                 const lsr_bwd_in *const *gin, float *dL_dlanguage, void *const *geom,
+                                 const void *const *binning, const void *const *img,
+                                 const int64_t *num_rendered, lsr_stream_t stream);
 int lsr_backward_preprocess_views(int32_t n_views, const lsr_settings *const *s, const lsr_fwd_in *in,
                                   lsr_bwd_out *gout, const void *const *geom, int32_t accumulate,
                                   lsr_stream_t stream);

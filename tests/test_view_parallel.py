@@ -169,6 +169,7 @@ def test_two_rank_step_equals_serial_batch(densify, batched, chunked):
 class _FakePending:
     def __init__(self, v, log):
         self.v, self.log, self.num_rendered = v, log, 0
+        self.ready = None                        # one binning batch
 
     def resolve(self, binning=False):
         self.log.append(("resolve", self.v))
@@ -218,6 +219,14 @@ def _lookahead_worker(rank, world, port, outdir, mode="lookahead"):
             for r0, r1 in (row_chunks or []):
                 on_rows(r0, r1)
 
+        def render_views_native(pfs):
+            return [render_native(pf) for pf in pfs]
+
+        def backward_composite_views_native(sts, gcs, gls, gds, dL_dlanguage=None):
+            return [backward_composite_native(st, gc, gl, gd) for st, gc, gl, gd in zip(sts, gcs, gls, gds)]
+
+        dgr.render_views_native, dgr.backward_composite_views_native = render_views_native, \
+            backward_composite_views_native
         dgr.preprocess_native, dgr.render_native = preprocess_native, render_native
         dgr.backward_composite_native = backward_composite_native
         dgr.backward_preprocess_views_native = backward_preprocess_views_native

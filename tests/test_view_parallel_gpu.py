@@ -133,3 +133,68 @@ def test_batched_side_binning_agrees(early):
     assert not torch.isnan(f1).any() and torch.equal(r0, r1)
     scale = float(f0.abs().max())
     assert scale > 0 and float((f0 - f1).abs().max()) <= 1e-5 * scale
+
+
+def _away_settings(W=160, H=120):
+    """A camera turned 180 degrees about y: every Gaussian of _setup's scene is behind it (K = 0)."""
+    import math
+    import numpy as np
+    fx = 2 * math.atan(0.6)
+    fy = 2 * math.atan(0.6 * H / W)
+    c = synthetic.make_camera(np.diag([-1.0, 1.0, -1.0]), np.zeros(3), fx, fy, W, H)
+    return dgr.GaussianRasterizationSettings(H, W, c.tanfovx, c.tanfovy, torch.ones(3, device="cuda"), 1.0,
+                                             c.world_view_transform.cuda(), c.full_proj_transform.cuda(), 3,
+                                             c.camera_center.cuda(), False, False, True)
+
+
+@pytest.mark.parametrize("split", [True, False])
+def test_composite_views_equals_per_view(split):
+    """lsr_forward_composite_views / lsr_backward_composite_views (one launch for a batch of views,
+    one of them with nothing listed) against the per-view launches on the same binned views:
+    images, depth and radii bit for bit, the compositor backward's sums within float-atomic
+    reordering (language gradients and, through the batched preprocess backward, every other
+    gradient)."""
+    sc, settings, grads = _setup(n_views=4)
+    settings = settings[:2] + [_away_settings()] + settings[2:]
+    grads = grads[:2] + [grads[0]] + grads[2:]
+    args = dict(shs=sc.shs, language_feature=sc.lang, scales=sc.scales, rotations=sc.rotations)
+    outs, gls, bwd = [], [], []
+    for batched in (False, True):
+        pfs = dgr.preprocess_views_native(settings, sc.means3D, sc.opacities, split_language=split, **args)
+        dgr.binning_views_native(pfs)
+        res = dgr.render_views_native(pfs) if batched else [dgr.render_native(pf) for pf in pfs]
+        gl = torch.zeros_like(sc.lang)
+        sts = [r[4] for r in res]
+        if batched:
+            parts = dgr.backward_composite_views_native(sts, [g[0] for g in grads], [g[1] for g in grads],
+                                                        dL_dlanguage=gl)
+        else:
+            parts = [dgr.backward_composite_native(st, g[0], g[1], None, dL_dlanguage=gl) for st, g in zip(sts, grads)]
+        b = GradBucket(sc.means3D.shape[0], sc.shs.shape[1], sc.lang.shape[1], "cuda", densify_stats=True)
+        dgr.backward_preprocess_views_native(parts, out=b.views, accumulate=False, need=b.need())
+        torch.cuda.synchronize()
+        outs.append([(c.clone(), l.clone(), r.clone(), d.clone(), st.num_rendered) for c, l, r, d, st in res])
+        gls.append(gl)
+        bwd.append(b.flat.clone())
+    assert outs[0][2][4] == 0 and all(o[4] > 0 for i, o in enumerate(outs[0]) if i != 2)
+    for a, c in zip(outs[0], outs[1]):
+        assert a[4] == c[4]
+        for x, y in zip(a[:4], c[:4]):
+            assert torch.equal(x, y)
+    for x, y in ((gls[0], gls[1]), (bwd[0], bwd[1])):
+        scale = float(x.abs().max())
+        assert scale > 0 and float((x - y).abs().max()) <= 1e-5 * scale
+
+
+@pytest.mark.parametrize("early", [0, 3])
+def test_batched_composite_step_agrees(early):
+    """ViewParallelStep through render_batch (the bench default: one compositor launch per binning
+    batch) against the per-view compositor launches of the same batched pipeline."""
+    sc, settings, grads = _setup(n_views=5)
+    f0, r0 = _run(sc, settings, grads, overlap="batched", deterministic=False, early_views=early,
+                  composite_batch=False)
+    f1, r1 = _run(sc, settings, grads, overlap="batched", deterministic=False, prefill=float("nan"),
+                  early_views=early)
+    assert not torch.isnan(f1).any() and torch.equal(r0, r1)
+    scale = float(f0.abs().max())
+    assert scale > 0 and float((f0 - f1).abs().max()) <= 1e-5 * scale
