@@ -44,9 +44,14 @@ __device__ unsigned long long g_bwd_stamps[12];
 #endif
 
 constexpr int WG = 16;       // compacted entries per MFMA group
-constexpr int WFP = 40;      // F row pitch in bf16 (32 channels + 8): 80-byte rows, 16-byte aligned
+constexpr int WFP = 48;      // F row pitch in bf16 (32 channels + 16): the MFMA1 b128 reads conflict-free
 constexpr int WGB = 48;      // G row pitch in bf16 at the one-off build: 32 language + 16 pad
-constexpr int WWP = 20;      // W / t row pitch in bf16 (16 entries + 4): 40-byte rows, 8-byte aligned
+// W / t rows [p][e]: 16 bf16 (32 B) per pixel p, unpadded and swizzled so that both the row
+// writes (ds_write_b64: 16-lane groups over 32 banks) and the transposing MFMA-operand reads
+// (ds_read_b64_tr_b16: 32-lane halves over 64 banks) are conflict-free: pixel p's row sits in row
+// slot p ^ 4 [(p >> 3) & 1] and its 8-byte chunk q (entries 4q .. 4q + 3) in chunk q ^ ((p >> 2) & 3).
+// (The padded 40-byte rows cost 2 extra LDS cycles per transposing read.)
+__device__ __forceinline__ int wt_off(int p, int q) { return (p ^ (((p >> 3) & 1) << 2)) * 16 + 4 * (q ^ ((p >> 2) & 3)); }
 constexpr int WFIFO = 128;   // compacted entries waiting (list positions and ids); power of two
 
 // C32: the 32-channel instantiation (headline), whose language rows are two float4 loads per lane
@@ -74,10 +79,10 @@ k_render_bwd_wave(RenderBwdBatch ab) {
     __shared__ __attribute__((aligned(16))) float s_R[WG], s_Gc[WG], s_Bc[WG], s_D[WG];
     __shared__ uint32_t s_gid[WG];
     __shared__ __attribute__((aligned(16))) uint32_t s_k[WG];
-    __shared__ float s_mom[WG][8];
+    __shared__ float s_mom[WG][10];   // pitch 10: the moment stores and loads conflict-free
     // results of the previous group, staged for its atomics (issued one iteration late, see 6.)
-    __shared__ float s_q[WG][16];   // per-entry scalar gradients in acc_small record order (0..9)
-    __shared__ float s_lq[WG][33];  // dL/dlanguage rows [e][c] (pitch 33: conflict-free stores)
+    __shared__ float s_q[WG][17];   // per-entry scalar gradients in acc_small record order (0..9); pitch 17 (banks)
+    __shared__ float s_lq[WG][36];  // dL/dlanguage rows [e][c] (pitch 36: conflict-free stores and loads)
     __shared__ uint32_t s_agid[WG];
     __shared__ uint32_t s_fk[WFIFO];
     __shared__ uint32_t s_fg[WFIFO];
@@ -184,7 +189,7 @@ k_render_bwd_wave(RenderBwdBatch ab) {
     __bf16* s_Fh = s_FR;              // F rows [e][c] of the group (MFMA1 A), hi
     __bf16* s_Fl = s_FR + WG * WFP;   // lo
     __bf16* s_Rh = s_FR;              // after MFMA1: W or t rows [p][e], hi
-    __bf16* s_Rl = s_FR + 64 * WWP;   // lo
+    __bf16* s_Rl = s_FR + 64 * 16;    // lo
 
     const float bg_dot = a.bg[0] * g0 + a.bg[1] * g1 + a.bg[2] * g2;
     const float ddelx_dx = 0.5f * (float)a.W, ddely_dy = 0.5f * (float)a.H;
@@ -448,15 +453,15 @@ k_render_bwd_wave(RenderBwdBatch ab) {
                     split_bf16(r[4 * q + j], h, l);
                     h4[j] = h; l4[j] = l;
                 }
-                *reinterpret_cast<bf16x4*>(s_Rh + lane * WWP + 4 * q) = h4;
-                *reinterpret_cast<bf16x4*>(s_Rl + lane * WWP + 4 * q) = l4;
+                *reinterpret_cast<bf16x4*>(s_Rh + wt_off(lane, q)) = h4;
+                *reinterpret_cast<bf16x4*>(s_Rl + wt_off(lane, q)) = l4;
             }
             wave_lds_sync();
         };
         auto read_a = [&](int kb, bf16x8& ah, bf16x8& al) {
-            const int row = 32 * kb + 8 * g4 + (l16 >> 2), col = 4 * (l16 & 3);
-            const bf16x4 h0 = ds_read_tr16(s_Rh + row * WWP + col), h1 = ds_read_tr16(s_Rh + (row + 4) * WWP + col);
-            const bf16x4 l0 = ds_read_tr16(s_Rl + row * WWP + col), l1 = ds_read_tr16(s_Rl + (row + 4) * WWP + col);
+            const int row = 32 * kb + 8 * g4 + (l16 >> 2), o0 = wt_off(row, l16 & 3), o1 = wt_off(row + 4, l16 & 3);
+            const bf16x4 h0 = ds_read_tr16(s_Rh + o0), h1 = ds_read_tr16(s_Rh + o1);
+            const bf16x4 l0 = ds_read_tr16(s_Rl + o0), l1 = ds_read_tr16(s_Rl + o1);
             ah = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
             al = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
         };
