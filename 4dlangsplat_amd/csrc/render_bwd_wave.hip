@@ -192,6 +192,7 @@ k_render_bwd_wave(RenderBwdBatch ab) {
     __bf16* s_Rl = s_FR + 64 * 16;    // lo
 
     const float bg_dot = a.bg[0] * g0 + a.bg[1] * g1 + a.bg[2] * g2;
+    const float bg_term = -T_final * bg_dot;   // the background term's per-pixel factor
     const float ddelx_dx = 0.5f * (float)a.W, ddely_dy = 0.5f * (float)a.H;
     float acc_dot = 0.0f, last_dot = 0.0f, last_alpha = 0.0f;
     const float pxf = (float)px, pyf = (float)py;
@@ -389,8 +390,11 @@ k_render_bwd_wave(RenderBwdBatch ab) {
         // ---- 4. serial back-to-front replay of the group: w = alpha T, t = G dL/dalpha --------
         // Per entry, everything but the T / accumulator recurrence is independent of the other
         // entries: computed branch-free for the whole group first (exp chains overlap), then the
-        // recurrence runs with selects (an inactive entry leaves T and the accumulators unchanged
-        // and gets w = t = 0, as in upstream's skip).
+        // recurrence.  An inactive entry (upstream skips it) runs the recurrence with alpha = 0,
+        // which leaves every state exactly as the skip does: T * rcp(1 - 0) = T * 1 = T; w = 0 T
+        // = 0; its fold fma(last_alpha, last_dot - acc, acc) is the one the next active entry
+        // would have made (same operands), and the next entry's fold, fma(0, x, acc) = acc, adds
+        // nothing.  Only alpha and t are selected; no selects on T, acc, last_dot, last_alpha or w.
         float wv[WG], tv[WG];
         constexpr int RB = 2;   // entries per branch-free batch: one packed-fp32 pair (register budget)
         const lsr_f2 px2 = {pxf, pxf}, py2 = {pyf, pyf};
@@ -415,28 +419,27 @@ k_render_bwd_wave(RenderBwdBatch ab) {
             for (int u = 0; u < 2; ++u) {
                 const int e = e0 + u;
                 const float power = u ? pw.y : pw.x;
+                const float al = fminf(0.99f, u ? og.y : og.x);
+                act[u] = (u ? kk.y : kk.x) < last_contributor && power <= 0.0f && al >= 1.0f / 255.0f;
+                alv[u] = act[u] ? al : 0.0f;
                 Gv[u] = u ? ge.y : ge.x;
-                alv[u] = fminf(0.99f, u ? og.y : og.x);
-                act[u] = (u ? kk.y : kk.x) < last_contributor && power <= 0.0f && alv[u] >= 1.0f / 255.0f;
-                romv[u] = __builtin_amdgcn_rcpf(1.0f - alv[u]);
+                romv[u] = __builtin_amdgcn_rcpf(1.0f - alv[u]);   // rcp(1) = 1 exactly
                 dotv[u] = (u ? dot.y : dot.x) + S[e];
             }
         }
 #pragma unroll
         for (int u = 0; u < RB; ++u) {
             const int e = e0 + u;
-            const bool on = act[u];
             const float alpha = alv[u], rom = romv[u], dot = dotv[u];
-            T = on ? T * rom : T;
+            T = T * rom;
             // upstream's last_alpha * last_c + (1 - last_alpha) * accum_rec, as one fma on the difference
-            const float acc_new = __builtin_fmaf(last_alpha, last_dot - acc_dot, acc_dot);
-            acc_dot = on ? acc_new : acc_dot;
-            last_dot = on ? dot : last_dot;
-            last_alpha = on ? alpha : last_alpha;
+            acc_dot = __builtin_fmaf(last_alpha, last_dot - acc_dot, acc_dot);
+            last_dot = dot;
+            last_alpha = alpha;
             float dL_dalpha = (dot - acc_dot) * T;
-            dL_dalpha = __builtin_fmaf(-T_final * rom, bg_dot, dL_dalpha);
-            wv[e] = on ? alpha * T : 0.0f;
-            tv[e] = on ? Gv[u] * dL_dalpha : 0.0f;
+            dL_dalpha = __builtin_fmaf(rom, bg_term, dL_dalpha);   // (-T_final / (1 - alpha)) bg . dL/dpix
+            wv[e] = alpha * T;
+            tv[e] = act[u] ? Gv[u] * dL_dalpha : 0.0f;
         }
         }
 
