@@ -30,10 +30,12 @@ from . import _lib
 
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "RasterizerState",
            "forward_native", "backward_native", "backward_views_native", "backward_composite_native",
-           "backward_preprocess_views_native"]
+           "backward_preprocess_views_native", "preprocess_views_native", "binning_views_native",
+           "render_views_native", "backward_composite_views_native", "language_split_native"]
 
 _lib.load()   # fail loudly at import if the native library is missing
 _BINNING_DELAY_CYCLES = 0   # tests only: GPU cycles slept on the stream before a side-stream binning
+_SPLIT_BEHIND_COUNTS = True  # preprocess_views_native: language split after the count event (A/B switch)
 
 
 class GaussianRasterizationSettings(NamedTuple):
@@ -249,16 +251,20 @@ def _run_binning(pf, stream):
     pf.ready_stream = stream
 
 
-def language_split_native(language_feature, stream=None):
+def language_split_native(language_feature, stream=None, out=None):
     """lsr_language_split: [P,32] fp32 -> [P,64] int16 holding the bf16 bit patterns (hi channels,
-    then lo) that the compositors' matrix-core operands use; lsr_fwd_in.language_feature_split."""
+    then lo) that the compositors' matrix-core operands use; lsr_fwd_in.language_feature_split.
+    `out` may be a preallocated [P,64] int16 tensor."""
     L = _lib.load()
     device = _check_device(language_feature)
     P, C = language_feature.shape
     stream = stream or torch.cuda.current_stream(device)
     lang = language_feature.detach().to(torch.float32).contiguous()
-    with torch.cuda.stream(stream):
-        out = torch.empty(P, 2 * C, dtype=torch.int16, device=device)
+    if out is None:
+        with torch.cuda.stream(stream):
+            out = torch.empty(P, 2 * C, dtype=torch.int16, device=device)
+    elif out.shape != (P, 2 * C) or out.dtype != torch.int16 or not out.is_contiguous():
+        raise ValueError("language_split_native: out must be a contiguous [P, 2C] int16 tensor")
     _lib.check(L.lsr_language_split(P, C, ctypes.c_void_p(lang.data_ptr()), ctypes.c_void_p(out.data_ptr()),
                                     ctypes.c_void_p(stream.cuda_stream)), "lsr_language_split")
     return out
@@ -281,9 +287,14 @@ def preprocess_views_native(raster_settings_list, means3D, opacities, shs=None, 
     stream = stream or torch.cuda.current_stream(device)
     fin, inputs, P = _fwd_inputs(means3D, opacities, shs, colors_precomp, language_feature, scales, rotations,
                                  cov3D_precomp)
-    if split_language and fin.C == 32 and P > 0:
-        inputs["language_feature_split"] = language_split_native(inputs["language_feature"], stream=stream)
+    split = split_language and fin.C == 32 and P > 0
+    if split:   # allocated now (fin carries the pointer), written behind the batch's count event
+        with torch.cuda.stream(stream):
+            inputs["language_feature_split"] = torch.empty(P, 64, dtype=torch.int16, device=device)
         fin.language_feature_split = inputs["language_feature_split"].data_ptr()
+        if not _SPLIT_BEHIND_COUNTS:
+            language_split_native(inputs["language_feature"], stream=stream, out=inputs["language_feature_split"])
+            split = False
     n = len(raster_settings_list)
     sts = [_NativeSettings(rs, device) for rs in raster_settings_list]
     with torch.cuda.stream(stream):
@@ -306,6 +317,8 @@ def preprocess_views_native(raster_settings_list, means3D, opacities, shs=None, 
         raise
     ev = torch.cuda.Event()
     ev.record(stream)
+    if split:   # only the compositors read it: it runs while the host waits for the counts
+        language_split_native(inputs["language_feature"], stream=stream, out=inputs["language_feature_split"])
     out = []
     for v, rs in enumerate(raster_settings_list):
         H, W = int(rs.image_height), int(rs.image_width)

@@ -156,16 +156,19 @@ class ViewParallelStep:
         if begin is not None:             # the renderer may look ahead only within this rank's views
             begin(self.views)
         flush = getattr(render_view, "flush", None)
-        if getattr(flush, "overwrites", False):
-            b.zero_accumulated_()        # the flush writes every other field (HBM write saved)
-        else:
-            b.zero_()
+        zero = b.zero_accumulated_ if getattr(flush, "overwrites", False) else b.zero_
+        # (the flush writes every other field: HBM write saved)
         batch = getattr(render_view, "render_batch", None)
         if batch is not None:             # every view of the rank at once (batched compositor launches)
-            radii_views = [r for r in batch(self.views, b) if r is not None]
+            if getattr(batch, "before_wait", False):
+                radii_views = [r for r in batch(self.views, b, before_wait=zero) if r is not None]
+            else:
+                zero()
+                radii_views = [r for r in batch(self.views, b) if r is not None]
             if b.radii is None:
                 radii_views = []
         else:
+            zero()
             radii_views = []
             for v in self.views:
                 radii = render_view(v, b)
@@ -287,14 +290,18 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
     batched = batch_backward and not deterministic
     held = []                             # (state, dL_dcolor, dL_dlang, dL_ddepth) awaiting flush
 
-    def batch_preprocess(v):
+    def batch_preprocess(v, before_wait=None):
         """The step's views from v on, as one batch: preprocess + depth sorts + instance scans, one
-        host wait for their counts, then their binning (lsr_forward_*_views)."""
+        host wait for their counts, then their binning (lsr_forward_*_views).  before_wait() is
+        enqueued behind the batch's launches, ahead of that wait (work that fills the device's
+        idle stretch while the host reads the counts)."""
         views = [w for w in step_views[0] if w >= v] if step_views[0] is not None else [v]
         views = [w for w in views if has_view(w)] or [v]
         pfs = dgr.preprocess_views_native([settings[w] for w in views], scene.means3D, scene.opacities,
                                           shs=scene.shs, language_feature=scene.lang, scales=scene.scales,
                                           rotations=scene.rotations)
+        if before_wait is not None:
+            before_wait()
         if 0 < early_views < len(pfs) and scene.means3D.is_cuda:
             dev = scene.means3D.device
             if bin_side[0] is None:
@@ -334,18 +341,24 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
             pending[v + 1] = preprocess(v + 1, stream=side)
         return radii
 
-    def render_batch(views, bucket: GradBucket):
+    def render_batch(views, bucket: GradBucket, before_wait=None):
         """Every view of the step at once (ViewParallelStep.run prefers this to per-view calls):
         forward phase 1 and binning as one batch, then per binning batch (the early views binned
         on this stream, the rest on the side stream) ONE compositor forward launch for its views,
         their upstream gradients (grad_fn, as train.py computes the loss on the stacked renders
         before backward), and ONE compositor backward launch.  Two launches per group instead of
-        two per view: the chip no longer drains at every view's last waves.  Returns the radii."""
+        two per view: the chip no longer drains at every view's last waves.  before_wait() (the
+        step's bucket zeroing) runs behind the preprocess launches, while the host waits for the
+        instance counts.  Returns the radii."""
         views = list(views)
         if not views:
+            if before_wait is not None:
+                before_wait()
             return []
         if views[0] not in pending:
-            batch_preprocess(views[0])
+            batch_preprocess(views[0], before_wait)
+        elif before_wait is not None:
+            before_wait()
         pfs = [pending.pop(v) for v in views]
         groups = []                        # consecutive views binned by one launch set (one event)
         for v, pf in zip(views, pfs):
@@ -403,5 +416,6 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
         render_view.flush = flush
         if batch_fwd and composite_batch:
             render_batch.last_num_rendered = []
+            render_batch.before_wait = True   # takes the step's zeroing into its host-wait stretch
             render_view.render_batch = render_batch
     return render_view

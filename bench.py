@@ -141,6 +141,9 @@ def parse_args(argv=None):
                     help="batched pipeline: views binned before compositing starts; the rest bin on a side stream "
                          "while they composite (0: all binned first)")
     ap.add_argument("--no-overlap", action="store_true", help="diagnostic: no side stream (uncontended phase times)")
+    ap.add_argument("--no-wait-fill", action="store_true",
+                    help="diagnostic: zero the bucket and split the language rows before the preprocess "
+                         "instead of while the host waits for the instance counts")
     ap.add_argument("--per-view-composite", action="store_true",
                     help="one compositor launch per view instead of one per binning batch of views")
     ap.add_argument("--pipeline", choices=("batched", "lookahead", "side"), default=None,
@@ -216,10 +219,13 @@ def run(args):
 
     if hasattr(render, "render_batch"):                    # one compositor launch per binning batch
 
-        def render_batch(views, b):
-            r = render.render_batch(views, b)
+        def render_batch(views, b, before_wait=None):
+            r = render.render_batch(views, b, before_wait=before_wait)
             Ks.extend(render.render_batch.last_num_rendered)
             return r
+        render_batch.before_wait = not args.no_wait_fill
+        if args.no_wait_fill:
+            dgr._SPLIT_BEHIND_COUNTS = False
         render_view.render_batch = render_batch
     if hasattr(render, "flush"):                           # batched backward of the step's views
         render_view.flush = render.flush

@@ -58,12 +58,13 @@ def test_bench_pipeline_matches_oracle_at_headline_size():
         radii[v] = r.clone()
         return r
 
-    def render_batch(views, b):             # the bench's path: one compositor launch per binning batch
-        rs = render.render_batch(views, b)
+    def render_batch(views, b, before_wait=None):   # the bench's path: one compositor launch per binning batch
+        rs = render.render_batch(views, b, before_wait=before_wait)
         for v, r in zip(views, rs):
             radii[v] = r.clone()
         return rs
 
+    render_batch.before_wait = True
     render_view.render_batch = render_batch
     render_view.flush, render_view.begin_step, render_view.end_step = render.flush, render.begin_step, render.end_step
     bucket = GradBucket(P, scene.shs.shape[1], C, "cuda", densify_stats=True)
