@@ -225,7 +225,8 @@ class ViewParallelStep:
 
 
 def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool = False, overlap: bool = True,
-                         batch_backward: bool = True, early_views: int = 3, composite_batch: bool = True):
+                         batch_backward: bool = True, early_views: int = 3, composite_batch: bool = True,
+                         side_priority: int = 0):
     """render_view callback for ViewParallelStep on the HIP rasterizer (the product path).
 
     scene    : object with means3D, opacities, shs, lang, scales, rotations device tensors
@@ -305,7 +306,7 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
         if 0 < early_views < len(pfs) and scene.means3D.is_cuda:
             dev = scene.means3D.device
             if bin_side[0] is None:
-                bin_side[0] = torch.cuda.Stream(device=dev)   # priorities -1 / +1 measured no better
+                bin_side[0] = torch.cuda.Stream(device=dev, priority=side_priority)
             side_b = bin_side[0]
             dgr.binning_views_native(pfs[:early_views])      # waits for the batch's counts
             side_b.wait_stream(torch.cuda.current_stream(dev))   # after the preprocess batch

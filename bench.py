@@ -141,6 +141,8 @@ def parse_args(argv=None):
                     help="batched pipeline: views binned before compositing starts; the rest bin on a side stream "
                          "while they composite (0: all binned first)")
     ap.add_argument("--no-overlap", action="store_true", help="diagnostic: no side stream (uncontended phase times)")
+    ap.add_argument("--side-priority", type=int, default=0,
+                    help="torch stream priority of the side-stream binning (negative = higher)")
     ap.add_argument("--no-wait-fill", action="store_true",
                     help="diagnostic: zero the bucket and split the language rows before the preprocess "
                          "instead of while the host waits for the instance counts")
@@ -209,7 +211,8 @@ def run(args):
     render = native_view_renderer(scene, settings, lambda v, color, lang, depth: (gcol, glang, None),
                                   overlap=False if args.no_overlap else (True if args.pipeline == "side"
                                                                          else args.pipeline),
-                                  early_views=args.early_views, composite_batch=not args.per_view_composite)
+                                  early_views=args.early_views, composite_batch=not args.per_view_composite,
+                                  side_priority=args.side_priority)
     Ks = []
 
     def render_view(v, b):
