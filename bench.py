@@ -143,6 +143,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-overlap", action="store_true", help="diagnostic: no side stream (uncontended phase times)")
     ap.add_argument("--side-priority", type=int, default=0,
                     help="torch stream priority of the side-stream binning (negative = higher)")
+    ap.add_argument("--side-after-binning", action="store_true",
+                    help="diagnostic: the side-stream binning waits for the early views' binning too")
     ap.add_argument("--no-wait-fill", action="store_true",
                     help="diagnostic: zero the bucket and split the language rows before the preprocess "
                          "instead of while the host waits for the instance counts")
@@ -212,7 +214,7 @@ def run(args):
                                   overlap=False if args.no_overlap else (True if args.pipeline == "side"
                                                                          else args.pipeline),
                                   early_views=args.early_views, composite_batch=not args.per_view_composite,
-                                  side_priority=args.side_priority)
+                                  side_priority=args.side_priority, side_from_preprocess=not args.side_after_binning)
     Ks = []
 
     def render_view(v, b):
