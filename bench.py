@@ -365,6 +365,9 @@ def run(args):
             value=round(value, 3), unit="frames/s", n_gpus=world, ranks=pg_ranks, steps=args.steps, warmup=args.warmup,
             ms_per_step=round(elapsed / args.steps * 1e3, 3), higher_is_better=True, scaling="weak",
             vs_baseline=None, dtype="f32", data="synthetic",
+            precision=("fp32 per-pixel arithmetic (T, alpha, RGB, depth, the recurrences); the language "
+                       "channel sums and the backward's per-Gaussian pixel sums on MFMA as bf16 hi/lo "
+                       "splits, three products, fp32 accumulation (~2^-17 relative)"),
             config=dict(workload="S2M synthetic (BASELINE configs[2] per GPU; configs[3] batch split)",
                         gaussians=P, width=W, height=H, channels=C, views_per_gpu_per_step=V,
                         global_batch=world * V, parallelism=f"dp{world}", pipeline="none" if args.no_overlap else args.pipeline, num_rendered_mean=int(Kmean),
