@@ -915,21 +915,31 @@ void launch_atb(const AtbArgs& a, int njobs, hipStream_t st) {
     hipLaunchKernelGGL(k_atb, dim3(nb, njobs), dim3(256), 0, st, a);
 }
 
-// packed channel-last gradient [H][W][16] -> torch [16][H][W], added
-__global__ void k_unpack_plane_grad(const float* __restrict__ src, float* __restrict__ dst, int H, int W, int replicas,
-                                    int64_t stride) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;   // over 16 * H * W destination floats
-    if (i >= H * W * 16) return;
-    const int hw = i % (H * W), c = i / (H * W);
-    float s = 0.0f;
-    for (int r = 0; r < replicas; ++r) s += src[(size_t)r * stride + (size_t)hw * 16 + c];
-    dst[i] += s;
+// packed channel-last gradient replicas [r][H][W][16] -> torch [16][H][W], summed over the replicas
+// and added.  One block per 16 texels (256 floats): each thread sums one float over the replicas
+// with coalesced reads, the block transposes through LDS (pitch 17) and writes each channel's 16
+// texels as one 64-byte run.  (A thread per destination float read 64-byte-strided words of every
+// replica: 0.38 ms per training iteration at configs[4]'s planes.)
+__global__ void __launch_bounds__(256) k_unpack_plane_grad(const float* __restrict__ src, float* __restrict__ dst,
+                                                           int H, int W, int replicas, int64_t stride) {
+    __shared__ float s_t[16][17];
+    const int HW = H * W, base = blockIdx.x * 16, t = threadIdx.x;
+    const int tex = t >> 4, ch = t & 15;
+    float acc = 0.0f;
+    if (base + tex < HW) {
+        const float* p = src + (size_t)base * 16 + t;
+        for (int r = 0; r < replicas; ++r) acc += p[(size_t)r * stride];
+    }
+    s_t[tex][ch] = acc;
+    __syncthreads();
+    const int c = t >> 4, tl = t & 15;
+    if (base + tl < HW) dst[(size_t)c * HW + base + tl] += s_t[tl][c];
 }
 
 void launch_unpack_plane_grad(const float* src, float* dst, int H, int W, int replicas, int64_t stride,
                               hipStream_t st) {
-    hipLaunchKernelGGL(k_unpack_plane_grad, dim3((H * W * 16 + 255) / 256), dim3(256), 0, st, src, dst, H, W,
-                       replicas, stride);
+    hipLaunchKernelGGL(k_unpack_plane_grad, dim3((H * W + 15) / 16), dim3(256), 0, st, src, dst, H, W, replicas,
+                       stride);
 }
 
 // ---- parameter packing ----------------------------------------------------------------------------
@@ -971,6 +981,54 @@ void launch_pack_weight_t(const float* src, __bf16* hi, __bf16* lo, int rows, in
                           hipStream_t st) {
     hipLaunchKernelGGL(k_pack_weight_t, dim3((cols_pad * k_pad + 255) / 256), dim3(256), 0, st, src, hi, lo, rows, cols,
                        k_pad, cols_pad);
+}
+
+// Every packing job of lsr_deform_prepare (planes, weights, transposed weights: ~34 per field) in
+// one launch: block b runs job j where first[j] <= b < first[j + 1] (a scalar search over <= 48
+// jobs); the element work is that of the single-job kernels above.  (One launch per job left the
+// device idle between ~34 tiny kernels every training iteration.)
+__global__ void __launch_bounds__(256) k_pack_batch(PackBatch pb) {
+    const uint32_t b = blockIdx.x;
+    int j = 0;
+    while (j + 1 < pb.n && b >= pb.j[j + 1].first_block) ++j;
+    const PackJob& q = pb.j[j];
+    const int i = (int)(b - q.first_block) * 256 + (int)threadIdx.x;
+    if (q.kind == PACK_PLANE) {   // [16][H][W] -> [H][W][16]; a = H * W
+        if (i >= q.a * 16) return;
+        reinterpret_cast<float*>(q.hi)[i] = q.src[(size_t)(i & 15) * q.a + (i >> 4)];
+        return;
+    }
+    float v;
+    if (q.kind == PACK_WEIGHT) {   // [rows][cols] -> [rows_pad][cols_pad]; a rows, b rows_pad, c cols, d cols_pad
+        if (i >= q.b * q.d) return;
+        const int r = i / q.d, c = i - r * q.d;
+        v = (r < q.a && c < q.c) ? q.src[(size_t)r * q.c + c] : 0.0f;
+    } else {                       // transposed: a rows, b cols, c k_pad, d cols_pad
+        if (i >= q.d * q.c) return;
+        const int c = i / q.c, r = i - c * q.c;
+        v = (r < q.a && c < q.b) ? q.src[(size_t)r * q.b + c] : 0.0f;
+    }
+    __bf16 h, l;
+    dsplit(v, h, l);
+    reinterpret_cast<__bf16*>(q.hi)[i] = h;
+    q.lo[i] = l;
+}
+
+void launch_pack_batch(PackJob* jobs, int n, hipStream_t st) {
+    for (int j0 = 0; j0 < n; j0 += PACK_MAX_JOBS) {
+        PackBatch pb{};
+        pb.n = std::min(PACK_MAX_JOBS, n - j0);
+        uint32_t blocks = 0;
+        for (int k = 0; k < pb.n; ++k) {
+            PackJob q = jobs[j0 + k];
+            const int64_t elems = q.kind == PACK_PLANE ? (int64_t)q.a * 16
+                                  : q.kind == PACK_WEIGHT ? (int64_t)q.b * q.d : (int64_t)q.d * q.c;
+            q.first_block = blocks;
+            blocks += (uint32_t)((elems + 255) / 256);
+            pb.j[k] = q;
+        }
+        if (blocks) hipLaunchKernelGGL(k_pack_batch, dim3(blocks), dim3(256), 0, st, pb);
+    }
 }
 
 void launch_pack_plane(const float* src, float* dst, int H, int W, hipStream_t st) {

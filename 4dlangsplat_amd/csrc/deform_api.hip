@@ -7,6 +7,7 @@
 #include "../../include/lsr.h"
 #include "../../include/lsr_deform.h"
 #include "lsr_internal.h"
+#include <vector>
 
 namespace lsr {
 int fail(int code, const std::string& msg);   // lsr_api.hip (thread-local lsr_last_error)
@@ -142,37 +143,50 @@ extern "C" int lsr_deform_prepare(const lsr_deform_net* net, void* workspace, vo
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const Layout L = layout(net);
     char* ws = reinterpret_cast<char*>(workspace);
+    std::vector<lsr::PackJob> jobs;   // every packing job, then one launch (lsr::launch_pack_batch)
+    auto plane = [&](const float* src, float* dst, int H, int W) {
+        lsr::PackJob q{};
+        q.kind = lsr::PACK_PLANE; q.a = H * W; q.src = src; q.hi = dst;
+        jobs.push_back(q);
+    };
+    auto wt = [&](int kind, const float* src, __bf16* h, __bf16* l, int a, int b, int c, int d) {
+        lsr::PackJob q{};
+        q.kind = kind; q.a = a; q.b = b; q.c = c; q.d = d; q.src = src; q.hi = h; q.lo = l;
+        jobs.push_back(q);
+    };
     for (int s = 0; s < net->n_scales; ++s)
         for (int ci = 0; ci < 6; ++ci) {
             int W, H;
             plane_dims(net, s, ci, W, H);
-            lsr::launch_pack_plane(net->planes[s][ci], reinterpret_cast<float*>(ws + L.plane_off[6 * s + ci]), H, W, st);
+            plane(net->planes[s][ci], reinterpret_cast<float*>(ws + L.plane_off[6 * s + ci]), H, W);
         }
     auto hi = [&](const Pack& p) { return reinterpret_cast<__bf16*>(ws + p.off); };
     auto lo = [&](const Pack& p) { return reinterpret_cast<__bf16*>(ws + p.off + align256(p.count * sizeof(__bf16))); };
     const int F = feat_dim(net), Fpad = (F + 31) / 32 * 32;
+    constexpr int PW = lsr::PACK_WEIGHT, PT = lsr::PACK_WEIGHT_T;
     for (int k = 0; k < nlayers(net); ++k) {
         const int K = k == 0 ? F : kW;
-        lsr::launch_pack_weight(net->w_feat[k], hi(L.wf[k]), lo(L.wf[k]), kW, kW, K, K, st);
-        lsr::launch_pack_weight_t(net->w_feat[k], hi(L.wft[k]), lo(L.wft[k]), kW, K, kW, k == 0 ? Fpad : kW, st);
+        wt(PW, net->w_feat[k], hi(L.wf[k]), lo(L.wf[k]), kW, kW, K, K);
+        wt(PT, net->w_feat[k], hi(L.wft[k]), lo(L.wft[k]), kW, K, kW, k == 0 ? Fpad : kW);
     }
     for (int hd = 0; hd < LSR_DEFORM_HEADS; ++hd) {
         if (!head_on(net, hd)) continue;
         const int nout = head_out(net, hd);
-        lsr::launch_pack_weight(net->w1[hd], hi(L.w1[hd]), lo(L.w1[hd]), kW, kW, kW, kW, st);
-        lsr::launch_pack_weight(net->w2[hd], hi(L.w2[hd]), lo(L.w2[hd]), nout, lsr::DEF_W2ROWS, kW, kW, st);
-        lsr::launch_pack_weight_t(net->w1[hd], hi(L.w1t[hd]), lo(L.w1t[hd]), kW, kW, kW, kW, st);
-        lsr::launch_pack_weight_t(net->w2[hd], hi(L.w2t[hd]), lo(L.w2t[hd]), nout, kW, 64, kW, st);
+        wt(PW, net->w1[hd], hi(L.w1[hd]), lo(L.w1[hd]), kW, kW, kW, kW);
+        wt(PW, net->w2[hd], hi(L.w2[hd]), lo(L.w2[hd]), nout, lsr::DEF_W2ROWS, kW, kW);
+        wt(PT, net->w1[hd], hi(L.w1t[hd]), lo(L.w1t[hd]), kW, kW, kW, kW);
+        wt(PT, net->w2[hd], hi(L.w2t[hd]), lo(L.w2t[hd]), nout, kW, 64, kW);
     }
     if (lang_mlp(net)) {
         const int kin = lang_kin(net), kp = lang_kpad(net), C = net->lang_dim;
-        lsr::launch_pack_weight(net->w_lang[0], hi(L.wl[0]), lo(L.wl[0]), kW, kW, kin, kp, st);
-        lsr::launch_pack_weight(net->w_lang[1], hi(L.wl[1]), lo(L.wl[1]), kW, kW, kW, kW, st);
-        lsr::launch_pack_weight(net->w_lang[2], hi(L.wl[2]), lo(L.wl[2]), C, 32, kW, kW, st);
-        lsr::launch_pack_weight_t(net->w_lang[0], hi(L.wlt[0]), lo(L.wlt[0]), kW, kin, kW, (kp + 31) / 32 * 32, st);
-        lsr::launch_pack_weight_t(net->w_lang[1], hi(L.wlt[1]), lo(L.wlt[1]), kW, kW, kW, kW, st);
-        lsr::launch_pack_weight_t(net->w_lang[2], hi(L.wlt[2]), lo(L.wlt[2]), C, kW, 32, kW, st);
+        wt(PW, net->w_lang[0], hi(L.wl[0]), lo(L.wl[0]), kW, kW, kin, kp);
+        wt(PW, net->w_lang[1], hi(L.wl[1]), lo(L.wl[1]), kW, kW, kW, kW);
+        wt(PW, net->w_lang[2], hi(L.wl[2]), lo(L.wl[2]), C, 32, kW, kW);
+        wt(PT, net->w_lang[0], hi(L.wlt[0]), lo(L.wlt[0]), kW, kin, kW, (kp + 31) / 32 * 32);
+        wt(PT, net->w_lang[1], hi(L.wlt[1]), lo(L.wlt[1]), kW, kW, kW, kW);
+        wt(PT, net->w_lang[2], hi(L.wlt[2]), lo(L.wlt[2]), C, kW, 32, kW);
     }
+    lsr::launch_pack_batch(jobs.data(), (int)jobs.size(), st);
     if (hipGetLastError() != hipSuccess) return lsr::fail(LSR_EHIP, "deformation packing launch failed");
     return LSR_OK;
 }

@@ -260,6 +260,18 @@ struct DeformArgs {
 };
 void launch_deform_fwd(const DeformArgs& a, hipStream_t st);
 void launch_pack_plane(const float* src, float* dst, int H, int W, hipStream_t st);
+// lsr_deform_prepare's packing jobs in one launch per PACK_MAX_JOBS (k_pack_batch)
+enum PackKind { PACK_PLANE = 0, PACK_WEIGHT = 1, PACK_WEIGHT_T = 2 };
+struct PackJob {
+    int kind, a, b, c, d;             // PLANE: a = H * W; WEIGHT: rows, rows_pad, cols, cols_pad; T: rows, cols, k_pad, cols_pad
+    uint32_t first_block;             // set by launch_pack_batch
+    const float* src;
+    void* hi;                         // PLANE: the float destination
+    __bf16* lo;
+};
+constexpr int PACK_MAX_JOBS = 64;
+struct PackBatch { PackJob j[PACK_MAX_JOBS]; int n; };
+void launch_pack_batch(PackJob* jobs, int n, hipStream_t st);
 void launch_pack_weight(const float* src, __bf16* hi, __bf16* lo, int rows, int rows_pad, int cols, int cols_pad,
                         hipStream_t st);
 // transposed packing: src fp32 [rows][cols] -> hi / lo [cols_pad][k_pad] with dst[c][r] = src[r][c],

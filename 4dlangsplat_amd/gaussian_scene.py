@@ -276,7 +276,9 @@ def render(viewpoint_camera, pc: GaussianScene, bg_color: torch.Tensor, scaling_
         projmatrix=viewpoint_camera.full_proj_transform.to(dev), sh_degree=pc.active_sh_degree,
         campos=viewpoint_camera.camera_center.to(dev), prefiltered=False, debug=debug,
         include_feature=include_feature)
-    t = torch.tensor(float(viewpoint_camera.time), device=dev).repeat(means3D.shape[0], 1)
+    # the reference builds this with torch.tensor(time).to(device).repeat (a host-to-device copy,
+    # which synchronises the stream): a fill gives the same values without the wait
+    t = torch.full((means3D.shape[0], 1), float(viewpoint_camera.time), device=dev)
     rasterizer = GaussianRasterizer(raster_settings=raster_settings)
     opacity = pc.opacity
     shs = pc.get_features

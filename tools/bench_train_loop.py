@@ -87,6 +87,12 @@ def build(args, dev):
     t_raw, t_fp = teacher(P, W, H, dev)
     # the dataloader's frames: `cameras` viewpoints x `frames` times
     rig = synthetic.camera_batch(args.cameras, W, H, tanfovx=0.6, seed=1, max_yaw=15.0, sigma_t=0.3)
+    # the reference's Camera keeps its matrices on the GPU (scene/cameras.py:56-67, .cuda()): no
+    # host-to-device copy (a stream synchronisation) per render
+    rig = [dataclasses.replace(c, world_view_transform=c.world_view_transform.to(dev),
+                               projection_matrix=c.projection_matrix.to(dev),
+                               full_proj_transform=c.full_proj_transform.to(dev),
+                               camera_center=c.camera_center.to(dev)) for c in rig]
     pool = [dataclasses.replace(c, time=f / max(1, args.frames - 1)) for f in range(args.frames) for c in rig]
     tfield = DeformationField({k: v.to(dev) for k, v in t_fp.items()}, NEU3D_RES, NEU3D_MULTIRES)
     tstep = TrainStep(GaussianTrainer(t_raw, feature_lrs()), tfield)
