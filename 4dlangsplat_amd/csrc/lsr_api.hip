@@ -806,6 +806,20 @@ int lsr_backward_views(int32_t n_views, const lsr_settings* const* s, const lsr_
                                          stream);
 }
 
+int lsr_radii_max(int32_t P, int32_t n_views, const int32_t* const* radii, int32_t* out, int32_t accumulate,
+                  lsr_stream_t stream) {
+    if (P < 0 || n_views < 0 || (P > 0 && n_views > 0 && (!radii || !out))) return fail(LSR_EINVAL, "bad lsr_radii_max arguments");
+    for (int v = 0; v < n_views; ++v)
+        if (P > 0 && (!radii[v] || (reinterpret_cast<uintptr_t>(radii[v]) & 15)))
+            return fail(LSR_EINVAL, "lsr_radii_max: every radii array must be a 16-byte aligned device pointer");
+    if (P > 0 && (reinterpret_cast<uintptr_t>(out) & 15)) return fail(LSR_EINVAL, "lsr_radii_max: out must be 16-byte aligned");
+    if (P == 0 || n_views == 0) return LSR_OK;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    lsr::launch_radii_max(P, n_views, reinterpret_cast<const int* const*>(radii), out, accumulate != 0, st);
+    LSR_LAUNCHED("radii max", st, false);
+    return LSR_OK;
+}
+
 int lsr_mark_visible(int32_t P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                      uint8_t* present, lsr_stream_t stream) {
     (void)projmatrix;

@@ -165,6 +165,7 @@ struct PreprocessBwdViewsArgs {
 void launch_preprocess_bwd_views(const PreprocessBwdViewsArgs& a, bool accumulate, hipStream_t st);
 
 void launch_language_split(int P, const float* lang, uint16_t* out, hipStream_t st);
+void launch_radii_max(int P, int n, const int* const* radii, int* out, bool accumulate, hipStream_t st);
 
 struct RenderFwdArgs {
     int W, H, grid_x, grid_y, C, include_feature;

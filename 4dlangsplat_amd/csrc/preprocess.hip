@@ -364,6 +364,37 @@ __global__ void k_mark_visible(int P, const float* __restrict__ means3D, const f
     const float3 p = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
     present[i] = xform4x3(view, p).z > 0.2f;
 }
+// out[i] = max(out[i] (accumulate) or 0, radii_0[i], ..., radii_{n-1}[i]): the radii MAX over a
+// step's views (train.py:270) in one pass, int4 vectors (P % 4 == 0 rows; the tail scalar)
+struct RadiiMaxArgs { const int* r[LSR_MAX_VIEWS]; };
+__global__ void __launch_bounds__(256) k_radii_max(int P, int n, RadiiMaxArgs ra, int* __restrict__ out, int accumulate) {
+    const int i4 = blockIdx.x * 256 + threadIdx.x, i = 4 * i4;
+    if (i >= P) return;
+    if (i + 4 <= P) {
+        int4 m = accumulate ? reinterpret_cast<const int4*>(out)[i4] : make_int4(0, 0, 0, 0);
+        for (int v = 0; v < n; ++v) {
+            const int4 x = reinterpret_cast<const int4*>(ra.r[v])[i4];
+            m = make_int4(max(m.x, x.x), max(m.y, x.y), max(m.z, x.z), max(m.w, x.w));
+        }
+        reinterpret_cast<int4*>(out)[i4] = m;
+    } else {
+        for (int k = i; k < P; ++k) {
+            int m = accumulate ? out[k] : 0;
+            for (int v = 0; v < n; ++v) m = max(m, ra.r[v][k]);
+            out[k] = m;
+        }
+    }
+}
+void launch_radii_max(int P, int n, const int* const* radii, int* out, bool accumulate, hipStream_t st) {
+    for (int v0 = 0; v0 < n; v0 += LSR_MAX_VIEWS) {
+        RadiiMaxArgs ra{};
+        const int nv = n - v0 < LSR_MAX_VIEWS ? n - v0 : LSR_MAX_VIEWS;
+        for (int k = 0; k < nv; ++k) ra.r[k] = radii[v0 + k];
+        hipLaunchKernelGGL(k_radii_max, dim3((unsigned)((P + 1023) / 1024)), dim3(256), 0, st, P, nv, ra, out,
+                           (accumulate || v0 > 0) ? 1 : 0);
+    }
+}
+
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st) {
     if (P == 0) return;
     hipLaunchKernelGGL(k_mark_visible, dim3((P + 255) / 256), dim3(256), 0, st, P, means3D, view, present);

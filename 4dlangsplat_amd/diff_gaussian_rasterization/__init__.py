@@ -31,7 +31,8 @@ from . import _lib
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "RasterizerState",
            "forward_native", "backward_native", "backward_views_native", "backward_composite_native",
            "backward_preprocess_views_native", "preprocess_views_native", "binning_views_native",
-           "render_views_native", "backward_composite_views_native", "language_split_native"]
+           "render_views_native", "backward_composite_views_native", "language_split_native",
+           "radii_max_native"]
 
 _lib.load()   # fail loudly at import if the native library is missing
 _BINNING_DELAY_CYCLES = 0   # tests only: GPU cycles slept on the stream before a side-stream binning
@@ -435,6 +436,27 @@ def render_native(pending: PendingForward):
         raise
     state = RasterizerState(pending.settings, pending.inputs, pending.fin, pending.geom, binning, img, K, pending.radii)
     return color, lang_out, pending.radii, depth, state
+
+
+def radii_max_native(radii, out, accumulate=False, stream=None):
+    """lsr_radii_max: out = max(out if accumulate, radii[0], ..., radii[n-1]) elementwise, int32 [P]
+    device tensors, one launch per 8 views on `stream` (default: current): the radii MAX over a
+    batch's views (train.py:270) without a stack copy or one launch per view."""
+    if not radii:
+        return out
+    L = _lib.load()
+    P = out.shape[0]
+    rs = [r.contiguous() for r in radii]
+    for r in rs:
+        if r.dtype != torch.int32 or r.shape != (P,) or r.device != out.device:
+            raise ValueError("radii_max_native: int32 [P] tensors on out's device")
+    if out.dtype != torch.int32 or not out.is_contiguous():
+        raise ValueError("radii_max_native: out must be a contiguous int32 tensor")
+    stream = stream or torch.cuda.current_stream(out.device)
+    arr = (ctypes.c_void_p * len(rs))(*[r.data_ptr() for r in rs])
+    _lib.check(L.lsr_radii_max(P, len(rs), arr, ctypes.c_void_p(out.data_ptr()), 1 if accumulate else 0,
+                               ctypes.c_void_p(stream.cuda_stream)), "lsr_radii_max")
+    return out
 
 
 def render_views_native(pendings):

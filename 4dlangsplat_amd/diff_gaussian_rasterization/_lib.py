@@ -162,6 +162,8 @@ SIGNATURES = {
                                                           ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]),
     "lsr_language_split": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_void_p]),
+    "lsr_radii_max": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p,
+                                     ctypes.c_int32, ctypes.c_void_p]),
     "lsr_mark_visible": (ctypes.c_int, [ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p]),
     "lsr_profile_enable": (ctypes.c_int, [ctypes.c_int32]),

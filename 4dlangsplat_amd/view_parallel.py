@@ -175,8 +175,10 @@ class ViewParallelStep:
                 if b.radii is not None and radii is not None:
                     radii_views.append(radii)
         # radii MAX over the views (train.py:270) after the views' launches, not between them
-        for radii in radii_views:
-            torch.maximum(b.radii, radii.to(torch.int32), out=b.radii)
+        # (a batch renderer may have reduced them itself, in one launch)
+        if not (batch is not None and getattr(batch, "radii_reduced", False)):
+            for radii in radii_views:
+                torch.maximum(b.radii, radii.to(torch.int32), out=b.radii)
         pending = []
         lo, hi = b.ranges["language_feature"]
         if self.world > 1 and b.radii is not None:   # final once the last view's forward ran
@@ -293,7 +295,7 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
     batched = batch_backward and not deterministic
     held = []                             # (state, dL_dcolor, dL_dlang, dL_ddepth) awaiting flush
 
-    def batch_preprocess(v, before_wait=None):
+    def batch_preprocess(v, before_wait=None, radii_out=None):
         """The step's views from v on, as one batch: preprocess + depth sorts + instance scans, one
         host wait for their counts, then their binning (lsr_forward_*_views).  before_wait() is
         enqueued behind the batch's launches, ahead of that wait (work that fills the device's
@@ -305,6 +307,8 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
                                           rotations=scene.rotations)
         if before_wait is not None:
             before_wait()
+        if radii_out is not None:     # the views' radii MAX, also while the host waits for the counts
+            dgr.radii_max_native([pf.radii for pf in pfs], radii_out)
         if 0 < early_views < len(pfs) and scene.means3D.is_cuda:
             dev = scene.means3D.device
             if bin_side[0] is None:
@@ -361,8 +365,10 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
             if before_wait is not None:
                 before_wait()
             return []
-        if views[0] not in pending:
-            batch_preprocess(views[0], before_wait)
+        reduce_radii = bucket.radii is not None and scene.means3D.is_cuda
+        fresh = views[0] not in pending
+        if fresh:
+            batch_preprocess(views[0], before_wait, radii_out=bucket.radii if reduce_radii else None)
         elif before_wait is not None:
             before_wait()
         pfs = [pending.pop(v) for v in views]
@@ -385,7 +391,10 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
                 ks.append(st.num_rendered)
             held.extend(dgr.backward_composite_views_native([x[4] for x in res], gcs, gls, gds,
                                                             dL_dlanguage=bucket.views["language_feature"]))
+        if reduce_radii and not fresh:
+            dgr.radii_max_native(radii, bucket.radii)
         render_batch.last_num_rendered = ks
+        render_batch.radii_reduced = reduce_radii   # bucket.radii already holds this rank's MAX
         return radii
 
     def flush(bucket: GradBucket, row_chunks=None, on_rows=None):

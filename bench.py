@@ -227,6 +227,7 @@ def run(args):
         def render_batch(views, b, before_wait=None):
             r = render.render_batch(views, b, before_wait=before_wait)
             Ks.extend(render.render_batch.last_num_rendered)
+            render_batch.radii_reduced = render.render_batch.radii_reduced
             return r
         render_batch.before_wait = not args.no_wait_fill
         if args.no_wait_fill:

@@ -243,6 +243,13 @@ int lsr_backward_preprocess_views_rows(int32_t n_views, const lsr_settings *cons
  * layout); on the caller's stream. */
 int lsr_language_split(int32_t P, int32_t C, const float *language_feature, uint16_t *out, lsr_stream_t stream);
 
+/* out[i] = max(out[i] if accumulate, radii_v[i] over the n_views views): the radii MAX of a training
+ * batch's views (/root/reference/train.py:270, torch.stack(radii_list).max(dim=0)), one pass over
+ * host array `radii` of 16-byte aligned device pointers.  No reference counterpart in the rasterizer
+ * (the reference reduces with PyTorch). */
+int lsr_radii_max(int32_t P, int32_t n_views, const int32_t *const *radii, int32_t *out, int32_t accumulate,
+                  lsr_stream_t stream);
+
 int lsr_mark_visible(int32_t P, const float *means3D, const float *viewmatrix, const float *projmatrix,
                      uint8_t *present, lsr_stream_t stream);
 

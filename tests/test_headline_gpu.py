@@ -60,6 +60,7 @@ def test_bench_pipeline_matches_oracle_at_headline_size():
 
     def render_batch(views, b, before_wait=None):   # the bench's path: one compositor launch per binning batch
         rs = render.render_batch(views, b, before_wait=before_wait)
+        render_batch.radii_reduced = render.render_batch.radii_reduced
         for v, r in zip(views, rs):
             radii[v] = r.clone()
         return rs

@@ -198,3 +198,17 @@ def test_batched_composite_step_agrees(early):
     assert not torch.isnan(f1).any() and torch.equal(r0, r1)
     scale = float(f0.abs().max())
     assert scale > 0 and float((f0 - f1).abs().max()) <= 1e-5 * scale
+
+
+def test_radii_max_native():
+    """lsr_radii_max against torch: the vector rows and the scalar tail, more views than one launch
+    takes (8), accumulate on and off."""
+    g = torch.Generator(device="cpu").manual_seed(4)
+    for P in (1, 7, 1001, 4096):
+        rs = [torch.randint(0, 50, (P,), generator=g, dtype=torch.int32).cuda() for _ in range(11)]
+        out = torch.full((P,), 7, dtype=torch.int32, device="cuda")
+        dgr.radii_max_native(rs, out, accumulate=True)
+        ref = torch.clamp_min(torch.stack(rs).amax(0), 7)
+        assert torch.equal(out, ref)
+        dgr.radii_max_native(rs[:3], out)
+        assert torch.equal(out, torch.stack(rs[:3]).amax(0))
