@@ -212,3 +212,40 @@ def test_radii_max_native():
         assert torch.equal(out, ref)
         dgr.radii_max_native(rs[:3], out)
         assert torch.equal(out, torch.stack(rs[:3]).amax(0))
+
+
+@pytest.mark.parametrize("C,include", [(0, True), (3, True), (16, True), (32, False)])
+def test_composite_views_other_channel_counts(C, include):
+    """The batched compositor launches of the other instantiations (VALU channel sums for C <= 16,
+    the no-language backward for C = 0 or include_feature off) against the per-view launches."""
+    sc, settings, grads = _setup(n_views=3, C=C)
+    settings = [s._replace(include_feature=include) for s in settings]
+    args = dict(shs=sc.shs, language_feature=sc.lang if C > 0 else None, scales=sc.scales, rotations=sc.rotations)
+    outs, gls, bwd = [], [], []
+    for batched in (False, True):
+        pfs = dgr.preprocess_views_native(settings, sc.means3D, sc.opacities, **args)
+        dgr.binning_views_native(pfs)
+        res = dgr.render_views_native(pfs) if batched else [dgr.render_native(pf) for pf in pfs]
+        gl = torch.zeros(sc.means3D.shape[0], C, device="cuda")
+        sts = [r[4] for r in res]
+        gcs = [g[0] for g in grads]
+        gll = [g[1] if C > 0 else None for g in grads]
+        if batched:
+            parts = dgr.backward_composite_views_native(sts, gcs, gll, dL_dlanguage=gl if C > 0 else None)
+        else:
+            parts = [dgr.backward_composite_native(st, a, b, None, dL_dlanguage=gl if C > 0 else None)
+                     for st, a, b in zip(sts, gcs, gll)]
+        b = GradBucket(sc.means3D.shape[0], sc.shs.shape[1], C, "cuda", densify_stats=True)
+        dgr.backward_preprocess_views_native(parts, out=b.views, accumulate=False, need=b.need())
+        torch.cuda.synchronize()
+        outs.append([(c.clone(), l.clone(), r.clone(), d.clone()) for c, l, r, d, _ in res])
+        gls.append(gl)
+        bwd.append(b.flat.clone())
+    for a, c in zip(outs[0], outs[1]):
+        for x, y in zip(a, c):
+            assert torch.equal(x, y)
+    scale = float(bwd[0].abs().max())
+    assert scale > 0 and float((bwd[0] - bwd[1]).abs().max()) <= 1e-5 * scale
+    if C > 0 and include:
+        s2 = float(gls[0].abs().max())
+        assert s2 > 0 and float((gls[0] - gls[1]).abs().max()) <= 1e-5 * s2
