@@ -572,6 +572,7 @@ __global__ void __launch_bounds__(1024) k_tile_order(int ntiles, TileOrderBatch 
     __shared__ uint32_t s_wave[16];
     const uint32_t* __restrict__ tile_max = tb.tile_max[blockIdx.x];
     uint32_t* __restrict__ order = tb.order[blockIdx.x];
+    if (!order || !tile_max) return;   // block-uniform: this view composites in tile order
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     s_cnt[tid] = 0;
     __syncthreads();
