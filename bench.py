@@ -351,6 +351,15 @@ def run(args):
                         limiter="valu-issue+atomics" if dom.startswith("render") else "hbm",
                         valu_issue_per_wave=pmc_rec.get("valu_issue_per_wave"),
                         mfma_busy_frac=pmc_rec.get("mfma_busy_frac"))
+        # whole-frame algorithmic bytes (SURVEY.md 8(d) formula with the measured K): every phase of a
+        # frame's fwd + bwd, each byte counted once, over the measured time per frame
+        fwd_b = P * 339 + Kmean * 216 + W * H * (4 * (3 + C + 1) + 8)
+        bwd_b = Kmean * 176 + W * H * (4 * (3 + C) + 8) + P * (44 + 4 * C) + P * 316 + P * 256
+        fb = fwd_b + bwd_b
+        frame_roof = dict(algorithmic_bytes_per_frame=int(fb), achieved=round(fb * value / 1e9, 1), peak=HBM_PEAK_GBS,
+                          unit="GB/s", frac=round(fb * value / 1e9 / HBM_PEAK_GBS, 4),
+                          formula="SURVEY.md 8(d): fwd P*339 + K*216 + Npix*(4(3+C+1)+8); bwd K*176 + "
+                                  "Npix*(4(3+C)+8) + P*(44+4C) + P*316 + P*256, K measured")
         cpu = None
         if not args.no_cpu_baseline:
             avail, host = host_cpu()
@@ -373,7 +382,7 @@ def run(args):
                         gaussians=P, width=W, height=H, channels=C, views_per_gpu_per_step=V,
                         global_batch=world * V, parallelism=f"dp{world}", pipeline="none" if args.no_overlap else args.pipeline, num_rendered_mean=int(Kmean),
                         visible=Pvis, visible_any_view=Pany, grad_bucket_mb=round(bucket.nbytes / 2**20, 1)),
-            roofline=roof, cpu_baseline=cpu, single_view=single,
+            roofline=roof, frame_roofline=frame_roof, cpu_baseline=cpu, single_view=single,
             phases={k: dict(mean_ms=round(v["mean_ms"], 4), gbs=round(v["gbs"], 1)) for k, v in phases.items()},
         )
         print(json.dumps(line))
