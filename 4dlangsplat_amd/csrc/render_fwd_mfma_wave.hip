@@ -73,6 +73,13 @@ __device__ unsigned long long g_fwd_stamps[8];
 #define FWD_STAMP(seg) do {} while (0)
 #endif
 
+// Diagnostic build only (-DLSR_FWD_COUNT): (entry, pixel) pairs the waves evaluate (inside the
+// image, entries of the group, while the wave runs) and the pairs that blend, summed into
+// g_fwd_count (lsr_debug_fwd_count): how much of the per-pair work contributes.
+#ifdef LSR_FWD_COUNT
+__device__ unsigned long long g_fwd_count[3];
+#endif
+
 #ifndef LSR_FWD_WAVES
 #define LSR_FWD_WAVES 4   // waves per SIMD the register budget targets (3: 0.293 ms, 4: 0.268 ms)
 #endif
@@ -119,6 +126,9 @@ k_render_fwd_wave_mfma(RenderFwdBatch ab) {
 #pragma unroll
         for (int nb = 0; nb < 4; ++nb) L[mb][nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     bool done = !inside;
+#ifdef LSR_FWD_COUNT
+    uint32_t c_eval = 0, c_act = 0;
+#endif
 
     uint32_t pos = range.x;  // list entries [pos, range.y) not yet scanned
     int head = 0, tail = 0;  // FIFO counters (wave-uniform)
@@ -185,6 +195,10 @@ k_render_fwd_wave_mfma(RenderFwdBatch ab) {
                     acc_rg = __builtin_elementwise_fma(s_RG[e], lsr_f2{w, w}, acc_rg);
                     acc_bd = __builtin_elementwise_fma(s_BD[e], lsr_f2{w, w}, acc_bd);
                     w8[u] = w;
+#ifdef LSR_FWD_COUNT
+                    c_eval += (inside && e < cnt) ? 1u : 0u;
+                    c_act += blend ? 1u : 0u;
+#endif
                     T = blend ? test_T : T;
                     last = blend ? s_k[e] : last;   // s_k holds the list position + 1
                 }
@@ -303,6 +317,21 @@ k_render_fwd_wave_mfma(RenderFwdBatch ab) {
             FWD_STAMP(4);
         }
     }
+#ifdef LSR_FWD_COUNT
+    {
+        unsigned long long ve = c_eval, va = c_act;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            ve += __shfl_xor(ve, off);
+            va += __shfl_xor(va, off);
+        }
+        if (lane == 0) {
+            atomicAdd(&g_fwd_count[0], ve);
+            atomicAdd(&g_fwd_count[1], va);
+            atomicAdd(&g_fwd_count[2], 1ull);
+        }
+    }
+#endif
 #ifdef LSR_FWD_STAMPS
     if (lane < 4) {
         unsigned long long v = 0;
@@ -382,6 +411,13 @@ void launch_render_fwd_wave_mfma_views(const RenderFwdArgs* a, int n, hipStream_
 
 }  // namespace lsr
 
+#ifdef LSR_FWD_COUNT
+extern "C" int lsr_debug_fwd_count(unsigned long long* out3) {
+    if (hipMemcpyFromSymbol(out3, HIP_SYMBOL(lsr::g_fwd_count), 3 * sizeof(unsigned long long)) != hipSuccess) return 2;
+    unsigned long long z[3] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(lsr::g_fwd_count), z, sizeof(z)) == hipSuccess ? 0 : 2;
+}
+#endif
 #ifdef LSR_FWD_STAMPS
 extern "C" int lsr_debug_fwd_stamps(unsigned long long* out5) {
     if (hipMemcpyFromSymbol(out5, HIP_SYMBOL(lsr::g_fwd_stamps), 5 * sizeof(unsigned long long)) != hipSuccess) return 2;
