@@ -361,7 +361,7 @@ def run(args):
                           formula="SURVEY.md 8(d): fwd P*339 + K*216 + Npix*(4(3+C+1)+8); bwd K*176 + "
                                   "Npix*(4(3+C)+8) + P*(44+4C) + P*316 + P*256, K measured")
         cpu = None
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:   # the contract's CPU leg: rank 0 at N = 1 only
             avail, host = host_cpu()
             threads = args.cpu_threads or avail
             nf = args.cpu_frames
