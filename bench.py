@@ -285,7 +285,7 @@ def run(args):
     value = frames / elapsed
 
     single = None
-    if args.single_view_steps > 0:
+    if args.single_view_steps > 0 and world == 1:   # configs[2] literally: one GPU
         # secondary figure: BASELINE configs[2] literally, one view at a time through the per-view
         # entry points (forward_native + backward_native, workspaces allocated per call), no batching
         v0 = dp.views[0]
