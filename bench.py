@@ -344,12 +344,18 @@ def run(args):
                     pmc_rec = {}
             # the HBM roofline is the contract's; the compositors are bound by VALU issue and atomics
             # (DESIGN.md 4), so the PMC VALU-issue share and matrix-core busy fraction ride along
+            # the compositors' VALU side: wave64 VALU instructions per launch (PMC SQ_INSTS_VALU) at
+            # the SIMD's peak rate of one per 2 cycles (MI355X_MICROARCH.md), 1024 SIMDs at 2.4 GHz
+            vi = pmc_rec.get("valu_insts_per_launch")
+            valu_frac = round(vi * 2 / (1024 * 2.4e9 * ms / n * 1e-3), 4) if vi else None
             roof = dict(kernel=dom, bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                         frac=round(ach / HBM_PEAK_GBS, 4), traffic=pmc_rec.get("hbm_bytes_per_launch"),
                         traffic_source="profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes)",
                         algorithmic_bytes=int(byts), mean_launch_ms=round(ms / n, 4),
-                        limiter="valu-issue+atomics" if dom.startswith("render") else "hbm",
-                        valu_issue_per_wave=pmc_rec.get("valu_issue_per_wave"),
+                        limiter=("latency+atomics (2 waves/SIMD; VALU instructions below the issue peak: "
+                                 "valu_issue_frac)") if dom == "render_bwd" else ("issue+latency" if dom == "render_fwd"
+                                                                                   else "hbm"),
+                        valu_issue_per_wave=pmc_rec.get("valu_issue_per_wave"), valu_issue_frac=valu_frac,
                         mfma_busy_frac=pmc_rec.get("mfma_busy_frac"))
         # whole-frame algorithmic bytes (SURVEY.md 8(d) formula with the measured K): every phase of a
         # frame's fwd + bwd, each byte counted once, over the measured time per frame

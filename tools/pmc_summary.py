@@ -83,6 +83,8 @@ def main(d, json_out=None):
                               dispatches=len(f["FETCH_SIZE"]))
             if "SQ_VALU_MFMA_BUSY_CYCLES" in f and "GRBM_GUI_ACTIVE" in f:
                 res[phase]["mfma_busy_frac"] = round(mfma_frac(f), 4)
+            if "SQ_INSTS_VALU" in f:   # wave-instructions per launch (each issues over 4 cycles on a SIMD)
+                res[phase]["valu_insts_per_launch"] = int(sum(f["SQ_INSTS_VALU"]) / len(f["SQ_INSTS_VALU"]))
             if "SQ_ACTIVE_INST_VALU" in f and "SQ_WAVE_CYCLES" in f:
                 # both count quad-cycles: the share of a resident wave's cycles that issue VALU
                 res[phase]["valu_issue_per_wave"] = round(sum(f["SQ_ACTIVE_INST_VALU"]) / max(sum(f["SQ_WAVE_CYCLES"]), 1), 4)
