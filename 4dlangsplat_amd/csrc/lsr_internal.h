@@ -431,8 +431,7 @@ struct RangesSeg {
 struct RangesBatch { RangesSeg s[LSR_MAX_VIEWS]; };
 void launch_tile_ranges(const RangesSeg* segs, int nseg, uint32_t ntiles, hipStream_t st);
 
-// compositing (render_fwd.hip / render_bwd.hip)
-void launch_render_fwd(const RenderFwdArgs& a, hipStream_t st);
+// compositing (render_fwd_wave.hip / render_bwd.hip)
 void launch_render_bwd(const RenderBwdArgs& a, hipStream_t st);
 void launch_render_fwd_wave_views(const RenderFwdArgs* a, int n, hipStream_t st);
 void launch_render_fwd_wave_mfma_views(const RenderFwdArgs* a, int n, hipStream_t st);   // 17..32 channels

@@ -1,7 +1,10 @@
 // render_fwd_wave.hip -- front-to-back compositing, one independent wave per 8x8 pixel quadrant.
 //
-// Same mathematics and per-pixel operation order as k_render_fwd (render_fwd.hip; upstream
-// renderCUDA).  About two thirds of a tile's list entries touch no pixel of
+// The compositor forward: upstream renderCUDA restated -- alpha <= 0.99,
+// skip alpha < 1/255, stop when T (1 - alpha) < 1e-4, RGB += T bg, language channels without
+// background, depth = sum z alpha T; per tile the largest n_contrib of its pixels (the backward's
+// replay bound).  Every channel count runs here: VALU sums for C <= 16 or > 32, and
+// render_fwd_mfma_wave.hip for 17..32 channels (sums on matrix cores).  About two thirds of a tile's list entries touch no pixel of
 // a given quadrant; an entry that no pixel of the quadrant blends leaves every pixel's T and
 // sums unchanged, and the contributor count upstream writes to n_contrib is the list position of
 // the last blended entry + 1, so skipping such entries is exact.  Each wave
@@ -213,6 +216,17 @@ void launch_render_fwd_wave_views(const RenderFwdArgs* a, int n, hipStream_t st)
         case 16: go_fwd_wave<16>(ab, n, st); break;
         default: go_fwd_wave<64>(ab, n, st); break;
     }
+}
+
+// the entry point of every forward composite: the forward takes no cost order, so
+// the tile-order scratch is not written
+void launch_render_fwd_views(const RenderFwdArgs* a, int n, hipStream_t st) {
+    RenderFwdArgs f[LSR_MAX_VIEWS];
+    for (int v = 0; v < n; ++v) {
+        f[v] = a[v];
+        f[v].tile_order = nullptr;
+    }
+    launch_render_fwd_wave_views(f, n, st);
 }
 
 }  // namespace lsr

@@ -125,14 +125,15 @@ class DeformationField:
             if tuple(self.p[k].shape) != shape:
                 raise ValueError(f"{k}: shape {tuple(self.p[k].shape)}, the configuration needs {shape}")
 
-    def _net(self, lang_mode):
+    def _net(self, lang_mode, coff_head: Optional[bool] = None):
+        coff_head = self.discrete if coff_head is None else coff_head
         n = _lib.DeformNet()
         n.n_scales, n.channels, n.width = len(self.multires), 16, 128
         for i in range(4):
             n.res[i] = int(self.resolution[i])
             n.multires[i] = int(self.multires[i]) if i < len(self.multires) else 1
         n.depth = self.depth
-        n.heads = sum(1 << h for h, on in enumerate(self.head_on) if on) | (32 if self.discrete else 0)
+        n.heads = sum(1 << h for h, on in enumerate(self.head_on) if on) | (32 if coff_head else 0)
         n.apply_rotation = int(self.apply_rotation)
         n.lang_mode, n.lang_dim, n.centers, n.time_pe = lang_mode, self.lang_dim, self.centers, self.time_pe
         n.aabb = self.p["grid.aabb"].data_ptr()
@@ -154,10 +155,16 @@ class DeformationField:
 
     def _call_net(self, no_dlang: Optional[bool]):
         """The net of one call: the reference's render() forces no_dlang = 1 in the 'base' stages
-        (gaussian_renderer/__init__.py:121-124); the discrete branch is taken regardless
-        (scene/deformation.py:156)."""
+        (gaussian_renderer/__init__.py:121-124).  The reference's discrete branch
+        (scene/deformation.py:156) runs regardless, on the zeros [P, language_feature_hiddendim] that
+        render() passes there: it slices and views them as centres and normalises zero vectors
+        (0/0, NaN language) and computes a coff that train.py collects but never uses (train.py:240-247).
+        Here a discrete field in a 'base' call runs without its coff head and passes the language
+        through, as the PASS mode does: coff is None and the (unused) language is the input."""
         if no_dlang and self.lang_mode in (LANG_RESIDUAL, LANG_NORESNET):
             return self._net(LANG_PASS)
+        if no_dlang and self.discrete:
+            return self._net(LANG_PASS, coff_head=False)
         return self.net
 
     # ---- construction from the reference ----------------------------------------------------------
@@ -275,6 +282,16 @@ class DeformationField:
                     no_do=not self.head_on[3], no_dshs=not self.head_on[4], apply_rotation=self.apply_rotation,
                     no_dlang=int(self.lang_mode == LANG_PASS), timebase_pe=self.time_pe)
 
+    def env_params(self) -> Dict[str, str]:
+        """The environment switches that select this field's language mode (config_from_reference's
+        `env`): language_feature_hiddendim, use_discrete_lang_f, centers_num, no_resnet."""
+        env = {"language_feature_hiddendim": str(self.lang_dim),
+               "use_discrete_lang_f": "t" if self.lang_mode == LANG_DISCRETE else "f",
+               "no_resnet": "t" if self.lang_mode == LANG_NORESNET else "f"}
+        if self.lang_mode == LANG_DISCRETE:
+            env["centers_num"] = str(self.centers)
+        return env
+
     @classmethod
     def from_reference_state_dict(cls, state_dict, resolution, multires, prefix="deformation_net.", device="cuda"):
         """The Neu3D structure (arguments/neu3d/default.py): defor_depth 0, every head, language
@@ -313,7 +330,7 @@ class DeformationField:
             outs[2] = torch.empty_like(ins[2])
         lang_in = f(lang, (P, self.lang_in)) if lang is not None and net.lang_mode != LANG_PASS else None
         out_lang = torch.empty(P, self.lang_dim, device=self.device) if net.lang_mode != LANG_PASS else None
-        out_coff = torch.empty(P, self.centers, device=self.device) if self.discrete else None
+        out_coff = torch.empty(P, self.centers, device=self.device) if net.lang_mode == LANG_DISCRETE else None
         if net.lang_mode != LANG_PASS and lang_in is None:
             raise ValueError("this field deforms the language feature: lang is required")
         vp = lambda x: ctypes.c_void_p(x.data_ptr() if x is not None else 0)   # noqa: E731
@@ -384,7 +401,7 @@ class DeformationField:
             self._scratch = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
         vp = lambda x: ctypes.c_void_p(x.data_ptr() if x is not None else 0)   # noqa: E731
         _lib.check(L.lsr_deform_backward(ctypes.byref(net), vp(self.workspace), P, vp(m), vp(rot), vp(lang_in), vp(t),
-                                         *[vp(u) for u in ups], vp(dl_up), vp(f(d_coff, (P, self.centers))), vp(dm),
+                                         *[vp(u) for u in ups], vp(dl_up), vp(f(d_coff, (P, self.centers)) if net.lang_mode == LANG_DISCRETE else None), vp(dm),
                                          vp(drot), vp(dlang), ctypes.byref(g), vp(self._scratch),
                                          ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)),
                    "lsr_deform_backward")
@@ -396,8 +413,9 @@ class DeformationField:
         if net.lang_mode == LANG_PASS:
             if dl_up is None:
                 dlang = None
-            else:
-                dlang = torch.zeros(P, self.lang_in, device=self.device)
+            else:   # the input's width: lang_in, or lang_dim when a 'base' call passes zeros [P, lang_dim]
+                width = lang.reshape(P, -1).shape[1] if lang is not None else self.lang_in
+                dlang = torch.zeros(P, width, device=self.device)
                 dlang[:, :self.lang_dim] = dl_up
         return tuple(d_in) + (dlang,)
 
@@ -407,7 +425,7 @@ class DeformationField:
         if lang is None:
             lang = torch.zeros(means3D.shape[0], self.lang_in, device=self.device)
         outs = _DeformFunction.apply(self, time, no_dlang, means3D, scales, rotations, opacity, shs, lang)
-        coff = outs[6] if self.discrete else None
+        coff = outs[6] if (self.discrete and outs[6].numel() > 0) else None
         return tuple(outs[:6]) + (coff,)
 
 
@@ -428,5 +446,6 @@ class _DeformFunction(torch.autograd.Function):
         means3D, rotations, lang = ctx.saved_tensors
         f = ctx.field
         grads = f.backward(means3D, ctx.time, dm, ds, dr, do, dsh, rotations=rotations, lang=lang, d_lang=dl,
-                           d_coff=dc if f.discrete else None, no_dlang=ctx.no_dlang)
+                           d_coff=dc if (f.discrete and dc is not None and dc.numel() > 0) else None,
+                           no_dlang=ctx.no_dlang)
         return (None, None, None) + tuple(grads)

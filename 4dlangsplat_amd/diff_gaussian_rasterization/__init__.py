@@ -36,7 +36,6 @@ __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gau
 
 _lib.load()   # fail loudly at import if the native library is missing
 _BINNING_DELAY_CYCLES = 0   # tests only: GPU cycles slept on the stream before a side-stream binning
-_SPLIT_BEHIND_COUNTS = True  # preprocess_views_native: language split after the count event (A/B switch)
 
 
 class GaussianRasterizationSettings(NamedTuple):
@@ -273,7 +272,7 @@ def language_split_native(language_feature, stream=None, out=None):
 
 def preprocess_views_native(raster_settings_list, means3D, opacities, shs=None, colors_precomp=None,
                             language_feature=None, scales=None, rotations=None, cov3D_precomp=None, stream=None,
-                            split_language=True):
+                            split_language=True, split_behind_counts=True):
     """Forward phase 1 of several views of the same Gaussians as one batch
     (lsr_forward_preprocess_views_async: one preprocess launch per 8 views reads each Gaussian once,
     the views' depth sorts and instance scans share their launches) on `stream`.  No host
@@ -282,7 +281,8 @@ def preprocess_views_native(raster_settings_list, means3D, opacities, shs=None, 
 
     split_language (C == 32): the language rows' bf16 hi / lo operands are made once here for all
     the batch's views (lsr_language_split) instead of per entry in every compositor wave (same
-    bits, same results)."""
+    bits, same results).  split_behind_counts: enqueue that split behind the batch's count event, so
+    it runs while the host waits for the counts (False: ahead of the preprocess; an A/B switch)."""
     device = _check_device(means3D)
     L = _lib.load()
     stream = stream or torch.cuda.current_stream(device)
@@ -293,7 +293,7 @@ def preprocess_views_native(raster_settings_list, means3D, opacities, shs=None, 
         with torch.cuda.stream(stream):
             inputs["language_feature_split"] = torch.empty(P, 64, dtype=torch.int16, device=device)
         fin.language_feature_split = inputs["language_feature_split"].data_ptr()
-        if not _SPLIT_BEHIND_COUNTS:
+        if not split_behind_counts:
             language_split_native(inputs["language_feature"], stream=stream, out=inputs["language_feature_split"])
             split = False
     n = len(raster_settings_list)

@@ -166,12 +166,39 @@ def read_model_dir(model_path: str, load_iteration: int = -1, load_stage: str = 
     return scene, state, it
 
 
-def load_model_dir(model_path: str, hidden, env=None, load_iteration: int = -1, load_stage: str = "fine-lang",
+DEFORM_CONFIG = "deformation_config.json"   # this build's sidecar next to deformation.pth
+
+
+def load_model_dir(model_path: str, hidden=None, env=None, load_iteration: int = -1, load_stage: str = "fine-lang",
                    max_sh_degree: int = 3, device="cuda"):
     """read_model_dir + the deformation field on the GPU (DeformationField.from_reference with the
-    ModelHiddenParams and env the model was trained with).  Returns (scene, iteration)."""
+    ModelHiddenParams and env the model was trained with).  Returns (scene, iteration).
+
+    The reference keeps the language mode in environment variables (no_dlang aside), which a
+    deformation.pth does not record: a model directory written by save_model_dir carries them in
+    `deformation_config.json` ({"hidden": ..., "env": ...}), which fills `hidden` / `env` when they are
+    None, and an explicit `env` whose language mode contradicts it raises.  Without the sidecar (a
+    directory the reference wrote) `hidden` is required and `env` defaults to os.environ."""
+    import json
+
     from deformation import DeformationField
     scene, state, it = read_model_dir(model_path, load_iteration, load_stage, max_sh_degree, device="cpu")
+    side = os.path.join(model_path, "point_cloud", f"{load_stage}_iteration_{it}", DEFORM_CONFIG)
+    if os.path.exists(side):
+        with open(side) as f:
+            rec = json.load(f)
+        if hidden is None:
+            hidden = rec["hidden"]
+        if env is None:
+            env = rec["env"]
+        else:
+            for k, v in rec["env"].items():
+                default = {"use_discrete_lang_f": "f", "no_resnet": "f", "language_feature_hiddendim": "3",
+                           "centers_num": "3"}[k]
+                if str(env.get(k, default)) != v:
+                    raise ValueError(f"env {k}={env.get(k, default)!r} contradicts the model's {DEFORM_CONFIG} ({v!r})")
+    elif hidden is None:
+        raise ValueError(f"{model_path}: no {DEFORM_CONFIG}; pass the ModelHiddenParams the model was trained with")
     scene = scene.to(device)
     scene.deformation = DeformationField.from_reference(state, hidden, env=env, device=device)
     return scene, it
@@ -179,12 +206,17 @@ def load_model_dir(model_path: str, hidden, env=None, load_iteration: int = -1, 
 
 def save_model_dir(scene: "GaussianScene", model_path: str, iteration: int, stage: str) -> str:
     """Scene.save (scene/__init__.py:98-101): point_cloud.ply + deformation.pth (+ the table and
-    accumulator when the scene carries them) under model_path/point_cloud/{stage}_iteration_{N}."""
+    accumulator when the scene carries them) under model_path/point_cloud/{stage}_iteration_{N},
+    plus deformation_config.json (the field's ModelHiddenParams and language-mode env switches,
+    which the reference keeps outside the checkpoint; load_model_dir reads it back)."""
     d = os.path.join(model_path, "point_cloud", f"{stage}_iteration_{iteration}")
     os.makedirs(d, exist_ok=True)
     scene.save_ply(os.path.join(d, "point_cloud.ply"))
     if scene.deformation is not None:
+        import json
         torch.save({k: v.cpu() for k, v in scene.deformation.state_dict().items()}, os.path.join(d, "deformation.pth"))
+        with open(os.path.join(d, DEFORM_CONFIG), "w") as f:
+            json.dump({"hidden": scene.deformation.hidden_params(), "env": scene.deformation.env_params()}, f)
     for k in ("deformation_table", "deformation_accum"):
         if k in scene.extra:
             torch.save(torch.as_tensor(scene.extra[k]).cpu(), os.path.join(d, f"{k}.pth"))
@@ -253,12 +285,22 @@ def read_ply_vertices(path: str) -> Dict[str, np.ndarray]:
 def render(viewpoint_camera, pc: GaussianScene, bg_color: torch.Tensor, scaling_modifier: float = 1.0,
            override_color=None, stage: str = "fine-lang", compute_cov3D_python: bool = False,
            convert_SHs_python: bool = False, debug: bool = False, nonormalized: bool = False,
-           language_feature_hiddendim: int = 3, _deformed=None):
+           language_feature_hiddendim: int = 3, cam_type: Optional[str] = None, _deformed=None):
     """The reference's render() on this build's rasterizer.  viewpoint_camera: FoVx, FoVy,
     image_width, image_height, world_view_transform, full_proj_transform, camera_center, time
-    (synthetic.Camera or the reference Camera).  Environment switches of the reference
+    (synthetic.Camera or the reference Camera); with cam_type == "PanopticSports" a dict
+    {"camera": GaussianRasterizationSettings, "time": t} as the Panoptic reader builds it
+    (scene/dataset_readers.py:491-516, `panoptic_camera` here), whose settings are used as they are
+    (gaussian_renderer/__init__.py:46, 74-76).  Environment switches of the reference
     (nonormalized, language_feature_hiddendim) are arguments here.  _deformed: this view's
-    deformation outputs, already evaluated (render_views); the field is then not called."""
+    deformation outputs, already evaluated (render_views); the field is then not called.
+
+    One deliberate divergence: with override_color (or convert_SHs_python) the reference passes
+    both shs_final and colors_precomp to the rasterizer (gaussian_renderer/__init__.py:219-228),
+    and the upstream GaussianRasterizer raises "Please provide excatly one of either SHs or
+    precomputed colors!" on that, so the reference's override path cannot run.  Here the SHs are
+    dropped when colours are precomputed, so the path renders the given colours; the rasterizer
+    itself (GaussianRasterizer.forward) keeps upstream's error for callers that pass both."""
     from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
 
     dev = pc.xyz.device
@@ -269,16 +311,23 @@ def render(viewpoint_camera, pc: GaussianScene, bg_color: torch.Tensor, scaling_
         pass
     means3D = pc.get_xyz
     include_feature = "base" not in stage
-    raster_settings = GaussianRasterizationSettings(
-        image_height=int(viewpoint_camera.image_height), image_width=int(viewpoint_camera.image_width),
-        tanfovx=math.tan(viewpoint_camera.FoVx * 0.5), tanfovy=math.tan(viewpoint_camera.FoVy * 0.5),
-        bg=bg_color, scale_modifier=scaling_modifier, viewmatrix=viewpoint_camera.world_view_transform.to(dev),
-        projmatrix=viewpoint_camera.full_proj_transform.to(dev), sh_degree=pc.active_sh_degree,
-        campos=viewpoint_camera.camera_center.to(dev), prefiltered=False, debug=debug,
-        include_feature=include_feature)
+    if cam_type != "PanopticSports":
+        raster_settings = GaussianRasterizationSettings(
+            image_height=int(viewpoint_camera.image_height), image_width=int(viewpoint_camera.image_width),
+            tanfovx=math.tan(viewpoint_camera.FoVx * 0.5), tanfovy=math.tan(viewpoint_camera.FoVy * 0.5),
+            bg=bg_color, scale_modifier=scaling_modifier, viewmatrix=viewpoint_camera.world_view_transform.to(dev),
+            projmatrix=viewpoint_camera.full_proj_transform.to(dev), sh_degree=pc.active_sh_degree,
+            campos=viewpoint_camera.camera_center.to(dev), prefiltered=False, debug=debug,
+            include_feature=include_feature)
+        cam_time = viewpoint_camera.time
+    else:
+        # the Panoptic reader's prebuilt settings, taken as they are (their include_feature, bg and
+        # sh_degree included), and the frame time from the dict
+        raster_settings = viewpoint_camera["camera"]
+        cam_time = viewpoint_camera["time"]
     # the reference builds this with torch.tensor(time).to(device).repeat (a host-to-device copy,
     # which synchronises the stream): a fill gives the same values without the wait
-    t = torch.full((means3D.shape[0], 1), float(viewpoint_camera.time), device=dev)
+    t = torch.full((means3D.shape[0], 1), float(cam_time), device=dev)
     rasterizer = GaussianRasterizer(raster_settings=raster_settings)
     opacity = pc.opacity
     shs = pc.get_features
@@ -321,7 +370,9 @@ def render(viewpoint_camera, pc: GaussianScene, bg_color: torch.Tensor, scaling_
     elif convert_SHs_python:
         # as the reference (gaussian_renderer/__init__.py:200-205): undeformed means and features
         shs_view = pc.get_features.transpose(1, 2).view(-1, 3, (pc.max_sh_degree + 1) ** 2)
-        dir_pp = pc.get_xyz - viewpoint_camera.camera_center.to(dev).repeat(pc.P, 1)
+        campos = raster_settings.campos.to(dev).reshape(1, 3) if cam_type == "PanopticSports" \
+            else viewpoint_camera.camera_center.to(dev)
+        dir_pp = pc.get_xyz - campos.repeat(pc.P, 1)
         dirs = dir_pp / dir_pp.norm(dim=1, keepdim=True)
         colors_precomp = torch.clamp_min(eval_sh(pc.active_sh_degree, shs_view, dirs) + 0.5, 0.0)
     image, lang_img, radii, depth = rasterizer(
@@ -366,6 +417,27 @@ def render_views(cams: Sequence, pc: GaussianScene, bg_color: torch.Tensor, stag
                    language_feature_hiddendim=language_feature_hiddendim,
                    _deformed=tuple(p[v] for p in parts), **kw) for v, c in enumerate(cams)]
 
+
+def panoptic_camera(w: int, h: int, k, w2c, time: float, near: float = 0.01, far: float = 100.0,
+                    device="cuda") -> dict:
+    """The Panoptic Sports reader's camera (scene/dataset_readers.py:491-516 setup_camera): raster
+    settings built from intrinsics k [3,3] and world-to-camera w2c [4,4] (OpenGL-style projection,
+    black background, sh_degree 0, debug on), with the frame time, as render(cam_type="PanopticSports")
+    takes it."""
+    from diff_gaussian_rasterization import GaussianRasterizationSettings
+    fx, fy, cx, cy = k[0][0], k[1][1], k[0][2], k[1][2]
+    w2c = torch.as_tensor(w2c, dtype=torch.float32, device=device)
+    cam_center = torch.inverse(w2c)[:3, 3]
+    w2c = w2c.unsqueeze(0).transpose(1, 2)
+    opengl_proj = torch.tensor([[2 * fx / w, 0.0, -(w - 2 * cx) / w, 0.0],
+                                [0.0, 2 * fy / h, -(h - 2 * cy) / h, 0.0],
+                                [0.0, 0.0, far / (far - near), -(far * near) / (far - near)],
+                                [0.0, 0.0, 1.0, 0.0]], dtype=torch.float32, device=device).unsqueeze(0).transpose(1, 2)
+    settings = GaussianRasterizationSettings(
+        image_height=h, image_width=w, tanfovx=w / (2 * fx), tanfovy=h / (2 * fy),
+        bg=torch.zeros(3, dtype=torch.float32, device=device), scale_modifier=1.0, viewmatrix=w2c,
+        projmatrix=w2c.bmm(opengl_proj), sh_degree=0, campos=cam_center, prefiltered=False, debug=True)
+    return {"camera": settings, "time": time}
 
 _SH_C0 = 0.28209479177387814
 _SH_C1 = 0.4886025119029199

@@ -228,7 +228,7 @@ class ViewParallelStep:
 
 def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool = False, overlap: bool = True,
                          batch_backward: bool = True, early_views: int = 3, composite_batch: bool = True,
-                         side_priority: int = 0, side_from_preprocess: bool = True):
+                         side_priority: int = 0, side_from_preprocess: bool = True, split_behind_counts: bool = True):
     """render_view callback for ViewParallelStep on the HIP rasterizer (the product path).
 
     scene    : object with means3D, opacities, shs, lang, scales, rotations device tensors
@@ -304,7 +304,7 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
         views = [w for w in views if has_view(w)] or [v]
         pfs = dgr.preprocess_views_native([settings[w] for w in views], scene.means3D, scene.opacities,
                                           shs=scene.shs, language_feature=scene.lang, scales=scene.scales,
-                                          rotations=scene.rotations)
+                                          rotations=scene.rotations, split_behind_counts=split_behind_counts)
         if before_wait is not None:
             before_wait()
         if radii_out is not None:     # the views' radii MAX, also while the host waits for the counts

@@ -214,7 +214,8 @@ def run(args):
                                   overlap=False if args.no_overlap else (True if args.pipeline == "side"
                                                                          else args.pipeline),
                                   early_views=args.early_views, composite_batch=not args.per_view_composite,
-                                  side_priority=args.side_priority, side_from_preprocess=not args.side_after_binning)
+                                  side_priority=args.side_priority, side_from_preprocess=not args.side_after_binning,
+                                  split_behind_counts=not args.no_wait_fill)
     Ks = []
 
     def render_view(v, b):
@@ -230,8 +231,6 @@ def run(args):
             render_batch.radii_reduced = render.render_batch.radii_reduced
             return r
         render_batch.before_wait = not args.no_wait_fill
-        if args.no_wait_fill:
-            dgr._SPLIT_BEHIND_COUNTS = False
         render_view.render_batch = render_batch
     if hasattr(render, "flush"):                           # batched backward of the step's views
         render_view.flush = render.flush

@@ -237,7 +237,6 @@ int lsr_backward_preprocess_views_rows(int32_t n_views, const lsr_settings *cons
                                        lsr_bwd_out *gout, const void *const *geom, int32_t accumulate,
                                        int32_t row_begin, int32_t row_count, lsr_stream_t stream);
 
-/* markVisible: present[i] = (view-space z of means3D[i]) > 0.2 */
 /* language_feature [P,C] fp32 -> out [P,2C] bf16 bit patterns (hi channels then lo channels) for
  * lsr_fwd_in.language_feature_split.  C must be 32.  No reference counterpart (an MI355X operand
  * layout); on the caller's stream. */
@@ -250,6 +249,7 @@ int lsr_language_split(int32_t P, int32_t C, const float *language_feature, uint
 int lsr_radii_max(int32_t P, int32_t n_views, const int32_t *const *radii, int32_t *out, int32_t accumulate,
                   lsr_stream_t stream);
 
+/* markVisible: present[i] = (view-space z of means3D[i]) > 0.2 */
 int lsr_mark_visible(int32_t P, const float *means3D, const float *viewmatrix, const float *projmatrix,
                      uint8_t *present, lsr_stream_t stream);
 

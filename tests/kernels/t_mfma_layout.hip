@@ -1,5 +1,5 @@
 // Test program (tests/test_kernels_gpu.py): exact-integer check of the v_mfma_f32_32x32x16_bf16
-// operand/result lane maps used by the compositor (render_fwd.hip / render_bwd.hip):
+// operand/result lane maps used by the compositors (render_fwd_mfma_wave.hip / render_bwd_wave.hip):
 //   A: lane l holds A[row l&31][k = 8(l>>5) + j], j = 0..7
 //   B: lane l holds B[k = 8(l>>5) + j][col l&31]
 //   D: lane l, register r holds D[row (r&3) + 8(r>>2) + 4(l>>5)][col l&31]

@@ -291,6 +291,45 @@ def test_variant_apply_autograd():
             assert _rel(x.grad.cpu().numpy(), r.cpu().numpy().reshape(x.shape)) < 1e-6, (name, k)
 
 
+
+def test_discrete_field_in_a_base_stage():
+    """A discrete-language field called as render() calls it in the 'base' stages (no_dlang forced,
+    zeros [P, language_feature_hiddendim] as the language; gaussian_renderer/__init__.py:99,121-124):
+    the geometry heads are those of the full call, the language passes through, coff is None, and
+    the autograd backward runs with finite gradients equal to the full call's under a zero language /
+    coff upstream."""
+    f, cfg, d = _variant_field("discrete")
+    P = d["means3D"].shape[0]
+    xs = [torch.tensor(d[k]).cuda() for k in ("means3D", "scales", "rotations", "opacity", "shs")]
+    t = torch.tensor(d["time"][:, 0]).cuda()
+    zeros = torch.zeros(P, f.lang_dim, device="cuda")
+    base = f.forward(*xs, zeros, t, no_dlang=True)
+    full = f.forward(*xs, torch.tensor(d["lang"]).cuda(), t)
+    for k in range(5):
+        assert torch.equal(base[k], full[k]), k
+    assert base[6] is None and torch.equal(base[5], zeros)
+    xg = [x.clone().requires_grad_(True) for x in xs]
+    outs = f.apply(*xg, zeros, t, no_dlang=True)
+    assert outs[6] is None
+    f.zero_grad()
+    sum((o * torch.tensor(d["up_" + k]).cuda()).sum()
+        for o, k in zip(outs[:5], ("means3D", "scales", "rotations", "opacity", "shs"))).backward()
+    grads_base = {k: v.clone() for k, v in f.grads.items()}
+    ref = lambda k: torch.tensor(d[k]).cuda()   # noqa: E731
+    f.zero_grad()
+    full_g = f.backward(ref("means3D"), t, ref("up_means3D"), ref("up_scales"), ref("up_rotations"),
+                        ref("up_opacity"), ref("up_shs"), rotations=ref("rotations"), lang=ref("lang"),
+                        d_lang=torch.zeros(P, f.lang_dim, device="cuda"), d_coff=torch.zeros(P, f.centers, device="cuda"))
+    for x, r, k in zip(xg, full_g, ("means3D", "scales", "rotations", "opacity", "shs")):
+        assert torch.isfinite(x.grad).all(), k
+        assert _rel(x.grad.cpu().numpy(), r.cpu().numpy().reshape(x.shape)) < 1e-5, k
+    for k, v in f.grads.items():
+        if k.startswith("discrete_coff_generator"):
+            assert float(grads_base[k].abs().max()) == 0.0, k
+        else:
+            assert torch.isfinite(grads_base[k]).all(), k
+            assert _rel(grads_base[k].cpu().numpy(), v.cpu().numpy()) < 1e-5, k
+
 def test_from_reference_is_strict():
     """deform_network.state_dict() + ModelHiddenParams + env: the unused modules the reference always
     builds are skipped; a key the configuration does not compute raises (a defor_depth 2 state dict

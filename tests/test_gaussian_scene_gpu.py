@@ -92,6 +92,39 @@ def test_fine_stage_applies_the_deformation_field():
     assert not torch.equal(out["render"], gs.render(cam, s, torch.ones(3, device="cuda"), stage="coarse-lang")["render"])
 
 
+
+def test_panoptic_dict_camera():
+    """cam_type == "PanopticSports" (gaussian_renderer/__init__.py:46, 74-76): the dict camera's
+    prebuilt settings (dataset_readers.py:491-516 setup_camera) are used as they are and its time
+    drives the deformation field."""
+    import test_deform_gpu as td
+    P = 2000
+    params, res, multires, _ = td._neu3d_case(P)
+    field = DeformationField({k: torch.tensor(v, dtype=torch.float32) for k, v in params.items()}, res, multires,
+                             device="cuda")
+    s = _scene(P=P)
+    s.deformation = field
+    fx = W / (2 * 0.6)
+    k = [[fx, 0.0, W / 2], [0.0, fx, H / 2], [0.0, 0.0, 1.0]]
+    w2c = np.eye(4, dtype=np.float32)
+    w2c[:3, 3] = [0.1, -0.05, 0.3]
+    cam = gs.panoptic_camera(W, H, k, w2c, 0.7)
+    rs = cam["camera"]
+    assert rs.sh_degree == 0 and rs.include_feature and float(rs.bg.abs().sum()) == 0.0
+    out = gs.render(cam, s, torch.ones(3, device="cuda"), stage="fine-lang", cam_type="PanopticSports")
+    t = torch.full((P, 1), 0.7, device="cuda")
+    lang = s.language_feature / (s.language_feature.norm(dim=-1, keepdim=True) + 1e-9)
+    m, sc, r, o, sh, l, _ = field(s.xyz, s.scaling, s.rotation, s.opacity, s.get_features, lang, t)
+    color, lang_img, radii, *_ = dgr.forward_native(rs, m, torch.sigmoid(o), shs=sh, language_feature=l,
+                                                    scales=torch.exp(sc), rotations=torch.nn.functional.normalize(r))
+    assert int((radii > 0).sum()) > 100
+    assert torch.equal(out["render"], color) and torch.equal(out["language_feature_image"], lang_img)
+    assert torch.equal(out["radii"], radii)
+    # the dict's time, not a camera attribute, reaches the field
+    cam2 = dict(cam, time=0.1)
+    assert not torch.equal(gs.render(cam2, s, torch.ones(3, device="cuda"), stage="fine-lang",
+                                     cam_type="PanopticSports")["render"], out["render"])
+
 def test_render_set_writes_eval_inputs(tmp_path):
     s = _scene(C=6)
     views = [_cam(t) for t in (0.0, 0.5, 1.0)]
@@ -131,3 +164,26 @@ def test_model_directory_load_and_render(tmp_path):
         assert torch.equal(a["radii"], b["radii"]), stage
     assert not torch.equal(gs.render(_cam(0.6), m, bg, stage="fine-lang")["render"],
                            gs.render(_cam(0.6), m, bg, stage="coarse-lang")["render"])
+
+
+def test_model_directory_records_the_language_mode(tmp_path):
+    """The reference selects lang_deform's residual / no_resnet / discrete modes by environment
+    variables that deformation.pth does not record; save_model_dir writes them next to it
+    (deformation_config.json) and load_model_dir restores the same mode without env, and refuses an
+    env that contradicts it (a NORESNET field must not reload as RESIDUAL with the same weights)."""
+    from deformation import LANG_NORESNET, LANG_RESIDUAL
+    P = 1500
+    s = _scene(P=P, C=3)
+    aabb = torch.stack([s.xyz.max(0).values, s.xyz.min(0).values]).cpu()
+    params = DeformationField.init_params([12, 10, 9, 7], [1, 2], aabb, seed=3, lang_mode=LANG_NORESNET, lang_dim=3)
+    s.deformation = DeformationField(params, [12, 10, 9, 7], [1, 2], lang_mode=LANG_NORESNET, lang_dim=3,
+                                     device="cuda")
+    gs.save_model_dir(s, str(tmp_path), 100, "fine-lang")
+    m, it = gs.load_model_dir(str(tmp_path))
+    assert it == 100 and m.deformation.lang_mode == LANG_NORESNET
+    bg = torch.ones(3, device="cuda")
+    a, b = gs.render(_cam(0.3), s, bg, stage="fine-lang"), gs.render(_cam(0.3), m, bg, stage="fine-lang")
+    assert torch.equal(a["language_feature_image"], b["language_feature_image"])
+    with pytest.raises(ValueError, match="no_resnet"):
+        gs.load_model_dir(str(tmp_path), env={})
+    assert LANG_RESIDUAL != LANG_NORESNET

@@ -170,3 +170,94 @@ def test_render_views_matches_per_view_render():
         scale = float(a["f"][k].abs().max())
         err = float((b["f"][k] - a["f"][k]).abs().max())
         assert err <= 1e-4 * scale + 1e-12, (k, err, scale)
+
+
+def test_configs4_standin_at_size():
+    """BASELINE configs[4] at its stand-in size (tools/bench_train_loop.py): 100k
+    Gaussians from create_from_pcd + distCUDA2, 2 views of 1352 x 1014 per iteration, the Neu3D field
+    (64^3 x 150, multires [1, 2]), ReferenceSchedule with the Neu3D overrides, fine-base, 700
+    iterations so the first densify (iteration 600, train.py:388-414 / arguments/neu3d/default.py:24-33)
+    fires.  Checks: the window losses fall up to the densify and stay below the first window after it;
+    densify events land on the reference iterations; the statistics track P; everything stays finite.
+    At iteration 650 one view's rasterizer call is checked against the C oracle: the Gaussian gradients
+    the training step's backward produced (inside autograd, on the training inputs) against the
+    oracle's backward on the same inputs and upstream gradient."""
+    import importlib.util
+    import os
+
+    import diff_gaussian_rasterization as dgr
+    import oracle
+    from lsr_testutil import grad_err
+
+    spec = importlib.util.spec_from_file_location(
+        "bench_train_loop", os.path.join(os.path.dirname(__file__), "..", "tools", "bench_train_loop.py"))
+    btl = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(btl)
+    args = type("A", (), dict(gaussians=100_000, width=1352, height=1014, cameras=8, frames=4, point_noise=0.02,
+                              densify_until_iter=10_000))()
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    step, sched, pool, gts, extent = btl.build(args, dev)
+    P0 = step.trainer.P
+    assert P0 == 100_000 and tuple(gts.shape) == (32, 3, 1014, 1352)
+    order = torch.Generator().manual_seed(5)
+    captured = []
+    real_backward = dgr.backward_native
+
+    def capture(state, grad_color, *a, **kw):     # one view of one iteration: inputs, upstream grad, result
+        g = real_backward(state, grad_color, *a, **kw)
+        captured.append((state.settings, {k: (None if v is None else v.detach().cpu()) for k, v in state.inputs.items()},
+                         grad_color.detach().cpu(), {k: (None if v is None else v.detach().cpu()) for k, v in g.items()}))
+        return g
+
+    windows, acc, iters, window = [], torch.zeros((), device=dev), 700, 100
+    for it in range(1, iters + 1):
+        idx = torch.randperm(len(pool), generator=order)[:2].tolist()
+        if it == 650:
+            dgr.backward_native = capture
+        try:
+            acc += step([pool[i] for i in idx], gts[idx], iteration=it)
+        finally:
+            dgr.backward_native = real_backward
+        if it == 650:
+            cams650 = [pool[i] for i in idx]
+        if it % window == 0:
+            windows.append(float(acc) / window)
+            acc.zero_()
+    torch.cuda.synchronize()
+    tr = step.trainer
+    assert all(math.isfinite(w) for w in windows), windows
+    # falls window over window up to the densify at 600; the densify moves the image (clone / split),
+    # after which the window stays well below the first
+    assert all(b < a for a, b in zip(windows[:6], windows[1:6])), windows
+    assert windows[6] < 0.5 * windows[0], windows
+    ev = [(e[0], e[1]) for e in sched.events]
+    assert ev and ev[0] == (600, "densify") and all(e[0] % 100 == 0 and e[0] > 500 for e in ev), sched.events
+    assert sched.events[0][2] == P0 and tr.P == sched.events[-1][3] > P0
+    assert tr.denom.shape[0] == tr.P and tr.xyz_gradient_accum.shape[0] == tr.P and tr.max_radii2D.shape[0] == tr.P
+    for k, v in tr.params.items():
+        assert torch.isfinite(v).all(), k
+    for k, v in step.field.p.items():
+        assert torch.isfinite(v).all(), k
+    # the oracle check on one of iteration 650's two views (matched to its camera by the view matrix)
+    assert len(captured) == 2
+    st, inp, gcol, g = captured[0]
+    view = st.view.detach().cpu().reshape(4, 4)
+    cam650 = [cam for cam in cams650 if torch.equal(cam.world_view_transform.detach().cpu().float(), view)]
+    assert len(cam650) >= 1
+    cam650 = cam650[0]
+    c = st.c
+    assert inp["colors_precomp"] is None and inp["cov3D_precomp"] is None and inp["language_feature"] is None
+    cam_np = lambda t: t.detach().cpu().numpy()   # noqa: E731
+    s = oracle.OracleSettings(c.image_height, c.image_width, c.tanfovx, c.tanfovy, np.ones(3, np.float32), 1.0,
+                              cam_np(cam650.world_view_transform), cam_np(cam650.full_proj_transform), 3,
+                              cam_np(cam650.camera_center), False)
+    ref = oracle.forward(s, inp["means3D"].numpy(), inp["opacities"].numpy(), shs=inp["shs"].numpy(),
+                         scales=inp["scales"].numpy(), rotations=inp["rotations"].numpy())
+    rg = ref.backward(gcol.numpy())
+    P = inp["means3D"].shape[0]
+    errs = {k: grad_err(g[n].numpy().reshape(P, -1), rg[r].reshape(P, -1))
+            for k, n, r in (("means3D", "means3D", "means3D"), ("means2D", "means2D", "means2D"),
+                            ("sh", "sh", "sh"), ("opacity", "opacities", "opacity"), ("scales", "scales", "scales"),
+                            ("rotations", "rotations", "rotations"))}
+    assert max(errs.values()) <= 1e-4, errs
