@@ -627,6 +627,26 @@ __global__ void __launch_bounds__(256) k_deform_bwd_a(DeformBwdArgs b) {
             for (int c = 0; c < 3; ++c)
                 b.d_means3D[3 * gg + c] = b.up[0][3 * gg + c] + dq[c] * (2.0f / (a.aabb[3 + c] - a.aabb[c]));
         }
+        if (b.daabb) {   // block-uniform
+            // normalize_aabb's gradient w.r.t. the box (hexplane.py:19-20): with n = (p - a0) s - 1,
+            // s = 2 / (a1 - a0): dn/da0 = s (n - 1) / 2, dn/da1 = -s (n + 1) / 2, and dq = dL/dn
+            float v[6];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const float gp = (ok && q == 0) ? dq[c] * (2.0f / (a.aabb[3 + c] - a.aabb[c])) : 0.0f;
+                v[c] = 0.5f * gp * (crd[c] - 1.0f);
+                v[3 + c] = -0.5f * gp * (crd[c] + 1.0f);
+            }
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) v[k] += __shfl_xor(v[k], off);
+            }
+            if ((tid & 63) == 0) {
+#pragma unroll
+                for (int k = 0; k < 6; ++k) atomicAdd(b.daabb + k, v[k]);
+            }
+        }
     }
 }
 

@@ -413,6 +413,7 @@ extern "C" int lsr_deform_backward(const lsr_deform_net* net, const void* worksp
     b.sG_rot = fp(S.Grot);
     b.sG_coff = fp(S.Gcoff);
     b.dplanes = fp(S.dplanes);
+    b.daabb = grads->aabb;
     b.replicas = kGradReplicas;
     b.plane_stride = (int64_t)(L.planes_end / sizeof(float));
     if (hipMemsetAsync(b.dplanes, 0, kGradReplicas * L.planes_end, st) != hipSuccess) return lsr::fail(LSR_EHIP, "memset");

@@ -303,6 +303,7 @@ struct DeformBwdArgs {
     float* sdZ1[DEF_HEADS];           //                    [P,128] gradient of Z1
     float* sG_rot;                    // apply_rotation: [P,4] gradient of the rotation head's output
     float* sG_coff;                   // DISCRETE: [P, centers] gradient of coff
+    float* daabb;                     // [2][3] gradient of the HexPlane box (accumulated), or null
 };
 void launch_deform_bwd_a(const DeformBwdArgs& a, hipStream_t st);
 struct AtbJob {                        // C[M][N] += sum_g L[g][m] R[g][n]; bias[m] += sum_g L[g][m]

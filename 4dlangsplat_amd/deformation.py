@@ -346,9 +346,16 @@ class DeformationField:
     __call__ = forward
 
     # ---- backward (lsr_deform_backward) -------------------------------------------------------
+    #: whether backward() also produces the HexPlane box's gradient grads["grid.aabb"].  The reference
+    #: trains the box whenever the whole field has requires_grad -- the base stages and joint_train
+    #: (scene/gaussian_model.py:258,291: requires_grad_(True) reaches the aabb Parameter that set_aabb
+    #: made with requires_grad=False, and get_grid_parameters gives "grid.aabb" to Adam); TrainStep
+    #: turns this on.  Off, the box is a constant (what a freshly built deform_network has).
+    train_aabb = False
+
     def zero_grad(self):
         """Parameter gradients (torch layouts, names as the parameters) set to zero."""
-        self.grads = {k: torch.zeros_like(v) for k, v in self.p.items() if k != "grid.aabb"}
+        self.grads = {k: torch.zeros_like(v) for k, v in self.p.items() if k != "grid.aabb" or self.train_aabb}
 
     def backward(self, means3D, time, d_means3D, d_scales, d_rotations, d_opacity, d_shs, rotations=None, lang=None,
                  d_lang=None, d_coff=None, no_dlang: Optional[bool] = None):
@@ -394,6 +401,8 @@ class DeformationField:
             for i, k in enumerate((1, 3, 5)):
                 g.w_lang[i] = self.grads[f"lang_deform.{k}.weight"].data_ptr()
                 g.b_lang[i] = self.grads[f"lang_deform.{k}.bias"].data_ptr()
+        if "grid.aabb" in self.grads:
+            g.aabb = self.grads["grid.aabb"].data_ptr()
         nbytes = int(L.lsr_deform_backward_scratch_bytes(ctypes.byref(net), P))
         if nbytes < 0:
             _lib.check(1, "lsr_deform_backward_scratch_bytes")

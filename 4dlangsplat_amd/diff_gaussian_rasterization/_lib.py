@@ -56,7 +56,7 @@ class BwdOut(ctypes.Structure):
 
 # every symbol include/lsr.h declares, with its ctypes signature
 class DeformNet(ctypes.Structure):
-    """include/lsr_deform.h lsr_deform_net (LSR_DEFORM_API_VERSION 2)"""
+    """include/lsr_deform.h lsr_deform_net (LSR_DEFORM_API_VERSION 3)"""
     _fields_ = [("n_scales", ctypes.c_int32), ("channels", ctypes.c_int32), ("width", ctypes.c_int32),
                 ("res", ctypes.c_int32 * 4), ("multires", ctypes.c_int32 * 4), ("depth", ctypes.c_int32),
                 ("heads", ctypes.c_uint32), ("apply_rotation", ctypes.c_int32), ("lang_mode", ctypes.c_int32),
@@ -64,14 +64,16 @@ class DeformNet(ctypes.Structure):
                 ("aabb", ctypes.c_void_p), ("planes", (ctypes.c_void_p * 6) * 4),
                 ("w_feat", ctypes.c_void_p * 4), ("b_feat", ctypes.c_void_p * 4),
                 ("w1", ctypes.c_void_p * 6), ("b1", ctypes.c_void_p * 6), ("w2", ctypes.c_void_p * 6),
-                ("b2", ctypes.c_void_p * 6), ("w_lang", ctypes.c_void_p * 3), ("b_lang", ctypes.c_void_p * 3)]
+                ("b2", ctypes.c_void_p * 6), ("w_lang", ctypes.c_void_p * 3), ("b_lang", ctypes.c_void_p * 3),
+                ("aabb", ctypes.c_void_p)]
 
 
 class DeformGrads(ctypes.Structure):
     """include/lsr_deform.h lsr_deform_grads"""
     _fields_ = [("planes", (ctypes.c_void_p * 6) * 4), ("w_feat", ctypes.c_void_p * 4), ("b_feat", ctypes.c_void_p * 4),
                 ("w1", ctypes.c_void_p * 6), ("b1", ctypes.c_void_p * 6), ("w2", ctypes.c_void_p * 6),
-                ("b2", ctypes.c_void_p * 6), ("w_lang", ctypes.c_void_p * 3), ("b_lang", ctypes.c_void_p * 3)]
+                ("b2", ctypes.c_void_p * 6), ("w_lang", ctypes.c_void_p * 3), ("b_lang", ctypes.c_void_p * 3),
+                ("aabb", ctypes.c_void_p)]
 
 
 class AdamGroup(ctypes.Structure):

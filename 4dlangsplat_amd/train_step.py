@@ -20,6 +20,18 @@ never equals the stage names it runs ('fine-base', 'fine-lang'), and lambda_dssi
 (arguments/__init__.py:146), so the base-stage loss is the L1 alone.
 set_reference_lr() installs the per-iteration learning-rate schedules of
 gaussian_model.py:302-330 (xyz, deformation MLPs, grid planes; OptimizationParams defaults).
+
+The 'lang' stages (coarse-lang, fine-lang, fine-lang-discrete) follow train.py:272-296 and
+training_setup's lang branch (scene/gaussian_model.py:226-270):
+  loss = lam * l1_loss(lang * mask, gt_lang * mask)                         train.py:287
+         (+ beta * cos_loss(lang * mask, gt_lang * mask) with addcosloss)   :289-292, utils/loss_utils.py:26-27
+         (+ l1_loss(images, gts[:, :3]) with joint_train)                   :293-296
+  trainable: the language features; the deformation field's lang_deform when it deforms the
+  language (no_dlang 0) and its discrete_coff_generator in a 'discrete' stage; with joint_train
+  every Gaussian group and the whole field as well.  Frozen groups get no gradient and Adam skips
+  them, as the reference's requires_grad_(False) parameters.  The renders' coff (discrete fields)
+  is collected as train.py:245-247 collects it; the reference computes no loss from it.
+  Densification statistics are gathered in the 'base' stages only (train.py:388).
 """
 from __future__ import annotations
 
@@ -87,14 +99,23 @@ class TrainStep:
 
     def __init__(self, trainer: GaussianTrainer, field=None, deform_lr: float = 1.6e-4, grid_lr: float = 1.6e-3,
                  bg: Optional[torch.Tensor] = None, stage: str = "fine-base", sh_degree: int = 3,
-                 densify: Optional[Callable[[GaussianTrainer, int], None]] = None, batch_views: bool = False):
+                 densify: Optional[Callable[[GaussianTrainer, int], None]] = None, batch_views: bool = False,
+                 joint_train: bool = False, lam: float = 0.2, beta: float = 0.01, addcosloss: bool = False):
         """densify(trainer, iteration): optional densify / prune / reset_opacity schedule, run
         between the densification statistics and the optimizer step (train.py:388-421).
         batch_views: the batch's views share one deformation-field launch (render_views)
         instead of one per view (render); same values.  Off by default: at configs[4] size
         the repeat / split copies around the one launch cost more than the per-call fixed work
-        saved (127.8 vs 140.5 iterations/s)."""
+        saved (127.8 vs 140.5 iterations/s).
+        joint_train, lam, beta, addcosloss: the 'lang' stages' switches (train.py --joint_coarse /
+        --joint_fine, --lam 0.2, --beta 0.01, env addcosloss)."""
+        if joint_train and "lang" not in stage:
+            raise ValueError("joint_train needs a 'lang' stage (train.py:103-104)")
+        if "lang" in stage and "language_feature" not in trainer.params:
+            raise ValueError("a 'lang' stage trains the language features: the trainer needs a language_feature group")
         self.trainer, self.field, self.stage = trainer, field, stage
+        self.joint_train, self.lam, self.beta, self.addcosloss = joint_train, lam, beta, addcosloss
+        self.coff = []              # the last iteration's renders' coff (train.py:240-247)
         self.batch_views = batch_views
         self.densify = densify
         self.iteration = 0
@@ -102,7 +123,10 @@ class TrainStep:
         self.bg = bg if bg is not None else torch.ones(3, device=trainer.device)
         self.field_opt = None
         if field is not None:
-            params = {k: v for k, v in field.p.items() if k != "grid.aabb"}
+            # the box trains too (gaussian_model.py:250-253,258,291: "grid.aabb" is among
+            # get_grid_parameters and has requires_grad once the whole module does)
+            field.train_aabb = True
+            params = dict(field.p)
             lrs = {k: (grid_lr if k.startswith("grid.") else deform_lr) for k in params}
             self.field_opt = TensorAdam(params, lrs)
 
@@ -129,20 +153,58 @@ class TrainStep:
             for k in self.field_opt.lr:
                 self.field_opt.lr[k] = lg if k.startswith("grid.") else ld
 
+    @property
+    def lang_stage(self) -> bool:
+        return "lang" in self.stage
+
+    def field_trainable(self, name: str) -> bool:
+        """Whether the field parameter `name` trains in this stage (training_setup,
+        scene/gaussian_model.py:248-262: _deformation.requires_grad_(joint_train), then
+        lang_deform.requires_grad_(no_dlang == 0), discrete_coff_generator on in 'discrete' stages)."""
+        if not self.lang_stage:
+            return True
+        if name.startswith("lang_deform."):
+            return True           # present only when the field deforms the language (no_dlang 0)
+        if name.startswith("discrete_coff_generator."):
+            return self.joint_train or "discrete" in self.stage
+        return self.joint_train
+
     def scene(self) -> GaussianScene:
         tr = self.trainer
         lang = tr.params.get("language_feature")
         if lang is None:
             lang = torch.zeros(tr.P, 3, device=tr.device)
-        return GaussianScene(tr["xyz"], tr["f_dc"], tr["f_rest"], lang, tr["opacity"], tr["scaling"], tr["rotation"],
-                             max_sh_degree=self.sh_degree, active_sh_degree=self.sh_degree, deformation=self.field)
+        # a 'lang' stage without joint_train freezes the geometry and colours (requires_grad_(False))
+        g = (lambda t: t) if (not self.lang_stage or self.joint_train) else (lambda t: t.detach())   # noqa: E731
+        return GaussianScene(g(tr["xyz"]), g(tr["f_dc"]), g(tr["f_rest"]), lang, g(tr["opacity"]), g(tr["scaling"]),
+                             g(tr["rotation"]), max_sh_degree=self.sh_degree, active_sh_degree=self.sh_degree,
+                             deformation=self.field)
 
-    def __call__(self, cams: Sequence, gts: torch.Tensor, iteration: Optional[int] = None) -> torch.Tensor:
-        """One iteration over the views `cams` with ground-truth images gts [V, 3, H, W].
-        Returns the loss (a device scalar; no host synchronisation here unless `densify` makes one)."""
-        tr = self.trainer
-        self.iteration = self.iteration + 1 if iteration is None else iteration
-        self.update_learning_rate(self.iteration)
+    def loss(self, outs, gts: Optional[torch.Tensor], gt_lang: Optional[torch.Tensor] = None,
+             lang_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """The stage's loss over the views' render outputs (train.py:272-296).  Base stages: L1 of the
+        images against gts [V, 3(+), H, W].  'lang' stages: gt_lang [V, C, H, W], lang_mask [V, 1, H, W]
+        (the reference trains them one view at a time, batch_size 1, where its cat over views is this
+        stack)."""
+        if not self.lang_stage:
+            images = torch.stack([o["render"] for o in outs])
+            return (images - gts[:, :3]).abs().mean()
+        if gt_lang is None or lang_mask is None:
+            raise ValueError("a 'lang' stage needs gt_lang and lang_mask")
+        lang = torch.stack([o["language_feature_image"] for o in outs])
+        a, b = lang * lang_mask, gt_lang * lang_mask
+        loss = self.lam * (a - b).abs().mean()
+        if self.addcosloss:
+            loss = loss + self.beta * (1 - torch.nn.functional.cosine_similarity(a, b, dim=-1).mean())
+        if self.joint_train:
+            images = torch.stack([o["render"] for o in outs])
+            loss = loss + (images - gts[:, :3]).abs().mean()
+        return loss
+
+    def forward_backward(self, cams: Sequence, gts: Optional[torch.Tensor], gt_lang: Optional[torch.Tensor] = None,
+                         lang_mask: Optional[torch.Tensor] = None):
+        """Render every view, the stage's loss, loss.backward() (train.py:242-339).  Leaves the
+        gradients in the trainer's parameters' .grad and the field's grads; returns (loss, outs)."""
         if self.field is not None:
             self.field.zero_grad()
         sc = self.scene()
@@ -150,11 +212,23 @@ class TrainStep:
             outs = render_views(cams, sc, self.bg, stage=self.stage)
         else:
             outs = [render(cam, sc, self.bg, stage=self.stage) for cam in cams]
-        images = torch.stack([o["render"] for o in outs])
-        loss = (images - gts).abs().mean()
+        self.coff = [o["coff"] for o in outs if o.get("coff") is not None]
+        loss = self.loss(outs, gts, gt_lang, lang_mask)
         loss.backward()
+        return loss, outs
+
+    def __call__(self, cams: Sequence, gts: Optional[torch.Tensor], iteration: Optional[int] = None,
+                 gt_lang: Optional[torch.Tensor] = None, lang_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """One iteration over the views `cams` with ground-truth images gts [V, 3, H, W] (and, in
+        the 'lang' stages, language features gt_lang [V, C, H, W] with masks lang_mask [V, 1, H, W]).
+        Returns the loss (a device scalar; no host synchronisation here unless `densify` makes one)."""
+        tr = self.trainer
+        self.iteration = self.iteration + 1 if iteration is None else iteration
+        self.update_learning_rate(self.iteration)
+        loss, outs = self.forward_backward(cams, gts, gt_lang, lang_mask)
         collect = getattr(self.densify, "collect_stats", None)
-        if collect is None or collect(self.iteration):   # train.py:388: while iteration < densify_until_iter
+        # train.py:388: while iteration < densify_until_iter, in the 'base' stages
+        if "base" in self.stage and (collect is None or collect(self.iteration)):
             radii = torch.stack([o["radii"] for o in outs]).max(dim=0).values
             vgrad = outs[0]["viewspace_points"].grad
             for o in outs[1:]:
@@ -165,6 +239,9 @@ class TrainStep:
         tr.step()
         tr.zero_grad(set_to_none=True)
         if self.field is not None:
-            self.field_opt.step(self.field.grads)
-            self.field.prepare()
+            grads = self.field.grads if not self.lang_stage else \
+                {k: v for k, v in self.field.grads.items() if self.field_trainable(k)}
+            if grads:
+                self.field_opt.step(grads)
+                self.field.prepare()
         return loss.detach()

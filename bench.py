@@ -323,24 +323,34 @@ def run(args):
         ntiles = ((W + 15) // 16) * ((H + 15) // 16)
         roof = None
         phases = {}
+        pmc_all = {}
+        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            try:
+                pmc_all = json.load(open(pmc))
+            except Exception:
+                pmc_all = {}
         if prof:
             for k, (ms, n) in prof_all.items():   # the untimed all-phase step
                 if n:   # per view (a batched launch serves several); preprocess_bwd_views: per launch
                     per = ms / n if k == "preprocess_bwd_views" else ms / len(dp.views)
-                    phases[k] = dict(mean_ms=per, launches=n, gbs=phase_bytes(k, P, Pvis, Kmean, W * H, ntiles, C, M, **pb)
-                                     / (per * 1e-3) / 1e9)
+                    rec = pmc_all.get(k, {}) if isinstance(pmc_all.get(k), dict) else {}
+                    # alg_gbs: the per-VIEW algorithmic bytes (phase_bytes) over the per-view time.  A
+                    # batched launch (preprocess, the compositors) reads a Gaussian's inputs once per
+                    # launch, not once per view, so for those this overstates what the chip moved;
+                    # pmc_gbs: the PMC bytes of one launch (profiles/pmc_traffic.json, the same step
+                    # structure) over the mean launch time -- the bandwidth really drawn
+                    phases[k] = dict(mean_ms=per, launches=n,
+                                     alg_gbs=phase_bytes(k, P, Pvis, Kmean, W * H, ntiles, C, M, **pb)
+                                     / (per * 1e-3) / 1e9,
+                                     pmc_gbs=(rec["hbm_bytes_per_launch"] / (ms / n * 1e-3) / 1e9)
+                                     if rec.get("hbm_bytes_per_launch") else None)
             ms, n = prof[dom]                      # live, over the timed region
             byts = phase_bytes(dom, P, Pvis, Kmean, W * H, ntiles, C, M, **pb)
             if dom.startswith("render"):           # per view; a batched launch composites several views
                 byts *= V * args.steps / n
             ach = byts / (ms / n * 1e-3) / 1e9
-            pmc_rec = {}
-            pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-            if os.path.exists(pmc):
-                try:
-                    pmc_rec = json.load(open(pmc)).get(dom, {})
-                except Exception:
-                    pmc_rec = {}
+            pmc_rec = pmc_all.get(dom, {}) if isinstance(pmc_all.get(dom), dict) else {}
             # the HBM roofline is the contract's; the compositors are bound by VALU issue and atomics
             # (DESIGN.md 4), so the PMC VALU-issue share and matrix-core busy fraction ride along
             # the compositors' VALU side: wave64 VALU instructions per launch (PMC SQ_INSTS_VALU) at
@@ -364,7 +374,26 @@ def run(args):
         frame_roof = dict(algorithmic_bytes_per_frame=int(fb), achieved=round(fb * value / 1e9, 1), peak=HBM_PEAK_GBS,
                           unit="GB/s", frac=round(fb * value / 1e9 / HBM_PEAK_GBS, 4),
                           formula="SURVEY.md 8(d): fwd P*339 + K*216 + Npix*(4(3+C+1)+8); bwd K*176 + "
-                                  "Npix*(4(3+C)+8) + P*(44+4C) + P*316 + P*256, K measured")
+                                  "Npix*(4(3+C)+8) + P*(44+4C) + P*316 + P*256, K measured",
+                          note="charges every frame the per-view preprocess (P-proportional) bytes; the batched "
+                               "step reads a Gaussian's inputs and writes its gradient rows once per launch of "
+                               "up to 8 views, so it moves less than this: see pmc_step (measured traffic) and "
+                               "single_view.frame_roofline (the per-frame path this formula describes)")
+        if prof and pmc_all:
+            # the step's measured HBM traffic: PMC bytes per launch of every profiled phase x its
+            # launches in one step, per frame (kernels without a PMC record, the sorts and scans,
+            # are left out, so this is a lower bound)
+            step_b = sum(pmc_all[k]["hbm_bytes_per_launch"] * n for k, (ms, n) in prof_all.items()
+                         if n and isinstance(pmc_all.get(k), dict) and pmc_all[k].get("hbm_bytes_per_launch"))
+            per_frame = step_b / len(dp.views)
+            frame_roof["pmc_step"] = dict(hbm_bytes_per_frame=int(per_frame), achieved=round(per_frame * value / 1e9, 1),
+                                          frac=round(per_frame * value / 1e9 / HBM_PEAK_GBS, 4),
+                                          phases=sorted(k for k in prof_all if isinstance(pmc_all.get(k), dict)),
+                                          source="profiles/pmc_traffic.json (sorts/scans not included)")
+        if single is not None:
+            single["frame_roofline"] = dict(algorithmic_bytes_per_frame=int(fb),
+                                            achieved=round(fb * single["value"] / 1e9, 1), peak=HBM_PEAK_GBS,
+                                            unit="GB/s", frac=round(fb * single["value"] / 1e9 / HBM_PEAK_GBS, 4))
         cpu = None
         if not args.no_cpu_baseline and world == 1:   # the contract's CPU leg: rank 0 at N = 1 only
             avail, host = host_cpu()
@@ -388,7 +417,11 @@ def run(args):
                         global_batch=world * V, parallelism=f"dp{world}", pipeline="none" if args.no_overlap else args.pipeline, num_rendered_mean=int(Kmean),
                         visible=Pvis, visible_any_view=Pany, grad_bucket_mb=round(bucket.nbytes / 2**20, 1)),
             roofline=roof, frame_roofline=frame_roof, cpu_baseline=cpu, single_view=single,
-            phases={k: dict(mean_ms=round(v["mean_ms"], 4), gbs=round(v["gbs"], 1)) for k, v in phases.items()},
+            phases={k: dict(mean_ms=round(v["mean_ms"], 4), alg_gbs=round(v["alg_gbs"], 1),
+                            pmc_gbs=None if v["pmc_gbs"] is None else round(v["pmc_gbs"], 1)) for k, v in phases.items()},
+            phases_note=("mean_ms per view (a batched launch's time / its views; preprocess_bwd_views per launch); "
+                         "alg_gbs = per-view algorithmic bytes / per-view time (overstates batched launches, which "
+                         "read the Gaussians once per launch); pmc_gbs = PMC HBM bytes per launch / launch time"),
         )
         print(json.dumps(line))
     if world > 1:

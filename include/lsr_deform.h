@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define LSR_DEFORM_API_VERSION 2   /* 2: depth, head mask, apply_rotation, language modes, coff */
+#define LSR_DEFORM_API_VERSION 3   /* 2: depth, head mask, apply_rotation, language modes, coff; 3: aabb gradient */
 #define LSR_DEFORM_HEADS 6         /* pos 3, scales 3, rotations 4, opacity 1, shs 48, coff (centers) */
 #define LSR_DEFORM_MAX_SCALES 4
 #define LSR_DEFORM_MAX_DEPTH 4     /* feature_out Linear layers */
@@ -91,6 +91,11 @@ typedef struct lsr_deform_grads {
     float *w1[LSR_DEFORM_HEADS], *b1[LSR_DEFORM_HEADS];
     float *w2[LSR_DEFORM_HEADS], *b2[LSR_DEFORM_HEADS];
     float *w_lang[3], *b_lang[3];
+    /* [2][3] gradient of HexPlaneField.aabb (xyz_max, xyz_min), accumulated; NULL: not computed.  The
+     * reference trains the box whenever the whole field has requires_grad (the base stages and
+     * joint_train: scene/gaussian_model.py:258,291 requires_grad_(True) reaches the aabb Parameter
+     * that set_aabb made with requires_grad=False, and get_grid_parameters hands "grid.aabb" to Adam). */
+    float *aabb;
 } lsr_deform_grads;
 
 /* Scratch of lsr_deform_backward for P Gaussians (saved activations). */
