@@ -1,4 +1,5 @@
-// binning.hip -- (Gaussian, tile) instance emission in depth order and per-tile ranges.
+// binning.hip -- (Gaussian, tile) instance emission in depth order.  The per-tile ranges are made
+// by the tile sort's last scatter pass (sort.hip).
 //
 // Upstream emits one 64-bit key (tile << 32 | depth bits) per instance and
 // radix-sorts all of them on 32 + log2(tiles) bits.  Here the depth order is established once on
@@ -109,43 +110,6 @@ void launch_scatter_inst_off(int P, const uint32_t* order, const uint32_t* offse
     if (P == 0) return;
     hipLaunchKernelGGL(k_scatter_inst_off, dim3((P + 255) / 256), dim3(256), 0, st, P, order, offsets, counts,
                        inst_off);
-}
-
-// Four keys per thread (one 16-byte load plus the two neighbours): one thread per key made ~190k
-// tiny blocks for 8 views of 6M instances, dispatch-bound at ~1.6 TB/s of key reads.
-__global__ void __launch_bounds__(256) k_tile_ranges(const RangesBatch rb, uint32_t ntiles) {
-    const RangesSeg& sg = rb.s[blockIdx.y];
-    const size_t K = sg.K;
-    const uint32_t* __restrict__ keys = sg.keys;
-    const size_t i0 = 4 * ((size_t)blockIdx.x * blockDim.x + threadIdx.x);
-    if (i0 >= K) return;
-    uint32_t k[6];   // keys i0 - 1 .. i0 + 4 (ntiles + 1 outside the list: never equal to a tile)
-    if (i0 + 4 <= K && (reinterpret_cast<uintptr_t>(keys + i0) & 15u) == 0) {
-        const uint4 v = *reinterpret_cast<const uint4*>(keys + i0);
-        k[1] = v.x; k[2] = v.y; k[3] = v.z; k[4] = v.w;
-    } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) k[1 + j] = i0 + j < K ? keys[i0 + j] : ntiles + 1u;
-    }
-    k[0] = i0 > 0 ? keys[i0 - 1] : ntiles + 1u;
-    k[5] = i0 + 4 < K ? keys[i0 + 4] : ntiles + 1u;
-#pragma unroll
-    for (int j = 1; j <= 4; ++j) {
-        const uint32_t t = k[j];
-        if (t >= ntiles) continue;   // dropped instances (past-the-end key) and slots past K
-        if (k[j - 1] != t) sg.ranges[t].x = (uint32_t)(i0 + j - 1);
-        if (k[j + 1] != t) sg.ranges[t].y = (uint32_t)(i0 + j);
-    }
-}
-
-void launch_tile_ranges(const RangesSeg* segs, int nseg, uint32_t ntiles, hipStream_t st) {
-    RangesBatch rb{};
-    int ns = 0;
-    size_t kmax = 0;
-    for (int i = 0; i < nseg; ++i)
-        if (segs[i].K > 0) { rb.s[ns++] = segs[i]; kmax = std::max(kmax, segs[i].K); }
-    if (ns == 0) return;
-    hipLaunchKernelGGL(k_tile_ranges, dim3((unsigned)((kmax + 1023) / 1024), ns), dim3(256), 0, st, rb, ntiles);
 }
 
 }  // namespace lsr

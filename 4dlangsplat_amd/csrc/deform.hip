@@ -18,6 +18,22 @@
 
 namespace lsr {
 
+// LDS poison build (-DLSR_LDS_POISON, build/variants/liblsr_ldspoison.so; tests/test_deform_lds_poison_gpu.py):
+// every kernel of this file fills its shared memory with all-ones words (NaN as fp32 and as bf16)
+// at block entry, so a read of LDS the block never wrote turns the results into NaN instead of
+// silently reusing what an earlier block on the CU left there.
+#ifdef LSR_LDS_POISON
+__device__ __forceinline__ void lds_poison(void* p, size_t bytes) {
+    uint32_t* w = static_cast<uint32_t*>(p);
+    for (size_t i = threadIdx.x; i < bytes / 4; i += blockDim.x) w[i] = 0xFFFFFFFFu;
+}
+#define LDS_POISON(arr) lds_poison(&(arr), sizeof(arr))
+#define LDS_POISON_DONE() __syncthreads()
+#else
+#define LDS_POISON(arr) do {} while (0)
+#define LDS_POISON_DONE() do {} while (0)
+#endif
+
 typedef __bf16 dbf16x8 __attribute__((ext_vector_type(8)));
 typedef float df32x16 __attribute__((ext_vector_type(16)));
 #define DMFMA(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
@@ -272,6 +288,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     __shared__ __attribute__((aligned(16))) __bf16 s_hh[2][DN * DAP];   // hidden rows, ping-pong
     __shared__ __attribute__((aligned(16))) __bf16 s_hl[2][DN * DAP];
     __shared__ float s_q[DN][9];                                         // per-Gaussian head outputs
+    LDS_POISON(s_hh); LDS_POISON(s_hl); LDS_POISON(s_q); LDS_POISON_DONE();
     // the features are read by the first layer only, which writes buffer 0: they use buffer 1 (72 KB
     // of LDS in all: two blocks per CU)
     __bf16* const s_xh = s_hh[1];
@@ -417,6 +434,8 @@ __global__ void __launch_bounds__(256) k_deform_bwd_a(DeformBwdArgs b) {
     __shared__ float s_sdv[4][16][17];   // plane scatter staging, per wave: dv of 16 Gaussians
     __shared__ int s_soff[4][16][4];     //   their 4 tap offsets
     __shared__ float s_sw[4][16][4];     //   and bilinear weights
+    LDS_POISON(s_hh); LDS_POISON(s_hl); LDS_POISON(s_gh); LDS_POISON(s_gl); LDS_POISON(s_dx);
+    LDS_POISON(s_sdv); LDS_POISON(s_soff); LDS_POISON(s_sw); LDS_POISON_DONE();
     const DeformArgs& a = b.f;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int g0 = blockIdx.x * DN;
@@ -743,6 +762,7 @@ __global__ void __launch_bounds__(256) k_lang_deform_fwd(LangDeformArgs a) {
     __shared__ __attribute__((aligned(16))) __bf16 s_hh[2][DN * DAP];
     __shared__ __attribute__((aligned(16))) __bf16 s_hl[2][DN * DAP];
     __shared__ float s_v[DN][33];
+    LDS_POISON(s_xh); LDS_POISON(s_xl); LDS_POISON(s_hh); LDS_POISON(s_hl); LDS_POISON(s_v); LDS_POISON_DONE();
     const int g0 = blockIdx.x * DN, tid = threadIdx.x;
     const int kpad = (a.kin + 15) / 16 * 16;
     lang_mlp_fwd(a, g0, kpad, s_xh, s_xl, s_hh, s_hl, s_v, false);
@@ -762,6 +782,8 @@ __global__ void __launch_bounds__(256) k_lang_deform_bwd(LangDeformArgs a) {
     __shared__ __attribute__((aligned(16))) __bf16 s_gh[DN * DLP];
     __shared__ __attribute__((aligned(16))) __bf16 s_gl[DN * DLP];
     __shared__ float s_v[DN][33];
+    LDS_POISON(s_xh); LDS_POISON(s_xl); LDS_POISON(s_hh); LDS_POISON(s_hl); LDS_POISON(s_gh); LDS_POISON(s_gl);
+    LDS_POISON(s_v); LDS_POISON_DONE();
     const int g0 = blockIdx.x * DN, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hh = lane >> 5;
     const int col = 32 * wave + (lane & 31);
     const int C = a.lang_dim, kpad = (a.kin + 15) / 16 * 16;
@@ -943,6 +965,7 @@ void launch_atb(const AtbArgs& a, int njobs, hipStream_t st) {
 __global__ void __launch_bounds__(256) k_unpack_plane_grad(const float* __restrict__ src, float* __restrict__ dst,
                                                            int H, int W, int replicas, int64_t stride) {
     __shared__ float s_t[16][17];
+    LDS_POISON(s_t); LDS_POISON_DONE();
     const int HW = H * W, base = blockIdx.x * 16, t = threadIdx.x;
     const int tex = t >> 4, ch = t & 15;
     float acc = 0.0f;

@@ -453,7 +453,6 @@ int lsr_forward_binning_views(int32_t n_views, const lsr_settings* const* s, con
         lsr::EmitBatch eb{};
         eb.P = P; eb.grid_x = gx; eb.grid_y = gy; eb.W = W; eb.H = H;
         lsr::SortSeg ss[lsr::LSR_MAX_VIEWS] = {};
-        lsr::RangesSeg rs[lsr::LSR_MAX_VIEWS] = {};
         int ne = 0;
         for (int k = 0; k < nv; ++k) {
             const int v = v0 + k;
@@ -466,18 +465,19 @@ int lsr_forward_binning_views(int32_t n_views, const lsr_settings* const* s, con
                 continue;
             }
             Binning b = carve_binning(binning[v], K, nullptr);
-            // the emission also clears the tile ranges and the per-tile replay bounds (no separate
-            // fill launches)
+            // the emission also presets the tile ranges (0xFFFFFFFF, 0) for the tile sort's last pass,
+            // which makes them, and clears the per-tile replay bounds (no separate fill launches); the
+            // forward compositor turns the ranges of empty tiles back into (0, 0)
             lsr::EmitView& e = eb.v[ne];
             e.order = g.val_a; e.offsets = g.offsets; e.counts = g.counts; e.rect_sorted = g.rect_sorted;
             e.xy = g.xy; e.conic_o = g.conic_o; e.keys = b.key_a; e.vals = b.val_a;
             e.clear.p[0] = reinterpret_cast<uint32_t*>(m.ranges);
             e.clear.n[0] = (uint32_t)(2 * ntiles);
+            e.clear.even[0] = 0xFFFFFFFFu;
             e.clear.p[1] = m.tile_max;
             e.clear.n[1] = (uint32_t)ntiles;
-            ss[ne] = lsr::SortSeg{b.key_a, b.val_a, b.key_b, b.val_b, b.sort_tmp, nullptr,
-                                  lsr::SortGather{nullptr, nullptr, nullptr}, K};
-            rs[ne++] = lsr::RangesSeg{K, tile_sort_in_b((int)ntiles) ? b.key_b : b.key_a, m.ranges};
+            ss[ne++] = lsr::SortSeg{b.key_a, b.val_a, b.key_b, b.val_b, b.sort_tmp, nullptr,
+                                    lsr::SortGather{nullptr, nullptr, nullptr}, K, m.ranges, (uint32_t)ntiles};
         }
         if (ne == 0) continue;
         {
@@ -491,11 +491,6 @@ int lsr_forward_binning_views(int32_t n_views, const lsr_settings* const* s, con
             if (in_b != tile_sort_in_b((int)ntiles)) return fail(LSR_EHIP, "internal: tile sort parity");
         }
         LSR_LAUNCHED("tile sort", st, s[0]->debug);
-        {
-            PhaseTimer t(LSR_PHASE_TILE_RANGES, st);
-            lsr::launch_tile_ranges(rs, ne, (uint32_t)ntiles, st);
-        }
-        LSR_LAUNCHED("tile ranges", st, s[0]->debug);
     }
     return LSR_OK;
 }

@@ -15,6 +15,7 @@ constexpr int ACC_PITCH = 16;
 struct ClearList {
     uint32_t* p[4];
     uint32_t n[4];
+    uint32_t even[4];   // value of the even-indexed words (odd ones are zeroed); 0 = plain clear
 };
 
 constexpr int LSR_MAX_VIEWS = 8;   // views per launch; more are processed in chunks
@@ -22,7 +23,7 @@ __device__ __forceinline__ void clear_words(const ClearList& c) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-        for (uint32_t i = t; i < c.n[k]; i += stride) c.p[k][i] = 0u;
+        for (uint32_t i = t; i < c.n[k]; i += stride) c.p[k][i] = (i & 1u) ? 0u : c.even[k];
 }
 
 // Packed binning rectangle [x0, x1) x [y0, y1) in tiles (12 bits each: <= 4096 tiles per axis)
@@ -169,7 +170,7 @@ void launch_radii_max(int P, int n, const int* const* radii, int* out, bool accu
 
 struct RenderFwdArgs {
     int W, H, grid_x, grid_y, C, include_feature;
-    const uint2* ranges;
+    uint2* ranges;                // read; an empty tile's preset (~0, 0) is rewritten to (0, 0)
     const uint32_t* point_list;
     const float2* xy;
     const float4* conic_o;
@@ -389,6 +390,10 @@ struct SortSeg {
     uint32_t* kept;
     SortGather gather;
     size_t n;
+    // tile sort: the per-key [start, end) ranges, made by the last pass's scatter (atomicMin /
+    // atomicMax at the key runs' ends; entries preset to (0xFFFFFFFF, 0), keys >= nranges skipped)
+    uint2* ranges;
+    uint32_t nranges;
 };
 struct SortBatch { SortSeg s[LSR_MAX_VIEWS]; };
 // Sorts up to LSR_MAX_VIEWS independent segments with one launch per kernel of each pass (every
@@ -424,13 +429,6 @@ void launch_emit_instances(const EmitBatch& eb, int nv, hipStream_t st);
 void launch_scatter_inst_off(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* counts,
                              uint32_t* inst_off, hipStream_t st);
 // Per-tile [start, end) of a batch of tile-sorted instance lists (one grid row per list).
-struct RangesSeg {
-    size_t K;
-    const uint32_t* keys;
-    uint2* ranges;
-};
-struct RangesBatch { RangesSeg s[LSR_MAX_VIEWS]; };
-void launch_tile_ranges(const RangesSeg* segs, int nseg, uint32_t ntiles, hipStream_t st);
 
 // compositing (render_fwd_wave.hip / render_bwd.hip)
 void launch_render_bwd(const RenderBwdArgs& a, hipStream_t st);

@@ -43,7 +43,11 @@ __global__ void __launch_bounds__(64) k_render_fwd_wave(RenderFwdBatch ab) {
     const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
     const bool inside = px < a.W && py < a.H;
     const float pxf = (float)px, pyf = (float)py;
-    const uint2 range = a.ranges[tile];
+    uint2 range = a.ranges[tile];
+    if (range.x > range.y) {   // an empty tile: the tile sort's range atomics left the preset (~0, 0)
+        range = make_uint2(0u, 0u);
+        if (quad == 0 && lane == 0) a.ranges[tile] = range;   // upstream's (0, 0) for the backward
+    }
     const int C = a.C;
 
     float T = 1.0f;

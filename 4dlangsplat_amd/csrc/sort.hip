@@ -503,11 +503,19 @@ __global__ void __launch_bounds__(256) k_rts_scatter(const SortBatch b, int pass
         }
         return;
     }
+    uint2* __restrict__ ranges = last ? sg.ranges : nullptr;
     for (int i = tid; i < ntile; i += 256) {
         const uint32_t k = s_key[i];
         const uint32_t dst = s_gbase[(k >> shift) & mask] + (uint32_t)i;
         keys_out[dst] = k;
         vals_out[dst] = s_val[i];
+        if (ranges && k < sg.nranges) {
+            // the tile ranges (upstream identifyTileRanges): a key's run inside this block's LDS is
+            // contiguous in the output (one digit run), so its first / last element's position bounds
+            // the key's range; runs of one key in neighbouring blocks meet through the atomics
+            if (i == 0 || s_key[i - 1] != k) atomicMin(&ranges[k].x, dst);
+            if (i == ntile - 1 || s_key[i + 1] != k) atomicMax(&ranges[k].y, dst + 1u);
+        }
     }
 }
 

@@ -52,8 +52,8 @@ def phase_bytes(phase, P, Pvis, K, npix, ntiles, C, M=16, accumulate=True, V=1, 
         return P * (4 + 4)
     if phase == "emit":                    # order, offsets, counts, rect (depth order) -> keys, values
         return P * (4 + 4 + 4 + 8) + K * 8
-    if phase == "tile_sort":
-        return 2 * K * (4 + 16)
+    if phase == "tile_sort":               # two passes; the last one also makes the tile ranges
+        return 2 * K * (4 + 16) + ntiles * 8
     if phase == "tile_ranges":
         return K * 4 + ntiles * 8
     if phase == "render_fwd":
