@@ -74,20 +74,26 @@ class GradBucket:
     language | optional [P,3] means2D), so one collective moves all of it.  `views` maps the
     rasterizer's gradient names onto slices of `flat` (pass it as backward_native(out=...))."""
 
-    def __init__(self, P: int, M: int, C: int, device, densify_stats: bool = False):
+    def __init__(self, P: int, M: int, C: int, device, densify_stats: bool = False, row_multiple: int = 1):
+        """row_multiple: every field is allocated with Pa >= P rows, a multiple of row_multiple (the
+        rows past P stay zero), so that a reduce-scatter can split each field into equal row shards
+        (ShardedAdam); the views cover the first P rows."""
         self.P, self.M, self.C = P, M, C
+        self.Pa = -(-P // row_multiple) * row_multiple if P > 0 else 0
         self.densify_stats = densify_stats
         fields = [(n, w if w is not None else (3 * M if n == "sh" else C)) for n, w in GRAD_FIELDS]
         if densify_stats:
             fields.append(("means2D", 3))
+        self.widths = dict(fields)
         self.floats_per_gaussian = sum(w for _, w in fields)
-        self.flat = torch.zeros(P * self.floats_per_gaussian, dtype=torch.float32, device=device)
+        Pa = self.Pa
+        self.flat = torch.zeros(Pa * self.floats_per_gaussian, dtype=torch.float32, device=device)
         self.views: Dict[str, Optional[torch.Tensor]] = {}
-        self.ranges: Dict[str, Tuple[int, int]] = {}     # field -> [start, end) in flat
+        self.ranges: Dict[str, Tuple[int, int]] = {}     # field -> [start, end) in flat (Pa rows)
         o = 0
         for name, w in fields:
-            seg = self.flat[o * P:(o + w) * P]
-            self.ranges[name] = (o * P, (o + w) * P)
+            seg = self.flat[o * Pa:o * Pa + w * P]
+            self.ranges[name] = (o * Pa, (o + w) * Pa)
             if w == 0:
                 self.views[name] = None
             elif name == "sh":
@@ -140,7 +146,11 @@ class ViewParallelStep:
     Afterwards the bucket holds the SUM over ALL views of the batch on every rank, and
     bucket.radii the MAX over all views (when densify_stats)."""
 
-    def __init__(self, bucket: GradBucket, n_views: int, group=None, flush_chunks: int = 4):
+    def __init__(self, bucket: GradBucket, n_views: int, group=None, flush_chunks: int = 4, update=None):
+        """update: a ShardedAdam.  Without it the step ends with the bucket SUM all-reduced on every
+        rank; with it the bucket is reduce-scattered by Gaussian rows, each rank runs Adam on its row
+        shard and the updated rasterizer inputs are all-gathered (update.step)."""
+        self.update = update
         self.bucket = bucket
         self.n_views = n_views
         self.group = group
@@ -183,18 +193,19 @@ class ViewParallelStep:
         lo, hi = b.ranges["language_feature"]
         if self.world > 1 and b.radii is not None:   # final once the last view's forward ran
             pending.append(dist.all_reduce(b.radii, op=dist.ReduceOp.MAX, group=self.group, async_op=True))
-        if self.world > 1 and flush is not None and hi > lo:
+        sharded = self.update is not None
+        if self.world > 1 and flush is not None and hi > lo and not sharded:
             # with the batched backward the language gradients are final once the last view's
             # compositor backward ran; their SUM runs during the flush (the preprocess backward,
             # which writes every other field) instead of after it
             pending.append(dist.all_reduce(b.flat[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True))
-        chunked = self.world > 1 and getattr(flush, "chunked", False) and self.flush_chunks > 1
+        chunked = self.world > 1 and getattr(flush, "chunked", False) and self.flush_chunks > 1 and not sharded
         if chunked:
             # the flush in Gaussian-row chunks: each chunk's rows of every other field are SUMmed
             # (asynchronously, behind that chunk's launch) while the next chunk is computed
             def on_rows(r0, r1):
                 for name, (f0, f1) in b.ranges.items():
-                    w = (f1 - f0) // b.P if b.P else 0
+                    w = b.widths[name]
                     if name == "language_feature" or w == 0 or r1 <= r0:
                         continue
                     pending.append(dist.all_reduce(b.flat[f0 + r0 * w:f0 + r1 * w], op=dist.ReduceOp.SUM,
@@ -205,7 +216,11 @@ class ViewParallelStep:
         end = getattr(render_view, "end_step", None)
         if end is not None:
             end()
-        if self.world > 1:
+        if sharded:
+            self.update.step(b)
+            for h in pending:
+                h.wait()
+        elif self.world > 1:
             if not chunked:
                 if flush is not None and hi > lo:
                     segs = (b.flat[:lo], b.flat[hi:])
@@ -434,3 +449,162 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
             render_batch.before_wait = True   # takes the step's zeroing into its host-wait stretch
             render_view.render_batch = render_batch
     return render_view
+
+
+class ShardedAdam:
+    """The optimizer step of a view-parallel training step, sharded by Gaussian rows (ZeRO-1 style;
+    the reference runs one process: loss.backward(), then optimizer.step(), train.py:339,420-421).
+
+    Every rank holds the ACTIVATED rasterizer inputs of all P Gaussians (what the views render: the
+    scene's means3D, scales, rotations, opacities, shs, lang); the raw parameters and both Adam moments
+    exist only for the rank's row shard [r0, r1).  step(bucket), once the views' gradients are in the
+    bucket:
+      1. reduce-scatter each gradient field by rows (one collective per field, all in flight at once):
+         the rank receives the SUM over every rank's views of its own rows only;
+      2. back through the activations (gaussian_renderer/__init__.py:95-97,191-193 and the model's
+         activations, scene/gaussian_model.py:38-47): scaling exp, opacity sigmoid, rotation and
+         language L2 normalisations; SH split into f_dc / f_rest;
+      3. Adam on the shard (lsr_adam_step; `adam` overrides it for the CPU tests), torch.optim.Adam's
+         arithmetic with eps 1e-15;
+      4. the activations again, on the shard, and an all-gather of each activated field back into the
+         scene's tensors, which the next step renders.
+    The traffic per rank is (N-1)/N of the bucket (reduce-scatter) plus (N-1)/N of the activated
+    inputs (all-gather) -- the volume of the all-reduce it replaces -- while the activation math and
+    Adam run on 1/N of the rows and the parameters' optimizer state shrinks N-fold.
+    Shard boundaries are multiples of `align` rows; the bucket must be built with
+    GradBucket(row_multiple=world * shard rows) (ShardedAdam.row_multiple)."""
+
+    GROUPS = ("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation", "language_feature")
+
+    @staticmethod
+    def row_multiple(P: int, world: int, align: int = 64) -> int:
+        rows = -(-P // max(1, world))
+        return -(-rows // align) * align * world
+
+    def __init__(self, scene, raw: Dict[str, torch.Tensor], lrs: Dict[str, float], group=None, align: int = 64,
+                 betas=(0.9, 0.999), eps: float = 1e-15, adam: Optional[Callable] = None, nonormalized: bool = False):
+        """scene: object with the activated tensors (means3D, scales, rotations, opacities, shs, lang);
+        they are re-bound to row-padded storage.  raw: the full raw parameters (xyz, f_dc, f_rest,
+        opacity, scaling, rotation, language_feature), of which this rank keeps its shard.
+        adam(p, g, m, v, lr, step): in place on one group's shard (default: lsr_adam_step)."""
+        self.distributed = dist.is_available() and dist.is_initialized()
+        self.group = group
+        self.world = dist.get_world_size(group) if self.distributed else 1
+        self.rank = dist.get_rank(group) if self.distributed else 0
+        self.P = P = scene.means3D.shape[0]
+        self.Pa = self.row_multiple(P, self.world, align) if P > 0 else 0
+        self.rows = self.Pa // self.world
+        self.r0 = min(P, self.rank * self.rows)
+        self.r1 = min(P, self.r0 + self.rows)
+        self.lrs, self.betas, self.eps, self.nonormalized = dict(lrs), betas, eps, nonormalized
+        self._adam = adam
+        self.scene = scene
+        dev = scene.means3D.device
+        # activated inputs in row-padded storage (all-gather target); the scene's tensors view it
+        self.act = {}
+        for name in ("means3D", "scales", "rotations", "opacities", "shs", "lang"):
+            t = getattr(scene, name)
+            buf = torch.zeros((self.Pa,) + tuple(t.shape[1:]), dtype=torch.float32, device=dev)
+            buf[:P] = t
+            self.act[name] = buf
+            setattr(scene, name, buf[:P])
+        self.raw = {n: raw[n][self.r0:self.r1].detach().to(dev, torch.float32).clone().contiguous()
+                    for n in self.GROUPS if n in raw}
+        self.exp_avg = {n: torch.zeros_like(t) for n, t in self.raw.items()}
+        self.exp_avg_sq = {n: torch.zeros_like(t) for n, t in self.raw.items()}
+        self.steps = {n: 0 for n in self.raw}
+
+    # ---- 1. reduce-scatter ------------------------------------------------------------------------
+    def _shard_grads(self, bucket) -> Dict[str, torch.Tensor]:
+        if bucket.Pa != self.Pa:
+            raise ValueError(f"bucket rows {bucket.Pa} != {self.Pa}: build it with GradBucket(row_multiple=...)")
+        out, handles = {}, []
+        for name in ("means3D", "scales", "rotations", "opacities", "sh", "language_feature"):
+            f0, f1 = bucket.ranges[name]
+            w = bucket.widths[name]
+            if w == 0:
+                continue
+            full = bucket.flat[f0:f1]
+            if self.world > 1:
+                shard = torch.empty(self.rows * w, dtype=torch.float32, device=full.device)
+                handles.append(dist.reduce_scatter_tensor(shard, full, group=self.group, async_op=True))
+            else:
+                shard = full
+            out[name] = shard.view(self.rows, w)[: self.r1 - self.r0]
+        for h in handles:
+            h.wait()
+        return out
+
+    # ---- 2. activations' backward, 3. Adam, 4. activations + all-gather ----------------------------------
+    def _lang_act(self, x):
+        return x if self.nonormalized else x / (x.norm(dim=-1, keepdim=True) + 1e-9)
+
+    def step(self, bucket) -> None:
+        g = self._shard_grads(bucket)
+        r0, r1 = self.r0, self.r1
+        raw = self.raw
+        grads = {}
+        if "means3D" in g:
+            grads["xyz"] = g["means3D"]
+        if "sh" in g:
+            sh = g["sh"].reshape(r1 - r0, -1, 3)
+            grads["f_dc"], grads["f_rest"] = sh[:, :1], sh[:, 1:]
+        if "opacities" in g:
+            o = torch.sigmoid(raw["opacity"])
+            grads["opacity"] = g["opacities"].reshape(o.shape) * o * (1 - o)
+        if "scales" in g:
+            grads["scaling"] = g["scales"] * torch.exp(raw["scaling"])
+        if "rotations" in g:
+            q = raw["rotation"]
+            n = q.norm(dim=-1, keepdim=True).clamp_min(1e-12)      # F.normalize's eps
+            r = q / n
+            gr = g["rotations"]
+            grads["rotation"] = (gr - r * (r * gr).sum(-1, keepdim=True)) / n
+        if "language_feature" in g and "language_feature" in raw:
+            x, gl = raw["language_feature"], g["language_feature"]
+            if self.nonormalized:
+                grads["language_feature"] = gl
+            else:
+                nx = x.norm(dim=-1, keepdim=True)
+                d = nx + 1e-9
+                grads["language_feature"] = gl / d - x * (x * gl).sum(-1, keepdim=True) / (nx.clamp_min(1e-30) * d * d)
+        for name, gr in grads.items():
+            if name not in raw or name not in self.lrs:
+                continue
+            gr = gr.reshape(raw[name].shape).contiguous()
+            self.steps[name] += 1
+            self._adam_group(raw[name], gr, self.exp_avg[name], self.exp_avg_sq[name], self.lrs[name], self.steps[name])
+        # 4. activated shard rows, gathered into every rank's scene tensors
+        act_rows = dict(means3D=raw.get("xyz"), scales=torch.exp(raw["scaling"]) if "scaling" in raw else None,
+                        rotations=torch.nn.functional.normalize(raw["rotation"]) if "rotation" in raw else None,
+                        opacities=torch.sigmoid(raw["opacity"]) if "opacity" in raw else None,
+                        shs=torch.cat([raw["f_dc"], raw["f_rest"]], dim=1) if "f_dc" in raw else None,
+                        lang=self._lang_act(raw["language_feature"]) if "language_feature" in raw else None)
+        handles = []
+        for name, rows in act_rows.items():
+            if rows is None:
+                continue
+            buf = self.act[name]
+            w = buf[0].numel() if self.Pa else 0
+            mine = buf.view(self.Pa, -1)[self.rank * self.rows:(self.rank + 1) * self.rows]
+            mine[: r1 - r0] = rows.reshape(r1 - r0, w)
+            if self.world > 1:
+                handles.append(dist.all_gather_into_tensor(buf.view(-1), mine.reshape(-1).clone(), group=self.group,
+                                                           async_op=True))
+        for h in handles:
+            h.wait()
+
+    def _adam_group(self, p, g, m, v, lr, step):
+        if self._adam is not None:
+            self._adam(p, g, m, v, lr, step)
+            return
+        import ctypes
+
+        from diff_gaussian_rasterization import _lib
+        L = _lib.load()
+        ag = _lib.AdamGroup()
+        ag.param, ag.grad, ag.exp_avg, ag.exp_avg_sq = p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr()
+        ag.n, ag.lr, ag.step = p.numel(), float(lr), int(step)
+        arr = (_lib.AdamGroup * 1)(ag)
+        _lib.check(L.lsr_adam_step(arr, 1, self.betas[0], self.betas[1], self.eps,
+                                   ctypes.c_void_p(torch.cuda.current_stream(p.device).cuda_stream)), "lsr_adam_step")

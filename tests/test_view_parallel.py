@@ -313,3 +313,102 @@ def test_launch_ranks_starts_world_ranks(world, monkeypatch):
     for o in outs:
         assert torch.equal(o["flat"], torch.full_like(o["flat"], 21.0))   # 1 + 2 + ... + 6
         assert torch.equal(o["radii"], torch.full((8,), 6, dtype=torch.int32))
+
+
+# ---- the sharded optimizer step (ShardedAdam: reduce-scatter, Adam on row shards, all-gather) --------
+LRS_SH = {"xyz": 1.6e-4, "f_dc": 2.5e-3, "f_rest": 2.5e-3 / 20, "opacity": 0.05, "scaling": 5e-3, "rotation": 1e-3,
+          "language_feature": 2.5e-3}
+
+
+def _np_adam(p, g, m, v, lr, step):
+    """the numpy restatement of torch.optim.Adam (oracle/train_oracle.py, pinned by train_golden.npz)."""
+    import train_oracle
+    pn, mn, vn = p.numpy(), m.numpy(), v.numpy()
+    train_oracle.adam_step(pn, g.numpy(), mn, vn, lr, step)
+
+
+def _raw_scene(seed=3):
+    """raw parameters and the scene of their activations (render()'s: exp, normalize, sigmoid, SH cat,
+    language / (|language| + 1e-9))."""
+    sc = synthetic.make_scene(P, C=C, tanfovx=0.6, tanfovy=0.6 * H / W, seed=seed, logscale_mean=-4.0)
+    g = torch.Generator().manual_seed(seed)
+    raw = dict(xyz=sc.means3D.clone(), f_dc=sc.shs[:, :1].clone(), f_rest=sc.shs[:, 1:].clone(),
+               opacity=torch.logit(sc.opacities.reshape(P, 1)).clone(), scaling=torch.log(sc.scales).clone(),
+               rotation=sc.rotations * (0.5 + torch.rand(P, 1, generator=g)),
+               language_feature=sc.lang * (1 + 2 * torch.rand(P, 1, generator=g)))
+    sc.rotations = torch.nn.functional.normalize(raw["rotation"])
+    sc.lang = raw["language_feature"] / (raw["language_feature"].norm(dim=-1, keepdim=True) + 1e-9)
+    return sc, raw
+
+
+def test_sharded_adam_single_rank_equals_autograd_and_torch_adam():
+    """world 1: the activations' backward and the Adam step of ShardedAdam against torch autograd
+    through the same activations and torch.optim.Adam(eps=1e-15) (gaussian_model.py:301)."""
+    from view_parallel import ShardedAdam
+    sc, raw = _raw_scene()
+    up = ShardedAdam(sc, raw, LRS_SH, adam=_np_adam)
+    b = GradBucket(P, 16, C, "cpu", row_multiple=ShardedAdam.row_multiple(P, 1))
+    gen = torch.Generator().manual_seed(5)
+    for name in ("means3D", "scales", "rotations", "opacities", "sh", "language_feature"):
+        b.views[name].copy_(torch.randn(b.views[name].shape, generator=gen) * 1e-3)
+    leaves = {k: v.clone().requires_grad_(True) for k, v in raw.items()}
+    act = dict(means3D=leaves["xyz"], scales=torch.exp(leaves["scaling"]),
+               rotations=torch.nn.functional.normalize(leaves["rotation"]),
+               opacities=torch.sigmoid(leaves["opacity"]), sh=torch.cat([leaves["f_dc"], leaves["f_rest"]], 1),
+               language_feature=leaves["language_feature"] / (leaves["language_feature"].norm(dim=-1, keepdim=True)
+                                                              + 1e-9))
+    sum((act[k] * b.views[k].reshape(act[k].shape)).sum() for k in act).backward()
+    opt = torch.optim.Adam([{"params": [leaves[k]], "lr": LRS_SH[k]} for k in leaves], lr=0.0, eps=1e-15)
+    opt.step()
+    up.step(b)
+    for k in raw:
+        ref = leaves[k].detach()
+        assert torch.allclose(up.raw[k], ref, rtol=1e-5, atol=1e-6), (k, float((up.raw[k] - ref).abs().max()))
+    # the scene now renders the updated parameters' activations
+    assert torch.allclose(sc.scales, torch.exp(leaves["scaling"].detach()), rtol=1e-5)
+    assert torch.allclose(sc.opacities, torch.sigmoid(leaves["opacity"].detach()), rtol=1e-5, atol=1e-7)
+
+
+def _sharded_worker(rank, world, port, outdir, steps):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from view_parallel import ShardedAdam
+        sc, raw = _raw_scene()
+        _, cams = _scene_and_cams()
+        up = ShardedAdam(sc, raw, LRS_SH, adam=_np_adam)
+        b = GradBucket(P, 16, C, "cpu", densify_stats=True, row_multiple=ShardedAdam.row_multiple(P, world))
+        step = ViewParallelStep(b, N_VIEWS, update=up)
+        render = oracle_renderer(sc, cams, batched=True)
+        for _ in range(steps):
+            step.run(render)
+        torch.save(dict(raw={k: v.clone() for k, v in up.raw.items()}, rows=(up.r0, up.r1),
+                        act={k: getattr(sc, k).clone() for k in ("means3D", "scales", "rotations", "opacities", "shs",
+                                                                  "lang")},
+                        radii=b.radii.clone()), os.path.join(outdir, f"rank{rank}.pt"))
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
+def test_sharded_step_two_ranks_equals_serial():
+    """Two optimizer steps of the view batch: world 2 (reduce-scatter, Adam on each rank's half of the
+    rows, all-gather) against one process doing every view and every row.  The parameters and the
+    activated inputs agree up to the fp32 reassociation of the view sums."""
+    with tempfile.TemporaryDirectory() as d:
+        _sharded_worker(0, 1, 0, d, 2)
+        ser = torch.load(os.path.join(d, "rank0.pt"), weights_only=True)
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_sharded_worker, args=(2, _free_port(), d, 2), nprocs=2, join=True)
+        outs = [torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(2)]
+    assert outs[0]["rows"][1] == outs[1]["rows"][0] and outs[1]["rows"][1] == P and outs[0]["rows"][0] == 0
+    for k, v in ser["raw"].items():
+        got = torch.cat([outs[0]["raw"][k], outs[1]["raw"][k]])
+        moved = (v - _raw_scene()[1][k]).abs().max()
+        assert float(moved) > 0, k
+        assert torch.allclose(got, v, rtol=1e-5, atol=1e-6), (k, float((got - v).abs().max()))
+    for k, v in ser["act"].items():
+        assert torch.equal(outs[0]["act"][k], outs[1]["act"][k]), k      # every rank renders the same scene
+        assert torch.allclose(outs[0]["act"][k], v, rtol=1e-5, atol=1e-6), k
+    assert torch.equal(outs[0]["radii"], ser["radii"])
