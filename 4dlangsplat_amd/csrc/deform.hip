@@ -406,10 +406,11 @@ void launch_deform_fwd(const DeformArgs& a, hipStream_t st) {
 
 // ==== backward ====================================================================================
 // Phase A, one block per 64 Gaussians (the forward's tiling): recompute the features X and the
-// chain A_k = relu(H_k) (saved); per head, Z1 = A W1^T + b1 (A1 = relu(Z1) saved), the gradient G
-// of the head's output (the upstream gradient, or for the quaternion product / the discrete
-// combination their per-Gaussian backward from the recomputed output), dZ1 = (G W2) * [Z1 > 0]
-// (saved), and dA += dZ1 W1, all on the bf16 hi/lo MFMA of the forward with transposed weight
+// chain A_k = relu(H_k) (saved); per head, Z1 = A W1^T + b1, the gradient G of the head's output
+// (the upstream gradient, or for the quaternion product / the discrete combination their
+// per-Gaussian backward from the recomputed output), dZ1 = (G W2) * [Z1 > 0], and dA += dZ1 W1
+// (the heads' Z1 / dZ1 are not saved: k_head_wgrad recomputes them for the weight gradients), all
+// on the bf16 hi/lo MFMA of the forward with transposed weight
 // packs; then back through the chain, dH_k = dA_k * [H_k > 0] (saved), dA_{k-1} = dH_k W_k, and
 // dX = dH_0 W_0; and per Gaussian the HexPlane backward: each plane's sample gets dX times the
 // product of the other five planes of its scale, scattered to the 4 bilinear taps (float atomics
@@ -421,21 +422,20 @@ constexpr int DGP = 64 + 8;   // LDS row pitch (bf16) of the upstream-gradient r
 // one-layer chain of every reference config gets its own instantiation: the runtime-length loops
 // cost registers (spills) even when they run once.
 template <int S, bool DEEP>
-__global__ void __launch_bounds__(256) k_deform_bwd_a(DeformBwdArgs b) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? 1 : 2, 2))) k_deform_bwd_a(DeformBwdArgs b) {
     constexpr int F = 16 * S, XP = F + 8;
     static_assert(XP <= DAP, "feature rows live in the second hidden buffer");
     __shared__ __attribute__((aligned(16))) __bf16 s_hh[2][DN * DAP];
     __shared__ __attribute__((aligned(16))) __bf16 s_hl[2][DN * DAP];
     __bf16* const s_xh = s_hh[1];   // read by the first layer only, which writes buffer 0
     __bf16* const s_xl = s_hl[1];
-    __shared__ __attribute__((aligned(16))) __bf16 s_gh[DN * DGP];
-    __shared__ __attribute__((aligned(16))) __bf16 s_gl[DN * DGP];
-    __shared__ float s_dx[DN][F + 1];
-    __shared__ float s_sdv[4][16][17];   // plane scatter staging, per wave: dv of 16 Gaussians
-    __shared__ int s_soff[4][16][4];     //   their 4 tap offsets
-    __shared__ float s_sw[4][16][4];     //   and bilinear weights
-    LDS_POISON(s_hh); LDS_POISON(s_hl); LDS_POISON(s_gh); LDS_POISON(s_gl); LDS_POISON(s_dx);
-    LDS_POISON(s_sdv); LDS_POISON(s_soff); LDS_POISON(s_sw); LDS_POISON_DONE();
+    // Everything else lives in a hidden buffer while that buffer is dead (68 KB in all: two blocks
+    // per CU): a head's G rows in the buffer its dZ1 rows take next (a barrier between the two), dX in
+    // the chain's dead buffer, the plane-scatter staging in its lo half; every hand-over is a
+    // __syncthreads, and the LDS-poison build checks that nothing reads a word its block never wrote.
+    static_assert(DN * (F + 1) * 4 <= DN * DAP * 2, "dX rows fit one hidden buffer");
+    static_assert((4 * 16 * 17 + 2 * 4 * 16 * 4) * 4 <= DN * DAP * 2, "scatter staging fits one hidden buffer");
+    LDS_POISON(s_hh); LDS_POISON(s_hl); LDS_POISON_DONE();
     const DeformArgs& a = b.f;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int g0 = blockIdx.x * DN;
@@ -469,7 +469,6 @@ __global__ void __launch_bounds__(256) k_deform_bwd_a(DeformBwdArgs b) {
     __bf16 *bh = s_hh[cur ^ 1], *bl = s_hl[cur ^ 1];
 
     df32x16 dA[2] = {df32x16{}, df32x16{}};
-    int slot = 0;
     for (int hd = 0; hd < DEF_HEADS; ++hd) {
         if (!((a.heads >> hd) & 1u)) continue;                       // block-uniform
         const int nout = head_out(a, hd);
@@ -480,18 +479,12 @@ __global__ void __launch_bounds__(256) k_deform_bwd_a(DeformBwdArgs b) {
             df32x16 z[2] = {df32x16{}, df32x16{}};
             mlp_ntile<DWID>(z, ah, al, DAP, wave, a.w1_h[hd], a.w1_l[hd]);
             const float bias = a.b1[hd][col];
-            float* sA1 = b.sA1[slot];
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    const float zz = z[mt][q] + bias;
-                    zpos |= zz > 0.0f ? 1u << (16 * mt + q) : 0u;
-                    const int r = row_of(mt, q, hh), g = g0 + r;
-                    if (g < a.P) sA1[(size_t)g * DWID + col] = fmaxf(zz, 0.0f);
-                }
+                for (int q = 0; q < 16; ++q) zpos |= z[mt][q] + bias > 0.0f ? 1u << (16 * mt + q) : 0u;
         }
-        // gradient rows of this head's output, K padded to 64
+        // gradient rows of this head's output, K padded to 64, in the buffer dZ1 takes next
         const float* G = coff ? b.sG_coff : quat ? b.sG_rot : b.up[hd];   // saved by the GRAD pass
         for (int i = tid; i < DN * 64; i += 256) {
             const int r = i >> 6, k = i & 63, g = g0 + r;
@@ -499,31 +492,27 @@ __global__ void __launch_bounds__(256) k_deform_bwd_a(DeformBwdArgs b) {
             if (k < nout && g < a.P) v = G[(size_t)g * nout + k];
             __bf16 hi, lo;
             dsplit(v, hi, lo);
-            s_gh[r * DGP + k] = hi;
-            s_gl[r * DGP + k] = lo;
+            bh[r * DGP + k] = hi;
+            bl[r * DGP + k] = lo;
         }
-        __syncthreads();   // G rows complete (and the A1 rows consumed)
+        __syncthreads();   // G rows complete
         df32x16 d[2] = {df32x16{}, df32x16{}};
-        mlp_ntile<64>(d, s_gh, s_gl, DGP, wave, b.w2t_h[hd], b.w2t_l[hd]);
-        {
-            float* sdZ1 = b.sdZ1[slot];
+        mlp_ntile<64>(d, bh, bl, DGP, wave, b.w2t_h[hd], b.w2t_l[hd]);
+        __syncthreads();   // every wave has read the G rows: dZ1 overwrites them
 #pragma unroll
-            for (int mt = 0; mt < 2; ++mt)
+        for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    const int r = row_of(mt, q, hh), g = g0 + r;
-                    const float v = (zpos >> (16 * mt + q)) & 1u ? d[mt][q] : 0.0f;
-                    __bf16 hi, lo;
-                    dsplit(v, hi, lo);
-                    bh[r * DAP + col] = hi;
-                    bl[r * DAP + col] = lo;
-                    if (g < a.P) sdZ1[(size_t)g * DWID + col] = v;
-                }
-        }
+            for (int q = 0; q < 16; ++q) {
+                const int r = row_of(mt, q, hh);
+                const float v = (zpos >> (16 * mt + q)) & 1u ? d[mt][q] : 0.0f;
+                __bf16 hi, lo;
+                dsplit(v, hi, lo);
+                bh[r * DAP + col] = hi;
+                bl[r * DAP + col] = lo;
+            }
         __syncthreads();   // dZ1 rows complete
         mlp_ntile<DWID>(dA, bh, bl, DAP, wave, b.w1t_h[hd], b.w1t_l[hd]);
-        __syncthreads();   // dZ1 / G rows consumed before the next head rewrites them
-        ++slot;
+        __syncthreads();   // dZ1 rows consumed before the next head's G rows overwrite them
     }
 
     // ---- back through the chain: dH_k = dA_k * [H_k > 0] (saved), dA_{k-1} = dH_k W_k -------------
@@ -555,15 +544,23 @@ __global__ void __launch_bounds__(256) k_deform_bwd_a(DeformBwdArgs b) {
             df32x16 acc[2] = {df32x16{}, df32x16{}};
             mlp_ntile<DWID>(acc, dh_h, dh_l, DAP, wave, b.wft_h[0], b.wft_l[0]);
             const int c = 32 * wave + (lane & 31);
+            // dX rows [64][F + 1] in the other hidden buffer (its rows died with the heads)
+            float* dxw = reinterpret_cast<float*>(s_hh[cur ^ 1]);
             if (c < F) {
 #pragma unroll
                 for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-                    for (int q = 0; q < 16; ++q) s_dx[row_of(mt, q, hh)][c] = acc[mt][q];
+                    for (int q = 0; q < 16; ++q) dxw[row_of(mt, q, hh) * (F + 1) + c] = acc[mt][q];
             }
         }
     }
     __syncthreads();
+    const float* s_dx = reinterpret_cast<const float*>(s_hh[cur ^ 1]);   // [64][F + 1]
+    // plane-scatter staging in the lo half of that buffer: per wave, dv of 16 Gaussians [16][17],
+    // their 4 tap offsets and bilinear weights
+    float* const s_sdv = reinterpret_cast<float*>(s_hl[cur ^ 1]);
+    int* const s_soff = reinterpret_cast<int*>(s_sdv + 4 * 16 * 17);
+    float* const s_sw = reinterpret_cast<float*>(s_soff + 4 * 16 * 4);
 
     // ---- HexPlane backward: 4 threads per Gaussian, 4 channels each ----------------------------------
     {
@@ -578,8 +575,8 @@ __global__ void __launch_bounds__(256) k_deform_bwd_a(DeformBwdArgs b) {
             float4 v[6];
 #pragma unroll
             for (int ci = 0; ci < 6; ++ci) v[ci] = sample4(a, 6 * s + ci, tap_of(a, 6 * s + ci, ci, crd), q);
-            const float dxv[4] = {s_dx[gl][16 * s + 4 * q], s_dx[gl][16 * s + 4 * q + 1], s_dx[gl][16 * s + 4 * q + 2],
-                                  s_dx[gl][16 * s + 4 * q + 3]};
+            const float* dxr = s_dx + gl * (F + 1) + 16 * s + 4 * q;
+            const float dxv[4] = {dxr[0], dxr[1], dxr[2], dxr[3]};
 #pragma unroll
             for (int ci = 0; ci < 6; ++ci) {
                 float4 oth = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
@@ -607,19 +604,21 @@ __global__ void __launch_bounds__(256) k_deform_bwd_a(DeformBwdArgs b) {
                 {
                     const int wl = gl & 15;
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) s_sdv[wave][wl][4 * q + i] = ok ? dv[i] : 0.0f;
+                    for (int i = 0; i < 4; ++i) s_sdv[(wave * 16 + wl) * 17 + 4 * q + i] = ok ? dv[i] : 0.0f;
                     if (q == 0) {
-                        s_soff[wave][wl][0] = (t.y0 * W + t.x0) * 16; s_soff[wave][wl][1] = (t.y0 * W + t.x1) * 16;
-                        s_soff[wave][wl][2] = (t.y1 * W + t.x0) * 16; s_soff[wave][wl][3] = (t.y1 * W + t.x1) * 16;
-                        s_sw[wave][wl][0] = w00; s_sw[wave][wl][1] = w01; s_sw[wave][wl][2] = w10; s_sw[wave][wl][3] = w11;
+                        int* so = s_soff + (wave * 16 + wl) * 4;
+                        float* sw = s_sw + (wave * 16 + wl) * 4;
+                        so[0] = (t.y0 * W + t.x0) * 16; so[1] = (t.y0 * W + t.x1) * 16;
+                        so[2] = (t.y1 * W + t.x0) * 16; so[3] = (t.y1 * W + t.x1) * 16;
+                        sw[0] = w00; sw[1] = w01; sw[2] = w10; sw[3] = w11;
                     }
                     wave_lds_sync();
                     float* gp = b.dplanes + (size_t)(blockIdx.x % b.replicas) * b.plane_stride + a.poff[pi];
                     const int tap = lane >> 4, ch = lane & 15;
 #pragma unroll 4
                     for (int j = 0; j < 16; ++j) {
-                        const float val = s_sdv[wave][j][ch] * s_sw[wave][j][tap];
-                        if (val != 0.0f) atomicAdd(gp + s_soff[wave][j][tap] + ch, val);
+                        const float val = s_sdv[(wave * 16 + j) * 17 + ch] * s_sw[(wave * 16 + j) * 4 + tap];
+                        if (val != 0.0f) atomicAdd(gp + s_soff[(wave * 16 + j) * 4 + tap] + ch, val);
                     }
                     wave_lds_sync();   // staging read before the next plane rewrites it
                 }
@@ -864,6 +863,180 @@ void launch_lang_deform_fwd(const LangDeformArgs& a, hipStream_t st) {
 }
 void launch_lang_deform_bwd(const LangDeformArgs& a, hipStream_t st) {
     if (a.P > 0) hipLaunchKernelGGL(k_lang_deform_bwd, dim3((a.P + DN - 1) / DN), dim3(256), 0, st, a);
+}
+
+// ==== head weight gradients by recompute ===========================================================
+// Round 3 saved every head's relu(Z1) and dZ1 rows in phase A (2 x 128 floats per Gaussian per head:
+// 10 GB written and read back at 2M Gaussians with five heads) for the split-K products of k_atb.
+// Here a block walks its rows in tiles of 64 and recomputes them from the saved trunk activation A
+// (512 B per row) and the head's output gradient G:
+//   Z1 = A W1^T + b1 (mlp_ntile, as the forward),  dZ1 = (G W2) * [Z1 > 0] (as phase A),
+//   dW1 += dZ1^T A,  dW2 += G^T relu(Z1),  db1 += sum dZ1,  db2 += sum G,
+// accumulating the block's partial products in registers over all its tiles; one atomic per output
+// element at the end.  The reduction index of the last two products is the row: wave w holds
+// dZ1 and relu(Z1) for its 32 columns in the MFMA result layout, whose rows split 4 / 4 between the
+// two half-waves, so one permlane32 swap per register pair turns them into the row-runs of 8 the
+// 32x32x16 operands take; the A and G operands come from their LDS rows through transposing reads.
+// Rows past P read as zero (their dZ1 and G vanish, so relu(b1) never reaches a product).
+__device__ __forceinline__ void wg_regs_to_op(const df32x16& v, int u, dbf16x8& oh, dbf16x8& ol) {
+    // rows 16u .. 16u + 15 of this 32-row M tile: lane half h gets rows 16u + 8h .. + 7
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[8 * u + i]), __float_as_uint(v[8 * u + 4 + i]),
+                                                  false, false);
+        const float x0 = __uint_as_float(r[0]), x1 = __uint_as_float(r[1]);
+        __bf16 h0, l0, h1, l1;
+        dsplit(x0, h0, l0);
+        dsplit(x1, h1, l1);
+        oh[i] = h0; ol[i] = l0;
+        oh[4 + i] = h1; ol[4 + i] = l1;
+    }
+}
+// 8 consecutive rows (16 ks + 8 h ..) of column c0 + (lane & 31) of a row-major bf16 LDS array,
+// through two ds_read_b64_tr_b16 (each 16-lane group reads a 4-row x 16-column block)
+__device__ __forceinline__ dbf16x8 wg_lds_op(const __bf16* base, int pitch, int ks, int c0) {
+    const int lane = threadIdx.x & 63, h = lane >> 5, l16 = lane & 15;
+    const __bf16* p = base + (16 * ks + 8 * h + (l16 >> 2)) * pitch + c0 + 16 * ((lane >> 4) & 1) + 4 * (l16 & 3);
+    typedef short s16x4 __attribute__((ext_vector_type(4)));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        reinterpret_cast<__attribute__((address_space(3))) s16x4*>(reinterpret_cast<size_t>(p)));
+    const s16x4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        reinterpret_cast<__attribute__((address_space(3))) s16x4*>(reinterpret_cast<size_t>(p + 4 * pitch)));
+    const s16x8 v = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(dbf16x8, v);
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) k_head_wgrad(HeadWgradArgs ha) {
+    __shared__ __attribute__((aligned(16))) __bf16 s_ah[DN * DAP];   // A rows [64][128] hi / lo
+    __shared__ __attribute__((aligned(16))) __bf16 s_al[DN * DAP];
+    __shared__ __attribute__((aligned(16))) __bf16 s_gh[DN * DGP];   // G rows [64][64 pad] hi / lo
+    __shared__ __attribute__((aligned(16))) __bf16 s_gl[DN * DGP];
+    LDS_POISON(s_ah); LDS_POISON(s_al); LDS_POISON(s_gh); LDS_POISON(s_gl); LDS_POISON_DONE();
+    const HeadWgradJob& j = ha.job[blockIdx.y];
+    const int64_t row0 = (int64_t)blockIdx.x * ha.rows_per_block;
+    const int64_t row1 = min((int64_t)ha.P, row0 + ha.rows_per_block);
+    if (row0 >= row1) return;                                            // block-uniform
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+    const int nout = j.nout, Mo = (nout + 31) / 32;                      // G^T M tiles (1 or 2)
+    const int col = 32 * wave + r;
+    const float b1c = j.b1[col];
+    df32x16 w1acc[4] = {df32x16{}, df32x16{}, df32x16{}, df32x16{}};   // dW1 rows 32 wave .., col tiles 0..3
+    df32x16 w2acc[2] = {df32x16{}, df32x16{}};                            // dW2 o tiles 0..1, col tile wave
+    float db1 = 0.0f, db2 = 0.0f;
+    for (int64_t t0 = row0; t0 < row1; t0 += DN) {
+        // ---- A and G rows of the tile into LDS (fp32 -> bf16 hi / lo); rows past P are zero --------
+        for (int i = tid; i < DN * (DWID / 4); i += 256) {
+            const int rr = i >> 5, c4 = (i & 31) * 4;
+            const int64_t g = t0 + rr;
+            const float4 v = g < row1 ? *reinterpret_cast<const float4*>(ha.A + g * DWID + c4)
+                                      : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            const float f[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                __bf16 hi, lo;
+                dsplit(f[e], hi, lo);
+                s_ah[rr * DAP + c4 + e] = hi;
+                s_al[rr * DAP + c4 + e] = lo;
+            }
+        }
+        for (int i = tid; i < DN * 64; i += 256) {
+            const int rr = i >> 6, k = i & 63;
+            const int64_t g = t0 + rr;
+            const float v = (k < nout && g < row1) ? j.G[g * nout + k] : 0.0f;
+            __bf16 hi, lo;
+            dsplit(v, hi, lo);
+            s_gh[rr * DGP + k] = hi;
+            s_gl[rr * DGP + k] = lo;
+        }
+        if (tid < nout) {   // db2: column sums of G over the tile (thread per output)
+            float sg = 0.0f;
+            for (int rr = 0; rr < DN; ++rr) {
+                const int64_t g = t0 + rr;
+                if (g < row1) sg += j.G[g * nout + tid];
+            }
+            db2 += sg;
+        }
+        __syncthreads();
+        // ---- Z1 for this wave's 32 columns (both row tiles): relu(Z1) -> dW2 += G^T relu(Z1) -------------
+        uint32_t zpos = 0;   // bit 16 mt + q: Z1 > 0
+        {
+            df32x16 z[2] = {df32x16{}, df32x16{}};
+            mlp_ntile<DWID>(z, s_ah, s_al, DAP, wave, j.w1_h, j.w1_l);
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const float zz = z[mt][q] + b1c;
+                    zpos |= zz > 0.0f ? 1u << (16 * mt + q) : 0u;
+                    z[mt][q] = fmaxf(zz, 0.0f);
+                }
+#pragma unroll
+            for (int ks = 0; ks < DN / 16; ++ks) {
+                dbf16x8 zh, zl;
+                wg_regs_to_op(z[ks >> 1], ks & 1, zh, zl);
+#pragma unroll
+                for (int mo = 0; mo < 2; ++mo) {
+                    if (mo >= Mo) break;
+                    const dbf16x8 gh = wg_lds_op(s_gh, DGP, ks, 32 * mo), gl = wg_lds_op(s_gl, DGP, ks, 32 * mo);
+                    w2acc[mo] = DMFMA(gh, zh, w2acc[mo]);
+                    w2acc[mo] = DMFMA(gh, zl, w2acc[mo]);
+                    w2acc[mo] = DMFMA(gl, zh, w2acc[mo]);
+                }
+            }
+        }
+        // ---- dZ1 = (G W2) [Z1 > 0] -> dW1 += dZ1^T A (rows 32 wave .. of dW1), db1 ------------------------
+        {
+            df32x16 d[2] = {df32x16{}, df32x16{}};
+            mlp_ntile<64>(d, s_gh, s_gl, DGP, wave, j.w2t_h, j.w2t_l);
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    d[mt][q] = (zpos >> (16 * mt + q)) & 1u ? d[mt][q] : 0.0f;
+                    db1 += d[mt][q];
+                }
+#pragma unroll
+            for (int ks = 0; ks < DN / 16; ++ks) {
+                dbf16x8 dh, dl;
+                wg_regs_to_op(d[ks >> 1], ks & 1, dh, dl);
+#pragma unroll
+                for (int nt = 0; nt < 4; ++nt) {
+                    const dbf16x8 bh = wg_lds_op(s_ah, DAP, ks, 32 * nt), bl = wg_lds_op(s_al, DAP, ks, 32 * nt);
+                    w1acc[nt] = DMFMA(dh, bh, w1acc[nt]);
+                    w1acc[nt] = DMFMA(dh, bl, w1acc[nt]);
+                    w1acc[nt] = DMFMA(dl, bh, w1acc[nt]);
+                }
+            }
+        }
+        __syncthreads();   // the tile's LDS rows read before the next tile overwrites them
+    }
+    // ---- the block's partial products: one atomic per element ------------------------------------------
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int m = 32 * wave + (q & 3) + 8 * (q >> 2) + 4 * hh;
+            atomicAdd(j.dW1 + (size_t)m * DWID + 32 * nt + r, w1acc[nt][q]);
+        }
+#pragma unroll
+    for (int mo = 0; mo < 2; ++mo) {
+        if (mo >= Mo) break;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int o = 32 * mo + (q & 3) + 8 * (q >> 2) + 4 * hh;
+            if (o < nout) atomicAdd(j.dW2 + (size_t)o * DWID + col, w2acc[mo][q]);
+        }
+    }
+    db1 += __shfl_xor(db1, 32);
+    if (hh == 0) atomicAdd(j.db1 + col, db1);
+    if (tid < nout) atomicAdd(j.db2 + tid, db2);
+}
+
+void launch_head_wgrad(const HeadWgradArgs& a, int njobs, hipStream_t st) {
+    if (a.P <= 0 || njobs <= 0) return;
+    const int nb = (a.P + a.rows_per_block - 1) / a.rows_per_block;
+    hipLaunchKernelGGL(k_head_wgrad, dim3(nb, njobs), dim3(256), 0, st, a);
 }
 
 // Phase B: C[M][N] += sum_g L[g][m] R[g][n] (M, N <= 128), bias[m] += sum_g L[g][m]; split-K over

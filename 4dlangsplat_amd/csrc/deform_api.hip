@@ -259,7 +259,7 @@ lsr::LangDeformArgs lang_args(const lsr_deform_net* net, const void* workspace, 
 // backward scratch: saved activations, then kGradReplicas copies of the packed gradient planes
 constexpr int kGradReplicas = 16;
 struct BwdScratch {
-    size_t X, A[LSR_DEFORM_MAX_DEPTH], dH[LSR_DEFORM_MAX_DEPTH], A1[LSR_DEFORM_HEADS], dZ1[LSR_DEFORM_HEADS];
+    size_t X, A[LSR_DEFORM_MAX_DEPTH], dH[LSR_DEFORM_MAX_DEPTH];
     size_t Grot, Gcoff, U0, U1, U2, dv, dZ2l, dZ1l, dplanes, total;
 };
 BwdScratch bwd_scratch(const lsr_deform_net* net, size_t P) {
@@ -275,13 +275,6 @@ BwdScratch bwd_scratch(const lsr_deform_net* net, size_t P) {
     for (int k = 0; k < nlayers(net); ++k) {
         s.A[k] = take(P * kW);
         s.dH[k] = take(P * kW);
-    }
-    int slot = 0;
-    for (int hd = 0; hd < LSR_DEFORM_HEADS; ++hd) {
-        if (!head_on(net, hd)) continue;
-        s.A1[slot] = take(P * kW);
-        s.dZ1[slot] = take(P * kW);
-        ++slot;
     }
     s.Grot = take(net->apply_rotation ? P * 4 : 1);
     s.Gcoff = take(net->lang_mode == LSR_DEFORM_LANG_DISCRETE ? P * net->centers : 1);
@@ -394,14 +387,10 @@ extern "C" int lsr_deform_backward(const lsr_deform_net* net, const void* worksp
         b.sA[k] = fp(S.A[k]);
         b.sdH[k] = fp(S.dH[k]);
     }
-    int slot = 0;
     for (int hd = 0; hd < LSR_DEFORM_HEADS; ++hd) {
         if (!head_on(net, hd)) continue;
         b.w1t_h[hd] = chi<__bf16>(ws, L.w1t[hd]); b.w1t_l[hd] = clo<__bf16>(ws, L.w1t[hd]);
         b.w2t_h[hd] = chi<__bf16>(ws, L.w2t[hd]); b.w2t_l[hd] = clo<__bf16>(ws, L.w2t[hd]);
-        b.sA1[slot] = fp(S.A1[slot]);
-        b.sdZ1[slot] = fp(S.dZ1[slot]);
-        ++slot;
     }
     for (int hd = 0; hd < 5; ++hd) b.up[hd] = ups[hd];
     b.up_lang = d_out_lang;
@@ -429,8 +418,9 @@ extern "C" int lsr_deform_backward(const lsr_deform_net* net, const void* worksp
         la.sdv = fp(S.dv); la.sdZ2 = fp(S.dZ2l); la.sdZ1 = fp(S.dZ1l);
         lsr::launch_lang_deform_bwd(la, st);
     }
-    // weight gradients, split-K over ~256 row blocks: the feature_out chain, every computed head,
-    // and lang_deform
+    // weight gradients, split-K over ~256 row blocks: the feature_out chain and lang_deform as A^T B
+    // products of saved rows (k_atb); every computed head by recompute from the trunk's last
+    // activation (k_head_wgrad: no per-head rows saved)
     lsr::AtbArgs g{};
     g.P = P;
     const int64_t per = ((int64_t)P + 255) / 256;
@@ -440,15 +430,18 @@ extern "C" int lsr_deform_backward(const lsr_deform_net* net, const void* worksp
     for (int k = 0; k < b.f.nlayers; ++k)
         g.job[nj++] = lsr::AtbJob{b.sdH[k], k == 0 ? b.sX : b.sA[k - 1], grads->w_feat[k], grads->b_feat[k], kW,
                                   k == 0 ? F : kW};
-    slot = 0;
-    const float* last = b.sA[b.f.nlayers - 1];
+    lsr::HeadWgradArgs hw{};
+    hw.A = b.sA[b.f.nlayers - 1];
+    hw.P = P;
+    hw.rows_per_block = g.rows_per_block;
+    int nh = 0;
     for (int hd = 0; hd < LSR_DEFORM_HEADS; ++hd) {
         if (!head_on(net, hd)) continue;
         const float* G = hd == 5 ? b.sG_coff : (hd == 2 && net->apply_rotation) ? b.sG_rot : ups[hd];
-        g.job[nj++] = lsr::AtbJob{b.sdZ1[slot], last, grads->w1[hd], grads->b1[hd], kW, kW};
-        g.job[nj++] = lsr::AtbJob{G, b.sA1[slot], grads->w2[hd], grads->b2[hd], head_out(net, hd), kW};
-        ++slot;
+        hw.job[nh++] = lsr::HeadWgradJob{G, b.f.w1_h[hd], b.f.w1_l[hd], b.f.b1[hd], b.w2t_h[hd], b.w2t_l[hd],
+                                         grads->w1[hd], grads->b1[hd], grads->w2[hd], grads->b2[hd], head_out(net, hd)};
     }
+    lsr::launch_head_wgrad(hw, nh, st);
     if (lang_mlp(net)) {
         g.job[nj++] = lsr::AtbJob{la.sdZ1, la.sU0, grads->w_lang[0], grads->b_lang[0], kW, la.kin};
         g.job[nj++] = lsr::AtbJob{la.sdZ2, la.sU1, grads->w_lang[1], grads->b_lang[1], kW, kW};

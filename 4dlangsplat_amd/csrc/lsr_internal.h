@@ -300,13 +300,30 @@ struct DeformBwdArgs {
     float* sX;                        // saved [P, 16 n_scales] features
     float* sA[DEF_MAX_LAYERS];        // saved [P,128] relu(H_k)
     float* sdH[DEF_MAX_LAYERS];       // saved [P,128] gradients of H_k
-    float* sA1[DEF_HEADS];            // per computed head: [P,128] relu(Z1)
-    float* sdZ1[DEF_HEADS];           //                    [P,128] gradient of Z1
     float* sG_rot;                    // apply_rotation: [P,4] gradient of the rotation head's output
     float* sG_coff;                   // DISCRETE: [P, centers] gradient of coff
     float* daabb;                     // [2][3] gradient of the HexPlane box (accumulated), or null
 };
 void launch_deform_bwd_a(const DeformBwdArgs& a, hipStream_t st);
+// Weight gradients of the computed heads by recompute (deform.hip k_head_wgrad): per head and block
+// of rows, from the saved last trunk activation A and the head's output gradient G,
+// Z1 = A W1^T + b1, dZ1 = (G W2) [Z1 > 0]; dW1 += dZ1^T A, db1 += sum dZ1, dW2 += G^T relu(Z1),
+// db2 += sum G.  One launch for every head (grid row = job).
+struct HeadWgradJob {
+    const float* G;                   // [P][nout]
+    const __bf16 *w1_h, *w1_l;        // forward pack [128][128]
+    const float* b1;
+    const __bf16 *w2t_h, *w2t_l;      // backward pack [128][64] (W2 transposed, K padded to 64)
+    float *dW1, *db1, *dW2, *db2;     // accumulated
+    int nout;
+};
+constexpr int DEF_WGRAD_MAX_JOBS = DEF_HEADS;
+struct HeadWgradArgs {
+    HeadWgradJob job[DEF_WGRAD_MAX_JOBS];
+    const float* A;                   // [P][128] the trunk's last activation (phase A saved it)
+    int P, rows_per_block;
+};
+void launch_head_wgrad(const HeadWgradArgs& a, int njobs, hipStream_t st);
 struct AtbJob {                        // C[M][N] += sum_g L[g][m] R[g][n]; bias[m] += sum_g L[g][m]
     const float* L;
     const float* R;

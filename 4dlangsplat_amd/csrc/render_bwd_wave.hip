@@ -45,7 +45,6 @@ __device__ unsigned long long g_bwd_stamps[12];
 
 constexpr int WG = 16;       // compacted entries per MFMA group
 constexpr int WFP = 48;      // F row pitch in bf16 (32 channels + 16): the MFMA1 b128 reads conflict-free
-constexpr int WGB = 48;      // G row pitch in bf16 at the one-off build: 32 language + 16 pad
 // W / t rows [p][e]: 16 bf16 (32 B) per pixel p, unpadded and swizzled so that both the row
 // writes (ds_write_b64: 16-lane groups over 32 banks) and the transposing MFMA-operand reads
 // (ds_read_b64_tr_b16: 32-lane halves over 64 banks) are conflict-free: pixel p's row sits in row
@@ -53,6 +52,12 @@ constexpr int WGB = 48;      // G row pitch in bf16 at the one-off build: 32 lan
 // (The padded 40-byte rows cost 2 extra LDS cycles per transposing read.)
 __device__ __forceinline__ int wt_off(int p, int q) { return (p ^ (((p >> 3) & 1) << 2)) * 16 + 4 * (q ^ ((p >> 2) & 3)); }
 constexpr int WFIFO = 128;   // compacted entries waiting (list positions and ids); power of two
+// G rows [p][c] (the pixels' language gradients, 32 channels, bf16 hi and lo) stay in LDS for the
+// whole wave instead of as 64 VGPRs of resident B fragments: 64 B per row, unpadded, with 16-byte
+// chunk q of row p in chunk q ^ ((p >> 2) & 3), so both per-group reads are conflict-free -- MFMA1's
+// B (row 16 pb + l16, chunk g4: 16 rows x 4 dwords over 64 banks) and MFMA-W's B through transposing
+// reads (4 rows x 16 columns per 16-lane group, two groups eight rows apart per half-wave).
+__device__ __forceinline__ int g_off(int p, int q) { return p * 32 + 8 * (q ^ ((p >> 2) & 3)); }
 
 // C32: the 32-channel instantiation (headline), whose language rows are two float4 loads per lane
 // with no per-channel predication.  NOL: no language channels in play (include_feature off or
@@ -71,7 +76,9 @@ __attribute__((amdgpu_waves_per_eu(NOL ? LSR_BWD_WAVES_NOL : LSR_BWD_WAVES, NOL 
 k_render_bwd_wave(RenderBwdBatch ab) {
     const RenderBwdArgs& a = ab.v[blockIdx.y];   // grid row = view
     static_assert(!(NOL && C32), "NOL has no language channels");
-    __shared__ __attribute__((aligned(16))) __bf16 s_FR[64 * WGB];       // G rows (build), then F / W / t rows
+    __shared__ __attribute__((aligned(16))) __bf16 s_FR[64 * 32];        // bm build, then F / W / t rows
+    __shared__ __attribute__((aligned(16))) __bf16 s_Gh[NOL ? 8 : 64 * 32];   // G rows (g_off), hi / lo
+    __shared__ __attribute__((aligned(16))) __bf16 s_Gl[NOL ? 8 : 64 * 32];
     // group entries' screen-space data, one array per field (a b128 read gives 4 entries, a b64
     // pair the operand of a packed-fp32 instruction): centre X, Y; staged conic -a/2, -b, -c/2 (gauss_power); opacity; rgb,
     // depth; list position k (0xFFFFFFFF past the group: never active)
@@ -116,49 +123,32 @@ k_render_bwd_wave(RenderBwdBatch ab) {
         if (a.dL_ddepth) gD = a.dL_ddepth[pid];
     }
 
-    // ---- B fragments, built once through LDS rows [p][c] (c < 32 language channels):
-    // b1[pb]     : MFMA1 B,  K = channel 8 g4 + j,       N = pixel 16 pb + l16
-    // b2[kb][nb] : MFMA-W B, K = pixel 32 kb + 8 g4 + j, N = channel 16 nb + l16
-    // bm[kb]     : MFMA-T and the rgb / depth part of MFMA-W, K = pixel 32 kb + 8 g4 + j, N = l16:
-    //              the moments {1, x, y, x^2, xy, y^2} (exact small integers) in columns 0..5, the
-    //              pixel's rgb + depth gradients as bf16 hi in 6..9 and lo in 10..13, 0 in 14, 15
-    //              (one fragment for both products: each reads only its own columns)
-    bf16x8 b1h[4], b1l[4], b2h[2][2], b2l[2][2], bm[2];
+    // ---- B operands.  The language ones are read from the G rows in LDS per group:
+    // MFMA1 B   (pixel block pb): K = channel 8 g4 + j,       N = pixel 16 pb + l16      (g_b1)
+    // MFMA-W B  (kb, nb)        : K = pixel 32 kb + 8 g4 + j, N = channel 16 nb + l16    (g_b2)
+    // bm[kb] (resident): MFMA-T and the rgb / depth part of MFMA-W, K = pixel 32 kb + 8 g4 + j,
+    //              N = l16: the moments {1, x, y, x^2, xy, y^2} (exact small integers) in columns
+    //              0..5, the pixel's rgb + depth gradients as bf16 hi in 6..9 and lo in 10..13, 0 in
+    //              14, 15 (one fragment for both products: each reads only its own columns)
+    bf16x8 bm[2];
     {
-        if constexpr (!NOL) {
-        float gl[32];
+        if constexpr (!NOL) {   // this lane's pixel row of G, hi and lo
+            float gl[32];
 #pragma unroll
-        for (int c = 0; c < 32; ++c)
-            gl[c] = (inside && a.dL_dlang && c < C) ? a.dL_dlang[(size_t)c * HW + pid] : 0.0f;
-#pragma unroll
-        for (int part = 0; part < 2; ++part) {
+            for (int c = 0; c < 32; ++c)
+                gl[c] = (inside && a.dL_dlang && c < C) ? a.dL_dlang[(size_t)c * HW + pid] : 0.0f;
 #pragma unroll
             for (int c8 = 0; c8 < 4; ++c8) {
-                bf16x8 v;
+                bf16x8 vh, vl;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     __bf16 h, l;
                     split_bf16(gl[8 * c8 + j], h, l);
-                    v[j] = part == 0 ? h : l;
+                    vh[j] = h; vl[j] = l;
                 }
-                *reinterpret_cast<bf16x8*>(s_FR + lane * WGB + 8 * c8) = v;
+                *reinterpret_cast<bf16x8*>(s_Gh + g_off(lane, c8)) = vh;
+                *reinterpret_cast<bf16x8*>(s_Gl + g_off(lane, c8)) = vl;
             }
-            wave_lds_sync();
-            bf16x8* B1 = part == 0 ? b1h : b1l;
-#pragma unroll
-            for (int pb = 0; pb < 4; ++pb)
-                B1[pb] = *reinterpret_cast<const bf16x8*>(s_FR + (16 * pb + l16) * WGB + 8 * g4);
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                for (int nb = 0; nb < 2; ++nb) {
-                    const __bf16* p = s_FR + (32 * kb + 8 * g4 + (l16 >> 2)) * WGB + 16 * nb + 4 * (l16 & 3);
-                    const bf16x4 lo4 = ds_read_tr16(p), hi4 = ds_read_tr16(p + 4 * WGB);
-                    const bf16x8 v = __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7);
-                    if (part == 0) b2h[kb][nb] = v; else b2l[kb][nb] = v;
-                }
-            wave_lds_sync();
-        }
         }
         // bm rows [p][n], pitch 16: pixel p = lane has local x = p & 7, y = p >> 3
         {
@@ -186,6 +176,16 @@ k_render_bwd_wave(RenderBwdBatch ab) {
             wave_lds_sync();
         }
     }
+    // MFMA1's B: pixel rows 16 pb + l16, channels 8 g4 .. + 7
+    auto g_b1 = [&](const __bf16* G, int pb) {
+        return *reinterpret_cast<const bf16x8*>(G + g_off(16 * pb + l16, g4));
+    };
+    // MFMA-W's B: pixels 32 kb + 8 g4 + j, channel 16 nb + l16 (two transposing reads, rows +0 / +4)
+    auto g_b2 = [&](const __bf16* G, int kb, int nb) {
+        const int p = 32 * kb + 8 * g4 + (l16 >> 2), q = 2 * nb + ((l16 & 3) >> 1), o = 4 * (l16 & 1);
+        const bf16x4 lo4 = ds_read_tr16(G + g_off(p, q) + o), hi4 = ds_read_tr16(G + g_off(p + 4, q) + o);
+        return __builtin_shufflevector(lo4, hi4, 0, 1, 2, 3, 4, 5, 6, 7);
+    };
     __bf16* s_Fh = s_FR;              // F rows [e][c] of the group (MFMA1 A), hi
     __bf16* s_Fl = s_FR + WG * WFP;   // lo
     __bf16* s_Rh = s_FR;              // after MFMA1: W or t rows [p][e], hi
@@ -370,10 +370,11 @@ k_render_bwd_wave(RenderBwdBatch ab) {
             f32x4 d[4];
 #pragma unroll
             for (int pb = 0; pb < 4; ++pb) {
+                const bf16x8 bh = g_b1(s_Gh, pb), bl = g_b1(s_Gl, pb);
                 d[pb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-                d[pb] = LSR_MFMA16(ah, b1h[pb], d[pb]);
-                d[pb] = LSR_MFMA16(ah, b1l[pb], d[pb]);
-                d[pb] = LSR_MFMA16(al, b1h[pb], d[pb]);
+                d[pb] = LSR_MFMA16(ah, bh, d[pb]);
+                d[pb] = LSR_MFMA16(ah, bl, d[pb]);
+                d[pb] = LSR_MFMA16(al, bh, d[pb]);
             }
             wave_lds_sync();   // F read before W overwrites it
             // d[pb][i] at lane (g4, c): entry 4 g4 + i, pixel 16 pb + c
@@ -398,23 +399,47 @@ k_render_bwd_wave(RenderBwdBatch ab) {
         float wv[WG], tv[WG];
         constexpr int RB = 2;   // entries per branch-free batch: one packed-fp32 pair (register budget)
         const lsr_f2 px2 = {pxf, pxf}, py2 = {pyf, pyf};
+        // the pairs' entry data (one broadcast b64 read per field = a packed-fp32 operand), software-
+        // pipelined: the next pair's reads are issued before this pair computes, so their LDS latency
+        // hides behind it (the scheduler otherwise places each read right before its first use)
+        struct PairIn {
+            lsr_f2 X, Y, A, B, Cc, O, R, Gc, Bc, D;
+            uint2 kk;
+        };
+        auto ld_pair = [&](int e0) __attribute__((always_inline)) {
+            auto ld2 = [&](const float* base) { return *reinterpret_cast<const lsr_f2*>(base + e0); };
+            PairIn q;
+            q.X = ld2(s_X); q.Y = ld2(s_Y); q.A = ld2(s_A); q.B = ld2(s_B); q.Cc = ld2(s_C); q.O = ld2(s_O);
+            q.R = ld2(s_R); q.Gc = ld2(s_Gc); q.Bc = ld2(s_Bc); q.D = ld2(s_D);
+            q.kk = *reinterpret_cast<const uint2*>(s_k + e0);
+            return q;
+        };
+        // (the RGB-only instantiation, at 3 waves per SIMD, has no registers for the prefetched pair)
+        constexpr bool PIPE = !NOL;
+        PairIn pin = ld_pair(0);
 #pragma unroll
         for (int e0 = 0; e0 < WG; e0 += RB) {
         float Gv[RB], alv[RB], romv[RB], dotv[RB];
         bool act[RB];
-        {   // the pair's entry data: one broadcast b64 read per field = a packed-fp32 operand
-            auto ld2 = [&](const float* base) { return *reinterpret_cast<const lsr_f2*>(base + e0); };
-            const lsr_f2 X = ld2(s_X), Y = ld2(s_Y), A = ld2(s_A), B = ld2(s_B), Cc = ld2(s_C), O = ld2(s_O);
-            const uint2 kk = *reinterpret_cast<const uint2*>(s_k + e0);
+        PairIn pnext;
+        if constexpr (PIPE) {
+            if (e0 + RB < WG) pnext = ld_pair(e0 + RB);
+            __builtin_amdgcn_sched_barrier(0);   // keep the next pair's reads issued here
+        } else if (e0 > 0) {
+            pin = ld_pair(e0);
+        }
+        {
+            const lsr_f2 X = pin.X, Y = pin.Y, A = pin.A, B = pin.B, Cc = pin.Cc, O = pin.O;
+            const uint2 kk = pin.kk;
             // the forward's operation order per component (bit-identical alpha decisions)
             const lsr_f2 dx = X - px2, dy = Y - py2;
             const lsr_f2 pw = gauss_power2(A, B, Cc, dx, dy);
             const lsr_f2 ge = expf_repro2(pw);
             const lsr_f2 og = O * ge;
-            lsr_f2 dot = ld2(s_R) * g0;
-            dot = __builtin_elementwise_fma(ld2(s_Gc), lsr_f2{g1, g1}, dot);
-            dot = __builtin_elementwise_fma(ld2(s_Bc), lsr_f2{g2, g2}, dot);
-            dot = __builtin_elementwise_fma(ld2(s_D), lsr_f2{gD, gD}, dot);
+            lsr_f2 dot = pin.R * g0;
+            dot = __builtin_elementwise_fma(pin.Gc, lsr_f2{g1, g1}, dot);
+            dot = __builtin_elementwise_fma(pin.Bc, lsr_f2{g2, g2}, dot);
+            dot = __builtin_elementwise_fma(pin.D, lsr_f2{gD, gD}, dot);
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
                 const int e = e0 + u;
@@ -440,6 +465,9 @@ k_render_bwd_wave(RenderBwdBatch ab) {
             dL_dalpha = __builtin_fmaf(rom, bg_term, dL_dalpha);   // (-T_final / (1 - alpha)) bg . dL/dpix
             wv[e] = alpha * T;
             tv[e] = act[u] ? Gv[u] * dL_dalpha : 0.0f;
+        }
+        if constexpr (PIPE) {
+            if (e0 + RB < WG) pin = pnext;
         }
         }
 
@@ -479,9 +507,10 @@ k_render_bwd_wave(RenderBwdBatch ab) {
             if constexpr (!NOL) {
 #pragma unroll
                 for (int nb = 0; nb < 2; ++nb) {
-                    dacc[nb] = LSR_MFMA16(ah, b2h[kb][nb], dacc[nb]);
-                    dacc[nb] = LSR_MFMA16(ah, b2l[kb][nb], dacc[nb]);
-                    dacc[nb] = LSR_MFMA16(al, b2h[kb][nb], dacc[nb]);
+                    const bf16x8 bh = g_b2(s_Gh, kb, nb), bl = g_b2(s_Gl, kb, nb);
+                    dacc[nb] = LSR_MFMA16(ah, bh, dacc[nb]);
+                    dacc[nb] = LSR_MFMA16(ah, bl, dacc[nb]);
+                    dacc[nb] = LSR_MFMA16(al, bh, dacc[nb]);
                 }
             }
             dacc[2] = LSR_MFMA16(ah, bm[kb], dacc[2]);   // w hi and lo times g hi (6..9) and lo (10..13)
