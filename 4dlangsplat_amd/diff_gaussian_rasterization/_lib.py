@@ -64,8 +64,7 @@ class DeformNet(ctypes.Structure):
                 ("aabb", ctypes.c_void_p), ("planes", (ctypes.c_void_p * 6) * 4),
                 ("w_feat", ctypes.c_void_p * 4), ("b_feat", ctypes.c_void_p * 4),
                 ("w1", ctypes.c_void_p * 6), ("b1", ctypes.c_void_p * 6), ("w2", ctypes.c_void_p * 6),
-                ("b2", ctypes.c_void_p * 6), ("w_lang", ctypes.c_void_p * 3), ("b_lang", ctypes.c_void_p * 3),
-                ("aabb", ctypes.c_void_p)]
+                ("b2", ctypes.c_void_p * 6), ("w_lang", ctypes.c_void_p * 3), ("b_lang", ctypes.c_void_p * 3)]
 
 
 class DeformGrads(ctypes.Structure):

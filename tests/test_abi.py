@@ -102,3 +102,40 @@ print("ok")
 """
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert out.returncode == 0 and "ok" in out.stdout, out.stderr
+
+
+STRUCTS = {"Settings": "lsr_settings", "FwdIn": "lsr_fwd_in", "FwdOut": "lsr_fwd_out", "BwdIn": "lsr_bwd_in",
+           "BwdOut": "lsr_bwd_out", "DeformNet": "lsr_deform_net", "DeformGrads": "lsr_deform_grads",
+           "AdamGroup": "lsr_adam_group", "RowTensor": "lsr_row_tensor"}
+
+
+def test_ctypes_structs_match_the_headers(tmp_path):
+    """Every ctypes mirror of an include/*.h struct has the C compiler's field offsets and size
+    (a duplicated or misplaced field in a mirror hands the library NULL or shifted pointers)."""
+    from diff_gaussian_rasterization import _lib
+    lines = ["#include <stddef.h>", "#include <stdio.h>"] + [f'#include "{h}"' for h in HEADERS] + ["int main(void) {"]
+    want = {}
+    for py, c in STRUCTS.items():
+        cls = getattr(_lib, py)
+        names = [f[0] for f in cls._fields_]
+        assert len(names) == len(set(names)), f"{py}: duplicate fields"
+        lines.append(f'printf("{py} size %zu\\n", sizeof({c}));')
+        want[(py, "size")] = ctypes_sizeof(cls)
+        for n in names:
+            lines.append(f'printf("{py} {n} %zu\\n", offsetof({c}, {n}));')
+            want[(py, n)] = getattr(cls, n).offset
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-o", str(exe), str(src)], check=True)
+    got = {}
+    for line in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines():
+        py, n, v = line.split()
+        got[(py, n)] = int(v)
+    assert got == want
+
+
+def ctypes_sizeof(cls):
+    import ctypes
+    return ctypes.sizeof(cls)
