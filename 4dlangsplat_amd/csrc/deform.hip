@@ -18,6 +18,12 @@
 
 namespace lsr {
 
+// Diagnostic build (-DLSR_DEFORM_DIAG): the plane scatter checks every staged tap offset and value
+// and counts the bad ones (lsr_debug_deform_diag) instead of adding them.
+#ifdef LSR_DEFORM_DIAG
+__device__ unsigned long long g_deform_diag[8];
+#endif
+
 // LDS poison build (-DLSR_LDS_POISON, build/variants/liblsr_ldspoison.so; tests/test_deform_lds_poison_gpu.py):
 // every kernel of this file fills its shared memory with all-ones words (NaN as fp32 and as bf16)
 // at block entry, so a read of LDS the block never wrote turns the results into NaN instead of
@@ -167,6 +173,9 @@ __device__ __forceinline__ void features_to_lds(const DeformArgs& a, int g0, __b
             const int pi = 6 * s + ci;
             const float4 v = sample4(a, pi, tap_of(a, pi, ci, crd), q);
             prod.x *= v.x; prod.y *= v.y; prod.z *= v.z; prod.w *= v.w;
+#ifdef LSR_DEFORM_FEAT_WAIT
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#endif
         }
         const float f[4] = {prod.x, prod.y, prod.z, prod.w};
 #pragma unroll
@@ -618,6 +627,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
 #pragma unroll 4
                     for (int j = 0; j < 16; ++j) {
                         const float val = s_sdv[(wave * 16 + j) * 17 + ch] * s_sw[(wave * 16 + j) * 4 + tap];
+#ifdef LSR_DEFORM_DIAG
+                        const int off = s_soff[(wave * 16 + j) * 4 + tap];
+                        if (off < 0 || off >= W * H * 16 || !(fabsf(val) < 1e30f)) {
+                            atomicAdd(&g_deform_diag[0], 1ull);
+                            atomicAdd(&g_deform_diag[1 + tap], 1ull);
+                            continue;
+                        }
+#endif
                         if (val != 0.0f) atomicAdd(gp + s_soff[(wave * 16 + j) * 4 + tap] + ch, val);
                     }
                     wave_lds_sync();   // staging read before the next plane rewrites it
@@ -669,9 +686,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
 }
 
 template <int S>
+#ifndef LSR_DEFORM_BWD_DYN_LDS
+#define LSR_DEFORM_BWD_DYN_LDS 0   // diagnostic builds: unused dynamic LDS per block (occupancy control)
+#endif
 static void go_bwd(const DeformBwdArgs& b, hipStream_t st) {
-    if (b.f.nlayers > 1) hipLaunchKernelGGL((k_deform_bwd_a<S, true>), dim3((b.f.P + DN - 1) / DN), dim3(256), 0, st, b);
-    else hipLaunchKernelGGL((k_deform_bwd_a<S, false>), dim3((b.f.P + DN - 1) / DN), dim3(256), 0, st, b);
+    const unsigned dyn = LSR_DEFORM_BWD_DYN_LDS;
+    if (b.f.nlayers > 1) hipLaunchKernelGGL((k_deform_bwd_a<S, true>), dim3((b.f.P + DN - 1) / DN), dim3(256), dyn, st, b);
+    else hipLaunchKernelGGL((k_deform_bwd_a<S, false>), dim3((b.f.P + DN - 1) / DN), dim3(256), dyn, st, b);
 }
 void launch_deform_bwd_a(const DeformBwdArgs& b, hipStream_t st) {
     if (b.f.P <= 0) return;
@@ -1257,3 +1278,12 @@ void launch_pack_weight(const float* src, __bf16* hi, __bf16* lo, int rows, int 
 }
 
 }  // namespace lsr
+
+#ifdef LSR_DEFORM_DIAG
+// diagnostic export (not part of include/lsr_deform.h): read and reset the counters
+extern "C" int lsr_debug_deform_diag(unsigned long long* out8) {
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(lsr::g_deform_diag), 8 * sizeof(unsigned long long)) != hipSuccess) return 2;
+    unsigned long long z[8] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(lsr::g_deform_diag), z, sizeof(z)) == hipSuccess ? 0 : 2;
+}
+#endif

@@ -2,6 +2,7 @@
 """Deformation backward repeatability and oracle agreement (diagnostic): the Neu3D-resolution case of
 tests/test_deform_gpu.py (P Gaussians, kink-ambiguous ones masked) run R times; d_means3D involves
 no atomics, so any run-to-run difference is a race.  LSR_LIBRARY selects a variant build."""
+import ctypes
 import os
 import sys
 
@@ -45,23 +46,48 @@ def main():
     f = T._field(params, res, multires)
     t = lambda a: torch.tensor(np.asarray(a, np.float32)).cuda()   # noqa: E731
     first = None
-    first_dx = None
     F = 16 * len(multires)
-    dx_off = ((P * F * 4 + 255) // 256) * 256          # deform_api.hip bwd_scratch: X, then dX
+    al = lambda n: ((n * 4 + 255) // 256) * 256    # noqa: E731  (deform_api.hip bwd_scratch: X, A0, dH0)
+    segs = {"X": (0, F), "A0": (al(P * F), 128), "dH0": (al(P * F) + al(P * 128), 128)}
+    first_seg = {}
+    from diff_gaussian_rasterization import _lib
+    f_lib = _lib.load()
+    try:
+        f_lib.lsr_debug_deform_diag
+    except AttributeError:
+        f_lib = None
+    # the forward (same LDS footprint class, features_to_lds) repeated: outputs must repeat bit for bit
+    fin = [t(inp[k]) for k in T.KEYS]
+    ref_out = None
+    for r in range(R):
+        out = [o.cpu().numpy() for o in f.forward(*fin, None, time)[:5]]
+        if ref_out is None:
+            ref_out = out
+        else:
+            for k, a_, b_ in zip(T.KEYS, out, ref_out):
+                if not np.array_equal(a_, b_):
+                    rows = np.nonzero((a_ != b_).reshape(P, -1).any(axis=1))[0]
+                    print(f"forward run {r}: {k} DIFFERS at {len(rows)} rows {rows[:8].tolist()} (in-block "
+                          f"{sorted(set((rows % 64).tolist()))[:16]})", flush=True)
+    print("forward repeats checked", flush=True)
     for r in range(R):
         f.zero_grad()
         got = f.backward(t(inp["means3D"]), time, *[t(ups[k]) for k in T.KEYS])
         torch.cuda.synchronize()
-        dx = f._scratch[dx_off:dx_off + P * F * 4].view(torch.float32).reshape(P, F).cpu().numpy()
-        if first_dx is None:
-            first_dx = dx.copy()
-        elif not np.array_equal(dx, first_dx):
-            rows = np.nonzero((dx != first_dx).any(axis=1))[0]
-            print(f"run {r}: dX DIFFERS at rows {rows[:12].tolist()}", flush=True)
-            for rr in rows[:2]:
-                cols = np.nonzero(dx[rr] != first_dx[rr])[0]
-                print(f"   row {rr} cols {cols.tolist()}\n   got  {np.round(dx[rr][cols][:8], 5).tolist()}\n"
-                      f"   want {np.round(first_dx[rr][cols][:8], 5).tolist()}", flush=True)
+        for name, (off, w) in segs.items():   # saved rows run to run: the first stage that differs
+            v = f._scratch[off:off + P * w * 4].view(torch.float32).reshape(P, w).cpu().numpy()
+            if name not in first_seg:
+                first_seg[name] = v.copy()
+            elif not np.array_equal(v, first_seg[name]):
+                rows = np.nonzero((v != first_seg[name]).any(axis=1))[0]
+                cols = np.nonzero((v != first_seg[name]).any(axis=0))[0]
+                print(f"run {r}: {name} DIFFERS at {len(rows)} rows {rows[:12].tolist()} (in-block "
+                      f"{sorted(set((rows % 64).tolist()))[:16]}) cols {cols[:40].tolist()}", flush=True)
+        diag = getattr(f_lib, "lsr_debug_deform_diag", None) if f_lib is not None else None
+        if diag is not None:
+            buf = (ctypes.c_ulonglong * 8)()
+            diag(buf)
+            print(f"run {r}: scatter diag bad={buf[0]} by tap {list(buf)[1:5]}", flush=True)
         dm = got[0].cpu().numpy()
         err = T._rel(dm, g_in["means3D"])
         perr = max(T._rel(g.cpu().numpy(), g_p[n].reshape(g.shape)) for n, g in f.grads.items())
