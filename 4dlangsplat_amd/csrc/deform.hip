@@ -413,6 +413,16 @@ void launch_deform_fwd(const DeformArgs& a, hipStream_t st) {
     go_fwd_s<false>(b, st);
 }
 
+// The heads with at most DEF_SMALL_OUT outputs (pos, scales, rotations, opacity: 3 / 3 / 4 / 1) take
+// G W2 and G^T relu(Z1) on the VALU from fp32 G rows (a float4 per row in LDS, read as a
+// broadcast by the half-wave that holds the row): as 64-padded MFMA products they were 61 / 64
+// zeros, with their weight fragments re-read from L2 every tile.
+constexpr int DEF_SMALL_OUT = 4;
+// W2 rows 0..3 of column c as fp32 (hi + lo of the forward pack; rows past nout are the pack's zeros)
+__device__ __forceinline__ void w2_column(const __bf16* w2h, const __bf16* w2l, int c, float (&w)[DEF_SMALL_OUT]) {
+#pragma unroll
+    for (int k = 0; k < DEF_SMALL_OUT; ++k) w[k] = (float)w2h[k * DWID + c] + (float)w2l[k * DWID + c];
+}
 // ==== backward ====================================================================================
 // Phase A, one block per 64 Gaussians (the forward's tiling): recompute the features X and the
 // chain A_k = relu(H_k) (saved); per head, Z1 = A W1^T + b1, the gradient G of the head's output
@@ -438,13 +448,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
     __shared__ __attribute__((aligned(16))) __bf16 s_hl[2][DN * DAP];
     __bf16* const s_xh = s_hh[1];   // read by the first layer only, which writes buffer 0
     __bf16* const s_xl = s_hl[1];
+    __shared__ __attribute__((aligned(16))) float4 s_g4[DN];   // small-output heads: fp32 G rows
     // Everything else lives in a hidden buffer while that buffer is dead (68 KB in all: two blocks
     // per CU): a head's G rows in the buffer its dZ1 rows take next (a barrier between the two), dX in
     // the chain's dead buffer, the plane-scatter staging in its lo half; every hand-over is a
     // __syncthreads, and the LDS-poison build checks that nothing reads a word its block never wrote.
     static_assert(DN * (F + 1) * 4 <= DN * DAP * 2, "dX rows fit one hidden buffer");
     static_assert((4 * 16 * 17 + 2 * 4 * 16 * 4) * 4 <= DN * DAP * 2, "scatter staging fits one hidden buffer");
-    LDS_POISON(s_hh); LDS_POISON(s_hl); LDS_POISON_DONE();
+    LDS_POISON(s_hh); LDS_POISON(s_hl); LDS_POISON(s_g4); LDS_POISON_DONE();
     const DeformArgs& a = b.f;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int g0 = blockIdx.x * DN;
@@ -493,8 +504,42 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
 #pragma unroll
                 for (int q = 0; q < 16; ++q) zpos |= z[mt][q] + bias > 0.0f ? 1u << (16 * mt + q) : 0u;
         }
-        // gradient rows of this head's output, K padded to 64, in the buffer dZ1 takes next
         const float* G = coff ? b.sG_coff : quat ? b.sG_rot : b.up[hd];   // saved by the GRAD pass
+        if (nout <= DEF_SMALL_OUT) {                                 // block-uniform
+            // dZ1 = (G W2) [Z1 > 0] on the VALU from fp32 G rows (k_head_wgrad's small-output path)
+            if (tid < DN) {
+                const int g = g0 + tid;
+                float v[DEF_SMALL_OUT] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+                for (int k = 0; k < DEF_SMALL_OUT; ++k)
+                    if (k < nout && g < a.P) v[k] = G[(size_t)g * nout + k];
+                s_g4[tid] = make_float4(v[0], v[1], v[2], v[3]);
+            }
+            float w2c[DEF_SMALL_OUT];
+            w2_column(a.w2_h[hd], a.w2_l[hd], col, w2c);
+            __syncthreads();   // G rows complete
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const int r = row_of(mt, q, hh);
+                    const float4 gv = s_g4[r];
+                    float dv = gv.x * w2c[0];
+                    dv = __builtin_fmaf(gv.y, w2c[1], dv);
+                    dv = __builtin_fmaf(gv.z, w2c[2], dv);
+                    dv = __builtin_fmaf(gv.w, w2c[3], dv);
+                    const float v = (zpos >> (16 * mt + q)) & 1u ? dv : 0.0f;
+                    __bf16 hi, lo;
+                    dsplit(v, hi, lo);
+                    bh[r * DAP + col] = hi;
+                    bl[r * DAP + col] = lo;
+                }
+            __syncthreads();   // dZ1 rows complete
+            mlp_ntile<DWID>(dA, bh, bl, DAP, wave, b.w1t_h[hd], b.w1t_l[hd]);
+            __syncthreads();   // dZ1 rows and the G rows consumed before the next head rewrites them
+            continue;
+        }
+        // gradient rows of this head's output, K padded to 64, in the buffer dZ1 takes next
         for (int i = tid; i < DN * 64; i += 256) {
             const int r = i >> 6, k = i & 63, g = g0 + r;
             float v = 0.0f;
@@ -635,7 +680,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
                             continue;
                         }
 #endif
+#ifndef LSR_DEFORM_ABL_NOSCATTER   // timing ablation only (wrong plane gradients)
                         if (val != 0.0f) atomicAdd(gp + s_soff[(wave * 16 + j) * 4 + tap] + ch, val);
+#endif
                     }
                     wave_lds_sync();   // staging read before the next plane rewrites it
                 }
@@ -928,13 +975,37 @@ __device__ __forceinline__ dbf16x8 wg_lds_op(const __bf16* base, int pitch, int 
     return __builtin_bit_cast(dbf16x8, v);
 }
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) k_head_wgrad(HeadWgradArgs ha) {
+// A rows of a 64-row tile into LDS as bf16 hi / lo (4 values per 8-byte store); rows past row1 are zero
+__device__ __forceinline__ void a_rows_to_lds(const float* __restrict__ A, int64_t t0, int64_t row1, __bf16* ah, __bf16* al) {
+    typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = tid; i < DN * (DWID / 4); i += 256) {
+        const int rr = i >> 5, c4 = (i & 31) * 4;
+        const int64_t g = t0 + rr;
+        const float4 v = g < row1 ? *reinterpret_cast<const float4*>(A + g * DWID + c4) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        const float f[4] = {v.x, v.y, v.z, v.w};
+        bf4 h4, l4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            __bf16 hi, lo;
+            dsplit(f[e], hi, lo);
+            h4[e] = hi; l4[e] = lo;
+        }
+        *reinterpret_cast<bf4*>(ah + rr * DAP + c4) = h4;
+        *reinterpret_cast<bf4*>(al + rr * DAP + c4) = l4;
+    }
+}
+
+template <bool SMALL>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) k_head_wgrad(HeadWgradArgs ha, int job0) {
     __shared__ __attribute__((aligned(16))) __bf16 s_ah[DN * DAP];   // A rows [64][128] hi / lo
     __shared__ __attribute__((aligned(16))) __bf16 s_al[DN * DAP];
-    __shared__ __attribute__((aligned(16))) __bf16 s_gh[DN * DGP];   // G rows [64][64 pad] hi / lo
-    __shared__ __attribute__((aligned(16))) __bf16 s_gl[DN * DGP];
-    LDS_POISON(s_ah); LDS_POISON(s_al); LDS_POISON(s_gh); LDS_POISON(s_gl); LDS_POISON_DONE();
-    const HeadWgradJob& j = ha.job[blockIdx.y];
+    __shared__ __attribute__((aligned(16))) __bf16 s_gh[SMALL ? 8 : DN * DGP];   // G rows [64][64 pad] hi / lo
+    __shared__ __attribute__((aligned(16))) __bf16 s_gl[SMALL ? 8 : DN * DGP];
+    __shared__ __attribute__((aligned(16))) float4 s_g4[SMALL ? DN : 1];        // SMALL: G rows fp32
+    LDS_POISON(s_ah); LDS_POISON(s_al); LDS_POISON(s_gh); LDS_POISON(s_gl); LDS_POISON(s_g4); LDS_POISON_DONE();
+    const HeadWgradJob& j = ha.job[job0 + blockIdx.y];
     const int64_t row0 = (int64_t)blockIdx.x * ha.rows_per_block;
     const int64_t row1 = min((int64_t)ha.P, row0 + ha.rows_per_block);
     if (row0 >= row1) return;                                            // block-uniform
@@ -943,44 +1014,47 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     const int col = 32 * wave + r;
     const float b1c = j.b1[col];
     df32x16 w1acc[4] = {df32x16{}, df32x16{}, df32x16{}, df32x16{}};   // dW1 rows 32 wave .., col tiles 0..3
-    df32x16 w2acc[2] = {df32x16{}, df32x16{}};                            // dW2 o tiles 0..1, col tile wave
+    df32x16 w2acc[SMALL ? 1 : 2];                                         // dW2 o tiles 0..1, col tile wave
+    float w2s[DEF_SMALL_OUT] = {0.0f, 0.0f, 0.0f, 0.0f};                 // SMALL: dW2 rows 0..3, column col
+    float w2c[DEF_SMALL_OUT] = {0.0f, 0.0f, 0.0f, 0.0f};                 // SMALL: W2 rows 0..3, column col
+    float4 db2v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if constexpr (SMALL) w2_column(j.w2_h, j.w2_l, col, w2c);
+    else { w2acc[0] = df32x16{}; w2acc[1] = df32x16{}; }
     float db1 = 0.0f, db2 = 0.0f;
     for (int64_t t0 = row0; t0 < row1; t0 += DN) {
-        // ---- A and G rows of the tile into LDS (fp32 -> bf16 hi / lo); rows past P are zero --------
-        for (int i = tid; i < DN * (DWID / 4); i += 256) {
-            const int rr = i >> 5, c4 = (i & 31) * 4;
-            const int64_t g = t0 + rr;
-            const float4 v = g < row1 ? *reinterpret_cast<const float4*>(ha.A + g * DWID + c4)
-                                      : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            const float f[4] = {v.x, v.y, v.z, v.w};
+        // ---- A and G rows of the tile into LDS; rows past P are zero ------------------------------------
+        a_rows_to_lds(ha.A, t0, row1, s_ah, s_al);
+        if constexpr (SMALL) {
+            if (tid < DN) {   // one row per thread: db2 accumulates in its float4
+                const int64_t g = t0 + tid;
+                float v[DEF_SMALL_OUT] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                __bf16 hi, lo;
-                dsplit(f[e], hi, lo);
-                s_ah[rr * DAP + c4 + e] = hi;
-                s_al[rr * DAP + c4 + e] = lo;
+                for (int k = 0; k < DEF_SMALL_OUT; ++k)
+                    if (k < nout && g < row1) v[k] = j.G[g * nout + k];
+                const float4 gv = make_float4(v[0], v[1], v[2], v[3]);
+                s_g4[tid] = gv;
+                db2v.x += gv.x; db2v.y += gv.y; db2v.z += gv.z; db2v.w += gv.w;
             }
-        }
-        for (int i = tid; i < DN * 64; i += 256) {
-            const int rr = i >> 6, k = i & 63;
-            const int64_t g = t0 + rr;
-            const float v = (k < nout && g < row1) ? j.G[g * nout + k] : 0.0f;
-            __bf16 hi, lo;
-            dsplit(v, hi, lo);
-            s_gh[rr * DGP + k] = hi;
-            s_gl[rr * DGP + k] = lo;
-        }
-        if (tid < nout) {   // db2: column sums of G over the tile (thread per output)
-            float sg = 0.0f;
-            for (int rr = 0; rr < DN; ++rr) {
+        } else {
+            // G rows; a thread always holds column k = tid & 63 (256 is a multiple of 64), so db2, the
+            // column sums of G, accumulate in its register (a per-tile loop of 64 dependent loads by
+            // the nout threads serialised the whole block)
+#pragma unroll
+            for (int i = tid; i < DN * 64; i += 256) {
+                const int rr = i >> 6, k = i & 63;
                 const int64_t g = t0 + rr;
-                if (g < row1) sg += j.G[g * nout + tid];
+                const float v = (k < nout && g < row1) ? j.G[g * nout + k] : 0.0f;
+                db2 += v;
+                __bf16 hi, lo;
+                dsplit(v, hi, lo);
+                s_gh[rr * DGP + k] = hi;
+                s_gl[rr * DGP + k] = lo;
             }
-            db2 += sg;
         }
         __syncthreads();
-        // ---- Z1 for this wave's 32 columns (both row tiles): relu(Z1) -> dW2 += G^T relu(Z1) -------------
+        // ---- Z1 for this wave's 32 columns (both row tiles), then dW2 and dZ1 ------------------------------
         uint32_t zpos = 0;   // bit 16 mt + q: Z1 > 0
+        df32x16 d[2] = {df32x16{}, df32x16{}};
         {
             df32x16 z[2] = {df32x16{}, df32x16{}};
             mlp_ntile<DWID>(z, s_ah, s_al, DAP, wave, j.w1_h, j.w1_l);
@@ -992,24 +1066,41 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
                     zpos |= zz > 0.0f ? 1u << (16 * mt + q) : 0u;
                     z[mt][q] = fmaxf(zz, 0.0f);
                 }
+            if constexpr (SMALL) {
+                // per row of the lane: dW2[k][col] += G[r][k] relu(Z1)[r][col], dZ1 = sum_k G[r][k] W2[k][col]
 #pragma unroll
-            for (int ks = 0; ks < DN / 16; ++ks) {
-                dbf16x8 zh, zl;
-                wg_regs_to_op(z[ks >> 1], ks & 1, zh, zl);
+                for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-                for (int mo = 0; mo < 2; ++mo) {
-                    if (mo >= Mo) break;
-                    const dbf16x8 gh = wg_lds_op(s_gh, DGP, ks, 32 * mo), gl = wg_lds_op(s_gl, DGP, ks, 32 * mo);
-                    w2acc[mo] = DMFMA(gh, zh, w2acc[mo]);
-                    w2acc[mo] = DMFMA(gh, zl, w2acc[mo]);
-                    w2acc[mo] = DMFMA(gl, zh, w2acc[mo]);
+                    for (int q = 0; q < 16; ++q) {
+                        const float4 gv = s_g4[row_of(mt, q, hh)];
+                        const float zz = z[mt][q];
+                        w2s[0] = __builtin_fmaf(gv.x, zz, w2s[0]); w2s[1] = __builtin_fmaf(gv.y, zz, w2s[1]);
+                        w2s[2] = __builtin_fmaf(gv.z, zz, w2s[2]); w2s[3] = __builtin_fmaf(gv.w, zz, w2s[3]);
+                        float dv = gv.x * w2c[0];
+                        dv = __builtin_fmaf(gv.y, w2c[1], dv);
+                        dv = __builtin_fmaf(gv.z, w2c[2], dv);
+                        dv = __builtin_fmaf(gv.w, w2c[3], dv);
+                        d[mt][q] = dv;
+                    }
+            } else {
+#pragma unroll
+                for (int ks = 0; ks < DN / 16; ++ks) {
+                    dbf16x8 zh, zl;
+                    wg_regs_to_op(z[ks >> 1], ks & 1, zh, zl);
+#pragma unroll
+                    for (int mo = 0; mo < 2; ++mo) {
+                        if (mo >= Mo) break;
+                        const dbf16x8 gh = wg_lds_op(s_gh, DGP, ks, 32 * mo), gl = wg_lds_op(s_gl, DGP, ks, 32 * mo);
+                        w2acc[mo] = DMFMA(gh, zh, w2acc[mo]);
+                        w2acc[mo] = DMFMA(gh, zl, w2acc[mo]);
+                        w2acc[mo] = DMFMA(gl, zh, w2acc[mo]);
+                    }
                 }
             }
         }
         // ---- dZ1 = (G W2) [Z1 > 0] -> dW1 += dZ1^T A (rows 32 wave .. of dW1), db1 ------------------------
         {
-            df32x16 d[2] = {df32x16{}, df32x16{}};
-            mlp_ntile<64>(d, s_gh, s_gl, DGP, wave, j.w2t_h, j.w2t_l);
+            if constexpr (!SMALL) mlp_ntile<64>(d, s_gh, s_gl, DGP, wave, j.w2t_h, j.w2t_l);
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
@@ -1040,24 +1131,49 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
             const int m = 32 * wave + (q & 3) + 8 * (q >> 2) + 4 * hh;
             atomicAdd(j.dW1 + (size_t)m * DWID + 32 * nt + r, w1acc[nt][q]);
         }
-#pragma unroll
-    for (int mo = 0; mo < 2; ++mo) {
-        if (mo >= Mo) break;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const int o = 32 * mo + (q & 3) + 8 * (q >> 2) + 4 * hh;
-            if (o < nout) atomicAdd(j.dW2 + (size_t)o * DWID + col, w2acc[mo][q]);
-        }
-    }
     db1 += __shfl_xor(db1, 32);
     if (hh == 0) atomicAdd(j.db1 + col, db1);
-    if (tid < nout) atomicAdd(j.db2 + tid, db2);
+    if constexpr (SMALL) {
+#pragma unroll
+        for (int k = 0; k < DEF_SMALL_OUT; ++k) {
+            const float v = w2s[k] + __shfl_xor(w2s[k], 32);   // the lane pair holds the column's two row halves
+            if (hh == 0 && k < nout) atomicAdd(j.dW2 + (size_t)k * DWID + col, v);
+        }
+        if (wave == 0) {   // db2: the 64 row threads' sums
+            float v[DEF_SMALL_OUT] = {db2v.x, db2v.y, db2v.z, db2v.w};
+#pragma unroll
+            for (int k = 0; k < DEF_SMALL_OUT; ++k) {
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) v[k] += __shfl_xor(v[k], off);
+                if (lane == 0 && k < nout) atomicAdd(j.db2 + k, v[k]);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int mo = 0; mo < 2; ++mo) {
+            if (mo >= Mo) break;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int o = 32 * mo + (q & 3) + 8 * (q >> 2) + 4 * hh;
+                if (o < nout) atomicAdd(j.dW2 + (size_t)o * DWID + col, w2acc[mo][q]);
+            }
+        }
+        if ((tid & 63) < nout) atomicAdd(j.db2 + (tid & 63), db2);   // one partial per wave
+    }
 }
 
 void launch_head_wgrad(const HeadWgradArgs& a, int njobs, hipStream_t st) {
     if (a.P <= 0 || njobs <= 0) return;
     const int nb = (a.P + a.rows_per_block - 1) / a.rows_per_block;
-    hipLaunchKernelGGL(k_head_wgrad, dim3(nb, njobs), dim3(256), 0, st, a);
+    // the small-output heads first (one launch), then the rest: jobs are reordered into two runs
+    HeadWgradArgs s = a;
+    int ns = 0, nbig = 0;
+    for (int i = 0; i < njobs; ++i)
+        if (a.job[i].nout <= DEF_SMALL_OUT) s.job[ns++] = a.job[i];
+    for (int i = 0; i < njobs; ++i)
+        if (a.job[i].nout > DEF_SMALL_OUT) { s.job[ns + nbig] = a.job[i]; ++nbig; }
+    if (ns) hipLaunchKernelGGL(k_head_wgrad<true>, dim3(nb, ns), dim3(256), 0, st, s, 0);
+    if (nbig) hipLaunchKernelGGL(k_head_wgrad<false>, dim3(nb, nbig), dim3(256), 0, st, s, ns);
 }
 
 // Phase B: C[M][N] += sum_g L[g][m] R[g][n] (M, N <= 128), bias[m] += sum_g L[g][m]; split-K over

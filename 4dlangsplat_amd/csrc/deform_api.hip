@@ -439,7 +439,8 @@ extern "C" int lsr_deform_backward(const lsr_deform_net* net, const void* worksp
         if (!head_on(net, hd)) continue;
         const float* G = hd == 5 ? b.sG_coff : (hd == 2 && net->apply_rotation) ? b.sG_rot : ups[hd];
         hw.job[nh++] = lsr::HeadWgradJob{G, b.f.w1_h[hd], b.f.w1_l[hd], b.f.b1[hd], b.w2t_h[hd], b.w2t_l[hd],
-                                         grads->w1[hd], grads->b1[hd], grads->w2[hd], grads->b2[hd], head_out(net, hd)};
+                                         b.f.w2_h[hd], b.f.w2_l[hd], grads->w1[hd], grads->b1[hd], grads->w2[hd],
+                                         grads->b2[hd], head_out(net, hd)};
     }
     lsr::launch_head_wgrad(hw, nh, st);
     if (lang_mlp(net)) {

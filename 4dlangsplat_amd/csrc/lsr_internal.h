@@ -314,6 +314,7 @@ struct HeadWgradJob {
     const __bf16 *w1_h, *w1_l;        // forward pack [128][128]
     const float* b1;
     const __bf16 *w2t_h, *w2t_l;      // backward pack [128][64] (W2 transposed, K padded to 64)
+    const __bf16 *w2_h, *w2_l;        // forward pack [64 pad][128] (the VALU path of nout <= 4)
     float *dW1, *db1, *dW2, *db2;     // accumulated
     int nout;
 };
