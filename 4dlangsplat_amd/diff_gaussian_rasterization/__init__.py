@@ -272,7 +272,7 @@ def language_split_native(language_feature, stream=None, out=None):
 
 def preprocess_views_native(raster_settings_list, means3D, opacities, shs=None, colors_precomp=None,
                             language_feature=None, scales=None, rotations=None, cov3D_precomp=None, stream=None,
-                            split_language=True, split_behind_counts=True):
+                            split_language=True, split_behind_counts=True, split_stream=None):
     """Forward phase 1 of several views of the same Gaussians as one batch
     (lsr_forward_preprocess_views_async: one preprocess launch per 8 views reads each Gaussian once,
     the views' depth sorts and instance scans share their launches) on `stream`.  No host
@@ -282,7 +282,9 @@ def preprocess_views_native(raster_settings_list, means3D, opacities, shs=None, 
     split_language (C == 32): the language rows' bf16 hi / lo operands are made once here for all
     the batch's views (lsr_language_split) instead of per entry in every compositor wave (same
     bits, same results).  split_behind_counts: enqueue that split behind the batch's count event, so
-    it runs while the host waits for the counts (False: ahead of the preprocess; an A/B switch)."""
+    it runs while the host waits for the counts (False: ahead of the preprocess; an A/B switch).
+    split_stream: enqueue the split there instead (after that stream waits for `stream`); the caller
+    orders the compositors after it."""
     device = _check_device(means3D)
     L = _lib.load()
     stream = stream or torch.cuda.current_stream(device)
@@ -318,7 +320,11 @@ def preprocess_views_native(raster_settings_list, means3D, opacities, shs=None, 
         raise
     ev = torch.cuda.Event()
     ev.record(stream)
-    if split:   # only the compositors read it: it runs while the host waits for the counts
+    if split and split_stream is not None:   # on the caller's side stream, beside the binning
+        split_stream.wait_stream(stream)
+        inputs["language_feature_split"].record_stream(split_stream)
+        language_split_native(inputs["language_feature"], stream=split_stream, out=inputs["language_feature_split"])
+    elif split:   # only the compositors read it: it runs while the host waits for the counts
         language_split_native(inputs["language_feature"], stream=stream, out=inputs["language_feature_split"])
     out = []
     for v, rs in enumerate(raster_settings_list):

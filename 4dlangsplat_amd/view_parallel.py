@@ -243,7 +243,8 @@ class ViewParallelStep:
 
 def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool = False, overlap: bool = True,
                          batch_backward: bool = True, early_views: int = 3, composite_batch: bool = True,
-                         side_priority: int = 0, side_from_preprocess: bool = True, split_behind_counts: bool = True):
+                         side_priority: int = 0, side_from_preprocess: bool = True, split_behind_counts: bool = True,
+                         fill_on_side: bool = False):
     """render_view callback for ViewParallelStep on the HIP rasterizer (the product path).
 
     scene    : object with means3D, opacities, shs, lang, scales, rotations device tensors
@@ -275,7 +276,10 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
     dependent launches that leave most of the GPU idle) runs on a side stream while those first
     views composite, and each later view's compositing waits for it (an event); the side binning
     starts right behind the preprocess batch, beside the early views' binning
-    (side_from_preprocess; behind it: 925 vs 941 frames/s same-box).  With
+    (side_from_preprocess; behind it: 925 vs 941 frames/s same-box).  fill_on_side: the language
+    split, the step's bucket zeroing and the radii MAX run on that side stream ahead of its
+    binning instead of on the main stream between the instance scan and the early views' emission
+    (the first compositor launch waits for them).  With
     composite_batch (batched only) the step runs through render_batch: one compositor forward and
     one compositor backward launch per binning batch instead of per view.
 
@@ -292,6 +296,7 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
             else None)
     bin_side = [None]                     # created at the first split batch (CUDA tensors only)
     pending = {}
+    fill_ready = [None]                   # fill_on_side: the side stream's fills (the compositors wait)
     params_ready = torch.cuda.Event() if side is not None else None
     step_views = [None]                   # this rank's views of the current step (begin_step)
 
@@ -317,19 +322,35 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
         idle stretch while the host reads the counts)."""
         views = [w for w in step_views[0] if w >= v] if step_views[0] is not None else [v]
         views = [w for w in views if has_view(w)] or [v]
+        split_side = 0 < early_views < len(views) and scene.means3D.is_cuda
+        if split_side and bin_side[0] is None:
+            bin_side[0] = torch.cuda.Stream(device=scene.means3D.device, priority=side_priority)
+        to_side = fill_on_side and split_side
         pfs = dgr.preprocess_views_native([settings[w] for w in views], scene.means3D, scene.opacities,
                                           shs=scene.shs, language_feature=scene.lang, scales=scene.scales,
-                                          rotations=scene.rotations, split_behind_counts=split_behind_counts)
-        if before_wait is not None:
-            before_wait()
-        if radii_out is not None:     # the views' radii MAX, also while the host waits for the counts
-            dgr.radii_max_native([pf.radii for pf in pfs], radii_out)
-        if 0 < early_views < len(pfs) and scene.means3D.is_cuda:
+                                          rotations=scene.rotations, split_behind_counts=split_behind_counts,
+                                          split_stream=bin_side[0] if to_side else None)
+        fill_ready[0] = None
+        if to_side:                   # the fills beside the early views' binning, ahead of the side binning
+            bin_side[0].wait_stream(torch.cuda.current_stream(scene.means3D.device))   # after the preprocess batch
+            with torch.cuda.stream(bin_side[0]):
+                if before_wait is not None:
+                    before_wait()
+                if radii_out is not None:
+                    for pf in pfs:
+                        pf.radii.record_stream(bin_side[0])
+                    dgr.radii_max_native([pf.radii for pf in pfs], radii_out, stream=bin_side[0])
+            fill_ready[0] = torch.cuda.Event()
+            fill_ready[0].record(bin_side[0])
+        else:
+            if before_wait is not None:
+                before_wait()
+            if radii_out is not None:     # the views' radii MAX, also while the host waits for the counts
+                dgr.radii_max_native([pf.radii for pf in pfs], radii_out)
+        if split_side:
             dev = scene.means3D.device
-            if bin_side[0] is None:
-                bin_side[0] = torch.cuda.Stream(device=dev, priority=side_priority)
             side_b = bin_side[0]
-            if side_from_preprocess:      # the side binning starts beside the early views' binning
+            if side_from_preprocess and not to_side:   # the side binning starts beside the early views' binning
                 side_b.wait_stream(torch.cuda.current_stream(dev))   # after the preprocess batch
             dgr.binning_views_native(pfs[:early_views])      # waits for the batch's counts
             if not side_from_preprocess:  # ... or behind it
@@ -387,6 +408,9 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
         elif before_wait is not None:
             before_wait()
         pfs = [pending.pop(v) for v in views]
+        if fill_ready[0] is not None:      # the language split and the bucket zeroing ran on the side stream
+            torch.cuda.current_stream(scene.means3D.device).wait_event(fill_ready[0])
+            fill_ready[0] = None
         groups = []                        # consecutive views binned by one launch set (one event)
         for v, pf in zip(views, pfs):
             if groups and groups[-1][0][1].ready is pf.ready:

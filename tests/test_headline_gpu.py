@@ -5,7 +5,8 @@ densification statistics on: one preprocess launch for the step's views, segment
 sorts, the later views binned on a side stream, compositors on the pre-split bf16 language
 operands, the compositor backward per view, then one batched preprocess backward (the flush).
 This runs exactly that on the headline workload (S2M, P = 2M, 1352 x 1014, C = 32; 4 views, so the
-fourth is side-binned) and holds every output to the oracle: radii exactly, RGB within 1e-4,
+fourth is side-binned), twice (the images must repeat bit for bit), and holds every output to the
+oracle: radii exactly, RGB within 1e-4,
 language within 1e-3, every gradient field of the bucket (means3D, scales, rotations, opacities,
 SH, language, means2D) within 1e-4 of the largest magnitude of the oracle's per-view sum.
 """
@@ -47,8 +48,11 @@ def test_bench_pipeline_matches_oracle_at_headline_size():
     gcs_d, gls_d = [x.cuda() for x in gcs], [x.cuda() for x in gls]
     images, radii = {}, {}
 
+    runs = {}
+
     def grad_fn(v, color, lang, depth):
         images[v] = (color.clone(), lang.clone())
+        runs.setdefault(v, []).append(images[v])
         return gcs_d[v], gls_d[v], None
 
     render = native_view_renderer(scene, settings, grad_fn, overlap="batched", early_views=3)
@@ -76,6 +80,11 @@ def test_bench_pipeline_matches_oracle_at_headline_size():
     torch.cuda.synchronize()
     assert not torch.isnan(bucket.flat).any()
     assert len(render.pending) == 0
+    # the forward is deterministic: both steps' images repeat bit for bit (a race or a lost
+    # hazard in any compositor shows here first; see DESIGN.md 4.5 on the packed-fp32 build flag)
+    for v in range(V):
+        assert len(runs[v]) == 2
+        assert all(torch.equal(a, b) for a, b in zip(runs[v][0], runs[v][1])), v
 
     total = None
     for v, cam in enumerate(cams):
