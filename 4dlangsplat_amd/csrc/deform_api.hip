@@ -7,6 +7,7 @@
 #include "../../include/lsr.h"
 #include "../../include/lsr_deform.h"
 #include "lsr_internal.h"
+#include <cstdlib>
 #include <vector>
 
 namespace lsr {
@@ -257,7 +258,20 @@ lsr::LangDeformArgs lang_args(const lsr_deform_net* net, const void* workspace, 
 }
 
 // backward scratch: saved activations, then kGradReplicas copies of the packed gradient planes
-constexpr int kGradReplicas = 16;
+constexpr int kGradReplicas = 16;   // the most; deform_replicas(P) picks the count of a call
+// Replica count of a call (every copy is zeroed and summed by the unpack, 9.5 MB each for the Neu3D
+// planes).  LSR_DEFORM_REPLICAS overrides (diagnostic A/B).
+int deform_replicas(size_t P) {
+    static const int forced = [] {
+        const char* e = std::getenv("LSR_DEFORM_REPLICAS");
+        return e ? std::max(1, std::min(kGradReplicas, std::atoi(e))) : 0;
+    }();
+    if (forced) return forced;
+    // measured (tools/gpu_replica_ab.sh): 4 copies backward 12.20 vs 12.22 ms at 2M (the atomics do
+    // not contend more), configs[4] stand-in 159 vs 139-152 iterations/s at 100k (less to zero and sum)
+    (void)P;
+    return 4;
+}
 struct BwdScratch {
     size_t X, A[LSR_DEFORM_MAX_DEPTH], dH[LSR_DEFORM_MAX_DEPTH];
     size_t Grot, Gcoff, U0, U1, U2, dv, dZ2l, dZ1l, dplanes, total;
@@ -403,9 +417,10 @@ extern "C" int lsr_deform_backward(const lsr_deform_net* net, const void* worksp
     b.sG_coff = fp(S.Gcoff);
     b.dplanes = fp(S.dplanes);
     b.daabb = grads->aabb;
-    b.replicas = kGradReplicas;
+    b.replicas = deform_replicas((size_t)P);
     b.plane_stride = (int64_t)(L.planes_end / sizeof(float));
-    if (hipMemsetAsync(b.dplanes, 0, kGradReplicas * L.planes_end, st) != hipSuccess) return lsr::fail(LSR_EHIP, "memset");
+    if (hipMemsetAsync(b.dplanes, 0, (size_t)b.replicas * L.planes_end, st) != hipSuccess)
+        return lsr::fail(LSR_EHIP, "memset");
     lsr::launch_deform_bwd_a(b, st);
     lsr::LangDeformArgs la{};
     if (lang_mlp(net)) {

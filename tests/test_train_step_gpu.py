@@ -163,9 +163,10 @@ def test_render_views_matches_per_view_render():
     a, b = res
     assert torch.equal(a["images"], b["images"]) and torch.equal(a["radii"], b["radii"])
     torch.testing.assert_close(b["vs"], a["vs"], rtol=1e-4, atol=1e-9)
-    for k in a["g"]:
-        torch.testing.assert_close(b["g"][k], a["g"][k], rtol=1e-4, atol=1e-8 * float(a["g"][k].abs().max()) + 1e-12,
-                                   msg=k)
+    for k in a["g"]:   # float atomics and the view sums reorder: max-normalised, as for the field below
+        scale = float(a["g"][k].abs().max())
+        err = float((b["g"][k] - a["g"][k]).abs().max())
+        assert err <= 1e-5 * scale + 1e-12, (k, err, scale)
     for k in a["f"]:
         scale = float(a["f"][k].abs().max())
         err = float((b["f"][k] - a["f"][k]).abs().max())
