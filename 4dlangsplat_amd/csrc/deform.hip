@@ -626,9 +626,28 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
         float dq[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-            float4 v[6];
+            // each plane's 4 taps loaded once: the sample (sample4's arithmetic) and its x / y derivatives
+            // (the coordinate gradient); 72 registers for the scale instead of re-reading the taps
+            float4 v[6], gxv[6], gyv[6];
 #pragma unroll
-            for (int ci = 0; ci < 6; ++ci) v[ci] = sample4(a, 6 * s + ci, tap_of(a, 6 * s + ci, ci, crd), q);
+            for (int ci = 0; ci < 6; ++ci) {
+                const int pi = 6 * s + ci, W = a.pw[pi];
+                const Tap t = tap_of(a, pi, ci, crd);
+                const float4* pl = reinterpret_cast<const float4*>(a.planes + a.poff[pi]) + q;
+                const float4 t00 = pl[(t.y0 * W + t.x0) * 4], t01 = pl[(t.y0 * W + t.x1) * 4];
+                const float4 t10 = pl[(t.y1 * W + t.x0) * 4], t11 = pl[(t.y1 * W + t.x1) * 4];
+                const float w00 = (1.0f - t.fx) * (1.0f - t.fy), w01 = t.fx * (1.0f - t.fy), w10 = (1.0f - t.fx) * t.fy,
+                            w11 = t.fx * t.fy;
+                v[ci] = make_float4(t00.x * w00 + t01.x * w01 + t10.x * w10 + t11.x * w11,
+                                    t00.y * w00 + t01.y * w01 + t10.y * w10 + t11.y * w11,
+                                    t00.z * w00 + t01.z * w01 + t10.z * w10 + t11.z * w11,
+                                    t00.w * w00 + t01.w * w01 + t10.w * w10 + t11.w * w11);
+                const float ux = 1.0f - t.fy, uy = 1.0f - t.fx;
+                gxv[ci] = make_float4((t01.x - t00.x) * ux + (t11.x - t10.x) * t.fy, (t01.y - t00.y) * ux + (t11.y - t10.y) * t.fy,
+                                      (t01.z - t00.z) * ux + (t11.z - t10.z) * t.fy, (t01.w - t00.w) * ux + (t11.w - t10.w) * t.fy);
+                gyv[ci] = make_float4((t10.x - t00.x) * uy + (t11.x - t01.x) * t.fx, (t10.y - t00.y) * uy + (t11.y - t01.y) * t.fx,
+                                      (t10.z - t00.z) * uy + (t11.z - t01.z) * t.fx, (t10.w - t00.w) * uy + (t11.w - t01.w) * t.fx);
+            }
             const float* dxr = s_dx + gl * (F + 1) + 16 * s + 4 * q;
             const float dxv[4] = {dxr[0], dxr[1], dxr[2], dxr[3]};
 #pragma unroll
@@ -645,9 +664,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
                 const float rx = (crd[kC0(ci)] + 1.0f) * 0.5f * (float)(W - 1);
                 const float ry = (crd[kC1(ci)] + 1.0f) * 0.5f * (float)(H - 1);
                 const Tap t = tap_of(a, pi, ci, crd);
-                const float4* pl = reinterpret_cast<const float4*>(a.planes + a.poff[pi]) + q;
-                const float4 t00 = pl[(t.y0 * W + t.x0) * 4], t01 = pl[(t.y0 * W + t.x1) * 4];
-                const float4 t10 = pl[(t.y1 * W + t.x0) * 4], t11 = pl[(t.y1 * W + t.x1) * 4];
                 const float w00 = (1.0f - t.fx) * (1.0f - t.fy), w01 = t.fx * (1.0f - t.fy),
                             w10 = (1.0f - t.fx) * t.fy, w11 = t.fx * t.fy;
                 // scatter: stage the wave's 16 Gaussians (16 channels, 4 taps each) in LDS, then one
@@ -686,13 +702,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
                     }
                     wave_lds_sync();   // staging read before the next plane rewrites it
                 }
-                const float a00[4] = {t00.x, t00.y, t00.z, t00.w}, a01[4] = {t01.x, t01.y, t01.z, t01.w};
-                const float a10[4] = {t10.x, t10.y, t10.z, t10.w}, a11[4] = {t11.x, t11.y, t11.z, t11.w};
+                const float gx4[4] = {gxv[ci].x, gxv[ci].y, gxv[ci].z, gxv[ci].w};
+                const float gy4[4] = {gyv[ci].x, gyv[ci].y, gyv[ci].z, gyv[ci].w};
                 float dix = 0.0f, diy = 0.0f;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    dix += dv[i] * ((a01[i] - a00[i]) * (1.0f - t.fy) + (a11[i] - a10[i]) * t.fy);
-                    diy += dv[i] * ((a10[i] - a00[i]) * (1.0f - t.fx) + (a11[i] - a01[i]) * t.fx);
+                    dix += dv[i] * gx4[i];
+                    diy += dv[i] * gy4[i];
                 }
                 if (rx > 0.0f && rx < (float)(W - 1)) dq[kC0(ci)] += dix * 0.5f * (float)(W - 1);
                 if (ry > 0.0f && ry < (float)(H - 1)) dq[kC1(ci)] += diy * 0.5f * (float)(H - 1);
