@@ -182,11 +182,15 @@ def run(args):
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # LSR_BENCH_BACKEND=gloo with LSR_BENCH_SHARE_DEVICE=1 rehearses the N > 1 path on a one-GPU box
+    # (ranks share the card, the bucket all-reduce goes through gloo); the product path is RCCL
+    backend = os.environ.get("LSR_BENCH_BACKEND", "nccl")
+    dev_index = local_rank % max(1, torch.cuda.device_count()) if os.environ.get("LSR_BENCH_SHARE_DEVICE") else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     pg_ranks = 1
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
         pg_ranks = dist.get_world_size()
 
     import diff_gaussian_rasterization as dgr
