@@ -29,7 +29,7 @@ namespace lsr {
 // Diagnostic build only (-DLSR_BWD_STAMPS): per-segment s_memtime sums of the group loop, summed
 // over all waves into g_bwd_stamps (read by lsr_debug_bwd_stamps).  Read shares, not times.
 #ifdef LSR_BWD_STAMPS
-__device__ unsigned long long g_bwd_stamps[12];
+__device__ unsigned long long g_bwd_stamps[16];
 #define BWD_STAMP(seg)                                                                           \
     do {                                                                                         \
         __builtin_amdgcn_sched_barrier(0);                                                       \
@@ -75,6 +75,10 @@ __global__ void __launch_bounds__(64)
 __attribute__((amdgpu_waves_per_eu(NOL ? LSR_BWD_WAVES_NOL : LSR_BWD_WAVES, NOL ? LSR_BWD_WAVES_NOL : LSR_BWD_WAVES)))
 k_render_bwd_wave(RenderBwdBatch ab) {
     const RenderBwdArgs& a = ab.v[blockIdx.y];   // grid row = view
+#ifdef LSR_BWD_STAMPS
+    unsigned long long st_entry;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_entry)::"memory");
+#endif
     static_assert(!(NOL && C32), "NOL has no language channels");
     __shared__ __attribute__((aligned(16))) __bf16 s_FR[64 * 32];        // bm build, then F / W / t rows
     __shared__ __attribute__((aligned(16))) __bf16 s_Gh[NOL ? 8 : 64 * 32];   // G rows (g_off), hi / lo
@@ -111,6 +115,10 @@ k_render_bwd_wave(RenderBwdBatch ab) {
     for (int off = 32; off >= 1; off >>= 1) nrep = max(nrep, (uint32_t)__shfl_xor((int)nrep, off));
     nrep = __builtin_amdgcn_readfirstlane(nrep);
     if (nrep == 0) return;                                           // wave-uniform
+#ifdef LSR_BWD_STAMPS
+    unsigned long long st_nrep;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_nrep)::"memory");
+#endif
     const uint2 range = a.ranges[tile];
     const int C = C32 ? 32 : (NOL ? 0 : (a.include_feature ? a.C : 0));   // language channels in play
     const float bx0 = (float)qx0, by0 = (float)qy0;
@@ -339,12 +347,17 @@ k_render_bwd_wave(RenderBwdBatch ab) {
         acnt = 0;
     };
 
+#ifdef LSR_BWD_STAMPS
+    unsigned long long st_scan;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_scan)::"memory");
+#endif
     scan_fill(WG);
     int cnt = min(WG, tail - head);
     Pf pf;
     if (cnt > 0) load_group(pf, cnt);
 #ifdef LSR_BWD_STAMPS
-    unsigned long long st_sum[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_prev = 0;
+    unsigned long long st_sum[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_prev = 0, st_loop;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_loop)::"memory");
 #endif
     while (cnt > 0) {
         BWD_STAMP(0);
@@ -582,6 +595,15 @@ k_render_bwd_wave(RenderBwdBatch ab) {
         atomicAdd(&g_bwd_stamps[lane], v);
     }
     if (lane == 8) atomicAdd(&g_bwd_stamps[8], 1ull);   // waves that ran groups
+    {   // the wave's setup in three parts, and its whole life
+        unsigned long long st_end;
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_end)::"memory");
+        if (lane == 9) atomicAdd(&g_bwd_stamps[9], st_loop - st_entry);
+        if (lane == 10) atomicAdd(&g_bwd_stamps[10], st_end - st_entry);
+        if (lane == 11) atomicAdd(&g_bwd_stamps[11], st_nrep - st_entry);   // pixel loads, replay bound
+        if (lane == 12) atomicAdd(&g_bwd_stamps[12], st_scan - st_nrep);    // G rows, B operands
+        if (lane == 13) atomicAdd(&g_bwd_stamps[13], st_loop - st_scan);    // first scan + prefetch
+    }
 #endif
 }
 
@@ -658,9 +680,9 @@ void launch_render_bwd_wave_views(const RenderBwdArgs* a, int n, hipStream_t st)
 
 #ifdef LSR_BWD_STAMPS
 // diagnostic export (not part of include/lsr.h): read and reset the stamp sums
-extern "C" int lsr_debug_bwd_stamps(unsigned long long* out9) {
-    if (hipMemcpyFromSymbol(out9, HIP_SYMBOL(lsr::g_bwd_stamps), 9 * sizeof(unsigned long long)) != hipSuccess) return 2;
-    unsigned long long z[12] = {};
+extern "C" int lsr_debug_bwd_stamps(unsigned long long* out14) {   // 8 segments, waves, setup, life, setup parts
+    if (hipMemcpyFromSymbol(out14, HIP_SYMBOL(lsr::g_bwd_stamps), 14 * sizeof(unsigned long long)) != hipSuccess) return 2;
+    unsigned long long z[16] = {};
     return hipMemcpyToSymbol(HIP_SYMBOL(lsr::g_bwd_stamps), z, sizeof(z)) == hipSuccess ? 0 : 2;
 }
 #endif

@@ -30,8 +30,8 @@ def main():
     fn.restype = ctypes.c_int
     sc = synthetic.make_scene(2_000_000, C=32).to("cuda")
     cams = synthetic.camera_batch(4, seed=1)
-    buf = (ctypes.c_ulonglong * 9)()
-    tot = [0] * 9
+    buf = (ctypes.c_ulonglong * 14)()
+    tot = [0] * 14
     for cam in cams:
         rs = raster_settings(cam)
         color, lang, radii, depth, st = dgr.forward_native(rs, sc.means3D, sc.opacities, shs=sc.shs,
@@ -46,12 +46,17 @@ def main():
         dgr.backward_composite_native(st, gc, gl, None, dL_dlanguage=dl)
         torch.cuda.synchronize()
         fn(buf)
-        for i in range(9):
+        for i in range(14):
             tot[i] += buf[i]
     s = sum(tot[:8])
     print("waves", tot[8], "cycles/wave", s / max(tot[8], 1))
     for i, n in enumerate(SEG):
         print(f"{n:14s} {100.0 * tot[i] / s:6.2f} %")
+    w = max(tot[8], 1)
+    print(f"per wave: life {tot[10] / w:.0f} cycles, setup (entry -> first group) {tot[9] / w:.0f} "
+          f"({100.0 * tot[9] / max(tot[10], 1):.1f} % of the lives), group loop {s / w:.0f}")
+    print(f"setup parts per wave: pixel loads + replay bound {tot[11] / w:.0f}, G rows {tot[12] / w:.0f}, "
+          f"first scan + prefetch {tot[13] / w:.0f}")
 
 
 if __name__ == "__main__":
