@@ -740,9 +740,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
 #pragma unroll
                 for (int off = 32; off >= 1; off >>= 1) v[k] += __shfl_xor(v[k], off);
             }
-            if ((tid & 63) == 0) {
+            if ((tid & 63) == 0) {   // one of DEF_AABB_SLOTS partial rows: every wave of a
+                                     // launch adding into the same six words serialised on one L2 line
+                float* row = b.daabb_part + (blockIdx.x % DEF_AABB_SLOTS) * 16;
 #pragma unroll
-                for (int k = 0; k < 6; ++k) atomicAdd(b.daabb + k, v[k]);
+                for (int k = 0; k < 6; ++k) atomicAdd(row + k, v[k]);
             }
         }
     }
@@ -1284,31 +1286,42 @@ void launch_atb(const AtbArgs& a, int njobs, hipStream_t st) {
 }
 
 // packed channel-last gradient replicas [r][H][W][16] -> torch [16][H][W], summed over the replicas
-// and added.  One block per 16 texels (256 floats): each thread sums one float over the replicas
-// with coalesced reads, the block transposes through LDS (pitch 17) and writes each channel's 16
-// texels as one 64-byte run.  (A thread per destination float read 64-byte-strided words of every
-// replica: 0.38 ms per training iteration at configs[4]'s planes.)
-__global__ void __launch_bounds__(256) k_unpack_plane_grad(const float* __restrict__ src, float* __restrict__ dst,
-                                                           int H, int W, int replicas, int64_t stride) {
+// and added, every plane of a call in one launch (one per plane was 12 launches of ~10 us each at
+// the Neu3D planes, mostly launch gaps).  One block per 16 texels (256 floats): each thread sums one
+// float over the replicas with coalesced reads, the block transposes through LDS (pitch 17) and
+// writes each channel's 16 texels as one 64-byte run.  (A thread per destination float read
+// 64-byte-strided words of every replica: 0.38 ms per training iteration at configs[4]'s planes.)
+// One extra block folds the box gradient's partial rows.
+__global__ void __launch_bounds__(256) k_unpack_planes(const UnpackBatch u) {
     __shared__ float s_t[16][17];
+    const int bid = blockIdx.x, t = threadIdx.x;
+    if (bid == u.block0[u.n]) {   // block-uniform: the box gradient
+        if (t < 6) {
+            float acc = 0.0f;
+            for (int r = 0; r < DEF_AABB_SLOTS; ++r) acc += u.daabb_part[r * 16 + t];
+            u.daabb[t] += acc;
+        }
+        return;
+    }
     LDS_POISON(s_t); LDS_POISON_DONE();
-    const int HW = H * W, base = blockIdx.x * 16, t = threadIdx.x;
+    int j = 0;
+    while (j + 1 < u.n && bid >= u.block0[j + 1]) ++j;
+    const int H = u.H[j], W = u.W[j], HW = H * W, base = (bid - u.block0[j]) * 16;
     const int tex = t >> 4, ch = t & 15;
     float acc = 0.0f;
     if (base + tex < HW) {
-        const float* p = src + (size_t)base * 16 + t;
-        for (int r = 0; r < replicas; ++r) acc += p[(size_t)r * stride];
+        const float* p = u.src + u.off[j] + (size_t)base * 16 + t;
+        for (int r = 0; r < u.replicas; ++r) acc += p[(size_t)r * u.stride];
     }
     s_t[tex][ch] = acc;
     __syncthreads();
     const int c = t >> 4, tl = t & 15;
-    if (base + tl < HW) dst[(size_t)c * HW + base + tl] += s_t[tl][c];
+    if (base + tl < HW) u.dst[j][(size_t)c * HW + base + tl] += s_t[tl][c];
 }
 
-void launch_unpack_plane_grad(const float* src, float* dst, int H, int W, int replicas, int64_t stride,
-                              hipStream_t st) {
-    hipLaunchKernelGGL(k_unpack_plane_grad, dim3((H * W + 15) / 16), dim3(256), 0, st, src, dst, H, W, replicas,
-                       stride);
+void launch_unpack_planes(const UnpackBatch& u, hipStream_t st) {
+    const int nb = u.block0[u.n] + (u.daabb ? 1 : 0);
+    if (nb > 0) hipLaunchKernelGGL(k_unpack_planes, dim3(nb), dim3(256), 0, st, u);
 }
 
 // ---- parameter packing ----------------------------------------------------------------------------

@@ -10,6 +10,8 @@
 #include <cstdlib>
 #include <vector>
 
+static_assert(lsr::DEF_UNPACK_MAX == 6 * LSR_DEFORM_MAX_SCALES, "one unpack slot per plane");
+
 namespace lsr {
 int fail(int code, const std::string& msg);   // lsr_api.hip (thread-local lsr_last_error)
 }
@@ -274,7 +276,7 @@ int deform_replicas(size_t P) {
 }
 struct BwdScratch {
     size_t X, A[LSR_DEFORM_MAX_DEPTH], dH[LSR_DEFORM_MAX_DEPTH];
-    size_t Grot, Gcoff, U0, U1, U2, dv, dZ2l, dZ1l, dplanes, total;
+    size_t Grot, Gcoff, U0, U1, U2, dv, dZ2l, dZ1l, daabb, dplanes, total;
 };
 BwdScratch bwd_scratch(const lsr_deform_net* net, size_t P) {
     BwdScratch s{};
@@ -300,6 +302,7 @@ BwdScratch bwd_scratch(const lsr_deform_net* net, size_t P) {
         s.dZ2l = take(P * kW);
         s.dZ1l = take(P * kW);
     }
+    s.daabb = take(lsr::DEF_AABB_SLOTS * 16);   // zeroed with the gradient planes (contiguous)
     s.dplanes = o;
     o += kGradReplicas * layout(net).planes_end;
     s.total = o;
@@ -417,9 +420,10 @@ extern "C" int lsr_deform_backward(const lsr_deform_net* net, const void* worksp
     b.sG_coff = fp(S.Gcoff);
     b.dplanes = fp(S.dplanes);
     b.daabb = grads->aabb;
+    b.daabb_part = fp(S.daabb);
     b.replicas = deform_replicas((size_t)P);
     b.plane_stride = (int64_t)(L.planes_end / sizeof(float));
-    if (hipMemsetAsync(b.dplanes, 0, (size_t)b.replicas * L.planes_end, st) != hipSuccess)
+    if (hipMemsetAsync(sc + S.daabb, 0, (S.dplanes - S.daabb) + (size_t)b.replicas * L.planes_end, st) != hipSuccess)
         return lsr::fail(LSR_EHIP, "memset");
     lsr::launch_deform_bwd_a(b, st);
     lsr::LangDeformArgs la{};
@@ -464,13 +468,24 @@ extern "C" int lsr_deform_backward(const lsr_deform_net* net, const void* worksp
         g.job[nj++] = lsr::AtbJob{la.sdv, la.sU2, grads->w_lang[2], grads->b_lang[2], net->lang_dim, kW};
     }
     lsr::launch_atb(g, nj, st);
+    lsr::UnpackBatch u{};
+    u.src = fp(S.dplanes);
+    u.replicas = b.replicas;
+    u.stride = b.plane_stride;
+    u.daabb_part = b.daabb_part;
+    u.daabb = grads->aabb;
     for (int s = 0; s < net->n_scales; ++s)
         for (int ci = 0; ci < 6; ++ci) {
             int W, H;
             plane_dims(net, s, ci, W, H);
-            lsr::launch_unpack_plane_grad(reinterpret_cast<const float*>(sc + S.dplanes + L.plane_off[6 * s + ci]),
-                                          grads->planes[s][ci], H, W, b.replicas, b.plane_stride, st);
+            const int j = u.n++;
+            u.off[j] = (int64_t)(L.plane_off[6 * s + ci] / sizeof(float));
+            u.dst[j] = grads->planes[s][ci];
+            u.H[j] = H;
+            u.W[j] = W;
+            u.block0[j + 1] = u.block0[j] + (H * W + 15) / 16;
         }
+    lsr::launch_unpack_planes(u, st);
     if (hipGetLastError() != hipSuccess) return lsr::fail(LSR_EHIP, "deformation backward launch failed");
     return LSR_OK;
 }

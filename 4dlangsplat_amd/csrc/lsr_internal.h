@@ -302,8 +302,12 @@ struct DeformBwdArgs {
     float* sdH[DEF_MAX_LAYERS];       // saved [P,128] gradients of H_k
     float* sG_rot;                    // apply_rotation: [P,4] gradient of the rotation head's output
     float* sG_coff;                   // DISCRETE: [P, centers] gradient of coff
-    float* daabb;                     // [2][3] gradient of the HexPlane box (accumulated), or null
+    float* daabb;                     // [2][3] gradient of the HexPlane box (accumulated), or null;
+                                      //   phase A adds into DEF_AABB_SLOTS partial rows of daabb_part
+                                      //   (block b: row b % slots, 64 B apart), the unpack sums them
+    float* daabb_part;
 };
+constexpr int DEF_AABB_SLOTS = 64;
 void launch_deform_bwd_a(const DeformBwdArgs& a, hipStream_t st);
 // Weight gradients of the computed heads by recompute (deform.hip k_head_wgrad): per head and block
 // of rows, from the saved last trunk activation A and the head's output gradient G,
@@ -339,8 +343,22 @@ struct AtbArgs {
     int rows_per_block;
 };
 void launch_atb(const AtbArgs& a, int njobs, hipStream_t st);
-void launch_unpack_plane_grad(const float* src, float* dst, int H, int W, int replicas, int64_t stride,
-                              hipStream_t st);
+// Every gradient plane of a call in one launch: plane j's packed replicas at src + off[j] (floats)
+// summed and added into dst[j] ([16][H][W]); with daabb set, the last block also adds the
+// DEF_AABB_SLOTS partial rows of daabb_part into daabb.
+constexpr int DEF_UNPACK_MAX = 24;   // 6 planes x LSR_DEFORM_MAX_SCALES
+struct UnpackBatch {
+    const float* src;
+    int64_t off[DEF_UNPACK_MAX];
+    float* dst[DEF_UNPACK_MAX];
+    int H[DEF_UNPACK_MAX], W[DEF_UNPACK_MAX];
+    int block0[DEF_UNPACK_MAX + 1];   // first block of plane j; block0[n] = the planes' blocks
+    int n, replicas;
+    int64_t stride;
+    const float* daabb_part;
+    float* daabb;
+};
+void launch_unpack_planes(const UnpackBatch& u, hipStream_t st);
 
 // lang_deform (RESIDUAL / NORESNET): relu([lang, poc_fre(t)]) -> Linear, ReLU, Linear, ReLU, Linear,
 // (+ lang), normalised.  Separate kernels: the MLP reads only the language rows and the time.
