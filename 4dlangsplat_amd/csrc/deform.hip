@@ -15,6 +15,7 @@
 //   below, on the same MFMA helpers.
 #include "lsr_common.h"
 #include "lsr_internal.h"
+#include <cstdlib>
 
 namespace lsr {
 
@@ -1180,9 +1181,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
 }
 
+// rows per block of a launch: LSR_WGRAD_ROWS_SMALL / LSR_WGRAD_ROWS_BIG override (diagnostic A/B)
+static int wgrad_rows(const char* env, int dflt) {
+    const char* e = std::getenv(env);
+    const int r = e ? std::atoi(e) : 0;
+    return r >= 64 ? r / 64 * 64 : dflt;
+}
 void launch_head_wgrad(const HeadWgradArgs& a, int njobs, hipStream_t st) {
     if (a.P <= 0 || njobs <= 0) return;
-    const int nb = (a.P + a.rows_per_block - 1) / a.rows_per_block;
     // the small-output heads first (one launch), then the rest: jobs are reordered into two runs
     HeadWgradArgs s = a;
     int ns = 0, nbig = 0;
@@ -1190,8 +1196,16 @@ void launch_head_wgrad(const HeadWgradArgs& a, int njobs, hipStream_t st) {
         if (a.job[i].nout <= DEF_SMALL_OUT) s.job[ns++] = a.job[i];
     for (int i = 0; i < njobs; ++i)
         if (a.job[i].nout > DEF_SMALL_OUT) { s.job[ns + nbig] = a.job[i]; ++nbig; }
-    if (ns) hipLaunchKernelGGL(k_head_wgrad<true>, dim3(nb, ns), dim3(256), 0, st, s, 0);
-    if (nbig) hipLaunchKernelGGL(k_head_wgrad<false>, dim3(nb, nbig), dim3(256), 0, st, s, ns);
+    if (ns) {
+        s.rows_per_block = wgrad_rows("LSR_WGRAD_ROWS_SMALL", a.rows_per_block);
+        const int nb = (a.P + s.rows_per_block - 1) / s.rows_per_block;
+        hipLaunchKernelGGL(k_head_wgrad<true>, dim3(nb, ns), dim3(256), 0, st, s, 0);
+    }
+    if (nbig) {
+        s.rows_per_block = wgrad_rows("LSR_WGRAD_ROWS_BIG", a.rows_per_block);
+        const int nb = (a.P + s.rows_per_block - 1) / s.rows_per_block;
+        hipLaunchKernelGGL(k_head_wgrad<false>, dim3(nb, nbig), dim3(256), 0, st, s, ns);
+    }
 }
 
 // Phase B: C[M][N] += sum_g L[g][m] R[g][n] (M, N <= 128), bias[m] += sum_g L[g][m]; split-K over

@@ -99,14 +99,16 @@ class TrainStep:
 
     def __init__(self, trainer: GaussianTrainer, field=None, deform_lr: float = 1.6e-4, grid_lr: float = 1.6e-3,
                  bg: Optional[torch.Tensor] = None, stage: str = "fine-base", sh_degree: int = 3,
-                 densify: Optional[Callable[[GaussianTrainer, int], None]] = None, batch_views: bool = False,
+                 densify: Optional[Callable[[GaussianTrainer, int], None]] = None, batch_views: bool = True,
                  joint_train: bool = False, lam: float = 0.2, beta: float = 0.01, addcosloss: bool = False):
         """densify(trainer, iteration): optional densify / prune / reset_opacity schedule, run
         between the densification statistics and the optimizer step (train.py:388-421).
         batch_views: the batch's views share one deformation-field launch (render_views)
-        instead of one per view (render); same values.  Off by default: at configs[4] size
-        the repeat / split copies around the one launch cost more than the per-call fixed work
-        saved (127.8 vs 140.5 iterations/s).
+        instead of one per view (render); same values.  On by default since round 4: with the
+        field's box-gradient atomics spread over partial rows the one launch fills the GPU better
+        than two half-size ones (configs[4] stand-in 187-188 vs 184-185 iterations/s, the field's
+        backward 1.45 vs 1.74 ms per iteration); round 3 had measured the opposite
+        (127.8 vs 140.5) while those atomics serialised.
         joint_train, lam, beta, addcosloss: the 'lang' stages' switches (train.py --joint_coarse /
         --joint_fine, --lam 0.2, --beta 0.01, env addcosloss)."""
         if joint_train and "lang" not in stage:

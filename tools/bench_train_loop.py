@@ -174,14 +174,15 @@ def main():
     ap.add_argument("--window", type=int, default=100)
     ap.add_argument("--point-noise", type=float, default=0.02)
     ap.add_argument("--densify-until-iter", type=int, default=10_000)
-    ap.add_argument("--batched-deform", action="store_true",
-                    help="one deformation launch per iteration over all views (render_views) instead of one per view")
+    ap.add_argument("--per-view-deform", action="store_true",
+                    help="one deformation launch per view (render) instead of one per iteration over all views "
+                         "(render_views, TrainStep's default)")
     args = ap.parse_args()
     dev = torch.device("cuda")
     torch.manual_seed(0)
     t_setup = time.perf_counter()
     step, sched, pool, gts, extent = build(args, dev)
-    step.batch_views = args.batched_deform
+    step.batch_views = not args.per_view_deform
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t_setup
     P0 = step.trainer.P
@@ -225,7 +226,7 @@ def main():
                 config=dict(workload="configs[4] stand-in: synthetic teacher, Neu3D field, fine-base",
                             gaussians=args.gaussians, views_per_iteration=args.views, width=args.width,
                             height=args.height, pool=len(pool), resolution=NEU3D_RES, multires=NEU3D_MULTIRES,
-                            deformation_launches="one per iteration" if args.batched_deform else "per view"),
+                            deformation_launches="per view" if args.per_view_deform else "one per iteration"),
                 data="synthetic")
     print(json.dumps(line))
 
