@@ -314,6 +314,15 @@ k_render_bwd_wave(RenderBwdBatch ab) {
     int acnt = 0;   // entries staged
     auto issue_atomics = [&]() {
         if (acnt == 0) return;
+#ifdef LSR_BWD_ABL_LANGONLY   // timing ablation only: the language rows' atomics, not the small rows'
+        constexpr bool kSmall = false;
+#else
+        constexpr bool kSmall = true;
+#endif
+#ifdef LSR_BWD_ABL_NOATOMIC   // timing ablation only (no gradients): the atomics' share
+        acnt = 0;
+        return;
+#endif
         // every staged value and row offset read from LDS first (one wait), then the atomics
         const int ch = lane & 31, q = lane & 15;
         float lv[WG / 2], sv[WG / 4];
@@ -343,7 +352,7 @@ k_render_bwd_wave(RenderBwdBatch ab) {
         }
 #pragma unroll
         for (int r = 0; r < WG / 4; ++r)
-            if ((lane >> 4) + 4 * r < acnt && q < 10 && sv[r] != 0.0f) atomicAdd(at32(a.acc_small, so[r]), sv[r]);
+            if (kSmall && (lane >> 4) + 4 * r < acnt && q < 10 && sv[r] != 0.0f) atomicAdd(at32(a.acc_small, so[r]), sv[r]);
         acnt = 0;
     };
 
