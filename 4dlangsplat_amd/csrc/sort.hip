@@ -9,6 +9,7 @@
 // Stable tile sort of depth-ordered instances == the upstream sort of (tile << 32 | depth) keys.
 #include "lsr_common.h"
 #include "lsr_internal.h"
+#include <cstdlib>
 
 namespace lsr {
 
@@ -312,50 +313,52 @@ __global__ void __launch_bounds__(256) k_rts_count(const SortBatch b, int pass, 
     counts[(size_t)blockIdx.x * 256 + tid] = s_h[0][tid] + s_h[1][tid] + s_h[2][tid] + s_h[3][tid];
 }
 
-// The scan, one block per (16-digit group, segment): thread t owns
-// SCAN16_ROWS consecutive block rows of a chunk and reads each row's 16 counts as one 64-byte
-// piece (four 16-byte loads, all in flight at once), so the count table is read once in whole
-// pieces instead of one 4-byte word per (row, digit block) -- a per-digit scan kernel touched every
-// line of the table from 256 blocks (33 us per depth pass, 58 us per tile pass on 8 views).
-// Digit groups past 2^nbits (the tile sort's 7- and 6-bit passes) only zero their totals.
-constexpr int SCAN16_ROWS = 8;
-__global__ void __launch_bounds__(256) k_rts_scan16(const SortBatch b, int pass, int it, int nbits) {
-    __shared__ uint32_t s_part[4][16];
+// The scan, one block per (DG-digit group, segment): thread t owns SCAN_ROWS consecutive block
+// rows of a chunk and reads each row's DG counts as DG / 4 16-byte loads (all in flight at once),
+// so the count table is read once in whole pieces instead of one 4-byte word per (row, digit
+// block) -- a per-digit scan kernel touched every line of the table from 256 blocks (33 us per
+// depth pass, 58 us per tile pass on 8 views).  Digit groups past 2^nbits (the tile sort's 7- and
+// 6-bit passes) only zero their totals.
+constexpr int SCAN_ROWS = 8;
+template <int DG>
+__global__ void __launch_bounds__(256) k_rts_scan(const SortBatch b, int pass, int it, int nbits) {
+    constexpr int Q = DG / 4;
+    __shared__ uint32_t s_part[4][DG];
     const SortSeg& sg = b.s[blockIdx.y];
-    const int d0 = 16 * (int)blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int d0 = DG * (int)blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t* __restrict__ totals = rts_totals(sg, pass);
     if (d0 >= (1 << nbits)) {                                        // block-uniform
-        if (tid < 16) totals[d0 + tid] = 0u;
+        if (tid < DG) totals[d0 + tid] = 0u;
         return;
     }
     const int nb = (int)rts_blocks(sg.n, it);
     uint32_t* __restrict__ counts = rts_rows(sg, pass, (size_t)nb);
-    uint32_t carry[16];
+    uint32_t carry[DG];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) carry[j] = 0u;
-    for (int c0 = 0; c0 < nb; c0 += 256 * SCAN16_ROWS) {
-        const int r0 = c0 + tid * SCAN16_ROWS;
-        uint4 v[SCAN16_ROWS][4];
+    for (int j = 0; j < DG; ++j) carry[j] = 0u;
+    for (int c0 = 0; c0 < nb; c0 += 256 * SCAN_ROWS) {
+        const int r0 = c0 + tid * SCAN_ROWS;
+        uint4 v[SCAN_ROWS][Q];
 #pragma unroll
-        for (int r = 0; r < SCAN16_ROWS; ++r) {
+        for (int r = 0; r < SCAN_ROWS; ++r) {
             const uint4* p = reinterpret_cast<const uint4*>(counts + (size_t)(r0 + r) * 256 + d0);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) v[r][q] = r0 + r < nb ? p[q] : make_uint4(0u, 0u, 0u, 0u);
+            for (int q = 0; q < Q; ++q) v[r][q] = r0 + r < nb ? p[q] : make_uint4(0u, 0u, 0u, 0u);
         }
-        uint32_t sum[16];
+        uint32_t sum[DG];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < Q; ++q) {
             sum[4 * q] = 0u; sum[4 * q + 1] = 0u; sum[4 * q + 2] = 0u; sum[4 * q + 3] = 0u;
 #pragma unroll
-            for (int r = 0; r < SCAN16_ROWS; ++r) {
+            for (int r = 0; r < SCAN_ROWS; ++r) {
                 sum[4 * q] += v[r][q].x; sum[4 * q + 1] += v[r][q].y;
                 sum[4 * q + 2] += v[r][q].z; sum[4 * q + 3] += v[r][q].w;
             }
         }
-        // exclusive scan of the 16 per-thread sums over the block's threads (rows in order)
-        uint32_t off[16], tot[16];
+        // exclusive scan of the DG per-thread sums over the block's threads (rows in order)
+        uint32_t off[DG], tot[DG];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
+        for (int j = 0; j < DG; ++j) {
             uint32_t inc = sum[j];
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
@@ -367,7 +370,7 @@ __global__ void __launch_bounds__(256) k_rts_scan16(const SortBatch b, int pass,
         }
         __syncthreads();
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
+        for (int j = 0; j < DG; ++j) {
             uint32_t before = 0u, all = 0u;
 #pragma unroll
             for (int w = 0; w < 4; ++w) {
@@ -379,25 +382,42 @@ __global__ void __launch_bounds__(256) k_rts_scan16(const SortBatch b, int pass,
             tot[j] = all;
         }
 #pragma unroll
-        for (int r = 0; r < SCAN16_ROWS; ++r) {
+        for (int r = 0; r < SCAN_ROWS; ++r) {
             if (r0 + r >= nb) break;
             uint4* p = reinterpret_cast<uint4*>(counts + (size_t)(r0 + r) * 256 + d0);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < Q; ++q) {
                 const uint4 x = v[r][q];
                 p[q] = make_uint4(off[4 * q], off[4 * q + 1], off[4 * q + 2], off[4 * q + 3]);
                 off[4 * q] += x.x; off[4 * q + 1] += x.y; off[4 * q + 2] += x.z; off[4 * q + 3] += x.w;
             }
         }
 #pragma unroll
-        for (int j = 0; j < 16; ++j) carry[j] += tot[j];
+        for (int j = 0; j < DG; ++j) carry[j] += tot[j];
         __syncthreads();   // s_part reused by the next chunk
     }
-    if (tid < 16) {
+    if (tid < DG) {
         uint32_t t = 0u;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) t = tid == j ? carry[j] : t;
+        for (int j = 0; j < DG; ++j) t = tid == j ? carry[j] : t;
         totals[d0 + tid] = t;
+    }
+}
+
+// digits per scan block: LSR_SCAN_DG = 4 / 8 / 16 overrides (diagnostic A/B)
+static int scan_dg() {
+    static const int dg = [] {
+        const char* e = std::getenv("LSR_SCAN_DG");
+        const int v = e ? std::atoi(e) : 0;
+        return (v == 4 || v == 8 || v == 16) ? v : 16;
+    }();
+    return dg;
+}
+static void launch_rts_scan(const SortBatch& bt, int ns, int p, int items, int nbits, hipStream_t st) {
+    switch (scan_dg()) {
+        case 4: hipLaunchKernelGGL(k_rts_scan<4>, dim3(64, ns), dim3(256), 0, st, bt, p, items, nbits); break;
+        case 8: hipLaunchKernelGGL(k_rts_scan<8>, dim3(32, ns), dim3(256), 0, st, bt, p, items, nbits); break;
+        default: hipLaunchKernelGGL(k_rts_scan<16>, dim3(16, ns), dim3(256), 0, st, bt, p, items, nbits); break;
     }
 }
 
@@ -548,7 +568,7 @@ bool radix_sort_batch(const SortSeg* segs, int nseg, int begin_bit, int end_bit,
             hipLaunchKernelGGL(k_rts_count<12>, dim3(nbi, ns), dim3(256), 0, st, bt, p, (int)in_b, shift, nbits);
         else
             hipLaunchKernelGGL(k_rts_count<OS_ITEMS>, dim3(nbi, ns), dim3(256), 0, st, bt, p, (int)in_b, shift, nbits);
-        hipLaunchKernelGGL(k_rts_scan16, dim3(16, ns), dim3(256), 0, st, bt, p, items, nbits);
+        launch_rts_scan(bt, ns, p, items, nbits, st);
         if (items == 12)
             hipLaunchKernelGGL(k_rts_scatter<12>, dim3(nbi, ns), dim3(256), 0, st, bt, p, (int)in_b, shift, nbits, last);
         else
