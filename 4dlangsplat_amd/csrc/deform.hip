@@ -15,6 +15,7 @@
 //   below, on the same MFMA helpers.
 #include "lsr_common.h"
 #include "lsr_internal.h"
+#include <algorithm>
 #include <cstdlib>
 
 namespace lsr {
@@ -1181,11 +1182,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
 }
 
-// rows per block of a launch: LSR_WGRAD_ROWS_SMALL / LSR_WGRAD_ROWS_BIG override (diagnostic A/B)
-static int wgrad_rows(const char* env, int dflt) {
+// Rows per block of a launch, for about `blocks` blocks per head: 128 for the small-output heads
+// (their per-block flush of dW1 / dW2 partials is most of their atomics), 400 for the SH head.
+// Measured against the split-K default of 256 blocks per head: deformation backward 11.96-11.99
+// -> 11.20-11.21 ms at 2M, configs[4] stand-in 1.449-1.454 -> 1.391-1.400 ms per iteration.
+// LSR_WGRAD_ROWS_SMALL / LSR_WGRAD_ROWS_BIG override (diagnostic A/B).
+static int wgrad_rows(const char* env, int P, int blocks) {
     const char* e = std::getenv(env);
     const int r = e ? std::atoi(e) : 0;
-    return r >= 64 ? r / 64 * 64 : dflt;
+    if (r >= 64) return r / 64 * 64;
+    return std::max(64, ((P + blocks - 1) / blocks + 63) / 64 * 64);
 }
 void launch_head_wgrad(const HeadWgradArgs& a, int njobs, hipStream_t st) {
     if (a.P <= 0 || njobs <= 0) return;
@@ -1197,12 +1203,12 @@ void launch_head_wgrad(const HeadWgradArgs& a, int njobs, hipStream_t st) {
     for (int i = 0; i < njobs; ++i)
         if (a.job[i].nout > DEF_SMALL_OUT) { s.job[ns + nbig] = a.job[i]; ++nbig; }
     if (ns) {
-        s.rows_per_block = wgrad_rows("LSR_WGRAD_ROWS_SMALL", a.rows_per_block);
+        s.rows_per_block = wgrad_rows("LSR_WGRAD_ROWS_SMALL", a.P, 128);
         const int nb = (a.P + s.rows_per_block - 1) / s.rows_per_block;
         hipLaunchKernelGGL(k_head_wgrad<true>, dim3(nb, ns), dim3(256), 0, st, s, 0);
     }
     if (nbig) {
-        s.rows_per_block = wgrad_rows("LSR_WGRAD_ROWS_BIG", a.rows_per_block);
+        s.rows_per_block = wgrad_rows("LSR_WGRAD_ROWS_BIG", a.P, 400);
         const int nb = (a.P + s.rows_per_block - 1) / s.rows_per_block;
         hipLaunchKernelGGL(k_head_wgrad<false>, dim3(nb, nbig), dim3(256), 0, st, s, ns);
     }

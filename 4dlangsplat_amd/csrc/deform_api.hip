@@ -452,7 +452,6 @@ extern "C" int lsr_deform_backward(const lsr_deform_net* net, const void* worksp
     lsr::HeadWgradArgs hw{};
     hw.A = b.sA[b.f.nlayers - 1];
     hw.P = P;
-    hw.rows_per_block = g.rows_per_block;
     int nh = 0;
     for (int hd = 0; hd < LSR_DEFORM_HEADS; ++hd) {
         if (!head_on(net, hd)) continue;

@@ -326,7 +326,7 @@ constexpr int DEF_WGRAD_MAX_JOBS = DEF_HEADS;
 struct HeadWgradArgs {
     HeadWgradJob job[DEF_WGRAD_MAX_JOBS];
     const float* A;                   // [P][128] the trunk's last activation (phase A saved it)
-    int P, rows_per_block;
+    int P, rows_per_block;            // rows_per_block: set per launch by launch_head_wgrad
 };
 void launch_head_wgrad(const HeadWgradArgs& a, int njobs, hipStream_t st);
 struct AtbJob {                        // C[M][N] += sum_g L[g][m] R[g][n]; bias[m] += sum_g L[g][m]
