@@ -1301,8 +1301,13 @@ __global__ void __launch_bounds__(256) k_atb(AtbArgs ga) {
 
 void launch_atb(const AtbArgs& a, int njobs, hipStream_t st) {
     if (a.P <= 0 || njobs <= 0) return;
-    const int nb = (a.P + a.rows_per_block - 1) / a.rows_per_block;
-    hipLaunchKernelGGL(k_atb, dim3(nb, njobs), dim3(256), 0, st, a);
+    AtbArgs s = a;
+    if (const char* e = std::getenv("LSR_ATB_BLOCKS")) {   // diagnostic A/B: blocks per job
+        const int nbt = std::max(1, std::atoi(e));
+        s.rows_per_block = std::max(64, ((a.P + nbt - 1) / nbt + 63) / 64 * 64);
+    }
+    const int nb = (s.P + s.rows_per_block - 1) / s.rows_per_block;
+    hipLaunchKernelGGL(k_atb, dim3(nb, njobs), dim3(256), 0, st, s);
 }
 
 // packed channel-last gradient replicas [r][H][W][16] -> torch [16][H][W], summed over the replicas
