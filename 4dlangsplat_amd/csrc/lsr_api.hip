@@ -200,7 +200,7 @@ int tile_bits(int ntiles) {
     return b;
 }
 bool tile_sort_in_b(int ntiles) { return ((tile_bits(ntiles) + 7) / 8) % 2 == 1; }
-int depth_sort_result_in_b() { return 0; }  // 32 key bits = 4 passes: result back in the (a) buffers
+int depth_sort_result_in_b() { return 0; }  // 4 passes, or 3 planned on the device: either way in the (a) buffers
 
 int check_common(const lsr_settings* s, const lsr_fwd_in* in) {
     if (g_caller_api.load() != LSR_API_VERSION)   // the structs' layout is that of this lsr.h only
@@ -327,7 +327,7 @@ int lsr_forward_preprocess_async(const lsr_settings* s, const lsr_fwd_in* in, ls
         // of culled Gaussians keep the zero counts the preprocess wrote)
         const lsr::SortGather gather{g.rect, g.counts, g.rect_sorted};
         in_b = lsr::radix_sort_pairs(g.key_a, g.val_a, g.key_b, g.val_b, (size_t)P, 0, 32, g.sort_tmp, st, g.total + 3,
-                                     &gather);
+                                     &gather, g.offsets);   // offsets: free until the instance scan
     }
     if (in_b != (bool)depth_sort_result_in_b()) return fail(LSR_EHIP, "internal: depth sort parity");
     LSR_LAUNCHED("depth sort", st, s->debug);
@@ -382,6 +382,7 @@ int lsr_forward_preprocess_views_async(int32_t n_views, const lsr_settings* cons
             // g.total[3]; the last pass writes the depth-ranked rectangles and instance counts)
             ss[k] = lsr::SortSeg{g.key_a, g.val_a, g.key_b, g.val_b, g.sort_tmp, g.total + 3,
                                  lsr::SortGather{g.rect, g.counts, g.rect_sorted}, (size_t)P};
+            ss[k].vals_c = g.offsets;   // the device-planned passes' scratch (free until the instance scan)
             sc[k] = lsr::ScanSeg{g.counts, g.offsets, g.total, reinterpret_cast<uint32_t*>(g.scan_tmp), (size_t)P};
             if (mapped) {   // the scan writes K straight to the caller's pinned word (the preprocess
                 sc[k].host_total = mapped + 2 * (v0 + k);   // zeroed a view's reserved word only on the

@@ -430,6 +430,9 @@ struct SortSeg {
     // atomicMax at the key runs' ends; entries preset to (0xFFFFFFFF, 0), keys >= nranges skipped)
     uint2* ranges;
     uint32_t nranges;
+    // depth sort (with kept and gather): [n] scratch for the values of the device-planned middle
+    // pass (sort.hip); set, the batch's passes are planned on the device (every segment sets it)
+    uint32_t* vals_c;
 };
 struct SortBatch { SortSeg s[LSR_MAX_VIEWS]; };
 // Sorts up to LSR_MAX_VIEWS independent segments with one launch per kernel of each pass (every
@@ -437,7 +440,7 @@ struct SortBatch { SortSeg s[LSR_MAX_VIEWS]; };
 bool radix_sort_batch(const SortSeg* segs, int nseg, int begin_bit, int end_bit, hipStream_t st);
 bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b, size_t n,
                       int begin_bit, int end_bit, void* temp, hipStream_t st, uint32_t* kept = nullptr,
-                      const SortGather* gather = nullptr);
+                      const SortGather* gather = nullptr, uint32_t* vals_c = nullptr);
 
 // binning (binning.hip)
 // Point-list values: Gaussian id in the low 28 bits, in the top 4 the quadrants (bit 28 + q,

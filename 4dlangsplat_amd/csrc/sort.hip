@@ -3,7 +3,8 @@
 // digit counts in LDS, and per-digit running offsets, so every pass is stable.
 //
 // Used twice per frame by the binning (binning.hip):
-//   1. depth order of all P Gaussians: key = view-space depth bits (culled = 0xFFFFFFFF), 4 passes;
+//   1. depth order of all P Gaussians: key = view-space depth bits (culled = 0xFFFFFFFF), 8 + 9 + 9
+//      bits above the kept keys' 256-aligned minimum when they span < 2^26 of it, else 4 x 8 bits;
 //   2. tile order of the K (Gaussian, tile) instances emitted in depth order: key = tile id,
 //      ceil(log2(tiles)) bits (2 passes at 5,440 tiles).
 // Stable tile sort of depth-ordered instances == the upstream sort of (tile << 32 | depth) keys.
@@ -219,14 +220,23 @@ uint32_t exclusive_scan_batch(const ScanSeg* segs, int nseg, hipStream_t st) {
 
 // ---- radix sort ---------------------------------------------------------------------------------
 // Reduce-then-scan LSD passes, 8 keys per thread (12 above 4M keys): per pass a count kernel writes
-// every block's 256 digit counts, a scan kernel turns them into each block's offset inside its
-// digit and the digit totals, and the scatter kernel ranks the block's keys again (ballot digit
-// matching per wave, stable), places them digit-sorted in LDS and writes runs (coalesced stores).
+// every block's digit counts, a scan kernel turns them into each block's offset inside its digit
+// and the digit totals, and the scatter kernel ranks the block's keys again (ballot digit matching
+// per wave, stable), places them digit-sorted in LDS and writes runs (coalesced stores).
 // There is no inter-block chain: a decoupled look-back (one pass kernel, blocks waiting on their
 // predecessors' published counts) crossed the 8 XCDs' non-coherent L2s at every hop and bounded a
 // pass by the chain length; it was removed in round 3.
+//
+// Digits are up to 9 bits (RDX = 512).  Host-planned sorts (the tile sort) give every launch its
+// shift / width; the depth sort (SortSeg::vals_c set) plans on the device: its first pass takes
+// the low 8 bits and records each block's smallest and largest kept key, its scan fixes
+// kbase = min & ~0xFF, and when the kept keys span less than 2^26 above kbase (depths within a
+// factor of 256) the sort finishes in two 9-bit passes over key - kbase instead of three 8-bit
+// ones.  Both plans leave the result in the (a) buffers: the three-pass plan's middle pass writes
+// its values to vals_c (free scratch) so that its last pass can gather into vals_a.
 constexpr int OS_ITEMS = 8;                   // keys per thread per pass (4 / 8 / 16 swept)
 constexpr int OS_TILE = 256 * OS_ITEMS;       // keys per block
+constexpr int RDX = 512;                      // digits of the widest pass (count rows' stride)
 
 // Peers of this lane's digit inside the wave (lanes with the same digit among the valid lanes).
 __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool valid, int nbits) {
@@ -265,34 +275,73 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t x, uint32_t* s_w
 __device__ __forceinline__ size_t rts_n(size_t n, const uint32_t* n_dev) {
     return n_dev ? min(n, (size_t)*n_dev) : n;
 }
-// A segment's workspace: digit totals [pass][256] at the front, then the per-pass count rows
-// [pass][block][256].
-constexpr size_t RTS_ROWS_OFF = 4 * 256 * 4;
+// A segment's workspace: digit totals [pass][RDX], the depth plan (kbase, three-pass flag), then
+// the per-pass count rows [pass][block][RDX] (the first pass's rows also carry the block's smallest
+// and largest kept key in words 256 / 257 when the plan is made on the device).
+constexpr size_t RTS_PLAN_OFF = 4 * RDX * 4;
+constexpr size_t RTS_ROWS_OFF = RTS_PLAN_OFF + 256;
 __device__ __forceinline__ size_t rts_blocks(size_t n, int it) { return (n + 256 * (size_t)it - 1) / (256 * (size_t)it); }
 __device__ __forceinline__ uint32_t* rts_rows(const SortSeg& g, int pass, size_t nbi) {
-    return reinterpret_cast<uint32_t*>(static_cast<char*>(g.temp) + RTS_ROWS_OFF) + (size_t)pass * nbi * 256;
+    return reinterpret_cast<uint32_t*>(static_cast<char*>(g.temp) + RTS_ROWS_OFF) + (size_t)pass * nbi * RDX;
 }
 __device__ __forceinline__ uint32_t* rts_totals(const SortSeg& g, int pass) {
-    return static_cast<uint32_t*>(g.temp) + pass * 256;
+    return static_cast<uint32_t*>(g.temp) + pass * RDX;
+}
+__device__ __forceinline__ uint32_t* rts_plan(const SortSeg& g) {
+    return reinterpret_cast<uint32_t*>(static_cast<char*>(g.temp) + RTS_PLAN_OFF);
+}
+
+// One pass of one segment: digit = ((key - kbase) >> shift) & (2^nbits - 1); buffers by id
+// (0: a, 1: b, 2: keys a with values in vals_c).
+struct PassDesc {
+    int active, shift, nbits, last, src, dst;
+    uint32_t kbase;
+};
+__device__ __forceinline__ PassDesc pass_desc(const SortSeg& sg, int pass, int in_b, int shift, int nbits, int last) {
+    PassDesc d{1, shift, nbits, last, in_b, in_b ^ 1, 0u};
+    if (!sg.vals_c) return d;                                      // host plan
+    if (pass == 0) return PassDesc{1, 0, 8, 0, 0, 1, 0u};
+    const uint32_t* pl = rts_plan(sg);
+    const uint32_t kbase = pl[0], three = pl[1];
+    if (three) {
+        if (pass == 1) return PassDesc{1, 8, 9, 0, 1, 2, kbase};
+        if (pass == 2) return PassDesc{1, 17, 9, 1, 2, 0, kbase};
+        return PassDesc{0, 0, 8, 0, 0, 0, kbase};
+    }
+    return PassDesc{1, 8 * pass, 8, pass == 3, pass & 1, (pass & 1) ^ 1, 0u};
+}
+__device__ __forceinline__ const uint32_t* keys_of(const SortSeg& g, int id) { return id == 1 ? g.keys_b : g.keys_a; }
+__device__ __forceinline__ uint32_t* keys_of_w(const SortSeg& g, int id) { return id == 1 ? g.keys_b : g.keys_a; }
+__device__ __forceinline__ const uint32_t* vals_of(const SortSeg& g, int id) {
+    return id == 1 ? g.vals_b : id == 2 ? g.vals_c : g.vals_a;
+}
+__device__ __forceinline__ uint32_t* vals_of_w(const SortSeg& g, int id) {
+    return id == 1 ? g.vals_b : id == 2 ? g.vals_c : g.vals_a;
 }
 
 // Every kernel of a pass serves all segments of a batch: blockIdx.y is the segment, blocks past
 // a segment's own count return at once (the grid is sized for the largest segment).
 template <int IT>
 __global__ void __launch_bounds__(256) k_rts_count(const SortBatch b, int pass, int in_b, int shift, int nbits) {
-    __shared__ uint32_t s_h[4][256];
+    __shared__ uint32_t s_h[4][RDX];
+    __shared__ uint32_t s_mm[2][4];
     const SortSeg& sg = b.s[blockIdx.y];
     const size_t nbi = rts_blocks(sg.n, IT);
     if (blockIdx.x >= nbi) return;                                   // block-uniform
-    const uint32_t* __restrict__ keys = in_b ? sg.keys_b : sg.keys_a;
+    const PassDesc pd = pass_desc(sg, pass, in_b, shift, nbits, 0);
+    if (!pd.active) return;                                          // segment-uniform
+    const uint32_t* __restrict__ keys = keys_of(sg, pd.src);
     const int drop = sg.kept && pass == 0;                         // first pass drops, later passes read
     const size_t n = rts_n(sg.n, sg.kept && pass > 0 ? sg.kept : nullptr);
     uint32_t* __restrict__ counts = rts_rows(sg, pass, nbi);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) s_h[w][tid] = 0;
+    for (int w = 0; w < 4; ++w) {
+        s_h[w][tid] = 0;
+        s_h[w][tid + 256] = 0;
+    }
     __syncthreads();
-    const uint32_t mask = (1u << nbits) - 1u;
+    const uint32_t mask = (1u << pd.nbits) - 1u;
     const uint64_t lt = lanemask_lt();
     const size_t base = (size_t)blockIdx.x * (256 * IT) + (size_t)wave * (64 * IT);
     uint32_t key[IT];
@@ -301,38 +350,86 @@ __global__ void __launch_bounds__(256) k_rts_count(const SortBatch b, int pass, 
         const size_t idx = base + (size_t)r * 64 + lane;
         key[r] = idx < n ? keys[idx] : 0u;
     }
+    uint32_t kmin = 0xFFFFFFFFu, kmax = 0u;
 #pragma unroll
     for (int r = 0; r < IT; ++r) {
         const bool valid = base + (size_t)r * 64 + lane < n && !(drop && key[r] == 0xFFFFFFFFu);
-        const uint32_t d = (key[r] >> shift) & mask;
-        const uint64_t peers = match_digit(d, valid, nbits);
+        if (valid) {
+            kmin = min(kmin, key[r]);
+            kmax = max(kmax, key[r]);
+        }
+        const uint32_t d = ((key[r] - pd.kbase) >> pd.shift) & mask;
+        const uint64_t peers = match_digit(d, valid, pd.nbits);
         if (valid && (peers & lt) == 0) s_h[wave][d] += (uint32_t)__popcll(peers);   // one leader per digit
         __builtin_amdgcn_wave_barrier();
     }
+    const bool plan = sg.vals_c && pass == 0;                      // segment-uniform
+    if (plan) {
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o));
+            kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
+        }
+        if (lane == 0) { s_mm[0][wave] = kmin; s_mm[1][wave] = kmax; }
+    }
     __syncthreads();
-    counts[(size_t)blockIdx.x * 256 + tid] = s_h[0][tid] + s_h[1][tid] + s_h[2][tid] + s_h[3][tid];
+    for (int d = tid; d < (1 << pd.nbits); d += 256)
+        counts[(size_t)blockIdx.x * RDX + d] = s_h[0][d] + s_h[1][d] + s_h[2][d] + s_h[3][d];
+    if (plan && tid < 2) {   // words 256 / 257 of the 8-bit pass's row: the block's kept-key range
+        const uint32_t v = tid == 0 ? min(min(s_mm[0][0], s_mm[0][1]), min(s_mm[0][2], s_mm[0][3]))
+                                    : max(max(s_mm[1][0], s_mm[1][1]), max(s_mm[1][2], s_mm[1][3]));
+        counts[(size_t)blockIdx.x * RDX + 256 + tid] = v;
+    }
 }
 
 // The scan, one block per (DG-digit group, segment): thread t owns SCAN_ROWS consecutive block
 // rows of a chunk and reads each row's DG counts as DG / 4 16-byte loads (all in flight at once),
 // so the count table is read once in whole pieces instead of one 4-byte word per (row, digit
 // block) -- a per-digit scan kernel touched every line of the table from 256 blocks (33 us per
-// depth pass, 58 us per tile pass on 8 views).  Digit groups past 2^nbits (the tile sort's 7- and
-// 6-bit passes) only zero their totals.
+// depth pass, 58 us per tile pass on 8 views).  Digit groups past 2^nbits only zero their totals.
+// For a device-planned segment, block 0 of the first pass also makes the plan from the rows'
+// key ranges.
 constexpr int SCAN_ROWS = 8;
 template <int DG>
-__global__ void __launch_bounds__(256) k_rts_scan(const SortBatch b, int pass, int it, int nbits) {
+__global__ void __launch_bounds__(256) k_rts_scan(const SortBatch b, int pass, int it, int in_b, int nbits_h) {
     constexpr int Q = DG / 4;
     __shared__ uint32_t s_part[4][DG];
     const SortSeg& sg = b.s[blockIdx.y];
+    const PassDesc pd = pass_desc(sg, pass, in_b, 0, nbits_h, 0);
+    if (!pd.active) return;                                          // segment-uniform
+    const int nbits = pd.nbits;
     const int d0 = DG * (int)blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t* __restrict__ totals = rts_totals(sg, pass);
+    const int nb = (int)rts_blocks(sg.n, it);
+    uint32_t* __restrict__ counts = rts_rows(sg, pass, (size_t)nb);
+    if (sg.vals_c && pass == 0 && blockIdx.x == 0) {   // the depth plan: smallest / largest kept key
+        uint32_t kmin = 0xFFFFFFFFu, kmax = 0u;
+        for (int r = tid; r < nb; r += 256) {
+            kmin = min(kmin, counts[(size_t)r * RDX + 256]);
+            kmax = max(kmax, counts[(size_t)r * RDX + 257]);
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o));
+            kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o));
+        }
+        if (lane == 0) { s_part[0][wave] = kmin; s_part[1][wave] = kmax; }
+        __syncthreads();
+        if (tid == 0) {
+            const uint32_t lo = min(min(s_part[0][0], s_part[0][1]), min(s_part[0][2], s_part[0][3]));
+            const uint32_t hi = max(max(s_part[1][0], s_part[1][1]), max(s_part[1][2], s_part[1][3]));
+            const uint32_t kbase = lo & ~0xFFu;
+            const bool three = lo <= hi && hi - kbase < (1u << 26);
+            uint32_t* pl = rts_plan(sg);
+            pl[0] = three ? kbase : 0u;
+            pl[1] = three ? 1u : 0u;
+        }
+        __syncthreads();   // s_part reused below
+    }
     if (d0 >= (1 << nbits)) {                                        // block-uniform
         if (tid < DG) totals[d0 + tid] = 0u;
         return;
     }
-    const int nb = (int)rts_blocks(sg.n, it);
-    uint32_t* __restrict__ counts = rts_rows(sg, pass, (size_t)nb);
     uint32_t carry[DG];
 #pragma unroll
     for (int j = 0; j < DG; ++j) carry[j] = 0u;
@@ -341,7 +438,7 @@ __global__ void __launch_bounds__(256) k_rts_scan(const SortBatch b, int pass, i
         uint4 v[SCAN_ROWS][Q];
 #pragma unroll
         for (int r = 0; r < SCAN_ROWS; ++r) {
-            const uint4* p = reinterpret_cast<const uint4*>(counts + (size_t)(r0 + r) * 256 + d0);
+            const uint4* p = reinterpret_cast<const uint4*>(counts + (size_t)(r0 + r) * RDX + d0);
 #pragma unroll
             for (int q = 0; q < Q; ++q) v[r][q] = r0 + r < nb ? p[q] : make_uint4(0u, 0u, 0u, 0u);
         }
@@ -384,7 +481,7 @@ __global__ void __launch_bounds__(256) k_rts_scan(const SortBatch b, int pass, i
 #pragma unroll
         for (int r = 0; r < SCAN_ROWS; ++r) {
             if (r0 + r >= nb) break;
-            uint4* p = reinterpret_cast<uint4*>(counts + (size_t)(r0 + r) * 256 + d0);
+            uint4* p = reinterpret_cast<uint4*>(counts + (size_t)(r0 + r) * RDX + d0);
 #pragma unroll
             for (int q = 0; q < Q; ++q) {
                 const uint4 x = v[r][q];
@@ -413,42 +510,48 @@ static int scan_dg() {
     }();
     return dg;
 }
-static void launch_rts_scan(const SortBatch& bt, int ns, int p, int items, int nbits, hipStream_t st) {
-    switch (scan_dg()) {
-        case 4: hipLaunchKernelGGL(k_rts_scan<4>, dim3(64, ns), dim3(256), 0, st, bt, p, items, nbits); break;
-        case 8: hipLaunchKernelGGL(k_rts_scan<8>, dim3(32, ns), dim3(256), 0, st, bt, p, items, nbits); break;
-        default: hipLaunchKernelGGL(k_rts_scan<16>, dim3(16, ns), dim3(256), 0, st, bt, p, items, nbits); break;
+static void launch_rts_scan(const SortBatch& bt, int ns, int p, int items, int in_b, int nbits, hipStream_t st) {
+    switch (scan_dg()) {   // the grid covers RDX digits (groups past a pass's digits exit)
+        case 4: hipLaunchKernelGGL(k_rts_scan<4>, dim3(RDX / 4, ns), dim3(256), 0, st, bt, p, items, in_b, nbits); break;
+        case 8: hipLaunchKernelGGL(k_rts_scan<8>, dim3(RDX / 8, ns), dim3(256), 0, st, bt, p, items, in_b, nbits); break;
+        default: hipLaunchKernelGGL(k_rts_scan<16>, dim3(RDX / 16, ns), dim3(256), 0, st, bt, p, items, in_b, nbits); break;
     }
 }
 
 template <int IT>
-__global__ void __launch_bounds__(256) k_rts_scatter(const SortBatch b, int pass, int in_b, int shift, int nbits,
-                                                     int last) {
+__global__ void __launch_bounds__(256) k_rts_scatter(const SortBatch b, int pass, int in_b, int shift, int nbits_h,
+                                                     int last_h) {
     __shared__ uint32_t s_key[(256 * IT)];
     __shared__ uint32_t s_val[(256 * IT)];
-    __shared__ uint32_t s_wcnt[4][256];
-    __shared__ uint32_t s_gbase[256];
-    __shared__ uint32_t s_lbase[256];
+    __shared__ uint32_t s_wcnt[4][RDX];
+    __shared__ uint32_t s_gbase[RDX];
+    __shared__ uint32_t s_lbase[RDX];
     __shared__ uint32_t s_wave[4];
     const SortSeg& sg = b.s[blockIdx.y];
     const size_t nbi = rts_blocks(sg.n, IT);
     const uint32_t bid = blockIdx.x;
     if (bid >= nbi) return;                                          // block-uniform
-    const uint32_t* __restrict__ keys_in = in_b ? sg.keys_b : sg.keys_a;
-    const uint32_t* __restrict__ vals_in = in_b ? sg.vals_b : sg.vals_a;
-    uint32_t* __restrict__ keys_out = in_b ? sg.keys_a : sg.keys_b;
-    uint32_t* __restrict__ vals_out = in_b ? sg.vals_a : sg.vals_b;
+    const PassDesc pd = pass_desc(sg, pass, in_b, shift, nbits_h, last_h);
+    if (!pd.active) return;                                          // segment-uniform
+    const uint32_t* __restrict__ keys_in = keys_of(sg, pd.src);
+    const uint32_t* __restrict__ vals_in = vals_of(sg, pd.src);
+    uint32_t* __restrict__ keys_out = keys_of_w(sg, pd.dst);
+    uint32_t* __restrict__ vals_out = vals_of_w(sg, pd.dst);
     const int drop = sg.kept && pass == 0;
     uint32_t* kept_out = drop ? sg.kept : nullptr;
     const uint32_t* __restrict__ totals = rts_totals(sg, pass);
     const uint32_t* __restrict__ offs = rts_rows(sg, pass, nbi);
-    const SortGather gather = last ? sg.gather : SortGather{nullptr, nullptr, nullptr};
+    const SortGather gather = pd.last ? sg.gather : SortGather{nullptr, nullptr, nullptr};
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int nd = 1 << pd.nbits;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) s_wcnt[w][tid] = 0;
+    for (int w = 0; w < 4; ++w) {
+        s_wcnt[w][tid] = 0;
+        s_wcnt[w][tid + 256] = 0;
+    }
     const size_t n = rts_n(sg.n, sg.kept && pass > 0 ? sg.kept : nullptr);
     __syncthreads();
-    const uint32_t mask = (1u << nbits) - 1u;
+    const uint32_t mask = (uint32_t)nd - 1u;
     const uint64_t lt = lanemask_lt();
     const size_t base = (size_t)bid * (256 * IT) + (size_t)wave * (64 * IT);
     uint32_t key[IT], val[IT], rank[IT];
@@ -459,14 +562,16 @@ __global__ void __launch_bounds__(256) k_rts_scatter(const SortBatch b, int pass
         key[r] = valid ? keys_in[idx] : 0u;
         val[r] = valid ? vals_in[idx] : 0u;
     }
-    // block offsets and digit starts: independent of the ranking, loaded while it runs
-    const uint32_t prefix = offs[(size_t)bid * 256 + tid];
-    const uint32_t hcount = totals[tid];
+    // block offsets and digit starts of this thread's two digits (2 tid, 2 tid + 1): independent of
+    // the ranking, loaded while it runs
+    const int da = 2 * tid, db = 2 * tid + 1;
+    const uint32_t pre_a = da < nd ? offs[(size_t)bid * RDX + da] : 0u, pre_b = db < nd ? offs[(size_t)bid * RDX + db] : 0u;
+    const uint32_t hc_a = da < nd ? totals[da] : 0u, hc_b = db < nd ? totals[db] : 0u;
 #pragma unroll
     for (int r = 0; r < IT; ++r) {
         const bool valid = base + (size_t)r * 64 + lane < n && !(drop && key[r] == 0xFFFFFFFFu);
-        const uint32_t d = (key[r] >> shift) & mask;
-        const uint64_t peers = match_digit(d, valid, nbits);
+        const uint32_t d = ((key[r] - pd.kbase) >> pd.shift) & mask;
+        const uint64_t peers = match_digit(d, valid, pd.nbits);
         const uint32_t before = s_wcnt[wave][d];
         const uint32_t pr = (uint32_t)__popcll(peers & lt);
         rank[r] = before + pr;
@@ -475,16 +580,24 @@ __global__ void __launch_bounds__(256) k_rts_scatter(const SortBatch b, int pass
         __builtin_amdgcn_wave_barrier();
     }
     __syncthreads();
-    const uint32_t c0 = s_wcnt[0][tid], c1 = s_wcnt[1][tid], c2 = s_wcnt[2][tid], c3 = s_wcnt[3][tid];
-    const uint32_t total = c0 + c1 + c2 + c3;
-    s_wcnt[0][tid] = 0; s_wcnt[1][tid] = c0; s_wcnt[2][tid] = c0 + c1; s_wcnt[3][tid] = c0 + c1 + c2;
-    const uint32_t dstart = block_excl_scan256(hcount, s_wave);      // global start of digit tid
-    const uint32_t lbase = block_excl_scan256(total, s_wave);        // local start of digit tid
-    s_lbase[tid] = lbase;
-    s_gbase[tid] = dstart + prefix - lbase;
+    uint32_t tot_a, tot_b;
+    {
+        const uint32_t a0 = s_wcnt[0][da], a1 = s_wcnt[1][da], a2 = s_wcnt[2][da], a3 = s_wcnt[3][da];
+        const uint32_t b0 = s_wcnt[0][db], b1 = s_wcnt[1][db], b2 = s_wcnt[2][db], b3 = s_wcnt[3][db];
+        tot_a = a0 + a1 + a2 + a3;
+        tot_b = b0 + b1 + b2 + b3;
+        s_wcnt[0][da] = 0; s_wcnt[1][da] = a0; s_wcnt[2][da] = a0 + a1; s_wcnt[3][da] = a0 + a1 + a2;
+        s_wcnt[0][db] = 0; s_wcnt[1][db] = b0; s_wcnt[2][db] = b0 + b1; s_wcnt[3][db] = b0 + b1 + b2;
+    }
+    const uint32_t dstart_a = block_excl_scan256(hc_a + hc_b, s_wave);   // global start of digit 2 tid
+    const uint32_t lbase_a = block_excl_scan256(tot_a + tot_b, s_wave);  // local start of digit 2 tid
+    s_lbase[da] = lbase_a;
+    s_lbase[db] = lbase_a + tot_a;
+    s_gbase[da] = dstart_a + pre_a - lbase_a;
+    s_gbase[db] = dstart_a + hc_a + pre_b - (lbase_a + tot_a);
     if (tid == 255) {
-        s_wave[0] = lbase + total;                                    // keys this block places
-        if (kept_out && bid == 0) *kept_out = dstart + hcount;        // keys kept over all blocks
+        s_wave[0] = lbase_a + tot_a + tot_b;                          // keys this block places
+        if (kept_out && bid == 0) *kept_out = dstart_a + hc_a + hc_b;  // keys kept over all blocks
     }
     __syncthreads();
     const int ntile = (int)s_wave[0];
@@ -492,7 +605,7 @@ __global__ void __launch_bounds__(256) k_rts_scatter(const SortBatch b, int pass
     for (int r = 0; r < IT; ++r) {
         const bool valid = base + (size_t)r * 64 + lane < n && !(drop && key[r] == 0xFFFFFFFFu);
         if (valid) {
-            const uint32_t d = (key[r] >> shift) & mask;
+            const uint32_t d = ((key[r] - pd.kbase) >> pd.shift) & mask;
             const uint32_t pos = s_lbase[d] + s_wcnt[wave][d] + rank[r];
             s_key[pos] = key[r];
             s_val[pos] = val[r];
@@ -510,7 +623,7 @@ __global__ void __launch_bounds__(256) k_rts_scatter(const SortBatch b, int pass
             const bool ok = i < ntile;
             const uint32_t k = s_key[ok ? i : 0], v = s_val[ok ? i : 0];
             vv[r] = v;
-            dd[r] = s_gbase[(k >> shift) & mask] + (uint32_t)i;
+            dd[r] = s_gbase[((k - pd.kbase) >> pd.shift) & mask] + (uint32_t)i;
             rc[r] = ok ? gather.rect[v] : make_uint2(0u, 0u);
         }
 #pragma unroll
@@ -523,10 +636,10 @@ __global__ void __launch_bounds__(256) k_rts_scatter(const SortBatch b, int pass
         }
         return;
     }
-    uint2* __restrict__ ranges = last ? sg.ranges : nullptr;
+    uint2* __restrict__ ranges = pd.last ? sg.ranges : nullptr;
     for (int i = tid; i < ntile; i += 256) {
         const uint32_t k = s_key[i];
-        const uint32_t dst = s_gbase[(k >> shift) & mask] + (uint32_t)i;
+        const uint32_t dst = s_gbase[((k - pd.kbase) >> pd.shift) & mask] + (uint32_t)i;
         keys_out[dst] = k;
         vals_out[dst] = s_val[i];
         if (ranges && k < sg.nranges) {
@@ -542,8 +655,8 @@ __global__ void __launch_bounds__(256) k_rts_scatter(const SortBatch b, int pass
 static size_t os_blocks(size_t n) { return (n + OS_TILE - 1) / OS_TILE; }
 
 size_t radix_temp_bytes(size_t n) {
-    // digit totals [4][256] | count rows [4][blocks][256] (blocks of OS_TILE keys: the most rows)
-    return RTS_ROWS_OFF + align_up(4 * os_blocks(n) * 256 * 4, 256);
+    // digit totals [4][RDX] | plan | count rows [4][blocks][RDX] (blocks of OS_TILE keys: the most rows)
+    return RTS_ROWS_OFF + align_up(4 * os_blocks(n) * RDX * 4, 256);
 }
 
 bool radix_sort_batch(const SortSeg* segs, int nseg, int begin_bit, int end_bit, hipStream_t st) {
@@ -553,36 +666,51 @@ bool radix_sort_batch(const SortSeg* segs, int nseg, int begin_bit, int end_bit,
     for (int i = 0; i < nseg; ++i)
         if (segs[i].n > 0) { bt.s[ns++] = segs[i]; nmax = std::max(nmax, segs[i].n); }
     if (ns == 0 || end_bit <= begin_bit) return false;
+    // keys per thread: 8 (2M keys: more, shorter blocks), 12 above 4M keys (the 6M-instance
+    // tile sort: longer digit runs per block); swept 8 / 12 / 16 on both sorts
+    // the device-planned depth sort takes 12 keys per thread: its 9-bit passes' digit runs are half
+    // as long, and longer blocks win them back (depth sort 0.086-0.087 vs 0.088-0.090 ms per view
+    // at 8; LSR_DEPTH_ITEMS=8 for A/B)
+    static const int depth_items = [] {
+        const char* e = std::getenv("LSR_DEPTH_ITEMS");
+        return e && std::atoi(e) == 8 ? OS_ITEMS : 12;
+    }();
+    const int items = nmax > ((size_t)4 << 20) ? 12 : (bt.s[0].vals_c ? depth_items : OS_ITEMS);
+    const unsigned nbi = (unsigned)((nmax + 256 * items - 1) / (256 * items));   // <= os_blocks: rows fit
+    auto pass = [&](int p, int in_b, int shift, int nbits, int last) {
+        if (items == 12)
+            hipLaunchKernelGGL(k_rts_count<12>, dim3(nbi, ns), dim3(256), 0, st, bt, p, in_b, shift, nbits);
+        else
+            hipLaunchKernelGGL(k_rts_count<OS_ITEMS>, dim3(nbi, ns), dim3(256), 0, st, bt, p, in_b, shift, nbits);
+        launch_rts_scan(bt, ns, p, items, in_b, nbits, st);
+        if (items == 12)
+            hipLaunchKernelGGL(k_rts_scatter<12>, dim3(nbi, ns), dim3(256), 0, st, bt, p, in_b, shift, nbits, last);
+        else
+            hipLaunchKernelGGL(k_rts_scatter<OS_ITEMS>, dim3(nbi, ns), dim3(256), 0, st, bt, p, in_b, shift, nbits,
+                               last);
+    };
+    if (bt.s[0].vals_c) {   // the depth sort's device plan (every segment of the batch has one)
+        for (int p = 0; p < 4; ++p) pass(p, 0, 0, 8, 0);
+        return false;       // either plan ends in the (a) buffers
+    }
     bool in_b = false;
     // the bits spread evenly over the passes (13 bits: 7 + 6, not 8 + 5): fewer digits in a pass
     // mean longer runs per digit in its scatter, i.e. fuller write segments
     const int npass = (end_bit - begin_bit + 7) / 8;
-    // keys per thread: 8 (2M keys: more, shorter blocks), 12 above 4M keys (the 6M-instance
-    // tile sort: longer digit runs per block); swept 8 / 12 / 16 on both sorts
-    const int items = nmax > ((size_t)4 << 20) ? 12 : OS_ITEMS;
-    const unsigned nbi = (unsigned)((nmax + 256 * items - 1) / (256 * items));   // <= os_blocks: rows fit
     for (int shift = begin_bit, nbits = 0, p = 0; shift < end_bit; shift += nbits, ++p) {
         nbits = (end_bit - begin_bit) / npass + (p < (end_bit - begin_bit) % npass ? 1 : 0);
-        const int last = shift + nbits >= end_bit;
-        if (items == 12)
-            hipLaunchKernelGGL(k_rts_count<12>, dim3(nbi, ns), dim3(256), 0, st, bt, p, (int)in_b, shift, nbits);
-        else
-            hipLaunchKernelGGL(k_rts_count<OS_ITEMS>, dim3(nbi, ns), dim3(256), 0, st, bt, p, (int)in_b, shift, nbits);
-        launch_rts_scan(bt, ns, p, items, nbits, st);
-        if (items == 12)
-            hipLaunchKernelGGL(k_rts_scatter<12>, dim3(nbi, ns), dim3(256), 0, st, bt, p, (int)in_b, shift, nbits, last);
-        else
-            hipLaunchKernelGGL(k_rts_scatter<OS_ITEMS>, dim3(nbi, ns), dim3(256), 0, st, bt, p, (int)in_b, shift, nbits,
-                               last);
+        pass(p, (int)in_b, shift, nbits, shift + nbits >= end_bit);
         in_b = !in_b;
     }
     return in_b;
 }
 
 bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b, size_t n,
-                      int begin_bit, int end_bit, void* temp, hipStream_t st, uint32_t* kept, const SortGather* gather) {
+                      int begin_bit, int end_bit, void* temp, hipStream_t st, uint32_t* kept, const SortGather* gather,
+                      uint32_t* vals_c) {
     if (n == 0 || end_bit <= begin_bit) return false;
     SortSeg sg{keys_a, vals_a, keys_b, vals_b, temp, kept, gather ? *gather : SortGather{nullptr, nullptr, nullptr}, n};
+    sg.vals_c = (vals_c && kept && gather && begin_bit == 0 && end_bit == 32) ? vals_c : nullptr;
     return radix_sort_batch(&sg, 1, begin_bit, end_bit, st);
 }
 

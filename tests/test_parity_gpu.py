@@ -53,6 +53,24 @@ def test_forward_matches_oracle(C):
     _assert_forward(nat, ref, C)
 
 
+@pytest.mark.parametrize("far", [False, True])
+def test_depth_sort_plans(far):
+    """The depth sort's pass plan, made on the device from the kept keys' range (sort.hip): depths
+    2-10 span under 2^26 key units above the minimum's 256-aligned base (low 8 bits, then two 9-bit
+    passes); every 7th Gaussian moved 60x further along its ray (depths up to ~600, a ratio above
+    256) takes the four 8-bit passes.  Both give upstream's per-tile order
+    (check_binning_against_upstream) and the oracle's images."""
+    sc, cam = small_case(P=3000, W=128, H=96, C=3, seed=21)
+    if far:
+        sc.means3D[::7] *= 60.0   # origin camera: same projection, 60x the depth
+    nat = run_native(sc, cam)
+    ref = run_oracle(sc, cam)
+    z = sc.means3D[:, 2].cpu().numpy()
+    vis = ref.radii > 0
+    assert (z[vis].max() / z[vis].min() > 256) == far
+    _assert_forward(nat, ref, 3)
+
+
 def test_forward_odd_size_and_big_splats():
     # ragged tiles (W, H not multiples of 16), 10 % large Gaussians, some behind the near plane
     sc, cam = small_case(P=2500, W=131, H=77, C=8, seed=5, big_frac=0.1)
