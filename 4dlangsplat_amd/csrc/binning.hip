@@ -19,15 +19,15 @@ namespace lsr {
 // Each instance also gets the 8x8 quadrants of its tile that the splat may reach (a conservative
 // test, emit_quad_mask) that the compositors' per-quadrant waves used to evaluate while scanning
 // every list entry (quad_may_touch); once per instance here, so their scans read only the point
-// list (no centre / conic gathers).  An instance reaching no quadrant would be
-// skipped at every pixel of its tile: it gets the past-the-end tile key (dropped from the lists).
+// list (no centre / conic gathers).  An instance reaching no quadrant would be skipped at every
+// pixel of its tile: it gets key 0xFFFFFFFF, which the tile sort's first pass drops.
 __global__ void __launch_bounds__(256) k_emit(const EmitBatch eb) {
     __shared__ uint32_t s_off[4][64];
     __shared__ uint2 s_rc[4][64];
     __shared__ uint32_t s_id[4][64];
     __shared__ EmitSplat s_sp[4][64];
     const EmitView& ev = eb.v[blockIdx.y];   // one view of the batch per grid row
-    const int P = eb.P, gx = eb.grid_x, gy = eb.grid_y, W = eb.W, H = eb.H;
+    const int P = eb.P, gx = eb.grid_x, W = eb.W, H = eb.H;
     const uint32_t* __restrict__ order = ev.order;
     const uint32_t* __restrict__ offsets = ev.offsets;
     const uint32_t* __restrict__ counts = ev.counts;
@@ -58,7 +58,6 @@ __global__ void __launch_bounds__(256) k_emit(const EmitBatch eb) {
     const bool big = ok && cnt > 0 && (ox1 - ox0 > 2 || oy1 - oy0 > 2);
     if (big) s_sp[w][lane] = emit_splat(xy[id], conic_o[id]);
     __builtin_amdgcn_wave_barrier();
-    const uint32_t ntiles = (uint32_t)(gx * gy);
     for (uint32_t j = start + lane; j < end; j += 64) {
         int k = 0;                                           // last rank with s_off <= j
 #pragma unroll
@@ -85,7 +84,7 @@ __global__ void __launch_bounds__(256) k_emit(const EmitBatch eb) {
             quads = emit_quad_mask(s_sp[w][k], (int)(x0 + dx) * LSR_TILE_X, (int)(y0 + dy) * LSR_TILE_Y, W, H);
         }
         const uint32_t tx = x0 + dx, ty = y0 + dy;
-        keys[j] = quads ? ty * (uint32_t)gx + tx : ntiles;
+        keys[j] = quads ? ty * (uint32_t)gx + tx : 0xFFFFFFFFu;   // dropped by the tile sort's first pass
         vals[j] = s_id[w][k] | (quads << PL_QUAD_SHIFT);
     }
 }

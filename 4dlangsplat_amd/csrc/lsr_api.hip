@@ -141,6 +141,7 @@ Geom carve_geom(void* base, size_t P, size_t* bytes) {
 struct Binning {
     uint32_t *key_a, *key_b, *val_a, *val_b;
     void* sort_tmp;
+    uint32_t* kept;   // the tile sort's listed-instance count (its first pass drops the unlisted)
 };
 Binning carve_binning(void* base, size_t K, size_t* bytes) {
     Carver c(base);
@@ -150,6 +151,7 @@ Binning carve_binning(void* base, size_t K, size_t* bytes) {
     b.val_a = c.take<uint32_t>(K);
     b.val_b = c.take<uint32_t>(K);
     b.sort_tmp = c.take<char>(lsr::radix_temp_bytes(K));
+    b.kept = c.take<uint32_t>(4);
     if (bytes) *bytes = c.off;
     return b;
 }
@@ -477,7 +479,9 @@ int lsr_forward_binning_views(int32_t n_views, const lsr_settings* const* s, con
             e.clear.even[0] = 0xFFFFFFFFu;
             e.clear.p[1] = m.tile_max;
             e.clear.n[1] = (uint32_t)ntiles;
-            ss[ne++] = lsr::SortSeg{b.key_a, b.val_a, b.key_b, b.val_b, b.sort_tmp, nullptr,
+            // kept: the first pass drops the instances that reach no quadrant (key 0xFFFFFFFF, about
+            // 10 % of them on the headline scene), the second sorts only the listed ones
+            ss[ne++] = lsr::SortSeg{b.key_a, b.val_a, b.key_b, b.val_b, b.sort_tmp, b.kept,
                                     lsr::SortGather{nullptr, nullptr, nullptr}, K, m.ranges, (uint32_t)ntiles};
         }
         if (ne == 0) continue;

@@ -445,7 +445,7 @@ bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint
 // binning (binning.hip)
 // Point-list values: Gaussian id in the low 28 bits, in the top 4 the quadrants (bit 28 + q,
 // q = (y >= 8) * 2 + (x >= 8) inside the 16x16 tile) the splat may reach (quad_may_touch); an
-// instance reaching none gets tile key ntiles and sorts past every list.
+// instance reaching none gets key 0xFFFFFFFF, dropped by the tile sort's first pass.
 constexpr uint32_t PL_ID_MASK = 0x0FFFFFFFu;
 constexpr int PL_QUAD_SHIFT = 28;
 // Instance emission of nv <= LSR_MAX_VIEWS views (one grid row per view; same P and tile grid).

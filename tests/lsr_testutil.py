@@ -58,7 +58,7 @@ def decode_point_list(state):
     W, H = state.settings.c.image_width, state.settings.c.image_height
     nt = ((W + 15) // 16) * ((H + 15) // 16)
     bits = 1
-    while (1 << bits) <= nt:        # tile keys 0..nt (nt: instances reaching no quadrant)
+    while (1 << bits) <= nt:        # tile keys 0..nt-1 (instances reaching no quadrant are dropped)
         bits += 1
     in_b = ((bits + 7) // 8) % 2 == 1
     raw = state.binning.cpu().numpy()

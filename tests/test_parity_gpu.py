@@ -335,8 +335,9 @@ def test_batched_forward_equals_per_view(precomp):
         assert a[4].num_rendered == b[4].num_rendered, v
         for x, y in zip(a[:4], b[:4]):
             assert torch.equal(x, y), v
-        if a[4].num_rendered:
-            assert np.array_equal(decode_point_list(a[4]), decode_point_list(b[4])), v
+        if a[4].num_rendered:   # the listed entries (the unlisted are dropped by the tile sort)
+            n = int(decode_img(a[4])[0][:, 1].max())
+            assert np.array_equal(decode_point_list(a[4])[:n], decode_point_list(b[4])[:n]), v
         for x, y in zip(decode_img(a[4]), decode_img(b[4])):
             assert np.array_equal(x, y), v
     g = torch.Generator(device="cpu").manual_seed(4)
@@ -404,7 +405,7 @@ def test_headline_properties_2m():
     assert 1_500_000 < vis.sum() < 1_950_000
     K = st.num_rendered
     assert 4_000_000 < K < 12_000_000        # after dropping instances that cannot contribute
-    # ranges tile the list in order; the instances reaching no quadrant of their tile sort past all
+    # ranges tile the list in order; the instances reaching no quadrant of their tile are dropped
     nz = ranges[:, 1] > ranges[:, 0]
     listed = int(ranges[nz, 1].sum() - ranges[nz, 0].sum())
     assert 0.5 * K < listed <= K and int(ranges[nz, 1].max()) == listed
