@@ -469,6 +469,13 @@ class _DeformFunction(torch.autograd.Function):
     def backward(ctx, dm, ds, dr, do, dsh, dl, dc):
         means3D, rotations, lang = ctx.saved_tensors
         f = ctx.field
+        if torch.are_deterministic_algorithms_enabled():
+            # the plane gradients are float-atomic scatters: no fixed-order variant
+            if not torch.is_deterministic_algorithms_warn_only_enabled():
+                raise RuntimeError("lsr_deform_backward does not have a deterministic implementation "
+                                   "(torch.use_deterministic_algorithms(True, warn_only=True) to run it anyway)")
+            import warnings
+            warnings.warn("lsr_deform_backward does not have a deterministic implementation")
         grads = f.backward(means3D, ctx.time, dm, ds, dr, do, dsh, rotations=rotations, lang=lang, d_lang=dl,
                            d_coff=dc if (f.discrete and dc is not None and dc.numel() > 0) else None,
                            no_dlang=ctx.no_dlang)

@@ -866,7 +866,10 @@ class _RasterizeGaussians(torch.autograd.Function):
         ng = ctx.needs_input_grad
         need = dict(means3D=ng[0], means2D=ng[1], sh=ng[2], colors=True, language_feature=ng[4], opacities=ng[5],
                     scales=ng[6], rotations=ng[7], cov3D=ng[8])
-        g = backward_native(st, grad_color, grad_lang if ctx.include_feature else None, grad_depth, need=need)
+        # torch.use_deterministic_algorithms(True) selects the fixed-order reduction (bitwise
+        # reproducible gradients, lsr_backward's deterministic mode) instead of float atomics
+        g = backward_native(st, grad_color, grad_lang if ctx.include_feature else None, grad_depth, need=need,
+                            deterministic=torch.are_deterministic_algorithms_enabled())
         shp = ctx.shapes
 
         def like(t, shape):

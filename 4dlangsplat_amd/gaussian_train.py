@@ -274,6 +274,56 @@ class GaussianTrainer:
     def state_rows(self) -> Iterable[str]:
         return tuple(self.params)
 
+    # ---- checkpoint state (capture / restore, scene/gaussian_model.py:71-154) ------------------
+    def adam_entry(self, n: str) -> Optional[dict]:
+        """torch.optim.Adam's per-parameter state for group n ({"step", "exp_avg", "exp_avg_sq"}),
+        None before its first step (torch creates the state lazily)."""
+        if self.steps.get(n, 0) == 0:
+            return None
+        return {"step": torch.tensor(float(self.steps[n])), "exp_avg": self.exp_avg[n].detach().clone(),
+                "exp_avg_sq": self.exp_avg_sq[n].detach().clone()}
+
+    def load_adam_entry(self, n: str, entry: Optional[dict]) -> None:
+        p = self.params[n]
+        if entry is None:
+            self.exp_avg[n], self.exp_avg_sq[n], self.steps[n] = torch.zeros_like(p), torch.zeros_like(p), 0
+            return
+        for k in ("exp_avg", "exp_avg_sq"):
+            if tuple(entry[k].shape) != tuple(p.shape):
+                raise ValueError(f"{n}: optimizer {k} of shape {tuple(entry[k].shape)}, parameter {tuple(p.shape)}")
+        self.exp_avg[n] = entry["exp_avg"].to(self.device, torch.float32).contiguous().clone()
+        self.exp_avg_sq[n] = entry["exp_avg_sq"].to(self.device, torch.float32).contiguous().clone()
+        self.steps[n] = int(float(entry["step"]))
+
+    @torch.no_grad()
+    def load_rows(self, params: Dict[str, torch.Tensor], max_radii2D: torch.Tensor, xyz_gradient_accum: torch.Tensor,
+                  denom: torch.Tensor, deformation_table: Optional[torch.Tensor] = None) -> None:
+        """Installs restored per-Gaussian tensors (the row count may differ from the current one):
+        parameters, densification statistics, deformation table; moments are reset (load_adam_entry
+        sets them).  The statistics the reference does not checkpoint (_deformation_accum) start at
+        zero, as its training_setup makes them (gaussian_model.py:224)."""
+        P = None
+        for n, t in params.items():
+            if n not in GROUPS:
+                raise ValueError(f"unknown parameter group {n}")
+            t = t.detach().to(self.device, torch.float32).contiguous().clone()
+            if P is not None and t.shape[0] != P:
+                raise ValueError(f"{n}: {t.shape[0]} rows, expected {P}")
+            P = t.shape[0]
+            self.params[n] = t.requires_grad_(True)
+            self.exp_avg[n], self.exp_avg_sq[n], self.steps[n] = torch.zeros_like(t), torch.zeros_like(t), 0
+        for n in list(self.params):
+            if n not in params:
+                raise ValueError(f"the checkpoint has no {n} group")
+        dev = self.device
+        self.max_radii2D = max_radii2D.detach().to(dev, torch.float32).reshape(P).contiguous().clone()
+        self.xyz_gradient_accum = xyz_gradient_accum.detach().to(dev, torch.float32).reshape(P, 1).contiguous().clone()
+        self.denom = denom.detach().to(dev, torch.float32).reshape(P, 1).contiguous().clone()
+        self._deformation_accum = torch.zeros((P, 3), device=dev)
+        self._deformation_table = (deformation_table.detach().to(dev, torch.bool).reshape(P).contiguous().clone()
+                                   if deformation_table is not None and deformation_table.numel() == P
+                                   else torch.ones(P, dtype=torch.bool, device=dev))
+
 
 class TensorAdam:
     """torch.optim.Adam over named tensors whose gradients arrive in a separate dict (the
@@ -288,6 +338,26 @@ class TensorAdam:
         self.exp_avg = {n: torch.zeros_like(t) for n, t in params.items()}
         self.exp_avg_sq = {n: torch.zeros_like(t) for n, t in params.items()}
         self.steps = {n: 0 for n in params}
+
+    def adam_entry(self, n: str) -> Optional[dict]:
+        """torch.optim.Adam's state for tensor n, None before its first step."""
+        if self.steps.get(n, 0) == 0:
+            return None
+        return {"step": torch.tensor(float(self.steps[n])), "exp_avg": self.exp_avg[n].detach().clone(),
+                "exp_avg_sq": self.exp_avg_sq[n].detach().clone()}
+
+    def load_adam_entry(self, n: str, entry: Optional[dict]) -> None:
+        p = self.params[n]
+        if entry is None:
+            self.exp_avg[n].zero_()
+            self.exp_avg_sq[n].zero_()
+            self.steps[n] = 0
+            return
+        for k, dst in (("exp_avg", self.exp_avg[n]), ("exp_avg_sq", self.exp_avg_sq[n])):
+            if tuple(entry[k].shape) != tuple(p.shape):
+                raise ValueError(f"{n}: optimizer {k} of shape {tuple(entry[k].shape)}, parameter {tuple(p.shape)}")
+            dst.copy_(entry[k])
+        self.steps[n] = int(float(entry["step"]))
 
     def step(self, grads: Dict[str, torch.Tensor]):
         groups = []

@@ -124,6 +124,7 @@ class TrainStep:
         self.sh_degree = sh_degree
         self.bg = bg if bg is not None else torch.ones(3, device=trainer.device)
         self.field_opt = None
+        self.spatial_lr_scale = 0.0
         if field is not None:
             # the box trains too (gaussian_model.py:250-253,258,291: "grid.aabb" is among
             # get_grid_parameters and has requires_grad once the whole module does)
@@ -140,6 +141,7 @@ class TrainStep:
         spatial_lr_scale (the scene's cameras_extent); applied at the start of every iteration as
         train.py:233 calls gaussians.update_learning_rate(iteration)."""
         s = spatial_lr_scale
+        self.spatial_lr_scale = float(s)
         self.trainer.set_xyz_schedule(position_lr_init * s, position_lr_final * s, position_lr_delay_mult,
                                       position_lr_max_steps)
         self._deform_sched = get_expon_lr_func(deformation_lr_init * s, deformation_lr_final * s,
@@ -247,3 +249,163 @@ class TrainStep:
                 self.field_opt.step(grads)
                 self.field.prepare()
         return loss.detach()
+
+    # ---- checkpoints (scene/gaussian_model.py:71-154, train.py:104-109,424-426,579) ---------------
+    def _group_layout(self):
+        """[(group name, [(owner, key, reference parameter name)])] in training_setup's order
+        (gaussian_model.py:273-288 base stages; :236-255 lang stages with joint_train)."""
+        tr, f = self.trainer, self.field
+        gauss = lambda n: [("g", n, "_" + n if n not in ("f_dc", "f_rest") else "_features_" + n[2:])]  # noqa: E731
+        mlp = [("f", k, "deformation_net." + k) for k in (f.p if f is not None else ()) if "grid" not in k]
+        grid = [("f", k, "deformation_net." + k) for k in (f.p if f is not None else ()) if "grid" in k]
+        if self.lang_stage and not self.joint_train:
+            order = ["deformation", "grid", "language_feature"]
+        else:
+            order = ["xyz", "deformation", "grid", "f_dc", "f_rest", "opacity", "scaling", "rotation",
+                     "language_feature"]
+        out = []
+        for name in order:
+            if name == "deformation":
+                if mlp:
+                    out.append((name, mlp))
+            elif name == "grid":
+                if grid:
+                    out.append((name, grid))
+            elif name in tr.params:
+                out.append((name, gauss(name)))
+        return out
+
+    def optimizer_state_dict(self) -> dict:
+        """The Gaussians' and the field's Adam state in torch.optim.Adam.state_dict()'s layout (one
+        optimizer over training_setup's groups, parameters numbered in group order, state only for
+        parameters that have stepped), with each group's reference parameter names (param_names)."""
+        tr, fo = self.trainer, self.field_opt
+        state, groups, i = {}, [], 0
+        for name, members in self._group_layout():
+            ids, names = [], []
+            for owner, key, ref in members:
+                e = tr.adam_entry(key) if owner == "g" else (fo.adam_entry(key) if fo is not None else None)
+                if e is not None:
+                    state[i] = e
+                ids.append(i)
+                names.append(ref)
+                i += 1
+            owner, key, _ = members[0]
+            lr = tr.lrs.get(key, 0.0) if owner == "g" else (fo.lr.get(key, 0.0) if fo is not None else 0.0)
+            groups.append({"params": ids, "lr": float(lr), "name": name, "betas": tuple(tr.betas), "eps": tr.eps,
+                           "weight_decay": 0, "amsgrad": False, "maximize": False, "foreach": None,
+                           "capturable": False, "differentiable": False, "fused": None, "param_names": names})
+        return {"state": state, "param_groups": groups}
+
+    def load_optimizer_state_dict(self, opt: dict) -> None:
+        """Inverse of optimizer_state_dict: by param_names when the groups carry them, else by the
+        group order of training_setup."""
+        tr, fo = self.trainer, self.field_opt
+        ref_to_key = {}
+        for _, members in self._group_layout():
+            for owner, key, ref in members:
+                ref_to_key[ref] = (owner, key)
+        layout = [m for _, ms in self._group_layout() for m in ms]
+        seen = set()
+        for gi, g in enumerate(opt["param_groups"]):
+            names = g.get("param_names")
+            for j, pid in enumerate(g["params"]):
+                if names is not None:
+                    if names[j] not in ref_to_key:
+                        raise ValueError(f"checkpoint parameter {names[j]} is not in this model")
+                    owner, key = ref_to_key[names[j]]
+                else:
+                    if pid >= len(layout):
+                        raise ValueError("checkpoint optimizer has more parameters than this model")
+                    owner, key, _ = layout[pid]
+                entry = opt["state"].get(pid)
+                if owner == "g":
+                    tr.load_adam_entry(key, entry)
+                    tr.lrs[key] = float(g["lr"])
+                elif fo is not None:
+                    fo.load_adam_entry(key, entry)
+                    fo.lr[key] = float(g["lr"])
+                seen.add((owner, key))
+        for owner, key, ref in layout:
+            if (owner, key) not in seen:
+                raise ValueError(f"the checkpoint's optimizer has no state for {ref}")
+
+    def capture(self, include_feature: Optional[bool] = None) -> tuple:
+        """GaussianModel.capture (gaussian_model.py:71-105): (active_sh_degree, _xyz, the field's
+        state_dict, _deformation_table, _features_dc, _features_rest, _scaling, _rotation, _opacity,
+        [_language_feature,] max_radii2D, xyz_gradient_accum, denom, optimizer.state_dict(),
+        spatial_lr_scale); 15 entries with include_feature (default: whether the trainer has a
+        language group), else 14.  Tensors are cloned: training on does not change a capture."""
+        tr = self.trainer
+        if include_feature is None:
+            include_feature = "language_feature" in tr.params
+        if include_feature and "language_feature" not in tr.params:
+            raise ValueError("include_feature needs a language_feature group")
+        c = lambda t: t.detach().clone()  # noqa: E731
+        head = (self.sh_degree, c(tr["xyz"]), self.field.state_dict() if self.field is not None else {},
+                c(tr._deformation_table), c(tr["f_dc"]), c(tr["f_rest"]), c(tr["scaling"]), c(tr["rotation"]),
+                c(tr["opacity"]))
+        lang = (c(tr["language_feature"]),) if include_feature else ()
+        return head + lang + (c(tr.max_radii2D), c(tr.xyz_gradient_accum), c(tr.denom), self.optimizer_state_dict(),
+                              float(self.spatial_lr_scale))
+
+    def restore(self, model_args: tuple, fresh_optimizer: bool = False) -> None:
+        """GaussianModel.restore (gaussian_model.py:107-154) of a capture(): parameters, field,
+        deformation table, statistics and the optimizer state.  The reference re-runs training_setup
+        after loading, which builds a fresh Adam (its moments and step counts are not resumed);
+        fresh_optimizer=True does the same, the default resumes them (training N iterations equals
+        training k, capture, restore, N - k more)."""
+        if len(model_args) == 15:
+            (sh, xyz, deform, table, f_dc, f_rest, scaling, rotation, opacity, lang, max_r, accum, denom, opt,
+             slr) = model_args
+        elif len(model_args) == 14:
+            (sh, xyz, deform, table, f_dc, f_rest, scaling, rotation, opacity, max_r, accum, denom, opt,
+             slr) = model_args
+            lang = None
+        else:
+            raise ValueError(f"a capture has 14 or 15 entries, got {len(model_args)}")
+        tr = self.trainer
+        params = dict(xyz=xyz, f_dc=f_dc, f_rest=f_rest, opacity=opacity, scaling=scaling, rotation=rotation)
+        if lang is not None:
+            params["language_feature"] = lang
+        elif "language_feature" in tr.params:
+            raise ValueError("this trainer has a language group; the capture has none (include_feature off)")
+        tr.load_rows(params, max_r, accum, denom, table)
+        self.sh_degree = int(sh)
+        self.spatial_lr_scale = float(slr)
+        if self.field is not None:
+            pre = "deformation_net."
+            sd = {k[len(pre):]: v for k, v in deform.items() if k.startswith(pre)}
+            missing = sorted(set(self.field.p) - set(sd))
+            if missing:
+                raise ValueError(f"the capture's field lacks {missing}")
+            with torch.no_grad():
+                for k, t in self.field.p.items():
+                    if tuple(sd[k].shape) != tuple(t.shape):
+                        raise ValueError(f"{k}: shape {tuple(sd[k].shape)} vs {tuple(t.shape)}")
+                    t.copy_(sd[k])
+            self.field.prepare()
+        if fresh_optimizer:
+            for n in tr.params:
+                tr.load_adam_entry(n, None)
+            if self.field_opt is not None:
+                for n in self.field_opt.params:
+                    self.field_opt.load_adam_entry(n, None)
+        else:
+            self.load_optimizer_state_dict(opt)
+
+    def save_checkpoint(self, model_path: str, iteration: int, include_feature: Optional[bool] = None) -> str:
+        """train.py:424-426: torch.save((capture(include_feature), iteration)) as
+        <model_path>/chkpnt_<stage>_<iteration>.pth.  Everything in it loads with weights_only=True."""
+        import os
+        path = os.path.join(model_path, f"chkpnt_{self.stage}_{iteration}.pth")
+        torch.save((self.capture(include_feature), int(iteration)), path)
+        return path
+
+    def load_checkpoint(self, path: str, fresh_optimizer: bool = False) -> int:
+        """train.py:104-109 (--start_checkpoint): restore a save_checkpoint file; returns its
+        iteration (the loop's first_iter), which also becomes self.iteration."""
+        model_args, first_iter = torch.load(path, map_location=self.trainer.device, weights_only=True)
+        self.restore(model_args, fresh_optimizer=fresh_optimizer)
+        self.iteration = int(first_iter)
+        return self.iteration

@@ -511,10 +511,16 @@ class ShardedAdam:
         they are re-bound to row-padded storage.  raw: the full raw parameters (xyz, f_dc, f_rest,
         opacity, scaling, rotation, language_feature), of which this rank keeps its shard.
         adam(p, g, m, v, lr, step): in place on one group's shard (default: lsr_adam_step)."""
+        if getattr(scene, "deformation", None) is not None:
+            # the bucket's means3D gradient is the xyz gradient and the gathered rows are the
+            # rasterizer's inputs only without a field between the parameters and the rasterizer
+            raise ValueError("ShardedAdam steps the rasterizer inputs directly: a scene with a deformation "
+                             "field needs the field's backward between the bucket and the parameters")
         self.distributed = dist.is_available() and dist.is_initialized()
         self.group = group
         self.world = dist.get_world_size(group) if self.distributed else 1
         self.rank = dist.get_rank(group) if self.distributed else 0
+        self.xyz_scheduler_args = None
         self.P = P = scene.means3D.shape[0]
         self.Pa = self.row_multiple(P, self.world, align) if P > 0 else 0
         self.rows = self.Pa // self.world
@@ -537,6 +543,19 @@ class ShardedAdam:
         self.exp_avg = {n: torch.zeros_like(t) for n, t in self.raw.items()}
         self.exp_avg_sq = {n: torch.zeros_like(t) for n, t in self.raw.items()}
         self.steps = {n: 0 for n in self.raw}
+
+    # ---- learning rate (gaussian_model.py:302-329; GaussianTrainer's schedule) ----------------------
+    def set_xyz_schedule(self, lr_init, lr_final, lr_delay_mult=0.01, max_steps=30000):
+        from gaussian_train import get_expon_lr_func
+        self.xyz_scheduler_args = get_expon_lr_func(lr_init=lr_init, lr_final=lr_final, lr_delay_mult=lr_delay_mult,
+                                                    max_steps=max_steps)
+
+    def update_learning_rate(self, iteration):
+        """train.py:233 calls gaussians.update_learning_rate(iteration) at every iteration: the xyz
+        group follows its exponential schedule (every rank computes the same value)."""
+        if self.xyz_scheduler_args is not None and "xyz" in self.lrs:
+            self.lrs["xyz"] = float(self.xyz_scheduler_args(iteration))
+        return self.lrs.get("xyz")
 
     # ---- 1. reduce-scatter ------------------------------------------------------------------------
     def _shard_grads(self, bucket) -> Dict[str, torch.Tensor]:

@@ -17,7 +17,8 @@ roofline: the dominant kernel (largest event-timed phase of one untimed all-phas
 algorithmic bytes per launch (the per-phase formulas below) / its mean launch time
 (hipEvents on the launch stream, recorded live over the timed region; only that phase carries
 events there, the per-phase breakdown comes from the untimed step).
-cpu_baseline: the C oracle (oracle/, OpenMP) on one headline frame fwd+bwd, rank 0 only.
+cpu_baseline: the C oracle (oracle/, OpenMP) on 3 headline frames fwd+bwd, rank 0 only; its
+configs0 entry: the oracle on BASELINE configs[0] at full size (50k, 400x400, RGB only).
 """
 import argparse
 import json
@@ -96,6 +97,65 @@ def cpu_baseline(scene, cams, C, threads):
     return tf + tb, tf, tb
 
 
+def configs0_leg(threads, dev, reps=20):
+    """BASELINE configs[0] at full size: 50k random Gaussians, one 400x400 camera,
+    RGB only (include_feature=False, a zeros language tensor as gaussian_renderer/__init__.py:96-99
+    passes), fwd + full bwd.  The C oracle on the host cores, and the same frame through liblsr.so on
+    the GPU for reference (device-resident inputs, per-call workspaces, as forward_native /
+    backward_native allocate them).  Returns (cpu dict, gpu frames/s)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    import synthetic
+    import diff_gaussian_rasterization as dgr
+    W = H = 400
+    sc = synthetic.make_scene(50_000, C=3, tanfovx=0.6, tanfovy=0.6, seed=0)
+    sc.lang = torch.zeros_like(sc.lang)
+    cam = synthetic.origin_camera(W, H, tanfovx=0.6, tanfovy=0.6)
+    s = oracle.OracleSettings(H, W, cam.tanfovx, cam.tanfovy, np.ones(3, np.float32), 1.0,
+                              cam.world_view_transform.numpy(), cam.full_proj_transform.numpy(), 3,
+                              cam.camera_center.numpy(), False)
+    gc = (np.random.default_rng(7).normal(size=(3, H, W)) * 1e-3).astype(np.float32)
+    args = dict(shs=sc.shs.numpy(), lang=sc.lang.numpy(), scales=sc.scales.numpy(), rotations=sc.rotations.numpy(),
+                nthreads=threads)
+    tf = tb = 0.0
+    n = 0
+    t_start = time.perf_counter()
+    while n < reps or time.perf_counter() - t_start < 2.0:
+        t0 = time.perf_counter()
+        r = oracle.forward(s, sc.means3D.numpy(), sc.opacities.numpy(), **args)
+        t1 = time.perf_counter()
+        r.backward(gc, None, None, nthreads=threads)
+        t2 = time.perf_counter()
+        r.close()
+        tf += t1 - t0
+        tb += t2 - t1
+        n += 1
+        if n >= 200:
+            break
+    cpu = dict(value=round(n / (tf + tb), 3), unit="frames/s", cores=threads, kind="port",
+               sample=f"BASELINE configs[0]: 50k Gaussians, 400x400, 3-ch RGB, include_feature=False, {n} frames "
+                      f"fwd {tf / n * 1e3:.1f} ms + bwd {tb / n * 1e3:.1f} ms per frame, C oracle, OpenMP {threads} threads")
+    gs = sc.to(dev)
+    rs = dgr.GaussianRasterizationSettings(H, W, cam.tanfovx, cam.tanfovy, torch.ones(3, device=dev), 1.0,
+                                           cam.world_view_transform.to(dev), cam.full_proj_transform.to(dev), 3,
+                                           cam.camera_center.to(dev), False, False, False)
+    gcd = torch.tensor(gc, device=dev)
+
+    def frame():
+        *_, st = dgr.forward_native(rs, gs.means3D, gs.opacities, shs=gs.shs, language_feature=gs.lang,
+                                    scales=gs.scales, rotations=gs.rotations)
+        dgr.backward_native(st, gcd, None, None)
+
+    for _ in range(3):
+        frame()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(50):
+        frame()
+    torch.cuda.synchronize(dev)
+    return cpu, round(50 / (time.perf_counter() - t0), 1)
+
+
 def host_cpu():
     """Host cores the CPU baseline may use (the process's affinity, capped by a cgroup CPU quota)
     and the host's description: os.cpu_count(), lscpu model, threads per core."""
@@ -134,6 +194,8 @@ def parse_args(argv=None):
                     help="oracle threads (0 = every core available to the process)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=3, help="headline frames timed on the CPU oracle")
+    ap.add_argument("--no-configs0", action="store_true",
+                    help="skip cpu_baseline.configs0 (BASELINE configs[0]: 50k, 400x400, RGB only, on the oracle)")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-densify-stats", action="store_true",
                     help="diagnostic: no means2D gradient / radii MAX in the step (train.py:350-352 needs them)")
@@ -411,6 +473,9 @@ def run(args):
                        sample=f"{nf} headline frames (P={P}, {W}x{H}, C={C}, the first cameras of the batch) "
                               f"fwd {tf:.2f}s + bwd {tb:.2f}s, C oracle oracle/lsr_oracle.c, OpenMP {threads} threads",
                        host=host)
+            if not args.no_configs0:
+                cpu["configs0"], gpu0 = configs0_leg(threads, dev)
+                cpu["configs0"]["gpu_frames_per_s"] = gpu0
         line = dict(
             metric="rasterizer fwd+bwd frames/sec @ 2M Gaussians, 1352x1014, 32-ch features",
             value=round(value, 3), unit="frames/s", n_gpus=world, ranks=pg_ranks, steps=args.steps, warmup=args.warmup,

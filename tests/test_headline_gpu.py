@@ -4,8 +4,9 @@ bench.py times native_view_renderer(overlap="batched", early_views=3) over a Gra
 densification statistics on: one preprocess launch for the step's views, segmented depth / tile
 sorts, the later views binned on a side stream, compositors on the pre-split bf16 language
 operands, the compositor backward per view, then one batched preprocess backward (the flush).
-This runs exactly that on the headline workload (S2M, P = 2M, 1352 x 1014, C = 32; 4 views, so the
-fourth is side-binned), twice (the images must repeat bit for bit), and holds every output to the
+This runs exactly that on the headline workload (S2M, P = 2M, 1352 x 1014, C = 32; the bench's 8
+views per step: the 8-view preprocess launch, the 3 early views binned and composited as one batch and
+the other 5 binned on the side stream and composited as the second), twice (the images must repeat bit for bit), and holds every output to the
 oracle: radii exactly, RGB within 1e-4,
 language within 1e-3, every gradient field of the bucket (means3D, scales, rotations, opacities,
 SH, language, means2D) within 1e-4 of the largest magnitude of the oracle's per-view sum.
@@ -33,7 +34,7 @@ FIELDS = (("means3D", "means3D"), ("scales", "scales"), ("rotations", "rotations
 
 
 def test_bench_pipeline_matches_oracle_at_headline_size():
-    P, W, H, C, V = 2_000_000, 1352, 1014, 32, 4
+    P, W, H, C, V = 2_000_000, 1352, 1014, 32, 8
     tanfovx = 0.6
     scene_cpu = synthetic.make_scene(P, C=C, tanfovx=tanfovx, tanfovy=tanfovx * H / W)   # bench.py's scene
     scene = scene_cpu.to("cuda")

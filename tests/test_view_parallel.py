@@ -412,3 +412,21 @@ def test_sharded_step_two_ranks_equals_serial():
         assert torch.equal(outs[0]["act"][k], outs[1]["act"][k]), k      # every rank renders the same scene
         assert torch.allclose(outs[0]["act"][k], v, rtol=1e-5, atol=1e-6), k
     assert torch.equal(outs[0]["radii"], ser["radii"])
+
+
+def test_sharded_adam_schedule_and_field_guard():
+    """ShardedAdam follows GaussianTrainer's xyz schedule (gaussian_model.py:315-329) and refuses a
+    scene with a deformation field (its bucket's means3D gradient is not the xyz gradient there)."""
+    from gaussian_train import get_expon_lr_func
+    from view_parallel import ShardedAdam
+    sc, raw = _raw_scene()
+    up = ShardedAdam(sc, raw, LRS_SH, adam=_np_adam)
+    assert up.update_learning_rate(100) == LRS_SH["xyz"]          # no schedule: the constant lr
+    up.set_xyz_schedule(1.6e-4 * 5, 1.6e-6 * 5, 0.01, 20_000)
+    ref = get_expon_lr_func(1.6e-4 * 5, 1.6e-6 * 5, lr_delay_mult=0.01, max_steps=20_000)
+    for it in (0, 1, 500, 19_999, 40_000):
+        assert up.update_learning_rate(it) == float(ref(it)) and up.lrs["xyz"] == float(ref(it))
+    sc2, raw2 = _raw_scene()
+    sc2.deformation = object()
+    with pytest.raises(ValueError, match="deformation field"):
+        ShardedAdam(sc2, raw2, LRS_SH, adam=_np_adam)
