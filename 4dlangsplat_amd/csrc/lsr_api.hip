@@ -342,28 +342,25 @@ int lsr_forward_preprocess_async(const lsr_settings* s, const lsr_fwd_in* in, ls
     return LSR_OK;
 }
 
-int lsr_forward_preprocess_views_async(int32_t n_views, const lsr_settings* const* s, const lsr_fwd_in* in,
-                                       lsr_fwd_out* const* out, void* const* geom, uint32_t* host_counts,
-                                       lsr_stream_t stream) {
-    if (n_views < 1 || !s || !out || !geom || !host_counts)
-        return fail(LSR_EINVAL, "n_views >= 1 and the per-view arrays and host_counts are required");
+namespace {
+int check_views(int32_t n_views, const lsr_settings* const* s, const lsr_fwd_in* in, void* const* geom) {
+    if (n_views < 1 || !s || !geom) return fail(LSR_EINVAL, "n_views >= 1 and the per-view arrays are required");
     for (int v = 0; v < n_views; ++v) {
         int rc = check_common(s[v], in);
         if (rc) return rc;
-        if (!out[v] || (!out[v]->radii && in->P > 0)) return fail(LSR_EINVAL, "radii output is required");
         if (!geom[v]) return fail(LSR_EINVAL, "geom workspaces are required");
         if (s[v]->image_width != s[0]->image_width || s[v]->image_height != s[0]->image_height ||
             s[v]->sh_degree != s[0]->sh_degree || s[v]->scale_modifier != s[0]->scale_modifier)
             return fail(LSR_EINVAL, "batched views must share the image size, sh_degree and scale_modifier");
     }
-    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    return LSR_OK;
+}
+
+// depth order + instance count of n_views preprocessed views (their geom workspaces), one set of
+// launches per 8 views; page-locked host_counts get the counts from the scan itself
+int depth_order_views(int32_t n_views, const lsr_settings* const* s, const lsr_fwd_in* in, void* const* geom,
+                      uint32_t* host_counts, hipStream_t st) {
     const int P = in->P;
-    if (P == 0) {
-        for (int v = 0; v < 2 * n_views; ++v) host_counts[v] = 0;
-        return LSR_OK;
-    }
-    // page-locked host_counts: the instance scan writes the counts into them itself (no copy
-    // launches); pageable memory gets the copies
     uint32_t* mapped = nullptr;
     {
         void* dptr = nullptr;
@@ -372,14 +369,10 @@ int lsr_forward_preprocess_views_async(int32_t n_views, const lsr_settings* cons
     }
     for (int v0 = 0; v0 < n_views; v0 += lsr::LSR_MAX_VIEWS) {
         const int nv = std::min(n_views - v0, lsr::LSR_MAX_VIEWS);
-        lsr::PreprocessArgs a{};
-        preprocess_shared(a, s[v0], in);
-        a.nv = nv;
         lsr::SortSeg ss[lsr::LSR_MAX_VIEWS] = {};
         lsr::ScanSeg sc[lsr::LSR_MAX_VIEWS] = {};
         for (int k = 0; k < nv; ++k) {
             Geom g = carve_geom(geom[v0 + k], (size_t)P, nullptr);
-            preprocess_view(a.v[k], s[v0 + k], g, out[v0 + k]->radii);
             // depth order of the visible Gaussians (the first pass drops culled keys, kept count in
             // g.total[3]; the last pass writes the depth-ranked rectangles and instance counts)
             ss[k] = lsr::SortSeg{g.key_a, g.val_a, g.key_b, g.val_b, g.sort_tmp, g.total + 3,
@@ -391,11 +384,6 @@ int lsr_forward_preprocess_views_async(int32_t n_views, const lsr_settings* cons
                 host_counts[2 * (v0 + k) + 1] = 0;           // device: the host clears it here)
             }
         }
-        {
-            PhaseTimer t(LSR_PHASE_PREPROCESS, st);
-            lsr::launch_preprocess(a, st);
-        }
-        LSR_LAUNCHED("preprocess", st, s[v0]->debug);
         {
             PhaseTimer t(LSR_PHASE_DEPTH_SORT, st);
             if (lsr::radix_sort_batch(ss, nv, 0, 32, st) != (bool)depth_sort_result_in_b())
@@ -416,6 +404,59 @@ int lsr_forward_preprocess_views_async(int32_t n_views, const lsr_settings* cons
         }
     }
     return LSR_OK;
+}
+}  // namespace
+
+int lsr_forward_preprocess_views_split_async(int32_t n_views, int32_t n_ordered, const lsr_settings* const* s,
+                                             const lsr_fwd_in* in, lsr_fwd_out* const* out, void* const* geom,
+                                             uint32_t* host_counts, lsr_stream_t stream) {
+    int rc = check_views(n_views, s, in, geom);
+    if (rc) return rc;
+    if (!out || (n_ordered > 0 && !host_counts) || n_ordered < 0 || n_ordered > n_views)
+        return fail(LSR_EINVAL, "0 <= n_ordered <= n_views, the outputs and host_counts are required");
+    for (int v = 0; v < n_views; ++v)
+        if (!out[v] || (!out[v]->radii && in->P > 0)) return fail(LSR_EINVAL, "radii output is required");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int P = in->P;
+    if (P == 0) {
+        for (int v = 0; v < 2 * n_ordered; ++v) host_counts[v] = 0;
+        return LSR_OK;
+    }
+    for (int v0 = 0; v0 < n_views; v0 += lsr::LSR_MAX_VIEWS) {
+        const int nv = std::min(n_views - v0, lsr::LSR_MAX_VIEWS);
+        lsr::PreprocessArgs a{};
+        preprocess_shared(a, s[v0], in);
+        a.nv = nv;
+        for (int k = 0; k < nv; ++k) {
+            Geom g = carve_geom(geom[v0 + k], (size_t)P, nullptr);
+            preprocess_view(a.v[k], s[v0 + k], g, out[v0 + k]->radii);
+        }
+        {
+            PhaseTimer t(LSR_PHASE_PREPROCESS, st);
+            lsr::launch_preprocess(a, st);
+        }
+        LSR_LAUNCHED("preprocess", st, s[v0]->debug);
+    }
+    return n_ordered > 0 ? depth_order_views(n_ordered, s, in, geom, host_counts, st) : LSR_OK;
+}
+
+int lsr_forward_depth_order_views_async(int32_t n_views, const lsr_settings* const* s, const lsr_fwd_in* in,
+                                        void* const* geom, uint32_t* host_counts, lsr_stream_t stream) {
+    int rc = check_views(n_views, s, in, geom);
+    if (rc) return rc;
+    if (!host_counts) return fail(LSR_EINVAL, "host_counts is required");
+    if (in->P == 0) {
+        for (int v = 0; v < 2 * n_views; ++v) host_counts[v] = 0;
+        return LSR_OK;
+    }
+    return depth_order_views(n_views, s, in, geom, host_counts, reinterpret_cast<hipStream_t>(stream));
+}
+
+int lsr_forward_preprocess_views_async(int32_t n_views, const lsr_settings* const* s, const lsr_fwd_in* in,
+                                       lsr_fwd_out* const* out, void* const* geom, uint32_t* host_counts,
+                                       lsr_stream_t stream) {
+    if (!host_counts) return fail(LSR_EINVAL, "host_counts is required");
+    return lsr_forward_preprocess_views_split_async(n_views, n_views, s, in, out, geom, host_counts, stream);
 }
 
 int lsr_forward_preprocess(const lsr_settings* s, const lsr_fwd_in* in, lsr_fwd_out* out, void* geom,

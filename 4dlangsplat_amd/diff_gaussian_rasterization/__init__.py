@@ -272,7 +272,8 @@ def language_split_native(language_feature, stream=None, out=None):
 
 def preprocess_views_native(raster_settings_list, means3D, opacities, shs=None, colors_precomp=None,
                             language_feature=None, scales=None, rotations=None, cov3D_precomp=None, stream=None,
-                            split_language=True, split_behind_counts=True, split_stream=None):
+                            split_language=True, split_behind_counts=True, split_stream=None, order_first=None,
+                            order_stream=None):
     """Forward phase 1 of several views of the same Gaussians as one batch
     (lsr_forward_preprocess_views_async: one preprocess launch per 8 views reads each Gaussian once,
     the views' depth sorts and instance scans share their launches) on `stream`.  No host
@@ -284,7 +285,13 @@ def preprocess_views_native(raster_settings_list, means3D, opacities, shs=None, 
     bits, same results).  split_behind_counts: enqueue that split behind the batch's count event, so
     it runs while the host waits for the counts (False: ahead of the preprocess; an A/B switch).
     split_stream: enqueue the split there instead (after that stream waits for `stream`); the caller
-    orders the compositors after it."""
+    orders the compositors after it.
+
+    order_first = k < n with order_stream: only the first k views are depth-ordered and counted on
+    `stream` (lsr_forward_preprocess_views_split_async); the other views' depth orders and counts run
+    on order_stream behind the preprocess (lsr_forward_depth_order_views_async), so the first views'
+    binning and compositing start before the later views' sorts.  Those views carry their own count
+    batch (binning_views_native waits for it on their first binning); same results."""
     device = _check_device(means3D)
     L = _lib.load()
     stream = stream or torch.cuda.current_stream(device)
@@ -306,20 +313,39 @@ def preprocess_views_native(raster_settings_list, means3D, opacities, shs=None, 
     fouts = [_lib.FwdOut() for _ in range(n)]
     for fo, r in zip(fouts, radii):
         fo.radii = r.data_ptr()
-    counts = torch.zeros(n, 2, dtype=torch.int32, pin_memory=True)
+    k = n if (order_first is None or order_stream is None) else max(0, min(int(order_first), n))
+    counts = torch.zeros(k, 2, dtype=torch.int32, pin_memory=True) if k > 0 else None
     s_arr = (ctypes.POINTER(_lib.Settings) * n)(*[ctypes.pointer(x.c) for x in sts])
     o_arr = (ctypes.POINTER(_lib.FwdOut) * n)(*[ctypes.pointer(fo) for fo in fouts])
     g_arr = (ctypes.c_void_p * n)(*[g.data_ptr() for g in geoms])
     try:
-        _lib.check(L.lsr_forward_preprocess_views_async(n, s_arr, ctypes.byref(fin), o_arr, g_arr,
-                                                        ctypes.c_void_p(counts.data_ptr()),
-                                                        ctypes.c_void_p(stream.cuda_stream)),
-                   "lsr_forward_preprocess_views_async")
+        _lib.check(L.lsr_forward_preprocess_views_split_async(n, k, s_arr, ctypes.byref(fin), o_arr, g_arr,
+                                                              ctypes.c_void_p(counts.data_ptr() if k else 0),
+                                                              ctypes.c_void_p(stream.cuda_stream)),
+                   "lsr_forward_preprocess_views_split_async")
     except RuntimeError:
         _dump_forward(raster_settings_list[0], inputs)
         raise
     ev = torch.cuda.Event()
     ev.record(stream)
+    late = None
+    if k < n:   # the later views' depth orders and counts on order_stream, behind the preprocess
+        order_stream.wait_event(ev)
+        for g in geoms[k:]:
+            g.record_stream(order_stream)
+        counts_b = torch.zeros(n - k, 2, dtype=torch.int32, pin_memory=True)
+        try:
+            _lib.check(L.lsr_forward_depth_order_views_async(n - k, (ctypes.POINTER(_lib.Settings) * (n - k))(*s_arr[k:]),
+                                                             ctypes.byref(fin), (ctypes.c_void_p * (n - k))(*g_arr[k:]),
+                                                             ctypes.c_void_p(counts_b.data_ptr()),
+                                                             ctypes.c_void_p(order_stream.cuda_stream)),
+                       "lsr_forward_depth_order_views_async")
+        except RuntimeError:
+            _dump_forward(raster_settings_list[0], inputs)
+            raise
+        ev_b = torch.cuda.Event()
+        ev_b.record(order_stream)
+        late = (counts_b, ev_b)
     if split and split_stream is not None:   # on the caller's side stream, beside the binning
         split_stream.wait_stream(stream)
         inputs["language_feature_split"].record_stream(split_stream)
@@ -330,8 +356,12 @@ def preprocess_views_native(raster_settings_list, means3D, opacities, shs=None, 
     for v, rs in enumerate(raster_settings_list):
         H, W = int(rs.image_height), int(rs.image_width)
         pf = PendingForward(rs, sts[v], fin, inputs, geoms[v], radii[v], None, device, H, W)
-        pf.count_host, pf.stream, pf.counted = counts[v], stream, ev
-        pf.count_batch = (counts, v)      # binning_views_native reads the whole batch at once
+        if v < k:
+            pf.count_host, pf.stream, pf.counted = counts[v], stream, ev
+            pf.count_batch = (counts, v)      # binning_views_native reads the whole batch at once
+        else:
+            pf.count_host, pf.stream, pf.counted = late[0][v - k], order_stream, late[1]
+            pf.count_batch = (late[0], v - k)
         out.append(pf)
     return out
 

@@ -121,6 +121,15 @@ SIGNATURES = {
                                                           ctypes.POINTER(FwdIn), ctypes.POINTER(ctypes.POINTER(FwdOut)),
                                                           ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p,
                                                           ctypes.c_void_p]),
+    "lsr_forward_preprocess_views_split_async": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32,
+                                                                ctypes.POINTER(ctypes.POINTER(Settings)),
+                                                                ctypes.POINTER(FwdIn),
+                                                                ctypes.POINTER(ctypes.POINTER(FwdOut)),
+                                                                ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p,
+                                                                ctypes.c_void_p]),
+    "lsr_forward_depth_order_views_async": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(ctypes.POINTER(Settings)),
+                                                           ctypes.POINTER(FwdIn), ctypes.POINTER(ctypes.c_void_p),
+                                                           ctypes.c_void_p, ctypes.c_void_p]),
     "lsr_forward_binning_views": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(ctypes.POINTER(Settings)),
                                                  ctypes.POINTER(FwdIn), ctypes.POINTER(ctypes.c_void_p),
                                                  ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),

@@ -244,7 +244,7 @@ class ViewParallelStep:
 def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool = False, overlap: bool = True,
                          batch_backward: bool = True, early_views: int = 3, composite_batch: bool = True,
                          side_priority: int = 0, side_from_preprocess: bool = True, split_behind_counts: bool = True,
-                         fill_on_side: bool = False):
+                         fill_on_side: bool = False, order_on_side: bool = False):
     """render_view callback for ViewParallelStep on the HIP rasterizer (the product path).
 
     scene    : object with means3D, opacities, shs, lang, scales, rotations device tensors
@@ -279,7 +279,10 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
     (side_from_preprocess; behind it: 925 vs 941 frames/s same-box).  fill_on_side: the language
     split, the step's bucket zeroing and the radii MAX run on that side stream ahead of its
     binning instead of on the main stream between the instance scan and the early views' emission
-    (the first compositor launch waits for them).  With
+    (the first compositor launch waits for them).  order_on_side: the later views' depth sorts and
+    instance scans run on that side stream too (the preprocess stays one launch for all views): the
+    early views' binning no longer waits for every view's depth order, and the later views are
+    binned once the early views' compositing is enqueued.  With
     composite_batch (batched only) the step runs through render_batch: one compositor forward and
     one compositor backward launch per binning batch instead of per view.
 
@@ -326,10 +329,13 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
         if split_side and bin_side[0] is None:
             bin_side[0] = torch.cuda.Stream(device=scene.means3D.device, priority=side_priority)
         to_side = fill_on_side and split_side
+        late_order = order_on_side and split_side and not to_side
         pfs = dgr.preprocess_views_native([settings[w] for w in views], scene.means3D, scene.opacities,
                                           shs=scene.shs, language_feature=scene.lang, scales=scene.scales,
                                           rotations=scene.rotations, split_behind_counts=split_behind_counts,
-                                          split_stream=bin_side[0] if to_side else None)
+                                          split_stream=bin_side[0] if to_side else None,
+                                          order_first=early_views if late_order else None,
+                                          order_stream=bin_side[0] if late_order else None)
         fill_ready[0] = None
         if to_side:                   # the fills beside the early views' binning, ahead of the side binning
             bin_side[0].wait_stream(torch.cuda.current_stream(scene.means3D.device))   # after the preprocess batch
@@ -347,7 +353,9 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
                 before_wait()
             if radii_out is not None:     # the views' radii MAX, also while the host waits for the counts
                 dgr.radii_max_native([pf.radii for pf in pfs], radii_out)
-        if split_side:
+        if late_order:   # the later views are binned by render_batch, after the early views' compositing
+            dgr.binning_views_native(pfs[:early_views])
+        elif split_side:
             dev = scene.means3D.device
             side_b = bin_side[0]
             if side_from_preprocess and not to_side:   # the side binning starts beside the early views' binning
@@ -419,6 +427,10 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
                 groups.append([(v, pf)])
         radii, ks = [], []
         for grp in groups:
+            unbinned = [pf for _, pf in grp if getattr(pf, "binning", True) is None]
+            if unbinned and unbinned[0].stream is not None and unbinned[0].stream != torch.cuda.current_stream(
+                    scene.means3D.device):   # depth-ordered on the side stream (order_on_side): binned there too
+                dgr.binning_views_native(unbinned, stream=unbinned[0].stream)
             res = dgr.render_views_native([pf for _, pf in grp])
             gcs, gls, gds = [], [], []
             for (v, _), (color, lang, r, depth, st) in zip(grp, res):

@@ -213,6 +213,9 @@ def parse_args(argv=None):
     ap.add_argument("--fill-on-side", action="store_true",
                     help="the language split, bucket zeroing and radii MAX on the side stream beside the early "
                          "views' binning instead of on the main stream before it")
+    ap.add_argument("--order-on-side", action="store_true",
+                    help="the views past --early-views are depth-sorted on the side stream too (the early views' "
+                         "binning no longer waits for every view's depth order)")
     ap.add_argument("--per-view-composite", action="store_true",
                     help="one compositor launch per view instead of one per binning batch of views")
     ap.add_argument("--pipeline", choices=("batched", "lookahead", "side"), default=None,
@@ -284,7 +287,8 @@ def run(args):
                                                                          else args.pipeline),
                                   early_views=args.early_views, composite_batch=not args.per_view_composite,
                                   side_priority=args.side_priority, side_from_preprocess=not args.side_after_binning,
-                                  split_behind_counts=not args.no_wait_fill, fill_on_side=args.fill_on_side)
+                                  split_behind_counts=not args.no_wait_fill, fill_on_side=args.fill_on_side,
+                                  order_on_side=args.order_on_side)
     Ks = []
 
     def render_view(v, b):

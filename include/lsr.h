@@ -154,6 +154,21 @@ int lsr_forward_preprocess_views_async(int32_t n_views, const lsr_settings *cons
                                        lsr_fwd_out *const *out, void *const *geom, uint32_t *host_counts,
                                        lsr_stream_t stream);
 
+/* lsr_forward_preprocess_views_async in two parts, so that the depth ordering of some views can
+ * run on a second stream (behind an event the caller records after this call) while the first
+ * views bin and composite: the preprocess of all n_views views (one launch per 8), then the depth
+ * ordering and instance counts of the first n_ordered (0 <= n_ordered <= n_views) on `stream`,
+ * their counts in host_counts[2v] as above.  The other views are then ordered by
+ * lsr_forward_depth_order_views_async (given their s / geom arrays).  Same results as
+ * lsr_forward_preprocess_views_async. */
+int lsr_forward_preprocess_views_split_async(int32_t n_views, int32_t n_ordered, const lsr_settings *const *s,
+                                             const lsr_fwd_in *in, lsr_fwd_out *const *out, void *const *geom,
+                                             uint32_t *host_counts, lsr_stream_t stream);
+/* Depth ordering + instance counts of n_views views whose preprocess already ran (geom[v] as that
+ * call left it): one set of sort and scan launches per 8 views; host_counts as above. */
+int lsr_forward_depth_order_views_async(int32_t n_views, const lsr_settings *const *s, const lsr_fwd_in *in,
+                                        void *const *geom, uint32_t *host_counts, lsr_stream_t stream);
+
 /* Forward, phase 2: tile binning and compositing of RGB + C language channels + depth.
  * `geom` is the buffer phase 1 filled; `binning` holds >= lsr_binning_bytes(num_rendered) bytes. */
 int lsr_forward_render(const lsr_settings *s, const lsr_fwd_in *in, lsr_fwd_out *out, void *geom,

@@ -57,3 +57,17 @@ def test_lds_dma_row_gather(tmp_path):
     r = subprocess.run(["timeout", "-k", "5", "60", exe], capture_output=True, text=True)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_packed_fp32_coresident(tmp_path):
+    """The deformation backward's SLP-formed packed-fp32 sequence (a broadcast v_pk_mul_f32 with op_sel
+    read by the next instruction with no wait state) run at 1, 2 and 4 blocks per CU,
+    against exact host products; the printed counts say whether the back-to-back form reproduces the
+    lanes-48..63 low-half corruption.  The forms this build relies on (scalar chains, packed ops with
+    a wait state) must be exact."""
+    src = os.path.join(ROOT, "tests", "kernels", "t_pk_coresident.hip")
+    exe = str(tmp_path / "t_pk")
+    subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-o", exe, src], check=True)
+    r = subprocess.run(["timeout", "-k", "5", "90", exe, "10"], capture_output=True, text=True)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr

@@ -186,17 +186,19 @@ def test_composite_views_equals_per_view(split):
         assert scale > 0 and float((x - y).abs().max()) <= 1e-5 * scale
 
 
-@pytest.mark.parametrize("early,fill_side", [(0, False), (3, False), (3, True)])
-def test_batched_composite_step_agrees(early, fill_side):
+@pytest.mark.parametrize("early,fill_side,order_side", [(0, False, False), (3, False, False), (3, True, False),
+                                                       (3, False, True), (1, False, True)])
+def test_batched_composite_step_agrees(early, fill_side, order_side):
     """ViewParallelStep through render_batch (the bench default: one compositor launch per binning
     batch) against the per-view compositor launches of the same batched pipeline; fill_side: the
     language split, bucket zeroing and radii MAX on the side stream (a NaN-prefilled bucket shows
-    any compositor that runs before the zeroing)."""
+    any compositor that runs before the zeroing); order_side: the later views' depth sorts on the
+    side stream too, binned after the early views' compositing is enqueued."""
     sc, settings, grads = _setup(n_views=5)
     f0, r0 = _run(sc, settings, grads, overlap="batched", deterministic=False, early_views=early,
                   composite_batch=False)
     f1, r1 = _run(sc, settings, grads, overlap="batched", deterministic=False, prefill=float("nan"),
-                  early_views=early, fill_on_side=fill_side)
+                  early_views=early, fill_on_side=fill_side, order_on_side=order_side)
     assert not torch.isnan(f1).any() and torch.equal(r0, r1)
     scale = float(f0.abs().max())
     assert scale > 0 and float((f0 - f1).abs().max()) <= 1e-5 * scale
