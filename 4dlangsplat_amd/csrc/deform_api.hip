@@ -1,4 +1,5 @@
 // deform_api.hip -- C ABI of the deformation field (include/lsr_deform.h).
+#include <atomic>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -97,7 +98,13 @@ Layout layout(const lsr_deform_net* n) {
     return L;
 }
 
+// the lsr_deform.h version the caller declared (lsr_deform_require_api); 0 = none yet
+std::atomic<int> g_deform_caller_api{0};
+
 int check(const lsr_deform_net* n) {
+    if (g_deform_caller_api.load() != LSR_DEFORM_API_VERSION)   // the structs' layout is this header's only
+        return lsr::fail(LSR_EINVAL, "call lsr_deform_require_api(LSR_DEFORM_API_VERSION) first: the caller must be "
+                                     "built against lsr_deform.h version " + std::to_string(LSR_DEFORM_API_VERSION));
     if (!n) return lsr::fail(LSR_EINVAL, "null deformation net");
     if (n->n_scales < 1 || n->n_scales > LSR_DEFORM_MAX_SCALES || n->channels != 16 || n->width != kW)
         return lsr::fail(LSR_EINVAL, "supported: 1..4 scales x 16 channels, width 128 (every HyperNeRF / Neu3D config)");
@@ -304,12 +311,20 @@ BwdScratch bwd_scratch(const lsr_deform_net* net, size_t P) {
     }
     s.daabb = take(lsr::DEF_AABB_SLOTS * 16);   // zeroed with the gradient planes (contiguous)
     s.dplanes = o;
-    o += kGradReplicas * layout(net).planes_end;
+    o += (size_t)deform_replicas(P) * layout(net).planes_end;   // the count every call of this process uses
     s.total = o;
     return s;
 }
 
 }  // namespace
+
+extern "C" int lsr_deform_require_api(int32_t caller_version) {
+    if (caller_version != LSR_DEFORM_API_VERSION)
+        return lsr::fail(LSR_EINVAL, "lsr_deform.h version mismatch: caller " + std::to_string(caller_version) +
+                                         ", library " + std::to_string(LSR_DEFORM_API_VERSION));
+    g_deform_caller_api.store(caller_version);
+    return LSR_OK;
+}
 
 extern "C" int lsr_deform_forward(const lsr_deform_net* net, const void* workspace, int32_t P, const float* means3D,
                                   const float* scales, const float* rotations, const float* opacity,

@@ -386,8 +386,8 @@ int depth_order_views(int32_t n_views, const lsr_settings* const* s, const lsr_f
         }
         {
             PhaseTimer t(LSR_PHASE_DEPTH_SORT, st);
-            if (lsr::radix_sort_batch(ss, nv, 0, 32, st) != (bool)depth_sort_result_in_b())
-                return fail(LSR_EHIP, "internal: depth sort parity");
+            if (lsr::radix_sort_batch(ss, nv, 0, 32, st) != depth_sort_result_in_b())
+                return fail(LSR_EHIP, "internal: depth sort batch or parity");
         }
         LSR_LAUNCHED("depth sort", st, s[v0]->debug);
         uint32_t wrote;
@@ -533,8 +533,9 @@ int lsr_forward_binning_views(int32_t n_views, const lsr_settings* const* s, con
         LSR_LAUNCHED("emit", st, s[0]->debug);
         {
             PhaseTimer t(LSR_PHASE_TILE_SORT, st);
-            const bool in_b = lsr::radix_sort_batch(ss, ne, 0, tbits, st);   // one set of launches for all views
-            if (in_b != tile_sort_in_b((int)ntiles)) return fail(LSR_EHIP, "internal: tile sort parity");
+            const int in_b = lsr::radix_sort_batch(ss, ne, 0, tbits, st);   // one set of launches for all views
+            if (in_b < 0 || (in_b == 1) != tile_sort_in_b((int)ntiles))
+                return fail(LSR_EHIP, "internal: tile sort batch or parity");
         }
         LSR_LAUNCHED("tile sort", st, s[0]->debug);
     }

@@ -437,7 +437,9 @@ struct SortSeg {
 struct SortBatch { SortSeg s[LSR_MAX_VIEWS]; };
 // Sorts up to LSR_MAX_VIEWS independent segments with one launch per kernel of each pass (every
 // segment the same key bits); returns whether the results are in the (b) buffers.
-bool radix_sort_batch(const SortSeg* segs, int nseg, int begin_bit, int end_bit, hipStream_t st);
+// 0: the result is in the (a) buffers, 1: in (b); -1: a batch mixing device-planned (vals_c) and
+// host-planned segments, or a planned sort over other than bits [0, 32) (nothing launched)
+int radix_sort_batch(const SortSeg* segs, int nseg, int begin_bit, int end_bit, hipStream_t st);
 bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b, size_t n,
                       int begin_bit, int end_bit, void* temp, hipStream_t st, uint32_t* kept = nullptr,
                       const SortGather* gather = nullptr, uint32_t* vals_c = nullptr);

@@ -659,13 +659,18 @@ size_t radix_temp_bytes(size_t n) {
     return RTS_ROWS_OFF + align_up(4 * os_blocks(n) * RDX * 4, 256);
 }
 
-bool radix_sort_batch(const SortSeg* segs, int nseg, int begin_bit, int end_bit, hipStream_t st) {
+int radix_sort_batch(const SortSeg* segs, int nseg, int begin_bit, int end_bit, hipStream_t st) {
     SortBatch bt{};
     int ns = 0;
     size_t nmax = 0;
     for (int i = 0; i < nseg; ++i)
         if (segs[i].n > 0) { bt.s[ns++] = segs[i]; nmax = std::max(nmax, segs[i].n); }
-    if (ns == 0 || end_bit <= begin_bit) return false;
+    if (ns == 0 || end_bit <= begin_bit) return 0;
+    // the device plan (vals_c) is the depth sort's and applies to the whole batch: every launch below
+    // serves every segment, so a batch mixing planned and host-planned segments cannot be sorted
+    for (int i = 1; i < ns; ++i)
+        if ((bt.s[i].vals_c == nullptr) != (bt.s[0].vals_c == nullptr)) return -1;
+    if (bt.s[0].vals_c && (begin_bit != 0 || end_bit != 32)) return -1;
     // keys per thread: 8 (2M keys: more, shorter blocks), 12 above 4M keys (the 6M-instance
     // tile sort: longer digit runs per block); swept 8 / 12 / 16 on both sorts
     // the device-planned depth sort takes 12 keys per thread: its 9-bit passes' digit runs are half
@@ -691,7 +696,7 @@ bool radix_sort_batch(const SortSeg* segs, int nseg, int begin_bit, int end_bit,
     };
     if (bt.s[0].vals_c) {   // the depth sort's device plan (every segment of the batch has one)
         for (int p = 0; p < 4; ++p) pass(p, 0, 0, 8, 0);
-        return false;       // either plan ends in the (a) buffers
+        return 0;           // either plan ends in the (a) buffers
     }
     bool in_b = false;
     // the bits spread evenly over the passes (13 bits: 7 + 6, not 8 + 5): fewer digits in a pass
@@ -702,7 +707,7 @@ bool radix_sort_batch(const SortSeg* segs, int nseg, int begin_bit, int end_bit,
         pass(p, (int)in_b, shift, nbits, shift + nbits >= end_bit);
         in_b = !in_b;
     }
-    return in_b;
+    return in_b ? 1 : 0;
 }
 
 bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint32_t* vals_b, size_t n,
@@ -711,7 +716,7 @@ bool radix_sort_pairs(uint32_t* keys_a, uint32_t* vals_a, uint32_t* keys_b, uint
     if (n == 0 || end_bit <= begin_bit) return false;
     SortSeg sg{keys_a, vals_a, keys_b, vals_b, temp, kept, gather ? *gather : SortGather{nullptr, nullptr, nullptr}, n};
     sg.vals_c = (vals_c && kept && gather && begin_bit == 0 && end_bit == 32) ? vals_c : nullptr;
-    return radix_sort_batch(&sg, 1, begin_bit, end_bit, st);
+    return radix_sort_batch(&sg, 1, begin_bit, end_bit, st) == 1;   // one segment: never mixed
 }
 
 }  // namespace lsr

@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("LSR_LIBRARY", os.path.join(_PKG, "build", "liblsr.so"
 
 c_float_p = ctypes.c_void_p  # device pointers are passed as opaque addresses
 API_VERSION = 4               # LSR_API_VERSION of the include/lsr.h these structs mirror
+DEFORM_API_VERSION = 3        # LSR_DEFORM_API_VERSION of include/lsr_deform.h (DeformNet, DeformGrads)
 
 
 class Settings(ctypes.Structure):
@@ -107,6 +108,7 @@ SIGNATURES = {
     "lsr_reset_opacity": (ctypes.c_int, [ctypes.c_int32, _vp, _vp, _vp, _vp]),
     "lsr_version": (ctypes.c_int, []),
     "lsr_require_api": (ctypes.c_int, [ctypes.c_int32]),
+    "lsr_deform_require_api": (ctypes.c_int, [ctypes.c_int32]),
     "lsr_last_error": (ctypes.c_char_p, []),
     "lsr_geom_bytes": (ctypes.c_int64, [ctypes.c_int32]),
     "lsr_binning_bytes": (ctypes.c_int64, [ctypes.c_int64]),
@@ -227,7 +229,7 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.lsr_require_api(API_VERSION) != 0:
+        if lib.lsr_require_api(API_VERSION) != 0 or lib.lsr_deform_require_api(DEFORM_API_VERSION) != 0:
             raise ImportError(f"{path}: {lib.lsr_last_error().decode()} (rebuild it: make -C 4dlangsplat_amd/csrc)")
         _LIB = lib
     return _LIB

@@ -68,6 +68,12 @@ typedef struct lsr_deform_net {
     const float *w_lang[3], *b_lang[3]; /* lang_deform.{1,3,5} (RESIDUAL / NORESNET) */
 } lsr_deform_net;
 
+/* Call once before any other lsr_deform_* entry point with LSR_DEFORM_API_VERSION from the
+ * lsr_deform.h the caller was built against: lsr_deform_net / lsr_deform_grads are read with THIS
+ * header's layout (version 3 added lsr_deform_grads.aabb), so a caller of another version is refused
+ * (LSR_EINVAL, every entry point) instead of having its structs misread. */
+int lsr_deform_require_api(int32_t caller_version);
+
 /* Workspace holding the packed planes (channel-last) and weights (bf16 hi/lo).  -1: bad net. */
 int64_t lsr_deform_workspace_bytes(const lsr_deform_net *net);
 /* Pack the parameters into the workspace; call again after every parameter update. */

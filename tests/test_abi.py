@@ -98,6 +98,13 @@ assert rc == 1 and b"lsr_require_api" in L.lsr_last_error()
 assert L.lsr_require_api(4) == 0
 rc = L.lsr_forward_preprocess(None, None, None, None, ctypes.byref(k), None)
 assert rc == 1 and b"null settings" in L.lsr_last_error(), L.lsr_last_error()
+# lsr_deform.h has its own handshake (its structs gained a trailing field in version 3)
+L.lsr_deform_workspace_bytes.restype = ctypes.c_int64
+assert L.lsr_deform_workspace_bytes(None) == -1 and b"lsr_deform_require_api" in L.lsr_last_error()
+assert L.lsr_deform_require_api(2) == 1 and b"mismatch" in L.lsr_last_error()
+assert L.lsr_deform_workspace_bytes(None) == -1 and b"lsr_deform_require_api" in L.lsr_last_error()
+assert L.lsr_deform_require_api(3) == 0
+assert L.lsr_deform_workspace_bytes(None) == -1 and b"null deformation net" in L.lsr_last_error()
 print("ok")
 """
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)

@@ -49,7 +49,7 @@ def _problem(stage, field_p=None):
     noise = {"f_dc": torch.randn(P, 1, 3, generator=g) * 0.5, "xyz": torch.randn(P, 3, generator=g) * 0.01}
 
     def student():
-        raw = _raw(sc)
+        raw = {k: v.clone() for k, v in _raw(sc).items()}   # fresh storage: training steps in place
         for k, v in noise.items():
             raw[k] = (raw[k] + v.to(dev)).contiguous()
         sched = ReferenceSchedule(8.0, stage=stage, densify_from_iter=12, densification_interval=5,
@@ -123,7 +123,7 @@ def test_capture_layout_and_restore_with_field():
         a(cams, gts, iteration=it)
     cap = a.capture()
     assert len(cap) == 14 and cap[0] == 3 and cap[-1] == 8.0
-    opt = cap[13]
+    opt = cap[12]
     names = [g["name"] for g in opt["param_groups"]]
     assert names == ["xyz", "deformation", "grid", "f_dc", "f_rest", "opacity", "scaling", "rotation"]
     assert all(k.startswith("deformation_net.") for k in cap[2])

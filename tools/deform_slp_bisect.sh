@@ -1,0 +1,20 @@
+#!/bin/bash
+# Diagnostic builds of deform.o for the packed-fp32 co-residency fault: SLP
+# vectorisation on (the build that failed), with the compiler's wait states padded (every instruction
+# preceded by s_nop), or with every s_waitcnt forced to zero.  Usage (here, CPU): tools/deform_slp_bisect.sh
+# Output: 4dlangsplat_amd/build/variants/liblsr_<name>.so; run tools/deform_race.py with LSR_LIBRARY=...
+set -e
+cd "$(dirname "$0")/../4dlangsplat_amd/csrc"
+make -s -j8
+OBJ=../build/obj; OUT=../build/variants; mkdir -p $OUT/obj
+FLAGS="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -munsafe-fp-atomics"
+build() {   # name, extra flags...
+    local name=$1; shift
+    /opt/rocm/bin/hipcc $FLAGS "$@" -c -o $OUT/obj/deform_$name.o deform.hip 2>/dev/null
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/liblsr_$name.so $(ls $OBJ/*.o | grep -v "/deform.o") $OUT/obj/deform_$name.o
+    echo "built $OUT/liblsr_$name.so"
+}
+build slp
+build slp_pad1 -Xarch_device -mllvm=-amdgpu-snop-padding=1
+build slp_pad2 -Xarch_device -mllvm=-amdgpu-snop-padding=2
+build slp_wz -Xarch_device -mllvm=-amdgpu-waitcnt-forcezero
