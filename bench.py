@@ -452,10 +452,18 @@ def run(args):
                                "step reads a Gaussian's inputs and writes its gradient rows once per launch of "
                                "up to 8 views, so it moves less than this: see pmc_step (measured traffic) and "
                                "single_view.frame_roofline (the per-frame path this formula describes)")
-        if prof and pmc_all:
-            # the step's measured HBM traffic: PMC bytes per launch of every profiled phase x its
-            # launches in one step, per frame (kernels without a PMC record, the sorts and scans,
-            # are left out, so this is a lower bound)
+        step_rec = pmc_all.get("_step") if isinstance(pmc_all.get("_step"), dict) else None
+        if step_rec and step_rec.get("hbm_bytes_per_step"):
+            # the step's measured HBM traffic: PMC bytes of EVERY dispatch of one 8-view step (the
+            # sorts, scans and fills included; tools/pmc_summary.py step_bytes), per frame
+            per_frame = step_rec["hbm_bytes_per_step"] / len(dp.views)
+            frame_roof["pmc_step"] = dict(hbm_bytes_per_frame=int(per_frame), achieved=round(per_frame * value / 1e9, 1),
+                                          frac=round(per_frame * value / 1e9 / HBM_PEAK_GBS, 4),
+                                          source="profiles/pmc_traffic.json _step: (2 FETCH_SIZE + WRITE_SIZE) over "
+                                                 "every dispatch of a step")
+        elif prof and pmc_all:
+            # older records: PMC bytes per launch of every profiled phase x its launches in one
+            # step, per frame (kernels without a PMC record, the sorts and scans, left out: a lower bound)
             step_b = sum(pmc_all[k]["hbm_bytes_per_launch"] * n for k, (ms, n) in prof_all.items()
                          if n and isinstance(pmc_all.get(k), dict) and pmc_all[k].get("hbm_bytes_per_launch"))
             per_frame = step_b / len(dp.views)

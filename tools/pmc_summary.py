@@ -43,6 +43,33 @@ def mfma_frac(c):
     return busy / max(active * N_SIMD, 1.0)
 
 
+STEP_FIRST, STEP_LAST = "k_preprocess<16, true>", "k_preprocess_bwd_views"
+
+
+def step_bytes(d, counter):
+    """Per bench step, the counter summed over EVERY dispatch of the step (the sorts, scans, fills
+    and torch kernels included): a step runs from the batched preprocess (k_preprocess<16, true>)
+    through the flush (k_preprocess_bwd_views); mean over the steps of the pass, in KB."""
+    totals = []
+    for f in sorted(glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True)):
+        rows = []
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row["Counter_Name"] == counter:
+                    rows.append((int(row["Dispatch_Id"]), short(row.get("Kernel_Name", "")), float(row["Counter_Value"])))
+        rows.sort()
+        cur = None
+        for _, k, v in rows:
+            if k == STEP_FIRST:
+                cur = 0.0
+            if cur is not None:
+                cur += v
+                if k.split("<")[0] == STEP_LAST:
+                    totals.append(cur)
+                    cur = None
+    return (sum(totals) / len(totals), len(totals)) if totals else (None, 0)
+
+
 def main(d, json_out=None):
     acc = defaultdict(lambda: defaultdict(list))
     for f in sorted(glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True)):
@@ -88,6 +115,15 @@ def main(d, json_out=None):
             if "SQ_ACTIVE_INST_VALU" in f and "SQ_WAVE_CYCLES" in f:
                 # both count quad-cycles: the share of a resident wave's cycles that issue VALU
                 res[phase]["valu_issue_per_wave"] = round(sum(f["SQ_ACTIVE_INST_VALU"]) / max(sum(f["SQ_WAVE_CYCLES"]), 1), 4)
+        fetch, nf = step_bytes(d, "FETCH_SIZE")
+        write, nw = step_bytes(d, "WRITE_SIZE")
+        if fetch is not None and write is not None:
+            res["_step"] = dict(fetch_size_kb=fetch, write_size_kb=write, steps=min(nf, nw),
+                                hbm_bytes_per_step=int((2 * fetch + write) * 1024),
+                                note="every dispatch from k_preprocess<16, true> through k_preprocess_bwd_views "
+                                     "(sorts, scans, fills included), mean over the pass's steps")
+            print(f"step: FETCH x2 {2 * fetch / 1024:.1f} MB + WRITE {write / 1024:.1f} MB = "
+                  f"{(2 * fetch + write) / 1024:.1f} MB per step ({min(nf, nw)} steps)")
         res["_note"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, bench.py --steps 1 (8 views); "
                         "hbm = (2*FETCH_SIZE + WRITE_SIZE)*1024 per MI355X_MICROARCH.md HBM section")
         with open(json_out, "w") as fh:
