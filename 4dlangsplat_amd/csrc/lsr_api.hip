@@ -440,6 +440,38 @@ int lsr_forward_preprocess_views_split_async(int32_t n_views, int32_t n_ordered,
     return n_ordered > 0 ? depth_order_views(n_ordered, s, in, geom, host_counts, st) : LSR_OK;
 }
 
+int lsr_forward_preprocess_views_rows_async(int32_t n_views, int32_t row0, int32_t row1, const lsr_settings* const* s,
+                                            const lsr_fwd_in* in, lsr_fwd_out* const* out, void* const* geom,
+                                            lsr_stream_t stream) {
+    int rc = check_views(n_views, s, in, geom);
+    if (rc) return rc;
+    if (!out || row0 < 0 || row1 < row0 || row1 > in->P || row0 % 256 != 0)
+        return fail(LSR_EINVAL, "0 <= row0 <= row1 <= P with row0 a multiple of 256, and the outputs are required");
+    for (int v = 0; v < n_views; ++v)
+        if (!out[v] || (!out[v]->radii && in->P > 0)) return fail(LSR_EINVAL, "radii output is required");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int P = in->P;
+    if (row1 == row0) return LSR_OK;
+    for (int v0 = 0; v0 < n_views; v0 += lsr::LSR_MAX_VIEWS) {
+        const int nv = std::min(n_views - v0, lsr::LSR_MAX_VIEWS);
+        lsr::PreprocessArgs a{};
+        preprocess_shared(a, s[v0], in);
+        a.nv = nv;
+        a.row0 = row0;
+        a.P = row1;   // the launch's bound (every per-Gaussian array is indexed by the global row)
+        for (int k = 0; k < nv; ++k) {
+            Geom g = carve_geom(geom[v0 + k], (size_t)P, nullptr);
+            preprocess_view(a.v[k], s[v0 + k], g, out[v0 + k]->radii);
+        }
+        {
+            PhaseTimer t(LSR_PHASE_PREPROCESS, st);
+            lsr::launch_preprocess(a, st);
+        }
+        LSR_LAUNCHED("preprocess", st, s[v0]->debug);
+    }
+    return LSR_OK;
+}
+
 int lsr_forward_depth_order_views_async(int32_t n_views, const lsr_settings* const* s, const lsr_fwd_in* in,
                                         void* const* geom, uint32_t* host_counts, lsr_stream_t stream) {
     int rc = check_views(n_views, s, in, geom);

@@ -88,6 +88,7 @@ struct PreprocessView {
 // inputs are read (and its cov3D built) once for all of them.
 struct PreprocessArgs {
     int P, M, deg, W, H, grid_x, grid_y, nv;
+    int row0;   // the launch covers Gaussians [row0, P) (a row chunk; a multiple of 256), usually 0
     float scale_modifier;
     const float* means3D;
     const float* scales;

@@ -319,7 +319,7 @@ __device__ __forceinline__ void zero_acc_rows(float4* acc, bool rect, int i) {
 
 template <int MS, bool MULTI>
 __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = a.row0 + blockIdx.x * blockDim.x + threadIdx.x;
     GaussIn<MS> g;
     if constexpr (!MULTI) {
         clear_words(a.v[0].clear);
@@ -338,8 +338,8 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
 }
 
 void launch_preprocess(const PreprocessArgs& a, hipStream_t st) {
-    if (a.P == 0 || a.nv <= 0) return;
-    const dim3 grid((a.P + 255) / 256), block(256);
+    if (a.P <= a.row0 || a.nv <= 0) return;
+    const dim3 grid((a.P - a.row0 + 255) / 256), block(256);
 #define LSR_PP(MS)                                                                   \
     do {                                                                             \
         if (a.nv > 1) hipLaunchKernelGGL((k_preprocess<MS, true>), grid, block, 0, st, a);  \

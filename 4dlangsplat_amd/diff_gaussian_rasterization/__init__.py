@@ -273,7 +273,7 @@ def language_split_native(language_feature, stream=None, out=None):
 def preprocess_views_native(raster_settings_list, means3D, opacities, shs=None, colors_precomp=None,
                             language_feature=None, scales=None, rotations=None, cov3D_precomp=None, stream=None,
                             split_language=True, split_behind_counts=True, split_stream=None, order_first=None,
-                            order_stream=None):
+                            order_stream=None, row_chunks=None):
     """Forward phase 1 of several views of the same Gaussians as one batch
     (lsr_forward_preprocess_views_async: one preprocess launch per 8 views reads each Gaussian once,
     the views' depth sorts and instance scans share their launches) on `stream`.  No host
@@ -291,7 +291,12 @@ def preprocess_views_native(raster_settings_list, means3D, opacities, shs=None, 
     `stream` (lsr_forward_preprocess_views_split_async); the other views' depth orders and counts run
     on order_stream behind the preprocess (lsr_forward_depth_order_views_async), so the first views'
     binning and compositing start before the later views' sorts.  Those views carry their own count
-    batch (binning_views_native waits for it on their first binning); same results."""
+    batch (binning_views_native waits for it on their first binning); same results.
+
+    row_chunks = [(r0, r1, before), ...] covering [0, P) in order (r0 multiples of 256): the
+    preprocess runs one launch per row chunk (lsr_forward_preprocess_views_rows_async), each after
+    before() (which makes `stream` wait for that chunk's rows, e.g. the sharded optimizer's
+    all-gather of them), and the depth orders follow once every chunk is in; same results."""
     device = _check_device(means3D)
     L = _lib.load()
     stream = stream or torch.cuda.current_stream(device)
@@ -319,10 +324,29 @@ def preprocess_views_native(raster_settings_list, means3D, opacities, shs=None, 
     o_arr = (ctypes.POINTER(_lib.FwdOut) * n)(*[ctypes.pointer(fo) for fo in fouts])
     g_arr = (ctypes.c_void_p * n)(*[g.data_ptr() for g in geoms])
     try:
-        _lib.check(L.lsr_forward_preprocess_views_split_async(n, k, s_arr, ctypes.byref(fin), o_arr, g_arr,
-                                                              ctypes.c_void_p(counts.data_ptr() if k else 0),
-                                                              ctypes.c_void_p(stream.cuda_stream)),
-                   "lsr_forward_preprocess_views_split_async")
+        if row_chunks:
+            covered = 0
+            for r0, r1, before in row_chunks:
+                if r0 != covered or r1 < r0:
+                    raise ValueError("row_chunks must cover [0, P) in order")
+                covered = r1
+                if before is not None:
+                    before()
+                _lib.check(L.lsr_forward_preprocess_views_rows_async(n, int(r0), int(r1), s_arr, ctypes.byref(fin),
+                                                                     o_arr, g_arr, ctypes.c_void_p(stream.cuda_stream)),
+                           "lsr_forward_preprocess_views_rows_async")
+            if covered != P:
+                raise ValueError("row_chunks must cover [0, P) in order")
+            if k > 0:
+                _lib.check(L.lsr_forward_depth_order_views_async(k, s_arr, ctypes.byref(fin), g_arr,
+                                                                 ctypes.c_void_p(counts.data_ptr()),
+                                                                 ctypes.c_void_p(stream.cuda_stream)),
+                           "lsr_forward_depth_order_views_async")
+        else:
+            _lib.check(L.lsr_forward_preprocess_views_split_async(n, k, s_arr, ctypes.byref(fin), o_arr, g_arr,
+                                                                  ctypes.c_void_p(counts.data_ptr() if k else 0),
+                                                                  ctypes.c_void_p(stream.cuda_stream)),
+                       "lsr_forward_preprocess_views_split_async")
     except RuntimeError:
         _dump_forward(raster_settings_list[0], inputs)
         raise

@@ -129,6 +129,11 @@ SIGNATURES = {
                                                                 ctypes.POINTER(ctypes.POINTER(FwdOut)),
                                                                 ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p,
                                                                 ctypes.c_void_p]),
+    "lsr_forward_preprocess_views_rows_async": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                                               ctypes.POINTER(ctypes.POINTER(Settings)),
+                                                               ctypes.POINTER(FwdIn),
+                                                               ctypes.POINTER(ctypes.POINTER(FwdOut)),
+                                                               ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p]),
     "lsr_forward_depth_order_views_async": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(ctypes.POINTER(Settings)),
                                                            ctypes.POINTER(FwdIn), ctypes.POINTER(ctypes.c_void_p),
                                                            ctypes.c_void_p, ctypes.c_void_p]),

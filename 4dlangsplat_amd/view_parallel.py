@@ -162,6 +162,19 @@ class ViewParallelStep:
 
     def run(self, render_view: Callable[[int, GradBucket], Optional[torch.Tensor]]) -> GradBucket:
         b = self.bucket
+        upd = self.update
+        defer = False
+        if upd is not None and hasattr(upd, "gather_waits"):
+            # the previous step's all-gathers may still be in flight: a renderer that preprocesses by
+            # row chunks waits for each chunk's rows itself, any other waits for all of them now
+            waits = upd.gather_waits()
+            setter = getattr(render_view, "set_row_waits", None)
+            if waits and setter is not None:
+                setter(waits)
+                upd._ag = []
+            else:
+                upd.wait_all()
+            defer = setter is not None
         begin = getattr(render_view, "begin_step", None)
         if begin is not None:             # the renderer may look ahead only within this rank's views
             begin(self.views)
@@ -200,7 +213,11 @@ class ViewParallelStep:
             # which writes every other field) instead of after it
             pending.append(dist.all_reduce(b.flat[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True))
         chunked = self.world > 1 and getattr(flush, "chunked", False) and self.flush_chunks > 1 and not sharded
-        if chunked:
+        sharded_chunks = sharded and getattr(flush, "chunked", False) and getattr(self.update, "chunks", 1) > 1
+        if sharded_chunks:
+            # the flush in the optimizer's row chunks: each chunk's reduce-scatters start behind it
+            flush(b, row_chunks=self.update.chunk_rows(), on_rows=lambda r0, r1: self.update.on_rows(b, r0, r1))
+        elif chunked:
             # the flush in Gaussian-row chunks: each chunk's rows of every other field are SUMmed
             # (asynchronously, behind that chunk's launch) while the next chunk is computed
             def on_rows(r0, r1):
@@ -217,7 +234,10 @@ class ViewParallelStep:
         if end is not None:
             end()
         if sharded:
-            self.update.step(b)
+            if defer:
+                self.update.step(b, wait_gather=False)   # the next step's preprocess waits per row chunk
+            else:
+                self.update.step(b)
             for h in pending:
                 h.wait()
         elif self.world > 1:
@@ -317,6 +337,16 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
 
     batched = batch_backward and not deterministic
     held = []                             # (state, dL_dcolor, dL_dlang, dL_ddepth) awaiting flush
+    row_waits = [None]                    # [(r0, r1, wait)]: the scene's rows still arriving (ShardedAdam)
+
+    def take_row_waits(chunked_ok):
+        """The pending row waits: returned for a row-chunked preprocess, else all waited for here."""
+        w, row_waits[0] = row_waits[0], None
+        if not w or chunked_ok:
+            return w
+        for _, _, fn in w:
+            fn()
+        return None
 
     def batch_preprocess(v, before_wait=None, radii_out=None):
         """The step's views from v on, as one batch: preprocess + depth sorts + instance scans, one
@@ -330,12 +360,14 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
             bin_side[0] = torch.cuda.Stream(device=scene.means3D.device, priority=side_priority)
         to_side = fill_on_side and split_side
         late_order = order_on_side and split_side and not to_side
+        waits = take_row_waits(scene.means3D.is_cuda)
         pfs = dgr.preprocess_views_native([settings[w] for w in views], scene.means3D, scene.opacities,
                                           shs=scene.shs, language_feature=scene.lang, scales=scene.scales,
                                           rotations=scene.rotations, split_behind_counts=split_behind_counts,
                                           split_stream=bin_side[0] if to_side else None,
                                           order_first=early_views if late_order else None,
-                                          order_stream=bin_side[0] if late_order else None)
+                                          order_stream=bin_side[0] if late_order else None,
+                                          row_chunks=waits)
         fill_ready[0] = None
         if to_side:                   # the fills beside the early views' binning, ahead of the side binning
             bin_side[0].wait_stream(torch.cuda.current_stream(scene.means3D.device))   # after the preprocess batch
@@ -373,6 +405,7 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
     def render_view(v: int, bucket: GradBucket):
         if batch_fwd and v not in pending:
             batch_preprocess(v)
+        take_row_waits(False)             # per-view preprocess: every row first
         pf = pending.pop(v, None)
         if pf is None:                    # first view of a step: the Gaussians are final here
             pf = preprocess(v)
@@ -474,8 +507,12 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
         pending.clear()                   # nothing is carried across steps (the Gaussians change)
         step_views[0] = None
 
+    def set_row_waits(waits):
+        row_waits[0] = list(waits) if waits else None
+
     render_view.begin_step = begin_step
     render_view.end_step = end_step
+    render_view.set_row_waits = set_row_waits
     render_view.pending = pending         # inspection (tests)
     render_view.last_num_rendered = 0
     if batched:
@@ -493,10 +530,9 @@ class ShardedAdam:
 
     Every rank holds the ACTIVATED rasterizer inputs of all P Gaussians (what the views render: the
     scene's means3D, scales, rotations, opacities, shs, lang); the raw parameters and both Adam moments
-    exist only for the rank's row shard [r0, r1).  step(bucket), once the views' gradients are in the
-    bucket:
-      1. reduce-scatter each gradient field by rows (one collective per field, all in flight at once):
-         the rank receives the SUM over every rank's views of its own rows only;
+    exist only for the rank's row shard.  step(bucket), once the views' gradients are in the bucket:
+      1. reduce-scatter each gradient field by rows: the rank receives the SUM over every rank's views
+         of its own rows only;
       2. back through the activations (gaussian_renderer/__init__.py:95-97,191-193 and the model's
          activations, scene/gaussian_model.py:38-47): scaling exp, opacity sigmoid, rotation and
          language L2 normalisations; SH split into f_dc / f_rest;
@@ -507,22 +543,41 @@ class ShardedAdam:
     The traffic per rank is (N-1)/N of the bucket (reduce-scatter) plus (N-1)/N of the activated
     inputs (all-gather) -- the volume of the all-reduce it replaces -- while the activation math and
     Adam run on 1/N of the rows and the parameters' optimizer state shrinks N-fold.
-    Shard boundaries are multiples of `align` rows; the bucket must be built with
-    GradBucket(row_multiple=world * shard rows) (ShardedAdam.row_multiple)."""
+
+    chunks = C > 1 pipelines it by row chunks.  The row space [0, Pa) is cut into C chunks of
+    Pa / C rows and each chunk into one piece per rank (the rank's shard is its C pieces), so every
+    chunk is reduce-scattered and all-gathered as a contiguous row range of its own:
+      * the flush (the batched preprocess backward, which writes every non-language gradient row)
+        runs in these chunks and reports each (on_rows): the chunk's reduce-scatters start right behind
+        its launch while the next chunk is computed;
+      * step() takes the chunks in order: wait for the chunk's reduce-scatters, activations' backward +
+        Adam + activations on the rank's piece, start the chunk's all-gathers -- and returns without
+        waiting for them;
+      * the next step's renderer preprocesses each row chunk once its all-gather is in
+        (gather_waits(), native_view_renderer's row waits: lsr_forward_preprocess_views_rows_async per
+        chunk), so the all-gather overlaps the last chunks' Adam and the first chunks' preprocess.
+        A renderer that cannot wait per chunk gets wait_all() before the step.
+    Shard boundaries are multiples of `align` rows (256 with chunks > 1, the preprocess's row-chunk
+    granularity); the bucket must be built with GradBucket(row_multiple=ShardedAdam.row_multiple(...))."""
 
     GROUPS = ("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation", "language_feature")
+    BUCKET_FIELDS = ("means3D", "scales", "rotations", "opacities", "sh", "language_feature")
+    ACT_FIELDS = ("means3D", "scales", "rotations", "opacities", "shs", "lang")
 
     @staticmethod
-    def row_multiple(P: int, world: int, align: int = 64) -> int:
-        rows = -(-P // max(1, world))
-        return -(-rows // align) * align * world
+    def row_multiple(P: int, world: int, align: int = 64, chunks: int = 1) -> int:
+        """Pa: a multiple of world * chunks * piece alignment covering P rows."""
+        align = max(align, 256) if chunks > 1 else align
+        unit = world * max(1, chunks) * align
+        return -(-max(P, 1) // unit) * unit
 
     def __init__(self, scene, raw: Dict[str, torch.Tensor], lrs: Dict[str, float], group=None, align: int = 64,
-                 betas=(0.9, 0.999), eps: float = 1e-15, adam: Optional[Callable] = None, nonormalized: bool = False):
+                 betas=(0.9, 0.999), eps: float = 1e-15, adam: Optional[Callable] = None, nonormalized: bool = False,
+                 chunks: int = 1):
         """scene: object with the activated tensors (means3D, scales, rotations, opacities, shs, lang);
         they are re-bound to row-padded storage.  raw: the full raw parameters (xyz, f_dc, f_rest,
         opacity, scaling, rotation, language_feature), of which this rank keeps its shard.
-        adam(p, g, m, v, lr, step): in place on one group's shard (default: lsr_adam_step)."""
+        adam(p, g, m, v, lr, step): in place on one group's rows (default: lsr_adam_step)."""
         if getattr(scene, "deformation", None) is not None:
             # the bucket's means3D gradient is the xyz gradient and the gathered rows are the
             # rasterizer's inputs only without a field between the parameters and the rasterizer
@@ -533,28 +588,46 @@ class ShardedAdam:
         self.world = dist.get_world_size(group) if self.distributed else 1
         self.rank = dist.get_rank(group) if self.distributed else 0
         self.xyz_scheduler_args = None
+        self.chunks = max(1, int(chunks))
         self.P = P = scene.means3D.shape[0]
-        self.Pa = self.row_multiple(P, self.world, align) if P > 0 else 0
-        self.rows = self.Pa // self.world
-        self.r0 = min(P, self.rank * self.rows)
-        self.r1 = min(P, self.r0 + self.rows)
+        self.Pa = self.row_multiple(P, self.world, align, self.chunks) if P > 0 else 0
+        self.Pc = self.Pa // self.chunks                # rows per chunk
+        self.piece = self.Pc // self.world              # rows per rank per chunk
+        self.rows = self.chunks * self.piece            # the shard (padding rows past P included)
+        # the rank's pieces: shard rows [c piece, (c + 1) piece) are global rows [g0, g0 + piece)
+        self.pieces = [(c * self.Pc + self.rank * self.piece, c * self.Pc + (self.rank + 1) * self.piece)
+                       for c in range(self.chunks)]
+        # chunks = 1: the shard is one contiguous row range [r0, r1) (clipped to P)
+        self.r0 = min(P, self.pieces[0][0]) if self.pieces else 0
+        self.r1 = min(P, self.pieces[0][1]) if self.pieces else 0
         self.lrs, self.betas, self.eps, self.nonormalized = dict(lrs), betas, eps, nonormalized
         self._adam = adam
         self.scene = scene
         dev = scene.means3D.device
         # activated inputs in row-padded storage (all-gather target); the scene's tensors view it
         self.act = {}
-        for name in ("means3D", "scales", "rotations", "opacities", "shs", "lang"):
+        for name in self.ACT_FIELDS:
             t = getattr(scene, name)
             buf = torch.zeros((self.Pa,) + tuple(t.shape[1:]), dtype=torch.float32, device=dev)
             buf[:P] = t
             self.act[name] = buf
             setattr(scene, name, buf[:P])
-        self.raw = {n: raw[n][self.r0:self.r1].detach().to(dev, torch.float32).clone().contiguous()
-                    for n in self.GROUPS if n in raw}
+        self.raw = {}
+        for n in self.GROUPS:
+            if n not in raw:
+                continue
+            src = raw[n].detach().to(dev, torch.float32)
+            t = torch.zeros((self.rows,) + tuple(src.shape[1:]), dtype=torch.float32, device=dev)
+            for c, (g0, g1) in enumerate(self.pieces):
+                hi = min(g1, P)
+                if hi > g0:
+                    t[c * self.piece:c * self.piece + hi - g0] = src[g0:hi]
+            self.raw[n] = t.contiguous()
         self.exp_avg = {n: torch.zeros_like(t) for n, t in self.raw.items()}
         self.exp_avg_sq = {n: torch.zeros_like(t) for n, t in self.raw.items()}
         self.steps = {n: 0 for n in self.raw}
+        self._rs = {}            # chunk -> (shard gradient rows per field, handles): reduce-scatters in flight
+        self._ag = []            # [(r0, r1, handles)]: the last step's all-gathers, not yet waited for
 
     # ---- learning rate (gaussian_model.py:302-329; GaussianTrainer's schedule) ----------------------
     def set_xyz_schedule(self, lr_init, lr_final, lr_delay_mult=0.01, max_steps=30000):
@@ -569,52 +642,99 @@ class ShardedAdam:
             self.lrs["xyz"] = float(self.xyz_scheduler_args(iteration))
         return self.lrs.get("xyz")
 
+    # ---- row chunks ----------------------------------------------------------------------------------
+    def chunk_rows(self):
+        """The chunks' global row ranges clipped to [0, P) (empty ones dropped): the flush's row_chunks."""
+        out = []
+        for c in range(self.chunks):
+            r0, r1 = c * self.Pc, min((c + 1) * self.Pc, self.P)
+            if r1 > r0:
+                out.append((r0, r1))
+        return out
+
+    def gather_waits(self):
+        """[(r0, r1, wait)] over [0, P) for the all-gathers still in flight (wait() makes the current
+        stream, or with gloo the host, wait for that chunk's rows); [] when none are."""
+        out = []
+        for r0, r1, hs in self._ag:
+            r1 = min(r1, self.P)
+            if r1 > r0:
+                out.append((r0, r1, (lambda hs=hs: [h.wait() for h in hs])))
+        return out
+
+    def wait_all(self):
+        for _, _, hs in self._ag:
+            for h in hs:
+                h.wait()
+        self._ag = []
+
     # ---- 1. reduce-scatter ------------------------------------------------------------------------
-    def _shard_grads(self, bucket) -> Dict[str, torch.Tensor]:
+    def _issue_rs(self, bucket, c):
+        if c in self._rs:
+            return
         if bucket.Pa != self.Pa:
             raise ValueError(f"bucket rows {bucket.Pa} != {self.Pa}: build it with GradBucket(row_multiple=...)")
         out, handles = {}, []
-        for name in ("means3D", "scales", "rotations", "opacities", "sh", "language_feature"):
-            f0, f1 = bucket.ranges[name]
+        for name in self.BUCKET_FIELDS:
+            f0, _ = bucket.ranges[name]
             w = bucket.widths[name]
             if w == 0:
                 continue
-            full = bucket.flat[f0:f1]
+            full = bucket.flat[f0 + c * self.Pc * w:f0 + (c + 1) * self.Pc * w]
             if self.world > 1:
-                shard = torch.empty(self.rows * w, dtype=torch.float32, device=full.device)
+                shard = torch.empty(self.piece * w, dtype=torch.float32, device=full.device)
                 handles.append(dist.reduce_scatter_tensor(shard, full, group=self.group, async_op=True))
             else:
                 shard = full
-            out[name] = shard.view(self.rows, w)[: self.r1 - self.r0]
-        for h in handles:
-            h.wait()
-        return out
+            out[name] = shard.view(self.piece, w)
+        self._rs[c] = (out, handles)
+
+    def on_rows(self, bucket, r0, r1):
+        """The flush finished rows [r0, r1) of every gradient field: reduce-scatter the chunks they complete."""
+        for c in range(self.chunks):
+            if r0 <= c * self.Pc and min((c + 1) * self.Pc, self.P) <= r1:
+                self._issue_rs(bucket, c)
 
     # ---- 2. activations' backward, 3. Adam, 4. activations + all-gather ----------------------------------
     def _lang_act(self, x):
         return x if self.nonormalized else x / (x.norm(dim=-1, keepdim=True) + 1e-9)
 
-    def step(self, bucket) -> None:
-        g = self._shard_grads(bucket)
-        r0, r1 = self.r0, self.r1
-        raw = self.raw
+    def step(self, bucket, wait_gather: bool = True) -> None:
+        """wait_gather=False returns with the all-gathers in flight (gather_waits / wait_all)."""
+        self.wait_all()   # a previous step's gathers (nothing may overwrite the scene rows under them)
+        for n in self.raw:
+            self.steps[n] += 1
+        for c in range(self.chunks):
+            self._issue_rs(bucket, c)
+        for c in range(self.chunks):
+            g, handles = self._rs.pop(c)
+            for h in handles:
+                h.wait()
+            self._step_chunk(c, g)
+        if wait_gather:
+            self.wait_all()
+
+    def _step_chunk(self, c, g):
+        sl = slice(c * self.piece, (c + 1) * self.piece)
+        raw = {n: t[sl] for n, t in self.raw.items()}
+        n_rows = self.piece
         grads = {}
         if "means3D" in g:
             grads["xyz"] = g["means3D"]
         if "sh" in g:
-            sh = g["sh"].reshape(r1 - r0, -1, 3)
+            sh = g["sh"].reshape(n_rows, -1, 3)
             grads["f_dc"], grads["f_rest"] = sh[:, :1], sh[:, 1:]
-        if "opacities" in g:
+        if "opacities" in g and "opacity" in raw:
             o = torch.sigmoid(raw["opacity"])
             grads["opacity"] = g["opacities"].reshape(o.shape) * o * (1 - o)
-        if "scales" in g:
+        if "scales" in g and "scaling" in raw:
             grads["scaling"] = g["scales"] * torch.exp(raw["scaling"])
-        if "rotations" in g:
+        if "rotations" in g and "rotation" in raw:
             q = raw["rotation"]
-            n = q.norm(dim=-1, keepdim=True).clamp_min(1e-12)      # F.normalize's eps
-            r = q / n
+            nq = q.norm(dim=-1, keepdim=True).clamp_min(1e-12)      # F.normalize's eps
+            r = q / nq
             gr = g["rotations"]
-            grads["rotation"] = (gr - r * (r * gr).sum(-1, keepdim=True)) / n
+            grads["rotation"] = (gr - r * (r * gr).sum(-1, keepdim=True)) / nq
         if "language_feature" in g and "language_feature" in raw:
             x, gl = raw["language_feature"], g["language_feature"]
             if self.nonormalized:
@@ -627,27 +747,43 @@ class ShardedAdam:
             if name not in raw or name not in self.lrs:
                 continue
             gr = gr.reshape(raw[name].shape).contiguous()
-            self.steps[name] += 1
-            self._adam_group(raw[name], gr, self.exp_avg[name], self.exp_avg_sq[name], self.lrs[name], self.steps[name])
-        # 4. activated shard rows, gathered into every rank's scene tensors
+            self._adam_group(raw[name], gr, self.exp_avg[name][sl], self.exp_avg_sq[name][sl], self.lrs[name],
+                             self.steps[name])
+        # 4. activated piece rows, gathered into every rank's scene tensors
         act_rows = dict(means3D=raw.get("xyz"), scales=torch.exp(raw["scaling"]) if "scaling" in raw else None,
                         rotations=torch.nn.functional.normalize(raw["rotation"]) if "rotation" in raw else None,
                         opacities=torch.sigmoid(raw["opacity"]) if "opacity" in raw else None,
                         shs=torch.cat([raw["f_dc"], raw["f_rest"]], dim=1) if "f_dc" in raw else None,
                         lang=self._lang_act(raw["language_feature"]) if "language_feature" in raw else None)
+        g0 = self.pieces[c][0]
+        valid = max(0, min(self.piece, self.P - g0))   # rows past P stay as they are (never rendered)
         handles = []
         for name, rows in act_rows.items():
             if rows is None:
                 continue
             buf = self.act[name]
             w = buf[0].numel() if self.Pa else 0
-            mine = buf.view(self.Pa, -1)[self.rank * self.rows:(self.rank + 1) * self.rows]
-            mine[: r1 - r0] = rows.reshape(r1 - r0, w)
+            flat = buf.view(self.Pa, -1)
+            mine = flat[g0:g0 + self.piece]
+            if valid > 0:
+                mine[:valid] = rows.reshape(self.piece, w)[:valid]
             if self.world > 1:
-                handles.append(dist.all_gather_into_tensor(buf.view(-1), mine.reshape(-1).clone(), group=self.group,
+                chunk = flat[c * self.Pc:(c + 1) * self.Pc]
+                handles.append(dist.all_gather_into_tensor(chunk.reshape(-1), mine.reshape(-1).clone(), group=self.group,
                                                            async_op=True))
-        for h in handles:
-            h.wait()
+        self._ag.append((c * self.Pc, (c + 1) * self.Pc, handles))
+
+    def full_rows(self, name: str) -> torch.Tensor:
+        """This rank's shard of raw group `name` as (global row index tensor, rows) clipped to P (tests)."""
+        idx, parts = [], []
+        for c, (g0, g1) in enumerate(self.pieces):
+            hi = min(g1, self.P)
+            if hi > g0:
+                idx.append(torch.arange(g0, hi))
+                parts.append(self.raw[name][c * self.piece:c * self.piece + hi - g0])
+        if not idx:
+            return torch.zeros(0, dtype=torch.long), self.raw[name][:0]
+        return torch.cat(idx), torch.cat(parts)
 
     def _adam_group(self, p, g, m, v, lr, step):
         if self._adam is not None:

@@ -164,6 +164,13 @@ int lsr_forward_preprocess_views_async(int32_t n_views, const lsr_settings *cons
 int lsr_forward_preprocess_views_split_async(int32_t n_views, int32_t n_ordered, const lsr_settings *const *s,
                                              const lsr_fwd_in *in, lsr_fwd_out *const *out, void *const *geom,
                                              uint32_t *host_counts, lsr_stream_t stream);
+/* The preprocess of lsr_forward_preprocess_views_split_async(n_ordered = 0) for the Gaussians
+ * [row0, row1) only (row0 a multiple of 256): a caller whose inputs arrive in row chunks (the sharded
+ * optimizer's all-gather) preprocesses each chunk as it lands, then orders the views with
+ * lsr_forward_depth_order_views_async once every row [0, P) was preprocessed. */
+int lsr_forward_preprocess_views_rows_async(int32_t n_views, int32_t row0, int32_t row1, const lsr_settings *const *s,
+                                            const lsr_fwd_in *in, lsr_fwd_out *const *out, void *const *geom,
+                                            lsr_stream_t stream);
 /* Depth ordering + instance counts of n_views views whose preprocess already ran (geom[v] as that
  * call left it): one set of sort and scan launches per 8 views; host_counts as above. */
 int lsr_forward_depth_order_views_async(int32_t n_views, const lsr_settings *const *s, const lsr_fwd_in *in,

@@ -41,7 +41,7 @@ def raw_scene(seed=5):
     return sc, raw
 
 
-def run_rank(rank, world, out, mode, steps):
+def run_rank(rank, world, out, mode, steps, chunks=1):
     import torch
     import torch.distributed as dist
 
@@ -67,21 +67,23 @@ def run_rank(rank, world, out, mode, steps):
         up = None
         rm = 1
         if mode == "sharded":
-            up = ShardedAdam(sc, {k: v.cuda() for k, v in raw.items()}, LRS)
-            rm = ShardedAdam.row_multiple(P, world)
+            up = ShardedAdam(sc, {k: v.cuda() for k, v in raw.items()}, LRS, chunks=chunks)
+            rm = ShardedAdam.row_multiple(P, world, chunks=chunks)
         b = GradBucket(P, sc.shs.shape[1], C, "cuda", densify_stats=True, row_multiple=rm)
         step = ViewParallelStep(b, N_VIEWS, update=up)
         render = native_view_renderer(sc, settings, lambda v, c, l, d: (grads[v][0], grads[v][1], None),
                                       overlap="batched", early_views=3)
         for _ in range(steps):
             step.run(render)
+        if up is not None:
+            up.wait_all()                 # the last step's all-gathers (the next step would wait per chunk)
         torch.cuda.synchronize()
         res = dict(world=world, views=list(step.views), radii=b.radii.cpu())
         if mode == "allreduce":
             res["grads"] = {k: (v.cpu().clone() if v is not None else None) for k, v in b.views.items()}
         else:
             res["rows"] = (up.r0, up.r1)
-            res["raw"] = {k: v.cpu().clone() for k, v in up.raw.items()}
+            res["full"] = {k: tuple(x.cpu().clone() for x in up.full_rows(k)) for k in up.raw}
             res["act"] = {k: getattr(sc, k).cpu().clone() for k in ("means3D", "scales", "rotations", "opacities",
                                                                       "shs", "lang")}
         if out:
@@ -92,8 +94,8 @@ def run_rank(rank, world, out, mode, steps):
             dist.destroy_process_group()
 
 
-def _child(rank, world, out, mode, steps):
-    run_rank(rank, world, out, mode, steps)
+def _child(rank, world, out, mode, steps, chunks):
+    run_rank(rank, world, out, mode, steps, chunks)
 
 
 def main():
@@ -102,12 +104,13 @@ def main():
     ap.add_argument("--world", type=int, default=2)
     ap.add_argument("--mode", choices=("allreduce", "sharded"), default="allreduce")
     ap.add_argument("--steps", type=int, default=1)
+    ap.add_argument("--chunks", type=int, default=1)
     a = ap.parse_args()
     if a.world > 1:
         from view_parallel import launch_ranks   # spawns before this process touches the GPU
-        launch_ranks(a.world, _child, (a.out, a.mode, a.steps))
+        launch_ranks(a.world, _child, (a.out, a.mode, a.steps, a.chunks))
     else:
-        run_rank(0, 1, a.out, a.mode, a.steps)
+        run_rank(0, 1, a.out, a.mode, a.steps, a.chunks)
 
 
 if __name__ == "__main__":

@@ -54,10 +54,10 @@ def test_bench_two_ranks_prints_one_line():
     assert line["roofline"]["kernel"] == "render_bwd" and line["cpu_baseline"] is None
 
 
-def _spawn(mode, steps):
+def _spawn(mode, steps, chunks=1):
     d = tempfile.mkdtemp(prefix="lsr_mp_")
     cmd = [sys.executable, os.path.join(HERE, "mp_view_parallel_gpu.py"), "--out", d, "--world", "2",
-           "--mode", mode, "--steps", str(steps)]
+           "--mode", mode, "--steps", str(steps), "--chunks", str(chunks)]
     r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-4000:]
     outs = [torch.load(os.path.join(d, f"rank{k}.pt"), weights_only=True) for k in range(2)]
@@ -87,21 +87,40 @@ def test_two_rank_bucket_equals_one_rank_sum():
     assert torch.equal(outs[0]["radii"], ser["radii"]) and torch.equal(outs[1]["radii"], ser["radii"])
 
 
+def _assemble(outs, k):
+    """[P, ...] rows of raw group k from the ranks' shards (ShardedAdam.full_rows: global row ids, rows)."""
+    rows0 = outs[0]["full"][k][1]
+    got = torch.zeros((mpv.P,) + tuple(rows0.shape[1:]), dtype=rows0.dtype)
+    seen = torch.zeros(mpv.P, dtype=torch.bool)
+    for o in outs:
+        idx, rows = o["full"][k]
+        assert not seen[idx].any()
+        got[idx], seen[idx] = rows, True
+    assert bool(seen.all()), k
+    return got
+
+
 @pytest.mark.timeout(300)
-def test_two_rank_sharded_adam_equals_serial():
+@pytest.mark.parametrize("chunks", [1, 4])
+def test_two_rank_sharded_adam_equals_serial(chunks):
     """Two optimizer steps with ShardedAdam (reduce-scatter by Gaussian rows, lsr_adam_step on each
-    rank's half, all-gather of the activated inputs) against one rank doing every view and row.
-    Both ranks render the same scene afterwards; parameters agree up to the view sums' fp32
-    reassociation (Adam's first step moves a parameter by about lr * sign(g), so a gradient within
-    rounding of zero may move either way: bounded by 2 lr per step)."""
+    rank's shard, all-gather of the activated inputs) against one rank doing every view and row.
+    chunks = 4: the chunk pipeline (each flush chunk's reduce-scatter behind its launch, Adam and the
+    all-gather chunk by chunk, and the second step's batched preprocess launched per row chunk as
+    each chunk's gather lands: lsr_forward_preprocess_views_rows_async).  Both ranks render the same
+    scene afterwards; parameters agree up to the view sums' fp32 reassociation (Adam's first step
+    moves a parameter by about lr * sign(g), so a gradient within rounding of zero may move either
+    way: bounded by 2 lr per step)."""
     steps = 2
     ser = mpv.run_rank(0, 1, None, "sharded", steps)
-    outs = _spawn("sharded", steps)
-    r0, r1 = outs[0]["rows"], outs[1]["rows"]
-    assert r0[0] == 0 and r0[1] == r1[0] and r1[1] == mpv.P
+    outs = _spawn("sharded", steps, chunks)
+    if chunks == 1:
+        r0, r1 = outs[0]["rows"], outs[1]["rows"]
+        assert r0[0] == 0 and r0[1] == r1[0] and r1[1] == mpv.P
     init = mpv.raw_scene()[1]
-    for k, v in ser["raw"].items():
-        got = torch.cat([outs[0]["raw"][k], outs[1]["raw"][k]])
+    for k in ser["full"]:
+        v = _assemble([ser], k)
+        got = _assemble(outs, k)
         assert float((v - init[k]).abs().max()) > 0, k               # the step moved the parameters
         d = (got - v).abs()
         tight = d <= 1e-6 + 1e-5 * v.abs()

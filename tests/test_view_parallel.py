@@ -363,13 +363,14 @@ def test_sharded_adam_single_rank_equals_autograd_and_torch_adam():
     up.step(b)
     for k in raw:
         ref = leaves[k].detach()
-        assert torch.allclose(up.raw[k], ref, rtol=1e-5, atol=1e-6), (k, float((up.raw[k] - ref).abs().max()))
+        got = up.full_rows(k)[1]          # world 1: the shard is every row (padding past P dropped)
+        assert torch.allclose(got, ref, rtol=1e-5, atol=1e-6), (k, float((got - ref).abs().max()))
     # the scene now renders the updated parameters' activations
     assert torch.allclose(sc.scales, torch.exp(leaves["scaling"].detach()), rtol=1e-5)
     assert torch.allclose(sc.opacities, torch.sigmoid(leaves["opacity"].detach()), rtol=1e-5, atol=1e-7)
 
 
-def _sharded_worker(rank, world, port, outdir, steps):
+def _sharded_worker(rank, world, port, outdir, steps, chunks=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -377,19 +378,40 @@ def _sharded_worker(rank, world, port, outdir, steps):
         from view_parallel import ShardedAdam
         sc, raw = _raw_scene()
         _, cams = _scene_and_cams()
-        up = ShardedAdam(sc, raw, LRS_SH, adam=_np_adam)
-        b = GradBucket(P, 16, C, "cpu", densify_stats=True, row_multiple=ShardedAdam.row_multiple(P, world))
+        up = ShardedAdam(sc, raw, LRS_SH, adam=_np_adam, chunks=chunks)
+        b = GradBucket(P, 16, C, "cpu", densify_stats=True,
+                       row_multiple=ShardedAdam.row_multiple(P, world, chunks=chunks))
         step = ViewParallelStep(b, N_VIEWS, update=up)
-        render = oracle_renderer(sc, cams, batched=True)
+        render = oracle_renderer(sc, cams, batched=True, chunked=chunks > 1)
+        issued = []
+        if chunks > 1:   # record the flush's chunk reports: each chunk's reduce-scatter starts behind it
+            on_rows = up.on_rows
+            up.on_rows = lambda bucket, r0, r1: (issued.append((r0, r1, len(up._rs))), on_rows(bucket, r0, r1))
         for _ in range(steps):
             step.run(render)
-        torch.save(dict(raw={k: v.clone() for k, v in up.raw.items()}, rows=(up.r0, up.r1),
+        full = {k: up.full_rows(k) for k in up.raw}
+        torch.save(dict(raw={k: v.clone() for k, v in up.raw.items()}, rows=(up.r0, up.r1), issued=issued,
+                        full={k: (i.clone(), r.clone()) for k, (i, r) in full.items()},
                         act={k: getattr(sc, k).clone() for k in ("means3D", "scales", "rotations", "opacities", "shs",
                                                                   "lang")},
                         radii=b.radii.clone()), os.path.join(outdir, f"rank{rank}.pt"))
     finally:
         if world > 1:
             dist.destroy_process_group()
+
+
+def _assemble(outs, k):
+    """The full [P, ...] rows of raw group k from the ranks' shards (ShardedAdam.full_rows)."""
+    idx0, rows0 = outs[0]["full"][k]
+    got = torch.zeros((P,) + tuple(rows0.shape[1:]), dtype=rows0.dtype)
+    seen = torch.zeros(P, dtype=torch.bool)
+    for o in outs:
+        idx, rows = o["full"][k]
+        assert not seen[idx].any()
+        got[idx] = rows
+        seen[idx] = True
+    assert bool(seen.all()), k                                          # the shards partition the rows
+    return got
 
 
 def test_sharded_step_two_ranks_equals_serial():
@@ -403,8 +425,9 @@ def test_sharded_step_two_ranks_equals_serial():
         mp.spawn(_sharded_worker, args=(2, _free_port(), d, 2), nprocs=2, join=True)
         outs = [torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(2)]
     assert outs[0]["rows"][1] == outs[1]["rows"][0] and outs[1]["rows"][1] == P and outs[0]["rows"][0] == 0
-    for k, v in ser["raw"].items():
-        got = torch.cat([outs[0]["raw"][k], outs[1]["raw"][k]])
+    for k in ser["raw"]:
+        v = _assemble([ser], k)
+        got = _assemble(outs, k)
         moved = (v - _raw_scene()[1][k]).abs().max()
         assert float(moved) > 0, k
         assert torch.allclose(got, v, rtol=1e-5, atol=1e-6), (k, float((got - v).abs().max()))
@@ -430,3 +453,26 @@ def test_sharded_adam_schedule_and_field_guard():
     sc2.deformation = object()
     with pytest.raises(ValueError, match="deformation field"):
         ShardedAdam(sc2, raw2, LRS_SH, adam=_np_adam)
+
+
+def test_sharded_chunked_pipeline_two_ranks_equals_serial():
+    """ShardedAdam(chunks=4): the shard is one piece per row chunk, the flush reports each chunk and that
+    chunk's reduce-scatter starts behind it, Adam runs chunk by chunk and each chunk's all-gather is
+    issued as soon as its rows are updated.  Two steps at world size 2 against the serial step
+    (world 1, one chunk): parameters and activated inputs agree up to the view sums' fp32
+    reassociation; every rank renders the same scene."""
+    with tempfile.TemporaryDirectory() as d:
+        _sharded_worker(0, 1, 0, d, 2)
+        ser = torch.load(os.path.join(d, "rank0.pt"), weights_only=True)
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_sharded_worker, args=(2, _free_port(), d, 2, 4), nprocs=2, join=True)
+        outs = [torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(2)]
+    for o in outs:   # 3 chunks hold rows (P = 1500 of 2048 padded rows), reported in order, each issued once
+        assert [(r0, r1) for r0, r1, _ in o["issued"][:3]] == [(0, 512), (512, 1024), (1024, 1500)]
+    for k in ser["raw"]:
+        v, got = _assemble([ser], k), _assemble(outs, k)
+        assert torch.allclose(got, v, rtol=1e-5, atol=1e-6), (k, float((got - v).abs().max()))
+    for k, v in ser["act"].items():
+        assert torch.equal(outs[0]["act"][k], outs[1]["act"][k]), k
+        assert torch.allclose(outs[0]["act"][k], v, rtol=1e-5, atol=1e-6), k
+    assert torch.equal(outs[0]["radii"], ser["radii"])
