@@ -3,7 +3,7 @@
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 VARIANTS="${VARIANTS:-slp slp_pad1 slp_pad2 slp_wz}" RACE_R=${RACE_R:-6} bash tools/gpu_deform_race.sh; echo "race rc=$?"
-timeout -k 10 1500 python -u -m pytest ${TESTS:-tests/test_multirank_gpu.py tests/test_checkpoint_gpu.py tests/test_deform_gpu.py tests/test_deform_lds_poison_gpu.py tests/test_train_step_gpu.py tests/test_view_parallel_gpu.py tests/test_abi.py} \
+timeout -k 10 780 python -u -m pytest ${TESTS:-tests/test_multirank_gpu.py tests/test_checkpoint_gpu.py tests/test_deform_gpu.py tests/test_deform_lds_poison_gpu.py tests/test_train_step_gpu.py tests/test_view_parallel_gpu.py tests/test_abi.py} \
     -m "gpu or not gpu" -v --timeout 420 --timeout-method thread -p no:cacheprovider > gpurun_out/r5d_tests.log 2>&1; rc=$?
 grep -E "PASSED|FAILED|ERROR|passed|failed" gpurun_out/r5d_tests.log | tail -60
 grep -E "^E " gpurun_out/r5d_tests.log | head -30
