@@ -77,7 +77,10 @@ __device__ unsigned long long g_fwd_stamps[8];
 // image, entries of the group, while the wave runs) and the pairs that blend, summed into
 // g_fwd_count (lsr_debug_fwd_count): how much of the per-pair work contributes.
 #ifdef LSR_FWD_COUNT
-__device__ unsigned long long g_fwd_count[3];
+// [0] pairs evaluated, [1] pairs blended, [2] waves, [3] compacted entries the waves processed, [4] of
+// those, entries that no pixel of the quadrant blends placed BEFORE the quadrant's last blending entry
+// (what the backward replays and an exact per-(entry, quadrant) activity bit would let it skip)
+__device__ unsigned long long g_fwd_count[5];
 #endif
 
 #ifndef LSR_FWD_WAVES
@@ -131,7 +134,7 @@ k_render_fwd_wave_mfma(RenderFwdBatch ab) {
         for (int nb = 0; nb < 4; ++nb) L[mb][nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     bool done = !inside;
 #ifdef LSR_FWD_COUNT
-    uint32_t c_eval = 0, c_act = 0;
+    uint32_t c_eval = 0, c_act = 0, c_ent = 0, c_inact_run = 0, c_inact_before = 0;
 #endif
 
     uint32_t pos = range.x;  // list entries [pos, range.y) not yet scanned
@@ -202,6 +205,11 @@ k_render_fwd_wave_mfma(RenderFwdBatch ab) {
 #ifdef LSR_FWD_COUNT
                     c_eval += (inside && e < cnt) ? 1u : 0u;
                     c_act += blend ? 1u : 0u;
+                    if (e < cnt) {   // wave-uniform
+                        ++c_ent;
+                        if (__ballot(blend) != 0) { c_inact_before += c_inact_run; c_inact_run = 0; }
+                        else ++c_inact_run;
+                    }
 #endif
                     T = blend ? test_T : T;
                     last = blend ? s_k[e] : last;   // s_k holds the list position + 1
@@ -333,6 +341,8 @@ k_render_fwd_wave_mfma(RenderFwdBatch ab) {
             atomicAdd(&g_fwd_count[0], ve);
             atomicAdd(&g_fwd_count[1], va);
             atomicAdd(&g_fwd_count[2], 1ull);
+            atomicAdd(&g_fwd_count[3], (unsigned long long)c_ent);
+            atomicAdd(&g_fwd_count[4], (unsigned long long)c_inact_before);
         }
     }
 #endif
@@ -416,9 +426,9 @@ void launch_render_fwd_wave_mfma_views(const RenderFwdArgs* a, int n, hipStream_
 }  // namespace lsr
 
 #ifdef LSR_FWD_COUNT
-extern "C" int lsr_debug_fwd_count(unsigned long long* out3) {
-    if (hipMemcpyFromSymbol(out3, HIP_SYMBOL(lsr::g_fwd_count), 3 * sizeof(unsigned long long)) != hipSuccess) return 2;
-    unsigned long long z[3] = {};
+extern "C" int lsr_debug_fwd_count(unsigned long long* out5) {
+    if (hipMemcpyFromSymbol(out5, HIP_SYMBOL(lsr::g_fwd_count), 5 * sizeof(unsigned long long)) != hipSuccess) return 2;
+    unsigned long long z[5] = {};
     return hipMemcpyToSymbol(HIP_SYMBOL(lsr::g_fwd_count), z, sizeof(z)) == hipSuccess ? 0 : 2;
 }
 #endif
