@@ -146,11 +146,29 @@ __device__ __forceinline__ Tap tap_of(const DeformArgs& a, int pi, int ci, const
     t.fx = ix - (float)t.x0; t.fy = iy - (float)t.y0;
     return t;
 }
+#ifdef LSR_FEAT_SCALAR
+// Diagnostic build (tools/deform_slp_bisect.sh feat_scalar): the HexPlane product's arithmetic as
+// scalar VALU instructions the SLP vectorizer cannot pair (same IEEE operations, same bits), so a
+// build with SLP on differs from the shipped one only outside features_to_lds.
+__device__ __forceinline__ float smul(float x, float y) { float r; asm volatile("v_mul_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y)); return r; }
+__device__ __forceinline__ float sadd(float x, float y) { float r; asm volatile("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y)); return r; }
+#endif
 __device__ __forceinline__ float4 sample4(const DeformArgs& a, int pi, const Tap& t, int q) {
     const int W = a.pw[pi];
     const float4* pl = reinterpret_cast<const float4*>(a.planes + a.poff[pi]) + q;
     const float4 v00 = pl[(t.y0 * W + t.x0) * 4], v01 = pl[(t.y0 * W + t.x1) * 4];
     const float4 v10 = pl[(t.y1 * W + t.x0) * 4], v11 = pl[(t.y1 * W + t.x1) * 4];
+#ifdef LSR_FEAT_SCALAR
+    {
+        const float ufx = sadd(1.0f, -t.fx), ufy = sadd(1.0f, -t.fy);
+        const float w00 = smul(ufx, ufy), w01 = smul(t.fx, ufy), w10 = smul(ufx, t.fy), w11 = smul(t.fx, t.fy);
+        auto c = [&](float a0, float a1, float a2, float a3) {
+            return sadd(sadd(sadd(smul(a0, w00), smul(a1, w01)), smul(a2, w10)), smul(a3, w11));
+        };
+        return make_float4(c(v00.x, v01.x, v10.x, v11.x), c(v00.y, v01.y, v10.y, v11.y), c(v00.z, v01.z, v10.z, v11.z),
+                           c(v00.w, v01.w, v10.w, v11.w));
+    }
+#endif
     const float w00 = (1.0f - t.fx) * (1.0f - t.fy), w01 = t.fx * (1.0f - t.fy), w10 = (1.0f - t.fx) * t.fy,
                 w11 = t.fx * t.fy;
     return make_float4(v00.x * w00 + v01.x * w01 + v10.x * w10 + v11.x * w11,
@@ -174,7 +192,11 @@ __device__ __forceinline__ void features_to_lds(const DeformArgs& a, int g0, __b
         for (int ci = 0; ci < 6; ++ci) {
             const int pi = 6 * s + ci;
             const float4 v = sample4(a, pi, tap_of(a, pi, ci, crd), q);
+#ifdef LSR_FEAT_SCALAR
+            prod.x = smul(prod.x, v.x); prod.y = smul(prod.y, v.y); prod.z = smul(prod.z, v.z); prod.w = smul(prod.w, v.w);
+#else
             prod.x *= v.x; prod.y *= v.y; prod.z *= v.z; prod.w *= v.w;
+#endif
 #ifdef LSR_DEFORM_FEAT_WAIT
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 #endif

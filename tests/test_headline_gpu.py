@@ -75,11 +75,21 @@ def test_bench_pipeline_matches_oracle_at_headline_size():
     render_view.flush, render_view.begin_step, render_view.end_step = render.flush, render.begin_step, render.end_step
     bucket = GradBucket(P, scene.shs.shape[1], C, "cuda", densify_stats=True)
     step = ViewParallelStep(bucket, V)
+    flats = []
     for _ in range(2):                      # the second step runs on warm streams / workspaces
         bucket.flat.fill_(float("nan"))     # every field is written or zeroed by the step
         step.run(render_view)
+        flats.append(bucket.flat.clone())
     torch.cuda.synchronize()
     assert not torch.isnan(bucket.flat).any()
+    # the backward repeats up to float-atomic reordering (a lost low half of a packed-fp32 result in
+    # any compositor lane, DESIGN.md 4.5, would move a gradient by far more than that): every field
+    # of the two steps' buckets within 1e-6 of its largest magnitude
+    for name, _ in FIELDS:
+        f0, f1 = bucket.ranges[name]
+        a_, b_ = flats[0][f0:f1], flats[1][f0:f1]
+        scale = float(a_.abs().max())
+        assert float((a_ - b_).abs().max()) <= 1e-6 * scale, (name, float((a_ - b_).abs().max()), scale)
     assert len(render.pending) == 0
     # the forward is deterministic: both steps' images repeat bit for bit (a race or a lost
     # hazard in any compositor shows here first; see DESIGN.md 4.5 on the packed-fp32 build flag)
