@@ -256,7 +256,7 @@ void preprocess_view(lsr::PreprocessView& v, const lsr_settings* s, const Geom& 
     v.conic_o = g.conic_o; v.rgbd = g.rgbd; v.clamped = g.clamped;
     v.order = g.val_a;
     v.rank_counts = g.counts;
-    v.acc = nullptr;   // zeroed by the forward compositor instead (zero_acc_share): the preprocess is HBM-bound
+    v.acc = g.acc;
     v.clear.p[0] = g.total;
     v.clear.n[0] = 4;
 }
@@ -618,7 +618,6 @@ int lsr_forward_composite_views(int32_t n_views, const lsr_settings* const* s, c
             a.tile_max_contrib = m.tile_max; a.tile_order = m.tile_order;
             a.out_color = out[v]->out_color; a.out_lang = out[v]->out_language_feature;
             a.out_depth = out[v]->out_depth;
-            a.acc_zero = g.acc; a.acc_rows = P;   // the split backward's accumulator rows (not the preprocess's job)
             if (C > 0 && !s[v]->include_feature)
                 LSR_HIP(hipMemsetAsync(out[v]->out_language_feature, 0, sizeof(float) * (size_t)C * W * H, st));
         }
@@ -767,7 +766,7 @@ int lsr_backward_composite_views(int32_t n_views, const lsr_settings* const* s, 
     for (int v = 0; v < n_views; ++v) {
         const size_t K = (size_t)num_rendered[v];
         if (K == 0) continue;   // nothing listed: no compositor work
-        Geom g = carve_geom(geom[v], (size_t)P, nullptr);   // g.acc: zeroed by the view's forward compositor (zero_acc_share)
+        Geom g = carve_geom(geom[v], (size_t)P, nullptr);   // g.acc: rows of listed Gaussians zeroed by the preprocess
         Binning b = carve_binning(const_cast<void*>(binning[v]), K, nullptr);
         Img m = carve_img(const_cast<void*>(img[v]), W, H, nullptr);
         lsr::RenderBwdArgs& a = r[nr++];

@@ -81,8 +81,7 @@ struct PreprocessView {
     uint32_t* order;  // if set: order[i] = i (the depth sort's initial values)
     uint32_t* rank_counts;   // if set: zeroed (per depth rank instance counts; the sort's last
                              // pass fills the visible ranks, the culled ones stay 0)
-    float4* acc;      // if set: [P, ACC_PITCH / 4] backward accumulators, zeroed for visible rows (the
-                      // batched path leaves it null: its forward compositors zero them, zero_acc_share)
+    float4* acc;      // if set: [P, ACC_PITCH / 4] backward accumulators, zeroed for visible rows
     ClearList clear;  // zeroed on the side (sort workspace, counters)
 };
 // Preprocess of nv <= LSR_MAX_VIEWS cameras over the same Gaussians: with nv > 1 a Gaussian's
@@ -187,21 +186,7 @@ struct RenderFwdArgs {
     float* out_color;
     float* out_lang;
     float* out_depth;
-    float4* acc_zero;             // [acc_rows, ACC_PITCH / 4]: the split backward's accumulator rows,
-    int acc_rows;                 // zeroed here (the compositor is VALU-bound: HBM idles) or null
 };
-
-// The split backward's per-Gaussian accumulator rows, zeroed by the forward compositor that precedes
-// every compositor backward of the view: block b of nb stores zeros over its contiguous share of
-// the rows (coalesced float4 runs, issued as the wave's last memory operations so that no load of
-// the wave waits behind them).  Every row: a superset of the rows the backward's atomics reach.
-__device__ __forceinline__ void zero_acc_share(float4* acc, int rows, int b, int nb) {
-    if (!acc || rows <= 0) return;
-    const uint32_t total = (uint32_t)rows * (uint32_t)(ACC_PITCH / 4);   // < 2^30 (P < 2^28)
-    const uint32_t per = (total + (uint32_t)nb - 1u) / (uint32_t)nb;
-    const uint32_t lo = (uint32_t)b * per, hi = min(total, lo + per);
-    for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) acc[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-}
 
 struct RenderBwdArgs {
     int W, H, grid_x, grid_y, C, include_feature;

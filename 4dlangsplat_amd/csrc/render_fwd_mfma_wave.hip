@@ -105,10 +105,7 @@ k_render_fwd_wave_mfma(RenderFwdBatch ab) {
 
     const int b = blockIdx.x;
     const int slot = (b >> 5) * 8 + (b & 7), quad = (b >> 3) & 3;   // a slot's 4 quadrants: one XCD
-    if (slot >= a.grid_x * a.grid_y) {
-        zero_acc_share(a.acc_zero, a.acc_rows, b, gridDim.x);
-        return;
-    }
+    if (slot >= a.grid_x * a.grid_y) return;
     // Slots walk the tiles column by column (no order array): measured 0.250 -> 0.232 ms against
     // raster order on the headline scene (either column direction; a per-quadrant makespan
     // simulation from the frame's composited-entry counts also favours it, 1.20 vs 1.26 of ideal).
@@ -387,7 +384,6 @@ k_render_fwd_wave_mfma(RenderFwdBatch ab) {
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
     if (lane == 0 && m > 0) atomicMax(a.tile_max_contrib + tile, m);
-    zero_acc_share(a.acc_zero, a.acc_rows, b, gridDim.x);
 }
 
 // lsr_language_split: per Gaussian the 32 channels' bf16 hi then lo (split_bf16), one thread per

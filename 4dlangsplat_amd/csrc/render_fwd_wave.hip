@@ -34,10 +34,7 @@ __global__ void __launch_bounds__(64) k_render_fwd_wave(RenderFwdBatch ab) {
 
     const int b = blockIdx.x;
     const int slot = (b >> 5) * 8 + (b & 7), quad = (b >> 3) & 3;   // a slot's 4 quadrants: one XCD
-    if (slot >= a.grid_x * a.grid_y) {
-        zero_acc_share(a.acc_zero, a.acc_rows, b, gridDim.x);
-        return;
-    }
+    if (slot >= a.grid_x * a.grid_y) return;
     // column by column, as k_render_fwd_wave_mfma (measured faster than raster order there)
     const int tile = a.tile_order ? (int)a.tile_order[slot] : (slot % a.grid_y) * a.grid_x + slot / a.grid_y;
     const int lane = threadIdx.x;
@@ -199,7 +196,6 @@ __global__ void __launch_bounds__(64) k_render_fwd_wave(RenderFwdBatch ab) {
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
     if (lane == 0 && m > 0) atomicMax(a.tile_max_contrib + tile, m);
-    zero_acc_share(a.acc_zero, a.acc_rows, b, gridDim.x);
 }
 
 template <int CPAD>
