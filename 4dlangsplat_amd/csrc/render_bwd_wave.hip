@@ -450,6 +450,29 @@ k_render_bwd_wave(RenderBwdBatch ab) {
         } else if (e0 > 0) {
             pin = ld_pair(e0);
         }
+#ifdef LSR_BWD_SCALAR
+        // A/B variant: the pair's alpha / dot arithmetic as scalar VALU (no packed-fp32 hazard nops
+        // between the dependent steps of the exp chain; build with -fno-slp-vectorize)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int e = e0 + u;
+            const float Xu = u ? pin.X.y : pin.X.x, Yu = u ? pin.Y.y : pin.Y.x;
+            const float power = gauss_power(u ? pin.A.y : pin.A.x, u ? pin.B.y : pin.B.x, u ? pin.Cc.y : pin.Cc.x,
+                                            Xu - pxf, Yu - pyf);
+            const float ge = expf_repro(power);
+            const float al = fminf(0.99f, (u ? pin.O.y : pin.O.x) * ge);
+            float d = (u ? pin.R.y : pin.R.x) * g0;
+            d = __builtin_fmaf(u ? pin.Gc.y : pin.Gc.x, g1, d);
+            d = __builtin_fmaf(u ? pin.Bc.y : pin.Bc.x, g2, d);
+            d = __builtin_fmaf(u ? pin.D.y : pin.D.x, gD, d);
+            act[u] = (u ? pin.kk.y : pin.kk.x) < last_contributor && power <= 0.0f && al >= 1.0f / 255.0f;
+            alv[u] = act[u] ? al : 0.0f;
+            Gv[u] = ge;
+            romv[u] = __builtin_amdgcn_rcpf(1.0f - alv[u]);
+            dotv[u] = d + S[e];
+        }
+        if (false)
+#endif
         {
             const lsr_f2 X = pin.X, Y = pin.Y, A = pin.A, B = pin.B, Cc = pin.Cc, O = pin.O;
             const uint2 kk = pin.kk;

@@ -177,6 +177,15 @@ k_render_fwd_wave_mfma(RenderFwdBatch ab) {
             if (8 * o < cnt && !__all(done)) {                    // wave-uniform
                 float al[8];
                 bool ok[8];
+#ifdef LSR_FWD_SCALAR
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {   // A/B variant: scalar VALU (build with -fno-slp-vectorize)
+                    const int e = 8 * o + u;
+                    const float pw = gauss_power(s_A[e], s_B[e], s_C[e], s_X[e] - pxf, s_Y[e] - pyf);
+                    al[u] = fminf(0.99f, s_O[e] * expf_repro(pw));
+                    ok[u] = pw <= 0.0f && al[u] >= 1.0f / 255.0f;
+                }
+#else
 #pragma unroll
                 for (int u = 0; u < 8; u += 2) {   // two entries per packed-fp32 operation
                     const int e = 8 * o + u;
@@ -190,6 +199,7 @@ k_render_fwd_wave_mfma(RenderFwdBatch ab) {
                     ok[u] = pw.x <= 0.0f && al[u] >= 1.0f / 255.0f;        // padding entries: O = 0
                     ok[u + 1] = pw.y <= 0.0f && al[u + 1] >= 1.0f / 255.0f;
                 }
+#endif
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
                     const int e = 8 * o + u;
