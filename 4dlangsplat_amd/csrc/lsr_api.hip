@@ -156,6 +156,26 @@ Binning carve_binning(void* base, size_t K, size_t* bytes) {
     return b;
 }
 
+// the tile-bucket binning's workspace: the sort path's layout (its point list buffer is where the
+// compositors read; key_a..key_b hold the 64-bit bucket keys: 8K bytes <= 2 al(4K)), then the
+// per-block tile count table and the long buckets' merge workspace
+struct BinningTb {
+    Binning b;
+    uint32_t* table;
+    uint64_t* tmp;
+};
+BinningTb carve_binning_tb(void* base, size_t K, size_t P, size_t ntiles, size_t* bytes) {
+    size_t head;
+    BinningTb t;
+    t.b = carve_binning(base, K, &head);
+    Carver c(base);
+    c.off = head;
+    t.table = c.take<uint32_t>((size_t)lsr::tb_blocks((int)P) * ntiles);
+    t.tmp = c.take<uint64_t>(K);
+    if (bytes) *bytes = c.off;
+    return t;
+}
+
 struct Img {
     uint2* ranges;
     uint32_t* tile_max;
@@ -283,6 +303,13 @@ int64_t lsr_geom_bytes(int32_t P) {
 int64_t lsr_binning_bytes(int64_t K) {
     size_t b;
     carve_binning(nullptr, (size_t)(K > 0 ? K : 1), &b);
+    return (int64_t)b;
+}
+int64_t lsr_binning_bytes_tb(int64_t K, int32_t P, int32_t W, int32_t H) {
+    if (W <= 0 || H <= 0 || P < 0) return -1;
+    const size_t ntiles = (size_t)((W + LSR_TILE_X - 1) / LSR_TILE_X) * ((H + LSR_TILE_Y - 1) / LSR_TILE_Y);
+    size_t b;
+    carve_binning_tb(nullptr, (size_t)(K > 0 ? K : 1), (size_t)(P > 0 ? P : 1), ntiles, &b);
     return (int64_t)b;
 }
 int64_t lsr_img_bytes(int32_t W, int32_t H) {
@@ -440,16 +467,18 @@ int lsr_forward_preprocess_views_split_async(int32_t n_views, int32_t n_ordered,
     return n_ordered > 0 ? depth_order_views(n_ordered, s, in, geom, host_counts, st) : LSR_OK;
 }
 
-int lsr_forward_preprocess_views_rows_async(int32_t n_views, int32_t row0, int32_t row1, const lsr_settings* const* s,
-                                            const lsr_fwd_in* in, lsr_fwd_out* const* out, void* const* geom,
-                                            lsr_stream_t stream) {
+namespace {
+// preprocess of rows [row0, row1) of n_views views, one launch per 8 views; counts_tiles: each
+// view's counts array gets the per-Gaussian instance counts by id (the tile-bucket binning's input)
+// instead of zeros (the depth sort's last pass fills it by depth rank)
+int preprocess_rows(int32_t n_views, int32_t row0, int32_t row1, int counts_tiles, const lsr_settings* const* s,
+                    const lsr_fwd_in* in, lsr_fwd_out* const* out, void* const* geom, hipStream_t st) {
     int rc = check_views(n_views, s, in, geom);
     if (rc) return rc;
     if (!out || row0 < 0 || row1 < row0 || row1 > in->P || row0 % 256 != 0)
         return fail(LSR_EINVAL, "0 <= row0 <= row1 <= P with row0 a multiple of 256, and the outputs are required");
     for (int v = 0; v < n_views; ++v)
         if (!out[v] || (!out[v]->radii && in->P > 0)) return fail(LSR_EINVAL, "radii output is required");
-    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const int P = in->P;
     if (row1 == row0) return LSR_OK;
     for (int v0 = 0; v0 < n_views; v0 += lsr::LSR_MAX_VIEWS) {
@@ -459,6 +488,7 @@ int lsr_forward_preprocess_views_rows_async(int32_t n_views, int32_t row0, int32
         a.nv = nv;
         a.row0 = row0;
         a.P = row1;   // the launch's bound (every per-Gaussian array is indexed by the global row)
+        a.counts_tiles = counts_tiles;
         for (int k = 0; k < nv; ++k) {
             Geom g = carve_geom(geom[v0 + k], (size_t)P, nullptr);
             preprocess_view(a.v[k], s[v0 + k], g, out[v0 + k]->radii);
@@ -470,6 +500,69 @@ int lsr_forward_preprocess_views_rows_async(int32_t n_views, int32_t row0, int32
         LSR_LAUNCHED("preprocess", st, s[v0]->debug);
     }
     return LSR_OK;
+}
+
+// the tile-bucket binning's instance count: the exclusive scan of the per-Gaussian counts in id
+// order (no depth sort), one launch set per 8 views; K to the page-locked host_counts as above
+int instance_scan_views(int32_t n_views, const lsr_fwd_in* in, void* const* geom, uint32_t* host_counts,
+                        hipStream_t st, bool debug) {
+    const int P = in->P;
+    uint32_t* mapped = nullptr;
+    {
+        void* dptr = nullptr;
+        if (hipHostGetDevicePointer(&dptr, host_counts, 0) == hipSuccess && dptr) mapped = static_cast<uint32_t*>(dptr);
+        else (void)hipGetLastError();
+    }
+    for (int v0 = 0; v0 < n_views; v0 += lsr::LSR_MAX_VIEWS) {
+        const int nv = std::min(n_views - v0, lsr::LSR_MAX_VIEWS);
+        lsr::ScanSeg sc[lsr::LSR_MAX_VIEWS] = {};
+        for (int k = 0; k < nv; ++k) {
+            Geom g = carve_geom(geom[v0 + k], (size_t)P, nullptr);
+            sc[k] = lsr::ScanSeg{g.counts, g.offsets, g.total, reinterpret_cast<uint32_t*>(g.scan_tmp), (size_t)P};
+            if (mapped) {
+                sc[k].host_total = mapped + 2 * (v0 + k);
+                host_counts[2 * (v0 + k) + 1] = 0;
+            }
+        }
+        uint32_t wrote;
+        {
+            PhaseTimer t(LSR_PHASE_INSTANCE_SCAN, st);
+            wrote = lsr::exclusive_scan_batch(sc, nv, st);
+        }
+        LSR_LAUNCHED("instance scan", st, debug);
+        for (int k = 0; k < nv; ++k) {
+            if ((wrote >> k) & 1u) continue;
+            Geom g = carve_geom(geom[v0 + k], (size_t)P, nullptr);
+            LSR_HIP(hipMemcpyAsync(host_counts + 2 * (v0 + k), g.total, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                   st));
+        }
+    }
+    return LSR_OK;
+}
+}  // namespace
+
+int lsr_forward_preprocess_views_rows_async(int32_t n_views, int32_t row0, int32_t row1, const lsr_settings* const* s,
+                                            const lsr_fwd_in* in, lsr_fwd_out* const* out, void* const* geom,
+                                            lsr_stream_t stream) {
+    return preprocess_rows(n_views, row0, row1, 0, s, in, out, geom, reinterpret_cast<hipStream_t>(stream));
+}
+
+int lsr_forward_preprocess_views_tb_async(int32_t n_views, int32_t row0, int32_t row1, const lsr_settings* const* s,
+                                          const lsr_fwd_in* in, lsr_fwd_out* const* out, void* const* geom,
+                                          lsr_stream_t stream) {
+    return preprocess_rows(n_views, row0, row1, 1, s, in, out, geom, reinterpret_cast<hipStream_t>(stream));
+}
+
+int lsr_forward_instance_scan_views_async(int32_t n_views, const lsr_settings* const* s, const lsr_fwd_in* in,
+                                          void* const* geom, uint32_t* host_counts, lsr_stream_t stream) {
+    int rc = check_views(n_views, s, in, geom);
+    if (rc) return rc;
+    if (!host_counts) return fail(LSR_EINVAL, "host_counts is required");
+    if (in->P == 0) {
+        for (int v = 0; v < 2 * n_views; ++v) host_counts[v] = 0;
+        return LSR_OK;
+    }
+    return instance_scan_views(n_views, in, geom, host_counts, reinterpret_cast<hipStream_t>(stream), s[0]->debug);
 }
 
 int lsr_forward_depth_order_views_async(int32_t n_views, const lsr_settings* const* s, const lsr_fwd_in* in,
@@ -570,6 +663,63 @@ int lsr_forward_binning_views(int32_t n_views, const lsr_settings* const* s, con
                 return fail(LSR_EHIP, "internal: tile sort batch or parity");
         }
         LSR_LAUNCHED("tile sort", st, s[0]->debug);
+    }
+    return LSR_OK;
+}
+
+int lsr_forward_binning_views_tb(int32_t n_views, const lsr_settings* const* s, const lsr_fwd_in* in, void* const* geom,
+                                 void* const* binning, void* const* img, const int64_t* num_rendered,
+                                 lsr_stream_t stream) {
+    if (n_views < 1 || !s || !geom || !binning || !img || !num_rendered)
+        return fail(LSR_EINVAL, "n_views >= 1 and the per-view arrays are required");
+    for (int v = 0; v < n_views; ++v) {
+        int rc = check_common(s[v], in);
+        if (rc) return rc;
+        if (s[v]->image_width != s[0]->image_width || s[v]->image_height != s[0]->image_height)
+            return fail(LSR_EINVAL, "batched views must share the image size");
+        if (!geom[v] || !img[v] || (num_rendered[v] > 0 && !binning[v])) return fail(LSR_EINVAL, "workspaces are required");
+    }
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int P = in->P, W = s[0]->image_width, H = s[0]->image_height;
+    const int gx = (W + LSR_TILE_X - 1) / LSR_TILE_X, gy = (H + LSR_TILE_Y - 1) / LSR_TILE_Y;
+    const size_t ntiles = (size_t)gx * gy;
+    // the per-block tile histograms live in LDS (4 bytes a tile)
+    if (ntiles > 12288)
+        return fail(LSR_EINVAL, "tile-bucket binning: more than 12288 tiles (use lsr_forward_binning_views)");
+    for (int v0 = 0; v0 < n_views; v0 += lsr::LSR_MAX_VIEWS) {
+        const int nv = std::min(n_views - v0, lsr::LSR_MAX_VIEWS);
+        lsr::TbBatch tb{};
+        tb.P = P; tb.grid_x = gx; tb.grid_y = gy; tb.W = W; tb.H = H; tb.ntiles = (int)ntiles;
+        int ne = 0;
+        for (int k = 0; k < nv; ++k) {
+            const int v = v0 + k;
+            const size_t K = (size_t)num_rendered[v];
+            Geom g = carve_geom(geom[v], (size_t)(P > 0 ? P : 1), nullptr);
+            Img m = carve_img(img[v], W, H, nullptr);
+            if (K == 0) {
+                LSR_HIP(hipMemsetAsync(m.ranges, 0, sizeof(uint2) * ntiles, st));
+                LSR_HIP(hipMemsetAsync(m.tile_max, 0, sizeof(uint32_t) * ntiles, st));
+                continue;
+            }
+            BinningTb b = carve_binning_tb(binning[v], K, (size_t)P, ntiles, nullptr);
+            lsr::TbView& t = tb.v[ne++];
+            t.counts = g.counts; t.offsets = g.offsets; t.rect = g.rect; t.xy = g.xy; t.conic_o = g.conic_o;
+            t.depth = g.key_a;
+            t.table = b.table;
+            t.tile_total = m.tile_order;   // backward scratch, written by the backward's tile order
+            t.tile_start = m.tile_max;     // zeroed again by the bucket sort
+            t.ranges = m.ranges;
+            t.keys = reinterpret_cast<uint64_t*>(b.b.key_a);
+            t.tmp = b.tmp;
+            t.words = tile_sort_in_b((int)ntiles) ? b.b.val_b : b.b.val_a;   // where the compositors read
+            t.tile_max = m.tile_max;
+        }
+        if (ne == 0) continue;
+        {
+            PhaseTimer t(LSR_PHASE_TILE_SORT, st);
+            lsr::launch_tile_bucket_binning(tb, ne, st);
+        }
+        LSR_LAUNCHED("tile-bucket binning", st, s[0]->debug);
     }
     return LSR_OK;
 }

@@ -89,6 +89,7 @@ struct PreprocessView {
 struct PreprocessArgs {
     int P, M, deg, W, H, grid_x, grid_y, nv;
     int row0;   // the launch covers Gaussians [row0, P) (a row chunk; a multiple of 256), usually 0
+    int counts_tiles;   // 1: rank_counts[i] = tiles[i] (the tile-bucket binning's index-order counts)
     float scale_modifier;
     const float* means3D;
     const float* scales;
@@ -470,7 +471,30 @@ struct EmitBatch {
 void launch_emit_instances(const EmitBatch& eb, int nv, hipStream_t st);
 void launch_scatter_inst_off(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* counts,
                              uint32_t* inst_off, hipStream_t st);
-// Per-tile [start, end) of a batch of tile-sorted instance lists (one grid row per list).
+// Tile-bucket binning (tilebin.hip): the instances of Gaussians in index order go straight to their
+// tile's bucket; each bucket is sorted by (depth, id) in LDS.  One grid row per view.
+struct TbView {
+    const uint32_t* counts;    // [P] instances per Gaussian (index order)
+    const uint32_t* offsets;   // [P] their exclusive scan
+    const uint2* rect;         // [P] binning rectangles by id
+    const float2* xy;
+    const float4* conic_o;
+    const uint32_t* depth;     // [P] depth key bits by id
+    uint32_t* table;           // [tb_blocks(P), ntiles] per-block tile counts, then their column scans
+    uint32_t* tile_total;      // [ntiles]
+    uint32_t* tile_start;      // [ntiles] (may alias tile_max: the sort zeroes it after the scatter)
+    uint2* ranges;             // [ntiles] (empty tiles: (0, 0))
+    uint64_t* keys;            // [K] depth bits << 32 | id << 4 | quadrant bits, bucketed by tile
+    uint64_t* tmp;             // [K] merge workspace of buckets longer than one LDS sort
+    uint32_t* words;           // [K] the point list (id | quadrant bits << PL_QUAD_SHIFT)
+    uint32_t* tile_max;        // [ntiles] zeroed
+};
+struct TbBatch {
+    int P, grid_x, grid_y, W, H, ntiles;
+    TbView v[LSR_MAX_VIEWS];
+};
+int tb_blocks(int P);   // rows of TbView::table
+void launch_tile_bucket_binning(const TbBatch& tb, int nv, hipStream_t st);
 
 // compositing (render_fwd_wave.hip / render_bwd.hip)
 void launch_render_bwd(const RenderBwdArgs& a, hipStream_t st);

@@ -294,6 +294,7 @@ __device__ __forceinline__ bool preprocess_one(const PreprocessArgs& a, const Pr
     // instances it will emit: a small rectangle's tiles with a reachable quadrant (none: the
     // Gaussian blends no pixel and is not listed -- its gradient is exactly zero)
     v.tiles[i] = rect_count(rc);
+    if (v.rank_counts && a.counts_tiles) v.rank_counts[i] = rect_count(rc);
     if (v.key) v.key[i] = __float_as_uint(pv.z);
     v.xy[i] = pix;
     v.conic_o[i] = conic;

@@ -118,6 +118,7 @@ class PendingForward:
         self.counted = None                # [K, reserved], valid once `counted` (an event) has passed
         self.stream = None
         self.count_batch = None            # (pinned [n, 2] counts of a batch, this view's row)
+        self.tile_bucket = False           # phase 1 prepared the tile-bucket binning (id-order counts)
 
     def resolve(self, binning=False):
         """Deferred-count forwards: wait for the instance count (host waits on the event only, not
@@ -273,7 +274,7 @@ def language_split_native(language_feature, stream=None, out=None):
 def preprocess_views_native(raster_settings_list, means3D, opacities, shs=None, colors_precomp=None,
                             language_feature=None, scales=None, rotations=None, cov3D_precomp=None, stream=None,
                             split_language=True, split_behind_counts=True, split_stream=None, order_first=None,
-                            order_stream=None, row_chunks=None):
+                            order_stream=None, row_chunks=None, tile_bucket=False):
     """Forward phase 1 of several views of the same Gaussians as one batch
     (lsr_forward_preprocess_views_async: one preprocess launch per 8 views reads each Gaussian once,
     the views' depth sorts and instance scans share their launches) on `stream`.  No host
@@ -296,7 +297,12 @@ def preprocess_views_native(raster_settings_list, means3D, opacities, shs=None, 
     row_chunks = [(r0, r1, before), ...] covering [0, P) in order (r0 multiples of 256): the
     preprocess runs one launch per row chunk (lsr_forward_preprocess_views_rows_async), each after
     before() (which makes `stream` wait for that chunk's rows, e.g. the sharded optimizer's
-    all-gather of them), and the depth orders follow once every chunk is in; same results."""
+    all-gather of them), and the depth orders follow once every chunk is in; same results.
+
+    tile_bucket: prepare the tile-bucket binning instead (lsr_forward_preprocess_views_tb_async +
+    lsr_forward_instance_scan_views_async: no depth sort; binning_views_native then buckets the
+    instances by tile and sorts each bucket in LDS, lsr_forward_binning_views_tb).  Same lists, same
+    results; the split into first views and order_stream views applies to the instance scans."""
     device = _check_device(means3D)
     L = _lib.load()
     stream = stream or torch.cuda.current_stream(device)
@@ -324,7 +330,22 @@ def preprocess_views_native(raster_settings_list, means3D, opacities, shs=None, 
     o_arr = (ctypes.POINTER(_lib.FwdOut) * n)(*[ctypes.pointer(fo) for fo in fouts])
     g_arr = (ctypes.c_void_p * n)(*[g.data_ptr() for g in geoms])
     try:
-        if row_chunks:
+        if tile_bucket:
+            for r0, r1, before in (row_chunks or [(0, P, None)]):
+                if before is not None:
+                    before()
+                _lib.check(L.lsr_forward_preprocess_views_tb_async(n, int(r0), int(r1), s_arr, ctypes.byref(fin), o_arr,
+                                                                   g_arr, ctypes.c_void_p(stream.cuda_stream)),
+                           "lsr_forward_preprocess_views_tb_async")
+            if row_chunks and (row_chunks[0][0] != 0 or row_chunks[-1][1] != P or
+                               any(a[1] != b[0] for a, b in zip(row_chunks, row_chunks[1:]))):
+                raise ValueError("row_chunks must cover [0, P) in order")
+            if k > 0:
+                _lib.check(L.lsr_forward_instance_scan_views_async(k, s_arr, ctypes.byref(fin), g_arr,
+                                                                   ctypes.c_void_p(counts.data_ptr()),
+                                                                   ctypes.c_void_p(stream.cuda_stream)),
+                           "lsr_forward_instance_scan_views_async")
+        elif row_chunks:
             covered = 0
             for r0, r1, before in row_chunks:
                 if r0 != covered or r1 < r0:
@@ -358,12 +379,12 @@ def preprocess_views_native(raster_settings_list, means3D, opacities, shs=None, 
         for g in geoms[k:]:
             g.record_stream(order_stream)
         counts_b = torch.zeros(n - k, 2, dtype=torch.int32, pin_memory=True)
+        fn, what = ((L.lsr_forward_instance_scan_views_async, "lsr_forward_instance_scan_views_async") if tile_bucket
+                    else (L.lsr_forward_depth_order_views_async, "lsr_forward_depth_order_views_async"))
         try:
-            _lib.check(L.lsr_forward_depth_order_views_async(n - k, (ctypes.POINTER(_lib.Settings) * (n - k))(*s_arr[k:]),
-                                                             ctypes.byref(fin), (ctypes.c_void_p * (n - k))(*g_arr[k:]),
-                                                             ctypes.c_void_p(counts_b.data_ptr()),
-                                                             ctypes.c_void_p(order_stream.cuda_stream)),
-                       "lsr_forward_depth_order_views_async")
+            _lib.check(fn(n - k, (ctypes.POINTER(_lib.Settings) * (n - k))(*s_arr[k:]), ctypes.byref(fin),
+                          (ctypes.c_void_p * (n - k))(*g_arr[k:]), ctypes.c_void_p(counts_b.data_ptr()),
+                          ctypes.c_void_p(order_stream.cuda_stream)), what)
         except RuntimeError:
             _dump_forward(raster_settings_list[0], inputs)
             raise
@@ -380,6 +401,7 @@ def preprocess_views_native(raster_settings_list, means3D, opacities, shs=None, 
     for v, rs in enumerate(raster_settings_list):
         H, W = int(rs.image_height), int(rs.image_width)
         pf = PendingForward(rs, sts[v], fin, inputs, geoms[v], radii[v], None, device, H, W)
+        pf.tile_bucket = bool(tile_bucket)
         if v < k:
             pf.count_host, pf.stream, pf.counted = counts[v], stream, ev
             pf.count_batch = (counts, v)      # binning_views_native reads the whole batch at once
@@ -397,6 +419,11 @@ def _align(nbytes, a=256):
 @functools.lru_cache(maxsize=4096)
 def _binning_bytes(K):   # pure size queries, asked on the device's critical path (the count wait)
     return _align(int(_lib.load().lsr_binning_bytes(K)))
+
+
+@functools.lru_cache(maxsize=4096)
+def _binning_bytes_tb(K, P, W, H):
+    return _align(int(_lib.load().lsr_binning_bytes_tb(K, P, W, H)))
 
 
 @functools.lru_cache(maxsize=64)
@@ -425,9 +452,13 @@ def binning_views_native(pendings, stream=None):
             pf.resolve()
     n = len(pendings)
     device = pendings[0].device
+    tb = pendings[0].tile_bucket
+    if any(pf.tile_bucket != tb for pf in pendings):
+        raise ValueError("binning_views_native: a batch mixes tile-bucket and sort-path views")
     sizes = []
     for pf in pendings:
-        sizes += [_binning_bytes(pf.num_rendered), _img_bytes(pf.W, pf.H)]
+        sizes += [_binning_bytes_tb(pf.num_rendered, pf.fin.P, pf.W, pf.H) if tb else _binning_bytes(pf.num_rendered),
+                  _img_bytes(pf.W, pf.H)]
     with torch.cuda.stream(stream):
         ws = torch.empty(sum(sizes), dtype=torch.uint8, device=device)
     off = 0
@@ -441,9 +472,11 @@ def binning_views_native(pendings, stream=None):
     b_arr = (ctypes.c_void_p * n)(*[pf.binning.data_ptr() for pf in pendings])
     i_arr = (ctypes.c_void_p * n)(*[pf.img.data_ptr() for pf in pendings])
     k_arr = (ctypes.c_int64 * n)(*[pf.num_rendered for pf in pendings])
+    fn, what = ((L.lsr_forward_binning_views_tb, "lsr_forward_binning_views_tb") if tb
+                else (L.lsr_forward_binning_views, "lsr_forward_binning_views"))
     try:
-        _lib.check(L.lsr_forward_binning_views(n, s_arr, ctypes.byref(pendings[0].fin), g_arr, b_arr, i_arr, k_arr,
-                                               ctypes.c_void_p(stream.cuda_stream)), "lsr_forward_binning_views")
+        _lib.check(fn(n, s_arr, ctypes.byref(pendings[0].fin), g_arr, b_arr, i_arr, k_arr,
+                      ctypes.c_void_p(stream.cuda_stream)), what)
     except RuntimeError:
         _dump_forward(pendings[0].raster_settings, pendings[0].inputs)
         raise
@@ -457,6 +490,8 @@ def render_native(pending: PendingForward):
     """Forward phase 2 (binning unless preprocess_native already did it, then compositing) on the
     current stream.  Returns (color, language_feature, radii, depth, state)."""
     L = _lib.load()
+    if pending.tile_bucket and pending.binning is None:   # lsr_forward_render bins the sort path's way
+        binning_views_native([pending], stream=torch.cuda.current_stream(pending.device))
     pending.resolve()
     device, H, W, C = pending.device, pending.H, pending.W, pending.fin.C
     stream = torch.cuda.current_stream(device)

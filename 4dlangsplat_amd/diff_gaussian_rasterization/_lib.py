@@ -141,6 +141,19 @@ SIGNATURES = {
                                                  ctypes.POINTER(FwdIn), ctypes.POINTER(ctypes.c_void_p),
                                                  ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
                                                  ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
+    "lsr_binning_bytes_tb": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
+    "lsr_forward_preprocess_views_tb_async": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                                             ctypes.POINTER(ctypes.POINTER(Settings)),
+                                                             ctypes.POINTER(FwdIn),
+                                                             ctypes.POINTER(ctypes.POINTER(FwdOut)),
+                                                             ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p]),
+    "lsr_forward_instance_scan_views_async": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(ctypes.POINTER(Settings)),
+                                                             ctypes.POINTER(FwdIn), ctypes.POINTER(ctypes.c_void_p),
+                                                             ctypes.c_void_p, ctypes.c_void_p]),
+    "lsr_forward_binning_views_tb": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(ctypes.POINTER(Settings)),
+                                                    ctypes.POINTER(FwdIn), ctypes.POINTER(ctypes.c_void_p),
+                                                    ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
+                                                    ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p]),
     "lsr_forward_render": (ctypes.c_int, [ctypes.POINTER(Settings), ctypes.POINTER(FwdIn), ctypes.POINTER(FwdOut),
                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                           ctypes.c_void_p]),

@@ -264,7 +264,7 @@ class ViewParallelStep:
 def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool = False, overlap: bool = True,
                          batch_backward: bool = True, early_views: int = 3, composite_batch: bool = True,
                          side_priority: int = 0, side_from_preprocess: bool = True, split_behind_counts: bool = True,
-                         fill_on_side: bool = False, order_on_side: bool = False):
+                         fill_on_side: bool = False, order_on_side: bool = False, tile_bucket: bool = False):
     """render_view callback for ViewParallelStep on the HIP rasterizer (the product path).
 
     scene    : object with means3D, opacities, shs, lang, scales, rotations device tensors
@@ -302,7 +302,9 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
     (the first compositor launch waits for them).  order_on_side: the later views' depth sorts and
     instance scans run on that side stream too (the preprocess stays one launch for all views): the
     early views' binning no longer waits for every view's depth order, and the later views are
-    binned once the early views' compositing is enqueued.  With
+    binned once the early views' compositing is enqueued.  tile_bucket (batched only): the
+    tile-bucket binning (no depth sort; instances bucketed by tile, each bucket sorted in LDS:
+    preprocess_views_native(tile_bucket=True)); same lists, same results.  With
     composite_batch (batched only) the step runs through render_batch: one compositor forward and
     one compositor backward launch per binning batch instead of per view.
 
@@ -367,7 +369,7 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
                                           split_stream=bin_side[0] if to_side else None,
                                           order_first=early_views if late_order else None,
                                           order_stream=bin_side[0] if late_order else None,
-                                          row_chunks=waits)
+                                          row_chunks=waits, tile_bucket=tile_bucket)
         fill_ready[0] = None
         if to_side:                   # the fills beside the early views' binning, ahead of the side binning
             bin_side[0].wait_stream(torch.cuda.current_stream(scene.means3D.device))   # after the preprocess batch

@@ -216,6 +216,10 @@ def parse_args(argv=None):
     ap.add_argument("--order-on-side", action="store_true",
                     help="the views past --early-views are depth-sorted on the side stream too (the early views' "
                          "binning no longer waits for every view's depth order)")
+    ap.add_argument("--binning", choices=("sort", "bucket"), default="sort",
+                    help="per-tile lists by a depth sort of the Gaussians + a stable 13-bit tile sort of the "
+                         "instances (sort), or by bucketing the instances by tile and sorting each bucket in LDS "
+                         "(bucket); same lists")
     ap.add_argument("--per-view-composite", action="store_true",
                     help="one compositor launch per view instead of one per binning batch of views")
     ap.add_argument("--pipeline", choices=("batched", "lookahead", "side"), default=None,
@@ -288,7 +292,7 @@ def run(args):
                                   early_views=args.early_views, composite_batch=not args.per_view_composite,
                                   side_priority=args.side_priority, side_from_preprocess=not args.side_after_binning,
                                   split_behind_counts=not args.no_wait_fill, fill_on_side=args.fill_on_side,
-                                  order_on_side=args.order_on_side)
+                                  order_on_side=args.order_on_side, tile_bucket=args.binning == "bucket")
     Ks = []
 
     def render_view(v, b):
@@ -498,7 +502,7 @@ def run(args):
                        "splits, three products, fp32 accumulation (~2^-17 relative)"),
             config=dict(workload="S2M synthetic (BASELINE configs[2] per GPU; configs[3] batch split)",
                         gaussians=P, width=W, height=H, channels=C, views_per_gpu_per_step=V,
-                        global_batch=world * V, parallelism=f"dp{world}", pipeline="none" if args.no_overlap else args.pipeline, num_rendered_mean=int(Kmean),
+                        global_batch=world * V, parallelism=f"dp{world}", pipeline="none" if args.no_overlap else args.pipeline, binning=args.binning, num_rendered_mean=int(Kmean),
                         visible=Pvis, visible_any_view=Pany, grad_bucket_mb=round(bucket.nbytes / 2**20, 1)),
             roofline=roof, frame_roofline=frame_roof, cpu_baseline=cpu, single_view=single,
             phases={k: dict(mean_ms=round(v["mean_ms"], 4), alg_gbs=round(v["alg_gbs"], 1),

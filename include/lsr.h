@@ -197,6 +197,27 @@ int lsr_forward_composite(const lsr_settings *s, const lsr_fwd_in *in, lsr_fwd_o
 int lsr_forward_binning_views(int32_t n_views, const lsr_settings *const *s, const lsr_fwd_in *in,
                               void *const *geom, void *const *binning, void *const *img,
                               const int64_t *num_rendered, lsr_stream_t stream);
+
+/* Tile-bucket binning: the same per-tile lists (same entries, same (depth, id) order) without the
+ * depth sort of the Gaussians or a sort of all instances.  Phase 1 is
+ * lsr_forward_preprocess_views_tb_async (the preprocess of rows [row0, row1) of n_views views; the
+ * per-Gaussian instance counts are kept in id order) over every row, then
+ * lsr_forward_instance_scan_views_async (their exclusive scans; num_rendered into host_counts as
+ * for lsr_forward_depth_order_views_async); phase 2 is lsr_forward_binning_views_tb (instances
+ * bucketed by tile, each bucket sorted in LDS) with binning[v] of >= lsr_binning_bytes_tb bytes, then
+ * lsr_forward_composite_views / lsr_backward as usual.  A geom workspace prepared by one binning
+ * must be binned by the same one.  At most 12288 tiles (LSR_EINVAL otherwise).  Replaces the same
+ * upstream stages as the sort path (rasterizer_impl.cu's InclusiveSum, duplicateWithKeys,
+ * SortPairs and identifyTileRanges). */
+int64_t lsr_binning_bytes_tb(int64_t num_rendered, int32_t P, int32_t image_width, int32_t image_height);
+int lsr_forward_preprocess_views_tb_async(int32_t n_views, int32_t row0, int32_t row1, const lsr_settings *const *s,
+                                          const lsr_fwd_in *in, lsr_fwd_out *const *out, void *const *geom,
+                                          lsr_stream_t stream);
+int lsr_forward_instance_scan_views_async(int32_t n_views, const lsr_settings *const *s, const lsr_fwd_in *in,
+                                          void *const *geom, uint32_t *host_counts, lsr_stream_t stream);
+int lsr_forward_binning_views_tb(int32_t n_views, const lsr_settings *const *s, const lsr_fwd_in *in,
+                                 void *const *geom, void *const *binning, void *const *img,
+                                 const int64_t *num_rendered, lsr_stream_t stream);
 /* lsr_forward_composite of n_views >= 1 binned views of the same Gaussians in ONE compositor
  * launch per 8 views (grid row = view: a view's last waves run beside the next view's first ones
  * instead of the chip draining between per-view launches).  out[v], geom[v], binning[v], img[v],
