@@ -25,8 +25,12 @@
 namespace lsr {
 
 namespace {
+constexpr int TB_WAVES = 16;                  // waves per count / scatter block
+constexpr int TB_THREADS = 64 * TB_WAVES;
 constexpr int TB_CHUNKS = 16;                 // 64-Gaussian chunks per wave
-constexpr int TB_GPB = 4 * 64 * TB_CHUNKS;    // Gaussians per count / scatter block (4096)
+constexpr int TB_GPB = TB_THREADS * TB_CHUNKS;   // Gaussians per count / scatter block (16384: ~8
+                                                 // listed instances per tile and block on the headline
+                                                 // scene, so the scatter's runs fill whole 64-byte lines)
 constexpr int TB_CAP = 2048;                  // bucket length sorted in LDS at once (2 x 16 KB)
 constexpr int TB_SEG = 16;                    // column-scan segments (and tiles) per block
 
@@ -43,13 +47,13 @@ __device__ __forceinline__ uint32_t tb_word(uint64_t k) {
 // quadrant of its tile -- the slot order and the quadrant bits of k_emit.
 template <typename F>
 __device__ __forceinline__ void tb_walk(const TbBatch& tb, const TbView& tv, F&& f) {
-    __shared__ uint32_t s_off[4][64];
-    __shared__ uint2 s_rc[4][64];
-    __shared__ EmitSplat s_sp[4][64];
+    __shared__ uint32_t s_off[TB_WAVES][64];
+    __shared__ uint2 s_rc[TB_WAVES][64];
+    __shared__ EmitSplat s_sp[TB_WAVES][64];
     const int P = tb.P, gx = tb.grid_x;
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int ch = 0; ch < TB_CHUNKS; ++ch) {
-        const int base = blockIdx.x * TB_GPB + (ch * 4 + w) * 64;
+        const int base = blockIdx.x * TB_GPB + (ch * TB_WAVES + w) * 64;
         if (base >= P) break;                               // wave-uniform
         const int g = base + lane;
         const bool ok = g < P;
@@ -97,15 +101,15 @@ __device__ __forceinline__ void tb_walk(const TbBatch& tb, const TbView& tv, F&&
 }
 }  // namespace
 
-__global__ void __launch_bounds__(256) k_tb_count(const TbBatch tb) {
+__global__ void __launch_bounds__(TB_THREADS) k_tb_count(const TbBatch tb) {
     extern __shared__ uint32_t s_hist[];   // [ntiles]
     const TbView& tv = tb.v[blockIdx.y];
-    for (int t = threadIdx.x; t < tb.ntiles; t += 256) s_hist[t] = 0u;
+    for (int t = threadIdx.x; t < tb.ntiles; t += TB_THREADS) s_hist[t] = 0u;
     __syncthreads();
     tb_walk(tb, tv, [&](uint32_t tile, uint32_t, uint32_t) { atomicAdd(&s_hist[tile], 1u); });
     __syncthreads();
     uint32_t* row = tv.table + (size_t)blockIdx.x * tb.ntiles;
-    for (int t = threadIdx.x; t < tb.ntiles; t += 256) row[t] = s_hist[t];
+    for (int t = threadIdx.x; t < tb.ntiles; t += TB_THREADS) row[t] = s_hist[t];
 }
 
 // per tile (TB_SEG tiles x TB_SEG segments of block rows per 256-thread block): the column's
@@ -174,11 +178,11 @@ __global__ void __launch_bounds__(1024) k_tb_tilescan(const TbBatch tb) {
     }
 }
 
-__global__ void __launch_bounds__(256) k_tb_scatter(const TbBatch tb) {
+__global__ void __launch_bounds__(TB_THREADS) k_tb_scatter(const TbBatch tb) {
     extern __shared__ uint32_t s_cur[];   // [ntiles]: the next slot of each tile in this block's run
     const TbView& tv = tb.v[blockIdx.y];
     const uint32_t* row = tv.table + (size_t)blockIdx.x * tb.ntiles;
-    for (int t = threadIdx.x; t < tb.ntiles; t += 256) s_cur[t] = tv.tile_start[t] + row[t];
+    for (int t = threadIdx.x; t < tb.ntiles; t += TB_THREADS) s_cur[t] = tv.tile_start[t] + row[t];
     __syncthreads();
     tb_walk(tb, tv, [&](uint32_t tile, uint32_t id, uint32_t quads) {
         const uint32_t pos = atomicAdd(&s_cur[tile], 1u);
@@ -187,17 +191,23 @@ __global__ void __launch_bounds__(256) k_tb_scatter(const TbBatch tb) {
 }
 
 namespace {
-// Sorts s[0, n2) ascending (n2 a power of two, 8 <= n2 <= TB_CAP) with the block's 256 threads;
-// returns the buffer holding the result (s or t, both [TB_CAP] in LDS).  Each thread sorts a run of
-// 8 keys in registers, then merge passes double the runs: thread i makes outputs [8 i, 8 i + 8) of
-// its pair of runs, finding where they start by a binary search along the merge path and merging 8
-// steps from there.  Keys are unique apart from the ~0 padding (equal, so either order is right).
-__device__ __forceinline__ uint64_t* lds_merge_sort(uint64_t* s, uint64_t* t, int n2) {
-    const int nt = n2 / 8, tid = threadIdx.x;
+// LDS slot of key i: one unused slot after every 8 keys, so that a thread's run of 8 (the register
+// sort, the merge outputs) starts 9 slots after its neighbour's: 2-way bank conflicts, not 16-way.
+__device__ __forceinline__ int pad8(int i) { return i + (i >> 3); }
+constexpr int TB_CAP_PAD = TB_CAP + TB_CAP / 8;
+
+// Sorts keys 0..n8-1 (slots pad8(i) of s; n8 a multiple of 8, 8 <= n8 <= TB_CAP) ascending with the
+// block's 256 threads; returns the buffer holding the result (s or t, both [TB_CAP_PAD] in LDS).
+// Each thread sorts a run of 8 keys in registers, then merge passes double the runs (the last run of
+// a pass may be short): thread i makes outputs [8 i, 8 i + 8) of its pair of runs, finding where they
+// start by a binary search along the merge path and merging 8 steps from there.  Keys are unique
+// apart from the ~0 padding (equal, so either order is right).
+__device__ __forceinline__ uint64_t* lds_merge_sort(uint64_t* s, uint64_t* t, int n8) {
+    const int nt = n8 / 8, tid = threadIdx.x;
     if (tid < nt) {
         uint64_t x[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) x[k] = s[8 * tid + k];
+        for (int k = 0; k < 8; ++k) x[k] = s[9 * tid + k];
         // odd-even transposition network on 8 registers (28 compare-exchanges, fully unrolled)
 #pragma unroll
         for (int r = 0; r < 8; ++r)
@@ -209,31 +219,34 @@ __device__ __forceinline__ uint64_t* lds_merge_sort(uint64_t* s, uint64_t* t, in
                 x[k + 1] = hi;
             }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) s[8 * tid + k] = x[k];
+        for (int k = 0; k < 8; ++k) s[9 * tid + k] = x[k];
     }
     __syncthreads();
     uint64_t* src = s;
     uint64_t* dst = t;
-    for (int w = 8; w < n2; w <<= 1) {
+    for (int w = 8; w < n8; w <<= 1) {
         if (tid < nt) {
             const int o = 8 * tid, lo = o & ~(2 * w - 1), d = o - lo;
-            const uint64_t* A = src + lo;
-            const uint64_t* B = A + w;
-            int a0 = max(0, d - w), a1 = min(d, w);   // keys taken from A among the pair's first d outputs
+            const int na = min(w, n8 - lo), nb = max(0, min(w, n8 - lo - w)), bo = lo + na;
+            int a0 = max(0, d - nb), a1 = min(d, na);   // keys taken from A = [lo, lo + na) among the first d
             while (a0 < a1) {
                 const int m = (a0 + a1) >> 1;
-                if (A[m] < B[d - m - 1]) a0 = m + 1;
+                if (src[pad8(lo + m)] < src[pad8(bo + d - m - 1)]) a0 = m + 1;
                 else a1 = m;
             }
             int i = a0, j = d - a0;
-            uint64_t* out = dst + o;
+            uint64_t av = i < na ? src[pad8(lo + i)] : ~0ull, bv = j < nb ? src[pad8(bo + j)] : ~0ull;
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                const uint64_t av = i < w ? A[i] : ~0ull, bv = j < w ? B[j] : ~0ull;
-                const bool ta = j >= w || (i < w && av < bv);
-                out[k] = ta ? av : bv;
-                i += ta;
-                j += !ta;
+                const bool ta = j >= nb || (i < na && av < bv);
+                dst[9 * tid + k] = ta ? av : bv;
+                if (ta) {
+                    ++i;
+                    av = i < na ? src[pad8(lo + i)] : ~0ull;
+                } else {
+                    ++j;
+                    bv = j < nb ? src[pad8(bo + j)] : ~0ull;
+                }
             }
         }
         __syncthreads();
@@ -256,16 +269,12 @@ __device__ __forceinline__ void merge_runs(const uint64_t* a, int na, const uint
         out[o] = take_a ? a[i] : b[jb];
     }
 }
-__device__ __forceinline__ int pow2_at_least(int n) {
-    int n2 = 8;
-    while (n2 < n) n2 <<= 1;
-    return n2;
-}
+__device__ __forceinline__ int round8(int n) { return (n + 7) & ~7; }
 }  // namespace
 
 __global__ void __launch_bounds__(256) k_tb_sort(const TbBatch tb) {
-    __shared__ uint64_t s_a[TB_CAP];
-    __shared__ uint64_t s_b[TB_CAP];
+    __shared__ uint64_t s_a[TB_CAP_PAD];
+    __shared__ uint64_t s_b[TB_CAP_PAD];
     const TbView& tv = tb.v[blockIdx.y];
     const int tile = blockIdx.x;
     const uint2 r = tv.ranges[tile];
@@ -273,19 +282,19 @@ __global__ void __launch_bounds__(256) k_tb_sort(const TbBatch tb) {
     uint64_t* keys = tv.keys + r.x;
     uint32_t* words = tv.words + r.x;
     if (n > 0 && n <= TB_CAP) {
-        const int n2 = pow2_at_least(n);
-        for (int i = threadIdx.x; i < n2; i += 256) s_a[i] = i < n ? keys[i] : ~0ull;
+        const int n8 = round8(n);
+        for (int i = threadIdx.x; i < n8; i += 256) s_a[pad8(i)] = i < n ? keys[i] : ~0ull;
         __syncthreads();
-        const uint64_t* res = lds_merge_sort(s_a, s_b, n2);
-        for (int i = threadIdx.x; i < n; i += 256) words[i] = tb_word(res[i]);
+        const uint64_t* res = lds_merge_sort(s_a, s_b, n8);
+        for (int i = threadIdx.x; i < n; i += 256) words[i] = tb_word(res[pad8(i)]);
     } else if (n > TB_CAP) {
         // long bucket: LDS-sorted chunks of TB_CAP, then merge passes between keys and tmp
         for (int c0 = 0; c0 < n; c0 += TB_CAP) {
-            const int m = min(TB_CAP, n - c0), m2 = pow2_at_least(m);
-            for (int i = threadIdx.x; i < m2; i += 256) s_a[i] = i < m ? keys[c0 + i] : ~0ull;
+            const int m = min(TB_CAP, n - c0), m8 = round8(m);
+            for (int i = threadIdx.x; i < m8; i += 256) s_a[pad8(i)] = i < m ? keys[c0 + i] : ~0ull;
             __syncthreads();
-            const uint64_t* res = lds_merge_sort(s_a, s_b, m2);
-            for (int i = threadIdx.x; i < m; i += 256) keys[c0 + i] = res[i];
+            const uint64_t* res = lds_merge_sort(s_a, s_b, m8);
+            for (int i = threadIdx.x; i < m; i += 256) keys[c0 + i] = res[pad8(i)];
             __syncthreads();
         }
         __threadfence_block();
@@ -311,10 +320,19 @@ void launch_tile_bucket_binning(const TbBatch& tb, int nv, hipStream_t st) {
     if (tb.P == 0 || nv <= 0) return;
     const int nb = tb_blocks(tb.P);
     const size_t hist = (size_t)tb.ntiles * sizeof(uint32_t);
-    hipLaunchKernelGGL(k_tb_count, dim3(nb, nv), dim3(256), hist, st, tb);
+    static bool attr = false;   // dynamic LDS beyond 64 KiB with the walk's static staging arrays
+    if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_tb_count),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_tb_scatter),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        (void)hipGetLastError();
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_tb_count, dim3(nb, nv), dim3(TB_THREADS), hist, st, tb);
     hipLaunchKernelGGL(k_tb_colscan, dim3((tb.ntiles + TB_SEG - 1) / TB_SEG, nv), dim3(256), 0, st, tb, nb);
     hipLaunchKernelGGL(k_tb_tilescan, dim3(nv), dim3(1024), 0, st, tb);
-    hipLaunchKernelGGL(k_tb_scatter, dim3(nb, nv), dim3(256), hist, st, tb);
+    hipLaunchKernelGGL(k_tb_scatter, dim3(nb, nv), dim3(TB_THREADS), hist, st, tb);
     hipLaunchKernelGGL(k_tb_sort, dim3(tb.ntiles, nv), dim3(256), 0, st, tb);
 }
 

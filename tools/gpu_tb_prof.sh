@@ -7,7 +7,7 @@ cd /tmp && export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 for b in bucket sort; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/$b -o run -- python bench.py \
-      --steps 5 --warmup 2 --no-cpu-baseline --single-view-steps 0 --binning $b > $out/bench_$b.json 2> $out/bench_$b.err \
+      --steps 5 --warmup 2 --no-cpu-baseline --single-view-steps 0 --binning $b $EXTRA > $out/bench_$b.json 2> $out/bench_$b.err \
       || { tail -20 $out/bench_$b.err; exit 1; }
 done
 find $out -name "*kernel_stats.csv"
