@@ -89,7 +89,10 @@ def main():
     bms = e0.elapsed_time(e1) / (args.iters // 2)
     # recompute of the forward MLP + data gradients (2 products per weight) + weight gradients (1)
     bflops = 2.0 * macs * 4 * P
-    saved = P * (32 + 128 + 128 + 5 * 128 + 5 * 128) * 4          # activations written then read
+    # rows written by the backward's phase A and read again (deform_api.hip bwd_scratch): the
+    # features X (32), the feature_out layer's activation A and its gradient dH (128 each); the five
+    # heads' hidden rows are recomputed by the weight-gradient kernels, not saved (round 4)
+    saved = P * (32 + 128 + 128) * 4
     print(json.dumps(dict(metric="deformation backward Gaussians/s (Neu3D structure)", value=round(P / (bms * 1e-3)),
                           unit="Gaussians/s", ms_per_call=round(bms, 4), gaussians=P,
                           mlp_tflops=round(bflops / (bms * 1e-3) / 1e12, 1),
