@@ -262,7 +262,7 @@ class ViewParallelStep:
 
 
 def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool = False, overlap: bool = True,
-                         batch_backward: bool = True, early_views: int = 3, composite_batch: bool = True,
+                         batch_backward: bool = True, early_views=3, composite_batch: bool = True,
                          side_priority: int = 0, side_from_preprocess: bool = True, split_behind_counts: bool = True,
                          fill_on_side: bool = False, order_on_side: bool = False, tile_bucket: bool = False):
     """render_view callback for ViewParallelStep on the HIP rasterizer (the product path).
@@ -291,6 +291,10 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
     for all views, one host wait for their counts); each view then only composites.  Needs the
     step's views (begin_step, as ViewParallelStep.run calls it); without them, views batch alone.
 
+    early_views may also be a tuple (e, s1, s2, ...): the first e views binned on the current stream,
+    then side-stream binning batches of s1, s2, ... views and one of the rest, in that order, each
+    with its own event, so render_batch composites each batch as soon as its own binning is done
+    (the first compositor launch waits only for e views' binning).
     With more than `early_views` views in the batch, only the first `early_views` are binned on
     the current stream; the others' binning (emission, tile sort, tile ranges: chains of short,
     dependent launches that leave most of the GPU idle) runs on a side stream while those first
@@ -357,7 +361,9 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
         idle stretch while the host reads the counts)."""
         views = [w for w in step_views[0] if w >= v] if step_views[0] is not None else [v]
         views = [w for w in views if has_view(w)] or [v]
-        split_side = 0 < early_views < len(views) and scene.means3D.is_cuda
+        sizes = tuple(early_views) if isinstance(early_views, (tuple, list)) else (early_views,)
+        e0 = int(sizes[0])
+        split_side = 0 < e0 < len(views) and scene.means3D.is_cuda
         if split_side and bin_side[0] is None:
             bin_side[0] = torch.cuda.Stream(device=scene.means3D.device, priority=side_priority)
         to_side = fill_on_side and split_side
@@ -367,7 +373,7 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
                                           shs=scene.shs, language_feature=scene.lang, scales=scene.scales,
                                           rotations=scene.rotations, split_behind_counts=split_behind_counts,
                                           split_stream=bin_side[0] if to_side else None,
-                                          order_first=early_views if late_order else None,
+                                          order_first=e0 if late_order else None,
                                           order_stream=bin_side[0] if late_order else None,
                                           row_chunks=waits, tile_bucket=tile_bucket)
         fill_ready[0] = None
@@ -388,18 +394,24 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
             if radii_out is not None:     # the views' radii MAX, also while the host waits for the counts
                 dgr.radii_max_native([pf.radii for pf in pfs], radii_out)
         if late_order:   # the later views are binned by render_batch, after the early views' compositing
-            dgr.binning_views_native(pfs[:early_views])
+            dgr.binning_views_native(pfs[:e0])
         elif split_side:
             dev = scene.means3D.device
             side_b = bin_side[0]
             if side_from_preprocess and not to_side:   # the side binning starts beside the early views' binning
                 side_b.wait_stream(torch.cuda.current_stream(dev))   # after the preprocess batch
-            dgr.binning_views_native(pfs[:early_views])      # waits for the batch's counts
+            dgr.binning_views_native(pfs[:e0])      # waits for the batch's counts
             if not side_from_preprocess:  # ... or behind it
                 side_b.wait_stream(torch.cuda.current_stream(dev))
-            for pf in pfs[early_views:]:
+            for pf in pfs[e0:]:
                 pf.geom.record_stream(side_b)
-            dgr.binning_views_native(pfs[early_views:], stream=side_b)
+            cuts = [e0]
+            for n in sizes[1:]:
+                if cuts[-1] + int(n) < len(views):
+                    cuts.append(cuts[-1] + int(n))
+            cuts.append(len(views))
+            for a0, a1 in zip(cuts, cuts[1:]):   # each side batch with its own event
+                dgr.binning_views_native(pfs[a0:a1], stream=side_b)
         else:
             dgr.binning_views_native(pfs)
         pending.update(zip(views, pfs))

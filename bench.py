@@ -180,6 +180,25 @@ def host_cpu():
     return min(n, quota) if quota else n, info
 
 
+def _early_views(text):
+    parts = [int(x) for x in str(text).split(",") if x.strip()]
+    if not parts or any(x < 0 for x in parts):
+        raise argparse.ArgumentTypeError("--early-views: e or e,s1,s2,... (non-negative)")
+    return parts[0] if len(parts) == 1 else tuple(parts)
+
+
+def _n_binning_batches(early, V):
+    """Binning batches (= compositor launch pairs) of a V-view step under --early-views."""
+    sizes = tuple(early) if isinstance(early, tuple) else (early,)
+    if not 0 < sizes[0] < V:
+        return 1
+    cuts = [sizes[0]]
+    for n in sizes[1:]:
+        if cuts[-1] + n < V:
+            cuts.append(cuts[-1] + n)
+    return len(cuts) + 1
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -199,9 +218,10 @@ def parse_args(argv=None):
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-densify-stats", action="store_true",
                     help="diagnostic: no means2D gradient / radii MAX in the step (train.py:350-352 needs them)")
-    ap.add_argument("--early-views", type=int, default=3,
+    ap.add_argument("--early-views", type=_early_views, default=3,
                     help="batched pipeline: views binned before compositing starts; the rest bin on a side stream "
-                         "while they composite (0: all binned first)")
+                         "while they composite (0: all binned first); 'e,s1,...': side binning batches of s1, ... "
+                         "views and one of the rest, each composited as soon as it is binned")
     ap.add_argument("--no-overlap", action="store_true", help="diagnostic: no side stream (uncontended phase times)")
     ap.add_argument("--side-priority", type=int, default=0,
                     help="torch stream priority of the side-stream binning (negative = higher)")
@@ -348,7 +368,7 @@ def run(args):
     _lib.profile_enable(False)
     # every view's backward ran, timed (a batched launch serves a binning batch of views)
     if hasattr(render, "render_batch"):
-        want = 2 if 0 < args.early_views < V else 1
+        want = _n_binning_batches(args.early_views, V)
     else:
         want = V
     if dom == "render_bwd" and prof["render_bwd"][1] != want * args.steps:
@@ -502,7 +522,7 @@ def run(args):
                        "splits, three products, fp32 accumulation (~2^-17 relative)"),
             config=dict(workload="S2M synthetic (BASELINE configs[2] per GPU; configs[3] batch split)",
                         gaussians=P, width=W, height=H, channels=C, views_per_gpu_per_step=V,
-                        global_batch=world * V, parallelism=f"dp{world}", pipeline="none" if args.no_overlap else args.pipeline, binning=args.binning, num_rendered_mean=int(Kmean),
+                        global_batch=world * V, parallelism=f"dp{world}", pipeline="none" if args.no_overlap else args.pipeline, binning=args.binning, early_views=args.early_views, num_rendered_mean=int(Kmean),
                         visible=Pvis, visible_any_view=Pany, grad_bucket_mb=round(bucket.nbytes / 2**20, 1)),
             roofline=roof, frame_roofline=frame_roof, cpu_baseline=cpu, single_view=single,
             phases={k: dict(mean_ms=round(v["mean_ms"], 4), alg_gbs=round(v["alg_gbs"], 1),

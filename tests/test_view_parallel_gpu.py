@@ -187,13 +187,15 @@ def test_composite_views_equals_per_view(split):
 
 
 @pytest.mark.parametrize("early,fill_side,order_side", [(0, False, False), (3, False, False), (3, True, False),
-                                                       (3, False, True), (1, False, True)])
+                                                       (3, False, True), (1, False, True), ((1, 2), False, False),
+                                                       ((1, 1, 1), False, False)])
 def test_batched_composite_step_agrees(early, fill_side, order_side):
     """ViewParallelStep through render_batch (the bench default: one compositor launch per binning
     batch) against the per-view compositor launches of the same batched pipeline; fill_side: the
     language split, bucket zeroing and radii MAX on the side stream (a NaN-prefilled bucket shows
     any compositor that runs before the zeroing); order_side: the later views' depth sorts on the
-    side stream too, binned after the early views' compositing is enqueued."""
+    side stream too, binned after the early views' compositing is enqueued; a tuple: several side
+    binning batches, each composited once its own binning is done."""
     sc, settings, grads = _setup(n_views=5)
     f0, r0 = _run(sc, settings, grads, overlap="batched", deterministic=False, early_views=early,
                   composite_batch=False)
