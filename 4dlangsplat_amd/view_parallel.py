@@ -473,11 +473,25 @@ def native_view_renderer(scene, settings, grad_fn: Callable, deterministic: bool
             else:
                 groups.append([(v, pf)])
         radii, ks = [], []
+        sizes = tuple(early_views) if isinstance(early_views, (tuple, list)) else (early_views,)
+        split_groups = []
         for grp in groups:
             unbinned = [pf for _, pf in grp if getattr(pf, "binning", True) is None]
             if unbinned and unbinned[0].stream is not None and unbinned[0].stream != torch.cuda.current_stream(
-                    scene.means3D.device):   # depth-ordered on the side stream (order_on_side): binned there too
-                dgr.binning_views_native(unbinned, stream=unbinned[0].stream)
+                    scene.means3D.device):   # depth-ordered on the side stream (order_on_side): binned there too,
+                # in the batches early_views[1:] names (each with its own event, so each composites as soon
+                # as it is binned), all enqueued before any of them composites
+                cuts = [0]
+                for n in sizes[1:]:
+                    if cuts[-1] + int(n) < len(grp):
+                        cuts.append(cuts[-1] + int(n))
+                cuts.append(len(grp))
+                for a0, a1 in zip(cuts, cuts[1:]):
+                    dgr.binning_views_native([pf for _, pf in grp[a0:a1]], stream=unbinned[0].stream)
+                    split_groups.append(grp[a0:a1])
+            else:
+                split_groups.append(grp)
+        for grp in split_groups:
             res = dgr.render_views_native([pf for _, pf in grp])
             gcs, gls, gds = [], [], []
             for (v, _), (color, lang, r, depth, st) in zip(grp, res):

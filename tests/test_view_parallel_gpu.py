@@ -188,7 +188,7 @@ def test_composite_views_equals_per_view(split):
 
 @pytest.mark.parametrize("early,fill_side,order_side", [(0, False, False), (3, False, False), (3, True, False),
                                                        (3, False, True), (1, False, True), ((1, 2), False, False),
-                                                       ((1, 1, 1), False, False)])
+                                                       ((1, 1, 1), False, False), ((1, 2), False, True)])
 def test_batched_composite_step_agrees(early, fill_side, order_side):
     """ViewParallelStep through render_batch (the bench default: one compositor launch per binning
     batch) against the per-view compositor launches of the same batched pipeline; fill_side: the
