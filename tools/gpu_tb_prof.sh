@@ -11,3 +11,7 @@ for b in bucket sort; do
       || { tail -20 $out/bench_$b.err; exit 1; }
 done
 find $out -name "*kernel_stats.csv"
+for b in bucket sort; do
+  t=$(find $out/$b -name "*kernel_trace.csv" | head -1)
+  python3 tools/step_timeline.py "$t" > $out/timeline_$b.txt && head -40 $out/timeline_$b.txt
+done
