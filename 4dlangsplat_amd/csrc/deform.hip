@@ -513,6 +513,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
     __bf16 *bh = s_hh[cur ^ 1], *bl = s_hl[cur ^ 1];
 
     df32x16 dA[2] = {df32x16{}, df32x16{}};
+#ifdef LSR_DEFORM_ABL_NOHEADS   // timing ablation only (wrong gradients): the heads' share of phase A
+    if (a.P < 0)
+#endif
     for (int hd = 0; hd < DEF_HEADS; ++hd) {
         if (!((a.heads >> hd) & 1u)) continue;                       // block-uniform
         const int nout = head_out(a, hd);
@@ -641,6 +644,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
     float* const s_sw = reinterpret_cast<float*>(s_soff + 4 * 16 * 4);
 
     // ---- HexPlane backward: 4 threads per Gaussian, 4 channels each ----------------------------------
+#ifdef LSR_DEFORM_ABL_NOHEX   // timing ablation only (wrong gradients): the HexPlane backward's share
+    if (a.P < 0)
+#endif
     {
         const int gl = tid >> 2, q = tid & 3;
         const bool ok = g0 + gl < a.P;
@@ -721,6 +727,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
                         }
 #endif
 #ifndef LSR_DEFORM_ABL_NOSCATTER   // timing ablation only (wrong plane gradients)
+#ifdef LSR_DEFORM_ABL_NOTIME        // timing ablation only: the time planes' (xt, yt, zt) atomics skipped
+                        if (ci == 2 || ci >= 4) continue;
+#endif
                         if (val != 0.0f) atomicAdd(gp + s_soff[(wave * 16 + j) * 4 + tap] + ch, val);
 #endif
                     }
