@@ -223,6 +223,9 @@ def parse_args(argv=None):
                          "while they composite (0: all binned first); 'e,s1,...': side binning batches of s1, ... "
                          "views and one of the rest, each composited as soon as it is binned")
     ap.add_argument("--no-overlap", action="store_true", help="diagnostic: no side stream (uncontended phase times)")
+    ap.add_argument("--main-priority", type=int, default=0,
+                    help="run the step on a stream of this torch priority (negative = higher than the side stream's "
+                         "binning; 0: the current stream)")
     ap.add_argument("--side-priority", type=int, default=0,
                     help="torch stream priority of the side-stream binning (negative = higher)")
     ap.add_argument("--side-after-binning", action="store_true",
@@ -335,8 +338,14 @@ def run(args):
         render_view.flush = render.flush
     render_view.begin_step, render_view.end_step = render.begin_step, render.end_step   # the step's views
 
+    main_stream = torch.cuda.Stream(device=dev, priority=args.main_priority) if args.main_priority else None
+
     def step():
-        dp.run(render_view)                                # fwd+bwd per view, SUM all-reduce (RCCL) if world > 1
+        if main_stream is None:
+            dp.run(render_view)                            # fwd+bwd per view, SUM all-reduce (RCCL) if world > 1
+        else:                                              # the step's own stream, at a higher priority than the side
+            with torch.cuda.stream(main_stream):           # stream's binning
+                dp.run(render_view)
 
     for _ in range(args.warmup):
         step()
