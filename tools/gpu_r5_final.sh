@@ -3,7 +3,7 @@
 # legs, rocprofv3 kernel trace + stats, step timeline, PMC passes incl. the whole-step record)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out/r5f
+mkdir -p gpurun_out/r5f; rm -rf gpurun_out/r5p
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
     > gpurun_out/r5f/gpu_tests.txt 2>&1; rc=$?
 tail -3 gpurun_out/r5f/gpu_tests.txt
