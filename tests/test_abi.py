@@ -59,6 +59,14 @@ def test_size_queries():
     assert lib.lsr_img_bytes(1352, 1014) >= 1352 * 1014 * 8
     assert lib.lsr_backward_bytes(2_000_000, 8_600_000, 32, 0) >= 2_000_000 * 48
     assert lib.lsr_backward_bytes(2_000_000, 8_600_000, 32, 1) >= 8_600_000 * 44 * 4
+    # the tile-bucket binning: the sort path's layout (the compositors read its point list), then the
+    # per-block tile count table and the long buckets' 8-byte merge workspace
+    K, P, W, H = 8_600_000, 2_000_000, 1352, 1014
+    tiles = ((W + 15) // 16) * ((H + 15) // 16)
+    tb = lib.lsr_binning_bytes_tb(K, P, W, H)
+    assert tb >= lib.lsr_binning_bytes(K) + 8 * K + 4 * tiles * (P // 16384)
+    assert lib.lsr_binning_bytes_tb(K, 2 * P, W, H) > tb                  # more Gaussians: more table rows
+    assert lib.lsr_binning_bytes_tb(K, P, 0, H) == -1                     # invalid image size
 
 
 def test_settings_validation_messages():
