@@ -146,35 +146,50 @@ __device__ __forceinline__ Tap tap_of(const DeformArgs& a, int pi, int ci, const
     t.fx = ix - (float)t.x0; t.fy = iy - (float)t.y0;
     return t;
 }
-#ifdef LSR_FEAT_SCALAR
-// Diagnostic build (tools/deform_slp_bisect.sh feat_scalar): the HexPlane product's arithmetic as
-// scalar VALU instructions the SLP vectorizer cannot pair (same IEEE operations, same bits), so a
-// build with SLP on differs from the shipped one only outside features_to_lds.
+// Diagnostic builds (tools/deform_slp_bisect.sh): parts of the HexPlane sampling product's arithmetic
+// as scalar VALU instructions the SLP vectorizer cannot pair (same IEEE operations, same bits), so a
+// build with SLP on differs from the shipped one only there.  LSR_FEAT_SCALAR: all of it;
+// LSR_FEAT_SCALAR_W: the bilinear weights; _SUM: the weighted tap sums; _PROD: the six-plane product.
+#if defined(LSR_FEAT_SCALAR)
+#define LSR_FEAT_SCALAR_W
+#define LSR_FEAT_SCALAR_SUM
+#define LSR_FEAT_SCALAR_PROD
+#endif
+#if defined(LSR_FEAT_SCALAR_W) || defined(LSR_FEAT_SCALAR_SUM) || defined(LSR_FEAT_SCALAR_PROD)
 __device__ __forceinline__ float smul(float x, float y) { float r; asm volatile("v_mul_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y)); return r; }
 __device__ __forceinline__ float sadd(float x, float y) { float r; asm volatile("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y)); return r; }
+#endif
+#ifdef LSR_FEAT_SCALAR_W
+#define FW_MUL(x, y) smul((x), (y))
+#define FW_SUB1(x) sadd(1.0f, -(x))
+#else
+#define FW_MUL(x, y) ((x) * (y))
+#define FW_SUB1(x) (1.0f - (x))
+#endif
+#ifdef LSR_FEAT_SCALAR_SUM
+#define FS_MUL(x, y) smul((x), (y))
+#define FS_ADD(x, y) sadd((x), (y))
+#else
+#define FS_MUL(x, y) ((x) * (y))
+#define FS_ADD(x, y) ((x) + (y))
+#endif
+#ifdef LSR_FEAT_SCALAR_PROD
+#define FP_MUL(x, y) smul((x), (y))
+#else
+#define FP_MUL(x, y) ((x) * (y))
 #endif
 __device__ __forceinline__ float4 sample4(const DeformArgs& a, int pi, const Tap& t, int q) {
     const int W = a.pw[pi];
     const float4* pl = reinterpret_cast<const float4*>(a.planes + a.poff[pi]) + q;
     const float4 v00 = pl[(t.y0 * W + t.x0) * 4], v01 = pl[(t.y0 * W + t.x1) * 4];
     const float4 v10 = pl[(t.y1 * W + t.x0) * 4], v11 = pl[(t.y1 * W + t.x1) * 4];
-#ifdef LSR_FEAT_SCALAR
-    {
-        const float ufx = sadd(1.0f, -t.fx), ufy = sadd(1.0f, -t.fy);
-        const float w00 = smul(ufx, ufy), w01 = smul(t.fx, ufy), w10 = smul(ufx, t.fy), w11 = smul(t.fx, t.fy);
-        auto c = [&](float a0, float a1, float a2, float a3) {
-            return sadd(sadd(sadd(smul(a0, w00), smul(a1, w01)), smul(a2, w10)), smul(a3, w11));
-        };
-        return make_float4(c(v00.x, v01.x, v10.x, v11.x), c(v00.y, v01.y, v10.y, v11.y), c(v00.z, v01.z, v10.z, v11.z),
-                           c(v00.w, v01.w, v10.w, v11.w));
-    }
-#endif
-    const float w00 = (1.0f - t.fx) * (1.0f - t.fy), w01 = t.fx * (1.0f - t.fy), w10 = (1.0f - t.fx) * t.fy,
-                w11 = t.fx * t.fy;
-    return make_float4(v00.x * w00 + v01.x * w01 + v10.x * w10 + v11.x * w11,
-                       v00.y * w00 + v01.y * w01 + v10.y * w10 + v11.y * w11,
-                       v00.z * w00 + v01.z * w01 + v10.z * w10 + v11.z * w11,
-                       v00.w * w00 + v01.w * w01 + v10.w * w10 + v11.w * w11);
+    const float ufx = FW_SUB1(t.fx), ufy = FW_SUB1(t.fy);
+    const float w00 = FW_MUL(ufx, ufy), w01 = FW_MUL(t.fx, ufy), w10 = FW_MUL(ufx, t.fy), w11 = FW_MUL(t.fx, t.fy);
+    auto c = [&](float a0, float a1, float a2, float a3) {   // left to right, as the reference's sum
+        return FS_ADD(FS_ADD(FS_ADD(FS_MUL(a0, w00), FS_MUL(a1, w01)), FS_MUL(a2, w10)), FS_MUL(a3, w11));
+    };
+    return make_float4(c(v00.x, v01.x, v10.x, v11.x), c(v00.y, v01.y, v10.y, v11.y), c(v00.z, v01.z, v10.z, v11.z),
+                       c(v00.w, v01.w, v10.w, v11.w));
 }
 
 // Stage 1 of both passes: the block's features into LDS rows (bf16 hi/lo, pitch XP), optionally
@@ -192,11 +207,8 @@ __device__ __forceinline__ void features_to_lds(const DeformArgs& a, int g0, __b
         for (int ci = 0; ci < 6; ++ci) {
             const int pi = 6 * s + ci;
             const float4 v = sample4(a, pi, tap_of(a, pi, ci, crd), q);
-#ifdef LSR_FEAT_SCALAR
-            prod.x = smul(prod.x, v.x); prod.y = smul(prod.y, v.y); prod.z = smul(prod.z, v.z); prod.w = smul(prod.w, v.w);
-#else
-            prod.x *= v.x; prod.y *= v.y; prod.z *= v.z; prod.w *= v.w;
-#endif
+            prod.x = FP_MUL(prod.x, v.x); prod.y = FP_MUL(prod.y, v.y); prod.z = FP_MUL(prod.z, v.z);
+            prod.w = FP_MUL(prod.w, v.w);
 #ifdef LSR_DEFORM_FEAT_WAIT
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 #endif

@@ -21,3 +21,7 @@ build ${ONLY:-slp}
 build slp_pad1 -Xarch_device -mllvm=-amdgpu-snop-padding=1
 build slp_pad2 -Xarch_device -mllvm=-amdgpu-snop-padding=2
 build slp_feat_scalar -DLSR_FEAT_SCALAR
+# round 5, second level: which part of features_to_lds (bilinear weights, tap sums, plane product)
+build slp_feat_w -DLSR_FEAT_SCALAR_W
+build slp_feat_sum -DLSR_FEAT_SCALAR_SUM
+build slp_feat_prod -DLSR_FEAT_SCALAR_PROD
