@@ -184,7 +184,21 @@ __device__ __forceinline__ float4 sample4(const DeformArgs& a, int pi, const Tap
     const float4 v00 = pl[(t.y0 * W + t.x0) * 4], v01 = pl[(t.y0 * W + t.x1) * 4];
     const float4 v10 = pl[(t.y1 * W + t.x0) * 4], v11 = pl[(t.y1 * W + t.x1) * 4];
     const float ufx = FW_SUB1(t.fx), ufy = FW_SUB1(t.fy);
+#ifdef LSR_FEAT_BCAST_ASM
+    // Diagnostic build: the four weights as the broadcast packed products the SLP build forms
+    // (v_pk_mul_f32 op_sel:[0,1] op_sel_hi:[0,1]: both halves = A.lo * B.hi), but never in place
+    // (early-clobber destinations), everything else left to the vectorizer
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    const f2v U = {ufx, ufy}, F = {t.fx, t.fy};
+    f2v P00, P01, P10, P11;
+    asm volatile("v_pk_mul_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[0,1]" : "=&v"(P00) : "v"(U));
+    asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[0,1]" : "=&v"(P01) : "v"(F), "v"(U));
+    asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[0,1]" : "=&v"(P10) : "v"(U), "v"(F));
+    asm volatile("v_pk_mul_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[0,1]" : "=&v"(P11) : "v"(F));
+    const float w00 = P00.x, w01 = P01.x, w10 = P10.x, w11 = P11.x;
+#else
     const float w00 = FW_MUL(ufx, ufy), w01 = FW_MUL(t.fx, ufy), w10 = FW_MUL(ufx, t.fy), w11 = FW_MUL(t.fx, t.fy);
+#endif
     auto c = [&](float a0, float a1, float a2, float a3) {   // left to right, as the reference's sum
         return FS_ADD(FS_ADD(FS_ADD(FS_MUL(a0, w00), FS_MUL(a1, w01)), FS_MUL(a2, w10)), FS_MUL(a3, w11));
     };

@@ -13,6 +13,11 @@
 //   mode 1  the same with s_nop 0 between them
 //   mode 2  broadcast producer -> consumer with s_nop 1
 //   mode 3  scalar v_mul_f32 chain (the -fno-slp-vectorize form)
+//   mode 4  the broadcast IN PLACE (destination = source pair, as 19 of the failing build's 48
+//           broadcasts are: v_pk_mul_f32 v[n:n+1], v[n:n+1], v[n:n+1] op_sel:[0,1] op_sel_hi:[0,1]),
+//           its source pair written by the packed move just before it, then the consumer
+//   mode 5  the in-place broadcast on a pair written long before, then the consumer
+// (round 5: the in-place form is the one only the failing build contains; modes 0-3 never mismatched)
 // Every result is a correctly rounded IEEE product or sum, so the expected values are exact on the host.
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -50,6 +55,16 @@ __global__ void __launch_bounds__(256) k_pk(const float2* __restrict__ w, const 
                              "s_nop 1\n\t"
                              "v_pk_mul_f32 %0, %2, %0"
                              : "=&v"(r) : "v"(wv), "v"(dv[j]));
+            } else if constexpr (MODE == 4) {
+                asm volatile("v_pk_mov_b32 %0, %1, %1 op_sel:[0,1]\n\t"
+                             "v_pk_mul_f32 %0, %0, %0 op_sel:[0,1] op_sel_hi:[0,1]\n\t"
+                             "v_pk_mul_f32 %0, %2, %0"
+                             : "=&v"(r) : "v"(wv), "v"(dv[j]));
+            } else if constexpr (MODE == 5) {
+                r = wv;
+                asm volatile("v_pk_mul_f32 %0, %0, %0 op_sel:[0,1] op_sel_hi:[0,1]\n\t"
+                             "v_pk_mul_f32 %0, %1, %0"
+                             : "+v"(r) : "v"(dv[j]));
             } else {
                 float p;
                 asm volatile("v_mul_f32 %0, %1, %2" : "=v"(p) : "v"(wv.x), "v"(wv.y));
@@ -95,16 +110,18 @@ int main(int argc, char** argv) {
     (void)hipMemcpy(dd, hd.data(), hd.size() * 8, hipMemcpyHostToDevice);
     const int reps = argc > 1 ? atoi(argv[1]) : 20;
     const size_t lds_for[3] = {100 * 1024, 70 * 1024, 36 * 1024};   // 1, 2, 4 blocks per CU
-    const char* names[4] = {"broadcast->consumer back to back", "broadcast, s_nop 0, consumer",
-                            "broadcast, s_nop 1, consumer", "scalar v_mul_f32"};
-    int total_bad = 0, bad_modes[4] = {0, 0, 0, 0};
+    const char* names[6] = {"broadcast->consumer back to back", "broadcast, s_nop 0, consumer",
+                            "broadcast, s_nop 1, consumer", "scalar v_mul_f32",
+                            "pk_mov -> in-place broadcast -> consumer", "in-place broadcast -> consumer"};
+    int total_bad = 0, bad_modes[6] = {0, 0, 0, 0, 0, 0};
     std::vector<float2> o(T);
-    for (int mode = 0; mode < 4; ++mode) {
+    for (int mode = 0; mode < 6; ++mode) {
         for (int li = 0; li < 3; ++li) {
             long bad = 0, bad_lo = 0, bad_hi = 0, by_quarter[4] = {0, 0, 0, 0};
             for (int r = 0; r < reps; ++r) {
                 (void)hipMemset(dout, 0xFF, T * 8);
-                auto kern = mode == 0 ? k_pk<0> : mode == 1 ? k_pk<1> : mode == 2 ? k_pk<2> : k_pk<3>;
+                auto kern = mode == 0 ? k_pk<0> : mode == 1 ? k_pk<1> : mode == 2 ? k_pk<2> : mode == 3 ? k_pk<3>
+                          : mode == 4 ? k_pk<4> : k_pk<5>;
                 hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), lds_for[li], 0, dw, dd, dout, n_per);
                 if (hipDeviceSynchronize() != hipSuccess) { printf("launch failed\n"); return 2; }
                 (void)hipMemcpy(o.data(), dout, T * 8, hipMemcpyDeviceToHost);
@@ -125,6 +142,6 @@ int main(int argc, char** argv) {
     }
     printf("packed fp32 co-residency: %s\n", total_bad ? "MISMATCHES" : "ok");
     // the exit status reports the forms the build uses: the scalar chain (mode 3) and the nop-separated
-    // packed forms must be exact; mode 0 is the reproducer and only reported
+    // packed forms must be exact; modes 0, 4 and 5 are the reproducer candidates and only reported
     return (bad_modes[1] || bad_modes[2] || bad_modes[3]) ? 1 : 0;
 }

@@ -16,8 +16,9 @@ build() {   # name, extra flags...
 }
 # results (round 5, tools/gpu_deform_race.sh): slp, slp_pad1 and slp_pad2 corrupt (pad: more rows);
 # slp_wz faulted in the forward (illegal address) and is not built any more
-build ${ONLY:-slp}
-[ -n "$ONLY" ] && exit 0
+[ -z "$ONLY" ] && build slp
+[ "$ONLY" = slp ] && { build slp; exit 0; }
+[ "$ONLY" = slp_bcast_asm ] && { build slp_bcast_asm -DLSR_FEAT_BCAST_ASM; exit 0; }
 build slp_pad1 -Xarch_device -mllvm=-amdgpu-snop-padding=1
 build slp_pad2 -Xarch_device -mllvm=-amdgpu-snop-padding=2
 build slp_feat_scalar -DLSR_FEAT_SCALAR
@@ -25,3 +26,5 @@ build slp_feat_scalar -DLSR_FEAT_SCALAR
 build slp_feat_w -DLSR_FEAT_SCALAR_W
 build slp_feat_sum -DLSR_FEAT_SCALAR_SUM
 build slp_feat_prod -DLSR_FEAT_SCALAR_PROD
+# the weights as the SLP build's broadcast products, but never in place (inline asm, early clobber)
+build slp_bcast_asm -DLSR_FEAT_BCAST_ASM
