@@ -191,10 +191,20 @@ __device__ __forceinline__ float4 sample4(const DeformArgs& a, int pi, const Tap
     typedef float f2v __attribute__((ext_vector_type(2)));
     const f2v U = {ufx, ufy}, F = {t.fx, t.fy};
     f2v P00, P01, P10, P11;
-    asm volatile("v_pk_mul_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[0,1]" : "=&v"(P00) : "v"(U));
-    asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[0,1]" : "=&v"(P01) : "v"(F), "v"(U));
-    asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[0,1]" : "=&v"(P10) : "v"(U), "v"(F));
-    asm volatile("v_pk_mul_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[0,1]" : "=&v"(P11) : "v"(F));
+#if defined(LSR_FEAT_BCAST_NOP_BEFORE)   // A/B: wait states between the operands' producers and the broadcast
+#define BC_PRE "s_nop 4\n\t"
+#define BC_POST ""
+#elif defined(LSR_FEAT_BCAST_NOP_AFTER)  // A/B: wait states between the broadcast and its consumers
+#define BC_PRE ""
+#define BC_POST "\n\ts_nop 4"
+#else
+#define BC_PRE ""
+#define BC_POST ""
+#endif
+    asm volatile(BC_PRE "v_pk_mul_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[0,1]" BC_POST : "=&v"(P00) : "v"(U));
+    asm volatile(BC_PRE "v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[0,1]" BC_POST : "=&v"(P01) : "v"(F), "v"(U));
+    asm volatile(BC_PRE "v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[0,1]" BC_POST : "=&v"(P10) : "v"(U), "v"(F));
+    asm volatile(BC_PRE "v_pk_mul_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[0,1]" BC_POST : "=&v"(P11) : "v"(F));
     const float w00 = P00.x, w01 = P01.x, w10 = P10.x, w11 = P11.x;
 #else
     const float w00 = FW_MUL(ufx, ufy), w01 = FW_MUL(t.fx, ufy), w10 = FW_MUL(ufx, t.fy), w11 = FW_MUL(t.fx, t.fy);
