@@ -22,6 +22,23 @@ namespace lsr {
 
 // Diagnostic build (-DLSR_DEFORM_DIAG): the plane scatter checks every staged tap offset and value
 // and counts the bad ones (lsr_debug_deform_diag) instead of adding them.
+// Diagnostic build only (-DLSR_DEFORM_STAMPS): wave 0 of every phase-A block sums per-segment
+// s_memtime cycles into g_deform_stamps (lsr_debug_deform_stamps; tools/deform_stamps.py).  Shares, not
+// times: the stamps cost cycles and constrain the schedule.
+#ifdef LSR_DEFORM_STAMPS
+__device__ unsigned long long g_deform_stamps[16];
+#define DSTAMP(seg)                                                                              \
+    do {                                                                                         \
+        __builtin_amdgcn_sched_barrier(0);                                                       \
+        unsigned long long t_;                                                                   \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");             \
+        __builtin_amdgcn_sched_barrier(0);                                                       \
+        if ((seg) >= 0) ds_sum[(seg)] += t_ - ds_prev;                                           \
+        ds_prev = t_;                                                                            \
+    } while (0)
+#else
+#define DSTAMP(seg) do {} while (0)
+#endif
 #ifdef LSR_DEFORM_DIAG
 __device__ unsigned long long g_deform_diag[8];
 #endif
@@ -521,10 +538,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
     const int g0 = blockIdx.x * DN;
     const int col = 32 * wave + (lane & 31), hh = lane >> 5;
     const int L = DEEP ? a.nlayers : 1;
+#ifdef LSR_DEFORM_STAMPS
+    unsigned long long ds_sum[13] = {}, ds_prev = 0;
+#endif
+    DSTAMP(-1);
 
     // ---- features (as the forward), saved as fp32 for the first layer's weight gradient ---------
     features_to_lds<S>(a, g0, s_xh, s_xl, XP, b.sX);
     __syncthreads();
+    DSTAMP(0);
 
     // ---- chain forward, A_k = relu(H_k) saved ------------------------------------------------------
     int cur = 0;
@@ -548,6 +570,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
     const __bf16 *ah = s_hh[cur], *al = s_hl[cur];
     __bf16 *bh = s_hh[cur ^ 1], *bl = s_hl[cur ^ 1];
 
+    DSTAMP(1);
     df32x16 dA[2] = {df32x16{}, df32x16{}};
 #ifdef LSR_DEFORM_ABL_NOHEADS   // timing ablation only (wrong gradients): the heads' share of phase A
     if (a.P < 0)
@@ -567,6 +590,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
 #pragma unroll
                 for (int q = 0; q < 16; ++q) zpos |= z[mt][q] + bias > 0.0f ? 1u << (16 * mt + q) : 0u;
         }
+        DSTAMP(2);
         const float* G = coff ? b.sG_coff : quat ? b.sG_rot : b.up[hd];   // saved by the GRAD pass
         if (nout <= DEF_SMALL_OUT) {                                 // block-uniform
             // dZ1 = (G W2) [Z1 > 0] on the VALU from fp32 G rows (k_head_wgrad's small-output path)
@@ -580,7 +604,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
             }
             float w2c[DEF_SMALL_OUT];
             w2_column(a.w2_h[hd], a.w2_l[hd], col, w2c);
+            DSTAMP(8);         // small head: G and W2 column loads issued, G rows stored
             __syncthreads();   // G rows complete
+            DSTAMP(9);         // small head: the first barrier
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
@@ -598,11 +624,35 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
                     bl[r * DAP + col] = lo;
                 }
             __syncthreads();   // dZ1 rows complete
+            DSTAMP(3);
             mlp_ntile<DWID>(dA, bh, bl, DAP, wave, b.w1t_h[hd], b.w1t_l[hd]);
+            DSTAMP(4);
             __syncthreads();   // dZ1 rows and the G rows consumed before the next head rewrites them
+            DSTAMP(5);
             continue;
         }
-        // gradient rows of this head's output, K padded to 64, in the buffer dZ1 takes next
+        // gradient rows of this head's output, K padded to 64, in the buffer dZ1 takes next: every load
+        // of the thread issued before the first conversion (a load-convert-store loop waited one memory
+        // latency per row: 12 % of phase A in the stamp build)
+#ifndef LSR_DEFORM_G_LOOP
+        {
+            constexpr int NJ = DN * 64 / 256;
+            float gv[NJ];
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int i = tid + 256 * j, r = i >> 6, k = i & 63, g = g0 + r;
+                gv[j] = (k < nout && g < a.P) ? G[(size_t)g * nout + k] : 0.0f;
+            }
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int i = tid + 256 * j, r = i >> 6, k = i & 63;
+                __bf16 hi, lo;
+                dsplit(gv[j], hi, lo);
+                bh[r * DGP + k] = hi;
+                bl[r * DGP + k] = lo;
+            }
+        }
+#else   // A/B: the round-4 loop
         for (int i = tid; i < DN * 64; i += 256) {
             const int r = i >> 6, k = i & 63, g = g0 + r;
             float v = 0.0f;
@@ -612,9 +662,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
             bh[r * DGP + k] = hi;
             bl[r * DGP + k] = lo;
         }
+#endif
+        DSTAMP(10);        // SH head: G rows loaded and stored
         __syncthreads();   // G rows complete
         df32x16 d[2] = {df32x16{}, df32x16{}};
         mlp_ntile<64>(d, bh, bl, DGP, wave, b.w2t_h[hd], b.w2t_l[hd]);
+        DSTAMP(11);        // SH head: barrier + G W2 product
         __syncthreads();   // every wave has read the G rows: dZ1 overwrites them
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt)
@@ -628,8 +681,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
                 bl[r * DAP + col] = lo;
             }
         __syncthreads();   // dZ1 rows complete
+        DSTAMP(3);
         mlp_ntile<DWID>(dA, bh, bl, DAP, wave, b.w1t_h[hd], b.w1t_l[hd]);
+        DSTAMP(4);
         __syncthreads();   // dZ1 rows consumed before the next head's G rows overwrite them
+        DSTAMP(5);
     }
 
     // ---- back through the chain: dH_k = dA_k * [H_k > 0] (saved), dA_{k-1} = dH_k W_k -------------
@@ -672,6 +728,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
         }
     }
     __syncthreads();
+    DSTAMP(6);
     const float* s_dx = reinterpret_cast<const float*>(s_hh[cur ^ 1]);   // [64][F + 1]
     // plane-scatter staging in the lo half of that buffer: per wave, dv of 16 Gaussians [16][17],
     // their 4 tap offsets and bilinear weights
@@ -690,10 +747,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
         float crd[4];
         coords(a, g, crd);
         float dq[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-        for (int s = 0; s < S; ++s) {
-            // each plane's 4 taps loaded once: the sample (sample4's arithmetic) and its x / y derivatives
-            // (the coordinate gradient); 72 registers for the scale instead of re-reading the taps
+        // a scale's plane gradients dv (24 registers) and its coordinate gradient: each plane's 4 taps
+        // loaded once for the sample (sample4's arithmetic) and its x / y derivatives
+        auto grad_scale = [&](int s, float4 (&dvo)[6]) __attribute__((always_inline)) {
             float4 v[6], gxv[6], gyv[6];
 #pragma unroll
             for (int ci = 0; ci < 6; ++ci) {
@@ -725,52 +781,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
                         oth.x *= v[cj].x; oth.y *= v[cj].y; oth.z *= v[cj].z; oth.w *= v[cj].w;
                     }
                 const float dv[4] = {dxv[0] * oth.x, dxv[1] * oth.y, dxv[2] * oth.z, dxv[3] * oth.w};
+                dvo[ci] = make_float4(dv[0], dv[1], dv[2], dv[3]);
                 const int pi = 6 * s + ci;
                 const int W = a.pw[pi], H = a.ph[pi];
                 const float rx = (crd[kC0(ci)] + 1.0f) * 0.5f * (float)(W - 1);
                 const float ry = (crd[kC1(ci)] + 1.0f) * 0.5f * (float)(H - 1);
-                const Tap t = tap_of(a, pi, ci, crd);
-                const float w00 = (1.0f - t.fx) * (1.0f - t.fy), w01 = t.fx * (1.0f - t.fy),
-                            w10 = (1.0f - t.fx) * t.fy, w11 = t.fx * t.fy;
-                // scatter: stage the wave's 16 Gaussians (16 channels, 4 taps each) in LDS, then one
-                // atomic instruction per Gaussian covers its 4 taps x 16 channels = four full
-                // 64-byte segments (lane = 16 tap + channel) instead of 16 partial ones; blocks add
-                // into one of b.replicas copies of the gradient planes (summed by the unpack), so
-                // the few cells every Gaussian of a frame shares (the time planes) are not one hot spot
-                {
-                    const int wl = gl & 15;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) s_sdv[(wave * 16 + wl) * 17 + 4 * q + i] = ok ? dv[i] : 0.0f;
-                    if (q == 0) {
-                        int* so = s_soff + (wave * 16 + wl) * 4;
-                        float* sw = s_sw + (wave * 16 + wl) * 4;
-                        so[0] = (t.y0 * W + t.x0) * 16; so[1] = (t.y0 * W + t.x1) * 16;
-                        so[2] = (t.y1 * W + t.x0) * 16; so[3] = (t.y1 * W + t.x1) * 16;
-                        sw[0] = w00; sw[1] = w01; sw[2] = w10; sw[3] = w11;
-                    }
-                    wave_lds_sync();
-                    float* gp = b.dplanes + (size_t)(blockIdx.x % b.replicas) * b.plane_stride + a.poff[pi];
-                    const int tap = lane >> 4, ch = lane & 15;
-#pragma unroll 4
-                    for (int j = 0; j < 16; ++j) {
-                        const float val = s_sdv[(wave * 16 + j) * 17 + ch] * s_sw[(wave * 16 + j) * 4 + tap];
-#ifdef LSR_DEFORM_DIAG
-                        const int off = s_soff[(wave * 16 + j) * 4 + tap];
-                        if (off < 0 || off >= W * H * 16 || !(fabsf(val) < 1e30f)) {
-                            atomicAdd(&g_deform_diag[0], 1ull);
-                            atomicAdd(&g_deform_diag[1 + tap], 1ull);
-                            continue;
-                        }
-#endif
-#ifndef LSR_DEFORM_ABL_NOSCATTER   // timing ablation only (wrong plane gradients)
-#ifdef LSR_DEFORM_ABL_NOTIME        // timing ablation only: the time planes' (xt, yt, zt) atomics skipped
-                        if (ci == 2 || ci >= 4) continue;
-#endif
-                        if (val != 0.0f) atomicAdd(gp + s_soff[(wave * 16 + j) * 4 + tap] + ch, val);
-#endif
-                    }
-                    wave_lds_sync();   // staging read before the next plane rewrites it
-                }
                 const float gx4[4] = {gxv[ci].x, gxv[ci].y, gxv[ci].z, gxv[ci].w};
                 const float gy4[4] = {gyv[ci].x, gyv[ci].y, gyv[ci].z, gyv[ci].w};
                 float dix = 0.0f, diy = 0.0f;
@@ -782,7 +797,75 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
                 if (rx > 0.0f && rx < (float)(W - 1)) dq[kC0(ci)] += dix * 0.5f * (float)(W - 1);
                 if (ry > 0.0f && ry < (float)(H - 1)) dq[kC1(ci)] += diy * 0.5f * (float)(H - 1);
             }
+        };
+        // scatter: stage the wave's 16 Gaussians (16 channels, 4 taps each) in LDS, then one atomic
+        // instruction per Gaussian covers its 4 taps x 16 channels = four full 64-byte segments (lane =
+        // 16 tap + channel) instead of 16 partial ones; blocks add into one of b.replicas copies of the
+        // gradient planes (summed by the unpack), so the few cells every Gaussian of a frame shares (the
+        // time planes) are not one hot spot
+        auto scatter_scale = [&](int s, const float4 (&dvo)[6]) __attribute__((always_inline)) {
+#pragma unroll
+            for (int ci = 0; ci < 6; ++ci) {
+                const int pi = 6 * s + ci, W = a.pw[pi];
+                const Tap t = tap_of(a, pi, ci, crd);
+                const float dv[4] = {dvo[ci].x, dvo[ci].y, dvo[ci].z, dvo[ci].w};
+                const float w00 = (1.0f - t.fx) * (1.0f - t.fy), w01 = t.fx * (1.0f - t.fy),
+                            w10 = (1.0f - t.fx) * t.fy, w11 = t.fx * t.fy;
+                const int wl = gl & 15;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) s_sdv[(wave * 16 + wl) * 17 + 4 * q + i] = ok ? dv[i] : 0.0f;
+                if (q == 0) {
+                    int* so = s_soff + (wave * 16 + wl) * 4;
+                    float* sw = s_sw + (wave * 16 + wl) * 4;
+                    so[0] = (t.y0 * W + t.x0) * 16; so[1] = (t.y0 * W + t.x1) * 16;
+                    so[2] = (t.y1 * W + t.x0) * 16; so[3] = (t.y1 * W + t.x1) * 16;
+                    sw[0] = w00; sw[1] = w01; sw[2] = w10; sw[3] = w11;
+                }
+                wave_lds_sync();
+                float* gp = b.dplanes + (size_t)(blockIdx.x % b.replicas) * b.plane_stride + a.poff[pi];
+                const int tap = lane >> 4, ch = lane & 15;
+#pragma unroll 4
+                for (int j = 0; j < 16; ++j) {
+                    const float val = s_sdv[(wave * 16 + j) * 17 + ch] * s_sw[(wave * 16 + j) * 4 + tap];
+#ifdef LSR_DEFORM_DIAG
+                    const int off = s_soff[(wave * 16 + j) * 4 + tap];
+                    const int H = a.ph[pi];
+                    if (off < 0 || off >= W * H * 16 || !(fabsf(val) < 1e30f)) {
+                        atomicAdd(&g_deform_diag[0], 1ull);
+                        atomicAdd(&g_deform_diag[1 + tap], 1ull);
+                        continue;
+                    }
+#endif
+#ifndef LSR_DEFORM_ABL_NOSCATTER   // timing ablation only (wrong plane gradients)
+#ifdef LSR_DEFORM_ABL_NOTIME        // timing ablation only: the time planes' (xt, yt, zt) atomics skipped
+                    if (ci == 2 || ci >= 4) continue;
+#endif
+                    if (val != 0.0f) atomicAdd(gp + s_soff[(wave * 16 + j) * 4 + tap] + ch, val);
+#endif
+                }
+                wave_lds_sync();   // staging read before the next plane rewrites it
+            }
+        };
+#ifndef LSR_DEFORM_HEX_INTERLEAVED
+        {
+            // every scale's taps loaded (and its coordinate gradient formed) before the first scatter:
+            // vmcnt retires in order and counts the atomics, so tap loads issued behind a scale's
+            // atomics waited for them; the scales' dv (24 registers each) stay live in between
+            float4 dvo[S][6];
+#pragma unroll
+            for (int s = 0; s < S; ++s) grad_scale(s, dvo[s]);
+            DSTAMP(12);        // taps, dv and the coordinate gradient of every scale
+#pragma unroll
+            for (int s = 0; s < S; ++s) scatter_scale(s, dvo[s]);
         }
+#else
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            float4 dvo[6];
+            grad_scale(s, dvo);
+            scatter_scale(s, dvo);
+        }
+#endif
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             dq[c] += __shfl_xor(dq[c], 1);
@@ -817,6 +900,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
             }
         }
     }
+#ifdef LSR_DEFORM_STAMPS
+    DSTAMP(7);
+    if (tid == 0) {
+#pragma unroll
+        for (int k = 0; k < 13; ++k) atomicAdd(&g_deform_stamps[k], ds_sum[k]);
+        atomicAdd(&g_deform_stamps[13], 1ull);
+    }
+#endif
 }
 
 template <int S>
@@ -1516,6 +1607,13 @@ void launch_pack_weight(const float* src, __bf16* hi, __bf16* lo, int rows, int 
 
 }  // namespace lsr
 
+#ifdef LSR_DEFORM_STAMPS
+extern "C" int lsr_debug_deform_stamps(unsigned long long* out14) {   // 13 segments + blocks; read and reset
+    if (hipMemcpyFromSymbol(out14, HIP_SYMBOL(lsr::g_deform_stamps), 14 * sizeof(unsigned long long)) != hipSuccess) return 2;
+    unsigned long long z[16] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(lsr::g_deform_stamps), z, sizeof(z)) == hipSuccess ? 0 : 2;
+}
+#endif
 #ifdef LSR_DEFORM_DIAG
 // diagnostic export (not part of include/lsr_deform.h): read and reset the counters
 extern "C" int lsr_debug_deform_diag(unsigned long long* out8) {

@@ -266,8 +266,8 @@ lsr::LangDeformArgs lang_args(const lsr_deform_net* net, const void* workspace, 
     return a;
 }
 
-// backward scratch: saved activations, then kGradReplicas copies of the packed gradient planes
-constexpr int kGradReplicas = 16;   // the most; deform_replicas(P) picks the count of a call
+// backward scratch: saved activations, then deform_replicas(P) copies of the packed gradient planes
+constexpr int kGradReplicas = 16;   // the most LSR_DEFORM_REPLICAS may ask for
 // Replica count of a call (every copy is zeroed and summed by the unpack, 9.5 MB each for the Neu3D
 // planes).  LSR_DEFORM_REPLICAS overrides (diagnostic A/B).
 int deform_replicas(size_t P) {

@@ -99,9 +99,11 @@ def test_backward_matches_reference_golden():
         assert _rel(g.cpu().numpy().reshape(ref.shape), ref) < 1e-4, name
 
 
-@pytest.mark.parametrize("P,time", [(20000, 0.37), (777, -0.8)])
+@pytest.mark.parametrize("P,time", [(20000, 0.37), (777, -0.8), (3000, 1.0), (3000, -1.0)])
 def test_backward_matches_oracle_at_neu3d_resolution(P, time):
-    """Neu3D resolution (64^3 x 150, multires [1, 2]); gradients accumulate over two calls."""
+    """Neu3D resolution (64^3 x 150, multires [1, 2]); gradients accumulate over two calls.  One time
+    for all Gaussians (the render path); +-1 put the time planes' taps on the clamped border rows
+    (y1 == y0 at +1, weight 0 on the second row at -1)."""
     params, res, multires, inp = _neu3d_case(P, seed=3)
     # the bilinear slope jumps at grid lines: keep the points 1e-3 cells away from every line (and
     # from the clamped borders), where float32 and float64 coordinates could pick different cells

@@ -19,6 +19,22 @@ from deformation import DeformationField, HEADS, HEAD_OUT  # noqa: E402
 BF16_DENSE_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: dense bf16 MFMA
 
 
+def _stamps_fn():
+    """lsr_debug_deform_stamps of a -DLSR_DEFORM_STAMPS build (LSR_LIBRARY), else None: read-and-reset."""
+    import ctypes
+    from diff_gaussian_rasterization import _lib
+    try:
+        fn = _lib.load().lsr_debug_deform_stamps
+    except AttributeError:
+        return None
+    buf = (ctypes.c_ulonglong * 14)()
+
+    def read():
+        fn(buf)
+        return list(buf)
+    return read
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gaussians", type=int, default=2_000_000)
@@ -81,12 +97,23 @@ def main():
     for _ in range(2):
         field.backward(means, 0.4, *ups)
     torch.cuda.synchronize()
+    stamps = _stamps_fn()            # diagnostic build only (-DLSR_DEFORM_STAMPS)
+    if stamps is not None:
+        stamps()
     e0.record()
     for _ in range(args.iters // 2):
         field.backward(means, 0.4, *ups)
     e1.record()
     torch.cuda.synchronize()
     bms = e0.elapsed_time(e1) / (args.iters // 2)
+    if stamps is not None:
+        seg = stamps()
+        names = ["features", "chain_fwd", "head_Z1", "head_dZ1_rest", "head_dA", "head_closing_sync",
+                 "chain_bwd_dX", "hexplane_bwd", "small_G_loads", "small_first_sync", "sh_G_rows",
+                 "sh_sync_GW2", "hexplane_grads"]   # hexplane_bwd: the scatter after hexplane_grads
+        tot = sum(seg[:13]) or 1
+        print(json.dumps(dict(phase_a_stamps={n: round(v / tot, 4) for n, v in zip(names, seg[:13])},
+                              blocks=seg[13], note="wave 0 of each phase-A block, s_memtime cycles; shares")))
     # recompute of the forward MLP + data gradients (2 products per weight) + weight gradients (1)
     bflops = 2.0 * macs * 4 * P
     # rows written by the backward's phase A and read again (deform_api.hip bwd_scratch): the
