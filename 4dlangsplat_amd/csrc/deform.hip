@@ -579,6 +579,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
         if (!((a.heads >> hd) & 1u)) continue;                       // block-uniform
         const int nout = head_out(a, hd);
         const bool quat = hd == 2 && a.apply_rotation, coff = hd == 5;
+        const float* G = coff ? b.sG_coff : quat ? b.sG_rot : b.up[hd];   // saved by the GRAD pass
+        // a large head's gradient rows (K padded to 64, 16 per thread) loaded before its Z1 product,
+        // which hides their latency (issued after Z1, the conversion below waited for them: 12 % of
+        // phase A in the stamp build)
+        constexpr int NJ = DN * 64 / 256;
+        float gv[NJ];
+#ifndef LSR_DEFORM_SHG_LATE
+        if (nout > DEF_SMALL_OUT) {                                  // block-uniform
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int i = tid + 256 * j, r = i >> 6, k = i & 63, g = g0 + r;
+                gv[j] = (k < nout && g < a.P) ? G[(size_t)g * nout + k] : 0.0f;
+            }
+        }
+#endif
         // Z1 for this wave's 32 columns (its rows finish before the sync below)
         uint32_t zpos = 0;   // bit 16 mt + q: Z1 > 0 (the ReLU mask of dZ1; Z1 itself dies here)
         {
@@ -591,9 +606,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
                 for (int q = 0; q < 16; ++q) zpos |= z[mt][q] + bias > 0.0f ? 1u << (16 * mt + q) : 0u;
         }
         DSTAMP(2);
-        const float* G = coff ? b.sG_coff : quat ? b.sG_rot : b.up[hd];   // saved by the GRAD pass
         if (nout <= DEF_SMALL_OUT) {                                 // block-uniform
             // dZ1 = (G W2) [Z1 > 0] on the VALU from fp32 G rows (k_head_wgrad's small-output path)
+            // (loaded after Z1: issued before it, as the SH head's rows, measured 10.65-10.72 vs
+            // 10.47-10.54 ms at 2M, 13 VGPRs spilled)
             if (tid < DN) {
                 const int g = g0 + tid;
                 float v[DEF_SMALL_OUT] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -633,16 +649,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
         }
         // gradient rows of this head's output, K padded to 64, in the buffer dZ1 takes next: every load
         // of the thread issued before the first conversion (a load-convert-store loop waited one memory
-        // latency per row: 12 % of phase A in the stamp build)
+        // latency per row)
 #ifndef LSR_DEFORM_G_LOOP
         {
-            constexpr int NJ = DN * 64 / 256;
-            float gv[NJ];
+#ifdef LSR_DEFORM_SHG_LATE   // A/B: loaded here, after Z1
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
                 const int i = tid + 256 * j, r = i >> 6, k = i & 63, g = g0 + r;
                 gv[j] = (k < nout && g < a.P) ? G[(size_t)g * nout + k] : 0.0f;
             }
+#endif
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
                 const int i = tid + 256 * j, r = i >> 6, k = i & 63;
@@ -747,6 +763,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
         float crd[4];
         coords(a, g, crd);
         float dq[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        // every Gaussian of this wave at the call's first time (a vote, no barrier)
+        const bool t_row = b.trow && __all(crd[3] == a.time[0]);
         // a scale's plane gradients dv (24 registers) and its coordinate gradient: each plane's 4 taps
         // loaded once for the sample (sample4's arithmetic) and its x / y derivatives
         auto grad_scale = [&](int s, float4 (&dvo)[6]) __attribute__((always_inline)) {
@@ -809,9 +827,34 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
                 const int pi = 6 * s + ci, W = a.pw[pi];
                 const Tap t = tap_of(a, pi, ci, crd);
                 const float dv[4] = {dvo[ci].x, dvo[ci].y, dvo[ci].z, dvo[ci].w};
+                const int wl = gl & 15;
+                if ((ci == 2 || ci >= 4) && t_row) {   // wave-uniform
+                    // a time plane of a wave at time[0]: its x-row (b.trow), 2 taps x 16 channels per
+                    // Gaussian, two Gaussians per atomic instruction (half the time planes' requests)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) s_sdv[(wave * 16 + wl) * 17 + 4 * q + i] = ok ? dv[i] : 0.0f;
+                    if (q == 0) {
+                        s_soff[(wave * 16 + wl) * 4 + 0] = t.x0 * 16;
+                        s_soff[(wave * 16 + wl) * 4 + 1] = t.x1 * 16;
+                        s_sw[(wave * 16 + wl) * 4 + 0] = 1.0f - t.fx;
+                        s_sw[(wave * 16 + wl) * 4 + 1] = t.fx;
+                    }
+                    wave_lds_sync();
+                    float* rp = b.trow + (size_t)(blockIdx.x % b.trow_reps) * b.trow_stride + b.toff[pi];
+                    const int tap = (lane >> 4) & 1, ch = lane & 15, half = lane >> 5;
+#pragma unroll 4
+                    for (int j = 0; j < 8; ++j) {
+                        const int e = wave * 16 + 2 * j + half;
+                        const float val = s_sdv[e * 17 + ch] * s_sw[e * 4 + tap];
+#ifndef LSR_DEFORM_ABL_NOTIME
+                        if (val != 0.0f) atomicAdd(rp + s_soff[e * 4 + tap] + ch, val);
+#endif
+                    }
+                    wave_lds_sync();   // staging read before the next plane rewrites it
+                    continue;
+                }
                 const float w00 = (1.0f - t.fx) * (1.0f - t.fy), w01 = t.fx * (1.0f - t.fy),
                             w10 = (1.0f - t.fx) * t.fy, w11 = t.fx * t.fy;
-                const int wl = gl & 15;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) s_sdv[(wave * 16 + wl) * 17 + 4 * q + i] = ok ? dv[i] : 0.0f;
                 if (q == 0) {
@@ -1495,6 +1538,20 @@ __global__ void __launch_bounds__(256) k_unpack_planes(const UnpackBatch u) {
     if (base + tex < HW) {
         const float* p = u.src + u.off[j] + (size_t)base * 16 + t;
         for (int r = 0; r < u.replicas; ++r) acc += p[(size_t)r * u.stride];
+    }
+    if (u.trow && u.toff[j] >= 0 && base + tex < HW) {   // block-uniform plane: its x-row, folded into
+        // the two rows of time0 (tap_of's arithmetic for the time coordinate)
+        const float iy = fminf(fmaxf((u.time0[0] + 1.0f) * 0.5f * (float)(H - 1), 0.0f), (float)(H - 1));
+        const int y0 = (int)floorf(iy), y1 = min(y0 + 1, H - 1);
+        const float fy = iy - (float)y0;
+        const int y = (base + tex) / W, x = (base + tex) - y * W;
+        if (y == y0 || y == y1) {
+            float r = 0.0f;
+            const float* rp = u.trow + u.toff[j] + x * 16 + ch;
+            for (int k = 0; k < u.trow_reps; ++k) r += rp[(size_t)k * u.trow_stride];
+            if (y == y0) acc += r * (1.0f - fy);
+            if (y == y1) acc += r * fy;
+        }
     }
     s_t[tex][ch] = acc;
     __syncthreads();

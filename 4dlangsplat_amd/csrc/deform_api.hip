@@ -283,8 +283,30 @@ int deform_replicas(size_t P) {
 }
 struct BwdScratch {
     size_t X, A[LSR_DEFORM_MAX_DEPTH], dH[LSR_DEFORM_MAX_DEPTH];
-    size_t Grot, Gcoff, U0, U1, U2, dv, dZ2l, dZ1l, daabb, dplanes, total;
+    size_t Grot, Gcoff, U0, U1, U2, dv, dZ2l, dZ1l, daabb, dplanes, trow, total;
 };
+// the time planes' x-rows (DeformBwdArgs.trow): copies, their floats, each plane's offset (-1: not a
+// time plane).  LSR_DEFORM_TIME_ROWS=0 turns them off (A/B).
+constexpr int kTimeRowReps = 32;
+int time_row_reps() {
+    static const int reps = [] {
+        const char* e = std::getenv("LSR_DEFORM_TIME_ROWS");
+        return e && std::atoi(e) == 0 ? 0 : kTimeRowReps;
+    }();
+    return reps;
+}
+size_t time_row_floats(const lsr_deform_net* net, int64_t* toff) {
+    size_t o = 0;
+    for (int s = 0; s < net->n_scales; ++s)
+        for (int ci = 0; ci < 6; ++ci) {
+            int W, H;
+            plane_dims(net, s, ci, W, H);
+            const bool tp = ci == 2 || ci >= 4;
+            if (toff) toff[6 * s + ci] = tp ? (int64_t)o : -1;
+            if (tp) o += (size_t)W * 16;
+        }
+    return o;
+}
 BwdScratch bwd_scratch(const lsr_deform_net* net, size_t P) {
     BwdScratch s{};
     size_t o = 0;
@@ -312,6 +334,8 @@ BwdScratch bwd_scratch(const lsr_deform_net* net, size_t P) {
     s.daabb = take(lsr::DEF_AABB_SLOTS * 16);   // zeroed with the gradient planes (contiguous)
     s.dplanes = o;
     o += (size_t)deform_replicas(P) * layout(net).planes_end;   // the count every call of this process uses
+    s.trow = o;                                                  // zeroed with the planes (contiguous)
+    o += align256((size_t)time_row_reps() * time_row_floats(net, nullptr) * f);
     s.total = o;
     return s;
 }
@@ -438,7 +462,10 @@ extern "C" int lsr_deform_backward(const lsr_deform_net* net, const void* worksp
     b.daabb_part = fp(S.daabb);
     b.replicas = deform_replicas((size_t)P);
     b.plane_stride = (int64_t)(L.planes_end / sizeof(float));
-    if (hipMemsetAsync(sc + S.daabb, 0, (S.dplanes - S.daabb) + (size_t)b.replicas * L.planes_end, st) != hipSuccess)
+    b.trow_reps = time_row_reps();
+    b.trow = b.trow_reps ? fp(S.trow) : nullptr;
+    b.trow_stride = (int64_t)time_row_floats(net, b.toff);
+    if (hipMemsetAsync(sc + S.daabb, 0, S.total - S.daabb, st) != hipSuccess)
         return lsr::fail(LSR_EHIP, "memset");
     lsr::launch_deform_bwd_a(b, st);
     lsr::LangDeformArgs la{};
@@ -490,12 +517,17 @@ extern "C" int lsr_deform_backward(const lsr_deform_net* net, const void* worksp
     u.stride = b.plane_stride;
     u.daabb_part = b.daabb_part;
     u.daabb = grads->aabb;
+    u.trow = b.trow;
+    u.trow_reps = b.trow_reps;
+    u.trow_stride = b.trow_stride;
+    u.time0 = time;
     for (int s = 0; s < net->n_scales; ++s)
         for (int ci = 0; ci < 6; ++ci) {
             int W, H;
             plane_dims(net, s, ci, W, H);
             const int j = u.n++;
             u.off[j] = (int64_t)(L.plane_off[6 * s + ci] / sizeof(float));
+            u.toff[j] = b.toff[6 * s + ci];
             u.dst[j] = grads->planes[s][ci];
             u.H[j] = H;
             u.W[j] = W;

@@ -299,6 +299,14 @@ struct DeformBwdArgs {
     float* dplanes;                   // packed channel-last gradient planes (same offsets as f.planes),
     int64_t plane_stride;             //   `replicas` copies plane_stride floats apart (block b adds
     int replicas;                     //   into copy b % replicas; the unpack sums them)
+    // time planes (xt, yt, zt) of waves whose Gaussians all have time[0] (the render path's one time
+    // per view): every tap lies in the rows y0, y1 of time[0] with weights 1 - fy, fy, so the wave adds
+    // dv (1 - fx), dv fx into one x-row [W][16] per plane (at trow + toff[pi], copy b % trow_reps),
+    // and the unpack adds (1 - fy) and fy times its sum into the two rows.  Null: off.
+    float* trow;
+    int64_t toff[24];
+    int64_t trow_stride;
+    int trow_reps;
     float* sX;                        // saved [P, 16 n_scales] features
     float* sA[DEF_MAX_LAYERS];        // saved [P,128] relu(H_k)
     float* sdH[DEF_MAX_LAYERS];       // saved [P,128] gradients of H_k
@@ -359,6 +367,13 @@ struct UnpackBatch {
     int64_t stride;
     const float* daabb_part;
     float* daabb;
+    // DeformBwdArgs.trow: plane j's x-row copies at trow + toff[j] (toff[j] < 0: none), folded into
+    // its rows of time time0[0]
+    const float* trow;
+    int64_t toff[DEF_UNPACK_MAX];
+    int64_t trow_stride;
+    int trow_reps;
+    const float* time0;
 };
 void launch_unpack_planes(const UnpackBatch& u, hipStream_t st);
 
