@@ -526,6 +526,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
     __bf16* const s_xh = s_hh[1];   // read by the first layer only, which writes buffer 0
     __bf16* const s_xl = s_hl[1];
     __shared__ __attribute__((aligned(16))) float4 s_g4[DN];   // small-output heads: fp32 G rows
+    __shared__ uint32_t s_apos[DEEP ? 1 : 256];   // one layer: each thread's A_0 > 0 bits
     // Everything else lives in a hidden buffer while that buffer is dead (68 KB in all: two blocks
     // per CU): a head's G rows in the buffer its dZ1 rows take next (a barrier between the two), dX in
     // the chain's dead buffer, the plane-scatter staging in its lo half; every hand-over is a
@@ -550,6 +551,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
 
     // ---- chain forward, A_k = relu(H_k) saved ------------------------------------------------------
     int cur = 0;
+    uint32_t apos = 0;   // one layer (!DEEP): bit 16 mt + q = A_0 > 0, the chain backward's ReLU mask,
+                         // parked in LDS across the heads (a live register there spilled 38)
     for (int k = 0; k < L; ++k) {
         df32x16 acc[2] = {df32x16{}, df32x16{}};
         if (k == 0) mlp_ntile<F>(acc, s_xh, s_xl, XP, wave, a.wf_h[0], a.wf_l[0]);
@@ -562,8 +565,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const int g = g0 + row_of(mt, q, hh);
-                if (g < a.P) b.sA[k][(size_t)g * DWID + col] = fmaxf(acc[mt][q] + bias, 0.0f);
+                const float av = fmaxf(acc[mt][q] + bias, 0.0f);
+                if (g < a.P) b.sA[k][(size_t)g * DWID + col] = av;
+                if (!DEEP) apos |= av > 0.0f ? 1u << (16 * mt + q) : 0u;
             }
+        if (!DEEP) s_apos[tid] = apos;
         __syncthreads();
         cur = dst;
     }
@@ -713,8 +719,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const int r = row_of(mt, q, hh), g = g0 + r;
-                const float av = g < a.P ? b.sA[k][(size_t)g * DWID + col] : 0.0f;   // this block wrote it
-                const float v = av > 0.0f ? dA[mt][q] : 0.0f;
+#ifndef LSR_DEFORM_CHAIN_RELOAD
+                // one layer: the mask from the registers (reloading A_0 put 32 dependent loads of rows
+                // this block had just written on the chain's critical path)
+                const bool on = DEEP ? (g < a.P && b.sA[k][(size_t)g * DWID + col] > 0.0f)
+                                     : (g < a.P && ((s_apos[tid] >> (16 * mt + q)) & 1u));
+#else
+                const bool on = g < a.P && b.sA[k][(size_t)g * DWID + col] > 0.0f;   // this block wrote it
+#endif
+                const float v = on ? dA[mt][q] : 0.0f;
                 __bf16 hi, lo;
                 dsplit(v, hi, lo);
                 dh_h[r * DAP + col] = hi;
