@@ -218,8 +218,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-densify-stats", action="store_true",
                     help="diagnostic: no means2D gradient / radii MAX in the step (train.py:350-352 needs them)")
-    ap.add_argument("--early-views", type=_early_views, default=3,
-                    help="batched pipeline: views binned before compositing starts; the rest bin on a side stream "
+    ap.add_argument("--early-views", type=_early_views, default=2,
+                    help="batched pipeline: views binned before compositing starts (2: same-box 985 vs 976 "
+                         "frames/s for 3 over 8 alternating runs, profiles/r05_g/ab_early_views.txt); the rest bin on a side stream "
                          "while they composite (0: all binned first); 'e,s1,...': side binning batches of s1, ... "
                          "views and one of the rest, each composited as soon as it is binned")
     ap.add_argument("--no-overlap", action="store_true", help="diagnostic: no side stream (uncontended phase times)")

@@ -38,7 +38,7 @@ def test_binning_batches(bench, early, V, n):
 
 def test_defaults(bench):
     a = bench.parse_args([])
-    assert a.gpus == 1 and a.early_views == 3 and a.order_on_side and a.binning == "sort"
+    assert a.gpus == 1 and a.early_views == 2 and a.order_on_side and a.binning == "sort"
     assert a.main_priority == 0 and a.side_priority == 0
     assert not bench.parse_args(["--no-order-on-side"]).order_on_side
     assert bench.parse_args(["--order-on-side"]).order_on_side

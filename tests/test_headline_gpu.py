@@ -1,12 +1,12 @@
 """The measured pipeline at the measured size, against the C oracle.
 
-bench.py times native_view_renderer(overlap="batched", early_views=3) over a GradBucket with the
+bench.py times native_view_renderer(overlap="batched", early_views=2) over a GradBucket with the
 densification statistics on: one preprocess launch for the step's views, segmented depth / tile
 sorts, the later views binned on a side stream, compositors on the pre-split bf16 language
 operands, the compositor backward per view, then one batched preprocess backward (the flush).
 This runs exactly that on the headline workload (S2M, P = 2M, 1352 x 1014, C = 32; the bench's 8
-views per step: the 8-view preprocess launch, the 3 early views binned and composited as one batch and
-the other 5 binned on the side stream and composited as the second), twice (the images must repeat bit for bit), and holds every output to the
+views per step: the 8-view preprocess launch, the 2 early views binned and composited as one batch and
+the other 6 binned on the side stream and composited as the second), twice (the images must repeat bit for bit), and holds every output to the
 oracle: radii exactly, RGB within 1e-4,
 language within 1e-3, every gradient field of the bucket (means3D, scales, rotations, opacities,
 SH, language, means2D) within 1e-4 of the largest magnitude of the oracle's per-view sum.
@@ -56,7 +56,7 @@ def test_bench_pipeline_matches_oracle_at_headline_size():
         runs.setdefault(v, []).append(images[v])
         return gcs_d[v], gls_d[v], None
 
-    render = native_view_renderer(scene, settings, grad_fn, overlap="batched", early_views=3)
+    render = native_view_renderer(scene, settings, grad_fn, overlap="batched", early_views=2)
 
     def render_view(v, b):
         r = render(v, b)
