@@ -99,13 +99,16 @@ def test_backward_matches_reference_golden():
         assert _rel(g.cpu().numpy().reshape(ref.shape), ref) < 1e-4, name
 
 
-@pytest.mark.parametrize("P,time", [(20000, 0.37), (777, -0.8), (3000, 1.0), (3000, -1.0), (20000, "mixed")])
+@pytest.mark.parametrize("P,time", [(20000, 0.37), (777, -0.8), (3000, 1.0), (3000, -1.0), (20000, "mixed"),
+                                    (20000, "views3"), (20000, "views10")])
 def test_backward_matches_oracle_at_neu3d_resolution(P, time):
     """Neu3D resolution (64^3 x 150, multires [1, 2]); gradients accumulate over two calls.  One time
     for all Gaussians (the render path: the time planes go through per-plane x-rows folded into the
     two rows of that time); +-1 put those taps on the clamped border rows (y1 == y0 at +1, weight 0
     on the second row at -1); "mixed": time 0.37 but every 97th Gaussian at -0.55, so that most waves
-    take the x-rows and the rest the four-tap scatter."""
+    take the x-rows and the rest the four-tap scatter; "views3" / "views10": consecutive runs of
+    Gaussians at 3 / 10 times (a batched call of several views: the first view's waves take the
+    x-rows, the others the four-tap scatter)."""
     params, res, multires, inp = _neu3d_case(P, seed=3)
     # the bilinear slope jumps at grid lines: keep the points 1e-3 cells away from every line (and
     # from the clamped borders), where float32 and float64 coordinates could pick different cells
@@ -118,9 +121,13 @@ def test_backward_matches_oracle_at_neu3d_resolution(P, time):
             keep &= np.abs(u - np.round(u)) > 1e-3
     inp = {k: v[keep] for k, v in inp.items()}
     P = int(keep.sum())
-    times = np.full((P, 1), 0.37 if time == "mixed" else time)
+    scalar = not isinstance(time, str)
+    times = np.full((P, 1), time if scalar else 0.37)
     if time == "mixed":
         times[::97] = -0.55
+    elif time.startswith("views") if not scalar else False:
+        nv = int(time[5:])
+        times[:, 0] = np.linspace(-0.9, 0.95, nv)[np.arange(P) * nv // P]
     f = _field(params, res, multires)
     rng = np.random.default_rng(5)
     ups = dict(means3D=rng.normal(size=(P, 3)), scales=rng.normal(size=(P, 3)), rotations=rng.normal(size=(P, 4)),
@@ -141,7 +148,7 @@ def test_backward_matches_oracle_at_neu3d_resolution(P, time):
     t = lambda a: torch.tensor(np.asarray(a, np.float32)).cuda()   # noqa: E731
     f.zero_grad()
     for _ in range(2):
-        got = f.backward(t(inp["means3D"]), t(times[:, 0]) if time == "mixed" else time, *[t(ups[k]) for k in KEYS])
+        got = f.backward(t(inp["means3D"]), time if scalar else t(times[:, 0]), *[t(ups[k]) for k in KEYS])
     torch.cuda.synchronize()
     # bf16 hi/lo MFMA products (~2^-17 relative) and fp32 atomics: 1e-4 of each tensor's range
     assert _rel(got[0].cpu().numpy(), g_in["means3D"]) < 1e-4
