@@ -62,6 +62,8 @@ __device__ __forceinline__ void lds_poison(void* p, size_t bytes) {
 typedef __bf16 dbf16x8 __attribute__((ext_vector_type(8)));
 typedef float df32x16 __attribute__((ext_vector_type(16)));
 #define DMFMA(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_bf16((a), (b), (c), 0, 0, 0)
+typedef float df32x4 __attribute__((ext_vector_type(4)));
+#define DMFMA16(a, b, c) __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (c), 0, 0, 0)
 
 constexpr int DN = 64;            // Gaussians per block
 constexpr int DWID = 128;         // MLP width
@@ -410,6 +412,72 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
         const bool quat = hd == 2 && a.apply_rotation, coff = hd == 5;
         const bool resid_add = !quat && !coff;
         if (GRAD && resid_add) continue;
+#ifndef LSR_DEFORM_FWD_W2_WIDE
+        if (nout <= 16) {                                            // block-uniform
+            // a head of at most 16 outputs (pos, scales, rotations, opacity, coff): its output layer as
+            // 16 x 16 x 32 MFMAs, one 16-row tile per wave (the 32-column tile of one wave computed
+            // 28-31 zero columns while the other three waved at the barrier)
+            const int c16 = lane & 15, g4 = lane >> 4;
+            float res16[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int g = g0 + 16 * wave + 4 * g4 + i;
+                res16[i] = (resid_add && c16 < nout && g < a.P) ? __builtin_nontemporal_load(a.in[hd] + (size_t)g * nout + c16)
+                                                               : 0.0f;
+            }
+            {
+                df32x16 acc[2] = {df32x16{}, df32x16{}};
+                mlp_ntile<DWID>(acc, ah, al, DAP, wave, a.w1_h[hd], a.w1_l[hd]);
+                store_hidden(acc, wave, a.b1[hd], bh, bl);
+            }
+            __syncthreads();
+            df32x4 o = df32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int ks = 0; ks < DWID / 32; ++ks) {
+                const int k0 = 32 * ks + 8 * g4;
+                const dbf16x8 xh = *reinterpret_cast<const dbf16x8*>(bh + (16 * wave + c16) * DAP + k0);
+                const dbf16x8 xl = *reinterpret_cast<const dbf16x8*>(bl + (16 * wave + c16) * DAP + k0);
+                const dbf16x8 wh = *reinterpret_cast<const dbf16x8*>(a.w2_h[hd] + (size_t)c16 * DWID + k0);
+                const dbf16x8 wl = *reinterpret_cast<const dbf16x8*>(a.w2_l[hd] + (size_t)c16 * DWID + k0);
+                o = DMFMA16(xh, wh, o);
+                o = DMFMA16(xh, wl, o);
+                o = DMFMA16(xl, wh, o);
+            }
+            if (c16 < nout) {
+                const float b2 = a.b2[hd][c16];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int r = 16 * wave + 4 * g4 + i, g = g0 + r;
+                    const float v = o[i] + b2;
+                    if (resid_add) {
+                        if (g < a.P) __builtin_nontemporal_store(res16[i] + v, a.out[hd] + (size_t)g * nout + c16);
+                    } else {
+                        s_q[r][c16] = v;
+                        if (!GRAD && coff && a.out_coff && g < a.P) a.out_coff[(size_t)g * nout + c16] = v;
+                    }
+                }
+            }
+            __syncthreads();   // the hidden rows read (and s_q complete) before they are reused
+            if (!resid_add && wave == 0) {                           // one Gaussian per lane
+                const int g = g0 + lane;
+                if (GRAD && g < a.P) {
+                    if (quat) quat_grad(b, g, s_q[lane]);
+                    else discrete_grad(b, g, s_q[lane]);
+                } else if (g < a.P) {
+                    if (quat) {   // rotations = normalize(rotations (x) d_rot)  (deformation.py:135-136)
+                        const float4 q1 = reinterpret_cast<const float4*>(a.in[2])[g];
+                        const float4 p = quat_mul(q1, make_float4(s_q[lane][0], s_q[lane][1], s_q[lane][2], s_q[lane][3]));
+                        const float inv = 1.0f / sqrtf(p.x * p.x + p.y * p.y + p.z * p.z + p.w * p.w);
+                        reinterpret_cast<float4*>(a.out[2])[g] = make_float4(p.x * inv, p.y * inv, p.z * inv, p.w * inv);
+                    } else {
+                        discrete_combine(a, g, s_q[lane], a.out_lang);
+                    }
+                }
+            }
+            if (!resid_add) __syncthreads();   // s_q read before the next head's outputs
+            continue;
+        }
+#endif
         const bool owner = wave < (nout + 31) / 32;     // 1 N tile, or 2 for the 48 SH coefficients
         const int col = 32 * wave + (lane & 31), h = lane >> 5;
         // the residual inputs of this wave's outputs, loaded now so the head's first layer hides
