@@ -51,9 +51,12 @@ def test_bench_two_ranks_prints_one_line():
     assert line["config"]["global_batch"] == 16 and line["config"]["parallelism"] == "dp2"
     assert line["steps"] == 2 and line["value"] > 0
     assert abs(line["value"] - 16 * 2 / (line["ms_per_step"] * 2e-3)) <= 1e-3 * line["value"]
-    # the dominant kernel is picked by event time; with both ranks on one device each rank's
-    # compositor launches overlap the other's, so either compositor may come out ahead here
-    assert line["roofline"]["kernel"] in ("render_bwd", "render_fwd") and line["cpu_baseline"] is None
+    # the dominant kernel is picked by event time; with both ranks on one device an event pair of one
+    # rank also spans the other rank's kernels, so which phase comes out ahead here is arbitrary (the
+    # one-GPU line, where it is render_bwd, is bench.py's own run)
+    assert line["roofline"]["kernel"] in ("render_bwd", "render_fwd", "preprocess", "preprocess_bwd_views",
+                                          "preprocess_bwd", "emit", "tile_ranges")
+    assert line["roofline"]["frac"] > 0 and line["cpu_baseline"] is None
 
 
 def _spawn(mode, steps, chunks=1):
