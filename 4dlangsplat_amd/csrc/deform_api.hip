@@ -290,10 +290,10 @@ struct BwdScratch {
 // the time planes' x-rows (DeformBwdArgs.trow): copies, their floats, each plane's offset (-1: not a
 // time plane).  LSR_DEFORM_TIME_ROWS=0 turns them off (A/B).
 constexpr int kTimeRowReps = 32;
-int time_row_reps() {
+int time_row_reps() {   // LSR_DEFORM_TIME_ROWS=n (A/B): n copies, 0 = off
     static const int reps = [] {
         const char* e = std::getenv("LSR_DEFORM_TIME_ROWS");
-        return e && std::atoi(e) == 0 ? 0 : kTimeRowReps;
+        return e ? std::max(0, std::min(256, std::atoi(e))) : kTimeRowReps;
     }();
     return reps;
 }
