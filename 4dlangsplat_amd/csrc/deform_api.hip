@@ -276,9 +276,9 @@ int deform_replicas(size_t P) {
         return e ? std::max(1, std::min(kGradReplicas, std::atoi(e))) : 0;
     }();
     if (forced) return forced;
-    // measured (tools/gpu_replica_ab.sh): 4 copies backward 12.20 vs 12.22 ms at 2M (the atomics do
+    // measured (tools/gpu.sh deform_ab): 4 copies backward 12.20 vs 12.22 ms at 2M (the atomics do
     // not contend more), configs[4] stand-in 159 vs 139-152 iterations/s at 100k (less to zero and sum);
-    // with the time planes through x-rows (round 5, tools/gpu_deform_env_ab.sh) 2 copies 10.08 vs 10.12
+    // with the time planes through x-rows (round 5, tools/gpu.sh deform_ab) 2 copies 10.08 vs 10.12
     // ms at 2M and 1.257-1.261 vs 1.257-1.273 ms per configs[4] iteration, 8 copies 10.10-10.19 / 1.29
     (void)P;
     return 2;

@@ -717,7 +717,9 @@ int lsr_forward_binning_views_tb(int32_t n_views, const lsr_settings* const* s, 
         if (ne == 0) continue;
         {
             PhaseTimer t(LSR_PHASE_TILE_SORT, st);
-            lsr::launch_tile_bucket_binning(tb, ne, st);
+            const hipError_t e = lsr::launch_tile_bucket_binning(tb, ne, st);
+            if (e != hipSuccess)
+                return fail(LSR_EHIP, std::string("tile-bucket binning: dynamic LDS attribute: ") + hipGetErrorString(e));
         }
         LSR_LAUNCHED("tile-bucket binning", st, s[0]->debug);
     }

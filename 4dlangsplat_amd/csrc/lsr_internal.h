@@ -509,7 +509,7 @@ struct TbBatch {
     TbView v[LSR_MAX_VIEWS];
 };
 int tb_blocks(int P);   // rows of TbView::table
-void launch_tile_bucket_binning(const TbBatch& tb, int nv, hipStream_t st);
+hipError_t launch_tile_bucket_binning(const TbBatch& tb, int nv, hipStream_t st);   // attribute errors returned
 
 // compositing (render_fwd_wave.hip / render_bwd.hip)
 void launch_render_bwd(const RenderBwdArgs& a, hipStream_t st);

@@ -19,6 +19,8 @@
 // Sorting a bucket by (depth bits, id) reproduces upstream's order exactly (its radix sort is
 // stable over instances emitted in id order), so the lists equal the sort path's: the same entries
 // (instances that reach no quadrant are not listed, emit_quad_mask), in the same order.
+#include <mutex>
+
 #include "lsr_common.h"
 #include "lsr_internal.h"
 
@@ -316,24 +318,34 @@ __global__ void __launch_bounds__(256) k_tb_sort(const TbBatch tb) {
 
 int tb_blocks(int P) { return (P + TB_GPB - 1) / TB_GPB; }
 
-void launch_tile_bucket_binning(const TbBatch& tb, int nv, hipStream_t st) {
-    if (tb.P == 0 || nv <= 0) return;
+hipError_t launch_tile_bucket_binning(const TbBatch& tb, int nv, hipStream_t st) {
+    if (tb.P == 0 || nv <= 0) return hipSuccess;
     const int nb = tb_blocks(tb.P);
     const size_t hist = (size_t)tb.ntiles * sizeof(uint32_t);
-    static bool attr = false;   // dynamic LDS beyond 64 KiB with the walk's static staging arrays
-    if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_tb_count),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k_tb_scatter),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-        (void)hipGetLastError();
-        attr = true;
-    }
+    // dynamic LDS beyond 64 KiB beside the walk's static staging arrays: a per-function attribute that
+    // HIP keeps per device, so it is set once per device (thread-safe) and its result kept
+    constexpr int kMaxDev = 64;
+    static std::once_flag once[kMaxDev];
+    static hipError_t attr_err[kMaxDev];
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= kMaxDev) return hipErrorInvalidDevice;
+    std::call_once(once[dev], [dev] {
+        hipError_t r = hipFuncSetAttribute(reinterpret_cast<const void*>(k_tb_count),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        if (r == hipSuccess)
+            r = hipFuncSetAttribute(reinterpret_cast<const void*>(k_tb_scatter),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+        attr_err[dev] = r;
+    });
+    if (attr_err[dev] != hipSuccess) return attr_err[dev];
     hipLaunchKernelGGL(k_tb_count, dim3(nb, nv), dim3(TB_THREADS), hist, st, tb);
     hipLaunchKernelGGL(k_tb_colscan, dim3((tb.ntiles + TB_SEG - 1) / TB_SEG, nv), dim3(256), 0, st, tb, nb);
     hipLaunchKernelGGL(k_tb_tilescan, dim3(nv), dim3(1024), 0, st, tb);
     hipLaunchKernelGGL(k_tb_scatter, dim3(nb, nv), dim3(TB_THREADS), hist, st, tb);
     hipLaunchKernelGGL(k_tb_sort, dim3(tb.ntiles, nv), dim3(256), 0, st, tb);
+    return hipSuccess;
 }
 
 }  // namespace lsr

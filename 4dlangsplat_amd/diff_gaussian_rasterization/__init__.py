@@ -308,12 +308,22 @@ def preprocess_views_native(raster_settings_list, means3D, opacities, shs=None, 
     stream = stream or torch.cuda.current_stream(device)
     fin, inputs, P = _fwd_inputs(means3D, opacities, shs, colors_precomp, language_feature, scales, rotations,
                                  cov3D_precomp)
+    if row_chunks:   # validated before anything is enqueued (both binning paths)
+        covered = 0
+        for r0, r1, _ in row_chunks:
+            if r0 != covered or r1 < r0 or r0 % 256:
+                raise ValueError("row_chunks must cover [0, P) in order, each r0 a multiple of 256")
+            covered = r1
+        if covered != P:
+            raise ValueError("row_chunks must cover [0, P) in order, each r0 a multiple of 256")
     split = split_language and fin.C == 32 and P > 0
     if split:   # allocated now (fin carries the pointer), written behind the batch's count event
         with torch.cuda.stream(stream):
             inputs["language_feature_split"] = torch.empty(P, 64, dtype=torch.int16, device=device)
         fin.language_feature_split = inputs["language_feature_split"].data_ptr()
-        if not split_behind_counts:
+        # with row_chunks the language rows may still be arriving (each chunk's before() waits for
+        # them): the split is then always enqueued behind the chunk loop
+        if not split_behind_counts and not row_chunks:
             language_split_native(inputs["language_feature"], stream=stream, out=inputs["language_feature_split"])
             split = False
     n = len(raster_settings_list)
@@ -337,27 +347,18 @@ def preprocess_views_native(raster_settings_list, means3D, opacities, shs=None, 
                 _lib.check(L.lsr_forward_preprocess_views_tb_async(n, int(r0), int(r1), s_arr, ctypes.byref(fin), o_arr,
                                                                    g_arr, ctypes.c_void_p(stream.cuda_stream)),
                            "lsr_forward_preprocess_views_tb_async")
-            if row_chunks and (row_chunks[0][0] != 0 or row_chunks[-1][1] != P or
-                               any(a[1] != b[0] for a, b in zip(row_chunks, row_chunks[1:]))):
-                raise ValueError("row_chunks must cover [0, P) in order")
             if k > 0:
                 _lib.check(L.lsr_forward_instance_scan_views_async(k, s_arr, ctypes.byref(fin), g_arr,
                                                                    ctypes.c_void_p(counts.data_ptr()),
                                                                    ctypes.c_void_p(stream.cuda_stream)),
                            "lsr_forward_instance_scan_views_async")
         elif row_chunks:
-            covered = 0
             for r0, r1, before in row_chunks:
-                if r0 != covered or r1 < r0:
-                    raise ValueError("row_chunks must cover [0, P) in order")
-                covered = r1
                 if before is not None:
                     before()
                 _lib.check(L.lsr_forward_preprocess_views_rows_async(n, int(r0), int(r1), s_arr, ctypes.byref(fin),
                                                                      o_arr, g_arr, ctypes.c_void_p(stream.cuda_stream)),
                            "lsr_forward_preprocess_views_rows_async")
-            if covered != P:
-                raise ValueError("row_chunks must cover [0, P) in order")
             if k > 0:
                 _lib.check(L.lsr_forward_depth_order_views_async(k, s_arr, ctypes.byref(fin), g_arr,
                                                                  ctypes.c_void_p(counts.data_ptr()),

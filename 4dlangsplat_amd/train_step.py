@@ -349,12 +349,21 @@ class TrainStep:
         return head + lang + (c(tr.max_radii2D), c(tr.xyz_gradient_accum), c(tr.denom), self.optimizer_state_dict(),
                               float(self.spatial_lr_scale))
 
-    def restore(self, model_args: tuple, fresh_optimizer: bool = False) -> None:
+    def restore(self, model_args: tuple, fresh_optimizer: bool = False, reference: bool = False) -> None:
         """GaussianModel.restore (gaussian_model.py:107-154) of a capture(): parameters, field,
         deformation table, statistics and the optimizer state.  The reference re-runs training_setup
         after loading, which builds a fresh Adam (its moments and step counts are not resumed);
         fresh_optimizer=True does the same, the default resumes them (training N iterations equals
-        training k, capture, restore, N - k more)."""
+        training k, capture, restore, N - k more).
+
+        A 14-entry capture (no language features) restored into a trainer with a language group
+        starts that group from zeros, as training_setup does for a language stage initialised from
+        an RGB model (gaussian_model.py:232-234), with a fresh optimizer (the reference loads no
+        optimizer state when include_feature is on: :146-147).
+
+        reference=True reproduces the reference's restore exactly: a fresh optimizer, and the
+        deformation field's state loaded only from a 14-entry capture (its 15-entry branch never
+        calls _deformation.load_state_dict: :111-129 vs :130-150)."""
         if len(model_args) == 15:
             (sh, xyz, deform, table, f_dc, f_rest, scaling, rotation, opacity, lang, max_r, accum, denom, opt,
              slr) = model_args
@@ -368,12 +377,14 @@ class TrainStep:
         params = dict(xyz=xyz, f_dc=f_dc, f_rest=f_rest, opacity=opacity, scaling=scaling, rotation=rotation)
         if lang is not None:
             params["language_feature"] = lang
-        elif "language_feature" in tr.params:
-            raise ValueError("this trainer has a language group; the capture has none (include_feature off)")
+        elif "language_feature" in tr.params:    # language stage from an RGB capture: zeros, fresh Adam
+            width = int(tr["language_feature"].shape[1])   # the trainer's language_feature_hiddendim
+            params["language_feature"] = torch.zeros(xyz.shape[0], width, dtype=torch.float32, device=xyz.device)
+            fresh_optimizer = True
         tr.load_rows(params, max_r, accum, denom, table)
         self.sh_degree = int(sh)
         self.spatial_lr_scale = float(slr)
-        if self.field is not None:
+        if self.field is not None and not (reference and len(model_args) == 15):
             pre = "deformation_net."
             sd = {k[len(pre):]: v for k, v in deform.items() if k.startswith(pre)}
             missing = sorted(set(self.field.p) - set(sd))
@@ -385,7 +396,7 @@ class TrainStep:
                         raise ValueError(f"{k}: shape {tuple(sd[k].shape)} vs {tuple(t.shape)}")
                     t.copy_(sd[k])
             self.field.prepare()
-        if fresh_optimizer:
+        if fresh_optimizer or reference:
             for n in tr.params:
                 tr.load_adam_entry(n, None)
             if self.field_opt is not None:
@@ -402,10 +413,11 @@ class TrainStep:
         torch.save((self.capture(include_feature), int(iteration)), path)
         return path
 
-    def load_checkpoint(self, path: str, fresh_optimizer: bool = False) -> int:
+    def load_checkpoint(self, path: str, fresh_optimizer: bool = False, reference: bool = False) -> int:
         """train.py:104-109 (--start_checkpoint): restore a save_checkpoint file; returns its
-        iteration (the loop's first_iter), which also becomes self.iteration."""
+        iteration (the loop's first_iter), which also becomes self.iteration.  fresh_optimizer /
+        reference: as restore()."""
         model_args, first_iter = torch.load(path, map_location=self.trainer.device, weights_only=True)
-        self.restore(model_args, fresh_optimizer=fresh_optimizer)
+        self.restore(model_args, fresh_optimizer=fresh_optimizer, reference=reference)
         self.iteration = int(first_iter)
         return self.iteration

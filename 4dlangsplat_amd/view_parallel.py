@@ -146,11 +146,19 @@ class ViewParallelStep:
     Afterwards the bucket holds the SUM over ALL views of the batch on every rank, and
     bucket.radii the MAX over all views (when densify_stats)."""
 
-    def __init__(self, bucket: GradBucket, n_views: int, group=None, flush_chunks: int = 4, update=None):
+    def __init__(self, bucket: GradBucket, n_views: int, group=None, flush_chunks: int = 4, update=None,
+                 defer_gather: bool = False):
         """update: a ShardedAdam.  Without it the step ends with the bucket SUM all-reduced on every
         rank; with it the bucket is reduce-scattered by Gaussian rows, each rank runs Adam on its row
-        shard and the updated rasterizer inputs are all-gathered (update.step)."""
+        shard and the updated rasterizer inputs are all-gathered (update.step).
+
+        defer_gather (opt-in, needs a renderer with set_row_waits): run() returns with the
+        all-gathers into the scene's tensors still in flight, and the next run()'s preprocess waits
+        for each row chunk as it lands.  Between such steps the scene's rows may be old or
+        half-written: call finish() before anything else reads the scene (evaluation,
+        densification, capture).  By default run() returns with the scene final."""
         self.update = update
+        self.defer_gather = bool(defer_gather)
         self.bucket = bucket
         self.n_views = n_views
         self.group = group
@@ -168,7 +176,7 @@ class ViewParallelStep:
             # the previous step's all-gathers may still be in flight: a renderer that preprocesses by
             # row chunks waits for each chunk's rows itself, any other waits for all of them now
             waits = upd.gather_waits()
-            setter = getattr(render_view, "set_row_waits", None)
+            setter = getattr(render_view, "set_row_waits", None) if self.defer_gather else None
             if waits and setter is not None:
                 setter(waits)
                 upd._ag = []
@@ -252,6 +260,11 @@ class ViewParallelStep:
             for h in pending:
                 h.wait()
         return b
+
+    def finish(self) -> None:
+        """Wait for the all-gathers a defer_gather step left in flight: the scene is final after it."""
+        if self.update is not None and hasattr(self.update, "wait_all"):
+            self.update.wait_all()
 
     def visibility(self) -> torch.Tensor:
         """ANY over the batch's views (train.py:271): a Gaussian is visible if some view gave it
@@ -656,6 +669,9 @@ class ShardedAdam:
         self.steps = {n: 0 for n in self.raw}
         self._rs = {}            # chunk -> (shard gradient rows per field, handles): reduce-scatters in flight
         self._ag = []            # [(r0, r1, handles)]: the last step's all-gathers, not yet waited for
+        # inspection (tests): grad_hook(step, g0, valid, grads) sees each piece's reduced gradients of
+        # the raw groups (after the activations' backward, before Adam): global rows [g0, g0 + valid)
+        self.grad_hook: Optional[Callable] = None
 
     # ---- learning rate (gaussian_model.py:302-329; GaussianTrainer's schedule) ----------------------
     def set_xyz_schedule(self, lr_init, lr_final, lr_delay_mult=0.01, max_steps=30000):
@@ -771,6 +787,10 @@ class ShardedAdam:
                 nx = x.norm(dim=-1, keepdim=True)
                 d = nx + 1e-9
                 grads["language_feature"] = gl / d - x * (x * gl).sum(-1, keepdim=True) / (nx.clamp_min(1e-30) * d * d)
+        if self.grad_hook is not None:
+            g0 = self.pieces[c][0]
+            self.grad_hook(max(self.steps.values(), default=0), g0, max(0, min(self.piece, self.P - g0)),
+                           {n: gr for n, gr in grads.items() if n in raw and n in self.lrs})
         for name, gr in grads.items():
             if name not in raw or name not in self.lrs:
                 continue

@@ -4,6 +4,7 @@ GPU per rank; the code path above the collectives -- rank spawn, device binding,
 bucket's SUM / radii MAX, ShardedAdam's reduce-scatter / all-gather -- is the same).
 
     python tests/mp_view_parallel_gpu.py --out DIR --world 2 --mode allreduce|sharded [--steps S]
+                                         [--chunks C] [--views V]
 
 world > 1: the parent starts the ranks with view_parallel.launch_ranks before it touches the GPU
 (fresh interpreters) and never initialises HIP itself; every rank writes DIR/rank{r}.pt.
@@ -41,7 +42,7 @@ def raw_scene(seed=5):
     return sc, raw
 
 
-def run_rank(rank, world, out, mode, steps, chunks=1):
+def run_rank(rank, world, out, mode, steps, chunks=1, n_views=N_VIEWS):
     import torch
     import torch.distributed as dist
 
@@ -56,33 +57,42 @@ def run_rank(rank, world, out, mode, steps, chunks=1):
     try:
         sc_cpu, raw = raw_scene()
         sc = sc_cpu.to("cuda")
-        cams = synthetic.camera_batch(N_VIEWS, W, H, tanfovx=0.6, seed=2)
+        cams = synthetic.camera_batch(n_views, W, H, tanfovx=0.6, seed=2)
         bg = torch.ones(3, device="cuda")
         settings = [dgr.GaussianRasterizationSettings(H, W, c.tanfovx, c.tanfovy, bg, 1.0,
                                                       c.world_view_transform.cuda(), c.full_proj_transform.cuda(),
                                                       3, c.camera_center.cuda(), False, False, True) for c in cams]
         g = torch.Generator(device="cpu").manual_seed(7)
         grads = [((torch.randn(3, H, W, generator=g) * 1e-2).cuda(), (torch.randn(C, H, W, generator=g) * 1e-2).cuda())
-                 for _ in range(N_VIEWS)]
+                 for _ in range(n_views)]
         up = None
         rm = 1
+        rec = {}                          # step -> group -> [(global row ids, reduced gradient rows)]
         if mode == "sharded":
             up = ShardedAdam(sc, {k: v.cuda() for k, v in raw.items()}, LRS, chunks=chunks)
             rm = ShardedAdam.row_multiple(P, world, chunks=chunks)
+
+            def hook(st, g0, valid, gr):
+                for k, x in gr.items():
+                    rec.setdefault(st, {}).setdefault(k, []).append(
+                        (torch.arange(g0, g0 + valid), x[:valid].detach().cpu().clone()))
+            up.grad_hook = hook
         b = GradBucket(P, sc.shs.shape[1], C, "cuda", densify_stats=True, row_multiple=rm)
-        step = ViewParallelStep(b, N_VIEWS, update=up)
+        # chunks > 1: the chunk pipeline, the next step's preprocess waiting per row chunk
+        step = ViewParallelStep(b, n_views, update=up, defer_gather=chunks > 1)
         render = native_view_renderer(sc, settings, lambda v, c, l, d: (grads[v][0], grads[v][1], None),
                                       overlap="batched", early_views=3)
         for _ in range(steps):
             step.run(render)
-        if up is not None:
-            up.wait_all()                 # the last step's all-gathers (the next step would wait per chunk)
+        step.finish()                     # the last step's all-gathers (deferred with chunks > 1)
         torch.cuda.synchronize()
         res = dict(world=world, views=list(step.views), radii=b.radii.cpu())
         if mode == "allreduce":
             res["grads"] = {k: (v.cpu().clone() if v is not None else None) for k, v in b.views.items()}
         else:
             res["rows"] = (up.r0, up.r1)
+            res["grads_rec"] = {st: {k: (torch.cat([i for i, _ in v]), torch.cat([x for _, x in v]))
+                                     for k, v in d.items()} for st, d in rec.items()}
             res["full"] = {k: tuple(x.cpu().clone() for x in up.full_rows(k)) for k in up.raw}
             res["act"] = {k: getattr(sc, k).cpu().clone() for k in ("means3D", "scales", "rotations", "opacities",
                                                                       "shs", "lang")}
@@ -94,8 +104,8 @@ def run_rank(rank, world, out, mode, steps, chunks=1):
             dist.destroy_process_group()
 
 
-def _child(rank, world, out, mode, steps, chunks):
-    run_rank(rank, world, out, mode, steps, chunks)
+def _child(rank, world, out, mode, steps, chunks, n_views):
+    run_rank(rank, world, out, mode, steps, chunks, n_views)
 
 
 def main():
@@ -105,12 +115,13 @@ def main():
     ap.add_argument("--mode", choices=("allreduce", "sharded"), default="allreduce")
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--chunks", type=int, default=1)
+    ap.add_argument("--views", type=int, default=N_VIEWS)
     a = ap.parse_args()
     if a.world > 1:
         from view_parallel import launch_ranks   # spawns before this process touches the GPU
-        launch_ranks(a.world, _child, (a.out, a.mode, a.steps, a.chunks))
+        launch_ranks(a.world, _child, (a.out, a.mode, a.steps, a.chunks, a.views))
     else:
-        run_rank(0, 1, a.out, a.mode, a.steps, a.chunks)
+        run_rank(0, 1, a.out, a.mode, a.steps, a.chunks, a.views)
 
 
 if __name__ == "__main__":

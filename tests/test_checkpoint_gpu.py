@@ -146,3 +146,57 @@ def test_capture_layout_and_restore_with_field():
     c.restore(cap, fresh_optimizer=True)
     assert all(s == 0 for s in c.trainer.steps.values())
     assert torch.equal(c.trainer["xyz"], cap[1])
+
+
+def test_reference_restore_semantics():
+    """restore(reference=True) is the reference's GaussianModel.restore + training_setup
+    (gaussian_model.py:111-154): a fresh optimizer; the field's state loaded from a 14-entry capture
+    only (its 15-entry branch never calls _deformation.load_state_dict).  A 14-entry (RGB) capture
+    restored into a trainer with a language group starts that group from zeros with a fresh optimizer
+    (training_setup, :232-234), in either mode, instead of raising."""
+    field_p = DeformationField.init_params(RES, MULTIRES, AABB, seed=1)
+    cams, gts, student = _problem("fine-base", field_p)
+    a, _ = student()
+    for it in range(1, 4):
+        a(cams, gts, iteration=it)
+    cap14 = a.capture()
+    assert len(cap14) == 14
+    b, _ = student()
+    f0 = {k: t.clone() for k, t in b.field.p.items()}
+    b.restore(cap14, reference=True)                  # 14 entries: the field comes back
+    assert all(torch.equal(b.field.p[k], a.field.p[k]) for k in f0)
+    assert all(s == 0 for s in b.trainer.steps.values())
+    assert all(float(b.field_opt.exp_avg[k].abs().max()) == 0 for k in b.field_opt.exp_avg)
+    # a 15-entry capture (a language stage's): the reference keeps the field it has
+    dev = torch.device("cuda")
+    lang_lrs = dict(LRS, language_feature=2.5e-3)
+    g = torch.Generator(device="cpu").manual_seed(4)
+
+    def lang_step(lang):
+        raw = {k: v.clone() for k, v in _raw(synthetic.make_scene(P, C=3, tanfovx=0.6, tanfovy=0.6 * H / W, seed=3,
+                                                                   logscale_mean=-3.0).to(dev)).items()}
+        raw["language_feature"] = lang.to(dev)
+        return TrainStep(GaussianTrainer(raw, lang_lrs),
+                         DeformationField({k: v.to(dev) for k, v in field_p.items()}, RES, MULTIRES), stage="fine-base")
+
+    c = lang_step(torch.randn(P, 3, generator=g))
+    cap15 = c.capture()
+    assert len(cap15) == 15
+    d = lang_step(torch.randn(P, 3, generator=g))
+    with torch.no_grad():
+        for t in d.field.p.values():
+            t.add_(0.5)                                # a field that differs from the capture's
+    fd = {k: t.clone() for k, t in d.field.p.items()}
+    d.restore(cap15, reference=True)
+    assert all(torch.equal(d.field.p[k], fd[k]) for k in fd)       # not loaded, as the reference
+    assert torch.equal(d.trainer["language_feature"], cap15[9])
+    d.restore(cap15)                                               # the resume mode loads it
+    assert all(torch.equal(d.field.p[k], c.field.p[k]) for k in fd)
+    # RGB capture into the language trainer: zeros, fresh Adam (both modes)
+    for ref in (False, True):
+        e = lang_step(torch.randn(P, 3, generator=g))
+        e.restore(cap14, reference=ref)
+        assert e.trainer["language_feature"].shape == (P, 3)
+        assert float(e.trainer["language_feature"].abs().max()) == 0
+        assert torch.equal(e.trainer["xyz"], cap14[1])
+        assert all(s == 0 for s in e.trainer.steps.values())

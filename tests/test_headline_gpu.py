@@ -82,14 +82,31 @@ def test_bench_pipeline_matches_oracle_at_headline_size():
         flats.append(bucket.flat.clone())
     torch.cuda.synchronize()
     assert not torch.isnan(bucket.flat).any()
-    # the backward repeats up to float-atomic reordering (a lost low half of a packed-fp32 result in
-    # any compositor lane, DESIGN.md 4.5, would move a gradient by far more than that): every field
-    # of the two steps' buckets within 1e-5 of its largest magnitude (measured: 2.2e-6 at most, scales)
+    # the backward against the deterministic-mode backward of the same views (lsr_backward's
+    # fixed-order reduction, views summed in order; bit-identical run to run), per element: the atomic
+    # bucket differs from it only by the reassociation of float-atomic sums, so every element holds
+    # |atomic - deterministic| <= 1e-4 |deterministic| + 1e-7 max|field| (a lost low half of a
+    # packed-fp32 result in any compositor lane, DESIGN.md 4.5, moves an element by O(itself))
+    det = native_view_renderer(scene, settings, lambda v, color, lang, depth: (gcs_d[v], gls_d[v], None),
+                               overlap="batched", early_views=2, deterministic=True)
+    dets = []
+    for _ in range(2):
+        bucket.flat.fill_(float("nan"))
+        step.run(det)
+        dets.append(bucket.flat.clone())
+    torch.cuda.synchronize()
+    assert torch.equal(dets[0], dets[1])
+    stats = {}
     for name, _ in FIELDS:
         f0, f1 = bucket.ranges[name]
-        a_, b_ = flats[0][f0:f1], flats[1][f0:f1]
-        scale = float(a_.abs().max())
-        assert float((a_ - b_).abs().max()) <= 1e-5 * scale, (name, float((a_ - b_).abs().max()), scale)
+        d_ = dets[0][f0:f1].double()
+        scale = float(d_.abs().max())
+        for a_ in (flats[0][f0:f1].double(), flats[1][f0:f1].double()):
+            err = (a_ - d_).abs()
+            bound = 1e-4 * d_.abs() + 1e-7 * scale
+            stats[name] = (float((err / (d_.abs() + 1e-30)).max()), float(err.max() / scale), int((err > bound).sum()))
+            assert bool((err <= bound).all()), (name, stats[name])
+    print("atomic vs deterministic (max rel, max abs/scale, over bound):", stats)
     assert len(render.pending) == 0
     # the forward is deterministic: both steps' images repeat bit for bit (a race or a lost
     # hazard in any compositor shows here first; see DESIGN.md 4.5 on the packed-fp32 build flag)

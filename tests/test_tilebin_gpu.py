@@ -125,6 +125,24 @@ def test_tile_bucket_split_scans_and_row_chunks():
                 assert np.array_equal(decode_point_words(a[4])[:n], decode_point_words(b[4])[:n]), v
 
 
+@pytest.mark.parametrize("tile_bucket", [True, False])
+def test_row_chunks_rejected_before_any_launch(tile_bucket):
+    """Invalid row chunks (a gap, r1 < r0, an unaligned start, short coverage) raise ValueError before
+    any preprocess launch or before() wait is enqueued, on both binning paths."""
+    sc, rss = _case("views10")
+    dev = sc.to("cuda")
+    kw = dict(scales=dev.scales, rotations=dev.rotations, shs=dev.shs, language_feature=dev.lang,
+              tile_bucket=tile_bucket)
+    P = dev.means3D.shape[0]
+    called = []
+    mark = lambda: called.append(1)   # noqa: E731
+    for chunks in ([(0, 1024, mark), (2048, P, mark)], [(0, 1024, mark), (1024, 512, mark), (512, P, mark)],
+                   [(0, 1000, mark), (1000, P, mark)], [(0, 1024, mark)]):
+        with pytest.raises(ValueError, match="row_chunks"):
+            dgr.preprocess_views_native(rss[:2], dev.means3D, dev.opacities, row_chunks=chunks, **kw)
+    assert not called
+
+
 def test_tile_bucket_single_view_render_native():
     """render_native of an unbinned tile-bucket view bins it the tile-bucket way first."""
     sc, rss = _case("views10")

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build the library of a git revision (default HEAD) into build/variants/liblsr_base.so for
-# same-box A/B runs against the working tree (tools/gpu_variants.sh benches every variant).
+# same-box A/B runs against the working tree (tools/gpu.sh ab benches the variants).
 set -e
 rev=${1:-HEAD}
 root=$(cd "$(dirname "$0")/.." && pwd)

@@ -1,16 +1,13 @@
 #!/bin/bash
-# Copy one round-profiling call's results (tools/gpu_round.sh + tools/gpu_mfma_pmc.sh) from
-# gpurun_out/ into profiles/<tag>/ and make its PMC traffic the one bench.py reports.
+# Copy one profiling call's results (tools/gpu.sh bench prof pmc mfma, OUT=<dir>) from
+# gpurun_out/<dir>/ into profiles/<tag>/ and make its PMC traffic the one bench.py reports.
 set -e
-tag=$1; [ -n "$tag" ] || { echo "usage: $0 <tag>"; exit 1; }
-root=$(cd "$(dirname "$0")/.." && pwd); o=$root/gpurun_out; d=$root/profiles/$tag
+tag=$1; src=${2:-run}; [ -n "$tag" ] || { echo "usage: $0 <tag> [gpurun_out subdir]"; exit 1; }
+root=$(cd "$(dirname "$0")/.." && pwd); o=$root/gpurun_out/$src; d=$root/profiles/$tag
 mkdir -p "$d"
-grep '^{' "$o/bench.log" | tail -1 > "$d/bench.json"
-grep '^{' "$o/prof_bench.log" | tail -1 > "$d/bench_under_rocprof.json" || true
-cp "$(find "$o/prof" -name '*kernel_stats.csv' | head -1)" "$d/kernel_stats.csv"
-cp "$o/pmc/summary.txt" "$d/pmc_summary.txt"
-cp "$o/pmc/pmc_traffic.json" "$d/pmc_traffic.json"
-cp "$o/pmc/pmc_traffic.json" "$root/profiles/pmc_traffic.json"
-[ -f "$o/mfma/raster_summary.txt" ] && cp "$o/mfma/raster_summary.txt" "$d/mfma_raster.txt"
-[ -f "$o/mfma/deform_summary.txt" ] && cp "$o/mfma/deform_summary.txt" "$d/mfma_deform.txt"
+for f in bench.json bench_under_rocprof.json kernel_stats.csv step_timeline.txt pmc_summary.txt pmc_traffic.json \
+         mfma_raster.txt mfma_deform.txt stall_summary.txt gpu_tests.txt ab.txt deform_ab.txt bench_deform.log; do
+    [ -f "$o/$f" ] && cp "$o/$f" "$d/$f"
+done
+[ -f "$o/pmc_traffic.json" ] && cp "$o/pmc_traffic.json" "$root/profiles/pmc_traffic.json"
 ls "$d"

@@ -14,7 +14,7 @@ build() {   # name, extra flags...
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/liblsr_$name.so $(ls $OBJ/*.o | grep -v "/deform.o") $OUT/obj/deform_$name.o
     echo "built $OUT/liblsr_$name.so"
 }
-# results (round 5, tools/gpu_deform_race.sh): slp, slp_pad1 and slp_pad2 corrupt (pad: more rows);
+# results (round 5, tools/gpu.sh race): slp, slp_pad1 and slp_pad2 corrupt (pad: more rows);
 # slp_wz faulted in the forward (illegal address) and is not built any more
 [ -z "$ONLY" ] && build slp
 [ "$ONLY" = slp ] && { build slp; exit 0; }
