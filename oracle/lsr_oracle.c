@@ -616,6 +616,14 @@ static void sh_backward(int deg, int M, const real *pos, const real *campos, con
     dL_dmean[2] += (-dir_orig[0] * dir_orig[2] * dLdx - dir_orig[1] * dir_orig[2] * dLdy + (sum2 - dir_orig[2] * dir_orig[2]) * dLdz) * invsum32;
 }
 
+/* Conditioning mode (test infrastructure): while on, the compositing backward adds the ABSOLUTE value
+ * of every per-pixel term of the directly accumulated gradients -- dL/dlanguage, dL/dopacity and
+ * dL/dmean2D -- so those outputs hold sum |term|, the scale of the rounding error any implementation's
+ * sum of them can carry.  Every other output is meaningless in this mode. */
+static int g_abs_terms = 0;
+void orc_set_abs_terms(int on) { g_abs_terms = on != 0; }
+#define TERM(v) (g_abs_terms ? ((v) < R(0.0) ? -(v) : (v)) : (v))
+
 /* dL_d* outputs are overwritten.  dL_ddepth_pix may be NULL (no depth gradient). */
 void orc_backward(const orc_state *st, const orc_settings *s,
                   const real *means3D, const real *shs, const real *colors_precomp, const real *lang,
@@ -687,7 +695,7 @@ void orc_backward(const orc_state *st, const orc_settings *s,
                             accF[c] = last_alpha * lastF[c] + (R(1.0) - last_alpha) * accF[c];
                             lastF[c] = f;
                             dL_dalpha += (f - accF[c]) * dF;
-                            ATOMIC_ADD(dL_dlang[(size_t)g * C + c], dchannel_dcolor * dF);
+                            ATOMIC_ADD(dL_dlang[(size_t)g * C + c], TERM(dchannel_dcolor * dF));
                         }
                     }
                     {
@@ -705,12 +713,12 @@ void orc_backward(const orc_state *st, const orc_settings *s,
                     const real gdx = G * dx, gdy = G * dy;
                     const real dG_ddelx = -gdx * co[0] - gdy * co[1];
                     const real dG_ddely = -gdy * co[2] - gdx * co[1];
-                    ATOMIC_ADD(dL_dmeans2D[3 * (size_t)g + 0], dL_dG * dG_ddelx * ddelx_dx);
-                    ATOMIC_ADD(dL_dmeans2D[3 * (size_t)g + 1], dL_dG * dG_ddely * ddely_dy);
+                    ATOMIC_ADD(dL_dmeans2D[3 * (size_t)g + 0], TERM(dL_dG * dG_ddelx * ddelx_dx));
+                    ATOMIC_ADD(dL_dmeans2D[3 * (size_t)g + 1], TERM(dL_dG * dG_ddely * ddely_dy));
                     ATOMIC_ADD(dL_dconic[3 * (size_t)g + 0], R(-0.5) * gdx * dx * dL_dG);
                     ATOMIC_ADD(dL_dconic[3 * (size_t)g + 1], R(-0.5) * gdx * dy * dL_dG);
                     ATOMIC_ADD(dL_dconic[3 * (size_t)g + 2], R(-0.5) * gdy * dy * dL_dG);
-                    ATOMIC_ADD(dL_dopacity[g], G * dL_dalpha);
+                    ATOMIC_ADD(dL_dopacity[g], TERM(G * dL_dalpha));
                 }
             }
         free(accF);

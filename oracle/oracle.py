@@ -142,7 +142,17 @@ class OracleResult:
             self._state = st
         return self._state
 
-    def backward(self, dL_dcolor, dL_dlang=None, dL_ddepth=None, nthreads=0):
+    def backward(self, dL_dcolor, dL_dlang=None, dL_ddepth=None, nthreads=0, abs_terms=False):
+        """abs_terms: the directly accumulated outputs (lang, opacity, means2D) hold the sums of the
+        absolute per-pixel terms instead (orc_set_abs_terms: each element's rounding-error scale);
+        the other outputs are then meaningless."""
+        self._lib.orc_set_abs_terms(ctypes.c_int(1 if abs_terms else 0))
+        try:
+            return self._backward(dL_dcolor, dL_dlang, dL_ddepth, nthreads)
+        finally:
+            self._lib.orc_set_abs_terms(ctypes.c_int(0))
+
+    def _backward(self, dL_dcolor, dL_dlang=None, dL_ddepth=None, nthreads=0):
         dt = np.float64 if self.double else np.float32
         P, M, C = self.P, self.M, self.C
         H, W = self.settings.image_height, self.settings.image_width

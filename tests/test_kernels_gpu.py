@@ -71,3 +71,24 @@ def test_packed_fp32_coresident(tmp_path):
     r = subprocess.run(["timeout", "-k", "5", "90", exe, "10"], capture_output=True, text=True)
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_waitcnt_forcezero_hazard(tmp_path):
+    """DESIGN.md 4.5, the -amdgpu-waitcnt-forcezero fault: the same division / sqrt fix-up patterns
+    (VALU writes a lane mask -> v_cndmask reads it), built as the library is (the hazard recognizer's
+    s_nop wait states) and with the debug flag (whose inserted s_waitcnt the recognizer counts as wait
+    states and drops the s_nop).  The library build must be exact; the flag build's count is reported:
+    wrong quotients there mean an s_waitcnt with nothing outstanding supplies no wait state, so that
+    flag's code under-pads the hazards (in k_pack_weight the quotient is a row index: an out-of-range
+    store, the illegal address)."""
+    src = os.path.join(ROOT, "tests", "kernels", "t_waitcnt_hazard.hip")
+    res = {}
+    for name, extra in (("plain", []), ("forcezero", ["-mllvm", "-amdgpu-waitcnt-forcezero"])):
+        exe = str(tmp_path / f"t_wc_{name}")
+        subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-fhip-fp32-correctly-rounded-divide-sqrt", *extra,
+                        "-o", exe, src], check=True)
+        r = subprocess.run(["timeout", "-k", "5", "60", exe], capture_output=True, text=True)
+        print(name, r.returncode, r.stdout)
+        assert r.returncode in (0, 1), r.stdout + r.stderr      # 1 = wrong values (reported), never a fault
+        res[name] = r.returncode
+    assert res["plain"] == 0
