@@ -69,13 +69,16 @@ constexpr int DN = 64;            // Gaussians per block
 constexpr int DWID = 128;         // MLP width
 constexpr int DAP = DWID + 8;     // LDS row pitch (bf16) of the hidden rows
 constexpr int DLP = 64 + 8;       // LDS row pitch (bf16) of rows of up to 64 entries
-__constant__ int kHeadOut[5] = {3, 3, 4, 1, 48};
+// head output widths {3, 3, 4, 1, 48} (pos, scales, rotations, opacity, SH), as arithmetic: no
+// constant-memory load (a PC-relative s_getpc_b64 sequence) on the heads' paths
 
 __device__ __forceinline__ void dsplit(float x, __bf16& hi, __bf16& lo) {
     hi = (__bf16)x;
     lo = (__bf16)(x - (float)hi);
 }
-__device__ __forceinline__ int head_out(const DeformArgs& a, int hd) { return hd < 5 ? kHeadOut[hd] : a.centers; }
+__device__ __forceinline__ int head_out(const DeformArgs& a, int hd) {
+    return hd < 2 ? 3 : hd == 2 ? 4 : hd == 3 ? 1 : hd == 4 ? 48 : a.centers;
+}
 __device__ __forceinline__ int row_of(int mt, int q, int hh) { return 32 * mt + (q & 3) + 8 * (q >> 2) + 4 * hh; }
 
 // Y[64 x 32] (+)= X[64 x K] W^T for N tile `nt`: both M tiles (the block's 64 Gaussians) share
@@ -1464,6 +1467,254 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
 }
 
+// Version 2 (round 6): the same products at ONE wave per SIMD, with what version 1 re-read per 64-row
+// tile held in registers for the whole block -- the wave's W1 fragments (its 32 columns, K = 128: 64
+// registers) and, for the wide heads, its W2^T fragments (K = 64: 32 registers) -- and the next tile's
+// A and G rows loaded into registers while the current tile computes (version 1 waited on an L2 round
+// trip of 64 KB of weight fragments and one of the tile's rows per tile, at 2 waves per SIMD with no
+// registers left to prefetch).  The accumulators move to AGPRs (512 registers per wave at one wave
+// per SIMD).  Blocks: 64 per small head (the four share each row range on one XCD: grid x is a
+// multiple of 8, so their A reads meet in that XCD's L2) and 256 for a wide head, one round of 256
+// CUs each.
+template <bool SMALL>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) k_head_wgrad2(HeadWgradArgs ha, int job0) {
+    __shared__ __attribute__((aligned(16))) __bf16 s_ah[DN * DAP];   // A rows [64][128] hi / lo
+    __shared__ __attribute__((aligned(16))) __bf16 s_al[DN * DAP];
+    __shared__ __attribute__((aligned(16))) __bf16 s_gh[SMALL ? 8 : DN * DGP];   // G rows [64][64 pad] hi / lo
+    __shared__ __attribute__((aligned(16))) __bf16 s_gl[SMALL ? 8 : DN * DGP];
+    __shared__ __attribute__((aligned(16))) float4 s_g4[SMALL ? DN : 1];        // SMALL: G rows fp32
+    __shared__ __attribute__((aligned(16))) __bf16 s_w2h[SMALL ? 8 : DWID * DLP];   // !SMALL: W2^T [128][64 pad]
+    __shared__ __attribute__((aligned(16))) __bf16 s_w2l[SMALL ? 8 : DWID * DLP];
+    LDS_POISON(s_ah); LDS_POISON(s_al); LDS_POISON(s_gh); LDS_POISON(s_gl); LDS_POISON(s_g4); LDS_POISON(s_w2h);
+    LDS_POISON(s_w2l); LDS_POISON_DONE();
+    typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+    const HeadWgradJob& j = ha.job[job0 + blockIdx.y];
+    const int64_t row0 = (int64_t)blockIdx.x * ha.rows_per_block;
+    const int64_t row1 = min((int64_t)ha.P, row0 + ha.rows_per_block);
+    if (row0 >= row1) return;                                            // block-uniform
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+    const int nout = j.nout, Mo = (nout + 31) / 32;                      // G^T M tiles (1 or 2)
+    const int col = 32 * wave + r;
+    const float b1c = j.b1[col];
+    // ---- the wave's weight fragments, once per block ---------------------------------------------------
+    dbf16x8 w1h[DWID / 16], w1l[DWID / 16];
+#pragma unroll
+    for (int ks = 0; ks < DWID / 16; ++ks) {
+        const size_t wo = (size_t)col * DWID + 16 * ks + 8 * hh;
+        w1h[ks] = *reinterpret_cast<const dbf16x8*>(j.w1_h + wo);
+        w1l[ks] = *reinterpret_cast<const dbf16x8*>(j.w1_l + wo);
+    }
+    if constexpr (!SMALL) {   // the wide head's W2^T in LDS (registers would spill), visible after the first barrier
+        for (int i = tid; i < DWID * 64 / 8; i += 256) {
+            const int rr = i >> 3, c8 = (i & 7) * 8;
+            *reinterpret_cast<dbf16x8*>(s_w2h + rr * DLP + c8) = *reinterpret_cast<const dbf16x8*>(j.w2t_h + rr * 64 + c8);
+            *reinterpret_cast<dbf16x8*>(s_w2l + rr * DLP + c8) = *reinterpret_cast<const dbf16x8*>(j.w2t_l + rr * 64 + c8);
+        }
+    }
+    df32x16 w1acc[4] = {df32x16{}, df32x16{}, df32x16{}, df32x16{}};   // dW1 rows 32 wave .., col tiles 0..3
+    df32x16 w2acc[SMALL ? 1 : 2];                                         // dW2 o tiles 0..1, col tile wave
+    float w2s[DEF_SMALL_OUT] = {0.0f, 0.0f, 0.0f, 0.0f};                 // SMALL: dW2 rows 0..3, column col
+    float w2c[DEF_SMALL_OUT] = {0.0f, 0.0f, 0.0f, 0.0f};                 // SMALL: W2 rows 0..3, column col
+    float4 db2v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if constexpr (SMALL) w2_column(j.w2_h, j.w2_l, col, w2c);
+    else { w2acc[0] = df32x16{}; w2acc[1] = df32x16{}; }
+    float db1 = 0.0f, db2 = 0.0f;
+    // ---- the tile's rows in registers: A (thread: 8 float4 of rows (tid + 256 i) >> 5), G ---------------
+    float4 pa[DN * DWID / 4 / 256];
+    float pg[SMALL ? DEF_SMALL_OUT : DN * 64 / 256];
+    auto load_tile = [&](int64_t t0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < DN * DWID / 4 / 256; ++i) {
+            const int e = tid + 256 * i, rr = e >> 5, c4 = (e & 31) * 4;
+            const int64_t g = t0 + rr;
+            pa[i] = g < row1 ? *reinterpret_cast<const float4*>(ha.A + g * DWID + c4) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        }
+        if constexpr (SMALL) {
+            const int64_t g = t0 + tid;
+#pragma unroll
+            for (int k = 0; k < DEF_SMALL_OUT; ++k) pg[k] = (tid < DN && k < nout && g < row1) ? j.G[g * nout + k] : 0.0f;
+        } else {
+#pragma unroll
+            for (int i = 0; i < DN * 64 / 256; ++i) {
+                const int e = tid + 256 * i, rr = e >> 6, k = e & 63;
+                const int64_t g = t0 + rr;
+                pg[i] = (k < nout && g < row1) ? j.G[g * nout + k] : 0.0f;
+            }
+        }
+    };
+    auto store_tile = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < DN * DWID / 4 / 256; ++i) {
+            const int e = tid + 256 * i, rr = e >> 5, c4 = (e & 31) * 4;
+            const float f[4] = {pa[i].x, pa[i].y, pa[i].z, pa[i].w};
+            bf4 h4, l4;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                __bf16 hi, lo;
+                dsplit(f[q], hi, lo);
+                h4[q] = hi; l4[q] = lo;
+            }
+            *reinterpret_cast<bf4*>(s_ah + rr * DAP + c4) = h4;
+            *reinterpret_cast<bf4*>(s_al + rr * DAP + c4) = l4;
+        }
+        if constexpr (SMALL) {
+            if (tid < DN) {
+                const float4 gv = make_float4(pg[0], pg[1], pg[2], pg[3]);
+                s_g4[tid] = gv;
+                db2v.x += gv.x; db2v.y += gv.y; db2v.z += gv.z; db2v.w += gv.w;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < DN * 64 / 256; ++i) {   // column k = tid & 63 for every i: db2 in a register
+                const int e = tid + 256 * i, rr = e >> 6, k = e & 63;
+                db2 += pg[i];
+                __bf16 hi, lo;
+                dsplit(pg[i], hi, lo);
+                s_gh[rr * DGP + k] = hi;
+                s_gl[rr * DGP + k] = lo;
+            }
+        }
+    };
+    load_tile(row0);
+    for (int64_t t0 = row0; t0 < row1; t0 += DN) {
+        store_tile();
+        __syncthreads();
+        if (t0 + DN < row1) load_tile(t0 + DN);   // in flight while this tile computes
+        // ---- Z1 for this wave's 32 columns (both row tiles), then dW2 and dZ1 ------------------------------
+        uint32_t zpos = 0;   // bit 16 mt + q: Z1 > 0
+        df32x16 d[2] = {df32x16{}, df32x16{}};
+        {
+            df32x16 z[2] = {df32x16{}, df32x16{}};
+#pragma unroll
+            for (int ks = 0; ks < DWID / 16; ++ks) {
+                const int k0 = 16 * ks + 8 * hh;
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) {
+                    const dbf16x8 ah = *reinterpret_cast<const dbf16x8*>(s_ah + (32 * mt + r) * DAP + k0);
+                    const dbf16x8 al = *reinterpret_cast<const dbf16x8*>(s_al + (32 * mt + r) * DAP + k0);
+                    z[mt] = DMFMA(ah, w1h[ks], z[mt]);
+                    z[mt] = DMFMA(ah, w1l[ks], z[mt]);
+                    z[mt] = DMFMA(al, w1h[ks], z[mt]);
+                }
+            }
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const float zz = z[mt][q] + b1c;
+                    zpos |= zz > 0.0f ? 1u << (16 * mt + q) : 0u;
+                    z[mt][q] = fmaxf(zz, 0.0f);
+                }
+            if constexpr (SMALL) {
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) {
+                        const float4 gv = s_g4[row_of(mt, q, hh)];
+                        const float zz = z[mt][q];
+                        w2s[0] = __builtin_fmaf(gv.x, zz, w2s[0]); w2s[1] = __builtin_fmaf(gv.y, zz, w2s[1]);
+                        w2s[2] = __builtin_fmaf(gv.z, zz, w2s[2]); w2s[3] = __builtin_fmaf(gv.w, zz, w2s[3]);
+                        float dv = gv.x * w2c[0];
+                        dv = __builtin_fmaf(gv.y, w2c[1], dv);
+                        dv = __builtin_fmaf(gv.z, w2c[2], dv);
+                        dv = __builtin_fmaf(gv.w, w2c[3], dv);
+                        d[mt][q] = dv;
+                    }
+            } else {
+#pragma unroll
+                for (int ks = 0; ks < DN / 16; ++ks) {
+                    dbf16x8 zh, zl;
+                    wg_regs_to_op(z[ks >> 1], ks & 1, zh, zl);
+#pragma unroll
+                    for (int mo = 0; mo < 2; ++mo) {
+                        if (mo >= Mo) break;
+                        const dbf16x8 gh = wg_lds_op(s_gh, DGP, ks, 32 * mo), gl = wg_lds_op(s_gl, DGP, ks, 32 * mo);
+                        w2acc[mo] = DMFMA(gh, zh, w2acc[mo]);
+                        w2acc[mo] = DMFMA(gh, zl, w2acc[mo]);
+                        w2acc[mo] = DMFMA(gl, zh, w2acc[mo]);
+                    }
+                }
+            }
+        }
+        // ---- dZ1 = (G W2) [Z1 > 0] -> dW1 += dZ1^T A (rows 32 wave .. of dW1), db1 ------------------------
+        {
+            if constexpr (!SMALL) {
+#pragma unroll
+                for (int ks = 0; ks < 4; ++ks) {
+                    const int k0 = 16 * ks + 8 * hh;
+                    const dbf16x8 w2h = *reinterpret_cast<const dbf16x8*>(s_w2h + col * DLP + k0);
+                    const dbf16x8 w2l = *reinterpret_cast<const dbf16x8*>(s_w2l + col * DLP + k0);
+#pragma unroll
+                    for (int mt = 0; mt < 2; ++mt) {
+                        const dbf16x8 gh = *reinterpret_cast<const dbf16x8*>(s_gh + (32 * mt + r) * DGP + k0);
+                        const dbf16x8 gl = *reinterpret_cast<const dbf16x8*>(s_gl + (32 * mt + r) * DGP + k0);
+                        d[mt] = DMFMA(gh, w2h, d[mt]);
+                        d[mt] = DMFMA(gh, w2l, d[mt]);
+                        d[mt] = DMFMA(gl, w2h, d[mt]);
+                    }
+                }
+            }
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    d[mt][q] = (zpos >> (16 * mt + q)) & 1u ? d[mt][q] : 0.0f;
+                    db1 += d[mt][q];
+                }
+#pragma unroll
+            for (int ks = 0; ks < DN / 16; ++ks) {
+                dbf16x8 dh, dl;
+                wg_regs_to_op(d[ks >> 1], ks & 1, dh, dl);
+#pragma unroll
+                for (int nt = 0; nt < 4; ++nt) {
+                    const dbf16x8 bh = wg_lds_op(s_ah, DAP, ks, 32 * nt), bl = wg_lds_op(s_al, DAP, ks, 32 * nt);
+                    w1acc[nt] = DMFMA(dh, bh, w1acc[nt]);
+                    w1acc[nt] = DMFMA(dh, bl, w1acc[nt]);
+                    w1acc[nt] = DMFMA(dl, bh, w1acc[nt]);
+                }
+            }
+        }
+        __syncthreads();   // the tile's LDS rows read before the next tile's are stored
+    }
+    // ---- the block's partial products: one atomic per element (as version 1) ---------------------------
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int m = 32 * wave + (q & 3) + 8 * (q >> 2) + 4 * hh;
+            atomicAdd(j.dW1 + (size_t)m * DWID + 32 * nt + r, w1acc[nt][q]);
+        }
+    db1 += __shfl_xor(db1, 32);
+    if (hh == 0) atomicAdd(j.db1 + col, db1);
+    if constexpr (SMALL) {
+#pragma unroll
+        for (int k = 0; k < DEF_SMALL_OUT; ++k) {
+            const float v = w2s[k] + __shfl_xor(w2s[k], 32);
+            if (hh == 0 && k < nout) atomicAdd(j.dW2 + (size_t)k * DWID + col, v);
+        }
+        if (wave == 0) {
+            float v[DEF_SMALL_OUT] = {db2v.x, db2v.y, db2v.z, db2v.w};
+#pragma unroll
+            for (int k = 0; k < DEF_SMALL_OUT; ++k) {
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) v[k] += __shfl_xor(v[k], off);
+                if (lane == 0 && k < nout) atomicAdd(j.db2 + k, v[k]);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int mo = 0; mo < 2; ++mo) {
+            if (mo >= Mo) break;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int o = 32 * mo + (q & 3) + 8 * (q >> 2) + 4 * hh;
+                if (o < nout) atomicAdd(j.dW2 + (size_t)o * DWID + col, w2acc[mo][q]);
+            }
+        }
+        if ((tid & 63) < nout) atomicAdd(j.db2 + (tid & 63), db2);
+    }
+}
+
 // Rows per block of a launch, for about `blocks` blocks per head: 128 for the small-output heads
 // (their per-block flush of dW1 / dW2 partials is most of their atomics), 400 for the SH head.
 // Measured against the split-K default of 256 blocks per head: deformation backward 11.96-11.99
@@ -1484,6 +1735,23 @@ void launch_head_wgrad(const HeadWgradArgs& a, int njobs, hipStream_t st) {
         if (a.job[i].nout <= DEF_SMALL_OUT) s.job[ns++] = a.job[i];
     for (int i = 0; i < njobs; ++i)
         if (a.job[i].nout > DEF_SMALL_OUT) { s.job[ns + nbig] = a.job[i]; ++nbig; }
+    // version 2 by default (2M backward 10.10 -> 9.34 ms); LSR_WGRAD_V=1: version 1 (diagnostic A/B)
+    static const int ver = [] { const char* e = std::getenv("LSR_WGRAD_V"); return e ? std::atoi(e) : 2; }();
+    if (ver == 2) {   // one round of 256 CUs per launch: 64 blocks per small head, 256 for a wide head
+        if (ns) {
+            const int nb = ns <= 4 ? 256 / ns / 8 * 8 : 32;
+            s.rows_per_block = std::max(64, ((a.P + nb - 1) / nb + 63) / 64 * 64);
+            hipLaunchKernelGGL(k_head_wgrad2<true>, dim3((a.P + s.rows_per_block - 1) / s.rows_per_block, ns), dim3(256),
+                               0, st, s, 0);
+        }
+        if (nbig) {
+            const int nb = std::max(8, 256 / nbig / 8 * 8);
+            s.rows_per_block = std::max(64, ((a.P + nb - 1) / nb + 63) / 64 * 64);
+            hipLaunchKernelGGL(k_head_wgrad2<false>, dim3((a.P + s.rows_per_block - 1) / s.rows_per_block, nbig),
+                               dim3(256), 0, st, s, ns);
+        }
+        return;
+    }
     if (ns) {
         s.rows_per_block = wgrad_rows("LSR_WGRAD_ROWS_SMALL", a.P, 128);
         const int nb = (a.P + s.rows_per_block - 1) / s.rows_per_block;

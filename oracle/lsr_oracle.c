@@ -616,13 +616,16 @@ static void sh_backward(int deg, int M, const real *pos, const real *campos, con
     dL_dmean[2] += (-dir_orig[0] * dir_orig[2] * dLdx - dir_orig[1] * dir_orig[2] * dLdy + (sum2 - dir_orig[2] * dir_orig[2]) * dLdz) * invsum32;
 }
 
-/* Conditioning mode (test infrastructure): while on, the compositing backward adds the ABSOLUTE value
- * of every per-pixel term of the directly accumulated gradients -- dL/dlanguage, dL/dopacity and
- * dL/dmean2D -- so those outputs hold sum |term|, the scale of the rounding error any implementation's
- * sum of them can carry.  Every other output is meaningless in this mode. */
+/* Conditioning mode (test infrastructure): while on, the compositing backward accumulates, for the
+ * directly accumulated gradients -- dL/dlanguage, dL/dopacity and dL/dmean2D -- the sum over pixels of
+ * the magnitude of every term an implementation's value is built from (dL/dalpha's channel products
+ * and blended predecessors taken in absolute value, dG/dmean's two products likewise), i.e. the scale
+ * relative to which any implementation's rounding of those sums is measured.  Every other output is
+ * meaningless in this mode. */
 static int g_abs_terms = 0;
 void orc_set_abs_terms(int on) { g_abs_terms = on != 0; }
-#define TERM(v) (g_abs_terms ? ((v) < R(0.0) ? -(v) : (v)) : (v))
+#define RABS(v) ((v) < R(0.0) ? -(v) : (v))
+#define TERM(v) (g_abs_terms ? RABS(v) : (v))
 
 /* dL_d* outputs are overwritten.  dL_ddepth_pix may be NULL (no depth gradient). */
 void orc_backward(const orc_state *st, const orc_settings *s,
@@ -653,8 +656,9 @@ void orc_backward(const orc_state *st, const orc_settings *s,
     for (int tile = 0; tile < gx * gy; ++tile) {
         const int tx = tile % gx, ty = tile / gx;
         const uint32_t r0 = st->ranges[2 * tile], r1 = st->ranges[2 * tile + 1];
-        real *accF = (real *)malloc(sizeof(real) * (size_t)(C > 0 ? 2 * C : 2));
+        real *accF = (real *)malloc(sizeof(real) * (size_t)(C > 0 ? 3 * C : 3));
         real *lastF = accF + (C > 0 ? C : 1);
+        real *accFA = lastF + (C > 0 ? C : 1);   /* conditioning mode: blends of |feature| */
         for (int py = ty * BLOCK_Y; py < imin(ty * BLOCK_Y + BLOCK_Y, H); ++py)
             for (int px = tx * BLOCK_X; px < imin(tx * BLOCK_X + BLOCK_X, W); ++px) {
                 const size_t pid = (size_t)py * W + px;
@@ -663,7 +667,8 @@ void orc_backward(const orc_state *st, const orc_settings *s,
                 const uint32_t last_contributor = st->n_contrib[pid];
                 uint32_t contributor = r1 - r0;
                 real acc[3] = {0, 0, 0}, lastc[3] = {0, 0, 0}, accD = 0, lastD = 0, last_alpha = 0;
-                for (int c = 0; c < C; ++c) { accF[c] = 0; lastF[c] = 0; }
+                real accA[3] = {0, 0, 0}, accDA = 0;   /* conditioning mode: blends of |colour|, |depth| */
+                for (int c = 0; c < C; ++c) { accF[c] = 0; lastF[c] = 0; accFA[c] = 0; }
                 real dpix[3];
                 for (int c = 0; c < 3; ++c) dpix[c] = dL_dpix[c * HW + pid];
                 const real dpixD = dL_dpix_depth ? dL_dpix_depth[pid] : R(0.0);
@@ -681,8 +686,15 @@ void orc_backward(const orc_state *st, const orc_settings *s,
                     T = T / (R(1.0) - alpha);
                     const real dchannel_dcolor = alpha * T;
                     real dL_dalpha = 0;
+                    /* conditioning mode: the scale of dL/dalpha's terms, T sum (|c| + blend |c_prev|) |dL/dpix|
+                     * (an implementation's dot(c, dL/dpix) - acc rounds relative to it, not to the difference) */
+                    real dLa_abs = 0;
                     for (int c = 0; c < 3; ++c) {
                         const real col = st->rgb[3 * (size_t)g + c];
+                        if (g_abs_terms) {
+                            accA[c] = last_alpha * RABS(lastc[c]) + (R(1.0) - last_alpha) * accA[c];
+                            dLa_abs += (RABS(col) + accA[c]) * RABS(dpix[c]);
+                        }
                         acc[c] = last_alpha * lastc[c] + (R(1.0) - last_alpha) * acc[c];
                         lastc[c] = col;
                         dL_dalpha += (col - acc[c]) * dpix[c];
@@ -692,6 +704,10 @@ void orc_backward(const orc_state *st, const orc_settings *s,
                         for (int c = 0; c < C; ++c) {
                             const real f = lang[(size_t)g * C + c];
                             const real dF = dL_dpix_lang[c * HW + pid];
+                            if (g_abs_terms) {
+                                accFA[c] = last_alpha * RABS(lastF[c]) + (R(1.0) - last_alpha) * accFA[c];
+                                dLa_abs += (RABS(f) + accFA[c]) * RABS(dF);
+                            }
                             accF[c] = last_alpha * lastF[c] + (R(1.0) - last_alpha) * accF[c];
                             lastF[c] = f;
                             dL_dalpha += (f - accF[c]) * dF;
@@ -700,6 +716,10 @@ void orc_backward(const orc_state *st, const orc_settings *s,
                     }
                     {
                         const real dep = st->depth[g];
+                        if (g_abs_terms) {
+                            accDA = last_alpha * RABS(lastD) + (R(1.0) - last_alpha) * accDA;
+                            dLa_abs += (RABS(dep) + accDA) * RABS(dpixD);
+                        }
                         accD = last_alpha * lastD + (R(1.0) - last_alpha) * accD;
                         lastD = dep;
                         dL_dalpha += (dep - accD) * dpixD;
@@ -713,12 +733,20 @@ void orc_backward(const orc_state *st, const orc_settings *s,
                     const real gdx = G * dx, gdy = G * dy;
                     const real dG_ddelx = -gdx * co[0] - gdy * co[1];
                     const real dG_ddely = -gdy * co[2] - gdx * co[1];
-                    ATOMIC_ADD(dL_dmeans2D[3 * (size_t)g + 0], TERM(dL_dG * dG_ddelx * ddelx_dx));
-                    ATOMIC_ADD(dL_dmeans2D[3 * (size_t)g + 1], TERM(dL_dG * dG_ddely * ddely_dy));
+                    if (g_abs_terms) {
+                        dLa_abs = dLa_abs * T + (T_final / (R(1.0) - alpha)) *
+                                  (RABS(s->bg[0] * dpix[0]) + RABS(s->bg[1] * dpix[1]) + RABS(s->bg[2] * dpix[2]));
+                        const real aG = RABS(co[3]) * dLa_abs;
+                        ATOMIC_ADD(dL_dmeans2D[3 * (size_t)g + 0], aG * (RABS(gdx * co[0]) + RABS(gdy * co[1])) * ddelx_dx);
+                        ATOMIC_ADD(dL_dmeans2D[3 * (size_t)g + 1], aG * (RABS(gdy * co[2]) + RABS(gdx * co[1])) * ddely_dy);
+                    } else {
+                        ATOMIC_ADD(dL_dmeans2D[3 * (size_t)g + 0], dL_dG * dG_ddelx * ddelx_dx);
+                        ATOMIC_ADD(dL_dmeans2D[3 * (size_t)g + 1], dL_dG * dG_ddely * ddely_dy);
+                    }
                     ATOMIC_ADD(dL_dconic[3 * (size_t)g + 0], R(-0.5) * gdx * dx * dL_dG);
                     ATOMIC_ADD(dL_dconic[3 * (size_t)g + 1], R(-0.5) * gdx * dy * dL_dG);
                     ATOMIC_ADD(dL_dconic[3 * (size_t)g + 2], R(-0.5) * gdy * dy * dL_dG);
-                    ATOMIC_ADD(dL_dopacity[g], TERM(G * dL_dalpha));
+                    ATOMIC_ADD(dL_dopacity[g], g_abs_terms ? G * dLa_abs : G * dL_dalpha);
                 }
             }
         free(accF);

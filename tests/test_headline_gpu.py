@@ -137,11 +137,14 @@ def test_bench_pipeline_matches_oracle_at_headline_size():
     # difference scales with the size of its per-pixel terms, not with its own value (a sum that cancels
     # keeps its terms' rounding).  For the gradients the compositor accumulates directly -- dL/dlanguage,
     # dL/dopacity, dL/dmean2D: every value the compositor's lanes produce reaches one of them -- the
-    # oracle gives that scale exactly: A = sum over the views' pixels of |term| (abs_terms), so
+    # oracle gives that scale: A = the sum over the views' pixels of the magnitudes of the terms each
+    # value is built from (abs_terms: dL/dalpha's channel products and blended predecessors, dG/dmean's
+    # products, all in absolute value -- dL/dalpha = (dot(c, dL/dpix) - acc) T cancels, and both paths
+    # round it relative to its terms), so
     #     |atomic - deterministic| <= 1e-4 |deterministic| + c A
-    # with c = 1e-4 (language, opacity: the same terms on both paths) and 2e-3 (means2D: the compositor
-    # forms it from quadrant-local pixel moments, X M0 - Mx, whose rounding is relative to sum |t| times
-    # the quadrant's 8-pixel extent rather than to sum |t (X - x)|).  No floor: a lost low half of a
+    # with c = 1e-4 (language, opacity) and 2e-3 (means2D: the compositor forms it from quadrant-local
+    # pixel moments, X M0 - Mx, whose rounding is relative to sum |t| times the quadrant's 8-pixel
+    # extent rather than to sum |t (X - x)|).  No floor: a lost low half of a
     # packed-fp32 result in a compositor lane moves an element by O(its terms) and fails
     # this for every Gaussian, small-magnitude ones included.  The other fields are linear maps of the
     # same accumulated rows through k_preprocess_bwd_views (no atomics), held per element to
@@ -168,9 +171,13 @@ def test_bench_pipeline_matches_oracle_at_headline_size():
                 st["max_err_over_A"] = float((err / (A + 1e-30)).max())
                 st["over_1e-4A"] = int((err > 1e-4 * d_.abs() + 1e-4 * A).sum())
             stats[(name, i)] = st
-            n_bad = int((err > bound).sum())
+            over = err > bound
+            n_bad = int(over.sum())
             if n_bad:
-                bad[(name, i)] = n_bad
+                o_ = torch.from_numpy(total[key]).reshape(P, -1)
+                idx = torch.nonzero(over)[:6]
+                bad[(name, i)] = (n_bad, [(int(g), int(c), float(a_[g, c]), float(d_[g, c]), float(o_[g, c]),
+                                           None if A is None else float(A[g, c])) for g, c in idx.tolist()])
     print("atomic vs deterministic:", stats)
     assert not bad, (bad, stats)
 

@@ -58,3 +58,32 @@ def test_pattern_matches_the_faulting_form():
     assert BROADCAST.search("v_pk_fma_f32 v[2:3], v[4:5], v[8:9], v[2:3] op_sel:[0,1,0] op_sel_hi:[0,1,1]")
     assert not BROADCAST.search("v_pk_mul_f32 v[2:3], v[4:5], v[8:9] op_sel_hi:[1,0]")
     assert not BROADCAST.search("v_pk_mul_f32 v[2:3], v[4:5], v[8:9] op_sel:[0,1] op_sel_hi:[0,0]")
+
+
+def test_pc_relative_sequences_are_unbroken(tmp_path):
+    """The -amdgpu-waitcnt-forcezero fault, found in round 6: a PC-relative address is
+    s_getpc_b64 s[n:n+1]; s_add_u32 sn, sn, sym@rel32@lo+4; s_addc_u32 sn+1, sn+1, sym@rel32@hi+12,
+    whose relocation addends assume the two adds follow s_getpc_b64 back to back.  That debug flag
+    inserted an s_waitcnt after s_getpc_b64 and another before s_addc_u32, so kHeadOut (the heads'
+    output widths, constant memory) was read 4 bytes early, a head's width came out wrong and its output
+    stores left their buffer: the illegal address of the first deformation forward.  Every shipped code
+    object must keep each such sequence contiguous."""
+    for lib in LIBS:
+        if not os.path.exists(lib):
+            continue
+        work = tmp_path / ("pc_" + os.path.basename(lib))
+        work.mkdir()
+        objs = disassemble(lib, work)
+        n = 0
+        for f, text in objs.items():
+            ins = [ln.split("//")[0].strip() for ln in text.splitlines()]
+            ins = [x for x in ins if x and not x.endswith(":") and not x.startswith("<") and "file format" not in x
+                   and not x.startswith("Disassembly")]
+            for i, x in enumerate(ins):
+                if x.startswith("s_getpc_b64"):
+                    n += 1
+                    reg = x.split()[1]                                   # s[a:b]
+                    lo, hi = reg[2:-1].split(":")
+                    assert ins[i + 1].startswith(f"s_add_u32 s{lo}, s{lo},"), (f, ins[i:i + 3])
+                    assert ins[i + 2].startswith(f"s_addc_u32 s{hi}, s{hi},"), (f, ins[i:i + 3])
+        assert n > 0   # the check saw the sequences it guards
