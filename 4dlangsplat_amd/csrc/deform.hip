@@ -1715,6 +1715,256 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
     }
 }
 
+// Version 3 (round 6, the small heads): version 2's products software-pipelined across tiles so that
+// one wave per SIMD keeps its matrix core fed.  Three LDS tile buffers; iteration t runs
+//   A: Z1 of tile t + 1 (MFMA, buffer t + 1)  beside  relu / dZ1 / dW2 of tile t (VALU, Z1(t) in registers)
+//   B: dW1 += dZ1(t)^T A(t) (MFMA, buffer t)   beside  tile t + 2's rows into buffer t + 2 (VALU + LDS stores)
+// then tile t + 3's rows are loaded into registers and one barrier ends the iteration (buffer t is
+// free for tile t + 3, tile t + 2 is visible).  An iteration is branch-free (loads at clamped rows,
+// zeros selected past the block's rows; Z1 past the last tile is computed and dropped) and each stage
+// interleaves its two chains by hand, K step by K step, fenced by sched_barrier (sched_group_barrier
+// patterns did not take: the compiler hoisted the VALU chain out of the MFMA region).  Version 2 ran
+// the chains one after the other: 2.27 -> 2.03 ms for the four small heads at 2M.  W1's lo half sits
+// in LDS (registers hold the hi half) so that nothing spills.
+template <bool SMALL>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) k_head_wgrad3(HeadWgradArgs ha, int job0) {
+    static_assert(SMALL, "version 3 covers the heads of at most DEF_SMALL_OUT outputs");
+    constexpr int NB = 3;
+    __shared__ __attribute__((aligned(16))) __bf16 s_ah[NB][DN * DAP];   // A rows [64][128] hi / lo
+    __shared__ __attribute__((aligned(16))) __bf16 s_al[NB][DN * DAP];
+    __shared__ __attribute__((aligned(16))) float4 s_g4[NB][DN];         // G rows fp32
+    __shared__ __attribute__((aligned(16))) __bf16 s_w1l[DWID * DAP];    // W1 lo [128][128] (hi in registers)
+    LDS_POISON(s_ah); LDS_POISON(s_al); LDS_POISON(s_g4); LDS_POISON(s_w1l); LDS_POISON_DONE();
+    typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+    const HeadWgradJob& j = ha.job[job0 + blockIdx.y];
+    const int64_t row0 = (int64_t)blockIdx.x * ha.rows_per_block;
+    const int64_t row1 = min((int64_t)ha.P, row0 + ha.rows_per_block);
+    if (row0 >= row1) return;                                            // block-uniform
+    const int T = (int)((row1 - row0 + DN - 1) / DN);                    // tiles of this block
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+    const int nout = j.nout;
+    const int col = 32 * wave + r;
+    const float b1c = j.b1[col];
+    dbf16x8 w1h[DWID / 16];
+#pragma unroll
+    for (int ks = 0; ks < DWID / 16; ++ks)
+        w1h[ks] = *reinterpret_cast<const dbf16x8*>(j.w1_h + (size_t)col * DWID + 16 * ks + 8 * hh);
+    for (int i = tid; i < DWID * DWID / 8; i += 256) {   // visible after the prologue's barrier
+        const int rr = i >> 4, c8 = (i & 15) * 8;
+        *reinterpret_cast<dbf16x8*>(&s_w1l[rr * DAP + c8]) = *reinterpret_cast<const dbf16x8*>(j.w1_l + rr * DWID + c8);
+    }
+    df32x16 w1acc[4] = {df32x16{}, df32x16{}, df32x16{}, df32x16{}};
+    float w2s[DEF_SMALL_OUT] = {0.0f, 0.0f, 0.0f, 0.0f};
+    float w2c[DEF_SMALL_OUT] = {0.0f, 0.0f, 0.0f, 0.0f};
+    float4 db2v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    w2_column(j.w2_h, j.w2_l, col, w2c);
+    float db1 = 0.0f;
+    float4 pa[DN * DWID / 4 / 256];
+    float pg[DEF_SMALL_OUT];
+    // branch-free (so that an iteration stays one scheduling region): every load is issued at a clamped
+    // row and rows past row1 (tiles past the block's last included) are selected to zero
+    auto load_tile = [&](int t) __attribute__((always_inline)) {
+        const int64_t t0 = row0 + (int64_t)t * DN;
+#pragma unroll
+        for (int i = 0; i < DN * DWID / 4 / 256; ++i) {
+            const int e = tid + 256 * i, rr = e >> 5, c4 = (e & 31) * 4;
+            const int64_t g = t0 + rr;
+            const float4 v = *reinterpret_cast<const float4*>(ha.A + min(g, row1 - 1) * DWID + c4);
+            const bool ok = g < row1;
+            pa[i] = make_float4(ok ? v.x : 0.0f, ok ? v.y : 0.0f, ok ? v.z : 0.0f, ok ? v.w : 0.0f);
+        }
+        const int64_t g = t0 + (tid & (DN - 1));
+#pragma unroll
+        for (int k = 0; k < DEF_SMALL_OUT; ++k) {
+            const float v = j.G[min(g, row1 - 1) * nout + min(k, nout - 1)];
+            pg[k] = (tid < DN && k < nout && g < row1) ? v : 0.0f;
+        }
+    };
+    auto store_tile = [&](int b) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < DN * DWID / 4 / 256; ++i) {
+            const int e = tid + 256 * i, rr = e >> 5, c4 = (e & 31) * 4;
+            const float f[4] = {pa[i].x, pa[i].y, pa[i].z, pa[i].w};
+            bf4 h4, l4;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                __bf16 hi, lo;
+                dsplit(f[q], hi, lo);
+                h4[q] = hi; l4[q] = lo;
+            }
+            *reinterpret_cast<bf4*>(&s_ah[b][rr * DAP + c4]) = h4;
+            *reinterpret_cast<bf4*>(&s_al[b][rr * DAP + c4]) = l4;
+        }
+        if (tid < DN) {
+            const float4 gv = make_float4(pg[0], pg[1], pg[2], pg[3]);
+            s_g4[b][tid] = gv;
+            db2v.x += gv.x; db2v.y += gv.y; db2v.z += gv.z; db2v.w += gv.w;
+        }
+    };
+    auto z1 = [&](int b, df32x16 (&z)[2]) __attribute__((always_inline)) {
+        z[0] = df32x16{}; z[1] = df32x16{};
+#pragma unroll
+        for (int ks = 0; ks < DWID / 16; ++ks) {
+            const int k0 = 16 * ks + 8 * hh;
+            const dbf16x8 wl = *reinterpret_cast<const dbf16x8*>(&s_w1l[col * DAP + k0]);
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                const dbf16x8 ah = *reinterpret_cast<const dbf16x8*>(&s_ah[b][(32 * mt + r) * DAP + k0]);
+                const dbf16x8 al = *reinterpret_cast<const dbf16x8*>(&s_al[b][(32 * mt + r) * DAP + k0]);
+                z[mt] = DMFMA(ah, w1h[ks], z[mt]);
+                z[mt] = DMFMA(ah, wl, z[mt]);
+                z[mt] = DMFMA(al, w1h[ks], z[mt]);
+            }
+        }
+    };
+    // relu(Z1 + b1), dW2 += G^T relu(Z1), dZ1 = (G W2) [Z1 > 0], db1, all per lane (tile in buffer b)
+    auto dz1 = [&](int b, const df32x16 (&z)[2], df32x16 (&d)[2]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const float zz = z[mt][q] + b1c;
+                const float zr = fmaxf(zz, 0.0f);
+                const float4 gv = s_g4[b][row_of(mt, q, hh)];
+                w2s[0] = __builtin_fmaf(gv.x, zr, w2s[0]); w2s[1] = __builtin_fmaf(gv.y, zr, w2s[1]);
+                w2s[2] = __builtin_fmaf(gv.z, zr, w2s[2]); w2s[3] = __builtin_fmaf(gv.w, zr, w2s[3]);
+                float dv = gv.x * w2c[0];
+                dv = __builtin_fmaf(gv.y, w2c[1], dv);
+                dv = __builtin_fmaf(gv.z, w2c[2], dv);
+                dv = __builtin_fmaf(gv.w, w2c[3], dv);
+                dv = zz > 0.0f ? dv : 0.0f;
+                db1 += dv;
+                d[mt][q] = dv;
+            }
+    };
+    // one element of dz1 (e = 16 mt + q)
+    auto dz1_elem = [&](int b, const df32x16 (&z)[2], df32x16 (&d)[2], int mt, int q) __attribute__((always_inline)) {
+        const float zz = z[mt][q] + b1c;
+        const float zr = fmaxf(zz, 0.0f);
+        const float4 gv = s_g4[b][row_of(mt, q, hh)];
+        w2s[0] = __builtin_fmaf(gv.x, zr, w2s[0]); w2s[1] = __builtin_fmaf(gv.y, zr, w2s[1]);
+        w2s[2] = __builtin_fmaf(gv.z, zr, w2s[2]); w2s[3] = __builtin_fmaf(gv.w, zr, w2s[3]);
+        float dv = gv.x * w2c[0];
+        dv = __builtin_fmaf(gv.y, w2c[1], dv);
+        dv = __builtin_fmaf(gv.z, w2c[2], dv);
+        dv = __builtin_fmaf(gv.w, w2c[3], dv);
+        dv = zz > 0.0f ? dv : 0.0f;
+        db1 += dv;
+        d[mt][q] = dv;
+    };
+    // row chunk i (of 8) of store_tile's A rows, and the G row with chunk 0
+    auto store_part = [&](int b, int i) __attribute__((always_inline)) {
+        const int e = tid + 256 * i, rr = e >> 5, c4 = (e & 31) * 4;
+        const float f[4] = {pa[i].x, pa[i].y, pa[i].z, pa[i].w};
+        bf4 h4, l4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            __bf16 hi, lo;
+            dsplit(f[q], hi, lo);
+            h4[q] = hi; l4[q] = lo;
+        }
+        *reinterpret_cast<bf4*>(&s_ah[b][rr * DAP + c4]) = h4;
+        *reinterpret_cast<bf4*>(&s_al[b][rr * DAP + c4]) = l4;
+        if (i == 0 && tid < DN) {
+            const float4 gv = make_float4(pg[0], pg[1], pg[2], pg[3]);
+            s_g4[b][tid] = gv;
+            db2v.x += gv.x; db2v.y += gv.y; db2v.z += gv.z; db2v.w += gv.w;
+        }
+    };
+    auto dw1 = [&](int b, const df32x16 (&d)[2]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int ks = 0; ks < DN / 16; ++ks) {
+            dbf16x8 dh, dl;
+            wg_regs_to_op(d[ks >> 1], ks & 1, dh, dl);
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) {
+                const dbf16x8 bh = wg_lds_op(s_ah[b], DAP, ks, 32 * nt), bl = wg_lds_op(s_al[b], DAP, ks, 32 * nt);
+                w1acc[nt] = DMFMA(dh, bh, w1acc[nt]);
+                w1acc[nt] = DMFMA(dh, bl, w1acc[nt]);
+                w1acc[nt] = DMFMA(dl, bh, w1acc[nt]);
+            }
+        }
+    };
+    // ---- prologue: tiles 0 and 1 in LDS, tile 2's rows in registers, Z1 of tile 0 --------------------------
+    load_tile(0);
+    store_tile(0);
+    load_tile(1);
+    store_tile(1);
+    load_tile(2);
+    __syncthreads();
+    df32x16 zc[2];
+    z1(0, zc);
+    for (int t = 0; t < T; ++t) {
+        // one scheduling region per iteration: past the block's last tiles, Z1 runs on a buffer whose
+        // result is dropped and stage B stores zero rows (load_tile's selects), so nothing branches
+        const int b0 = t % NB, b1 = (t + 1) % NB, b2 = (t + 2) % NB;
+        df32x16 d[2];
+        df32x16 zn[2];
+        // stage A: Z1(t + 1) on the matrix core, tile t's relu / dZ1 / dW2 on the VALU, interleaved by
+        // hand (4 of the 32 per-lane elements after each K step's 6 MFMAs; sched_barrier keeps the chunks)
+        zn[0] = df32x16{}; zn[1] = df32x16{};
+#pragma unroll
+        for (int ks = 0; ks < DWID / 16; ++ks) {
+            const int k0 = 16 * ks + 8 * hh;
+            const dbf16x8 wl = *reinterpret_cast<const dbf16x8*>(&s_w1l[col * DAP + k0]);
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                const dbf16x8 ah = *reinterpret_cast<const dbf16x8*>(&s_ah[b1][(32 * mt + r) * DAP + k0]);
+                const dbf16x8 al = *reinterpret_cast<const dbf16x8*>(&s_al[b1][(32 * mt + r) * DAP + k0]);
+                zn[mt] = DMFMA(ah, w1h[ks], zn[mt]);
+                zn[mt] = DMFMA(ah, wl, zn[mt]);
+                zn[mt] = DMFMA(al, w1h[ks], zn[mt]);
+            }
+#pragma unroll
+            for (int e = 4 * ks; e < 4 * ks + 4; ++e) dz1_elem(b0, zc, d, e >> 4, e & 15);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // stage B: dW1(t) on the matrix core, tile t + 2's rows into LDS on the VALU (2 row chunks per K step)
+#pragma unroll
+        for (int ks = 0; ks < DN / 16; ++ks) {
+            dbf16x8 dh, dl;
+            wg_regs_to_op(d[ks >> 1], ks & 1, dh, dl);
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) {
+                const dbf16x8 bh = wg_lds_op(s_ah[b0], DAP, ks, 32 * nt), bl = wg_lds_op(s_al[b0], DAP, ks, 32 * nt);
+                w1acc[nt] = DMFMA(dh, bh, w1acc[nt]);
+                w1acc[nt] = DMFMA(dh, bl, w1acc[nt]);
+                w1acc[nt] = DMFMA(dl, bh, w1acc[nt]);
+            }
+            store_part(b2, 2 * ks);
+            store_part(b2, 2 * ks + 1);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        load_tile(t + 3);
+        __syncthreads();
+        zc[0] = zn[0]; zc[1] = zn[1];
+    }
+    // ---- the block's partial products: one atomic per element (as version 1) ---------------------------
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int m = 32 * wave + (q & 3) + 8 * (q >> 2) + 4 * hh;
+            atomicAdd(j.dW1 + (size_t)m * DWID + 32 * nt + r, w1acc[nt][q]);
+        }
+    db1 += __shfl_xor(db1, 32);
+    if (hh == 0) atomicAdd(j.db1 + col, db1);
+#pragma unroll
+    for (int k = 0; k < DEF_SMALL_OUT; ++k) {
+        const float v = w2s[k] + __shfl_xor(w2s[k], 32);
+        if (hh == 0 && k < nout) atomicAdd(j.dW2 + (size_t)k * DWID + col, v);
+    }
+    if (wave == 0) {
+        float v[DEF_SMALL_OUT] = {db2v.x, db2v.y, db2v.z, db2v.w};
+#pragma unroll
+        for (int k = 0; k < DEF_SMALL_OUT; ++k) {
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) v[k] += __shfl_xor(v[k], off);
+            if (lane == 0 && k < nout) atomicAdd(j.db2 + k, v[k]);
+        }
+    }
+}
+
 // Rows per block of a launch, for about `blocks` blocks per head: 128 for the small-output heads
 // (their per-block flush of dW1 / dW2 partials is most of their atomics), 400 for the SH head.
 // Measured against the split-K default of 256 blocks per head: deformation backward 11.96-11.99
@@ -1735,14 +1985,16 @@ void launch_head_wgrad(const HeadWgradArgs& a, int njobs, hipStream_t st) {
         if (a.job[i].nout <= DEF_SMALL_OUT) s.job[ns++] = a.job[i];
     for (int i = 0; i < njobs; ++i)
         if (a.job[i].nout > DEF_SMALL_OUT) { s.job[ns + nbig] = a.job[i]; ++nbig; }
-    // version 2 by default (2M backward 10.10 -> 9.34 ms); LSR_WGRAD_V=1: version 1 (diagnostic A/B)
-    static const int ver = [] { const char* e = std::getenv("LSR_WGRAD_V"); return e ? std::atoi(e) : 2; }();
-    if (ver == 2) {   // one round of 256 CUs per launch: 64 blocks per small head, 256 for a wide head
+    // version 3 for the small heads, 2 for the wide by default (2M backward 10.10 -> 9.34 (v2) -> 9.13-9.15 ms);
+    // LSR_WGRAD_V=1 / 2: the earlier versions (diagnostic A/B)
+    static const int ver = [] { const char* e = std::getenv("LSR_WGRAD_V"); return e ? std::atoi(e) : 3; }();
+    if (ver >= 2) {   // one round of 256 CUs per launch: 64 blocks per small head, 256 for a wide head
         if (ns) {
             const int nb = ns <= 4 ? 256 / ns / 8 * 8 : 32;
             s.rows_per_block = std::max(64, ((a.P + nb - 1) / nb + 63) / 64 * 64);
-            hipLaunchKernelGGL(k_head_wgrad2<true>, dim3((a.P + s.rows_per_block - 1) / s.rows_per_block, ns), dim3(256),
-                               0, st, s, 0);
+            const dim3 grid((a.P + s.rows_per_block - 1) / s.rows_per_block, ns);
+            if (ver == 3) hipLaunchKernelGGL(k_head_wgrad3<true>, grid, dim3(256), 0, st, s, 0);
+            else hipLaunchKernelGGL(k_head_wgrad2<true>, grid, dim3(256), 0, st, s, 0);
         }
         if (nbig) {
             const int nb = std::max(8, 256 / nbig / 8 * 8);
