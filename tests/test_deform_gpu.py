@@ -99,8 +99,19 @@ def test_backward_matches_reference_golden():
         assert _rel(g.cpu().numpy().reshape(ref.shape), ref) < 1e-4, name
 
 
+def _morton(pts):
+    """Order of the points along a 30-bit Morton curve of their bounding box."""
+    q = ((pts - pts.min(0)) / np.maximum(np.ptp(pts, 0), 1e-12) * 1023).astype(np.int64)
+    code = np.zeros(len(pts), np.int64)
+    for bit in range(10):
+        for c in range(3):
+            code |= ((q[:, c] >> bit) & 1) << (3 * bit + c)
+    return np.argsort(code, kind="stable")
+
+
 @pytest.mark.parametrize("P,time", [(20000, 0.37), (777, -0.8), (3000, 1.0), (3000, -1.0), (20000, "mixed"),
-                                    (20000, "views3"), (20000, "views10")])
+                                    (20000, "views3"), (20000, "views10"), (20000, "morton"),
+                                    (20000, "morton_dense"), (20000, "morton_views3")])
 def test_backward_matches_oracle_at_neu3d_resolution(P, time):
     """Neu3D resolution (64^3 x 150, multires [1, 2]); gradients accumulate over two calls.  One time
     for all Gaussians (the render path: the time planes go through per-plane x-rows folded into the
@@ -108,8 +119,17 @@ def test_backward_matches_oracle_at_neu3d_resolution(P, time):
     on the second row at -1); "mixed": time 0.37 but every 97th Gaussian at -0.55, so that most waves
     take the x-rows and the rest the four-tap scatter; "views3" / "views10": consecutive runs of
     Gaussians at 3 / 10 times (a batched call of several views: the first view's waves take the
-    x-rows, the others the four-tap scatter)."""
+    x-rows, the others the four-tap scatter).  "morton*": the Gaussians stored along a Morton curve,
+    so that waves share taps and sum them in their LDS windows first (deform.hip b.window): at time
+    0.37 over the whole box, squeezed into a box of 1/6 the extent (nearly every wave inside its
+    windows), and at 3 times (the time planes through the general windows)."""
     params, res, multires, inp = _neu3d_case(P, seed=3)
+    morton = isinstance(time, str) and time.startswith("morton")
+    if morton:
+        if time == "morton_dense":
+            c = inp["means3D"].mean(0)
+            inp["means3D"] = c + (inp["means3D"] - c) / 6.0
+        time = "views3" if time == "morton_views3" else 0.37
     # the bilinear slope jumps at grid lines: keep the points 1e-3 cells away from every line (and
     # from the clamped borders), where float32 and float64 coordinates could pick different cells
     a0, a1 = params["grid.aabb"][0], params["grid.aabb"][1]
@@ -121,6 +141,9 @@ def test_backward_matches_oracle_at_neu3d_resolution(P, time):
             keep &= np.abs(u - np.round(u)) > 1e-3
     inp = {k: v[keep] for k, v in inp.items()}
     P = int(keep.sum())
+    if morton:
+        order = _morton(inp["means3D"])
+        inp = {k: v[order] for k, v in inp.items()}
     scalar = not isinstance(time, str)
     times = np.full((P, 1), time if scalar else 0.37)
     if time == "mixed":

@@ -14,7 +14,7 @@
 #   ab         same-box A/B: REPS rounds alternating CONFIGS ('|'-separated "<variant> <bench flags...>";
 #              variant cur = build/liblsr.so, else build/variants/liblsr_<variant>.so)
 #   deform     tools/bench_deform.py at 2M (forward / backward per kernel)
-#   deform_ab  deformation bench + a short configs[4] loop per VARIANTS ("cur name ..." library variants,
+#   deform_ab  deformation bench (DEFORM_ARGS) + a short configs[4] loop per VARIANTS ("cur name ..." library variants,
 #              or "name:VAR=val[,VAR2=val2]" environment variants), REPS rounds
 #   race       tools/deform_race.py (deformation backward repeatability) per library VARIANTS
 #   side       the side benches: configs[1] stand-in (bench_render), configs[4] loop (bench_train_loop)
@@ -106,7 +106,7 @@ for task in "$@"; do
         for spec in ${VARIANTS:-cur}; do
           name=${spec%%:*}; envs=""; lib=$(lib_of cur)
           if [[ $spec == *:* ]]; then envs=${spec#*:}; envs=${envs//,/ }; else lib=$(lib_of "$name"); fi
-          env $envs LSR_LIBRARY=$lib timeout -k 10 200 python tools/bench_deform.py --no-torch --iters 10 \
+          env $envs LSR_LIBRARY=$lib timeout -k 10 200 python tools/bench_deform.py --no-torch --iters 10 ${DEFORM_ARGS:-} \
               > "$O/d_$name.log" 2>&1 || { tail -5 "$O/d_$name.log"; fail "deform $name"; }
           if [ "${NO_LOOP:-0}" != 1 ]; then
             env $envs LSR_LIBRARY=$lib timeout -k 10 300 python tools/bench_train_loop.py ${LOOP_ARGS:-} \
