@@ -153,10 +153,6 @@ __device__ __forceinline__ void coords(const DeformArgs& a, int g, float (&crd)[
 __device__ constexpr int kC0(int ci) { return ci < 3 ? 0 : (ci < 5 ? 1 : 2); }
 __device__ constexpr int kC1(int ci) { return ci == 0 ? 1 : (ci == 1 || ci == 3) ? 2 : 3; }
 
-// float add into LDS (ds_add_f32; the generic pointer would make it a flat atomic)
-__device__ __forceinline__ void lds_add(float* p, float v) {
-    __hip_atomic_fetch_add((__attribute__((address_space(3))) float*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 struct Tap {
     int x0, x1, y0, y1;
     float fx, fy;
@@ -839,14 +835,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
     float* const s_sdv = reinterpret_cast<float*>(s_hl[cur ^ 1]);
     int* const s_soff = reinterpret_cast<int*>(s_sdv + 4 * 16 * 17);
     float* const s_sw = reinterpret_cast<float*>(s_soff + 4 * 16 * 4);
-    int* const s_swo = reinterpret_cast<int*>(s_sw + 4 * 16 * 4);   // taps' window cells (-1: outside)
-    // per-wave gradient windows (b.window): 64 cells x 16 channels in the buffer the chain's last
-    // product read (dead since the barrier above); zero, and every flush leaves them zero
-    float* const s_win = reinterpret_cast<float*>(s_hh[cur]);
-    if (b.window) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) s_win[wave * 1024 + 64 * i + lane] = 0.0f;
-    }
 
     // ---- HexPlane backward: 4 threads per Gaussian, 4 channels each ----------------------------------
 #ifdef LSR_DEFORM_ABL_NOHEX   // timing ablation only (wrong gradients): the HexPlane backward's share
@@ -924,75 +912,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ?
                 const Tap t = tap_of(a, pi, ci, crd);
                 const float dv[4] = {dvo[ci].x, dvo[ci].y, dvo[ci].z, dvo[ci].w};
                 const int wl = gl & 15;
-                if (b.window) {   // block-uniform
-                    // Spatially coherent waves (Gaussians stored in Morton order) share most of their
-                    // taps: sum them in a per-wave LDS window first (LDS float adds), then one memory
-                    // atomic per touched cell and channel.  The window: 8 x 8 cells from the wave's
-                    // smallest taps (a time row: 64 cells); a wave with fewer than 12 of its 16
-                    // Gaussians inside takes the direct paths below, Gaussians outside add directly.
-                    const bool trw = (ci == 2 || ci >= 4) && t_row;   // wave-uniform
-                    int mx = ok ? t.x0 : 0x7fffffff, my = (ok && !trw) ? t.y0 : 0x7fffffff;
-#pragma unroll
-                    for (int off = 32; off >= 4; off >>= 1) {   // the 4 lanes of a Gaussian agree
-                        mx = min(mx, __shfl_xor(mx, off));
-                        my = min(my, __shfl_xor(my, off));
-                    }
-                    mx = mx == 0x7fffffff ? 0 : mx;
-                    my = my == 0x7fffffff ? 0 : my;
-                    const bool inwin = !ok || (t.x1 - mx < (trw ? 64 : 8) && (trw || t.y1 - my < 8));
-                    if (__popcll(__ballot(inwin)) >= 48) {
-                        float* const win = s_win + wave * 1024;
-                        const int e4 = (wave * 16 + wl) * 4;
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) s_sdv[(wave * 16 + wl) * 17 + 4 * q + i] = ok ? dv[i] : 0.0f;
-                        if (q == 0) {
-                            if (trw) {
-                                s_soff[e4 + 0] = t.x0 * 16; s_soff[e4 + 1] = t.x1 * 16;
-                                s_sw[e4 + 0] = 1.0f - t.fx; s_sw[e4 + 1] = t.fx;
-                                s_swo[e4 + 0] = inwin ? t.x0 - mx : -1;
-                                s_swo[e4 + 1] = inwin ? t.x1 - mx : -1;
-                            } else {
-                                s_soff[e4 + 0] = (t.y0 * W + t.x0) * 16; s_soff[e4 + 1] = (t.y0 * W + t.x1) * 16;
-                                s_soff[e4 + 2] = (t.y1 * W + t.x0) * 16; s_soff[e4 + 3] = (t.y1 * W + t.x1) * 16;
-                                s_sw[e4 + 0] = (1.0f - t.fx) * (1.0f - t.fy); s_sw[e4 + 1] = t.fx * (1.0f - t.fy);
-                                s_sw[e4 + 2] = (1.0f - t.fx) * t.fy; s_sw[e4 + 3] = t.fx * t.fy;
-                                const int c0 = (t.y0 - my) * 8 + t.x0 - mx, dx = t.x1 - t.x0, dy = (t.y1 - t.y0) * 8;
-                                s_swo[e4 + 0] = inwin ? c0 : -1;
-                                s_swo[e4 + 1] = inwin ? c0 + dx : -1;
-                                s_swo[e4 + 2] = inwin ? c0 + dy : -1;
-                                s_swo[e4 + 3] = inwin ? c0 + dy + dx : -1;
-                            }
-                        }
-                        wave_lds_sync();
-                        float* const gb = trw ? b.trow + (size_t)(blockIdx.x % b.trow_reps) * b.trow_stride + b.toff[pi]
-                                              : b.dplanes + (size_t)(blockIdx.x % b.replicas) * b.plane_stride + a.poff[pi];
-                        const int ch = lane & 15;
-                        // taps into the window: a time row 2 Gaussians x 2 taps per step, else 1 x 4
-#pragma unroll 4
-                        for (int j = 0; j < (trw ? 8 : 16); ++j) {
-                            const int e = wave * 16 + (trw ? 2 * j + (lane >> 5) : j);
-                            const int tap = trw ? (lane >> 4) & 1 : lane >> 4;
-                            const float val = s_sdv[e * 17 + ch] * s_sw[e * 4 + tap];
-                            const int wo = s_swo[e * 4 + tap];
-                            if (wo >= 0) lds_add(win + wo * 16 + ch, val);
-                            else if (val != 0.0f) atomicAdd(gb + s_soff[e * 4 + tap] + ch, val);
-                        }
-                        wave_lds_sync();
-                        // flush: 4 cells x 16 channels per step, the touched ones only
-#pragma unroll 4
-                        for (int k = 0; k < 16; ++k) {
-                            const int c = 4 * k + (lane >> 4);
-                            const float v = win[c * 16 + ch];
-                            if (v != 0.0f) {
-                                win[c * 16 + ch] = 0.0f;
-                                const int cell = trw ? mx + c : (my + (c >> 3)) * W + mx + (c & 7);
-                                atomicAdd(gb + cell * 16 + ch, v);
-                            }
-                        }
-                        wave_lds_sync();   // staging and window read before the next plane
-                        continue;
-                    }
-                }
                 if ((ci == 2 || ci >= 4) && t_row) {   // wave-uniform
                     // a time plane of a wave at time[0]: its x-row (b.trow), 2 taps x 16 channels per
                     // Gaussian, two Gaussians per atomic instruction (half the time planes' requests)

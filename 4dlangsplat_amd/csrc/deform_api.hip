@@ -297,15 +297,6 @@ int time_row_reps() {   // LSR_DEFORM_TIME_ROWS=n (A/B): n copies, 0 = off
     }();
     return reps;
 }
-// the backward's per-wave LDS windows over the plane taps (DeformBwdArgs.window); LSR_DEFORM_WINDOW=0
-// turns them off (A/B)
-int plane_windows() {
-    static const int on = [] {
-        const char* e = std::getenv("LSR_DEFORM_WINDOW");
-        return e ? (std::atoi(e) != 0) : 1;
-    }();
-    return on;
-}
 size_t time_row_floats(const lsr_deform_net* net, int64_t* toff) {
     size_t o = 0;
     for (int s = 0; s < net->n_scales; ++s)
@@ -476,7 +467,6 @@ extern "C" int lsr_deform_backward(const lsr_deform_net* net, const void* worksp
     b.trow_reps = time_row_reps();
     b.trow = b.trow_reps ? fp(S.trow) : nullptr;
     b.trow_stride = (int64_t)time_row_floats(net, b.toff);
-    b.window = plane_windows();
     if (hipMemsetAsync(sc + S.daabb, 0, S.total - S.daabb, st) != hipSuccess)
         return lsr::fail(LSR_EHIP, "memset");
     lsr::launch_deform_bwd_a(b, st);

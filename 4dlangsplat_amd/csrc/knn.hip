@@ -235,24 +235,4 @@ int lsr_knn_mean_dist(int32_t P, const float* points, float* mean_dist, void* wo
     return LSR_OK;
 }
 
-// Morton order of the points (the first steps above): order[k] = index of the k-th point along the
-// 30-bit curve of their bounding box, ties in index order (the radix sort is stable)
-int lsr_morton_order(int32_t P, const float* points, int32_t* order, void* workspace, void* stream) {
-    if (P < 0) return lsr::fail(LSR_EINVAL, "P must be >= 0");
-    if (P == 0) return LSR_OK;
-    if (!points || !order || !workspace) return lsr::fail(LSR_EINVAL, "points, order and workspace are required");
-    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    KnnWs w = carve(workspace, (size_t)P);
-    const int nblk = (P + 255) / 256, nred = std::min(KNN_RED_BLOCKS, nblk);
-    hipLaunchKernelGGL(k_bbox_partial, dim3(nred), dim3(256), 0, st, P, points, w.partial);
-    hipLaunchKernelGGL(k_bbox_final, dim3(1), dim3(256), 0, st, nred, (const Bounds*)w.partial, w.bbox);
-    hipLaunchKernelGGL(k_morton, dim3(nblk), dim3(256), 0, st, P, points, (const Bounds*)w.bbox, w.code_a, w.idx_a);
-    const bool in_b = lsr::radix_sort_pairs(w.code_a, w.idx_a, w.code_b, w.idx_b, (size_t)P, 0, 30, w.sort_tmp, st);
-    if (hipMemcpyAsync(order, in_b ? w.idx_b : w.idx_a, 4 * (size_t)P, hipMemcpyDeviceToDevice, st) != hipSuccess)
-        return lsr::fail(LSR_EHIP, "morton order: copy");
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return lsr::fail(LSR_EHIP, std::string("morton order: ") + hipGetErrorString(e));
-    return LSR_OK;
-}
-
 }  // extern "C"

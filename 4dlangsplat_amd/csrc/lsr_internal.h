@@ -307,8 +307,7 @@ struct DeformBwdArgs {
     int64_t toff[24];
     int64_t trow_stride;
     int trow_reps;
-    int window;                       // plane taps summed in per-wave LDS windows first (deform.hip)
-    float* sX;                       // saved [P, 16 n_scales] features
+    float* sX;                        // saved [P, 16 n_scales] features
     float* sA[DEF_MAX_LAYERS];        // saved [P,128] relu(H_k)
     float* sdH[DEF_MAX_LAYERS];       // saved [P,128] gradients of H_k
     float* sG_rot;                    // apply_rotation: [P,4] gradient of the rotation head's output

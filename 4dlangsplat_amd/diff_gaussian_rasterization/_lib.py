@@ -201,8 +201,6 @@ SIGNATURES = {
     "lsr_knn_workspace_bytes": (ctypes.c_int64, [ctypes.c_int32]),
     "lsr_knn_mean_dist": (ctypes.c_int, [ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p]),
-    "lsr_morton_order": (ctypes.c_int, [ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                        ctypes.c_void_p]),
     "lsr_deform_workspace_bytes": (ctypes.c_int64, [ctypes.POINTER(DeformNet)]),
     "lsr_deform_prepare": (ctypes.c_int, [ctypes.POINTER(DeformNet), ctypes.c_void_p, ctypes.c_void_p]),
     "lsr_deform_forward": (ctypes.c_int, [ctypes.POINTER(DeformNet), ctypes.c_void_p, ctypes.c_int32]

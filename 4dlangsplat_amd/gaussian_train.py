@@ -261,24 +261,6 @@ class GaussianTrainer:
         return P - kept
 
     @torch.no_grad()
-    def reorder_spatial(self) -> torch.Tensor:
-        """Store every row tensor along a Morton curve of xyz (lsr_morton_order, then the row gather
-        of densify / prune): the same model, rows in another order.  No reference counterpart (its
-        rows stay in creation order); the deformation backward's per-wave LDS windows sum the plane
-        taps of spatially coherent waves before the atomics.  Gradients of the old
-        order are dropped, as after densify.  Returns the order (new row k = old row order[k])."""
-        P = self.P
-        order = torch.empty(max(P, 1), dtype=torch.int32, device=self.device)
-        if P == 0:
-            return order[:0]
-        xyz = self.params["xyz"].detach().contiguous()
-        ws = torch.empty(int(self._L.lsr_knn_workspace_bytes(P)), dtype=torch.uint8, device=self.device)
-        _lib.check(self._L.lsr_morton_order(P, _ptr(xyz), _ptr(order), _ptr(ws), _stream(self.device)),
-                   "lsr_morton_order")
-        self._install(self._gather(order, P, zero_from=P, stats_keep=True))
-        return order
-
-    @torch.no_grad()
     def reset_opacity(self):
         """gaussian_model.py:391-394: opacity <- inverse_sigmoid(min(sigmoid(opacity), 0.01)), its
         Adam moments zeroed (replace_tensor_to_optimizer, :446-459).  Like the fresh nn.Parameter

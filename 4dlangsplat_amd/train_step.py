@@ -100,8 +100,7 @@ class TrainStep:
     def __init__(self, trainer: GaussianTrainer, field=None, deform_lr: float = 1.6e-4, grid_lr: float = 1.6e-3,
                  bg: Optional[torch.Tensor] = None, stage: str = "fine-base", sh_degree: int = 3,
                  densify: Optional[Callable[[GaussianTrainer, int], None]] = None, batch_views: bool = True,
-                 joint_train: bool = False, lam: float = 0.2, beta: float = 0.01, addcosloss: bool = False,
-                 spatial_order: bool = False):
+                 joint_train: bool = False, lam: float = 0.2, beta: float = 0.01, addcosloss: bool = False):
         """densify(trainer, iteration): optional densify / prune / reset_opacity schedule, run
         between the densification statistics and the optimizer step (train.py:388-421).
         batch_views: the batch's views share one deformation-field launch (render_views)
@@ -111,11 +110,7 @@ class TrainStep:
         backward 1.45 vs 1.74 ms per iteration); round 3 had measured the opposite
         (127.8 vs 140.5) while those atomics serialised.
         joint_train, lam, beta, addcosloss: the 'lang' stages' switches (train.py --joint_coarse /
-        --joint_fine, --lam 0.2, --beta 0.01, env addcosloss).
-        spatial_order: keep the Gaussians' rows in Morton order of xyz (GaussianTrainer.reorder_spatial
-        at construction and whenever densify / prune replaced the rows, whose gradients are dropped
-        then anyway): the same model in another row order, under which the deformation backward sums
-        most plane taps in LDS before its atomics.  Off: the reference's row order."""
+        --joint_fine, --lam 0.2, --beta 0.01, env addcosloss)."""
         if joint_train and "lang" not in stage:
             raise ValueError("joint_train needs a 'lang' stage (train.py:103-104)")
         if "lang" in stage and "language_feature" not in trainer.params:
@@ -125,9 +120,6 @@ class TrainStep:
         self.coff = []              # the last iteration's renders' coff (train.py:240-247)
         self.batch_views = batch_views
         self.densify = densify
-        self.spatial_order = spatial_order
-        if spatial_order:
-            trainer.reorder_spatial()
         self.iteration = 0
         self.sh_degree = sh_degree
         self.bg = bg if bg is not None else torch.ones(3, device=trainer.device)
@@ -247,10 +239,7 @@ class TrainStep:
                 vgrad = vgrad + o["viewspace_points"].grad
             tr.add_densification_stats(vgrad, radii)
         if self.densify is not None:
-            rows = tr.params["xyz"]
             self.densify(tr, self.iteration)
-            if self.spatial_order and tr.params["xyz"] is not rows:   # densify / prune installed new rows
-                tr.reorder_spatial()
         tr.step()
         tr.zero_grad(set_to_none=True)
         if self.field is not None:

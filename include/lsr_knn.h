@@ -24,11 +24,6 @@ extern "C" {
 
 int64_t lsr_knn_workspace_bytes(int32_t P);
 int lsr_knn_mean_dist(int32_t P, const float *points, float *mean_dist, void *workspace, void *stream);
-/* order [P] int32: the points' indices along the same 30-bit Morton curve of their bounding box
- * (ties in index order).  No reference counterpart: the spatial storage order of the Gaussians
- * (GaussianTrainer.reorder_spatial) under which the deformation backward's per-wave LDS windows
- * sum most plane taps before the atomics.  Same workspace size. */
-int lsr_morton_order(int32_t P, const float *points, int32_t *order, void *workspace, void *stream);
 
 #ifdef __cplusplus
 }

@@ -120,9 +120,9 @@ def test_backward_matches_oracle_at_neu3d_resolution(P, time):
     take the x-rows and the rest the four-tap scatter; "views3" / "views10": consecutive runs of
     Gaussians at 3 / 10 times (a batched call of several views: the first view's waves take the
     x-rows, the others the four-tap scatter).  "morton*": the Gaussians stored along a Morton curve,
-    so that waves share taps and sum them in their LDS windows first (deform.hip b.window): at time
-    0.37 over the whole box, squeezed into a box of 1/6 the extent (nearly every wave inside its
-    windows), and at 3 times (the time planes through the general windows)."""
+    so that a wave's Gaussians share most of their cells and its atomics add into the same words
+    back to back: at time 0.37 over the whole box, squeezed into a box of 1/6 the extent, and at 3
+    times (the time planes through the four-tap scatter)."""
     params, res, multires, inp = _neu3d_case(P, seed=3)
     morton = isinstance(time, str) and time.startswith("morton")
     if morton:

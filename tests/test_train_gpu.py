@@ -188,44 +188,3 @@ def test_gather_rows_bit_exact(dtype, cols, offset):
     ref = src.cpu().numpy()[idx]
     ref[zf:] = 0
     np.testing.assert_array_equal(dst.cpu().numpy(), ref)
-
-
-def _morton_codes(xyz):
-    """knn.hip k_morton in numpy: 10-bit quantisation over the bounding box, bits interleaved x, y, z."""
-    x = xyz.astype(np.float32)
-    mn, mx = x.min(0), x.max(0)
-    t = (x - mn) / (mx - mn) * np.float32(1023.0)
-    q = np.where(t >= 0, np.minimum(t, 1023.0), 0).astype(np.int64)
-    code = np.zeros(len(x), np.int64)
-    for bit in range(10):
-        for c in range(3):
-            code |= ((q[:, c] >> bit) & 1) << (3 * bit + c)
-    return code
-
-
-def test_reorder_spatial_permutes_every_row_tensor(gold):
-    """reorder_spatial: the rows of every parameter, Adam moment, statistic and the deformation table
-    follow one permutation (bit-exact), which sorts the Morton codes of xyz stably (ties in row order);
-    step counts are kept and gradients of the old order dropped."""
-    tr = _trainer(gold, "adam_", moments="adam")
-    rng = np.random.default_rng(4)
-    P = tr.P
-    tr.xyz_gradient_accum.copy_(_cuda(rng.random((P, 1), dtype=np.float32)))
-    tr.denom.copy_(_cuda(rng.integers(0, 9, size=(P, 1)).astype(np.float32)))
-    tr.max_radii2D.copy_(_cuda(rng.random(P, dtype=np.float32)))
-    tr["xyz"].grad = torch.ones_like(tr["xyz"])
-    before = {("p", n): tr[n].detach().cpu().numpy() for n in NAMES}
-    before.update({("m", n): tr.exp_avg[n].cpu().numpy() for n in NAMES})
-    before.update({("v", n): tr.exp_avg_sq[n].cpu().numpy() for n in NAMES})
-    for s in ("xyz_gradient_accum", "denom", "max_radii2D", "_deformation_accum", "_deformation_table"):
-        before[("s", s)] = getattr(tr, s).cpu().numpy()
-    steps = dict(tr.steps)
-    order = tr.reorder_spatial().cpu().numpy()
-    torch.cuda.synchronize()
-    code = _morton_codes(before[("p", "xyz")])
-    np.testing.assert_array_equal(order, np.argsort(code, kind="stable"))
-    for (kind, n), old in before.items():
-        got = (tr[n].detach() if kind == "p" else tr.exp_avg[n] if kind == "m" else
-               tr.exp_avg_sq[n] if kind == "v" else getattr(tr, n)).cpu().numpy()
-        np.testing.assert_array_equal(got, old[order], err_msg=f"{kind} {n}")
-    assert tr.steps == steps and tr["xyz"].grad is None and tr["xyz"].requires_grad

@@ -115,7 +115,7 @@ def build(args, dev):
     extent = cameras_extent(rig)
     tr = GaussianTrainer(s_raw, feature_lrs())
     sched = ReferenceSchedule(extent, stage="fine-base", densify_until_iter=args.densify_until_iter)
-    step = TrainStep(tr, field, densify=sched, stage="fine-base", spatial_order=args.spatial_order)
+    step = TrainStep(tr, field, densify=sched, stage="fine-base")
     step.set_reference_lr(extent)
     return step, sched, pool, gts, extent
 
@@ -177,8 +177,6 @@ def main():
     ap.add_argument("--per-view-deform", action="store_true",
                     help="one deformation launch per view (render) instead of one per iteration over all views "
                          "(render_views, TrainStep's default)")
-    ap.add_argument("--spatial-order", action="store_true",
-                    help="TrainStep(spatial_order=True): rows kept in Morton order of xyz")
     args = ap.parse_args()
     dev = torch.device("cuda")
     torch.manual_seed(0)
@@ -228,8 +226,7 @@ def main():
                 config=dict(workload="configs[4] stand-in: synthetic teacher, Neu3D field, fine-base",
                             gaussians=args.gaussians, views_per_iteration=args.views, width=args.width,
                             height=args.height, pool=len(pool), resolution=NEU3D_RES, multires=NEU3D_MULTIRES,
-                            deformation_launches="per view" if args.per_view_deform else "one per iteration",
-                            row_order="morton (spatial_order)" if args.spatial_order else "creation"),
+                            deformation_launches="per view" if args.per_view_deform else "one per iteration"),
                 data="synthetic")
     print(json.dumps(line))
 
