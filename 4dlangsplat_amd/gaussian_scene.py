@@ -293,7 +293,8 @@ def render(viewpoint_camera, pc: GaussianScene, bg_color: torch.Tensor, scaling_
     (scene/dataset_readers.py:491-516, `panoptic_camera` here), whose settings are used as they are
     (gaussian_renderer/__init__.py:46, 74-76).  Environment switches of the reference
     (nonormalized, language_feature_hiddendim) are arguments here.  _deformed: this view's
-    deformation outputs, already evaluated (render_views); the field is then not called.
+    deformation outputs, already evaluated and activated (render_views); the field is then not
+    called.
 
     One deliberate divergence: with override_color (or convert_SHs_python) the reference passes
     both shs_final and colors_precomp to the rasterizer (gaussian_renderer/__init__.py:219-228),
@@ -325,45 +326,49 @@ def render(viewpoint_camera, pc: GaussianScene, bg_color: torch.Tensor, scaling_
         # sh_degree included), and the frame time from the dict
         raster_settings = viewpoint_camera["camera"]
         cam_time = viewpoint_camera["time"]
-    # the reference builds this with torch.tensor(time).to(device).repeat (a host-to-device copy,
-    # which synchronises the stream): a fill gives the same values without the wait
-    t = torch.full((means3D.shape[0], 1), float(cam_time), device=dev)
     rasterizer = GaussianRasterizer(raster_settings=raster_settings)
     opacity = pc.opacity
-    shs = pc.get_features
-    if include_feature:
-        lang = pc.get_language_feature
-        if not nonormalized:
-            lang = lang / (lang.norm(dim=-1, keepdim=True) + 1e-9)
-    else:
-        lang = torch.zeros((pc.P, language_feature_hiddendim), dtype=opacity.dtype, device=dev)
     scales = rotations = cov3D_precomp = None
-    if compute_cov3D_python:
-        cov3D_precomp = _covariance(pc.get_scaling, scaling_modifier, pc.rotation)
-    else:
-        scales, rotations = pc.scaling, pc.rotation
     coff = None
-    if _deformed is not None:
+    activated = False
+    if _deformed is not None:   # render_views: the field's outputs for this view, activated there
         m3, s3, r3, o3, sh3, l3, coff = _deformed
-    elif "coarse" in stage:
-        m3, s3, r3, o3, sh3, l3 = means3D, scales, rotations, opacity, shs, lang
-    elif "fine" in stage:
-        if pc.deformation is None:
-            raise ValueError("a 'fine' stage needs the scene's deformation field")
-        if cov3D_precomp is not None:
-            raise ValueError("compute_cov3D_python with a deformation field is not supported")
-        # inside autograd (training) the field's backward runs (DeformationField.apply)
-        deform = pc.deformation.apply if (torch.is_grad_enabled() and hasattr(pc.deformation, "apply")) \
-            else pc.deformation
-        # 'base' stages pass the language through (the reference sets no_dlang = 1 there,
-        # gaussian_renderer/__init__.py:121-124)
-        m3, s3, r3, o3, sh3, l3, coff = deform(means3D, scales, rotations, opacity, shs, lang, t,
-                                               no_dlang=True if "base" in stage else None)
+        activated = True
     else:
-        raise NotImplementedError(stage)
-    s3 = torch.exp(s3) if s3 is not None else None
-    r3 = torch.nn.functional.normalize(r3) if r3 is not None else None
-    o3 = torch.sigmoid(o3)
+        # the reference builds this with torch.tensor(time).to(device).repeat (a host-to-device copy,
+        # which synchronises the stream): a fill gives the same values without the wait
+        t = torch.full((means3D.shape[0], 1), float(cam_time), device=dev)
+        shs = pc.get_features
+        if include_feature:
+            lang = pc.get_language_feature
+            if not nonormalized:
+                lang = lang / (lang.norm(dim=-1, keepdim=True) + 1e-9)
+        else:
+            lang = torch.zeros((pc.P, language_feature_hiddendim), dtype=opacity.dtype, device=dev)
+        if compute_cov3D_python:
+            cov3D_precomp = _covariance(pc.get_scaling, scaling_modifier, pc.rotation)
+        else:
+            scales, rotations = pc.scaling, pc.rotation
+        if "coarse" in stage:
+            m3, s3, r3, o3, sh3, l3 = means3D, scales, rotations, opacity, shs, lang
+        elif "fine" in stage:
+            if pc.deformation is None:
+                raise ValueError("a 'fine' stage needs the scene's deformation field")
+            if cov3D_precomp is not None:
+                raise ValueError("compute_cov3D_python with a deformation field is not supported")
+            # inside autograd (training) the field's backward runs (DeformationField.apply)
+            deform = pc.deformation.apply if (torch.is_grad_enabled() and hasattr(pc.deformation, "apply")) \
+                else pc.deformation
+            # 'base' stages pass the language through (the reference sets no_dlang = 1 there,
+            # gaussian_renderer/__init__.py:121-124)
+            m3, s3, r3, o3, sh3, l3, coff = deform(means3D, scales, rotations, opacity, shs, lang, t,
+                                                   no_dlang=True if "base" in stage else None)
+        else:
+            raise NotImplementedError(stage)
+    if not activated:
+        s3 = torch.exp(s3) if s3 is not None else None
+        r3 = torch.nn.functional.normalize(r3) if r3 is not None else None
+        o3 = torch.sigmoid(o3)
     colors_precomp = None
     if override_color is not None:
         colors_precomp = override_color
@@ -410,8 +415,13 @@ def render_views(cams: Sequence, pc: GaussianScene, bg_color: torch.Tensor, stag
     t = torch.cat([torch.full((P,), float(c.time), device=dev) for c in cams])
     deform = pc.deformation.apply if (torch.is_grad_enabled() and hasattr(pc.deformation, "apply")) \
         else pc.deformation
-    outs = deform(rep(pc.get_xyz), rep(pc.scaling), rep(pc.rotation), rep(pc.opacity), rep(pc.get_features),
-                  rep(lang), t, no_dlang=True if "base" in stage else None)
+    outs = list(deform(rep(pc.get_xyz), rep(pc.scaling), rep(pc.rotation), rep(pc.opacity), rep(pc.get_features),
+                       rep(lang), t, no_dlang=True if "base" in stage else None))
+    # the activations (render(), gaussian_renderer/__init__.py:131-133) once over the V * P rows: the
+    # same values row by row, a third of the launches forward and backward
+    outs[1] = torch.exp(outs[1]) if outs[1] is not None else None
+    outs[2] = torch.nn.functional.normalize(outs[2]) if outs[2] is not None else None
+    outs[3] = torch.sigmoid(outs[3])
     parts = [o.split(P) if o is not None else (None,) * V for o in outs]
     return [render(c, pc, bg_color, stage=stage, nonormalized=nonormalized,
                    language_feature_hiddendim=language_feature_hiddendim,
