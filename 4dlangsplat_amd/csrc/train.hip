@@ -229,6 +229,57 @@ __global__ void k_reset_opacity(int P, float* opacity, float* m, float* v) {
     if (v) v[i] = 0.0f;
 }
 
+// The render path's activations (gaussian_renderer/__init__.py:191-193 with gaussian_model.py:38-46:
+// torch.exp, torch.nn.functional.normalize (x / max(|x|, 1e-12)), torch.sigmoid), one thread per row
+// of all three, in PyTorch's order of operations: bit for bit its results (checked on 4M random rows:
+// its norm sums the squares pairwise, (x0^2 + x1^2) + (x2^2 + x3^2); exp and 1 / (1 + exp(-x)) as here).
+__global__ void __launch_bounds__(256) k_activate(int P, const float* __restrict__ rs, const float* __restrict__ rr,
+                                                  const float* __restrict__ ro, float* __restrict__ s,
+                                                  float* __restrict__ r, float* __restrict__ o) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= P) return;
+    if (rs) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) s[3 * i + c] = expf(rs[3 * i + c]);
+    }
+    if (rr) {
+        const float4 q = reinterpret_cast<const float4*>(rr)[i];
+        const float n = fmaxf(sqrtf((q.x * q.x + q.y * q.y) + (q.z * q.z + q.w * q.w)), 1e-12f);
+        reinterpret_cast<float4*>(r)[i] = make_float4(q.x / n, q.y / n, q.z / n, q.w / n);
+    }
+    if (ro) o[i] = 1.0f / (1.0f + expf(-ro[i]));
+}
+// Their backward (the autograd formulas of the three ops): d exp = d s, d normalize = (d - y (y . d)) / |x|
+// for |x| > 1e-12 (d / 1e-12 below, where the clamp is constant), d sigmoid = d o (1 - o).
+__global__ void __launch_bounds__(256) k_activate_bwd(int P, const float* __restrict__ s, const float* __restrict__ rr,
+                                                      const float* __restrict__ o, const float* __restrict__ ds,
+                                                      const float* __restrict__ dr, const float* __restrict__ dop,
+                                                      float* __restrict__ dsr, float* __restrict__ drr,
+                                                      float* __restrict__ dor) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= P) return;
+    if (dsr) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) dsr[3 * i + c] = ds ? ds[3 * i + c] * s[3 * i + c] : 0.0f;
+    }
+    if (drr) {
+        const float4 q = reinterpret_cast<const float4*>(rr)[i];
+        const float4 d = dr ? reinterpret_cast<const float4*>(dr)[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        const float len = sqrtf((q.x * q.x + q.y * q.y) + (q.z * q.z + q.w * q.w));
+        float4 g;
+        if (len > 1e-12f) {
+            const float4 y = make_float4(q.x / len, q.y / len, q.z / len, q.w / len);
+            const float yd = y.x * d.x + y.y * d.y + y.z * d.z + y.w * d.w;
+            g = make_float4((d.x - y.x * yd) / len, (d.y - y.y * yd) / len, (d.z - y.z * yd) / len,
+                            (d.w - y.w * yd) / len);
+        } else {
+            g = make_float4(d.x / 1e-12f, d.y / 1e-12f, d.z / 1e-12f, d.w / 1e-12f);
+        }
+        reinterpret_cast<float4*>(drr)[i] = g;
+    }
+    if (dor) dor[i] = dop ? dop[i] * o[i] * (1.0f - o[i]) : 0.0f;
+}
+
 struct TrainWs {
     uint32_t *f0, *f1, *o0, *o1, *totals;
     void* scan_tmp;
@@ -400,6 +451,34 @@ int lsr_reset_opacity(int32_t P, float* opacity, float* exp_avg, float* exp_avg_
     hipLaunchKernelGGL(k_reset_opacity, dim3((P + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), P,
                        opacity, exp_avg, exp_avg_sq);
     return launched("reset opacity");
+}
+
+int lsr_activate(int32_t P, const float* raw_scales, const float* raw_rotations, const float* raw_opacity,
+                 float* scales, float* rotations, float* opacity, void* stream) {
+    if (P < 0) return lsr::fail(LSR_EINVAL, "lsr_activate: P >= 0");
+    if ((raw_scales && !scales) || (raw_rotations && !rotations) || (raw_opacity && !opacity))
+        return lsr::fail(LSR_EINVAL, "lsr_activate: every given input needs its output");
+    if (raw_rotations && (!al16(raw_rotations) || !al16(rotations)))
+        return lsr::fail(LSR_EINVAL, "lsr_activate: rotation rows must be 16-byte aligned");
+    if (P == 0) return LSR_OK;
+    hipLaunchKernelGGL(k_activate, dim3((P + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), P,
+                       raw_scales, raw_rotations, raw_opacity, scales, rotations, opacity);
+    return launched("activate");
+}
+
+int lsr_activate_backward(int32_t P, const float* scales, const float* raw_rotations, const float* opacity,
+                          const float* d_scales, const float* d_rotations, const float* d_opacity,
+                          float* d_raw_scales, float* d_raw_rotations, float* d_raw_opacity, void* stream) {
+    if (P < 0) return lsr::fail(LSR_EINVAL, "lsr_activate_backward: P >= 0");
+    if ((d_raw_scales && !scales) || (d_raw_rotations && !raw_rotations) || (d_raw_opacity && !opacity))
+        return lsr::fail(LSR_EINVAL, "lsr_activate_backward: every requested gradient needs its forward values");
+    if (d_raw_rotations && (!al16(raw_rotations) || !al16(d_raw_rotations) || (d_rotations && !al16(d_rotations))))
+        return lsr::fail(LSR_EINVAL, "lsr_activate_backward: rotation rows must be 16-byte aligned");
+    if (P == 0) return LSR_OK;
+    hipLaunchKernelGGL(k_activate_bwd, dim3((P + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), P,
+                       scales, raw_rotations, opacity, d_scales, d_rotations, d_opacity, d_raw_scales, d_raw_rotations,
+                       d_raw_opacity);
+    return launched("activate backward");
 }
 
 }  // extern "C"

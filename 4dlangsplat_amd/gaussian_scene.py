@@ -282,6 +282,50 @@ def read_ply_vertices(path: str) -> Dict[str, np.ndarray]:
 
 
 # ---- render(): gaussian_renderer/__init__.py:19-248 -----------------------------------------------
+class _Activate(torch.autograd.Function):
+    """exp(scales), normalize(rotations), sigmoid(opacity) (gaussian_renderer/__init__.py:191-193) in one
+    launch forward and one backward (lsr_activate / lsr_activate_backward, include/lsr_train.h)
+    instead of about five PyTorch kernels forward and eight backward."""
+
+    @staticmethod
+    def forward(ctx, s_raw, r_raw, o_raw):
+        from diff_gaussian_rasterization import _lib
+        L = _lib.load()
+        s_raw, r_raw, o_raw = s_raw.contiguous(), r_raw.contiguous(), o_raw.contiguous()
+        if s_raw.dtype != torch.float32 or r_raw.shape[-1] != 4 or s_raw.shape[-1] != 3 \
+                or not (s_raw.shape[0] == r_raw.shape[0] == o_raw.shape[0]) or o_raw.numel() != o_raw.shape[0]:
+            raise ValueError("activate: float32 scales [N,3], rotations [N,4], opacity [N,1]")
+        s, r, o = torch.empty_like(s_raw), torch.empty_like(r_raw), torch.empty_like(o_raw)
+        p = lambda t: t.data_ptr()   # noqa: E731
+        st = torch.cuda.current_stream(s_raw.device).cuda_stream
+        _lib.check(L.lsr_activate(s_raw.shape[0], p(s_raw), p(r_raw), p(o_raw), p(s), p(r), p(o), st), "lsr_activate")
+        ctx.save_for_backward(s, r_raw, o)
+        return s, r, o
+
+    @staticmethod
+    def backward(ctx, ds, dr, do):
+        from diff_gaussian_rasterization import _lib
+        L = _lib.load()
+        s, r_raw, o = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        outs = [torch.empty_like(x) if need[k] else None for k, x in enumerate((s, r_raw, o))]
+        g = [None if x is None else x.contiguous() for x in (ds, dr, do)]
+        p = lambda t: None if t is None else t.data_ptr()   # noqa: E731
+        st = torch.cuda.current_stream(s.device).cuda_stream
+        _lib.check(L.lsr_activate_backward(s.shape[0], p(s), p(r_raw), p(o), p(g[0]), p(g[1]), p(g[2]),
+                                           p(outs[0]), p(outs[1]), p(outs[2]), st), "lsr_activate_backward")
+        return tuple(outs)
+
+
+def activate(scales, rotations, opacity):
+    """The render path's activations: one native launch each way on the GPU (_Activate); the PyTorch
+    ops for host tensors or a missing input."""
+    if scales is not None and rotations is not None and scales.is_cuda:
+        return _Activate.apply(scales, rotations, opacity)
+    return (torch.exp(scales) if scales is not None else None,
+            torch.nn.functional.normalize(rotations) if rotations is not None else None, torch.sigmoid(opacity))
+
+
 def render(viewpoint_camera, pc: GaussianScene, bg_color: torch.Tensor, scaling_modifier: float = 1.0,
            override_color=None, stage: str = "fine-lang", compute_cov3D_python: bool = False,
            convert_SHs_python: bool = False, debug: bool = False, nonormalized: bool = False,
@@ -366,9 +410,7 @@ def render(viewpoint_camera, pc: GaussianScene, bg_color: torch.Tensor, scaling_
         else:
             raise NotImplementedError(stage)
     if not activated:
-        s3 = torch.exp(s3) if s3 is not None else None
-        r3 = torch.nn.functional.normalize(r3) if r3 is not None else None
-        o3 = torch.sigmoid(o3)
+        s3, r3, o3 = activate(s3, r3, o3)
     colors_precomp = None
     if override_color is not None:
         colors_precomp = override_color
@@ -419,9 +461,7 @@ def render_views(cams: Sequence, pc: GaussianScene, bg_color: torch.Tensor, stag
                        rep(lang), t, no_dlang=True if "base" in stage else None))
     # the activations (render(), gaussian_renderer/__init__.py:131-133) once over the V * P rows: the
     # same values row by row, a third of the launches forward and backward
-    outs[1] = torch.exp(outs[1]) if outs[1] is not None else None
-    outs[2] = torch.nn.functional.normalize(outs[2]) if outs[2] is not None else None
-    outs[3] = torch.sigmoid(outs[3])
+    outs[1], outs[2], outs[3] = activate(outs[1], outs[2], outs[3])
     parts = [o.split(P) if o is not None else (None,) * V for o in outs]
     return [render(c, pc, bg_color, stage=stage, nonormalized=nonormalized,
                    language_feature_hiddendim=language_feature_hiddendim,

@@ -15,6 +15,8 @@
  *       -> lsr_prune_plan (+ lsr_gather_rows)
  *   - reset_opacity                                        gaussian_model.py:391-394, 446-459
  *       -> lsr_reset_opacity
+ *   - exp / normalize / sigmoid of the render path          gaussian_renderer/__init__.py:191-193
+ *       -> lsr_activate, lsr_activate_backward
  *
  * Conventions as lsr.h: device pointers, float32 unless stated, contiguous rows; the library
  * allocates nothing (plans take a workspace of lsr_train_workspace_bytes(P)); every launch on
@@ -106,6 +108,21 @@ int lsr_split_fixup(int64_t n_new, int64_t base, int32_t n_copies, const int32_t
 /* opacity = inverse_sigmoid(min(sigmoid(opacity), 0.01)); its Adam moments zeroed (exp_avg and
  * exp_avg_sq may be NULL). */
 int lsr_reset_opacity(int32_t P, float *opacity, float *exp_avg, float *exp_avg_sq, void *stream);
+
+/* The render path's activations over P rows in one launch (gaussian_renderer/__init__.py:191-193,
+ * gaussian_model.py:38-46; replaces torch.exp / torch.nn.functional.normalize / torch.sigmoid and
+ * their autograd backward there, GaussianScene.render_views):
+ *   scales = exp(raw_scales) [P,3];  rotations = raw / max(|raw|, 1e-12) [P,4];  opacity = sigmoid(raw) [P]
+ * Any raw input may be NULL (that output is skipped); rotation rows 16-byte aligned. */
+int lsr_activate(int32_t P, const float *raw_scales, const float *raw_rotations, const float *raw_opacity,
+                 float *scales, float *rotations, float *opacity, void *stream);
+/* Their backward from the forward's outputs (scales, opacity) and the raw rotations:
+ *   d_raw_scales = d_scales * scales;  d_raw_opacity = d_opacity * opacity * (1 - opacity);
+ *   d_raw_rotations = (d - y (y . d)) / |raw| with y = raw / |raw| (d / 1e-12 when |raw| <= 1e-12).
+ * A NULL upstream gradient counts as zero; a NULL output gradient is not computed. */
+int lsr_activate_backward(int32_t P, const float *scales, const float *raw_rotations, const float *opacity,
+                          const float *d_scales, const float *d_rotations, const float *d_opacity,
+                          float *d_raw_scales, float *d_raw_rotations, float *d_raw_opacity, void *stream);
 
 #ifdef __cplusplus
 }

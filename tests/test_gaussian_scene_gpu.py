@@ -187,3 +187,38 @@ def test_model_directory_records_the_language_mode(tmp_path):
     with pytest.raises(ValueError, match="no_resnet"):
         gs.load_model_dir(str(tmp_path), env={})
     assert LANG_RESIDUAL != LANG_NORESNET
+
+
+def test_native_activations_match_torch():
+    """lsr_activate / lsr_activate_backward (the render path's exp / normalize / sigmoid) against the
+    PyTorch ops and their autograd: the forward bit for bit, the gradients within float rounding;
+    including a zero quaternion (the normalize clamp) and a call where only one input needs a gradient."""
+    g = torch.Generator(device="cpu").manual_seed(3)
+    N = 100_003
+    s = (torch.randn(N, 3, generator=g) * 2).cuda()
+    r = torch.randn(N, 4, generator=g).cuda()
+    r[7] = 0.0
+    r[8] = 1e-14
+    o = (torch.randn(N, 1, generator=g) * 3).cuda()
+    ds, dr, do = (torch.randn(N, k, generator=g).cuda() for k in (3, 4, 1))
+    leaves = [t.clone().requires_grad_(True) for t in (s, r, o)]
+    got = gs._Activate.apply(*leaves)
+    torch.autograd.backward(got, (ds, dr, do))
+    refl = [t.clone().requires_grad_(True) for t in (s, r, o)]
+    ref = (torch.exp(refl[0]), torch.nn.functional.normalize(refl[1]), torch.sigmoid(refl[2]))
+    torch.autograd.backward(ref, (ds, dr, do))
+    for a, b in zip(got, ref):   # the forward in PyTorch's order of operations: bit for bit
+        assert torch.equal(a, b)
+    for a, b, name in zip(leaves, refl, ("scales", "rotations", "opacity")):
+        if name == "rotations":   # the zero rows: 1 / clamp(1e-12), huge in both; compare the rest
+            keep = torch.ones(N, dtype=torch.bool, device="cuda")
+            keep[7:9] = False
+            torch.testing.assert_close(a.grad[keep], b.grad[keep], rtol=1e-5, atol=1e-6)
+            torch.testing.assert_close(a.grad[7:9], b.grad[7:9], rtol=1e-5, atol=0.0)
+        else:
+            torch.testing.assert_close(a.grad, b.grad, rtol=1e-5, atol=1e-7)
+    # only the opacity needs a gradient: the others are not computed
+    o2 = o.clone().requires_grad_(True)
+    _, _, oo = gs._Activate.apply(s, r, o2)
+    oo.sum().backward()
+    torch.testing.assert_close(o2.grad, (torch.sigmoid(o) * (1 - torch.sigmoid(o))), rtol=1e-5, atol=1e-7)
