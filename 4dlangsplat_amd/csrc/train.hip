@@ -280,6 +280,35 @@ __global__ void __launch_bounds__(256) k_activate_bwd(int P, const float* __rest
     if (dor) dor[i] = dop ? dop[i] * o[i] * (1.0f - o[i]) : 0.0f;
 }
 
+// render_views' V views of P Gaussians (gaussian_scene.py): a tensor's rows repeated V times
+// (torch.Tensor.repeat(V, 1, ...)) and, backward, the V row blocks summed, every tensor of the call
+// in one launch (grid row = tensor); rows of whole floats, flat element index e.
+struct RowBlocksArgs {
+    const float* src[LSR_GATHER_MAX_TENSORS];
+    float* dst[LSR_GATHER_MAX_TENSORS];
+    int64_t n[LSR_GATHER_MAX_TENSORS];   // floats of one block (n_rows * row floats)
+    int nb;                              // blocks (views)
+};
+__global__ void __launch_bounds__(256) k_repeat_rows(RowBlocksArgs a) {
+    const float* __restrict__ src = a.src[blockIdx.y];
+    float* __restrict__ dst = a.dst[blockIdx.y];
+    const int64_t n = a.n[blockIdx.y];
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+        const float v = src[e];
+        for (int b = 0; b < a.nb; ++b) dst[(int64_t)b * n + e] = v;
+    }
+}
+__global__ void __launch_bounds__(256) k_sum_row_blocks(RowBlocksArgs a) {
+    const float* __restrict__ src = a.src[blockIdx.y];
+    float* __restrict__ dst = a.dst[blockIdx.y];
+    const int64_t n = a.n[blockIdx.y];
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+        float v = src[e];
+        for (int b = 1; b < a.nb; ++b) v += src[(int64_t)b * n + e];
+        dst[e] = v;
+    }
+}
+
 struct TrainWs {
     uint32_t *f0, *f1, *o0, *o1, *totals;
     void* scan_tmp;
@@ -451,6 +480,37 @@ int lsr_reset_opacity(int32_t P, float* opacity, float* exp_avg, float* exp_avg_
     hipLaunchKernelGGL(k_reset_opacity, dim3((P + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), P,
                        opacity, exp_avg, exp_avg_sq);
     return launched("reset opacity");
+}
+
+static int row_blocks(const char* what, bool sum, int32_t n_tensors, const lsr_row_tensor* t, int64_t n_rows,
+                      int32_t n_blocks, void* stream) {
+    if (n_tensors < 0 || n_tensors > LSR_GATHER_MAX_TENSORS || n_rows < 0 || n_blocks < 1 || (n_tensors > 0 && !t))
+        return lsr::fail(LSR_EINVAL, std::string(what) + ": 0 <= n_tensors <= LSR_GATHER_MAX_TENSORS, n_rows >= 0, "
+                                                       "n_blocks >= 1");
+    if (n_tensors == 0 || n_rows == 0) return LSR_OK;
+    RowBlocksArgs a{};
+    a.nb = n_blocks;
+    int64_t most = 0;
+    for (int k = 0; k < n_tensors; ++k) {
+        if (!t[k].src || !t[k].dst || t[k].row_bytes <= 0 || t[k].row_bytes % 4)
+            return lsr::fail(LSR_EINVAL, std::string(what) + ": src, dst and rows of whole floats required");
+        a.src[k] = static_cast<const float*>(t[k].src);
+        a.dst[k] = static_cast<float*>(t[k].dst);
+        a.n[k] = n_rows * (t[k].row_bytes / 4);
+        most = std::max(most, a.n[k]);
+    }
+    const dim3 grid((unsigned)std::min<int64_t>((most + 255) / 256, 4096), n_tensors);
+    if (sum) hipLaunchKernelGGL(k_sum_row_blocks, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
+    else hipLaunchKernelGGL(k_repeat_rows, grid, dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
+    return launched(what);
+}
+
+int lsr_repeat_rows(int32_t n_tensors, const lsr_row_tensor* t, int64_t n_rows, int32_t n_blocks, void* stream) {
+    return row_blocks("lsr_repeat_rows", false, n_tensors, t, n_rows, n_blocks, stream);
+}
+
+int lsr_sum_row_blocks(int32_t n_tensors, const lsr_row_tensor* t, int64_t n_rows, int32_t n_blocks, void* stream) {
+    return row_blocks("lsr_sum_row_blocks", true, n_tensors, t, n_rows, n_blocks, stream);
 }
 
 int lsr_activate(int32_t P, const float* raw_scales, const float* raw_rotations, const float* raw_opacity,

@@ -107,6 +107,9 @@ SIGNATURES = {
                                        _vp, _vp]),
     "lsr_reset_opacity": (ctypes.c_int, [ctypes.c_int32, _vp, _vp, _vp, _vp]),
     "lsr_activate": (ctypes.c_int, [ctypes.c_int32] + [_vp] * 7),
+    "lsr_repeat_rows": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(RowTensor), ctypes.c_int64, ctypes.c_int32, _vp]),
+    "lsr_sum_row_blocks": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(RowTensor), ctypes.c_int64, ctypes.c_int32,
+                                          _vp]),
     "lsr_activate_backward": (ctypes.c_int, [ctypes.c_int32] + [_vp] * 10),
     "lsr_version": (ctypes.c_int, []),
     "lsr_require_api": (ctypes.c_int, [ctypes.c_int32]),

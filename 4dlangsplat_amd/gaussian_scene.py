@@ -317,6 +317,59 @@ class _Activate(torch.autograd.Function):
         return tuple(outs)
 
 
+class _RepeatViews(torch.autograd.Function):
+    """x.repeat(V, 1, ...) of several tensors in one launch, and their backward (the V row blocks
+    summed) in one (lsr_repeat_rows / lsr_sum_row_blocks, include/lsr_train.h)."""
+
+    @staticmethod
+    def _jobs(pairs):
+        from diff_gaussian_rasterization import _lib
+        rows = (_lib.RowTensor * len(pairs))()
+        for k, (src, dst) in enumerate(pairs):
+            rows[k].src, rows[k].dst = src.data_ptr(), dst.data_ptr()
+            rows[k].row_bytes, rows[k].zero_from = src[0].numel() * 4 if src.shape[0] else 4, 0
+        return rows
+
+    @staticmethod
+    def forward(ctx, V, *xs):
+        from diff_gaussian_rasterization import _lib
+        xs = [x.contiguous() for x in xs]
+        P = xs[0].shape[0]
+        if any(x.dtype != torch.float32 or x.shape[0] != P for x in xs):
+            raise ValueError("repeat_views: float32 tensors of the same row count")
+        outs = [x.new_empty((V * P,) + tuple(x.shape[1:])) for x in xs]
+        ctx.V, ctx.P, ctx.shapes = V, P, [tuple(x.shape) for x in xs]
+        st = torch.cuda.current_stream(xs[0].device).cuda_stream
+        _lib.check(_lib.load().lsr_repeat_rows(len(xs), _RepeatViews._jobs(list(zip(xs, outs))), P, V, st),
+                   "lsr_repeat_rows")
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        from diff_gaussian_rasterization import _lib
+        need = ctx.needs_input_grad[1:]
+        grads, pairs = [], []
+        for k, g in enumerate(gs):
+            if not need[k] or g is None:
+                grads.append(None)
+                continue
+            d = g.new_empty(ctx.shapes[k])
+            pairs.append((g.contiguous(), d))
+            grads.append(d)
+        if pairs:
+            st = torch.cuda.current_stream(pairs[0][0].device).cuda_stream
+            _lib.check(_lib.load().lsr_sum_row_blocks(len(pairs), _RepeatViews._jobs(pairs), ctx.P, ctx.V, st),
+                       "lsr_sum_row_blocks")
+        return (None,) + tuple(grads)
+
+
+def repeat_views(V, *xs):
+    """The tensors' rows repeated V times (render_views): one native launch each way on the GPU."""
+    if xs[0].is_cuda and xs[0].shape[0] > 0:
+        return _RepeatViews.apply(V, *xs)
+    return tuple(x.repeat(V, *([1] * (x.dim() - 1))) for x in xs)
+
+
 def activate(scales, rotations, opacity):
     """The render path's activations: one native launch each way on the GPU (_Activate); the PyTorch
     ops for host tensors or a missing input."""
@@ -447,18 +500,19 @@ def render_views(cams: Sequence, pc: GaussianScene, bg_color: torch.Tensor, stag
                        language_feature_hiddendim=language_feature_hiddendim, **kw) for c in cams]
     dev = pc.xyz.device
     V, P = len(cams), pc.P
+    t = torch.cat([torch.full((P,), float(c.time), device=dev) for c in cams])
+    deform = pc.deformation.apply if (torch.is_grad_enabled() and hasattr(pc.deformation, "apply")) \
+        else pc.deformation
+    ins = [pc.get_xyz, pc.scaling, pc.rotation, pc.opacity, pc.get_features]
     if "base" not in stage:
         lang = pc.get_language_feature
         if not nonormalized:
             lang = lang / (lang.norm(dim=-1, keepdim=True) + 1e-9)
-    else:
-        lang = torch.zeros((P, language_feature_hiddendim), dtype=pc.opacity.dtype, device=dev)
-    rep = lambda x: x.repeat(V, *([1] * (x.dim() - 1)))   # noqa: E731
-    t = torch.cat([torch.full((P,), float(c.time), device=dev) for c in cams])
-    deform = pc.deformation.apply if (torch.is_grad_enabled() and hasattr(pc.deformation, "apply")) \
-        else pc.deformation
-    outs = list(deform(rep(pc.get_xyz), rep(pc.scaling), rep(pc.rotation), rep(pc.opacity), rep(pc.get_features),
-                       rep(lang), t, no_dlang=True if "base" in stage else None))
+        ins = list(repeat_views(V, *ins, lang))
+    else:   # the passed-through zeros, made at the batch's size
+        ins = list(repeat_views(V, *ins)) + [torch.zeros((V * P, language_feature_hiddendim), dtype=pc.opacity.dtype,
+                                                          device=dev)]
+    outs = list(deform(*ins, t, no_dlang=True if "base" in stage else None))
     # the activations (render(), gaussian_renderer/__init__.py:131-133) once over the V * P rows: the
     # same values row by row, a third of the launches forward and backward
     outs[1], outs[2], outs[3] = activate(outs[1], outs[2], outs[3])

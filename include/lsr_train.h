@@ -109,6 +109,14 @@ int lsr_split_fixup(int64_t n_new, int64_t base, int32_t n_copies, const int32_t
  * exp_avg_sq may be NULL). */
 int lsr_reset_opacity(int32_t P, float *opacity, float *exp_avg, float *exp_avg_sq, void *stream);
 
+/* render_views' V views of P Gaussians (gaussian_scene.py), every tensor in one launch (t[k].src /
+ * dst / row_bytes, rows of whole floats; zero_from unused):
+ *   lsr_repeat_rows:    dst row j = src row j mod n_rows, j < n_blocks * n_rows  (torch.Tensor.repeat)
+ *   lsr_sum_row_blocks: dst row j = sum over b < n_blocks of src row b * n_rows + j, in b order (its
+ *                       backward; torch sums two blocks the same way) */
+int lsr_repeat_rows(int32_t n_tensors, const lsr_row_tensor *t, int64_t n_rows, int32_t n_blocks, void *stream);
+int lsr_sum_row_blocks(int32_t n_tensors, const lsr_row_tensor *t, int64_t n_rows, int32_t n_blocks, void *stream);
+
 /* The render path's activations over P rows in one launch (gaussian_renderer/__init__.py:191-193,
  * gaussian_model.py:38-46; replaces torch.exp / torch.nn.functional.normalize / torch.sigmoid and
  * their autograd backward there, GaussianScene.render_views):

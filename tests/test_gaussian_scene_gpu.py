@@ -222,3 +222,29 @@ def test_native_activations_match_torch():
     _, _, oo = gs._Activate.apply(s, r, o2)
     oo.sum().backward()
     torch.testing.assert_close(o2.grad, (torch.sigmoid(o) * (1 - torch.sigmoid(o))), rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("V", [2, 3])
+def test_repeat_views_matches_torch(V):
+    """lsr_repeat_rows / lsr_sum_row_blocks (render_views' inputs repeated once per view) against
+    Tensor.repeat and its autograd: the copies bit for bit, the folded gradients bit for bit at two
+    views (one addition either way) and within rounding at three; an input without a gradient and
+    a gradient that does not reach one output."""
+    g = torch.Generator(device="cpu").manual_seed(V)
+    P = 50_001
+    xs = [torch.randn(P, *shape, generator=g).cuda() for shape in ((3,), (4,), (1,), (16, 3))]
+    a = [x.clone().requires_grad_(k != 2) for k, x in enumerate(xs)]
+    b = [x.clone().requires_grad_(k != 2) for k, x in enumerate(xs)]
+    got = gs.repeat_views(V, *a)
+    ref = [x.repeat(V, *([1] * (x.dim() - 1))) for x in b]
+    for u, w in zip(got, ref):
+        assert torch.equal(u, w)
+    ups = [torch.randn(u.shape, generator=g).cuda() for u in got]
+    torch.autograd.backward([got[0], got[1], got[3]], [ups[0], ups[1], ups[3]])
+    torch.autograd.backward([ref[0], ref[1], ref[3]], [ups[0], ups[1], ups[3]])
+    assert a[2].grad is None
+    for k in (0, 1, 3):
+        if V == 2:
+            assert torch.equal(a[k].grad, b[k].grad)
+        else:
+            torch.testing.assert_close(a[k].grad, b[k].grad, rtol=1e-6, atol=1e-6)
