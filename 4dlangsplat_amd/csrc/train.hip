@@ -309,6 +309,56 @@ __global__ void __launch_bounds__(256) k_sum_row_blocks(RowBlocksArgs a) {
     }
 }
 
+// The base stages' loss (train.py:272-276, utils/loss_utils.py l1_loss): mean |image_v - gt_v| over the
+// views' [3, H, W] images without stacking them; the per-block partial sums are added in a fixed
+// order by one block (deterministic), and the backward is PyTorch's abs / mean backward,
+// sign(x) * (g * (1 / N)), bit for bit.
+constexpr int L1_MAX_VIEWS = 8, L1_BLOCKS = 256;
+struct L1Args {
+    const float* img[L1_MAX_VIEWS];
+    float* grad[L1_MAX_VIEWS];
+    const float* gt;
+    int64_t gt_stride, n;     // floats between the views' gt blocks; floats per view
+    int64_t total;            // V n
+    const float* d_loss;
+    float* partial;           // [V][L1_BLOCKS]
+    float* loss;
+};
+__global__ void __launch_bounds__(256) k_l1_partial(L1Args a) {
+    __shared__ float s_w[4];
+    const float* __restrict__ x = a.img[blockIdx.y];
+    const float* __restrict__ y = a.gt + blockIdx.y * a.gt_stride;
+    float acc = 0.0f;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < a.n; e += (int64_t)gridDim.x * 256) acc += fabsf(x[e] - y[e]);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) a.partial[blockIdx.y * gridDim.x + blockIdx.x] = (s_w[0] + s_w[1]) + (s_w[2] + s_w[3]);
+}
+__global__ void __launch_bounds__(256) k_l1_final(L1Args a, int nparts) {
+    __shared__ float s_w[4];
+    float acc = 0.0f;
+    for (int i = threadIdx.x; i < nparts; i += 256) acc += a.partial[i];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) a.loss[0] = ((s_w[0] + s_w[1]) + (s_w[2] + s_w[3])) * (1.0f / (float)a.total);
+}
+__global__ void __launch_bounds__(256) k_l1_grad(L1Args a) {
+    const float* __restrict__ x = a.img[blockIdx.y];
+    const float* __restrict__ y = a.gt + blockIdx.y * a.gt_stride;
+    float* __restrict__ d = a.grad[blockIdx.y];
+    // mean's backward, g / N, as PyTorch's division by a host scalar runs it (times the float reciprocal),
+    // then abs's: * sign
+    const float s = a.d_loss[0] * (1.0f / (float)a.total);
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < a.n; e += (int64_t)gridDim.x * 256) {
+        const float v = x[e] - y[e];
+        d[e] = s * (v > 0.0f ? 1.0f : (v < 0.0f ? -1.0f : 0.0f));
+    }
+}
+
 struct TrainWs {
     uint32_t *f0, *f1, *o0, *o1, *totals;
     void* scan_tmp;
@@ -511,6 +561,52 @@ int lsr_repeat_rows(int32_t n_tensors, const lsr_row_tensor* t, int64_t n_rows, 
 
 int lsr_sum_row_blocks(int32_t n_tensors, const lsr_row_tensor* t, int64_t n_rows, int32_t n_blocks, void* stream) {
     return row_blocks("lsr_sum_row_blocks", true, n_tensors, t, n_rows, n_blocks, stream);
+}
+
+int64_t lsr_l1_workspace_bytes(int32_t V) { return (int64_t)(V > 0 ? V : 1) * L1_BLOCKS * (int64_t)sizeof(float); }
+
+static int l1_args(const char* what, int32_t V, int64_t n, const float* const* images, const float* gt,
+                   int64_t gt_view_stride, L1Args& a) {
+    if (V < 1 || V > L1_MAX_VIEWS || n < 0 || !images || !gt || gt_view_stride < n)
+        return lsr::fail(LSR_EINVAL, std::string(what) + ": 1 <= V <= 8, n >= 0, gt_view_stride >= n, images and gt");
+    a = L1Args{};
+    for (int v = 0; v < V; ++v) {
+        if (!images[v]) return lsr::fail(LSR_EINVAL, std::string(what) + ": null image");
+        a.img[v] = images[v];
+    }
+    a.gt = gt;
+    a.gt_stride = gt_view_stride;
+    a.n = n;
+    a.total = (int64_t)V * n;
+    return LSR_OK;
+}
+
+int lsr_l1_loss_views(int32_t V, int64_t n, const float* const* images, const float* gt, int64_t gt_view_stride,
+                      float* loss, void* workspace, void* stream) {
+    L1Args a;
+    if (int rc = l1_args("lsr_l1_loss_views", V, n, images, gt, gt_view_stride, a)) return rc;
+    if (!loss || !workspace) return lsr::fail(LSR_EINVAL, "lsr_l1_loss_views: loss and workspace required");
+    a.partial = static_cast<float*>(workspace);
+    a.loss = loss;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(k_l1_partial, dim3(L1_BLOCKS, V), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_l1_final, dim3(1), dim3(256), 0, st, a, V * L1_BLOCKS);
+    return launched("l1 loss");
+}
+
+int lsr_l1_loss_views_backward(int32_t V, int64_t n, const float* const* images, const float* gt,
+                               int64_t gt_view_stride, const float* d_loss, float* const* d_images, void* stream) {
+    L1Args a;
+    if (int rc = l1_args("lsr_l1_loss_views_backward", V, n, images, gt, gt_view_stride, a)) return rc;
+    if (!d_loss || !d_images) return lsr::fail(LSR_EINVAL, "lsr_l1_loss_views_backward: d_loss and d_images required");
+    for (int v = 0; v < V; ++v) {
+        if (!d_images[v]) return lsr::fail(LSR_EINVAL, "lsr_l1_loss_views_backward: null gradient image");
+        a.grad[v] = d_images[v];
+    }
+    a.d_loss = d_loss;
+    const unsigned bx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 1024));
+    hipLaunchKernelGGL(k_l1_grad, dim3(bx, V), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
+    return launched("l1 loss backward");
 }
 
 int lsr_activate(int32_t P, const float* raw_scales, const float* raw_rotations, const float* raw_opacity,

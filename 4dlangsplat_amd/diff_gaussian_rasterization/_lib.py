@@ -107,6 +107,10 @@ SIGNATURES = {
                                        _vp, _vp]),
     "lsr_reset_opacity": (ctypes.c_int, [ctypes.c_int32, _vp, _vp, _vp, _vp]),
     "lsr_activate": (ctypes.c_int, [ctypes.c_int32] + [_vp] * 7),
+    "lsr_l1_workspace_bytes": (ctypes.c_int64, [ctypes.c_int32]),
+    "lsr_l1_loss_views": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int64, _vp, _vp, ctypes.c_int64, _vp, _vp, _vp]),
+    "lsr_l1_loss_views_backward": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int64, _vp, _vp, ctypes.c_int64, _vp, _vp,
+                                                  _vp]),
     "lsr_repeat_rows": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(RowTensor), ctypes.c_int64, ctypes.c_int32, _vp]),
     "lsr_sum_row_blocks": (ctypes.c_int, [ctypes.c_int32, ctypes.POINTER(RowTensor), ctypes.c_int64, ctypes.c_int32,
                                           _vp]),

@@ -37,10 +37,59 @@ from __future__ import annotations
 
 from typing import Callable, Optional, Sequence
 
+import ctypes
+
 import torch
 
 from gaussian_scene import GaussianScene, render, render_views
 from gaussian_train import GaussianTrainer, TensorAdam, get_expon_lr_func
+
+
+class _L1Views(torch.autograd.Function):
+    """l1_loss(stack(images), gts[:, :3]) (train.py:272-276) over the views' renders without stacking
+    them: two launches forward, one backward (lsr_l1_loss_views / _backward, include/lsr_train.h); the
+    gradient PyTorch's bit for bit, the loss's partial sums added in a fixed order."""
+
+    @staticmethod
+    def forward(ctx, gts3, *images):
+        from diff_gaussian_rasterization import _lib
+        L = _lib.load()
+        V = len(images)
+        imgs = [x.contiguous() for x in images]
+        n = imgs[0].numel()
+        if gts3.shape[0] != V or any(x.shape != imgs[0].shape or x.dtype != torch.float32 for x in imgs) \
+                or tuple(gts3.shape[1:]) != tuple(imgs[0].shape) or gts3[0].stride() != imgs[0].stride():
+            raise ValueError("l1 loss: V float32 images of one shape and gts[:, :3] of that shape")
+        ptrs = (ctypes.c_void_p * V)(*[x.data_ptr() for x in imgs])
+        ws = torch.empty(int(L.lsr_l1_workspace_bytes(V)), dtype=torch.uint8, device=imgs[0].device)
+        loss = torch.empty((), device=imgs[0].device)
+        st = torch.cuda.current_stream(imgs[0].device).cuda_stream
+        _lib.check(L.lsr_l1_loss_views(V, n, ptrs, gts3.data_ptr(), gts3.stride(0), loss.data_ptr(), ws.data_ptr(), st),
+                   "lsr_l1_loss_views")
+        ctx.save_for_backward(gts3, *imgs)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        from diff_gaussian_rasterization import _lib
+        gts3, *imgs = ctx.saved_tensors
+        V = len(imgs)
+        grads = [torch.empty_like(x) for x in imgs]
+        g = g.contiguous()
+        st = torch.cuda.current_stream(g.device).cuda_stream
+        _lib.check(_lib.load().lsr_l1_loss_views_backward(
+            V, imgs[0].numel(), (ctypes.c_void_p * V)(*[x.data_ptr() for x in imgs]), gts3.data_ptr(), gts3.stride(0),
+            g.data_ptr(), (ctypes.c_void_p * V)(*[x.data_ptr() for x in grads]), st), "lsr_l1_loss_views_backward")
+        return (None,) + tuple(grads)
+
+
+def l1_loss_views(images, gts):
+    """mean |stack(images) - gts[:, :3]| with its gradient (the base stages' loss); native on the GPU
+    for up to 8 views, PyTorch otherwise."""
+    gts3 = gts[:, :3]
+    if images[0].is_cuda and 1 <= len(images) <= 8 and gts3[0].is_contiguous():
+        return _L1Views.apply(gts3, *images)
+    return (torch.stack(images) - gts3).abs().mean()
 
 
 class ReferenceSchedule:
@@ -191,8 +240,7 @@ class TrainStep:
         (the reference trains them one view at a time, batch_size 1, where its cat over views is this
         stack)."""
         if not self.lang_stage:
-            images = torch.stack([o["render"] for o in outs])
-            return (images - gts[:, :3]).abs().mean()
+            return l1_loss_views([o["render"] for o in outs], gts)
         if gt_lang is None or lang_mask is None:
             raise ValueError("a 'lang' stage needs gt_lang and lang_mask")
         lang = torch.stack([o["language_feature_image"] for o in outs])

@@ -17,6 +17,8 @@
  *       -> lsr_reset_opacity
  *   - exp / normalize / sigmoid of the render path          gaussian_renderer/__init__.py:191-193
  *       -> lsr_activate, lsr_activate_backward
+ *   - the base stages' L1 image loss                         train.py:272-276
+ *       -> lsr_l1_loss_views, lsr_l1_loss_views_backward
  *
  * Conventions as lsr.h: device pointers, float32 unless stated, contiguous rows; the library
  * allocates nothing (plans take a workspace of lsr_train_workspace_bytes(P)); every launch on
@@ -116,6 +118,18 @@ int lsr_reset_opacity(int32_t P, float *opacity, float *exp_avg, float *exp_avg_
  *                       backward; torch sums two blocks the same way) */
 int lsr_repeat_rows(int32_t n_tensors, const lsr_row_tensor *t, int64_t n_rows, int32_t n_blocks, void *stream);
 int lsr_sum_row_blocks(int32_t n_tensors, const lsr_row_tensor *t, int64_t n_rows, int32_t n_blocks, void *stream);
+
+/* The base stages' image loss (train.py:272-276: l1_loss(cat(images), cat(gts)[:, :3]) = mean |x - y|)
+ * over V <= 8 views without stacking them: images[v] [n] floats (one [3,H,W] render), the view's
+ * gt at gt + v * gt_view_stride (its first n floats: gts[v, :3]).  loss: one device float,
+ * sum * (1 / (V n)), the partial sums added in a fixed order (deterministic; not PyTorch's order);
+ * workspace >= lsr_l1_workspace_bytes(V).  The backward writes d_images[v] = sign(x - y) * (d_loss * (1 / (V n))),
+ * PyTorch's abs / mean backward bit for bit. */
+int64_t lsr_l1_workspace_bytes(int32_t V);
+int lsr_l1_loss_views(int32_t V, int64_t n, const float *const *images, const float *gt, int64_t gt_view_stride,
+                      float *loss, void *workspace, void *stream);
+int lsr_l1_loss_views_backward(int32_t V, int64_t n, const float *const *images, const float *gt,
+                               int64_t gt_view_stride, const float *d_loss, float *const *d_images, void *stream);
 
 /* The render path's activations over P rows in one launch (gaussian_renderer/__init__.py:191-193,
  * gaussian_model.py:38-46; replaces torch.exp / torch.nn.functional.normalize / torch.sigmoid and

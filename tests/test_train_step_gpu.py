@@ -262,3 +262,25 @@ def test_configs4_standin_at_size():
                             ("sh", "sh", "sh"), ("opacity", "opacities", "opacity"), ("scales", "scales", "scales"),
                             ("rotations", "rotations", "rotations"))}
     assert max(errs.values()) <= 1e-4, errs
+
+
+@pytest.mark.parametrize("V,ch", [(2, 3), (4, 4), (1, 3)])
+def test_l1_loss_views_matches_torch(V, ch):
+    """lsr_l1_loss_views (the base stages' loss over the views' renders, not stacked) against
+    (stack(images) - gts[:, :3]).abs().mean(): the loss within float summation order, the images'
+    gradients bit for bit (PyTorch's sign(x) * (g * (1 / N))); gts with a fourth channel read through its
+    view stride; exact zeros (sign 0) included."""
+    from train_step import l1_loss_views
+    g = torch.Generator(device="cpu").manual_seed(V)
+    H, W = 97, 131
+    imgs = [torch.rand(3, H, W, generator=g).cuda().requires_grad_(True) for _ in range(V)]
+    gts = torch.rand(V, ch, H, W, generator=g).cuda()
+    gts[0, :3, :5] = imgs[0].detach()[:, :5]   # exact zeros
+    ref_imgs = [x.detach().clone().requires_grad_(True) for x in imgs]
+    got = l1_loss_views(imgs, gts)
+    ref = (torch.stack(ref_imgs) - gts[:, :3]).abs().mean()
+    torch.testing.assert_close(got, ref, rtol=2e-6, atol=0.0)
+    (got * 3.0).backward()
+    (ref * 3.0).backward()
+    for a, b in zip(imgs, ref_imgs):
+        assert torch.equal(a.grad, b.grad)
