@@ -363,6 +363,72 @@ class _RepeatViews(torch.autograd.Function):
         return (None,) + tuple(grads)
 
 
+_ZEROS = {}   # device -> a zero float buffer (the source of the absent views' gradient rows)
+
+
+def _zeros_source(device, nbytes):
+    z = _ZEROS.get(device)
+    if z is None or z.numel() * 4 < nbytes:
+        z = _ZEROS[device] = torch.zeros((nbytes + 3) // 4, device=device)
+    return z
+
+
+class _SplitViews(torch.autograd.Function):
+    """The field's outputs over V * P rows split into the V views' row blocks (views, no copy), whose
+    backward assembles every output's gradient from the views' in one launch (lsr_repeat_rows with
+    one block: a multi-tensor copy) instead of one concatenation per output; absent view gradients
+    read zeros."""
+
+    @staticmethod
+    def forward(ctx, V, *xs):
+        P = xs[0].shape[0] // V
+        ctx.V, ctx.P, ctx.shapes = V, P, [tuple(x.shape) for x in xs]
+        ctx.set_materialize_grads(False)   # absent view gradients stay None (no zero tensors made)
+        outs = []
+        for x in xs:
+            outs.extend(x.split(P))
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        from diff_gaussian_rasterization import _lib
+        V, P = ctx.V, ctx.P
+        res, jobs, keep = [], [], []
+        for k, shp in enumerate(ctx.shapes):
+            part = gs[k * V:(k + 1) * V]
+            if not ctx.needs_input_grad[1 + k] or all(g is None for g in part):
+                res.append(None)
+                continue
+            ref = next(g for g in part if g is not None)
+            out = ref.new_empty(shp)
+            res.append(out)
+            row = out[0].numel() * 4
+            for b, g in enumerate(part):
+                src = _zeros_source(out.device, P * row) if g is None else g.contiguous()
+                keep.append(src)
+                jobs.append((src.data_ptr(), out.data_ptr() + b * P * row, row))
+        if not jobs:
+            return (None,) + tuple(res)
+        st = torch.cuda.current_stream(next(r for r in res if r is not None).device).cuda_stream
+        L = _lib.load()
+        for i in range(0, len(jobs), 32):
+            chunk = jobs[i:i + 32]
+            rows = (_lib.RowTensor * len(chunk))()
+            for k, (src, dst, row) in enumerate(chunk):
+                rows[k].src, rows[k].dst, rows[k].row_bytes, rows[k].zero_from = src, dst, row, 0
+            _lib.check(L.lsr_repeat_rows(len(chunk), rows, P, 1, st), "lsr_repeat_rows")
+        return (None,) + tuple(res)
+
+
+def split_views(V, *xs):
+    """xs' row blocks per view (tuples of V views each); on the GPU the backward is one launch."""
+    live = [x for x in xs if x is not None]
+    if not live or not live[0].is_cuda or live[0].shape[0] == 0:
+        return [x.split(x.shape[0] // V) if x is not None else (None,) * V for x in xs]
+    parts = iter(_SplitViews.apply(V, *live))
+    return [tuple(next(parts) for _ in range(V)) if x is not None else (None,) * V for x in xs]
+
+
 def repeat_views(V, *xs):
     """The tensors' rows repeated V times (render_views): one native launch each way on the GPU."""
     if xs[0].is_cuda and xs[0].shape[0] > 0:
@@ -516,7 +582,7 @@ def render_views(cams: Sequence, pc: GaussianScene, bg_color: torch.Tensor, stag
     # the activations (render(), gaussian_renderer/__init__.py:131-133) once over the V * P rows: the
     # same values row by row, a third of the launches forward and backward
     outs[1], outs[2], outs[3] = activate(outs[1], outs[2], outs[3])
-    parts = [o.split(P) if o is not None else (None,) * V for o in outs]
+    parts = split_views(V, *outs)
     return [render(c, pc, bg_color, stage=stage, nonormalized=nonormalized,
                    language_feature_hiddendim=language_feature_hiddendim,
                    _deformed=tuple(p[v] for p in parts), **kw) for v, c in enumerate(cams)]

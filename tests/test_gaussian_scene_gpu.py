@@ -248,3 +248,25 @@ def test_repeat_views_matches_torch(V):
             assert torch.equal(a[k].grad, b[k].grad)
         else:
             torch.testing.assert_close(a[k].grad, b[k].grad, rtol=1e-6, atol=1e-6)
+
+
+def test_split_views_matches_torch():
+    """split_views (render_views' per-view blocks of the field's outputs) against Tensor.split: the
+    same views, and the assembled gradients bit for bit, with a view whose gradient never arrives
+    (zeros) and an output no view's gradient reaches (None)."""
+    g = torch.Generator(device="cpu").manual_seed(11)
+    V, P = 3, 20_011
+    xs = [torch.randn(V * P, *shape, generator=g).cuda() for shape in ((3,), (16, 3), (1,))]
+    a = [x.clone().requires_grad_(True) for x in xs]
+    b = [x.clone().requires_grad_(True) for x in xs]
+    pa = gs.split_views(V, *a, None)
+    pb = [x.split(P) for x in b]
+    assert pa[3] == (None,) * V
+    for u, w in zip(pa[:3], pb):
+        for x, y in zip(u, w):
+            assert torch.equal(x, y)
+    ups = {(k, v): torch.randn(pa[k][v].shape, generator=g).cuda() for k in (0, 1) for v in range(V) if (k, v) != (1, 1)}
+    torch.autograd.backward([pa[k][v] for k, v in ups], list(ups.values()))
+    torch.autograd.backward([pb[k][v] for k, v in ups], list(ups.values()))
+    assert torch.equal(a[0].grad, b[0].grad) and torch.equal(a[1].grad, b[1].grad)
+    assert a[2].grad is None and b[2].grad is None
