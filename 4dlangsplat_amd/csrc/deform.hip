@@ -1817,26 +1817,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
             }
         }
     };
-    // relu(Z1 + b1), dW2 += G^T relu(Z1), dZ1 = (G W2) [Z1 > 0], db1, all per lane (tile in buffer b)
-    auto dz1 = [&](int b, const df32x16 (&z)[2], df32x16 (&d)[2]) __attribute__((always_inline)) {
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const float zz = z[mt][q] + b1c;
-                const float zr = fmaxf(zz, 0.0f);
-                const float4 gv = s_g4[b][row_of(mt, q, hh)];
-                w2s[0] = __builtin_fmaf(gv.x, zr, w2s[0]); w2s[1] = __builtin_fmaf(gv.y, zr, w2s[1]);
-                w2s[2] = __builtin_fmaf(gv.z, zr, w2s[2]); w2s[3] = __builtin_fmaf(gv.w, zr, w2s[3]);
-                float dv = gv.x * w2c[0];
-                dv = __builtin_fmaf(gv.y, w2c[1], dv);
-                dv = __builtin_fmaf(gv.z, w2c[2], dv);
-                dv = __builtin_fmaf(gv.w, w2c[3], dv);
-                dv = zz > 0.0f ? dv : 0.0f;
-                db1 += dv;
-                d[mt][q] = dv;
-            }
-    };
     // one element of dz1 (e = 16 mt + q)
     auto dz1_elem = [&](int b, const df32x16 (&z)[2], df32x16 (&d)[2], int mt, int q) __attribute__((always_inline)) {
         const float zz = z[mt][q] + b1c;
@@ -1869,20 +1849,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))
             const float4 gv = make_float4(pg[0], pg[1], pg[2], pg[3]);
             s_g4[b][tid] = gv;
             db2v.x += gv.x; db2v.y += gv.y; db2v.z += gv.z; db2v.w += gv.w;
-        }
-    };
-    auto dw1 = [&](int b, const df32x16 (&d)[2]) __attribute__((always_inline)) {
-#pragma unroll
-        for (int ks = 0; ks < DN / 16; ++ks) {
-            dbf16x8 dh, dl;
-            wg_regs_to_op(d[ks >> 1], ks & 1, dh, dl);
-#pragma unroll
-            for (int nt = 0; nt < 4; ++nt) {
-                const dbf16x8 bh = wg_lds_op(s_ah[b], DAP, ks, 32 * nt), bl = wg_lds_op(s_al[b], DAP, ks, 32 * nt);
-                w1acc[nt] = DMFMA(dh, bh, w1acc[nt]);
-                w1acc[nt] = DMFMA(dh, bl, w1acc[nt]);
-                w1acc[nt] = DMFMA(dl, bh, w1acc[nt]);
-            }
         }
     };
     // ---- prologue: tiles 0 and 1 in LDS, tile 2's rows in registers, Z1 of tile 0 --------------------------
