@@ -31,7 +31,7 @@ from . import _lib
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "RasterizerState",
            "forward_native", "backward_native", "backward_views_native", "backward_composite_native",
            "backward_preprocess_views_native", "preprocess_views_native", "binning_views_native",
-           "render_views_native", "backward_composite_views_native", "language_split_native",
+           "render_views_native", "backward_composite_views_native", "language_split_native", "rasterize_views",
            "radii_max_native"]
 
 _lib.load()   # fail loudly at import if the native library is missing
@@ -952,35 +952,97 @@ class _RasterizeGaussians(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad_color, grad_lang, grad_radii, grad_depth):
-        st = ctx.state
-        ng = ctx.needs_input_grad
-        need = dict(means3D=ng[0], means2D=ng[1], sh=ng[2], colors=True, language_feature=ng[4], opacities=ng[5],
-                    scales=ng[6], rotations=ng[7], cov3D=ng[8])
-        # torch.use_deterministic_algorithms(True) selects the fixed-order reduction (bitwise
-        # reproducible gradients, lsr_backward's deterministic mode) instead of float atomics
-        g = backward_native(st, grad_color, grad_lang if ctx.include_feature else None, grad_depth, need=need,
-                            deterministic=torch.are_deterministic_algorithms_enabled())
-        shp = ctx.shapes
+        return _raster_backward(ctx.state, ctx.shapes, ctx.include_feature, ctx.needs_input_grad[:9], grad_color,
+                                grad_lang, grad_depth) + (None,)
 
-        def like(t, shape):
-            return None if (t is None or shape is None) else t.reshape(shape)
 
-        grad_lang_in = None
-        if ng[4] and shp["lang"] is not None and len(shp["lang"]) > 0:
-            if g["language_feature"] is not None:
-                grad_lang_in = g["language_feature"].reshape(shp["lang"])
-            else:
-                grad_lang_in = torch.zeros(shp["lang"], dtype=torch.float32, device=st.inputs["means3D"].device)
-        return (g["means3D"] if ng[0] else None,
-                g["means2D"] if ng[1] else None,
-                like(g["sh"], shp["sh"]) if ng[2] else None,
-                g["colors"] if ng[3] else None,
-                grad_lang_in,
-                like(g["opacities"], shp["opacities"]) if ng[5] else None,
-                g["scales"] if ng[6] else None,
-                g["rotations"] if ng[7] else None,
-                g["cov3D"] if ng[8] else None,
-                None)
+def _raster_backward(st, shp, include_feature, ng, grad_color, grad_lang, grad_depth):
+    """The 9 input gradients of one view's rasterization (means3D, means2D, sh, colors_precomp,
+    language_feature_precomp, opacities, scales, rotations, cov3D_precomp); ng: which are needed."""
+    need = dict(means3D=ng[0], means2D=ng[1], sh=ng[2], colors=True, language_feature=ng[4], opacities=ng[5],
+                scales=ng[6], rotations=ng[7], cov3D=ng[8])
+    # torch.use_deterministic_algorithms(True) selects the fixed-order reduction (bitwise
+    # reproducible gradients, lsr_backward's deterministic mode) instead of float atomics
+    g = backward_native(st, grad_color, grad_lang if include_feature else None, grad_depth, need=need,
+                        deterministic=torch.are_deterministic_algorithms_enabled())
+
+    def like(t, shape):
+        return None if (t is None or shape is None) else t.reshape(shape)
+
+    grad_lang_in = None
+    if ng[4] and shp["lang"] is not None and len(shp["lang"]) > 0:
+        if g["language_feature"] is not None:
+            grad_lang_in = g["language_feature"].reshape(shp["lang"])
+        else:
+            grad_lang_in = torch.zeros(shp["lang"], dtype=torch.float32, device=st.inputs["means3D"].device)
+    return (g["means3D"] if ng[0] else None,
+            g["means2D"] if ng[1] else None,
+            like(g["sh"], shp["sh"]) if ng[2] else None,
+            g["colors"] if ng[3] else None,
+            grad_lang_in,
+            like(g["opacities"], shp["opacities"]) if ng[5] else None,
+            g["scales"] if ng[6] else None,
+            g["rotations"] if ng[7] else None,
+            g["cov3D"] if ng[8] else None)
+
+
+class _RasterizeViews(torch.autograd.Function):
+    """_RasterizeGaussians for several views with their own Gaussians (a batch's deformed copies,
+    gaussian_scene.render_views): every view's preprocess is enqueued first with its instance count
+    deferred, then each view is binned and composited, so the host waits on view v's count while the
+    device runs the later views' preprocesses (one stream synchronisation per view in a row before:
+    the device idled through each).  Same kernels per view, same results; per-view backward."""
+
+    @staticmethod
+    def forward(ctx, settings_list, *flat):
+        pfs = []
+        for v, rs in enumerate(settings_list):
+            m3, _, sh, cp, lang, op, sc, rot, cov = flat[9 * v:9 * v + 9]
+            pfs.append(preprocess_native(rs, m3, op, shs=sh, colors_precomp=cp,
+                                         language_feature=lang if rs.include_feature else None, scales=sc,
+                                         rotations=rot, cov3D_precomp=cov, defer_count=True))
+        outs, radii_all = [], []
+        ctx.views = []
+        for v, (rs, pf) in enumerate(zip(settings_list, pfs)):
+            color, lang, radii, depth, state = render_native(pf)
+            lang_in, sh, op = flat[9 * v + 4], flat[9 * v + 2], flat[9 * v + 5]
+            if not rs.include_feature and lang_in is not None and lang_in.numel() > 0:
+                lang = torch.zeros((lang_in.shape[-1],) + tuple(color.shape[1:]), dtype=color.dtype,
+                                   device=color.device)
+            ctx.views.append((state, dict(sh=None if sh is None else sh.shape, opacities=op.shape,
+                                          lang=None if lang_in is None else lang_in.shape), rs.include_feature))
+            outs += [color, lang, radii, depth]
+            radii_all.append(radii)
+        ctx.mark_non_differentiable(*radii_all)
+        ctx.set_materialize_grads(False)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        res = []
+        for v, (state, shapes, include_feature) in enumerate(ctx.views):
+            gc, gl, _, gd = grads[4 * v:4 * v + 4]
+            res.extend(_raster_backward(state, shapes, include_feature, ctx.needs_input_grad[1 + 9 * v:10 + 9 * v],
+                                        gc, gl, gd))
+        return (None,) + tuple(res)
+
+
+def rasterize_views(settings_list, views):
+    """GaussianRasterizer forward for several views, each with its own inputs: views[v] =
+    dict(means3D=, means2D=, shs=, colors_precomp=, language_feature_precomp=, opacities=, scales=,
+    rotations=, cov3D_precomp=).  Returns [(color, language_feature, radii, depth)] per view
+    (_RasterizeViews: the views' preprocesses enqueued ahead of their count waits)."""
+    flat = []
+    for rs, kw in zip(settings_list, views):
+        if (kw.get("shs") is None) == (kw.get("colors_precomp") is None):
+            raise Exception("Please provide excatly one of either SHs or precomputed colors!")
+        if ((kw.get("scales") is None or kw.get("rotations") is None) == (kw.get("cov3D_precomp") is None)):
+            raise Exception("Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!")
+        flat += [kw["means3D"], kw["means2D"], kw.get("shs"), kw.get("colors_precomp"),
+                 kw.get("language_feature_precomp"), kw["opacities"], kw.get("scales"), kw.get("rotations"),
+                 kw.get("cov3D_precomp")]
+    out = _RasterizeViews.apply(list(settings_list), *flat)
+    return [tuple(out[4 * v:4 * v + 4]) for v in range(len(settings_list))]
 
 
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, language_feature_precomp, opacities, scales, rotations,

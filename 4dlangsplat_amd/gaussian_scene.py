@@ -445,6 +445,35 @@ def activate(scales, rotations, opacity):
             torch.nn.functional.normalize(rotations) if rotations is not None else None, torch.sigmoid(opacity))
 
 
+def _screenspace(pc):
+    """The screen-space gradient carrier (gaussian_renderer/__init__.py:30-35): zeros + 0, grad retained."""
+    sp = torch.zeros_like(pc.get_xyz, requires_grad=True, device=pc.xyz.device) + 0
+    try:
+        sp.retain_grad()
+    except RuntimeError:
+        pass
+    return sp
+
+
+def _raster_settings(viewpoint_camera, pc, bg_color, scaling_modifier, debug, include_feature, cam_type):
+    """render()'s GaussianRasterizationSettings (gaussian_renderer/__init__.py:49-63, 74-76) and the
+    view's time."""
+    from diff_gaussian_rasterization import GaussianRasterizationSettings
+    dev = pc.xyz.device
+    if cam_type != "PanopticSports":
+        rs = GaussianRasterizationSettings(
+            image_height=int(viewpoint_camera.image_height), image_width=int(viewpoint_camera.image_width),
+            tanfovx=math.tan(viewpoint_camera.FoVx * 0.5), tanfovy=math.tan(viewpoint_camera.FoVy * 0.5),
+            bg=bg_color, scale_modifier=scaling_modifier, viewmatrix=viewpoint_camera.world_view_transform.to(dev),
+            projmatrix=viewpoint_camera.full_proj_transform.to(dev), sh_degree=pc.active_sh_degree,
+            campos=viewpoint_camera.camera_center.to(dev), prefiltered=False, debug=debug,
+            include_feature=include_feature)
+        return rs, viewpoint_camera.time
+    # the Panoptic reader's prebuilt settings, taken as they are (their include_feature, bg and
+    # sh_degree included), and the frame time from the dict
+    return viewpoint_camera["camera"], viewpoint_camera["time"]
+
+
 def render(viewpoint_camera, pc: GaussianScene, bg_color: torch.Tensor, scaling_modifier: float = 1.0,
            override_color=None, stage: str = "fine-lang", compute_cov3D_python: bool = False,
            convert_SHs_python: bool = False, debug: bool = False, nonormalized: bool = False,
@@ -465,30 +494,14 @@ def render(viewpoint_camera, pc: GaussianScene, bg_color: torch.Tensor, scaling_
     precomputed colors!" on that, so the reference's override path cannot run.  Here the SHs are
     dropped when colours are precomputed, so the path renders the given colours; the rasterizer
     itself (GaussianRasterizer.forward) keeps upstream's error for callers that pass both."""
-    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    from diff_gaussian_rasterization import GaussianRasterizer
 
     dev = pc.xyz.device
-    screenspace_points = torch.zeros_like(pc.get_xyz, requires_grad=True, device=dev) + 0
-    try:
-        screenspace_points.retain_grad()
-    except RuntimeError:
-        pass
+    screenspace_points = _screenspace(pc)
     means3D = pc.get_xyz
     include_feature = "base" not in stage
-    if cam_type != "PanopticSports":
-        raster_settings = GaussianRasterizationSettings(
-            image_height=int(viewpoint_camera.image_height), image_width=int(viewpoint_camera.image_width),
-            tanfovx=math.tan(viewpoint_camera.FoVx * 0.5), tanfovy=math.tan(viewpoint_camera.FoVy * 0.5),
-            bg=bg_color, scale_modifier=scaling_modifier, viewmatrix=viewpoint_camera.world_view_transform.to(dev),
-            projmatrix=viewpoint_camera.full_proj_transform.to(dev), sh_degree=pc.active_sh_degree,
-            campos=viewpoint_camera.camera_center.to(dev), prefiltered=False, debug=debug,
-            include_feature=include_feature)
-        cam_time = viewpoint_camera.time
-    else:
-        # the Panoptic reader's prebuilt settings, taken as they are (their include_feature, bg and
-        # sh_degree included), and the frame time from the dict
-        raster_settings = viewpoint_camera["camera"]
-        cam_time = viewpoint_camera["time"]
+    raster_settings, cam_time = _raster_settings(viewpoint_camera, pc, bg_color, scaling_modifier, debug,
+                                                 include_feature, cam_type)
     rasterizer = GaussianRasterizer(raster_settings=raster_settings)
     opacity = pc.opacity
     scales = rotations = cov3D_precomp = None
@@ -583,9 +596,30 @@ def render_views(cams: Sequence, pc: GaussianScene, bg_color: torch.Tensor, stag
     # same values row by row, a third of the launches forward and backward
     outs[1], outs[2], outs[3] = activate(outs[1], outs[2], outs[3])
     parts = split_views(V, *outs)
-    return [render(c, pc, bg_color, stage=stage, nonormalized=nonormalized,
-                   language_feature_hiddendim=language_feature_hiddendim,
-                   _deformed=tuple(p[v] for p in parts), **kw) for v, c in enumerate(cams)]
+    if set(kw) - {"scaling_modifier", "debug"}:   # override / python paths: render() per view
+        return [render(c, pc, bg_color, stage=stage, nonormalized=nonormalized,
+                       language_feature_hiddendim=language_feature_hiddendim,
+                       _deformed=tuple(p[v] for p in parts), **kw) for v, c in enumerate(cams)]
+    # the views rasterized as one batch (their preprocesses ahead of their count waits), each
+    # exactly as render() rasterizes it
+    from diff_gaussian_rasterization import rasterize_views
+    include_feature = "base" not in stage
+    rss, sps, ins = [], [], []
+    for v, c in enumerate(cams):
+        rs, _ = _raster_settings(c, pc, bg_color, kw.get("scaling_modifier", 1.0), kw.get("debug", False),
+                                 include_feature, None)
+        m3, s3, r3, o3, sh3, l3, _ = (p[v] for p in parts)
+        sp = _screenspace(pc)
+        rss.append(rs)
+        sps.append(sp)
+        ins.append(dict(means3D=m3, means2D=sp, shs=sh3, language_feature_precomp=l3, opacities=o3, scales=s3,
+                        rotations=r3))
+    res = []
+    for v, (image, lang_img, radii, depth) in enumerate(rasterize_views(rss, ins)):
+        res.append({"render": image, "language_feature_image": None if "base" in stage else lang_img,
+                    "viewspace_points": sps[v], "visibility_filter": radii > 0, "radii": radii, "depth": depth,
+                    "coff": parts[6][v]})
+    return res
 
 
 def panoptic_camera(w: int, h: int, k, w2c, time: float, near: float = 0.01, far: float = 100.0,
