@@ -281,7 +281,12 @@ class TrainStep:
         collect = getattr(self.densify, "collect_stats", None)
         # train.py:388: while iteration < densify_until_iter, in the 'base' stages
         if "base" in self.stage and (collect is None or collect(self.iteration)):
-            radii = torch.stack([o["radii"] for o in outs]).max(dim=0).values
+            rl = [o["radii"] for o in outs]
+            if rl[0].is_cuda and rl[0].dtype == torch.int32:   # train.py:266's max over the views, one launch
+                from diff_gaussian_rasterization import radii_max_native
+                radii = radii_max_native(rl, torch.empty_like(rl[0]))
+            else:
+                radii = torch.stack(rl).max(dim=0).values
             vgrad = outs[0]["viewspace_points"].grad
             for o in outs[1:]:
                 vgrad = vgrad + o["viewspace_points"].grad
