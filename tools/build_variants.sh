@@ -12,6 +12,7 @@ for spec in "$@"; do
     name=${spec%%:*}; rest=${spec#*:}; src=${rest%%:*}; defs=${rest#*:}; defs=${defs//,/ }
     base=${src%.hip}
     [ "$base" = preprocess ] && defs="$defs -fno-slp-vectorize"   # as in the Makefile
+    [ "$base" = train ] && defs="$defs -fno-slp-vectorize"
     [ "$base" = deform ] && defs="$defs -fno-slp-vectorize"
     /opt/rocm/bin/hipcc $FLAGS $defs -c -o $OUT/obj/${base}_$name.o $src
     objs=$(ls $OBJ/*.o | grep -v "/$base.o")
