@@ -69,6 +69,36 @@ def test_size_queries():
     assert lib.lsr_binning_bytes_tb(K, P, 0, H) == -1                     # invalid image size
 
 
+def test_train_glue_argument_checks():
+    """The training-step glue (include/lsr_train.h: activations, view repeat / sum, the multi-view L1)
+    refuses bad arguments with a message and accepts empty work, before anything touches a device."""
+    import ctypes
+    from diff_gaussian_rasterization import _lib
+    lib = _lib.load()
+    err = lambda: lib.lsr_last_error().decode()
+    assert lib.lsr_l1_workspace_bytes(1) == 256 * 4 and lib.lsr_l1_workspace_bytes(8) == 8 * 256 * 4
+    assert lib.lsr_l1_workspace_bytes(0) == 256 * 4
+    p = ctypes.c_void_p(64)                                    # never dereferenced: every call below fails early
+    imgs = (ctypes.c_void_p * 9)(*([64] * 9))
+    for V, n, stride in ((0, 4, 4), (9, 4, 4), (2, -1, 4), (2, 8, 4)):
+        assert lib.lsr_l1_loss_views(V, n, imgs, p, stride, p, p, None) != 0
+        assert "1 <= V <= 8" in err()
+    assert lib.lsr_l1_loss_views(2, 4, imgs, p, 4, None, p, None) != 0 and "workspace required" in err()
+    assert lib.lsr_l1_loss_views_backward(2, 4, imgs, p, 4, None, imgs, None) != 0 and "d_loss" in err()
+    holes = (ctypes.c_void_p * 2)(64, None)
+    assert lib.lsr_l1_loss_views(2, 4, holes, p, 4, p, p, None) != 0 and "null image" in err()
+    assert lib.lsr_l1_loss_views_backward(2, 4, imgs, p, 4, p, holes, None) != 0 and "null gradient" in err()
+    assert lib.lsr_activate(-1, None, None, None, None, None, None, None) != 0 and "P >= 0" in err()
+    assert lib.lsr_activate(4, p, None, None, None, None, None, None) != 0 and "needs its output" in err()
+    assert lib.lsr_activate(4, None, ctypes.c_void_p(72), None, None, ctypes.c_void_p(64), None, None) != 0
+    assert "16-byte aligned" in err()
+    assert lib.lsr_activate(0, p, p, p, p, p, p, None) == 0    # no rows: no launch
+    rt = (_lib.RowTensor * 1)()
+    assert lib.lsr_repeat_rows(1, rt, 4, 0, None) != 0 and "n_blocks >= 1" in err()
+    assert lib.lsr_sum_row_blocks(1, rt, 4, 2, None) != 0 and "rows of whole floats" in err()
+    assert lib.lsr_repeat_rows(0, None, 4, 2, None) == 0 and lib.lsr_sum_row_blocks(1, rt, 0, 2, None) == 0
+
+
 def test_settings_validation_messages():
     """Upstream's exactly-one-of errors are raised before anything touches a device."""
     import torch
